@@ -1,0 +1,197 @@
+/*
+ * nmz_gpu.h -- C ABI of libnmz_gpu.so, the MI355X (gfx950) engine behind
+ * Namazu's explore-policy decision path and historystorage similarity search.
+ *
+ * This is the drop-in boundary: plain pointers and sizes, no HIP or torch
+ * types, every call returns an int status (NMZ_OK == 0, <0 on error, message
+ * in nmz_last_error()). A Go host binds it through cgo;
+ * the Python host mirror in namazu_amd/ binds it through ctypes.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * reference tree, nmz/):
+ *
+ *   nmz_replayable_sweep*  -> Replayable.determineInterval / QueueEvent
+ *                             explorepolicy/replayable/replayablepolicy.go:100-126
+ *                             (FNV-1a64(seed || hint) % maxInterval), batched over
+ *                             seeds x events.
+ *   nmz_random_sweep*      -> Random.QueueEvent + makeActionForEvent
+ *                             explorepolicy/random/randompolicy.go:300-316,332-346
+ *                             + util/queue/impl.go:35-46,94-128 (Int63n delay,
+ *                             Intn(999) fault draw), batched over seeds x events
+ *                             under the deterministic per-event seeding contract
+ *                             documented in DESIGN.md section 2.
+ *   nmz_random_params_resolve -> Random.LoadConfig's interval/probability
+ *                             semantics randompolicy.go:156-228,332-340.
+ *   nmz_ed_pairs / nmz_ed_allpairs_knn -> HistoryStorage similarity search
+ *                             (optional interface next to Search /
+ *                             SearchWithConverter, historystorage/historystorage.go:50-51,
+ *                             naive/naive.go:235-257); distance 0 <=> SingleTrace.Equals
+ *                             (util/trace/trace.go:29-31).
+ *
+ * Buffers passed to the host-pointer entry points are borrowed for the call
+ * only and never retained (cgo pointer rules). The *_dev entry points take
+ * device pointers that are already resident in HBM plus a hipStream_t passed
+ * as void*; they enqueue asynchronously on that stream.
+ *
+ * Threading: a context is bound to one device; calls on one context are
+ * serialized by a mutex inside it and call hipSetDevice on entry, so a Go
+ * caller may invoke them from any OS thread.
+ */
+#ifndef NMZ_GPU_H
+#define NMZ_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NMZ_ABI_VERSION 1
+
+/* status codes */
+#define NMZ_OK 0
+#define NMZ_EINVAL (-1)   /* bad argument (mirrors LoadConfig errors / queue panics) */
+#define NMZ_EHIP (-2)     /* HIP runtime error */
+#define NMZ_ENOMEM (-3)   /* device allocation failed */
+#define NMZ_ERANGE (-4)   /* a decision needed more Go rng outputs than the kernel's closed form covers */
+
+/* per-event class bits for the random policy (one uint8 per event) */
+#define NMZ_EV_PRIORITIZED 0x01u /* EntityID() in prioritizedEntities (randompolicy.go:335) */
+#define NMZ_EV_FAULTABLE 0x02u   /* DefaultFaultAction() != nil: deferred Packet/Filesystem
+                                    event (event_packet.go:45-47, event_filesystem.go:58-60) */
+
+/* stats flags */
+#define NMZ_STAT_RNG_OVERFLOW 0x01u
+
+#define NMZ_NONE 0xffffffffu
+
+/* Per-schedule statistics (one per seed), 32 bytes.
+ * delays are time.Duration values (int64 ns). */
+typedef struct nmz_sched_stats {
+    uint64_t sum_delay_ns;  /* sum of delays, mod 2^64 (two's complement)          */
+    int64_t max_delay_ns;   /* max delay (signed); INT64_MIN when there are no events */
+    uint32_t argmax_event;  /* first event attaining max_delay_ns; NMZ_NONE if none */
+    uint32_t n_fault;       /* number of fault actions chosen                        */
+    uint32_t first_fault;   /* first event given a fault action; NMZ_NONE if none    */
+    uint32_t flags;         /* NMZ_STAT_* bits                                       */
+} nmz_sched_stats;
+
+/* Failure-schedule candidate, ordered by (n_fault desc, sum_delay desc as int64,
+ * seed asc). */
+typedef struct nmz_topk_entry {
+    uint64_t seed;
+    int64_t sum_delay_ns;
+    uint32_t n_fault;
+    uint32_t first_fault;
+} nmz_topk_entry;
+
+/* Resolved random-policy parameters: the kernel consumes integers only.
+ * Index 0 = ordinary entity, 1 = prioritized entity (x0.8 intervals). */
+typedef struct nmz_random_params {
+    int64_t min_ns[2];
+    int64_t max_ns[2];
+    int32_t fault_threshold; /* int(faultActionProbability * 1000.0) */
+    uint32_t reserved;
+} nmz_random_params;
+
+typedef struct nmz_ctx nmz_ctx;
+
+/* ---- context ---------------------------------------------------------- */
+int nmz_open(int device, nmz_ctx **out);
+int nmz_close(nmz_ctx *ctx);
+const char *nmz_last_error(void); /* thread-local, valid until the next call on this thread */
+int nmz_abi_version(void);
+int nmz_device_count(int *count);
+
+/* ---- parameter resolution (host only, no device work) -------------------
+ * min/max are time.Duration ns as parsed by LoadConfig; probability as float64.
+ * Applies the prioritized x0.8 truncation in IEEE double exactly like
+ * randompolicy.go:337-339, the threshold int(p*1000.0) of :310, and the
+ * validity checks of :223-225 (probability) and util/queue/impl.go:36-38
+ * (min > max). */
+int nmz_random_params_resolve(int64_t min_ns, int64_t max_ns, double fault_probability,
+                              nmz_random_params *out);
+
+/* ---- replayable policy sweep ------------------------------------------
+ * For each seed s (CSR: seed_off[n_seeds+1] into seed_bytes) and event e
+ * (CSR: hint_off[n_events+1] into hint_bytes, the events' ReplayHint()):
+ *     delay[s][e] = int64( FNV1a64(seed_s || hint_e) % uint64(max_interval_ns) )
+ * and 0 for every event when max_interval_ns == 0 (replayablepolicy.go:101-104).
+ * Outputs (each may be NULL):
+ *   stats[n_seeds]
+ *   delays[n_dump_seeds * n_events]  row-major, for the first n_dump_seeds seeds
+ *   topk[k]   best k seeds by (sum_delay desc, seed index asc); entry .seed is
+ *             the seed's index in the CSR.                                    */
+int nmz_replayable_sweep(nmz_ctx *ctx, const uint32_t *seed_off, const uint8_t *seed_bytes,
+                         uint64_t n_seeds, const uint32_t *hint_off, const uint8_t *hint_bytes,
+                         uint32_t n_events, int64_t max_interval_ns, nmz_sched_stats *stats,
+                         int64_t *delays, uint64_t n_dump_seeds, uint32_t k,
+                         nmz_topk_entry *topk);
+
+/* Device-resident variant (all pointers are device pointers; hipStream_t as void*).
+ * Requires a prior nmz_replayable_plan() for the same hint table. */
+typedef struct nmz_replayable_plan nmz_replayable_plan;
+int nmz_replayable_plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hint_bytes,
+                               uint32_t n_events, int64_t max_interval_ns,
+                               uint64_t max_seeds, nmz_replayable_plan **out);
+int nmz_replayable_plan_destroy(nmz_replayable_plan *plan);
+int nmz_replayable_sweep_dev(nmz_replayable_plan *plan, const uint32_t *d_seed_off,
+                             const uint8_t *d_seed_bytes, uint64_t n_seeds,
+                             nmz_sched_stats *d_stats, void *stream);
+
+/* ---- random policy sweep ------------------------------------------------
+ * Seeds are the integers seed0 .. seed0+n_seeds-1. For seed s and event e
+ * (evhash[e], evclass[e] = NMZ_EV_* bits) the decision is made by a fresh
+ *     rng = rand.New(rand.NewSource(int64(FNV1a64(le64(s) || le64(evhash[e])))))
+ * drawing, in this order,
+ *     delay = rng.Int63n(max-min) + min   if min != max  (else delay = min, no draw)
+ *     fault = rng.Intn(999) < fault_threshold            if NMZ_EV_FAULTABLE
+ * with (min,max) = params->{min,max}_ns[prioritized].
+ * Outputs (each may be NULL): stats[n_seeds]; delays/faults[n_dump_seeds*n_events];
+ * topk[k] by (n_fault desc, sum_delay desc, seed asc), .seed = the seed value. */
+int nmz_random_sweep(nmz_ctx *ctx, uint64_t seed0, uint64_t n_seeds, const uint64_t *evhash,
+                     const uint8_t *evclass, uint32_t n_events, const nmz_random_params *params,
+                     nmz_sched_stats *stats, int64_t *delays, uint8_t *faults,
+                     uint64_t n_dump_seeds, uint32_t k, nmz_topk_entry *topk);
+
+/* Device-resident variant: per-event tables are built once in the plan; the
+ * sweep enqueues on `stream` and writes d_stats[n_seeds] (device memory). */
+typedef struct nmz_random_plan nmz_random_plan;
+int nmz_random_plan_create(nmz_ctx *ctx, const uint64_t *evhash, const uint8_t *evclass,
+                           uint32_t n_events, const nmz_random_params *params, uint64_t max_seeds,
+                           nmz_random_plan **out);
+int nmz_random_plan_destroy(nmz_random_plan *plan);
+int nmz_random_sweep_dev(nmz_random_plan *plan, uint64_t seed0, uint64_t n_seeds,
+                         nmz_sched_stats *d_stats, void *stream);
+
+/* ---- trace similarity (banded Levenshtein over event-hash sequences) ------
+ * Traces in CSR: off[n_traces+1] (element offsets) into sym[] (uint64 event
+ * hashes). ED_w(a,b) = min(D(n,m), w+1) where D is unit-cost Levenshtein
+ * restricted to cells |i-j| <= w (cells outside the band are +inf).
+ * ED_w == 0  <=>  the traces are equal element-wise (SingleTrace.Equals). */
+int nmz_ed_pairs(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, uint32_t n_traces,
+                 const uint32_t *pairs /* [2*n_pairs] */, uint64_t n_pairs, uint32_t band,
+                 uint32_t *dist /* [n_pairs] */);
+
+/* All pairs i != j; for each trace the k nearest others by (dist asc, id asc).
+ * knn_id/knn_dist are [n_traces * k]; missing entries are NMZ_NONE. */
+int nmz_ed_allpairs_knn(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
+                        uint32_t n_traces, uint32_t band, uint32_t k, uint32_t *knn_id,
+                        uint32_t *knn_dist);
+
+/* Device-resident variant: the plan remaps symbols to dense ids and builds the
+ * lane-interleaved candidate layout once; searches then run on resident data.
+ * d_knn_keys[n_traces * k] (device) receives sorted keys (dist << 32 | id),
+ * UINT64_MAX for missing entries. k in [1, 64]. */
+typedef struct nmz_ed_plan nmz_ed_plan;
+int nmz_ed_plan_create(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, uint32_t n_traces,
+                       uint32_t band, nmz_ed_plan **out);
+int nmz_ed_plan_destroy(nmz_ed_plan *plan);
+int nmz_ed_plan_is_fast(const nmz_ed_plan *plan);
+int nmz_ed_allpairs_knn_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NMZ_GPU_H */

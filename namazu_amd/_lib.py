@@ -1,0 +1,178 @@
+"""ctypes binding of libnmz_gpu.so (the C ABI declared in include/nmz_gpu.h).
+
+The HIP library is the only compute path: if it is missing this module raises
+NmzLibraryError instead of falling back to anything on the CPU.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libnmz_gpu.so")
+
+NMZ_OK = 0
+NMZ_EINVAL = -1
+NMZ_EHIP = -2
+NMZ_ENOMEM = -3
+NMZ_ERANGE = -4
+
+NMZ_EV_PRIORITIZED = 0x01
+NMZ_EV_FAULTABLE = 0x02
+NMZ_STAT_RNG_OVERFLOW = 0x01
+NMZ_NONE = 0xFFFFFFFF
+
+SCHED_STATS_DTYPE = np.dtype([
+    ("sum_delay_ns", "<u8"), ("max_delay_ns", "<i8"), ("argmax_event", "<u4"),
+    ("n_fault", "<u4"), ("first_fault", "<u4"), ("flags", "<u4")])
+assert SCHED_STATS_DTYPE.itemsize == 32
+TOPK_DTYPE = np.dtype([("seed", "<u8"), ("sum_delay_ns", "<i8"), ("n_fault", "<u4"),
+                       ("first_fault", "<u4")])
+assert TOPK_DTYPE.itemsize == 24
+
+
+class NmzLibraryError(RuntimeError):
+    """libnmz_gpu.so is missing or failed to load (no CPU fallback exists)."""
+
+
+class NmzError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"nmz error {code}: {msg}")
+        self.code = code
+
+
+class NmzInvalidArgument(NmzError, ValueError):
+    pass
+
+
+class RandomParams(ctypes.Structure):
+    _fields_ = [("min_ns", ctypes.c_int64 * 2), ("max_ns", ctypes.c_int64 * 2),
+                ("fault_threshold", ctypes.c_int32), ("reserved", ctypes.c_uint32)]
+
+
+# every entry point declared in include/nmz_gpu.h: name -> (restype, argtypes)
+_P = ctypes.c_void_p
+_u64, _i64, _u32, _i32 = ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint32, ctypes.c_int32
+_int = ctypes.c_int
+SIGNATURES = {
+    "nmz_open": (_int, [_int, ctypes.POINTER(_P)]),
+    "nmz_close": (_int, [_P]),
+    "nmz_last_error": (ctypes.c_char_p, []),
+    "nmz_abi_version": (_int, []),
+    "nmz_device_count": (_int, [ctypes.POINTER(_int)]),
+    "nmz_random_params_resolve": (_int, [_i64, _i64, ctypes.c_double, _P]),
+    "nmz_replayable_sweep": (_int, [_P, _P, _P, _u64, _P, _P, _u32, _i64, _P, _P, _u64, _u32, _P]),
+    "nmz_replayable_plan_create": (_int, [_P, _P, _P, _u32, _i64, _u64, ctypes.POINTER(_P)]),
+    "nmz_replayable_plan_destroy": (_int, [_P]),
+    "nmz_replayable_sweep_dev": (_int, [_P, _P, _P, _u64, _P, _P]),
+    "nmz_random_sweep": (_int, [_P, _u64, _u64, _P, _P, _u32, _P, _P, _P, _P, _u64, _u32, _P]),
+    "nmz_random_plan_create": (_int, [_P, _P, _P, _u32, _P, _u64, ctypes.POINTER(_P)]),
+    "nmz_random_plan_destroy": (_int, [_P]),
+    "nmz_random_sweep_dev": (_int, [_P, _u64, _u64, _P, _P]),
+    "nmz_ed_pairs": (_int, [_P, _P, _P, _u32, _P, _u64, _u32, _P]),
+    "nmz_ed_allpairs_knn": (_int, [_P, _P, _P, _u32, _u32, _u32, _P, _P]),
+    "nmz_ed_plan_create": (_int, [_P, _P, _P, _u32, _u32, ctypes.POINTER(_P)]),
+    "nmz_ed_plan_destroy": (_int, [_P]),
+    "nmz_ed_plan_is_fast": (_int, [_P]),
+    "nmz_ed_allpairs_knn_dev": (_int, [_P, _u32, _P, _P]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load libnmz_gpu.so (fails loudly; there is no CPU fallback)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NmzLibraryError(
+                f"{LIB_PATH} not found: build it with `make -C namazu_amd/csrc` "
+                "(or __graft_entry__.build()); the engine has no CPU fallback")
+        try:
+            import torch  # noqa: F401  (pin one HIP runtime per process when torch is present)
+        except Exception:
+            pass
+        try:
+            L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:
+            raise NmzLibraryError(f"failed to load {LIB_PATH}: {e}") from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+        return L
+
+
+def last_error():
+    return load().nmz_last_error().decode(errors="replace")
+
+
+def check(rc):
+    if rc != NMZ_OK:
+        msg = last_error()
+        if rc == NMZ_EINVAL:
+            raise NmzInvalidArgument(rc, msg)
+        raise NmzError(rc, msg)
+
+
+def ptr(a):
+    """Data pointer of a numpy array (None for None)."""
+    if a is None:
+        return None
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def resolve_random_params(min_ns, max_ns, probability):
+    p = RandomParams()
+    check(load().nmz_random_params_resolve(int(min_ns), int(max_ns), float(probability),
+                                           ctypes.byref(p)))
+    return p
+
+
+class Context:
+    """One device context (libnmz_gpu nmz_ctx). Use as a context manager."""
+
+    def __init__(self, device=0):
+        self._lib = load()
+        h = ctypes.c_void_p()
+        check(self._lib.nmz_open(int(device), ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            self._lib.nmz_close(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def device_count():
+    n = ctypes.c_int()
+    check(load().nmz_device_count(ctypes.byref(n)))
+    return n.value
+
+
+_default_ctx = {}
+
+
+def default_context(device=0):
+    ctx = _default_ctx.get(device)
+    if ctx is None:
+        ctx = _default_ctx[device] = Context(device)
+    return ctx

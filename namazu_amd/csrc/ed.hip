@@ -1,0 +1,591 @@
+// K3 -- banded Levenshtein over event-hash sequences + all-pairs k-NN.
+//
+// ED_w(a,b) = min(D(n,m), w+1), D restricted to |i-j| <= w (outside = +inf).
+// Distance 0 <=> element-wise equal traces (SingleTrace.Equals,
+// util/trace/trace.go:29-31); see DESIGN.md section 4.
+//
+// Fast path (k_ed_tile<W>), MI355X-first:
+//  * symbols are remapped to dense 16-bit ids (exact: equality preserved);
+//  * one lane per candidate trace b and TWO query traces (q1,q2) per wave,
+//    packed in the lo/hi u16 halves of every register, so each packed VALU
+//    op advances two DP cells; the band row (2W+1 cells) and a sliding window
+//    of 2W+R candidate symbols live in VGPRs -- no cross-lane traffic, all 64
+//    lanes busy (a wave-per-pair anti-diagonal mapping keeps at most w+1 of
+//    64 lanes busy per step for w = 32);
+//  * query symbols are wave-uniform scalar loads; candidate symbols come
+//    from a lane-interleaved layout ([group][pos][64 lanes], one coalesced
+//    128-B line per position), prefetched one row block ahead;
+//  * Ukkonen cut-off: the band minimum of a row never decreases, so once it
+//    exceeds W for both halves of every lane the wave stops (result W+1).
+// Results go straight into per-trace top-k lists (u64 keys dist<<32|id,
+// cascade atomicMin insertion: lock-free and order-independent).
+//
+// Generic path (k_ed_generic): one thread per pair, any band, u64 symbols,
+// band row in global scratch. Used for nmz_ed_pairs and as the fallback.
+#include <algorithm>
+#include <unordered_map>
+#include <vector>
+
+#include "nmz_common.h"
+#include "nmz_internal.h"
+
+namespace nmz {
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+constexpr uint16_t CAND_PAD = 0xffff;  // candidate symbol past its end (never a real id)
+constexpr uint16_t QUERY_PAD = 0xfffe; // query symbol past its end
+constexpr uint16_t INF16 = 0x7f00;     // +inf for u16 DP cells (grows by < W before leaving the band)
+constexpr int ED_R = 8;                // rows per unrolled block
+constexpr uint32_t MAX_FAST_LEN = 0x7000;
+constexpr uint32_t MAX_FAST_SYMBOLS = 0xfffd;
+
+__device__ __forceinline__ u16x2 pk_min(u16x2 a, u16x2 b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ u16x2 splat(uint16_t v) { return u16x2{v, v}; }
+__device__ __forceinline__ u16x2 as_pk(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+// ---------------------------------------------------------------------------
+// top-k lists: k u64 slots per trace, ascending, UINT64_MAX = empty
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void knn_insert(uint64_t *list, uint32_t k, uint64_t key) {
+    if (key >= __hip_atomic_load(&list[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    for (uint32_t s = 0; s < k; ++s) {
+        const uint64_t old = atomicMin((unsigned long long *)&list[s], (unsigned long long)key);
+        if (old == UINT64_MAX) return;
+        key = old > key ? old : key;
+    }
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint64_t o = __shfl_xor(v, off, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+// insert the wave's k best keys for one query trace (all lanes participate)
+__device__ __forceinline__ void knn_insert_wave(uint64_t *list, uint32_t k, uint64_t key, uint32_t lane) {
+    for (uint32_t r = 0; r < k; ++r) {
+        const uint64_t best = wave_min_u64(key);
+        if (best == UINT64_MAX) return;
+        if (best >= __hip_atomic_load(&list[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+        if (lane == (uint32_t)__builtin_amdgcn_readfirstlane(__ffsll(__ballot(key == best)) - 1))
+            knn_insert(list, k, best);
+        if (key == best) key = UINT64_MAX;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// wave -> (query pair, candidate group) over the upper triangle of 64x64 blocks
+//   block b (queries 64b..64b+63 = 32 query pairs) x groups g in [b, G)
+//   waves in block b: 32*(G-b); inner order keeps one candidate group for
+//   32 consecutive waves (8 workgroups) so the group's symbols are re-read
+//   from the same L2.
+// ---------------------------------------------------------------------------
+__host__ __device__ inline uint64_t tri_prefix(uint64_t b, uint64_t G) { return 32 * (b * G - b * (b - 1) / 2); }
+
+struct EdArgs {
+    const uint16_t *qsym;       // query symbols, CSR order
+    const uint64_t *qoff;       // [N+1]
+    const uint16_t *csym;       // candidate symbols, [group][pos][64]
+    const uint64_t *coff;       // [G] element offset of each group block
+    const uint32_t *gmax;       // [G] padded length of each group
+    const uint32_t *len;        // [N]
+    uint32_t N, G, k;
+    uint64_t n_waves;
+    uint64_t *knn;              // [N][k]
+};
+
+template <int W>
+__global__ __launch_bounds__(256) void k_ed_tile(EdArgs A) {
+    constexpr int NB = 2 * W + 1;       // band cells
+    constexpr int NW = 2 * W + ED_R;    // window symbols
+    // XCD-aware: hardware block b runs on XCD b%8; give each XCD a contiguous
+    // range of logical blocks so waves sharing a candidate group share an L2.
+    const uint32_t nblk = gridDim.x, per_xcd = nblk / 8;
+    const uint32_t hb = blockIdx.x;
+    const uint32_t lb = (hb % 8) * per_xcd + hb / 8;
+    const uint64_t wave = (uint64_t)lb * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (wave >= A.n_waves) return;
+
+    // locate block b: largest b with tri_prefix(b) <= wave
+    uint32_t lo = 0, hi = A.G;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (tri_prefix(mid, A.G) <= wave) lo = mid; else hi = mid;
+    }
+    const uint32_t b = lo;
+    const uint64_t idx = wave - tri_prefix(b, A.G);
+    const uint32_t g = b + (uint32_t)(idx / 32);
+    const uint32_t q1 = 64 * b + 2 * (uint32_t)(idx % 32), q2 = q1 + 1;
+    const uint32_t j = 64 * g + lane;
+
+    const bool v1 = q1 < A.N && j < A.N && j > q1;
+    const bool v2 = q2 < A.N && j < A.N && j > q2;
+    const uint32_t n1 = q1 < A.N ? A.len[q1] : 0, n2 = q2 < A.N ? A.len[q2] : 0;
+    const uint32_t m = j < A.N ? A.len[j] : 0;
+    const uint16_t *__restrict__ a1 = A.qsym + (q1 < A.N ? A.qoff[q1] : 0);
+    const uint16_t *__restrict__ a2 = A.qsym + (q2 < A.N ? A.qoff[q2] : 0);
+    const uint16_t *__restrict__ cs = A.csym + A.coff[g] + lane;
+    const uint32_t glen = A.gmax[g];
+
+    // per-half state: result, whether still running
+    uint32_t r1 = W + 1, r2 = W + 1;
+    bool run1 = v1, run2 = v2;
+    const int32_t d1 = (int32_t)m - (int32_t)n1, d2 = (int32_t)m - (int32_t)n2;
+    if (run1 && (d1 > W || d1 < -W)) run1 = false;  // |n-m| > W: W+1
+    if (run2 && (d2 > W || d2 < -W)) run2 = false;
+    if (run1 && n1 == 0) { r1 = m; run1 = false; }
+    if (run2 && n2 == 0) { r2 = m; run2 = false; }
+
+    const uint32_t nrows = __builtin_amdgcn_readfirstlane(max(n1, n2));  // n_h = 0 for q_h >= N
+    u16x2 D[NB];
+    uint32_t win[NW];  // packed (b, b) symbols for window positions i0-W .. i0-W+NW-1
+#pragma unroll
+    for (int t = 0; t < NB; ++t) D[t] = splat(t >= W ? (uint16_t)(t - W) : INF16);
+    auto load_sym = [&](int64_t pos) -> uint32_t {
+        const uint32_t s = (pos >= 0 && pos < (int64_t)glen) ? (uint32_t)cs[(uint64_t)pos * 64] : (uint32_t)CAND_PAD;
+        return s | (s << 16);
+    };
+#pragma unroll
+    for (int t = 0; t < NW; ++t) win[t] = load_sym((int64_t)t - W);
+
+    const u16x2 one = splat(1);
+    uint32_t i0 = 0;
+    const bool any_run = __builtin_amdgcn_readfirstlane((uint32_t)__any(run1 || run2)) != 0;
+    if (any_run) {
+        while (i0 < nrows) {
+            // next extraction row for the halves that are still alive
+            const uint32_t stop = min(nrows, min(n1 > i0 ? n1 : nrows, n2 > i0 ? n2 : nrows));
+            const uint32_t stop_u = __builtin_amdgcn_readfirstlane(stop);
+            if (i0 + ED_R <= stop_u) {
+                // prefetch the symbols entering the window after this block
+                uint32_t nxt[ED_R];
+#pragma unroll
+                for (int r = 0; r < ED_R; ++r) nxt[r] = load_sym((int64_t)i0 - W + NW + r);
+#pragma unroll
+                for (int r = 0; r < ED_R; ++r) {
+                    const uint32_t i = i0 + r;  // computing row i+1, symbols a[i]
+                    const uint32_t s1 = i < n1 ? a1[i] : QUERY_PAD, s2 = i < n2 ? a2[i] : QUERY_PAD;
+                    const uint32_t ap = __builtin_amdgcn_readfirstlane(s1 | (s2 << 16));
+                    u16x2 left = splat(INF16);
+#pragma unroll
+                    for (int t = 0; t < NB; ++t) {
+                        const u16x2 c = pk_min(as_pk(win[r + t] ^ ap), one);
+                        const u16x2 diag = D[t] + c;
+                        const u16x2 up = (t + 1 < NB) ? D[t + 1] : splat(INF16);
+                        const u16x2 nd = pk_min(diag, pk_min(up, left) + one);
+                        D[t] = nd;
+                        left = nd;
+                    }
+                }
+#pragma unroll
+                for (int t = 0; t < NW - ED_R; ++t) win[t] = win[t + ED_R];
+#pragma unroll
+                for (int r = 0; r < ED_R; ++r) win[NW - ED_R + r] = nxt[r];
+                i0 += ED_R;
+            } else {
+                // single row (lands exactly on an extraction row)
+                const uint32_t i = i0;
+                const uint32_t s1 = i < n1 ? a1[i] : QUERY_PAD, s2 = i < n2 ? a2[i] : QUERY_PAD;
+                const uint32_t ap = __builtin_amdgcn_readfirstlane(s1 | (s2 << 16));
+                u16x2 left = splat(INF16);
+#pragma unroll
+                for (int t = 0; t < NB; ++t) {
+                    const u16x2 c = pk_min(as_pk(win[t] ^ ap), one);
+                    const u16x2 diag = D[t] + c;
+                    const u16x2 up = (t + 1 < NB) ? D[t + 1] : splat(INF16);
+                    const u16x2 nd = pk_min(diag, pk_min(up, left) + one);
+                    D[t] = nd;
+                    left = nd;
+                }
+                const uint32_t nx = load_sym((int64_t)i0 - W + NW);
+#pragma unroll
+                for (int t = 0; t < NW - 1; ++t) win[t] = win[t + 1];
+                win[NW - 1] = nx;
+                i0 += 1;
+            }
+            // extraction at row n_h: D(n, m) sits on diagonal m - n
+            if (i0 == n1 && run1) {
+                uint32_t v = W + 1;
+#pragma unroll
+                for (int t = 0; t < NB; ++t) v = (t - W == d1) ? (uint32_t)D[t].x : v;
+                r1 = min(v, (uint32_t)W + 1);
+                run1 = false;
+            }
+            if (i0 == n2 && run2) {
+                uint32_t v = W + 1;
+#pragma unroll
+                for (int t = 0; t < NB; ++t) v = (t - W == d2) ? (uint32_t)D[t].y : v;
+                r2 = min(v, (uint32_t)W + 1);
+                run2 = false;
+            }
+            // cut-off: row band minimum > W stays > W
+            if ((i0 & 15) == 0 || !(run1 || run2)) {
+                u16x2 mn = D[0];
+#pragma unroll
+                for (int t = 1; t < NB; ++t) mn = pk_min(mn, D[t]);
+                if (mn.x > W) run1 = false;
+                if (mn.y > W) run2 = false;
+                if (!__any(run1 || run2)) break;
+            }
+        }
+    }
+    // publish: candidate lists (per lane) and query lists (wave-reduced)
+    const uint64_t key1 = v1 ? (((uint64_t)r1 << 32) | j) : UINT64_MAX;
+    const uint64_t key2 = v2 ? (((uint64_t)r2 << 32) | j) : UINT64_MAX;
+    if (v1) knn_insert(A.knn + (uint64_t)j * A.k, A.k, ((uint64_t)r1 << 32) | q1);
+    if (v2) knn_insert(A.knn + (uint64_t)j * A.k, A.k, ((uint64_t)r2 << 32) | q2);
+    if (q1 < A.N) knn_insert_wave(A.knn + (uint64_t)q1 * A.k, A.k, key1, lane);
+    if (q2 < A.N) knn_insert_wave(A.knn + (uint64_t)q2 * A.k, A.k, key2, lane);
+}
+
+// ---------------------------------------------------------------------------
+// generic: one thread per pair, u64 symbols, band row in global scratch
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_ed_generic(const uint64_t *__restrict__ off, const uint64_t *__restrict__ sym,
+                                                    const uint32_t *__restrict__ pairs, uint64_t n_pairs, uint32_t W,
+                                                    uint32_t *__restrict__ scratch, uint32_t *__restrict__ dist) {
+    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t NB = 2 * W + 1;
+    const uint32_t INF = 0x3fffffffu;
+    for (uint64_t p = tid; p < n_pairs; p += nthr) {
+        const uint32_t ia = pairs[2 * p], ib = pairs[2 * p + 1];
+        const uint64_t *a = sym + off[ia], *b = sym + off[ib];
+        const int64_t n = (int64_t)(off[ia + 1] - off[ia]), m = (int64_t)(off[ib + 1] - off[ib]);
+        const int64_t dd = m - n;
+        if (dd > (int64_t)W || dd < -(int64_t)W) {
+            dist[p] = W + 1;
+            continue;
+        }
+        // D[t] = cell (i, i + t - W); row 0: D(0, j) = j
+        for (uint32_t t = 0; t < NB; ++t) scratch[t * nthr + tid] = (t >= W) ? (t - W) : INF;
+        for (int64_t i = 1; i <= n; ++i) {
+            uint32_t left = INF;
+            for (uint32_t t = 0; t < NB; ++t) {
+                const int64_t jj = i + (int64_t)t - (int64_t)W;
+                uint32_t v;
+                if (jj < 0 || jj > m) {
+                    v = INF;
+                } else if (jj == 0) {
+                    v = (uint32_t)i;
+                } else {
+                    const uint32_t diag = scratch[t * nthr + tid];
+                    const uint32_t up = (t + 1 < NB) ? scratch[(t + 1) * nthr + tid] : INF;
+                    v = diag + (a[i - 1] != b[jj - 1] ? 1u : 0u);
+                    v = min(v, min(up, left) + 1);
+                    v = min(v, INF);
+                }
+                scratch[t * nthr + tid] = v;
+                left = v;
+            }
+        }
+        const uint32_t v = scratch[(uint32_t)(dd + W) * nthr + tid];
+        dist[p] = min(v, W + 1);
+    }
+}
+
+__global__ void k_knn_init(uint64_t *knn, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) knn[i] = UINT64_MAX;
+}
+
+__global__ void k_knn_final(const uint64_t *__restrict__ knn, uint64_t n, uint32_t *__restrict__ ids,
+                            uint32_t *__restrict__ ds) {
+    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t key = knn[i];
+    ids[i] = key == UINT64_MAX ? NMZ_NONE : (uint32_t)key;
+    ds[i] = key == UINT64_MAX ? NMZ_NONE : (uint32_t)(key >> 32);
+}
+
+// all-pairs via the generic kernel (fallback): pair list = upper triangle
+__global__ void k_pairs_upper(uint32_t N, uint64_t start, uint64_t count, uint32_t *pairs) {
+    uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= count) return;
+    uint64_t p = start + t;  // p-th pair (i<j), row-major
+    // i = largest with i*(2N-i-1)/2 <= p
+    double Nd = N;
+    uint64_t i = (uint64_t)floor(((2 * Nd - 1) - sqrt((2 * Nd - 1) * (2 * Nd - 1) - 8.0 * (double)p)) / 2);
+    auto base = [&](uint64_t r) { return r * (2 * (uint64_t)N - r - 1) / 2; };
+    while (i > 0 && base(i) > p) --i;
+    while (base(i + 1) <= p) ++i;
+    const uint64_t jj = i + 1 + (p - base(i));
+    pairs[2 * t] = (uint32_t)i;
+    pairs[2 * t + 1] = (uint32_t)jj;
+}
+
+__global__ void k_knn_from_pairs(const uint32_t *__restrict__ pairs, const uint32_t *__restrict__ dist, uint64_t count,
+                                 uint64_t *knn, uint32_t k) {
+    uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= count) return;
+    const uint32_t i = pairs[2 * t], j = pairs[2 * t + 1];
+    const uint64_t d = dist[t];
+    knn_insert(knn + (uint64_t)i * k, k, (d << 32) | j);
+    knn_insert(knn + (uint64_t)j * k, k, (d << 32) | i);
+}
+
+}  // namespace nmz
+
+// ---------------------------------------------------------------------------
+// ED plan: symbol remap + device layouts (reused across searches)
+// ---------------------------------------------------------------------------
+struct nmz_ed_plan {
+    nmz_ctx *ctx = nullptr;
+    uint32_t n = 0, band = 0, G = 0;
+    bool fast = false;
+    nmz::DevBuf mem;
+    uint16_t *d_qsym = nullptr, *d_csym = nullptr;
+    uint64_t *d_qoff = nullptr, *d_coff = nullptr;
+    uint32_t *d_gmax = nullptr, *d_len = nullptr;
+    // generic path
+    uint64_t *d_off64 = nullptr, *d_sym64 = nullptr;
+};
+
+namespace nmz {
+
+static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, uint32_t N, uint32_t band,
+                         nmz_ed_plan **out) {
+    NMZ_CHECK(ctx && out, "NULL argument");
+    NMZ_CHECK(N == 0 || off, "off is NULL");
+    *out = nullptr;
+    auto *p = new nmz_ed_plan();
+    p->ctx = ctx;
+    p->n = N;
+    p->band = band;
+    hipStream_t st = ctx->stream;
+    const uint64_t total = N ? off[N] : 0;
+    uint32_t maxlen = 0;
+    for (uint32_t i = 0; i < N; ++i) maxlen = std::max<uint32_t>(maxlen, (uint32_t)(off[i + 1] - off[i]));
+    // dense symbol ids (exact remap: a == b <=> id(a) == id(b))
+    std::vector<uint16_t> ids;
+    bool fast = (band == 8 || band == 16 || band == 32) && maxlen + band < MAX_FAST_LEN;
+    if (fast) {
+        std::unordered_map<uint64_t, uint32_t> dict;
+        dict.reserve(1024);
+        ids.resize(total);
+        for (uint64_t t = 0; t < total && fast; ++t) {
+            auto it = dict.find(sym[t]);
+            uint32_t id;
+            if (it == dict.end()) {
+                id = (uint32_t)dict.size();
+                if (id >= MAX_FAST_SYMBOLS) fast = false;
+                dict.emplace(sym[t], id);
+            } else {
+                id = it->second;
+            }
+            ids[t] = (uint16_t)id;
+        }
+    }
+    p->fast = fast;
+    auto cleanup = [&](int code) {
+        p->mem.release();
+        delete p;
+        return code;
+    };
+    if (fast) {
+        const uint32_t G = (N + 63) / 64;
+        p->G = G;
+        std::vector<uint32_t> gmax(G + 1, 0), len(N + 1, 0);
+        std::vector<uint64_t> coff(G + 1, 0);
+        for (uint32_t i = 0; i < N; ++i) {
+            len[i] = (uint32_t)(off[i + 1] - off[i]);
+            gmax[i / 64] = std::max(gmax[i / 64], len[i]);
+        }
+        for (uint32_t g = 0; g < G; ++g) coff[g + 1] = coff[g] + (uint64_t)gmax[g] * 64;
+        std::vector<uint16_t> cs(coff[G] + 1, CAND_PAD);
+        for (uint32_t i = 0; i < N; ++i) {
+            const uint64_t base = coff[i / 64] + (i % 64);
+            for (uint32_t t = 0; t < len[i]; ++t) cs[base + (uint64_t)t * 64] = ids[off[i] + t];
+        }
+        size_t need = Carve::bytes_for(total + 1, 2) + Carve::bytes_for(cs.size(), 2) +
+                      Carve::bytes_for(N + 1, 8) + Carve::bytes_for(G + 1, 8) + Carve::bytes_for(G + 1, 4) +
+                      Carve::bytes_for(N + 1, 4);
+        int rc = p->mem.ensure(need);
+        if (rc != NMZ_OK) return cleanup(rc);
+        Carve cv(p->mem.ptr);
+        p->d_qsym = cv.take<uint16_t>(total + 1);
+        p->d_csym = cv.take<uint16_t>(cs.size());
+        p->d_qoff = cv.take<uint64_t>(N + 1);
+        p->d_coff = cv.take<uint64_t>(G + 1);
+        p->d_gmax = cv.take<uint32_t>(G + 1);
+        p->d_len = cv.take<uint32_t>(N + 1);
+        if ((total && hipMemcpyAsync(p->d_qsym, ids.data(), total * 2, hipMemcpyHostToDevice, st)) ||
+            hipMemcpyAsync(p->d_csym, cs.data(), cs.size() * 2, hipMemcpyHostToDevice, st) ||
+            hipMemcpyAsync(p->d_qoff, off, (N + 1) * 8, hipMemcpyHostToDevice, st) ||
+            hipMemcpyAsync(p->d_coff, coff.data(), (G + 1) * 8, hipMemcpyHostToDevice, st) ||
+            hipMemcpyAsync(p->d_gmax, gmax.data(), (G + 1) * 4, hipMemcpyHostToDevice, st) ||
+            hipMemcpyAsync(p->d_len, len.data(), (N + 1) * 4, hipMemcpyHostToDevice, st) ||
+            hipStreamSynchronize(st))
+            return cleanup(fail(NMZ_EHIP, "ED plan upload failed"));
+    } else {
+        size_t need = Carve::bytes_for(N + 1, 8) + Carve::bytes_for(total + 1, 8);
+        int rc = p->mem.ensure(need);
+        if (rc != NMZ_OK) return cleanup(rc);
+        Carve cv(p->mem.ptr);
+        p->d_off64 = cv.take<uint64_t>(N + 1);
+        p->d_sym64 = cv.take<uint64_t>(total + 1);
+        if (hipMemcpyAsync(p->d_off64, off, (N + 1) * 8, hipMemcpyHostToDevice, st) ||
+            (total && hipMemcpyAsync(p->d_sym64, sym, total * 8, hipMemcpyHostToDevice, st)) ||
+            hipStreamSynchronize(st))
+            return cleanup(fail(NMZ_EHIP, "ED plan upload failed"));
+    }
+    *out = p;
+    return NMZ_OK;
+}
+
+static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_knn) {
+    const uint32_t N = p->n;
+    if (N == 0 || k == 0) return NMZ_OK;
+    hipLaunchKernelGGL(k_knn_init, dim3(ceil_div((uint64_t)N * k, 256)), dim3(256), 0, st, d_knn, (uint64_t)N * k);
+    if (p->fast) {
+        EdArgs A;
+        A.qsym = p->d_qsym;
+        A.qoff = p->d_qoff;
+        A.csym = p->d_csym;
+        A.coff = p->d_coff;
+        A.gmax = p->d_gmax;
+        A.len = p->d_len;
+        A.N = N;
+        A.G = p->G;
+        A.k = k;
+        A.knn = d_knn;
+        A.n_waves = tri_prefix(p->G, p->G);
+        uint64_t blocks = (A.n_waves + 3) / 4;
+        blocks = (blocks + 7) / 8 * 8;  // multiple of 8 for the XCD remap
+        NMZ_CHECK(blocks < (1ULL << 31), "too many traces for one launch");
+        switch (p->band) {
+            case 8: hipLaunchKernelGGL(k_ed_tile<8>, dim3((unsigned)blocks), dim3(256), 0, st, A); break;
+            case 16: hipLaunchKernelGGL(k_ed_tile<16>, dim3((unsigned)blocks), dim3(256), 0, st, A); break;
+            case 32: hipLaunchKernelGGL(k_ed_tile<32>, dim3((unsigned)blocks), dim3(256), 0, st, A); break;
+            default: return fail(NMZ_EINVAL, "internal: band has no fast kernel");
+        }
+        NMZ_HIP(hipGetLastError());
+        return NMZ_OK;
+    }
+    // generic fallback: upper-triangle pair list in chunks
+    const uint64_t total_pairs = (uint64_t)N * (N - 1) / 2;
+    const uint64_t chunk = std::min<uint64_t>(total_pairs, 1ULL << 22);
+    const unsigned gthreads = 256 * 1024;
+    DevBuf &scr = p->ctx->buf[3];
+    NMZ_TRY(scr.ensure(Carve::bytes_for(chunk * 2 + 1, 4) + Carve::bytes_for(chunk + 1, 4) +
+                       Carve::bytes_for((uint64_t)(2 * p->band + 1) * gthreads, 4)));
+    Carve cv(scr.ptr);
+    uint32_t *d_pairs = cv.take<uint32_t>(chunk * 2 + 1);
+    uint32_t *d_dist = cv.take<uint32_t>(chunk + 1);
+    uint32_t *d_row = cv.take<uint32_t>((uint64_t)(2 * p->band + 1) * gthreads);
+    for (uint64_t s = 0; s < total_pairs; s += chunk) {
+        const uint64_t c = std::min(chunk, total_pairs - s);
+        hipLaunchKernelGGL(k_pairs_upper, dim3(ceil_div(c, 256)), dim3(256), 0, st, N, s, c, d_pairs);
+        hipLaunchKernelGGL(k_ed_generic, dim3(gthreads / 256), dim3(256), 0, st, p->d_off64, p->d_sym64, d_pairs, c,
+                           p->band, d_row, d_dist);
+        hipLaunchKernelGGL(k_knn_from_pairs, dim3(ceil_div(c, 256)), dim3(256), 0, st, d_pairs, d_dist, c, d_knn, k);
+    }
+    NMZ_HIP(hipGetLastError());
+    return NMZ_OK;
+}
+
+}  // namespace nmz
+
+using namespace nmz;
+
+extern "C" {
+
+int nmz_ed_plan_create(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, uint32_t n_traces, uint32_t band,
+                       nmz_ed_plan **out) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    return ed_plan_build(ctx, off, sym, n_traces, band, out);
+}
+
+int nmz_ed_plan_destroy(nmz_ed_plan *plan) {
+    if (!plan) return NMZ_OK;
+    {
+        CtxGuard g(plan->ctx);
+        plan->mem.release();
+    }
+    delete plan;
+    return NMZ_OK;
+}
+
+int nmz_ed_plan_is_fast(const nmz_ed_plan *plan) { return plan && plan->fast ? 1 : 0; }
+
+int nmz_ed_allpairs_knn_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys, void *stream) {
+    NMZ_CHECK(plan != nullptr, "plan is NULL");
+    NMZ_CHECK(k >= 1 && k <= 64, "k must be in [1, 64]");
+    CtxGuard g(plan->ctx);
+    NMZ_TRY(g.rc);
+    return ed_knn_run(plan, stream ? (hipStream_t)stream : plan->ctx->stream, k, d_knn_keys);
+}
+
+int nmz_ed_allpairs_knn(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, uint32_t n_traces, uint32_t band,
+                        uint32_t k, uint32_t *knn_id, uint32_t *knn_dist) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    NMZ_CHECK(k <= 64, "k must be <= 64");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    if (n_traces == 0 || k == 0) return NMZ_OK;
+    nmz_ed_plan *plan = nullptr;
+    NMZ_TRY(ed_plan_build(ctx, off, sym, n_traces, band, &plan));
+    struct G {
+        nmz_ed_plan *p;
+        ~G() {
+            p->mem.release();
+            delete p;
+        }
+    } pg{plan};
+    hipStream_t st = ctx->stream;
+    const uint64_t nk = (uint64_t)n_traces * k;
+    NMZ_TRY(ctx->buf[2].ensure(Carve::bytes_for(nk, 8) + Carve::bytes_for(nk, 4) * 2));
+    Carve cv(ctx->buf[2].ptr);
+    uint64_t *d_knn = cv.take<uint64_t>(nk);
+    uint32_t *d_id = cv.take<uint32_t>(nk);
+    uint32_t *d_ds = cv.take<uint32_t>(nk);
+    NMZ_TRY(ed_knn_run(plan, st, k, d_knn));
+    hipLaunchKernelGGL(k_knn_final, dim3(ceil_div(nk, 256)), dim3(256), 0, st, d_knn, nk, d_id, d_ds);
+    NMZ_HIP(hipGetLastError());
+    if (knn_id) NMZ_HIP(hipMemcpyAsync(knn_id, d_id, nk * 4, hipMemcpyDeviceToHost, st));
+    if (knn_dist) NMZ_HIP(hipMemcpyAsync(knn_dist, d_ds, nk * 4, hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipStreamSynchronize(st));
+    return NMZ_OK;
+}
+
+int nmz_ed_pairs(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, uint32_t n_traces, const uint32_t *pairs,
+                 uint64_t n_pairs, uint32_t band, uint32_t *dist) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    NMZ_CHECK(band < (1u << 20), "band too large");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    if (n_pairs == 0) return NMZ_OK;
+    NMZ_CHECK(pairs && dist && off, "NULL argument");
+    for (uint64_t t = 0; t < 2 * n_pairs; ++t) NMZ_CHECK(pairs[t] < n_traces, "pair index out of range");
+    hipStream_t st = ctx->stream;
+    const uint64_t total = n_traces ? off[n_traces] : 0;
+    const unsigned gthreads = (unsigned)std::min<uint64_t>(256 * 1024, (n_pairs + 255) / 256 * 256);
+    NMZ_TRY(ctx->buf[4].ensure(Carve::bytes_for(n_traces + 1, 8) + Carve::bytes_for(total + 1, 8) +
+                               Carve::bytes_for(2 * n_pairs, 4) + Carve::bytes_for(n_pairs, 4) +
+                               Carve::bytes_for((uint64_t)(2 * band + 1) * gthreads, 4)));
+    Carve cv(ctx->buf[4].ptr);
+    uint64_t *d_off = cv.take<uint64_t>(n_traces + 1);
+    uint64_t *d_sym = cv.take<uint64_t>(total + 1);
+    uint32_t *d_pairs = cv.take<uint32_t>(2 * n_pairs);
+    uint32_t *d_dist = cv.take<uint32_t>(n_pairs);
+    uint32_t *d_row = cv.take<uint32_t>((uint64_t)(2 * band + 1) * gthreads);
+    NMZ_HIP(hipMemcpyAsync(d_off, off, (n_traces + 1) * 8, hipMemcpyHostToDevice, st));
+    if (total) NMZ_HIP(hipMemcpyAsync(d_sym, sym, total * 8, hipMemcpyHostToDevice, st));
+    NMZ_HIP(hipMemcpyAsync(d_pairs, pairs, 2 * n_pairs * 4, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_ed_generic, dim3(gthreads / 256), dim3(256), 0, st, d_off, d_sym, d_pairs, n_pairs, band, d_row,
+                       d_dist);
+    NMZ_HIP(hipGetLastError());
+    NMZ_HIP(hipMemcpyAsync(dist, d_dist, n_pairs * 4, hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipStreamSynchronize(st));
+    return NMZ_OK;
+}
+
+}  // extern "C"

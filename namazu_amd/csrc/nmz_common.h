@@ -1,0 +1,165 @@
+// Shared host/device definitions for libnmz_gpu.so (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <string>
+
+#include "../../include/nmz_gpu.h"
+
+// ---------------------------------------------------------------------------
+// error plumbing (thread-local message, int status codes of nmz_gpu.h)
+// ---------------------------------------------------------------------------
+namespace nmz {
+
+void set_error(const std::string &msg);
+int fail(int code, const std::string &msg);
+
+#define NMZ_HIP(call)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (call);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return ::nmz::fail(NMZ_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define NMZ_CHECK(cond, msg)                                                            \
+    do {                                                                                \
+        if (!(cond)) return ::nmz::fail(NMZ_EINVAL, (msg));                             \
+    } while (0)
+
+#define NMZ_TRY(expr)                                                                   \
+    do {                                                                                \
+        int rc_ = (expr);                                                               \
+        if (rc_ != NMZ_OK) return rc_;                                                  \
+    } while (0)
+
+// Grow-only device scratch buffer owned by a context.
+struct DevBuf {
+    void *ptr = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes);
+    void release();
+    template <typename T>
+    T *as() const { return static_cast<T *>(ptr); }
+};
+
+}  // namespace nmz
+
+struct nmz_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    int n_cu = 0;
+    // scratch slots reused across calls (host-pointer entry points)
+    nmz::DevBuf buf[16];
+};
+
+namespace nmz {
+
+// RAII: bind the calling OS thread to the context's device (cgo threads migrate).
+struct CtxGuard {
+    std::lock_guard<std::mutex> lk;
+    int rc = NMZ_OK;
+    explicit CtxGuard(nmz_ctx *c) : lk(c->mu) {
+        if (hipSetDevice(c->device) != hipSuccess) rc = fail(NMZ_EHIP, "hipSetDevice failed");
+    }
+};
+
+// ---------------------------------------------------------------------------
+// FNV-1a 64 (Go hash/fnv New64a) and the low-byte decomposition used by the
+// sweep kernels:  F_hint(h) = h * P^len + C_hint[h & 0xff]   (mod 2^64)
+// The low byte of the FNV state evolves independently of the high bits
+// (x * P mod 256 only sees x mod 256), so every XOR a hint byte applies is an
+// additive offset that depends only on h & 0xff.
+// ---------------------------------------------------------------------------
+constexpr uint64_t FNV_OFFSET = 0xcbf29ce484222325ULL;
+constexpr uint64_t FNV_PRIME = 0x100000001b3ULL;
+
+__host__ __device__ inline uint64_t fnv_step(uint64_t h, uint32_t b) {
+    return (h ^ (uint64_t)b) * FNV_PRIME;
+}
+
+__host__ __device__ inline uint64_t fnv_pow(uint32_t n) {
+    uint64_t r = 1, b = FNV_PRIME;
+    while (n) {
+        if (n & 1) r *= b;
+        b *= b;
+        n >>= 1;
+    }
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+// u64 modulus by a launch constant m.
+//   FAST   : 0 < m < 2^30, used through the carry decomposition (see replayable.hip)
+//   GENERAL: any m > 0 (u64 remainder)
+// ---------------------------------------------------------------------------
+enum ModKind : int { MOD_ZERO = 0, MOD_FAST = 1, MOD_GENERAL = 2 };
+
+struct ModParams {
+    uint64_t m;
+    uint32_t m32;
+    uint32_t k64;   // 2^64 mod m (FAST only)
+    uint32_t m_k64; // (m - k64) mod m, added when the 64-bit add carried
+    int kind;
+};
+
+inline ModParams make_mod(uint64_t m) {
+    ModParams p{};
+    p.m = m;
+    if (m == 0) {
+        p.kind = MOD_ZERO;
+    } else if (m < (1ULL << 30)) {
+        p.kind = MOD_FAST;
+        p.m32 = (uint32_t)m;
+        uint64_t k = (uint64_t)(((unsigned __int128)1 << 64) % m);
+        p.k64 = (uint32_t)k;
+        p.m_k64 = (uint32_t)((m - k) % m);
+    } else {
+        p.kind = MOD_GENERAL;
+    }
+    return p;
+}
+
+// Reduce s in [0, 3m) to [0, m) for m < 2^30 with two branch-free min steps.
+__device__ inline uint32_t reduce3m(uint32_t s, uint32_t m) {
+    s = min(s, s - m);
+    return min(s, s - m);
+}
+
+// ---------------------------------------------------------------------------
+// per-seed statistics accumulator
+// ---------------------------------------------------------------------------
+__host__ __device__ inline void stats_empty(nmz_sched_stats &s) {
+    s.sum_delay_ns = 0;
+    s.max_delay_ns = INT64_MIN;
+    s.argmax_event = NMZ_NONE;
+    s.n_fault = 0;
+    s.first_fault = NMZ_NONE;
+    s.flags = 0;
+}
+
+// ---------------------------------------------------------------------------
+// launch helpers
+// ---------------------------------------------------------------------------
+inline unsigned ceil_div(uint64_t a, uint64_t b) { return (unsigned)((a + b - 1) / b); }
+
+// seed bucketing by FNV low byte (shared by both sweeps)
+struct Buckets {
+    uint32_t *count;       // [256]
+    uint32_t *offset;      // [257]
+    uint32_t *cursor;      // [256]
+    uint32_t *n_units;     // [1]
+    uint4 *units;          // [max_units] {L, start, count, 0}
+    uint64_t *sorted_h0;   // [S]
+    uint32_t *sorted_idx;  // [S]
+};
+
+int bucket_seeds(hipStream_t st, const uint64_t *d_h0, uint64_t n_seeds, uint32_t seeds_per_unit,
+                 uint64_t max_units, Buckets &b);
+
+__global__ void k_bucket_hist(const uint64_t *h0, uint64_t n, uint32_t *count);
+
+}  // namespace nmz

@@ -1,0 +1,198 @@
+// Context management, error plumbing, parameter resolution and the seed
+// bucketing pass shared by the replayable and random sweeps.
+#include <cstdio>
+#include <cstring>
+#include <new>
+
+#include "nmz_common.h"
+
+namespace nmz {
+
+static thread_local std::string g_err;
+
+void set_error(const std::string &msg) { g_err = msg; }
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+int DevBuf::ensure(size_t bytes) {
+    if (bytes <= cap) return NMZ_OK;
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+    size_t want = bytes < 256 ? 256 : bytes;
+    if (hipMalloc(&ptr, want) != hipSuccess) {
+        ptr = nullptr;
+        return fail(NMZ_ENOMEM, "hipMalloc of " + std::to_string(want) + " bytes failed");
+    }
+    cap = want;
+    return NMZ_OK;
+}
+
+void DevBuf::release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+}
+
+// ---------------------------------------------------------------------------
+// Seed bucketing: counting sort of seeds by (FNV prefix state & 0xff), so a
+// wave's lanes share one row of the per-event tables and every table read in
+// the sweep loop is wave-uniform (scalar loads, no LDS, no gathers).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_bucket_hist(const uint64_t *__restrict__ h0, uint64_t n,
+                                                     uint32_t *__restrict__ count) {
+    __shared__ uint32_t hist[256];
+    hist[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+        atomicAdd(&hist[h0[i] & 0xff], 1u);
+    __syncthreads();
+    if (hist[threadIdx.x]) atomicAdd(&count[threadIdx.x], hist[threadIdx.x]);
+}
+
+// one block of 256 threads: exclusive scan of the 256 bucket counts and the
+// work-unit table (bucket, start, count) with units of `per_unit` seeds.
+__global__ __launch_bounds__(256) void k_bucket_scan(const uint32_t *__restrict__ count,
+                                                     uint32_t *__restrict__ offset,
+                                                     uint32_t *__restrict__ cursor,
+                                                     uint32_t per_unit, uint4 *__restrict__ units,
+                                                     uint32_t *__restrict__ n_units) {
+    __shared__ uint32_t off[257];
+    __shared__ uint32_t uoff[257];
+    const uint32_t t = threadIdx.x;
+    if (t == 0) {
+        uint32_t acc = 0, uacc = 0;
+        for (int i = 0; i < 256; ++i) {
+            off[i] = acc;
+            uoff[i] = uacc;
+            acc += count[i];
+            uacc += (count[i] + per_unit - 1) / per_unit;
+        }
+        off[256] = acc;
+        uoff[256] = uacc;
+        *n_units = uacc;
+    }
+    __syncthreads();
+    offset[t] = off[t];
+    if (t == 0) offset[256] = off[256];
+    cursor[t] = 0;
+    const uint32_t c = count[t];
+    uint32_t u = uoff[t];
+    for (uint32_t s = 0; s < c; s += per_unit, ++u)
+        units[u] = make_uint4(t, off[t] + s, min(per_unit, c - s), 0);
+}
+
+__global__ __launch_bounds__(256) void k_bucket_scatter(const uint64_t *__restrict__ h0, uint64_t n,
+                                                        const uint32_t *__restrict__ offset,
+                                                        uint32_t *__restrict__ cursor,
+                                                        uint64_t *__restrict__ sorted_h0,
+                                                        uint32_t *__restrict__ sorted_idx) {
+    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint64_t h = h0[i];
+    uint32_t L = (uint32_t)(h & 0xff);
+    uint32_t pos = offset[L] + atomicAdd(&cursor[L], 1u);
+    sorted_h0[pos] = h;
+    sorted_idx[pos] = (uint32_t)i;
+}
+
+int bucket_seeds(hipStream_t st, const uint64_t *d_h0, uint64_t n_seeds, uint32_t per_unit,
+                 uint64_t max_units, Buckets &b) {
+    (void)max_units;
+    NMZ_HIP(hipMemsetAsync(b.count, 0, 256 * sizeof(uint32_t), st));
+    if (n_seeds) {
+        unsigned grid = ceil_div(n_seeds, 256);
+        if (grid > 2048) grid = 2048;
+        hipLaunchKernelGGL(k_bucket_hist, dim3(grid), dim3(256), 0, st, d_h0, n_seeds, b.count);
+    }
+    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(256), 0, st, b.count, b.offset, b.cursor, per_unit,
+                       b.units, b.n_units);
+    if (n_seeds)
+        hipLaunchKernelGGL(k_bucket_scatter, dim3(ceil_div(n_seeds, 256)), dim3(256), 0, st, d_h0,
+                           n_seeds, b.offset, b.cursor, b.sorted_h0, b.sorted_idx);
+    NMZ_HIP(hipGetLastError());
+    return NMZ_OK;
+}
+
+}  // namespace nmz
+
+using namespace nmz;
+
+extern "C" {
+
+const char *nmz_last_error(void) { return g_err.c_str(); }
+
+int nmz_abi_version(void) { return NMZ_ABI_VERSION; }
+
+int nmz_device_count(int *count) {
+    NMZ_CHECK(count != nullptr, "count is NULL");
+    int n = 0;
+    NMZ_HIP(hipGetDeviceCount(&n));
+    *count = n;
+    return NMZ_OK;
+}
+
+int nmz_open(int device, nmz_ctx **out) {
+    NMZ_CHECK(out != nullptr, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    NMZ_HIP(hipGetDeviceCount(&n));
+    NMZ_CHECK(device >= 0 && device < n, "device ordinal out of range");
+    NMZ_HIP(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    NMZ_HIP(hipGetDeviceProperties(&prop, device));
+    NMZ_CHECK(std::strncmp(prop.gcnArchName, "gfx950", 6) == 0,
+              std::string("libnmz_gpu is built for gfx950 only, device is ") + prop.gcnArchName);
+    nmz_ctx *c = new (std::nothrow) nmz_ctx();
+    if (!c) return fail(NMZ_ENOMEM, "out of host memory");
+    c->device = device;
+    c->n_cu = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return fail(NMZ_EHIP, "hipStreamCreate failed");
+    }
+    *out = c;
+    return NMZ_OK;
+}
+
+int nmz_close(nmz_ctx *ctx) {
+    if (!ctx) return NMZ_OK;
+    {
+        CtxGuard g(ctx);
+        for (auto &b : ctx->buf) b.release();
+        if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    }
+    delete ctx;
+    return NMZ_OK;
+}
+
+int nmz_random_params_resolve(int64_t min_ns, int64_t max_ns, double p, nmz_random_params *out) {
+    NMZ_CHECK(out != nullptr, "out is NULL");
+    // randompolicy.go:223-225: "bad faultActionProbability"
+    if (!(p >= 0.0 && p <= 1.0)) {
+        char m[96];
+        std::snprintf(m, sizeof m, "bad faultActionProbability %f", p);
+        return fail(NMZ_EINVAL, m);
+    }
+    out->min_ns[0] = min_ns;
+    out->max_ns[0] = max_ns;
+    // randompolicy.go:337-339: time.Duration(float64(x) * 0.8), IEEE double, trunc toward 0
+    out->min_ns[1] = (int64_t)((double)min_ns * 0.8);
+    out->max_ns[1] = (int64_t)((double)max_ns * 0.8);
+    out->fault_threshold = (int32_t)(p * 1000.0);  // randompolicy.go:310 int(p*1000.0)
+    out->reserved = 0;
+    for (int i = 0; i < 2; ++i) {
+        if (out->min_ns[i] > out->max_ns[i]) {  // util/queue/impl.go:36-38
+            char m[128];
+            std::snprintf(m, sizeof m, "minDuration %lldns > maxDuration %lldns",
+                          (long long)out->min_ns[i], (long long)out->max_ns[i]);
+            return fail(NMZ_EINVAL, m);
+        }
+    }
+    return NMZ_OK;
+}
+
+}  // extern "C"

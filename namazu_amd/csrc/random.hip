@@ -1,0 +1,442 @@
+// K2 -- random-policy fault-injection sweep.
+//
+// Reference decision (randompolicy.go:300-316,332-346; util/queue/impl.go:94-128):
+//   (min,max) = intervals, x0.8 for prioritized entities
+//   delay = min == max ? min : rand.Int63n(max-min) + min
+//   fault = DefaultFaultAction() != nil && rand.Intn(999) < int(p*1000)
+// under the deterministic restatement: each decision
+// uses rand.New(rand.NewSource(int64(FNV1a64(le64(seed) || le64(evhash_e)))))
+// and draws the delay first, then the fault.
+//
+// Kernel structure: one seed per lane; seeds bucketed by the low byte of
+// their FNV prefix so the per-event FNV correction (same decomposition as
+// the replayable sweep, hint = le64(evhash)) is a wave-uniform scalar load;
+// the Go seed reduction uses (Hm + Cm - 4*(carry + sign)) mod (2^31-1); the
+// first two Go outputs come from closed forms (6 constant modmuls each);
+// rejected draws (probability ~1e-7 per Intn(999)) fall back to the general
+// closed form y_t, t < 607, per lane.
+#include <cstring>
+
+#include "go_rand.h"
+#include "nmz_common.h"
+#include "nmz_internal.h"
+
+namespace nmz {
+
+constexpr uint64_t MASK63 = 0x7fffffffffffffffULL;
+constexpr uint32_t INTN_N = 999;
+constexpr uint32_t INT31N_MAX = 0x7fffffffu - (0x80000000u % INTN_N);  // rand.go Int31n
+
+__constant__ uint64_t d_cooked[gorand::LEN] = NMZ_GO_RNG_COOKED_INIT;
+__device__ const gorand::PowTable d_powa = gorand::make_pow_table();
+
+// seeded vec[p] for a runtime index (slow path)
+__device__ uint64_t vec_rt(uint32_t s, int p) {
+    const uint32_t xa = gorand::modmul(s, d_powa.v[21 + 3 * p]);
+    const uint32_t xb = gorand::modmul(s, d_powa.v[22 + 3 * p]);
+    const uint32_t xc = gorand::modmul(s, d_powa.v[23 + 3 * p]);
+    const uint64_t ck = d_cooked[p];
+    const uint32_t lo = (xb << 20) ^ xc ^ (uint32_t)ck;
+    const uint32_t hi = (xa << 8) ^ (xb >> 12) ^ (uint32_t)(ck >> 32);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// y_t for 0 <= t < 607: y_t = y_{t-607} + y_{t-273}, y_s (s<0) = vec[(333-s) mod 607]
+__device__ uint64_t go_output(uint32_t s, int t) {
+    uint64_t acc = 0;
+    int u = t;
+    while (u >= 0) {
+        acc += vec_rt(s, (333 - (u - 607)) % 607);
+        u -= 273;
+    }
+    return acc + vec_rt(s, ((333 - u) % 607 + 607) % 607);
+}
+
+struct ClassParams {
+    int64_t min;
+    uint64_t n;          // max - min (0 => fixed duration, no draw)
+    uint64_t max_accept; // Int63n rejection bound
+    uint64_t mu;         // floor(2^64 / n) (Barrett), 0 if n is a power of two
+};
+
+struct RandomKParams {
+    ClassParams cls[2];
+    int32_t fault_threshold;
+};
+
+// v mod n for v < 2^63, n not a power of two, mu = floor(2^64/n)
+__device__ __forceinline__ uint64_t mod_barrett(uint64_t v, uint64_t n, uint64_t mu) {
+    const uint64_t q = __umul64hi(v, mu);
+    uint64_t r = v - q * n;
+    return r >= n ? r - n : r;
+}
+
+struct Decision {
+    int64_t delay;
+    uint32_t fault;
+    uint32_t overflow;
+};
+
+// One decision given the reduced Go seed s (1 <= s < 2^31-1) and uniform class bits.
+__device__ __forceinline__ Decision decide(uint32_t s, uint32_t cls, const RandomKParams &P) {
+    Decision d{0, 0, 0};
+    const ClassParams &cp = P.cls[cls & NMZ_EV_PRIORITIZED];
+    int t = 0;
+    if (cp.n) {
+        uint64_t v = gorand::out0(s) & MASK63;
+        t = 1;
+        if (cp.mu) {
+            while (v > cp.max_accept) {  // rare: re-draw
+                if (t >= gorand::LEN) {
+                    d.overflow = 1;
+                    break;
+                }
+                v = go_output(s, t++) & MASK63;
+            }
+            d.delay = (int64_t)mod_barrett(v, cp.n, cp.mu) + cp.min;
+        } else {
+            d.delay = (int64_t)(v & (cp.n - 1)) + cp.min;
+        }
+    } else {
+        d.delay = cp.min;
+    }
+    if (cls & NMZ_EV_FAULTABLE) {
+        uint64_t y = (t == 0) ? gorand::out0(s) : (t == 1 ? gorand::out1(s) : go_output(s, t));
+        ++t;
+        uint32_t v = (uint32_t)(y >> 32) & 0x7fffffffu;
+        while (v > INT31N_MAX) {  // rare: re-draw
+            if (t >= gorand::LEN) {
+                d.overflow = 1;
+                break;
+            }
+            v = (uint32_t)(go_output(s, t++) >> 32) & 0x7fffffffu;
+        }
+        d.fault = ((int32_t)(v % INTN_N) < P.fault_threshold) ? 1u : 0u;
+    }
+    return d;
+}
+
+// Go seed for (prefix state h0 -> H = h0 * P^8, its residue Hm = H mod M31) and
+// one table entry q = {C lo, C hi, C mod M31, class}
+__device__ __forceinline__ uint32_t go_seed_from_table(uint64_t H, uint32_t Hm, uint4 q) {
+    const uint64_t C = ((uint64_t)q.y << 32) | q.x;
+    const uint64_t u = H + C;
+    const uint32_t k = (uint32_t)(u < H) + (uint32_t)(u >> 63);  // wrap carry + sign
+    uint32_t s1 = Hm + q.z;                                      // < 2*M31
+    s1 = min(s1, s1 - gorand::M31);
+    const uint32_t dd = s1 - 4u * k;
+    uint32_t s = min(dd, dd + gorand::M31);
+    return s == 0 ? 89482311u : s;
+}
+
+// per-event table: FNV correction for hint = le64(evhash), class bits
+__global__ __launch_bounds__(256) void k_random_table(const uint64_t *__restrict__ evhash,
+                                                      const uint8_t *__restrict__ evclass, uint32_t E,
+                                                      uint4 *__restrict__ table) {
+    const uint32_t e = blockIdx.x, L = threadIdx.x;
+    const uint64_t eh = evhash[e];
+    uint64_t h = L;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h = fnv_step(h, (uint32_t)(eh >> (8 * i)) & 0xff);
+    const uint64_t C = h - (uint64_t)L * fnv_pow(8);
+    table[(uint64_t)L * E + e] = make_uint4((uint32_t)C, (uint32_t)(C >> 32), (uint32_t)(C % gorand::M31),
+                                            evclass[e]);
+}
+
+__device__ __forceinline__ uint64_t seed_prefix(uint64_t seed) {
+    uint64_t h = FNV_OFFSET;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h = fnv_step(h, (uint32_t)(seed >> (8 * i)) & 0xff);
+    return h;
+}
+
+__global__ __launch_bounds__(256) void k_random_prefix(uint64_t seed0, uint64_t n, uint64_t *__restrict__ h0) {
+    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) h0[i] = seed_prefix(seed0 + i);
+}
+
+__global__ __launch_bounds__(256) void k_random_sweep(const uint4 *__restrict__ units,
+                                                      const uint32_t *__restrict__ n_units,
+                                                      const uint64_t *__restrict__ sorted_h0,
+                                                      const uint32_t *__restrict__ sorted_idx,
+                                                      const uint4 *__restrict__ table, uint32_t E,
+                                                      RandomKParams P, nmz_sched_stats *__restrict__ stats) {
+    const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * 256 + threadIdx.x) >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (wave >= *n_units) return;
+    const uint4 u = units[wave];
+    const uint32_t L = __builtin_amdgcn_readfirstlane(u.x);
+    const uint32_t start = __builtin_amdgcn_readfirstlane(u.y);
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(u.z);
+    const bool active = lane < cnt;
+    const uint64_t h0 = active ? sorted_h0[start + lane] : 0;
+    const uint64_t H = h0 * fnv_pow(8);
+    const uint32_t Hm = (uint32_t)(H % gorand::M31);
+    const uint4 *__restrict__ row = table + (uint64_t)L * E;
+
+    uint64_t sum = 0;
+    int64_t best = INT64_MIN;
+    uint32_t arg = NMZ_NONE, nf = 0, ff = NMZ_NONE, ovf = 0;
+    for (uint32_t e = 0; e < E; ++e) {
+        const uint4 q = row[e];
+        const uint32_t cls = __builtin_amdgcn_readfirstlane(q.w);
+        const uint32_t s = go_seed_from_table(H, Hm, q);
+        const Decision d = decide(s, cls, P);
+        sum += (uint64_t)d.delay;
+        if (d.delay > best || arg == NMZ_NONE) {
+            best = d.delay;
+            arg = e;
+        }
+        nf += d.fault;
+        ff = (d.fault && ff == NMZ_NONE) ? e : ff;
+        ovf |= d.overflow;
+    }
+    if (active) {
+        nmz_sched_stats st;
+        st.sum_delay_ns = sum;
+        st.max_delay_ns = best;
+        st.argmax_event = arg;
+        st.n_fault = nf;
+        st.first_fault = ff;
+        st.flags = ovf ? NMZ_STAT_RNG_OVERFLOW : 0u;
+        stats[sorted_idx[start + lane]] = st;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_random_dump(uint64_t seed0, uint64_t n_dump, const uint4 *__restrict__ table,
+                                                     uint32_t E, RandomKParams P, int64_t *__restrict__ delays,
+                                                     uint8_t *__restrict__ faults, uint32_t *__restrict__ overflow) {
+    uint64_t idx = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= n_dump * E) return;
+    const uint64_t sidx = idx / E;
+    const uint32_t e = (uint32_t)(idx % E);
+    const uint64_t h0 = seed_prefix(seed0 + sidx);
+    const uint64_t H = h0 * fnv_pow(8);
+    const uint4 q = table[(h0 & 0xff) * E + e];
+    // direct form: int64 seed, Go's reduction, no residue shortcut
+    const uint64_t u = H + (((uint64_t)q.y << 32) | q.x);
+    const uint32_t s = gorand::seed_reduce((int64_t)u);
+    const Decision d = decide(s, q.w, P);
+    delays[idx] = d.delay;
+    faults[idx] = (uint8_t)d.fault;
+    if (d.overflow) atomicOr(overflow, 1u);
+}
+
+}  // namespace nmz
+
+struct nmz_random_plan {
+    nmz_ctx *ctx = nullptr;
+    uint32_t n_events = 0;
+    nmz::RandomKParams kp{};
+    uint4 *d_table = nullptr;
+    uint64_t max_seeds = 0;
+    nmz::DevBuf table_mem;
+    nmz::DevBuf seed_scratch;
+};
+
+namespace nmz {
+
+static int make_kparams(const nmz_random_params *p, RandomKParams &kp) {
+    NMZ_CHECK(p != nullptr, "params is NULL");
+    std::memset(&kp, 0, sizeof kp);
+    for (int i = 0; i < 2; ++i) {
+        NMZ_CHECK(p->min_ns[i] <= p->max_ns[i], "minDuration > maxDuration (util/queue/impl.go:36)");
+        ClassParams &c = kp.cls[i];
+        c.min = p->min_ns[i];
+        c.n = (uint64_t)(p->max_ns[i] - p->min_ns[i]);
+        if (c.n) {
+            NMZ_CHECK(c.n <= (uint64_t)INT64_MAX, "interval span exceeds int64");
+            if ((c.n & (c.n - 1)) == 0) {
+                c.mu = 0;
+                c.max_accept = UINT64_MAX;
+            } else {
+                c.mu = (uint64_t)(((unsigned __int128)1 << 64) / c.n);
+                c.max_accept = (uint64_t)INT64_MAX - ((1ULL << 63) % c.n);  // rand.go Int63n
+            }
+        }
+    }
+    kp.fault_threshold = p->fault_threshold;
+    return NMZ_OK;
+}
+
+static size_t random_seed_scratch_bytes(uint64_t S) {
+    return Carve::bytes_for(S, 8) * 2 + Carve::bytes_for(S, 4) + Carve::bytes_for(1024, 4) +
+           Carve::bytes_for(S / 64 + 257, 16);
+}
+
+static Buckets carve_random(void *p, uint64_t S, uint64_t **h0) {
+    Carve cv(p);
+    *h0 = cv.take<uint64_t>(S);
+    Buckets b;
+    b.sorted_h0 = cv.take<uint64_t>(S);
+    b.sorted_idx = cv.take<uint32_t>(S);
+    uint32_t *small = cv.take<uint32_t>(1024);
+    b.count = small;
+    b.offset = small + 256;
+    b.cursor = small + 256 + 260;
+    b.n_units = small + 256 + 260 + 256;
+    b.units = cv.take<uint4>(S / 64 + 257);
+    return b;
+}
+
+static int random_plan_create(nmz_ctx *ctx, const uint64_t *evhash, const uint8_t *evclass, uint32_t E,
+                              const nmz_random_params *params, uint64_t max_seeds, nmz_random_plan **out) {
+    NMZ_CHECK(ctx && out, "NULL argument");
+    NMZ_CHECK(E == 0 || (evhash && evclass), "evhash/evclass is NULL");
+    for (uint32_t e = 0; e < E; ++e)
+        NMZ_CHECK((evclass[e] & ~(NMZ_EV_PRIORITIZED | NMZ_EV_FAULTABLE)) == 0,
+                  "evclass has unknown bits (ProcSetEvent decisions are out of scope)");
+    RandomKParams kp;
+    NMZ_TRY(make_kparams(params, kp));
+    auto *p = new nmz_random_plan();
+    p->ctx = ctx;
+    p->n_events = E;
+    p->kp = kp;
+    p->max_seeds = max_seeds;
+    hipStream_t st = ctx->stream;
+    auto cleanup = [&](int code) {
+        p->table_mem.release();
+        p->seed_scratch.release();
+        delete p;
+        return code;
+    };
+    int rc = p->table_mem.ensure(Carve::bytes_for((size_t)256 * E + 1, 16) + Carve::bytes_for(E + 1, 8) +
+                                 Carve::bytes_for(E + 1, 1));
+    if (rc == NMZ_OK) rc = p->seed_scratch.ensure(random_seed_scratch_bytes(max_seeds));
+    if (rc != NMZ_OK) return cleanup(rc);
+    Carve cv(p->table_mem.ptr);
+    p->d_table = cv.take<uint4>((size_t)256 * E + 1);
+    uint64_t *d_eh = cv.take<uint64_t>(E + 1);
+    uint8_t *d_ec = cv.take<uint8_t>(E + 1);
+    if (E) {
+        if (hipMemcpyAsync(d_eh, evhash, (size_t)E * 8, hipMemcpyHostToDevice, st) ||
+            hipMemcpyAsync(d_ec, evclass, E, hipMemcpyHostToDevice, st))
+            return cleanup(fail(NMZ_EHIP, "plan upload failed"));
+        hipLaunchKernelGGL(k_random_table, dim3(E), dim3(256), 0, st, d_eh, d_ec, E, p->d_table);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+            return cleanup(fail(NMZ_EHIP, "random table kernel failed"));
+    }
+    *out = p;
+    return NMZ_OK;
+}
+
+static int random_run(nmz_random_plan *p, hipStream_t st, uint64_t seed0, uint64_t S, nmz_sched_stats *d_stats) {
+    if (S == 0) return NMZ_OK;
+    NMZ_CHECK(S <= p->max_seeds, "more seeds than the plan was created for");
+    const uint32_t E = p->n_events;
+    uint64_t *d_h0;
+    Buckets b = carve_random(p->seed_scratch.ptr, p->max_seeds, &d_h0);
+    hipLaunchKernelGGL(k_random_prefix, dim3(ceil_div(S, 256)), dim3(256), 0, st, seed0, S, d_h0);
+    const uint64_t max_units = S / 64 + 256;
+    NMZ_TRY(bucket_seeds(st, d_h0, S, 64, max_units, b));
+    hipLaunchKernelGGL(k_random_sweep, dim3(ceil_div(max_units, 4)), dim3(256), 0, st, b.units, b.n_units,
+                       b.sorted_h0, b.sorted_idx, p->d_table, E, p->kp, d_stats);
+    NMZ_HIP(hipGetLastError());
+    return NMZ_OK;
+}
+
+}  // namespace nmz
+
+using namespace nmz;
+
+extern "C" {
+
+int nmz_random_plan_create(nmz_ctx *ctx, const uint64_t *evhash, const uint8_t *evclass, uint32_t n_events,
+                           const nmz_random_params *params, uint64_t max_seeds, nmz_random_plan **out) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    NMZ_CHECK(max_seeds < (1ULL << 32), "at most 2^32-1 seeds per plan");
+    return random_plan_create(ctx, evhash, evclass, n_events, params, max_seeds, out);
+}
+
+int nmz_random_plan_destroy(nmz_random_plan *plan) {
+    if (!plan) return NMZ_OK;
+    {
+        CtxGuard g(plan->ctx);
+        plan->table_mem.release();
+        plan->seed_scratch.release();
+    }
+    delete plan;
+    return NMZ_OK;
+}
+
+int nmz_random_sweep_dev(nmz_random_plan *plan, uint64_t seed0, uint64_t n_seeds, nmz_sched_stats *d_stats,
+                         void *stream) {
+    NMZ_CHECK(plan != nullptr, "plan is NULL");
+    CtxGuard g(plan->ctx);
+    NMZ_TRY(g.rc);
+    return random_run(plan, stream ? (hipStream_t)stream : plan->ctx->stream, seed0, n_seeds, d_stats);
+}
+
+int nmz_random_sweep(nmz_ctx *ctx, uint64_t seed0, uint64_t n_seeds, const uint64_t *evhash, const uint8_t *evclass,
+                     uint32_t n_events, const nmz_random_params *params, nmz_sched_stats *stats, int64_t *delays,
+                     uint8_t *faults, uint64_t n_dump_seeds, uint32_t k, nmz_topk_entry *topk) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    NMZ_CHECK(n_dump_seeds <= n_seeds, "n_dump_seeds > n_seeds");
+    NMZ_CHECK(n_seeds < (1ULL << 32), "at most 2^32-1 seeds per call");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    hipStream_t st = ctx->stream;
+    nmz_random_plan *plan = nullptr;
+    NMZ_TRY(random_plan_create(ctx, evhash, evclass, n_events, params, n_seeds, &plan));
+    struct PlanGuard {
+        nmz_random_plan *p;
+        ~PlanGuard() {
+            p->table_mem.release();
+            p->seed_scratch.release();
+            delete p;
+        }
+    } pg{plan};
+    const uint64_t nd = n_dump_seeds * n_events;
+    const uint64_t tk_entries = topk_scratch_entries(n_seeds, k);
+    size_t need = Carve::bytes_for(n_seeds + 1, sizeof(nmz_sched_stats)) + Carve::bytes_for(nd + 1, 8) +
+                  Carve::bytes_for(nd + 1, 1) + Carve::bytes_for(4, 4) + Carve::bytes_for(tk_entries + k + 1, 24);
+    NMZ_TRY(ctx->buf[1].ensure(need));
+    Carve cv(ctx->buf[1].ptr);
+    nmz_sched_stats *d_stats = cv.take<nmz_sched_stats>(n_seeds + 1);
+    int64_t *d_del = cv.take<int64_t>(nd + 1);
+    uint8_t *d_flt = cv.take<uint8_t>(nd + 1);
+    uint32_t *d_ovf = cv.take<uint32_t>(4);
+    nmz_topk_entry *d_tk = cv.take<nmz_topk_entry>(tk_entries + k + 1);
+    NMZ_HIP(hipMemsetAsync(d_ovf, 0, 4, st));
+    if (n_events == 0) {
+        for (uint64_t i = 0; i < n_seeds && stats; ++i) stats_empty(stats[i]);
+    }
+    if (n_events) NMZ_TRY(random_run(plan, st, seed0, n_seeds, d_stats));
+    if (nd) {
+        hipLaunchKernelGGL(k_random_dump, dim3(ceil_div(nd, 256)), dim3(256), 0, st, seed0, n_dump_seeds,
+                           plan->d_table, n_events, plan->kp, d_del, d_flt, d_ovf);
+        NMZ_HIP(hipGetLastError());
+    }
+    if (k && n_events) NMZ_TRY(topk_select(st, d_stats, n_seeds, seed0, k, d_tk, d_tk + tk_entries));
+    uint32_t ovf = 0;
+    if (stats && n_seeds && n_events)
+        NMZ_HIP(hipMemcpyAsync(stats, d_stats, n_seeds * sizeof(nmz_sched_stats), hipMemcpyDeviceToHost, st));
+    if (delays && nd) NMZ_HIP(hipMemcpyAsync(delays, d_del, nd * 8, hipMemcpyDeviceToHost, st));
+    if (faults && nd) NMZ_HIP(hipMemcpyAsync(faults, d_flt, nd, hipMemcpyDeviceToHost, st));
+    if (topk && k && n_events)
+        NMZ_HIP(hipMemcpyAsync(topk, d_tk + tk_entries, k * sizeof(nmz_topk_entry), hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipMemcpyAsync(&ovf, d_ovf, 4, hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipStreamSynchronize(st));
+    if (ovf) return fail(NMZ_ERANGE, "a decision needed more than 607 Go rng outputs");
+    if (topk && k && n_events == 0) {
+        // no events: every seed ties at (0 faults, sum 0) -> smallest seeds first
+        for (uint32_t i = 0; i < k; ++i) {
+            if (i < n_seeds) {
+                topk[i].seed = seed0 + i;
+                topk[i].sum_delay_ns = 0;
+                topk[i].n_fault = 0;
+                topk[i].first_fault = NMZ_NONE;
+            } else {
+                topk[i].seed = UINT64_MAX;
+                topk[i].sum_delay_ns = INT64_MIN;
+                topk[i].n_fault = 0;
+                topk[i].first_fault = NMZ_NONE;
+            }
+        }
+    }
+    return NMZ_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,485 @@
+// K1 -- replayable-policy seed sweep (replayablepolicy.go:100-126).
+//
+//   delay(seed, event) = FNV1a64(seed || hint_e) % uint64(MaxInterval)
+//
+// Algorithm (MI355X-native, not the reference's per-event hasher):
+//  1. Per event, FNV over the hint bytes is an affine map of the incoming
+//     state h0 with a correction that depends only on h0's low byte:
+//         FNV_hint(h0) = h0 * P^len + C_e[h0 & 0xff]         (mod 2^64)
+//     A plan kernel builds C_e[L] for all 256 L (one table row per L).
+//  2. Seeds are FNV-hashed once (prefix state h0) and bucketed by h0 & 0xff,
+//     so every lane of a wave reads the same table row: table reads are
+//     wave-uniform scalar loads.
+//  3. Events are grouped by hint length; per (seed, length class) the lane
+//     precomputes H = h0*P^len, Hm = H mod m and ~H. Per decision:
+//         h = H + C (mod 2^64),  carry = C > ~H
+//         h mod m = (Hm + (C mod m) + carry*((-2^64) mod m)) mod m
+//     i.e. one 64-bit compare, a select, an add and two min-reductions.
+//  4. Per-seed statistics (sum, max with first-index argmax) accumulate in
+//     registers; the argmax tie-break uses the key (t << 32 | ~e) so the
+//     class-sorted event order still yields the first original index.
+#include <algorithm>
+#include <numeric>
+#include <vector>
+
+#include "nmz_common.h"
+#include "nmz_internal.h"
+
+namespace nmz {
+
+struct ClassInfo {
+    uint64_t pn;     // P^len
+    uint32_t start;  // first position in the length-sorted event order
+    uint32_t count;
+};
+
+}  // namespace nmz
+
+struct nmz_replayable_plan {
+    nmz_ctx *ctx = nullptr;
+    uint32_t n_events = 0;
+    int64_t max_interval = 0;
+    nmz::ModParams mod{};
+    uint32_t n_classes = 0;
+    nmz::ClassInfo *d_classes = nullptr;
+    uint4 *d_table = nullptr;          // [256][E] {C lo, C hi, C mod m, ~e}
+    uint32_t *d_pos_of_event = nullptr; // original e -> sorted position
+    uint64_t *d_pn_of_event = nullptr;  // original e -> P^len
+    uint64_t max_seeds = 0;
+    nmz::DevBuf seed_scratch;           // h0, buckets, sorted seeds
+    nmz::DevBuf plan_mem;
+};
+
+namespace nmz {
+
+constexpr int REPLAY_U = 4;  // seeds per lane
+constexpr uint32_t REPLAY_SEEDS_PER_UNIT = 64 * REPLAY_U;
+
+// ---------------------------------------------------------------------------
+// plan: per-(L, event) correction table
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_replayable_table(const uint32_t *__restrict__ hoff,
+                                                          const uint8_t *__restrict__ hbytes,
+                                                          const uint32_t *__restrict__ perm, uint32_t E,
+                                                          uint64_t m, int fast, uint4 *__restrict__ table) {
+    const uint32_t pos = blockIdx.x;  // sorted position
+    const uint32_t L = threadIdx.x;
+    const uint32_t e = perm[pos];
+    const uint32_t b0 = hoff[e], b1 = hoff[e + 1];
+    uint64_t h = L;
+    for (uint32_t i = b0; i < b1; ++i) h = fnv_step(h, hbytes[i]);
+    const uint64_t C = h - (uint64_t)L * fnv_pow(b1 - b0);
+    const uint32_t cm = fast ? (uint32_t)(C % m) : 0u;
+    table[(uint64_t)L * E + pos] = make_uint4((uint32_t)C, (uint32_t)(C >> 32), cm, ~e);
+}
+
+// ---------------------------------------------------------------------------
+// seed prefix: h0 = FNV(seed bytes)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_seed_prefix(const uint32_t *__restrict__ soff,
+                                                     const uint8_t *__restrict__ sbytes, uint64_t n,
+                                                     uint64_t *__restrict__ h0) {
+    uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= n) return;
+    uint64_t h = FNV_OFFSET;
+    for (uint32_t i = soff[s], end = soff[s + 1]; i < end; ++i) h = fnv_step(h, sbytes[i]);
+    h0[s] = h;
+}
+
+// ---------------------------------------------------------------------------
+// the sweep (MOD_FAST): one wave per work unit of up to 64*U seeds that share
+// the FNV low byte L; U seeds per lane.
+// ---------------------------------------------------------------------------
+template <int U>
+__global__ __launch_bounds__(256) void k_replayable_sweep_fast(
+    const uint4 *__restrict__ units, const uint32_t *__restrict__ n_units,
+    const uint64_t *__restrict__ sorted_h0, const uint32_t *__restrict__ sorted_idx,
+    const uint4 *__restrict__ table, uint32_t E, const ClassInfo *__restrict__ classes,
+    uint32_t n_classes, uint64_t m, uint32_t m_k64, nmz_sched_stats *__restrict__ stats) {
+    const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * 256 + threadIdx.x) >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (wave >= *n_units) return;
+    const uint4 u = units[wave];
+    const uint32_t L = __builtin_amdgcn_readfirstlane(u.x);
+    const uint32_t start = __builtin_amdgcn_readfirstlane(u.y);
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(u.z);
+    const uint32_t m32 = (uint32_t)m;
+
+    uint64_t h0[U];
+    uint32_t acc[U], sum_lo[U], sum_hi[U];
+    uint64_t key[U];
+#pragma unroll
+    for (int r = 0; r < U; ++r) {
+        const uint32_t j = lane + 64 * r;
+        h0[r] = (j < cnt) ? sorted_h0[start + j] : 0;
+        acc[r] = 0;
+        sum_lo[r] = 0;
+        sum_hi[r] = 0;
+        key[r] = 0;
+    }
+    const uint4 *__restrict__ row = table + (uint64_t)L * E;
+
+    for (uint32_t c = 0; c < n_classes; ++c) {
+        const ClassInfo ci = classes[c];
+        uint64_t nH[U];
+        uint32_t Hm[U], Hm2[U];
+#pragma unroll
+        for (int r = 0; r < U; ++r) {
+            const uint64_t H = h0[r] * ci.pn;
+            nH[r] = ~H;
+            Hm[r] = (uint32_t)(H % m);
+            Hm2[r] = reduce3m(Hm[r] + m_k64, m32);
+        }
+        const uint4 *__restrict__ q = row + ci.start;
+        uint32_t i = 0;
+        // 4 events per step: each partial sum of 4 delays (< 2^30 each) fits u32
+        for (; i + 4 <= ci.count; i += 4) {
+            uint4 qq[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) qq[t] = q[i + t];
+#pragma unroll
+            for (int r = 0; r < U; ++r) {
+                uint32_t part = 0;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const uint64_t C = ((uint64_t)qq[t].y << 32) | qq[t].x;
+                    const uint32_t base = (C > nH[r]) ? Hm2[r] : Hm[r];
+                    const uint32_t d = reduce3m(base + qq[t].z, m32);
+                    part += d;
+                    const uint64_t k = ((uint64_t)d << 32) | qq[t].w;
+                    key[r] = k > key[r] ? k : key[r];
+                }
+                const uint32_t lo = sum_lo[r] + part;
+                sum_hi[r] += (lo < part);
+                sum_lo[r] = lo;
+            }
+        }
+        for (; i < ci.count; ++i) {
+            const uint4 qq = q[i];
+            const uint64_t C = ((uint64_t)qq.y << 32) | qq.x;
+#pragma unroll
+            for (int r = 0; r < U; ++r) {
+                const uint32_t base = (C > nH[r]) ? Hm2[r] : Hm[r];
+                const uint32_t d = reduce3m(base + qq.z, m32);
+                const uint32_t lo = sum_lo[r] + d;
+                sum_hi[r] += (lo < d);
+                sum_lo[r] = lo;
+                const uint64_t k = ((uint64_t)d << 32) | qq.w;
+                key[r] = k > key[r] ? k : key[r];
+            }
+        }
+    }
+    (void)acc;
+#pragma unroll
+    for (int r = 0; r < U; ++r) {
+        const uint32_t j = lane + 64 * r;
+        if (j < cnt) {
+            nmz_sched_stats st;
+            st.sum_delay_ns = ((uint64_t)sum_hi[r] << 32) | sum_lo[r];
+            st.max_delay_ns = (int64_t)(key[r] >> 32);
+            st.argmax_event = ~(uint32_t)key[r];
+            st.n_fault = 0;
+            st.first_fault = NMZ_NONE;
+            st.flags = 0;
+            stats[sorted_idx[start + j]] = st;
+        }
+    }
+}
+
+// general modulus (m >= 2^30, including uint64(negative duration)): one seed per lane
+__global__ __launch_bounds__(256) void k_replayable_sweep_general(
+    const uint4 *__restrict__ units, const uint32_t *__restrict__ n_units,
+    const uint64_t *__restrict__ sorted_h0, const uint32_t *__restrict__ sorted_idx,
+    const uint4 *__restrict__ table, uint32_t E, const ClassInfo *__restrict__ classes,
+    uint32_t n_classes, uint64_t m, nmz_sched_stats *__restrict__ stats) {
+    const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * 256 + threadIdx.x) >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (wave >= *n_units) return;
+    const uint4 u = units[wave];
+    const uint32_t L = __builtin_amdgcn_readfirstlane(u.x);
+    const uint32_t start = __builtin_amdgcn_readfirstlane(u.y);
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(u.z);
+    const uint4 *__restrict__ row = table + (uint64_t)L * E;
+    for (uint32_t j = lane; j < cnt; j += 64) {
+        const uint64_t h0 = sorted_h0[start + j];
+        uint64_t sum = 0;
+        int64_t best = INT64_MIN;
+        uint32_t arg = NMZ_NONE;
+        for (uint32_t c = 0; c < n_classes; ++c) {
+            const ClassInfo ci = classes[c];
+            const uint64_t H = h0 * ci.pn;
+            for (uint32_t i = 0; i < ci.count; ++i) {
+                const uint4 qq = row[ci.start + i];
+                const uint64_t h = H + (((uint64_t)qq.y << 32) | qq.x);
+                const int64_t d = (int64_t)(h % m);
+                const uint32_t e = ~qq.w;
+                sum += (uint64_t)d;
+                if (arg == NMZ_NONE || d > best || (d == best && e < arg)) {
+                    best = d;
+                    arg = e;
+                }
+            }
+        }
+        nmz_sched_stats st;
+        st.sum_delay_ns = sum;
+        st.max_delay_ns = best;
+        st.argmax_event = arg;
+        st.n_fault = 0;
+        st.first_fault = NMZ_NONE;
+        st.flags = 0;
+        stats[sorted_idx[start + j]] = st;
+    }
+}
+
+// maxInterval == 0 (every delay is 0) or no events
+__global__ __launch_bounds__(256) void k_stats_constant(uint64_t n, uint32_t E,
+                                                        nmz_sched_stats *__restrict__ stats) {
+    uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= n) return;
+    nmz_sched_stats st;
+    stats_empty(st);
+    if (E) {
+        st.max_delay_ns = 0;
+        st.argmax_event = 0;
+    }
+    stats[s] = st;
+}
+
+// full per-decision dump for the first n_dump seeds (parity / debugging path)
+__global__ __launch_bounds__(256) void k_replayable_dump(const uint32_t *__restrict__ soff,
+                                                         const uint8_t *__restrict__ sbytes,
+                                                         uint64_t n_dump, const uint4 *__restrict__ table,
+                                                         uint32_t E, const uint32_t *__restrict__ pos_of,
+                                                         const uint64_t *__restrict__ pn_of, uint64_t m,
+                                                         int64_t *__restrict__ out) {
+    uint64_t idx = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= n_dump * E) return;
+    const uint64_t s = idx / E;
+    const uint32_t e = (uint32_t)(idx % E);
+    uint64_t h = FNV_OFFSET;
+    for (uint32_t i = soff[s], end = soff[s + 1]; i < end; ++i) h = fnv_step(h, sbytes[i]);
+    const uint4 q = table[(uint64_t)(h & 0xff) * E + pos_of[e]];
+    h = h * pn_of[e] + (((uint64_t)q.y << 32) | q.x);
+    out[idx] = m ? (int64_t)(h % m) : 0;
+}
+
+static size_t seed_scratch_bytes(uint64_t S) {
+    uint64_t max_units = S / REPLAY_SEEDS_PER_UNIT + 257;
+    return Carve::bytes_for(S, 8) * 2 + Carve::bytes_for(S, 4) + Carve::bytes_for(1024, 4) +
+           Carve::bytes_for(max_units, 16);
+}
+
+struct SeedScratch {
+    uint64_t *h0;
+    Buckets b;
+};
+
+static SeedScratch carve_seed_scratch(void *p, uint64_t S) {
+    Carve cv(p);
+    SeedScratch s;
+    s.h0 = cv.take<uint64_t>(S);
+    s.b.sorted_h0 = cv.take<uint64_t>(S);
+    s.b.sorted_idx = cv.take<uint32_t>(S);
+    uint32_t *small = cv.take<uint32_t>(1024);
+    s.b.count = small;
+    s.b.offset = small + 256;
+    s.b.cursor = small + 256 + 260;
+    s.b.n_units = small + 256 + 260 + 256;
+    s.b.units = cv.take<uint4>(S / REPLAY_SEEDS_PER_UNIT + 257);
+    return s;
+}
+
+// enqueue the sweep for device-resident seeds
+static int replayable_run(nmz_replayable_plan *p, hipStream_t st, const uint32_t *d_soff,
+                          const uint8_t *d_sbytes, uint64_t S, nmz_sched_stats *d_stats) {
+    if (S == 0) return NMZ_OK;
+    const uint32_t E = p->n_events;
+    if (E == 0 || p->mod.kind == MOD_ZERO) {
+        hipLaunchKernelGGL(k_stats_constant, dim3(ceil_div(S, 256)), dim3(256), 0, st, S, E, d_stats);
+        NMZ_HIP(hipGetLastError());
+        return NMZ_OK;
+    }
+    NMZ_CHECK(S <= p->max_seeds, "more seeds than the plan was created for");
+    SeedScratch sc = carve_seed_scratch(p->seed_scratch.ptr, p->max_seeds);
+    hipLaunchKernelGGL(k_seed_prefix, dim3(ceil_div(S, 256)), dim3(256), 0, st, d_soff, d_sbytes, S, sc.h0);
+    const uint64_t max_units = S / REPLAY_SEEDS_PER_UNIT + 256;
+    NMZ_TRY(bucket_seeds(st, sc.h0, S, p->mod.kind == MOD_FAST ? REPLAY_SEEDS_PER_UNIT : 64, max_units, sc.b));
+    if (p->mod.kind == MOD_FAST) {
+        hipLaunchKernelGGL(k_replayable_sweep_fast<REPLAY_U>, dim3(ceil_div(max_units, 4)), dim3(256), 0, st,
+                           sc.b.units, sc.b.n_units, sc.b.sorted_h0, sc.b.sorted_idx, p->d_table, E,
+                           p->d_classes, p->n_classes, p->mod.m, p->mod.m_k64, d_stats);
+    } else {
+        const uint64_t units64 = S / 64 + 256;
+        hipLaunchKernelGGL(k_replayable_sweep_general, dim3(ceil_div(units64, 4)), dim3(256), 0, st,
+                           sc.b.units, sc.b.n_units, sc.b.sorted_h0, sc.b.sorted_idx, p->d_table, E,
+                           p->d_classes, p->n_classes, p->mod.m, d_stats);
+    }
+    NMZ_HIP(hipGetLastError());
+    return NMZ_OK;
+}
+
+static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hint_bytes, uint32_t E,
+                       int64_t max_interval, uint64_t max_seeds, nmz_replayable_plan **out) {
+    NMZ_CHECK(ctx && out, "NULL argument");
+    NMZ_CHECK(E == 0 || hint_off, "hint_off is NULL");
+    *out = nullptr;
+    auto *p = new nmz_replayable_plan();
+    p->ctx = ctx;
+    p->n_events = E;
+    p->max_interval = max_interval;
+    p->mod = make_mod((uint64_t)max_interval);  // uint64(r.MaxInterval), replayablepolicy.go:110
+    p->max_seeds = max_seeds;
+    hipStream_t st = ctx->stream;
+
+    // length classes (stable, so original order is kept inside a class)
+    std::vector<uint32_t> perm(E), pos_of(E);
+    std::iota(perm.begin(), perm.end(), 0u);
+    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) {
+        return hint_off[a + 1] - hint_off[a] < hint_off[b + 1] - hint_off[b];
+    });
+    std::vector<ClassInfo> cls;
+    std::vector<uint64_t> pn_of(E);
+    for (uint32_t i = 0; i < E; ++i) {
+        const uint32_t e = perm[i];
+        pos_of[e] = i;
+        const uint32_t len = hint_off[e + 1] - hint_off[e];
+        pn_of[e] = fnv_pow(len);
+        if (cls.empty() || fnv_pow(len) != cls.back().pn ||
+            len != hint_off[perm[cls.back().start] + 1] - hint_off[perm[cls.back().start]])
+            cls.push_back(ClassInfo{fnv_pow(len), i, 0});
+        cls.back().count++;
+    }
+    p->n_classes = (uint32_t)cls.size();
+    const uint64_t nbytes = E ? hint_off[E] : 0;
+
+    size_t need = Carve::bytes_for(cls.size() + 1, sizeof(ClassInfo)) + Carve::bytes_for((size_t)256 * E + 1, 16) +
+                  Carve::bytes_for(E + 1, 4) * 3 + Carve::bytes_for(E + 1, 8) + Carve::bytes_for(nbytes + 1, 1);
+    int rc = p->plan_mem.ensure(need);
+    if (rc == NMZ_OK && E && p->mod.kind != MOD_ZERO) rc = p->seed_scratch.ensure(seed_scratch_bytes(max_seeds));
+    if (rc != NMZ_OK) {
+        p->plan_mem.release();
+        delete p;
+        return rc;
+    }
+    Carve cv(p->plan_mem.ptr);
+    p->d_classes = cv.take<ClassInfo>(cls.size() + 1);
+    p->d_table = cv.take<uint4>((size_t)256 * E + 1);
+    p->d_pos_of_event = cv.take<uint32_t>(E + 1);
+    uint32_t *d_perm = cv.take<uint32_t>(E + 1);
+    uint32_t *d_hoff = cv.take<uint32_t>(E + 1);
+    p->d_pn_of_event = cv.take<uint64_t>(E + 1);
+    uint8_t *d_hbytes = cv.take<uint8_t>(nbytes + 1);
+    auto cleanup = [&](int code) {
+        p->plan_mem.release();
+        p->seed_scratch.release();
+        delete p;
+        return code;
+    };
+    if (E) {
+        if (hipMemcpyAsync(p->d_classes, cls.data(), cls.size() * sizeof(ClassInfo), hipMemcpyHostToDevice, st) ||
+            hipMemcpyAsync(p->d_pos_of_event, pos_of.data(), E * 4, hipMemcpyHostToDevice, st) ||
+            hipMemcpyAsync(d_perm, perm.data(), E * 4, hipMemcpyHostToDevice, st) ||
+            hipMemcpyAsync(d_hoff, hint_off, (E + 1) * 4, hipMemcpyHostToDevice, st) ||
+            hipMemcpyAsync(p->d_pn_of_event, pn_of.data(), E * 8, hipMemcpyHostToDevice, st) ||
+            (nbytes && hipMemcpyAsync(d_hbytes, hint_bytes, nbytes, hipMemcpyHostToDevice, st)))
+            return cleanup(fail(NMZ_EHIP, "plan upload failed"));
+        hipLaunchKernelGGL(k_replayable_table, dim3(E), dim3(256), 0, st, d_hoff, d_hbytes, d_perm, E, p->mod.m,
+                           p->mod.kind == MOD_FAST ? 1 : 0, p->d_table);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+            return cleanup(fail(NMZ_EHIP, "plan table kernel failed"));
+    }
+    *out = p;
+    return NMZ_OK;
+}
+
+}  // namespace nmz
+
+using namespace nmz;
+
+extern "C" {
+
+int nmz_replayable_plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hint_bytes,
+                               uint32_t n_events, int64_t max_interval_ns, uint64_t max_seeds,
+                               nmz_replayable_plan **out) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    return plan_create(ctx, hint_off, hint_bytes, n_events, max_interval_ns, max_seeds, out);
+}
+
+int nmz_replayable_plan_destroy(nmz_replayable_plan *plan) {
+    if (!plan) return NMZ_OK;
+    {
+        CtxGuard g(plan->ctx);
+        plan->plan_mem.release();
+        plan->seed_scratch.release();
+    }
+    delete plan;
+    return NMZ_OK;
+}
+
+int nmz_replayable_sweep_dev(nmz_replayable_plan *plan, const uint32_t *d_seed_off, const uint8_t *d_seed_bytes,
+                             uint64_t n_seeds, nmz_sched_stats *d_stats, void *stream) {
+    NMZ_CHECK(plan != nullptr, "plan is NULL");
+    CtxGuard g(plan->ctx);
+    NMZ_TRY(g.rc);
+    hipStream_t st = stream ? (hipStream_t)stream : plan->ctx->stream;
+    return replayable_run(plan, st, d_seed_off, d_seed_bytes, n_seeds, d_stats);
+}
+
+int nmz_replayable_sweep(nmz_ctx *ctx, const uint32_t *seed_off, const uint8_t *seed_bytes, uint64_t n_seeds,
+                         const uint32_t *hint_off, const uint8_t *hint_bytes, uint32_t n_events,
+                         int64_t max_interval_ns, nmz_sched_stats *stats, int64_t *delays,
+                         uint64_t n_dump_seeds, uint32_t k, nmz_topk_entry *topk) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    NMZ_CHECK(n_seeds == 0 || seed_off, "seed_off is NULL");
+    NMZ_CHECK(n_dump_seeds <= n_seeds, "n_dump_seeds > n_seeds");
+    NMZ_CHECK(n_seeds < (1ULL << 32), "at most 2^32-1 seeds per call");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    hipStream_t st = ctx->stream;
+    nmz_replayable_plan *plan = nullptr;
+    NMZ_TRY(plan_create(ctx, hint_off, hint_bytes, n_events, max_interval_ns, n_seeds, &plan));
+    struct PlanGuard {
+        nmz_replayable_plan *p;
+        ~PlanGuard() {
+            p->plan_mem.release();
+            p->seed_scratch.release();
+            delete p;
+        }
+    } pg{plan};
+
+    const uint64_t sbytes = n_seeds ? seed_off[n_seeds] : 0;
+    const uint64_t tk_entries = topk_scratch_entries(n_seeds, k);
+    size_t need = Carve::bytes_for(n_seeds + 1, 4) + Carve::bytes_for(sbytes + 1, 1) +
+                  Carve::bytes_for(n_seeds + 1, sizeof(nmz_sched_stats)) +
+                  Carve::bytes_for(n_dump_seeds * n_events + 1, 8) + Carve::bytes_for(tk_entries + k + 1, 24);
+    NMZ_TRY(ctx->buf[0].ensure(need));
+    Carve cv(ctx->buf[0].ptr);
+    uint32_t *d_soff = cv.take<uint32_t>(n_seeds + 1);
+    uint8_t *d_sb = cv.take<uint8_t>(sbytes + 1);
+    nmz_sched_stats *d_stats = cv.take<nmz_sched_stats>(n_seeds + 1);
+    int64_t *d_dump = cv.take<int64_t>(n_dump_seeds * n_events + 1);
+    nmz_topk_entry *d_tk = cv.take<nmz_topk_entry>(tk_entries + k + 1);
+    if (n_seeds) {
+        NMZ_HIP(hipMemcpyAsync(d_soff, seed_off, (n_seeds + 1) * 4, hipMemcpyHostToDevice, st));
+        if (sbytes) NMZ_HIP(hipMemcpyAsync(d_sb, seed_bytes, sbytes, hipMemcpyHostToDevice, st));
+    }
+    NMZ_TRY(replayable_run(plan, st, d_soff, d_sb, n_seeds, d_stats));
+    if (n_dump_seeds && n_events) {
+        hipLaunchKernelGGL(k_replayable_dump, dim3(ceil_div(n_dump_seeds * n_events, 256)), dim3(256), 0, st, d_soff,
+                           d_sb, n_dump_seeds, plan->d_table, n_events, plan->d_pos_of_event, plan->d_pn_of_event,
+                           plan->mod.m, d_dump);
+        NMZ_HIP(hipGetLastError());
+    }
+    if (k) NMZ_TRY(topk_select(st, d_stats, n_seeds, 0, k, d_tk, d_tk + tk_entries));
+    if (stats && n_seeds)
+        NMZ_HIP(hipMemcpyAsync(stats, d_stats, n_seeds * sizeof(nmz_sched_stats), hipMemcpyDeviceToHost, st));
+    if (delays && n_dump_seeds && n_events)
+        NMZ_HIP(hipMemcpyAsync(delays, d_dump, n_dump_seeds * n_events * 8, hipMemcpyDeviceToHost, st));
+    if (topk && k) NMZ_HIP(hipMemcpyAsync(topk, d_tk + tk_entries, k * sizeof(nmz_topk_entry), hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipStreamSynchronize(st));
+    return NMZ_OK;
+}
+
+}  // extern "C"
