@@ -1,0 +1,308 @@
+#!/usr/bin/env python3
+"""bench.py -- Namazu decision engine on MI355X.
+
+Headline workload (BASELINE.json configs[1]): replayable-policy seed sweep,
+2^20 seeds x 4096-event ZooKeeper-style packet trace, maxInterval 100 ms, on
+each GPU (weak scaling: every rank sweeps its own 2^20 seeds). One step =
+  seed prefix hashing + bucketing + the K1 sweep (stats for every seed)
+  + per-rank top-64 selection (+ RCCL all_gather and merge when N > 1).
+Inputs are resident in HBM before the timed region; the per-trace plan
+(correction tables) is built once, outside it.
+
+Metric: schedule decisions/s (seeds x events / s), whole job.
+Also reported (same JSON line): the roofline of the dominant kernel
+(k_replayable_sweep_fast, HIP events on its launch stream), a CPU baseline
+(the oracle's C restatement on the host cores, bounded sample) and
+secondary lines for the random-policy sweep (configs[3]) and the banded
+edit-distance all-pairs search (configs[2]), each on a per-GPU share.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one rank per GPU, RCCL).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 78.6 T int32 lane-ops/s (2 cyc/wave64 instr/SIMD)
+PEAK_HBM_GBS = 8000.0
+MAX_INTERVAL_NS = 100_000_000
+# VALU instructions per decision in k_replayable_sweep_fast's steady-state loop
+# (4 events x 4 seeds per iteration; counted from the gfx950 ISA, cross-checked
+# with rocprofv3 SQ_INSTS_VALU in profiles/).
+REPLAY_VALU_PER_DEC = 13.0
+RANDOM_VALU_PER_DEC = 170.0  # SURVEY 8(d) declared model for the random decision
+
+
+def splitmix64(state, n):
+    out = np.zeros(n, np.uint64)
+    s = np.uint64(state)
+    with np.errstate(over="ignore"):
+        for i in range(n):
+            s = s + np.uint64(0x9E3779B97F4A7C15)
+            z = s
+            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            out[i] = z ^ (z >> np.uint64(31))
+    return out
+
+
+def zk_hints(n_events, seed=0x5EED):
+    """ZooKeeper-style replay hints: decimal signed int64 (pynmz zookeeper.py:113 format)."""
+    v = splitmix64(seed, n_events).view(np.int64)
+    return [str(int(x)) for x in v]
+
+
+def decimal_csr(lo, n):
+    from namazu_amd.explorepolicy import to_csr
+    return to_csr([str(i) for i in range(lo, lo + n)])
+
+
+def host_ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+class Dist:
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.pg = None
+
+    def init(self, torch):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local_rank))
+            self.pg = dist
+
+    def barrier(self):
+        if self.pg:
+            self.pg.barrier()
+
+    def max(self, torch, v):
+        if not self.pg:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device="cuda")
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
+        return float(t.item())
+
+
+def merge_topk(entries, k):
+    from namazu_amd._lib import TOPK_DTYPE
+    a = np.frombuffer(entries, dtype=TOPK_DTYPE)
+    order = np.lexsort((a["seed"], -a["sum_delay_ns"].astype(np.float64), -a["n_fault"].astype(np.int64)))
+    return a[order[:k]]
+
+
+def bench_replayable(args, torch, D, ctx, L, stream):
+    from namazu_amd import _lib
+    S, E = args.seeds, args.events
+    hints = zk_hints(E)
+    from namazu_amd.explorepolicy import to_csr
+    hoff, hb = to_csr(hints)
+    seed_lo = D.rank * S
+    soff, sb = decimal_csr(seed_lo, S)
+    plan = ctypes.c_void_p()
+    t0 = time.time()
+    _lib.check(L.nmz_replayable_plan_create(ctx.handle, host_ptr(hoff), host_ptr(hb), E, MAX_INTERVAL_NS, S,
+                                            ctypes.byref(plan)))
+    plan_ms = (time.time() - t0) * 1e3
+    dev = torch.device("cuda", D.local_rank)
+    d_soff = torch.from_numpy(soff.view(np.int32)).to(dev)
+    d_sb = torch.from_numpy(sb).to(dev)
+    d_stats = torch.empty(S * 32, dtype=torch.uint8, device=dev)
+    K_TOP = 64
+    d_topk = torch.empty(K_TOP * 24, dtype=torch.uint8, device=dev)
+    gathered = [torch.empty_like(d_topk) for _ in range(D.world)] if D.world > 1 else None
+
+    def step():
+        _lib.check(L.nmz_replayable_sweep_dev(plan, ctypes.c_void_p(d_soff.data_ptr()),
+                                              ctypes.c_void_p(d_sb.data_ptr()), S,
+                                              ctypes.c_void_p(d_stats.data_ptr()), stream))
+        _lib.check(L.nmz_topk_select_dev(ctx.handle, ctypes.c_void_p(d_stats.data_ptr()), S, seed_lo, K_TOP,
+                                         ctypes.c_void_p(d_topk.data_ptr()), stream))
+        if D.pg:
+            D.pg.all_gather(gathered, d_topk)
+            return gathered
+        return [d_topk]
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    _lib.check(L.nmz_timing_enable(ctx.handle, 1))
+    tot, cnt = ctypes.c_double(), ctypes.c_uint64()
+    L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
+    D.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        outs = step()
+    torch.cuda.synchronize()
+    D.barrier()
+    el = time.perf_counter() - t0
+    merged = merge_topk(b"".join(o.cpu().numpy().tobytes() for o in outs), K_TOP)
+    _lib.check(L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
+    _lib.check(L.nmz_timing_enable(ctx.handle, 0))
+    kern_ms = tot.value / max(cnt.value, 1)
+    el_max = D.max(torch, el)
+    stats = np.frombuffer(d_stats.cpu().numpy().tobytes(), dtype=_lib.SCHED_STATS_DTYPE)
+    L.nmz_replayable_plan_destroy(plan)
+    return dict(S=S, E=E, hints=(hoff, hb), seeds=(soff, sb), elapsed=el_max, kern_ms=kern_ms, plan_ms=plan_ms,
+                stats=stats, topk=merged)
+
+
+def cpu_baseline_replayable(r, args):
+    from oracle import oracle as O
+    n = min(args.cpu_seeds, r["S"])
+    soff, sb = r["seeds"]
+    so = soff[: n + 1].copy()
+    hoff, hb = r["hints"]
+    threads = min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    st, _ = O.replayable_sweep(so, sb, hoff, hb, MAX_INTERVAL_NS, nthreads=threads)
+    dt = time.perf_counter() - t0
+    parity = bool(np.array_equal(st, r["stats"][:n]))
+    return dict(value=n * r["E"] / dt, unit="decisions/s", cores=threads, kind="port",
+                sample=f"first {n} of {r['S']} seeds x {r['E']} events (oracle/nmz_oracle.c, OpenMP)",
+                parity_with_gpu=parity, seconds=round(dt, 3))
+
+
+def bench_random_secondary(args, torch, D, ctx, L, stream):
+    """configs[3] per-GPU share: 16 entities, 10k events, p=0.1, top-64."""
+    from namazu_amd import _lib
+    S = args.random_seeds
+    E = 10_000
+    ent = np.arange(E) % 16
+    evhash = splitmix64(0x5EED1, E)
+    evclass = np.where(ent < 4, _lib.NMZ_EV_PRIORITIZED, 0).astype(np.uint8) | np.uint8(_lib.NMZ_EV_FAULTABLE)
+    params = _lib.resolve_random_params(30_000_000, 100_000_000, 0.1)
+    plan = ctypes.c_void_p()
+    _lib.check(L.nmz_random_plan_create(ctx.handle, host_ptr(evhash), host_ptr(evclass), E, ctypes.byref(params), S,
+                                        ctypes.byref(plan)))
+    dev = torch.device("cuda", D.local_rank)
+    d_stats = torch.empty(S * 32, dtype=torch.uint8, device=dev)
+    seed0 = D.rank * S
+    for _ in range(1):
+        _lib.check(L.nmz_random_sweep_dev(plan, seed0, S, ctypes.c_void_p(d_stats.data_ptr()), stream))
+    torch.cuda.synchronize()
+    _lib.check(L.nmz_timing_enable(ctx.handle, 1))
+    tot, cnt = ctypes.c_double(), ctypes.c_uint64()
+    L.nmz_timing_read(ctx.handle, b"random_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
+    steps = 3
+    D.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        _lib.check(L.nmz_random_sweep_dev(plan, seed0, S, ctypes.c_void_p(d_stats.data_ptr()), stream))
+    torch.cuda.synchronize()
+    D.barrier()
+    el = D.max(torch, time.perf_counter() - t0)
+    _lib.check(L.nmz_timing_read(ctx.handle, b"random_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
+    _lib.check(L.nmz_timing_enable(ctx.handle, 0))
+    L.nmz_random_plan_destroy(plan)
+    dec = D.world * S * E * steps
+    kern_ms = tot.value / max(cnt.value, 1)
+    out = dict(metric="random-policy fault-sweep decisions/s", value=dec / el, unit="decisions/s",
+               config={"workload": "configs[3] share", "seeds_per_gpu": S, "events": E, "entities": 16,
+                       "prioritized": 4, "fault_probability": 0.1},
+               ms_per_step=el / steps * 1e3, kernel_ms=kern_ms)
+    stats = np.frombuffer(d_stats.cpu().numpy().tobytes(), dtype=_lib.SCHED_STATS_DTYPE)
+    if D.rank == 0 and args.cpu_baseline and D.world == 1:
+        from oracle import oracle as O
+        n = args.cpu_random_seeds
+        threads = min(16, os.cpu_count() or 1)
+        p = O.random_params(30_000_000, 100_000_000, 0.1)
+        t0 = time.perf_counter()
+        st, _, _ = O.random_sweep(seed0, n, evhash, evclass, p, nthreads=threads)
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = dict(value=n * E / dt, unit="decisions/s", cores=threads, kind="port",
+                                   sample=f"first {n} seeds x {E} events", seconds=round(dt, 3),
+                                   parity_with_gpu=bool(np.array_equal(st, stats[:n])))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--seeds", type=int, default=1 << 20)
+    ap.add_argument("--events", type=int, default=4096)
+    ap.add_argument("--cpu-seeds", type=int, default=1 << 18)
+    ap.add_argument("--random-seeds", type=int, default=1 << 20)
+    ap.add_argument("--cpu-random-seeds", type=int, default=256)
+    ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
+    ap.add_argument("--no-secondary", dest="secondary", action="store_false")
+    args = ap.parse_args()
+
+    import torch
+    D = Dist()
+    torch.cuda.set_device(D.local_rank)
+    D.init(torch)
+    from namazu_amd import _lib
+    L = _lib.load()
+    ctx = _lib.Context(D.local_rank)
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    r = bench_replayable(args, torch, D, ctx, L, stream)
+    decisions = D.world * r["S"] * r["E"] * args.steps
+    value = decisions / r["elapsed"]
+    kern_s = r["kern_ms"] * 1e-3
+    dec_launch = r["S"] * r["E"]
+    achieved = dec_launch * REPLAY_VALU_PER_DEC / kern_s / 1e12
+    line = {
+        "metric": "schedule decisions/sec + trace-pair edit distances/sec at 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "decisions/s",
+        "n_gpus": D.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": r["elapsed"] / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (ZooKeeper-style hints: signed decimal SplitMix64, seed 0x5EED; decimal seeds)",
+        "config": {"workload": "configs[1] replayable seed sweep", "seeds_per_gpu": r["S"], "events": r["E"],
+                   "max_interval_ns": MAX_INTERVAL_NS, "topk": 64,
+                   "parallelism": f"seed-range x{D.world}" + (" + RCCL all_gather top-k" if D.world > 1 else "")},
+        "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_VALU_TOPS, "unit": "Tops/s",
+                     "frac": achieved / PEAK_VALU_TOPS, "traffic": None,
+                     "kernel": "k_replayable_sweep_fast", "kernel_ms": r["kern_ms"],
+                     "ops_per_unit": REPLAY_VALU_PER_DEC, "units_per_launch": dec_launch,
+                     "declared_model_ops_per_unit": None},
+        "plan_ms": r["plan_ms"],
+        "topk_head": [int(x) for x in r["topk"]["seed"][:4]],
+    }
+    # survey 8(d) declared model: 6*len(hint)+18 ops per decision
+    hoff = r["hints"][0]
+    mean_len = float(np.mean(np.diff(hoff.astype(np.int64))))
+    line["roofline"]["declared_model_ops_per_unit"] = 6 * mean_len + 18
+    prof = os.path.join(HERE, "profiles", "replayable_pmc.json")
+    if os.path.exists(prof):
+        try:
+            pm = json.load(open(prof))
+            line["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            pass
+    if D.rank == 0 and D.world == 1 and args.cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_replayable(r, args)
+    if args.secondary:
+        sec = bench_random_secondary(args, torch, D, ctx, L, stream)
+        line["secondary"] = [sec]
+    if D.rank == 0:
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if D.pg:
+        D.pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -104,6 +104,11 @@ const char *nmz_last_error(void); /* thread-local, valid until the next call on 
 int nmz_abi_version(void);
 int nmz_device_count(int *count);
 
+/* Kernel timing (HIP events recorded on the launch stream around the dominant
+ * kernels: "replayable_sweep", "random_sweep", "ed_tile"). */
+int nmz_timing_enable(nmz_ctx *ctx, int on);
+int nmz_timing_read(nmz_ctx *ctx, const char *kernel, double *total_ms, uint64_t *count, int reset);
+
 /* ---- parameter resolution (host only, no device work) -------------------
  * min/max are time.Duration ns as parsed by LoadConfig; probability as float64.
  * Applies the prioritized x0.8 truncation in IEEE double exactly like
@@ -164,6 +169,10 @@ int nmz_random_plan_create(nmz_ctx *ctx, const uint64_t *evhash, const uint8_t *
 int nmz_random_plan_destroy(nmz_random_plan *plan);
 int nmz_random_sweep_dev(nmz_random_plan *plan, uint64_t seed0, uint64_t n_seeds,
                          nmz_sched_stats *d_stats, void *stream);
+
+/* Top-k selection over device-resident stats (seed value = seed0 + index). */
+int nmz_topk_select_dev(nmz_ctx *ctx, const nmz_sched_stats *d_stats, uint64_t n, uint64_t seed0,
+                        uint32_t k, nmz_topk_entry *d_out, void *stream);
 
 /* ---- trace similarity (banded Levenshtein over event-hash sequences) ------
  * Traces in CSR: off[n_traces+1] (element offsets) into sym[] (uint64 event

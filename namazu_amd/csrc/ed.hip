@@ -459,6 +459,7 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
         uint64_t blocks = (A.n_waves + 3) / 4;
         blocks = (blocks + 7) / 8 * 8;  // multiple of 8 for the XCD remap
         NMZ_CHECK(blocks < (1ULL << 31), "too many traces for one launch");
+        KernelTimer kt(p->ctx, st, "ed_tile");
         switch (p->band) {
             case 8: hipLaunchKernelGGL(k_ed_tile<8>, dim3((unsigned)blocks), dim3(256), 0, st, A); break;
             case 16: hipLaunchKernelGGL(k_ed_tile<16>, dim3((unsigned)blocks), dim3(256), 0, st, A); break;

@@ -4,8 +4,10 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <map>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/nmz_gpu.h"
 
@@ -47,6 +49,13 @@ struct DevBuf {
 
 }  // namespace nmz
 
+// Optional HIP-event timing of the dominant kernels (bench.py reads it).
+struct NmzTiming {
+    bool enabled = false;
+    std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> events;
+    std::vector<hipEvent_t> pool;
+};
+
 struct nmz_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -54,9 +63,20 @@ struct nmz_ctx {
     int n_cu = 0;
     // scratch slots reused across calls (host-pointer entry points)
     nmz::DevBuf buf[16];
+    NmzTiming timing;
 };
 
 namespace nmz {
+
+// Records start/stop events around a kernel launch when timing is enabled.
+struct KernelTimer {
+    nmz_ctx *ctx;
+    hipStream_t st;
+    const char *name;
+    hipEvent_t a = nullptr, b = nullptr;
+    KernelTimer(nmz_ctx *c, hipStream_t s, const char *n);
+    ~KernelTimer();
+};
 
 // RAII: bind the calling OS thread to the context's device (cgo threads migrate).
 struct CtxGuard {

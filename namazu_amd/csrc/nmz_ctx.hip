@@ -37,6 +37,30 @@ void DevBuf::release() {
     cap = 0;
 }
 
+static hipEvent_t timing_event(nmz_ctx *c) {
+    if (!c->timing.pool.empty()) {
+        hipEvent_t e = c->timing.pool.back();
+        c->timing.pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+KernelTimer::KernelTimer(nmz_ctx *c, hipStream_t s, const char *n) : ctx(c), st(s), name(n) {
+    if (!ctx || !ctx->timing.enabled) return;
+    a = timing_event(ctx);
+    b = timing_event(ctx);
+    if (a) (void)hipEventRecord(a, st);
+}
+
+KernelTimer::~KernelTimer() {
+    if (!a || !b) return;
+    (void)hipEventRecord(b, st);
+    ctx->timing.events[name].push_back({a, b});
+}
+
 // ---------------------------------------------------------------------------
 // Seed bucketing: counting sort of seeds by (FNV prefix state & 0xff), so a
 // wave's lanes share one row of the per-event tables and every table read in
@@ -163,9 +187,47 @@ int nmz_close(nmz_ctx *ctx) {
     {
         CtxGuard g(ctx);
         for (auto &b : ctx->buf) b.release();
+        for (auto &kv : ctx->timing.events)
+            for (auto &ab : kv.second) {
+                (void)hipEventDestroy(ab.first);
+                (void)hipEventDestroy(ab.second);
+            }
+        for (auto e : ctx->timing.pool) (void)hipEventDestroy(e);
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     }
     delete ctx;
+    return NMZ_OK;
+}
+
+int nmz_timing_enable(nmz_ctx *ctx, int on) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->timing.enabled = on != 0;
+    return NMZ_OK;
+}
+
+int nmz_timing_read(nmz_ctx *ctx, const char *kernel, double *total_ms, uint64_t *count, int reset) {
+    NMZ_CHECK(ctx && kernel && total_ms && count, "NULL argument");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    *total_ms = 0;
+    *count = 0;
+    auto it = ctx->timing.events.find(kernel);
+    if (it == ctx->timing.events.end()) return NMZ_OK;
+    for (auto &ab : it->second) {
+        NMZ_HIP(hipEventSynchronize(ab.second));
+        float ms = 0;
+        NMZ_HIP(hipEventElapsedTime(&ms, ab.first, ab.second));
+        *total_ms += ms;
+        *count += 1;
+    }
+    if (reset) {
+        for (auto &ab : it->second) {
+            ctx->timing.pool.push_back(ab.first);
+            ctx->timing.pool.push_back(ab.second);
+        }
+        it->second.clear();
+    }
     return NMZ_OK;
 }
 

@@ -329,6 +329,7 @@ static int random_run(nmz_random_plan *p, hipStream_t st, uint64_t seed0, uint64
     hipLaunchKernelGGL(k_random_prefix, dim3(ceil_div(S, 256)), dim3(256), 0, st, seed0, S, d_h0);
     const uint64_t max_units = S / 64 + 256;
     NMZ_TRY(bucket_seeds(st, d_h0, S, 64, max_units, b));
+    KernelTimer kt(p->ctx, st, "random_sweep");
     hipLaunchKernelGGL(k_random_sweep, dim3(ceil_div(max_units, 4)), dim3(256), 0, st, b.units, b.n_units,
                        b.sorted_h0, b.sorted_idx, p->d_table, E, p->kp, d_stats);
     NMZ_HIP(hipGetLastError());

@@ -304,6 +304,7 @@ static int replayable_run(nmz_replayable_plan *p, hipStream_t st, const uint32_t
     hipLaunchKernelGGL(k_seed_prefix, dim3(ceil_div(S, 256)), dim3(256), 0, st, d_soff, d_sbytes, S, sc.h0);
     const uint64_t max_units = S / REPLAY_SEEDS_PER_UNIT + 256;
     NMZ_TRY(bucket_seeds(st, sc.h0, S, p->mod.kind == MOD_FAST ? REPLAY_SEEDS_PER_UNIT : 64, max_units, sc.b));
+    KernelTimer kt(p->ctx, st, "replayable_sweep");
     if (p->mod.kind == MOD_FAST) {
         hipLaunchKernelGGL(k_replayable_sweep_fast<REPLAY_U>, dim3(ceil_div(max_units, 4)), dim3(256), 0, st,
                            sc.b.units, sc.b.n_units, sc.b.sorted_h0, sc.b.sorted_idx, p->d_table, E,

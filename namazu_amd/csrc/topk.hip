@@ -113,3 +113,16 @@ int topk_select(hipStream_t st, const nmz_sched_stats *d_stats, uint64_t n, uint
 }
 
 }  // namespace nmz
+
+using namespace nmz;
+
+extern "C" int nmz_topk_select_dev(nmz_ctx *ctx, const nmz_sched_stats *d_stats, uint64_t n, uint64_t seed0,
+                                   uint32_t k, nmz_topk_entry *d_out, void *stream) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    if (k == 0) return NMZ_OK;
+    NMZ_TRY(ctx->buf[5].ensure(topk_scratch_entries(n, k) * sizeof(nmz_topk_entry) + 256));
+    return topk_select(stream ? (hipStream_t)stream : ctx->stream, d_stats, n, seed0, k,
+                       ctx->buf[5].as<nmz_topk_entry>(), d_out);
+}
