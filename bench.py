@@ -95,10 +95,8 @@ class Dist:
 
 
 def merge_topk(entries, k):
-    from namazu_amd._lib import TOPK_DTYPE
-    a = np.frombuffer(entries, dtype=TOPK_DTYPE)
-    order = np.lexsort((a["seed"], -a["sum_delay_ns"].astype(np.float64), -a["n_fault"].astype(np.int64)))
-    return a[order[:k]]
+    from namazu_amd.dist import merge_topk as _merge
+    return _merge([entries], k)
 
 
 def bench_replayable(args, torch, D, ctx, L, stream):

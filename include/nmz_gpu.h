@@ -199,6 +199,14 @@ int nmz_ed_plan_create(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, u
 int nmz_ed_plan_destroy(nmz_ed_plan *plan);
 int nmz_ed_plan_is_fast(const nmz_ed_plan *plan);
 int nmz_ed_allpairs_knn_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys, void *stream);
+/* Multi-GPU: shard `shard` of `n_shards` processes every n_shards-th group of
+ * 32 waves (one candidate group each, equal cells per group for equal-length
+ * traces); its keys are partial lists. nmz_knn_merge_dev merges n_parts
+ * partial lists ([n_parts][n_traces][k], e.g. after an RCCL all_gather). */
+int nmz_ed_allpairs_knn_shard_dev(nmz_ed_plan *plan, uint32_t k, uint32_t shard, uint32_t n_shards,
+                                  uint64_t *d_knn_keys, void *stream);
+int nmz_knn_merge_dev(nmz_ctx *ctx, const uint64_t *d_parts, uint32_t n_parts, uint32_t n_traces,
+                      uint32_t k, uint64_t *d_out, void *stream);
 
 #ifdef __cplusplus
 }

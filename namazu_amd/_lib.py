@@ -76,6 +76,8 @@ SIGNATURES = {
     "nmz_ed_plan_destroy": (_int, [_P]),
     "nmz_ed_plan_is_fast": (_int, [_P]),
     "nmz_ed_allpairs_knn_dev": (_int, [_P, _u32, _P, _P]),
+    "nmz_ed_allpairs_knn_shard_dev": (_int, [_P, _u32, _u32, _u32, _P, _P]),
+    "nmz_knn_merge_dev": (_int, [_P, _P, _u32, _u32, _u32, _P, _P]),
     "nmz_topk_select_dev": (_int, [_P, _P, _u64, _u64, _u32, _P, _P]),
     "nmz_timing_enable": (_int, [_P, _int]),
     "nmz_timing_read": (_int, [_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),

@@ -95,7 +95,8 @@ struct EdArgs {
     const uint32_t *gmax;       // [G] padded length of each group
     const uint32_t *len;        // [N]
     uint32_t N, G, k;
-    uint64_t n_waves;
+    uint64_t n_waves;           // waves of this shard
+    uint32_t shard, n_shards;   // 32-wave groups dealt round-robin over shards
     uint64_t *knn;              // [N][k]
 };
 
@@ -108,9 +109,10 @@ __global__ __launch_bounds__(256) void k_ed_tile(EdArgs A) {
     const uint32_t nblk = gridDim.x, per_xcd = nblk / 8;
     const uint32_t hb = blockIdx.x;
     const uint32_t lb = (hb % 8) * per_xcd + hb / 8;
-    const uint64_t wave = (uint64_t)lb * 4 + (threadIdx.x >> 6);
+    const uint64_t lwave = (uint64_t)lb * 4 + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
-    if (wave >= A.n_waves) return;
+    if (lwave >= A.n_waves) return;
+    const uint64_t wave = ((lwave / 32) * A.n_shards + A.shard) * 32 + lwave % 32;
 
     // locate block b: largest b with tri_prefix(b) <= wave
     uint32_t lo = 0, hi = A.G;
@@ -439,7 +441,8 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
     return NMZ_OK;
 }
 
-static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_knn) {
+static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_knn, uint32_t shard = 0,
+                      uint32_t n_shards = 1) {
     const uint32_t N = p->n;
     if (N == 0 || k == 0) return NMZ_OK;
     hipLaunchKernelGGL(k_knn_init, dim3(ceil_div((uint64_t)N * k, 256)), dim3(256), 0, st, d_knn, (uint64_t)N * k);
@@ -455,7 +458,11 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
         A.G = p->G;
         A.k = k;
         A.knn = d_knn;
-        A.n_waves = tri_prefix(p->G, p->G);
+        const uint64_t groups = tri_prefix(p->G, p->G) / 32;
+        A.shard = shard;
+        A.n_shards = n_shards;
+        A.n_waves = (shard < groups ? (groups - shard + n_shards - 1) / n_shards : 0) * 32;
+        if (A.n_waves == 0) return NMZ_OK;
         uint64_t blocks = (A.n_waves + 3) / 4;
         blocks = (blocks + 7) / 8 * 8;  // multiple of 8 for the XCD remap
         NMZ_CHECK(blocks < (1ULL << 31), "too many traces for one launch");
@@ -480,7 +487,7 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
     uint32_t *d_pairs = cv.take<uint32_t>(chunk * 2 + 1);
     uint32_t *d_dist = cv.take<uint32_t>(chunk + 1);
     uint32_t *d_row = cv.take<uint32_t>((uint64_t)(2 * p->band + 1) * gthreads);
-    for (uint64_t s = 0; s < total_pairs; s += chunk) {
+    for (uint64_t s = (uint64_t)shard * chunk; s < total_pairs; s += (uint64_t)n_shards * chunk) {
         const uint64_t c = std::min(chunk, total_pairs - s);
         hipLaunchKernelGGL(k_pairs_upper, dim3(ceil_div(c, 256)), dim3(256), 0, st, N, s, c, d_pairs);
         hipLaunchKernelGGL(k_ed_generic, dim3(gthreads / 256), dim3(256), 0, st, p->d_off64, p->d_sym64, d_pairs, c,
@@ -518,11 +525,51 @@ int nmz_ed_plan_destroy(nmz_ed_plan *plan) {
 int nmz_ed_plan_is_fast(const nmz_ed_plan *plan) { return plan && plan->fast ? 1 : 0; }
 
 int nmz_ed_allpairs_knn_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys, void *stream) {
+    return nmz_ed_allpairs_knn_shard_dev(plan, k, 0, 1, d_knn_keys, stream);
+}
+
+int nmz_ed_allpairs_knn_shard_dev(nmz_ed_plan *plan, uint32_t k, uint32_t shard, uint32_t n_shards,
+                                  uint64_t *d_knn_keys, void *stream) {
     NMZ_CHECK(plan != nullptr, "plan is NULL");
     NMZ_CHECK(k >= 1 && k <= 64, "k must be in [1, 64]");
+    NMZ_CHECK(n_shards >= 1 && shard < n_shards, "bad shard");
     CtxGuard g(plan->ctx);
     NMZ_TRY(g.rc);
-    return ed_knn_run(plan, stream ? (hipStream_t)stream : plan->ctx->stream, k, d_knn_keys);
+    return ed_knn_run(plan, stream ? (hipStream_t)stream : plan->ctx->stream, k, d_knn_keys, shard, n_shards);
+}
+
+// merge n_parts partial k-NN key lists ([n_parts][N][k], each sorted) into [N][k]
+__global__ void k_knn_merge(const uint64_t *__restrict__ parts, uint32_t n_parts, uint32_t N, uint32_t k,
+                            uint64_t *__restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    uint32_t pos[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t s = 0; s < k; ++s) {
+        uint64_t best = UINT64_MAX;
+        uint32_t bp = 0;
+        for (uint32_t p = 0; p < n_parts; ++p) {
+            const uint64_t v = pos[p] < k ? parts[((uint64_t)p * N + i) * k + pos[p]] : UINT64_MAX;
+            if (v < best) {
+                best = v;
+                bp = p;
+            }
+        }
+        if (best != UINT64_MAX) pos[bp]++;
+        out[(uint64_t)i * k + s] = best;
+    }
+}
+
+int nmz_knn_merge_dev(nmz_ctx *ctx, const uint64_t *d_parts, uint32_t n_parts, uint32_t n_traces, uint32_t k,
+                      uint64_t *d_out, void *stream) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    NMZ_CHECK(n_parts >= 1 && n_parts <= 8, "n_parts must be in [1, 8]");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    if (n_traces == 0 || k == 0) return NMZ_OK;
+    hipLaunchKernelGGL(k_knn_merge, dim3(ceil_div(n_traces, 256)), dim3(256), 0,
+                       stream ? (hipStream_t)stream : ctx->stream, d_parts, n_parts, n_traces, k, d_out);
+    NMZ_HIP(hipGetLastError());
+    return NMZ_OK;
 }
 
 int nmz_ed_allpairs_knn(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, uint32_t n_traces, uint32_t band,

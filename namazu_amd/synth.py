@@ -1,0 +1,62 @@
+"""Synthetic inputs shaped like BASELINE.json's configs (no datasets here).
+
+* zk_hints: replay hints in pynmz's format (misc/pynmz/inspector/zookeeper.py:113,
+  str(hash(frozenset(...))) = decimal signed int64), from SplitMix64.
+* synth_traces: SURVEY 8(d) config 3 -- a ZooKeeper-style Markov base sequence
+  over 48 event symbols (the stored example traces hold 38 distinct events),
+  each trace = base + adjacent transpositions at 2% + substitutions at 0.5%,
+  fixed length; symbols are 64-bit event hashes.
+"""
+import numpy as np
+
+GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+
+
+def splitmix64(seed, n):
+    """Vectorised SplitMix64 stream (state += golden; finalize)."""
+    with np.errstate(over="ignore"):
+        s = np.uint64(seed) + GOLDEN * np.arange(1, n + 1, dtype=np.uint64)
+        z = (s ^ (s >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def zk_hints(n, seed=0x5EED):
+    return [str(int(x)) for x in splitmix64(seed, n).view(np.int64)]
+
+
+def _markov_base(length, n_symbols, rng):
+    succ = rng.integers(0, n_symbols, size=(n_symbols, 4))
+    out = np.empty(length, np.int64)
+    s = int(rng.integers(0, n_symbols))
+    for i in range(length):
+        out[i] = s
+        s = int(succ[s, rng.integers(0, 4)]) if rng.random() < 0.9 else int(rng.integers(0, n_symbols))
+    return out
+
+
+def synth_traces(n, length, seed=0x5EED, n_symbols=48, p_transpose=0.02, p_subst=0.005):
+    """Returns a historystorage.TraceSet of n traces of `length` event hashes."""
+    from .historystorage import TraceSet
+    rng = np.random.default_rng(seed)
+    base = _markov_base(length, n_symbols, rng)
+    sym_hash = splitmix64(seed ^ 0xABCDEF, n_symbols)
+    ts = TraceSet([])
+    ts.off = np.arange(n + 1, dtype=np.uint64) * np.uint64(length)
+    ids = np.empty((n, length), np.int64)
+    chunk = 4096
+    for c0 in range(0, n, chunk):
+        c = min(chunk, n - c0)
+        t = np.broadcast_to(base, (c, length)).copy()
+        # adjacent transpositions (non-overlapping: drop a swap right after another)
+        sw = rng.random((c, length - 1)) < p_transpose
+        sw[:, 1:] &= ~sw[:, :-1]
+        r, i = np.nonzero(sw)
+        a = t[r, i].copy()
+        t[r, i] = t[r, i + 1]
+        t[r, i + 1] = a
+        sub = rng.random((c, length)) < p_subst
+        t[sub] = rng.integers(0, n_symbols, size=int(sub.sum()))
+        ids[c0:c0 + c] = t
+    ts.sym = sym_hash[ids.reshape(-1)]
+    return ts

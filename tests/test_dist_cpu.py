@@ -1,0 +1,114 @@
+"""CPU (gloo, world_size 2): the N>1 path -- seed-range sharding, all_gather of
+per-rank top-k and k-NN partial lists, deterministic merges -- checked against
+the single-process oracle result."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from namazu_amd import dist as nd
+from oracle import oracle as O
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        E, S, K = 40, 300, 16
+        rng = np.random.default_rng(3)
+        eh = rng.integers(0, 2**64, size=E, dtype=np.uint64)
+        ec = rng.integers(0, 4, size=E, dtype=np.uint8)
+        p = O.random_params(30_000_000, 100_000_000, 0.3)
+        lo, hi = nd.shard_range(S, world, rank)
+        # per-rank stats from the oracle stand in for the rank's GPU sweep here
+        st, _, _ = O.random_sweep(1000 + lo, hi - lo, eh, ec, p)
+        local = O.topk_from_stats(st, 1000 + lo, K)
+        merged = nd.gather_topk(dist, local, K)
+        # k-NN partial lists: each rank computes a disjoint subset of pairs
+        N, k, w = 24, 5, 4
+        trs = [rng.integers(0, 3, rng.integers(3, 10)).astype(np.uint64) for _ in range(N)]
+        off = np.zeros(N + 1, np.uint64)
+        off[1:] = np.cumsum([len(t) for t in trs])
+        sym = np.concatenate(trs)
+        pairs = np.array([[i, j] for i in range(N) for j in range(i + 1, N)], np.uint32)
+        mine = pairs[rank::world]
+        d = O.ed_pairs(off, sym, mine, w)
+        keys = np.full((N, k), np.iinfo(np.uint64).max, np.uint64)
+        for (i, j), dd in zip(mine, d):
+            for a, b in ((i, j), (j, i)):
+                row = np.append(keys[a], np.uint64((int(dd) << 32) | int(b)))
+                keys[a] = np.sort(row)[:k]
+        import torch
+        t = torch.from_numpy(keys.view(np.uint8).reshape(-1).copy())
+        parts = nd.all_gather_bytes(dist, t)
+        merged_knn = nd.merge_knn_keys([pp.numpy().view(np.uint64).reshape(N, k) for pp in parts], k)
+        q.put((rank, merged.tobytes(), merged_knn.tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_sharded_topk_and_knn(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # reference: single-process oracle over all seeds / all pairs
+    E, S, K = 40, 300, 16
+    rng = np.random.default_rng(3)
+    eh = rng.integers(0, 2**64, size=E, dtype=np.uint64)
+    ec = rng.integers(0, 4, size=E, dtype=np.uint8)
+    st, _, _ = O.random_sweep(1000, S, eh, ec, O.random_params(30_000_000, 100_000_000, 0.3))
+    exp = O.topk_from_stats(st, 1000, K)
+    N, k, w = 24, 5, 4
+    trs = [rng.integers(0, 3, rng.integers(3, 10)).astype(np.uint64) for _ in range(N)]
+    off = np.zeros(N + 1, np.uint64)
+    off[1:] = np.cumsum([len(t) for t in trs])
+    oi, od = O.ed_allpairs_knn(off, np.concatenate(trs), w, k)
+    for rank, tk, kn in res:
+        assert np.frombuffer(tk, O.TOPK_DTYPE).tolist() == exp.tolist()
+        keys = np.frombuffer(kn, np.uint64).reshape(N, k)
+        ids = (keys & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+        ds = (keys >> np.uint64(32)).astype(np.uint32)
+        empty = keys == np.iinfo(np.uint64).max
+        ids[empty] = 0xFFFFFFFF
+        ds[empty] = 0xFFFFFFFF
+        assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+
+
+def test_shard_range_partitions():
+    for total in [0, 1, 7, 1 << 20, 10_000_001]:
+        for world in [1, 2, 3, 8]:
+            rs = [nd.shard_range(total, world, r) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == total
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+            assert max(h - l for l, h in rs) - min(h - l for l, h in rs) <= 1
+
+
+def test_merge_topk_is_order_independent():
+    a = np.zeros(5, O.TOPK_DTYPE)
+    a["seed"] = [5, 1, 9, 2, 7]
+    a["n_fault"] = [1, 2, 2, 0, 1]
+    a["sum_delay_ns"] = [10, 3, 3, 50, 10]
+    m1 = nd.merge_topk([a[:2], a[2:]], 4)
+    m2 = nd.merge_topk([a[3:], a[:3]], 4)
+    assert m1.tolist() == m2.tolist()
+    assert m1["seed"].tolist() == [1, 9, 5, 7]

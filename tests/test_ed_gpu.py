@@ -1,0 +1,151 @@
+"""GPU parity: banded edit distance (K3 fast tile kernel and the generic
+kernel), all-pairs k-NN, storage search and uniqueness, vs the CPU oracle."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from namazu_amd import _lib
+from namazu_amd import historystorage as hs
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RNG = np.random.default_rng(0xED)
+
+
+def make_traces(n, lmin, lmax, mut, alphabet=12, rng=RNG):
+    base = rng.integers(0, alphabet, size=max(lmax, 1))
+    out = []
+    for _ in range(n):
+        l = int(rng.integers(lmin, lmax + 1))
+        t = base[:l].copy()
+        m = rng.random(l) < mut
+        t[m] = rng.integers(0, alphabet, size=int(m.sum()))
+        out.append(t.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(3))
+    return hs.TraceSet(out)
+
+
+def knn(ctx, ts, w, k):
+    return hs.allpairs_knn(ts, k, w, ctx=ctx)
+
+
+@pytest.mark.parametrize("n,lmin,lmax,w,mut,k", [
+    (70, 0, 40, 8, 0.3, 6), (150, 180, 260, 32, 0.05, 8), (130, 100, 300, 16, 0.02, 5),
+    (97, 1, 70, 32, 0.5, 4), (65, 30, 30, 32, 0.0, 3), (200, 50, 90, 32, 0.1, 64),
+    (3, 5, 9, 32, 0.2, 8), (2, 0, 0, 8, 0.0, 1), (128, 500, 520, 8, 0.01, 2)])
+def test_knn_fast_kernel(ctx, n, lmin, lmax, w, mut, k):
+    ts = make_traces(n, lmin, lmax, mut)
+    ids, ds = knn(ctx, ts, w, k)
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, w, k)
+    assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+
+
+@pytest.mark.parametrize("w", [0, 1, 5, 31, 33, 100])
+def test_knn_generic_bands(ctx, w):
+    ts = make_traces(60, 0, 60, 0.2)
+    ids, ds = knn(ctx, ts, w, 5)
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, w, 5)
+    assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+
+
+def test_knn_large_alphabet_falls_back(ctx):
+    """> 65533 distinct symbols -> exact generic path."""
+    rng = np.random.default_rng(5)
+    trs = [rng.integers(0, 2**64, size=700, dtype=np.uint64) for _ in range(100)]
+    trs[7] = trs[3].copy()
+    ts = hs.TraceSet(trs)
+    ids, ds = knn(ctx, ts, 32, 2)
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, 32, 2)
+    assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+    assert ds[7][0] == 0 and ids[7][0] == 3
+
+
+def test_ed_pairs(ctx):
+    ts = make_traces(50, 0, 120, 0.1)
+    pairs = RNG.integers(0, 50, size=(2000, 2)).astype(np.uint32)
+    for w in [0, 3, 8, 32, 200]:
+        assert np.array_equal(hs.ed_pairs(ts, pairs, w, ctx=ctx), O.ed_pairs(ts.off, ts.sym, pairs, w))
+
+
+def test_ed_kat(ctx, golden):
+    pairs = golden("ed_kat.json")["pairs"]
+    ts = hs.TraceSet([np.frombuffer(p[k].encode(), np.uint8).astype(np.uint64) for p in pairs for k in "ab"])
+    idx = np.array([[2 * i, 2 * i + 1] for i in range(len(pairs))], np.uint32)
+    d = hs.ed_pairs(ts, idx, 32, ctx=ctx)
+    assert d.tolist() == [p["d"] for p in pairs]
+
+
+def test_zk_traces_golden(ctx, golden):
+    z = golden("zk_traces.json")
+    ts = hs.TraceSet([np.array([int(h, 16) for h in t["evhash"]], np.uint64) for t in z["traces"]])
+    n = len(ts)
+    pairs = np.array([[i, j] for i in range(n) for j in range(n)], np.uint32)
+    for w, mat in z["banded"].items():
+        d = hs.ed_pairs(ts, pairs, int(w), ctx=ctx).reshape(n, n)
+        assert d.tolist() == mat
+    d = hs.ed_pairs(ts, pairs, 64, ctx=ctx).reshape(n, n)
+    assert d.tolist() == z["levenshtein"]
+    for w in (8, 32):
+        ids, ds = knn(ctx, ts, w, 3)
+        oi, od = O.ed_allpairs_knn(ts.off, ts.sym, w, 3)
+        assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+
+
+def test_distance_zero_iff_equal(ctx):
+    ts = make_traces(80, 10, 40, 0.3, alphabet=3)
+    pairs = np.array([[i, j] for i in range(80) for j in range(80)], np.uint32)
+    d = hs.ed_pairs(ts, pairs, 8, ctx=ctx).reshape(80, 80)
+    for i in range(80):
+        for j in range(80):
+            assert (d[i, j] == 0) == np.array_equal(ts.trace(i), ts.trace(j))
+
+
+def test_unique_curve_and_search(ctx, tmp_path):
+    from namazu_amd.signal import Event
+    from tests.test_host import _make_storage
+    evs = [Event.packet(f"entity-{i % 3}", "a", "b", {"n": i}) for i in range(8)]
+    runs = [evs[:4], evs[1:6], evs[:4], evs[2:8], evs[1:6], evs[:3]]
+    _make_storage(str(tmp_path), runs)
+    st = hs.LoadStorage(str(tmp_path))
+    ts = st.load_all()
+    assert hs.unique_trace_curve(ts, ctx=ctx) == [1, 2, 2, 3, 3, 4]
+    t0, _ = st.GetStoredHistory(0)
+    # latest trace (id 5) is excluded, as in naive.go:238
+    assert st.Search(t0) == [0, 2]
+    assert st.SearchWithConverter(hs.SingleTrace(t0.symbols[:3]), lambda t: hs.SingleTrace(t.symbols[:3])) == [0, 2]
+    near = st.SearchSimilar(t0, 3, 8)
+    assert near[0] == (0, 0) and near[1] == (2, 0)
+
+
+def test_knn_device_plan_api(ctx):
+    import torch
+    L = _lib.load()
+    ts = make_traces(300, 150, 200, 0.03)
+    plan = ctypes.c_void_p()
+    _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), len(ts), 32, ctypes.byref(plan)))
+    assert L.nmz_ed_plan_is_fast(plan) == 1
+    k = 8
+    d_keys = torch.empty(len(ts) * k, dtype=torch.int64, device="cuda")
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(L.nmz_ed_allpairs_knn_dev(plan, k, ctypes.c_void_p(d_keys.data_ptr()), stream))
+    torch.cuda.synchronize()
+    keys = d_keys.cpu().numpy().view(np.uint64).reshape(-1, k)
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, 32, k)
+    assert np.array_equal((keys >> np.uint64(32)).astype(np.uint32), od)
+    assert np.array_equal((keys & np.uint64(0xFFFFFFFF)).astype(np.uint32), oi)
+    L.nmz_ed_plan_destroy(plan)
+
+
+def test_knn_config3_shape_sampled(ctx):
+    """configs[2] trace shape (L = 2048, w = 32, k = 8, ZK-style mutations) at
+    N = 2048: sampled brute-force parity for a few queries."""
+    from namazu_amd.synth import synth_traces
+    ts = synth_traces(2048, 2048, seed=7)
+    ids, ds = knn(ctx, ts, 32, 8)
+    for q in [0, 1, 777, 2047]:
+        pairs = np.array([[q, c] for c in range(len(ts)) if c != q], np.uint32)
+        d = O.ed_pairs(ts.off, ts.sym, pairs, 32, nthreads=8)
+        order = np.lexsort((pairs[:, 1], d))[:8]
+        assert ds[q].tolist() == d[order].tolist()
+        assert ids[q].tolist() == pairs[order, 1].tolist()

@@ -1,0 +1,234 @@
+"""GPU parity: K1 replayable sweep and K2 random sweep vs the CPU oracle,
+through the C ABI (libnmz_gpu.so). Bit-exact comparison everywhere."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from namazu_amd import _lib
+from namazu_amd.explorepolicy import Random, Replayable, to_csr
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RNG = np.random.default_rng(0xBEEF)
+
+
+def zk_hints(n, rng=RNG):
+    v = rng.integers(-2**63, 2**63 - 1, size=n, dtype=np.int64)
+    return [str(int(x)) for x in v]
+
+
+def rep_oracle(seeds, hints, m, n_dump=0):
+    so, sb = O.to_csr(seeds)
+    ho, hb = O.to_csr(hints)
+    return O.replayable_sweep(so, sb, ho, hb, m, n_dump=n_dump)
+
+
+# ---------------------------------------------------------------- K1
+def test_replayable_golden_foobar(ctx, golden):
+    for case in golden("replayable_foobar.json")["cases"]:
+        p = Replayable()
+        p.MaxInterval = case["max_interval_ns"]
+        seeds = [case["seed"]] if "seed" in case else case["seed_list"]
+        r = p.Sweep(seeds, case["hints"], n_dump=len(seeds), ctx=ctx)
+        exp = [case["delays_ns"]] if "seed" in case else case["delays_ns"]
+        assert r.delays.tolist() == exp
+
+
+@pytest.mark.parametrize("m", [100_000_000, 1_000_000_000, 10_000_000, 1, 2, 999, 2**30 - 1, 2**30, 2**30 + 5,
+                               2**62 + 11, 2**63 - 1, -5_000_000, -1, 0])
+def test_replayable_moduli(ctx, m):
+    seeds = [str(i) for i in range(700)] + ["", "foobar", "x" * 50]
+    hints = zk_hints(97) + ["", "a", "hint-entity-0-0", "z" * 33]
+    p = Replayable()
+    p.MaxInterval = m
+    r = p.Sweep(seeds, hints, n_dump=20, k=10, ctx=ctx)
+    st, dl = rep_oracle(seeds, hints, m, n_dump=20)
+    assert np.array_equal(r.stats, st)
+    assert np.array_equal(r.delays, dl)
+    assert np.array_equal(r.topk, O.topk_from_stats(st, 0, 10))
+
+
+def test_replayable_many_length_classes_and_ties(ctx):
+    """Hints of every length 0..40 (41 classes) and a tiny modulus (many ties):
+    argmax must be the first original event index."""
+    hints = ["h" * (i % 41) + str(i % 3) * (i % 2) for i in range(300)]
+    seeds = [str(i) for i in range(600)]
+    for m in [3, 7, 1000]:
+        p = Replayable()
+        p.MaxInterval = m
+        r = p.Sweep(seeds, hints, ctx=ctx)
+        st, _ = rep_oracle(seeds, hints, m)
+        assert np.array_equal(r.stats, st)
+
+
+def test_replayable_empty_inputs(ctx):
+    p = Replayable()
+    p.MaxInterval = 10_000_000
+    r = p.Sweep([], ["a"], ctx=ctx)
+    assert len(r.stats) == 0
+    r = p.Sweep(["s1", "s2"], [], k=2, ctx=ctx)
+    st, _ = rep_oracle(["s1", "s2"], [], 10_000_000)
+    assert np.array_equal(r.stats, st)
+    assert r.stats["argmax_event"].tolist() == [_lib.NMZ_NONE] * 2
+
+
+def test_replayable_bucket_boundaries(ctx):
+    """Seed counts around the 256-seed work unit and bucket sizes."""
+    hints = zk_hints(33)
+    for n in [1, 63, 64, 255, 256, 257, 4095, 20000]:
+        seeds = [f"s{i}" for i in range(n)]
+        p = Replayable()
+        p.MaxInterval = 100_000_000
+        r = p.Sweep(seeds, hints, ctx=ctx)
+        st, _ = rep_oracle(seeds, hints, 100_000_000)
+        assert np.array_equal(r.stats, st), n
+
+
+def test_replayable_full_size_properties(ctx):
+    """BASELINE configs[1] size (2^20 seeds x 4096 events): sampled bit-exact
+    parity + size-independent invariants."""
+    S, E, m = 1 << 20, 4096, 100_000_000
+    hints = zk_hints(E, np.random.default_rng(0x5EED))
+    seeds = [str(i) for i in range(S)]
+    p = Replayable()
+    p.MaxInterval = m
+    r = p.Sweep(seeds, hints, n_dump=8, k=64, ctx=ctx)
+    st = r.stats
+    assert (st["max_delay_ns"] >= 0).all() and (st["max_delay_ns"] < m).all()
+    assert (st["argmax_event"] < E).all()
+    assert (st["sum_delay_ns"] <= st["max_delay_ns"].astype(np.uint64) * np.uint64(E)).all()
+    # dump rows agree with the stats of the same seeds
+    assert np.array_equal(r.delays.sum(1).astype(np.uint64), st["sum_delay_ns"][:8])
+    assert np.array_equal(r.delays.max(1), st["max_delay_ns"][:8])
+    assert np.array_equal(r.delays.argmax(1), st["argmax_event"][:8])
+    # sampled oracle parity (first, last and scattered seeds)
+    idx = np.unique(np.concatenate([np.arange(64), np.arange(S - 64, S), RNG.integers(0, S, 256)]))
+    so, sb = O.to_csr([seeds[i] for i in idx])
+    ho, hb = O.to_csr(hints)
+    ost, _ = O.replayable_sweep(so, sb, ho, hb, m)
+    assert np.array_equal(st[idx], ost)
+    # top-k is consistent with the stats it was selected from
+    order = np.lexsort((np.arange(S), -st["sum_delay_ns"].astype(np.float64)))
+    assert r.topk["seed"].tolist() == order[:64].tolist()
+
+
+def test_replayable_device_plan_api(ctx):
+    """nmz_replayable_plan_create + nmz_replayable_sweep_dev on resident buffers."""
+    import torch
+    L = _lib.load()
+    hints = zk_hints(128)
+    seeds = [str(i) for i in range(3000)]
+    ho, hb = to_csr(hints)
+    so, sb = to_csr(seeds)
+    plan = ctypes.c_void_p()
+    _lib.check(L.nmz_replayable_plan_create(ctx.handle, _lib.ptr(ho), _lib.ptr(hb), len(hints), 100_000_000,
+                                            len(seeds), ctypes.byref(plan)))
+    d_so = torch.from_numpy(so.view(np.int32)).cuda()
+    d_sb = torch.from_numpy(sb).cuda()
+    d_st = torch.empty(len(seeds) * 32, dtype=torch.uint8, device="cuda")
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(L.nmz_replayable_sweep_dev(plan, ctypes.c_void_p(d_so.data_ptr()), ctypes.c_void_p(d_sb.data_ptr()),
+                                          len(seeds), ctypes.c_void_p(d_st.data_ptr()), stream))
+    d_tk = torch.empty(16 * 24, dtype=torch.uint8, device="cuda")
+    _lib.check(L.nmz_topk_select_dev(ctx.handle, ctypes.c_void_p(d_st.data_ptr()), len(seeds), 0, 16,
+                                     ctypes.c_void_p(d_tk.data_ptr()), stream))
+    torch.cuda.synchronize()
+    got = np.frombuffer(d_st.cpu().numpy().tobytes(), dtype=_lib.SCHED_STATS_DTYPE)
+    st, _ = rep_oracle(seeds, hints, 100_000_000)
+    assert np.array_equal(got, st)
+    tk = np.frombuffer(d_tk.cpu().numpy().tobytes(), dtype=_lib.TOPK_DTYPE)
+    assert np.array_equal(tk, O.topk_from_stats(st, 0, 16))
+    # more seeds than planned -> error, not a fault
+    rc = L.nmz_replayable_sweep_dev(plan, ctypes.c_void_p(d_so.data_ptr()), ctypes.c_void_p(d_sb.data_ptr()),
+                                    len(seeds) + 1, ctypes.c_void_p(d_st.data_ptr()), stream)
+    assert rc == _lib.NMZ_EINVAL
+    L.nmz_replayable_plan_destroy(plan)
+
+
+# ---------------------------------------------------------------- K2
+PARAMS = [(30_000_000, 100_000_000, 0.1), (5_000_000, 5_000_000, 0.5), (0, 1 << 20, 1.0),
+          (80_000_000, 3_000_000_000, 0.999), (0, 0, 0.0), (-5_000_000, 5_000_000, 0.3), (7, 9, 0.25),
+          (1, 1 + (1 << 40), 0.05)]
+
+
+@pytest.mark.parametrize("mn,mx,p", PARAMS)
+def test_random_params_grid(ctx, mn, mx, p):
+    E = 301
+    eh = RNG.integers(0, 2**64, size=E, dtype=np.uint64)
+    ec = RNG.integers(0, 4, size=E, dtype=np.uint8)
+    rp = Random()
+    rp.MinInterval, rp.MaxInterval, rp.FaultActionProbability = mn, mx, p
+    seed0 = int(RNG.integers(0, 2**63))
+    r = rp.Sweep(seed0, 600, eh, ec, n_dump=12, k=20, ctx=ctx)
+    st, dl, fl = O.random_sweep(seed0, 600, eh, ec, O.random_params(mn, mx, p), n_dump=12)
+    assert np.array_equal(r.stats, st)
+    assert np.array_equal(r.delays, dl) and np.array_equal(r.faults, fl)
+    assert np.array_equal(r.topk, O.topk_from_stats(st, seed0, 20))
+
+
+def test_random_golden_decisions(ctx, golden):
+    rp = Random()
+    for rec in golden("random_decisions.json")["decisions"]:
+        rp.MinInterval, rp.MaxInterval, rp.FaultActionProbability = rec["min_ns"], rec["max_ns"], rec["p"]
+        r = rp.Sweep(rec["seed"], 1, np.array([rec["evhash"]], np.uint64), np.array([rec["evclass"]], np.uint8),
+                     n_dump=1, ctx=ctx)
+        assert int(r.delays[0, 0]) == rec["delay_ns"]
+        assert bool(r.faults[0, 0]) == rec["fault"]
+
+
+def test_random_rejection_path(ctx):
+    """Force Go rejection re-draws: Int63n with n just above 2^62 rejects ~half the draws,
+    so many decisions take the general closed-form path (outputs t >= 2)."""
+    E = 64
+    eh = RNG.integers(0, 2**64, size=E, dtype=np.uint64)
+    ec = np.full(E, 2, np.uint8)  # faultable, not prioritized
+    rp = Random()
+    rp.MinInterval, rp.MaxInterval, rp.FaultActionProbability = 0, (1 << 62) + 1, 0.5
+    r = rp.Sweep(11, 500, eh, ec, n_dump=500, ctx=ctx)
+    st, dl, fl = O.random_sweep(11, 500, eh, ec, O.random_params(0, (1 << 62) + 1, 0.5), n_dump=500)
+    assert np.array_equal(r.stats, st) and np.array_equal(r.delays, dl) and np.array_equal(r.faults, fl)
+    # check rejection actually happened in the inputs
+    nouts = [O.random_decide(11 + s, int(eh[e]), 2, O.random_params(0, (1 << 62) + 1, 0.5))[2]
+             for s in range(20) for e in range(E)]
+    assert max(nouts) >= 3
+
+
+def test_random_edge_cases(ctx):
+    rp = Random()
+    rp.MinInterval, rp.MaxInterval, rp.FaultActionProbability = 30_000_000, 100_000_000, 0.1
+    r = rp.Sweep(0, 5, np.zeros(0, np.uint64), np.zeros(0, np.uint8), k=3, ctx=ctx)
+    assert r.stats["argmax_event"].tolist() == [_lib.NMZ_NONE] * 5
+    assert r.topk["seed"].tolist() == [0, 1, 2]
+    with pytest.raises(_lib.NmzInvalidArgument):
+        rp.Sweep(0, 5, np.zeros(2, np.uint64), np.array([4, 0], np.uint8), ctx=ctx)  # ProcSet-like class bit
+    rp.MinInterval, rp.MaxInterval = 10, 5
+    with pytest.raises(_lib.NmzInvalidArgument):
+        rp.Sweep(0, 5, np.zeros(2, np.uint64), np.zeros(2, np.uint8), ctx=ctx)
+    # seed range wrapping past 2^64
+    rp.MinInterval, rp.MaxInterval = 1, 1000
+    eh = RNG.integers(0, 2**64, size=50, dtype=np.uint64)
+    ec = RNG.integers(0, 4, size=50, dtype=np.uint8)
+    r = rp.Sweep(2**64 - 3, 7, eh, ec, ctx=ctx)
+    st, _, _ = O.random_sweep(2**64 - 3, 7, eh, ec, O.random_params(1, 1000, 0.1))
+    assert np.array_equal(r.stats, st)
+
+
+def test_random_config4_scale_sampled(ctx):
+    """configs[3] shape (16 entities, 10k events, p=0.1) at 2^18 seeds: sampled parity."""
+    E, S = 10_000, 1 << 18
+    eh = RNG.integers(0, 2**64, size=E, dtype=np.uint64)
+    ec = (np.where(np.arange(E) % 16 < 4, 1, 0) | 2).astype(np.uint8)
+    rp = Random()
+    rp.MinInterval, rp.MaxInterval, rp.FaultActionProbability = 30_000_000, 100_000_000, 0.1
+    r = rp.Sweep(1000, S, eh, ec, k=64, ctx=ctx)
+    st = r.stats
+    assert (st["flags"] == 0).all()
+    frac = st["n_fault"].mean() / E
+    assert 0.09 < frac < 0.11  # Intn(999) < 100 -> p = 100/999
+    for s in [0, 1, S // 2, S - 1]:
+        ost, _, _ = O.random_sweep(1000 + s, 1, eh, ec, O.random_params(30_000_000, 100_000_000, 0.1))
+        assert np.array_equal(st[s:s + 1], ost)
+    best = st[r.topk["seed"][0] - 1000]
+    assert best["n_fault"] == st["n_fault"].max()
