@@ -109,18 +109,42 @@ __global__ __launch_bounds__(256) void k_bucket_scan(const uint32_t *__restrict_
         units[u] = make_uint4(t, off[t] + s, min(per_unit, c - s), 0);
 }
 
+// Scatter with block-local ranks: LDS atomics rank each seed inside its
+// (block, bucket) pair and one global atomic per non-empty pair reserves the
+// range, so the 256 global cursors see <= 256 atomics per block instead of one
+// per seed. Order inside a bucket is irrelevant: results go to the original index.
+constexpr uint32_t SCATTER_PER_THREAD = 16;
+
 __global__ __launch_bounds__(256) void k_bucket_scatter(const uint64_t *__restrict__ h0, uint64_t n,
                                                         const uint32_t *__restrict__ offset,
                                                         uint32_t *__restrict__ cursor,
                                                         uint64_t *__restrict__ sorted_h0,
                                                         uint32_t *__restrict__ sorted_idx) {
-    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    uint64_t h = h0[i];
-    uint32_t L = (uint32_t)(h & 0xff);
-    uint32_t pos = offset[L] + atomicAdd(&cursor[L], 1u);
-    sorted_h0[pos] = h;
-    sorted_idx[pos] = (uint32_t)i;
+    __shared__ uint32_t cnt[256], base[256];
+    const uint32_t t = threadIdx.x;
+    cnt[t] = 0;
+    __syncthreads();
+    const uint64_t b0 = (uint64_t)blockIdx.x * 256 * SCATTER_PER_THREAD;
+    uint64_t hv[SCATTER_PER_THREAD];
+    uint32_t rk[SCATTER_PER_THREAD];
+#pragma unroll
+    for (uint32_t r = 0; r < SCATTER_PER_THREAD; ++r) {
+        const uint64_t i = b0 + (uint64_t)r * 256 + t;
+        hv[r] = i < n ? h0[i] : 0;
+        rk[r] = i < n ? atomicAdd(&cnt[hv[r] & 0xff], 1u) : 0u;
+    }
+    __syncthreads();
+    if (cnt[t]) base[t] = offset[t] + atomicAdd(&cursor[t], cnt[t]);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < SCATTER_PER_THREAD; ++r) {
+        const uint64_t i = b0 + (uint64_t)r * 256 + t;
+        if (i < n) {
+            const uint32_t pos = base[hv[r] & 0xff] + rk[r];
+            sorted_h0[pos] = hv[r];
+            sorted_idx[pos] = (uint32_t)i;
+        }
+    }
 }
 
 int bucket_seeds(hipStream_t st, const uint64_t *d_h0, uint64_t n_seeds, uint32_t per_unit,
@@ -128,15 +152,14 @@ int bucket_seeds(hipStream_t st, const uint64_t *d_h0, uint64_t n_seeds, uint32_
     (void)max_units;
     NMZ_HIP(hipMemsetAsync(b.count, 0, 256 * sizeof(uint32_t), st));
     if (n_seeds) {
-        unsigned grid = ceil_div(n_seeds, 256);
-        if (grid > 2048) grid = 2048;
+        unsigned grid = ceil_div(n_seeds, 256 * 16);
         hipLaunchKernelGGL(k_bucket_hist, dim3(grid), dim3(256), 0, st, d_h0, n_seeds, b.count);
     }
     hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(256), 0, st, b.count, b.offset, b.cursor, per_unit,
                        b.units, b.n_units);
     if (n_seeds)
-        hipLaunchKernelGGL(k_bucket_scatter, dim3(ceil_div(n_seeds, 256)), dim3(256), 0, st, d_h0,
-                           n_seeds, b.offset, b.cursor, b.sorted_h0, b.sorted_idx);
+        hipLaunchKernelGGL(k_bucket_scatter, dim3(ceil_div(n_seeds, 256 * SCATTER_PER_THREAD)), dim3(256), 0, st,
+                           d_h0, n_seeds, b.offset, b.cursor, b.sorted_h0, b.sorted_idx);
     NMZ_HIP(hipGetLastError());
     return NMZ_OK;
 }

@@ -19,6 +19,7 @@
 //     registers; the argmax tie-break uses the key (t << 32 | ~e) so the
 //     class-sorted event order still yields the first original index.
 #include <algorithm>
+#include <cstdlib>
 #include <numeric>
 #include <vector>
 
@@ -47,13 +48,23 @@ struct nmz_replayable_plan {
     uint64_t *d_pn_of_event = nullptr;  // original e -> P^len
     uint64_t max_seeds = 0;
     nmz::DevBuf seed_scratch;           // h0, buckets, sorted seeds
+    nmz::DevBuf partial;                // per-chunk partial (sum, key) per seed
     nmz::DevBuf plan_mem;
 };
 
 namespace nmz {
 
-constexpr int REPLAY_U = 4;  // seeds per lane
-constexpr uint32_t REPLAY_SEEDS_PER_UNIT = 64 * REPLAY_U;
+constexpr uint32_t REPLAY_SEEDS_PER_UNIT_MIN = 64 * 2;
+
+// seeds per lane (default 2, the fastest measured; NMZ_REPLAY_U=2|4|8 for tuning)
+static int replay_u() {
+    static int u = [] {
+        const char *e = getenv("NMZ_REPLAY_U");
+        int v = e ? atoi(e) : 2;
+        return (v == 2 || v == 4 || v == 8) ? v : 2;
+    }();
+    return u;
+}
 
 // ---------------------------------------------------------------------------
 // plan: per-(L, event) correction table
@@ -89,101 +100,209 @@ __global__ __launch_bounds__(256) void k_seed_prefix(const uint32_t *__restrict_
 // ---------------------------------------------------------------------------
 // the sweep (MOD_FAST): one wave per work unit of up to 64*U seeds that share
 // the FNV low byte L; U seeds per lane.
+//
+// Per decision (m < 2^30):
+//   carry = C > ~H                       v_cmp_gt_u64      (one 64-bit compare)
+//   s     = (carry ? Hm' : Hm) + (C % m)  v_cndmask, v_add  (s < 2m)
+//   t     = min(s, s - m)                v_sub, v_min_u32
+//   max   : 64-bit key (t << 32 | ~e) max -- first original index wins ties
+//           even though events run class-sorted; straight-line, no SALU masks
+//   sum   : u32 partial over 4 events (< 2^32 since t < 2^30), folded into u64
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t vgpr(uint32_t x) {
+    // keep a launch constant in a VGPR: VGPR-only v_sub_u32 issues at full rate,
+    // the SGPR-operand form at half rate on gfx950
+    uint32_t v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(x));
+    return v;
+}
+
+// One decision, VOP2 carry/borrow chains only (the forms gfx950 issues at
+// ~2.25 cycles; v_cmp_* and v_min/max_u32 take ~4.1, cmp64+2 selects ~5.8 --
+// tools/ubench/valu_patterns.hip):
+//   vcc = carry(H + C)            v_add_co / v_addc_co      (sums discarded)
+//   s   = (vcc ? Hm2 : Hm) + Cm   v_cndmask, v_add
+//   t   = s < m ? s : s - m       v_sub_co (borrow), v_cndmask
+//   key = max(key, t:~e)          v_sub_co / v_subb_co (64-bit borrow), 2 x v_cndmask
+//   part += t                     v_add
+__device__ __forceinline__ void decide_fast(uint32_t Hlo, uint32_t Hhi, uint32_t Hm, uint32_t Hm2, uint32_t Clo,
+                                            uint32_t Chi, uint32_t Cm, uint32_t ne, uint32_t mv, uint32_t &klo,
+                                            uint32_t &khi, uint32_t &part) {
+    uint32_t t0, t1, sv, cv;
+    asm("v_add_co_u32 %[t0], vcc, %[Clo], %[Hlo]\n\t"
+        "v_addc_co_u32 %[t1], vcc, %[Chi], %[Hhi], vcc\n\t"
+        "v_cndmask_b32 %[sv], %[Hm], %[Hm2], vcc\n\t"
+        "v_add_u32 %[sv], %[Cm], %[sv]\n\t"
+        "v_sub_co_u32 %[cv], vcc, %[sv], %[mv]\n\t"
+        "v_cndmask_b32 %[sv], %[cv], %[sv], vcc\n\t"
+        "v_sub_co_u32 %[t0], vcc, %[klo], %[ne]\n\t"
+        "v_subb_co_u32 %[t1], vcc, %[khi], %[sv], vcc\n\t"
+        "v_cndmask_b32 %[klo], %[klo], %[ne], vcc\n\t"
+        "v_cndmask_b32 %[khi], %[khi], %[sv], vcc\n\t"
+        "v_add_u32 %[part], %[part], %[sv]"
+        : [t0] "=&v"(t0), [t1] "=&v"(t1), [sv] "=&v"(sv), [cv] "=&v"(cv), [klo] "+v"(klo), [khi] "+v"(khi),
+          [part] "+v"(part)
+        : [Hlo] "v"(Hlo), [Hhi] "v"(Hhi), [Hm] "v"(Hm), [Hm2] "v"(Hm2), [Clo] "v"(Clo), [Chi] "v"(Chi),
+          [Cm] "v"(Cm), [ne] "v"(ne), [mv] "v"(mv)
+        : "vcc");
+}
+
+// Work item = (seed group of <= 64*U seeds sharing the low byte L, chunk of
+// `ec` events in the length-sorted order). Items are handed out dynamically
+// (one global atomic per item) to a persistent grid, so the last round is
+// never a half-empty second pass of whole seed groups; each item writes its
+// partial (sum, key) per seed and k_replayable_merge combines the chunks.
 template <int U>
 __global__ __launch_bounds__(256) void k_replayable_sweep_fast(
     const uint4 *__restrict__ units, const uint32_t *__restrict__ n_units,
-    const uint64_t *__restrict__ sorted_h0, const uint32_t *__restrict__ sorted_idx,
-    const uint4 *__restrict__ table, uint32_t E, const ClassInfo *__restrict__ classes,
-    uint32_t n_classes, uint64_t m, uint32_t m_k64, nmz_sched_stats *__restrict__ stats) {
-    const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * 256 + threadIdx.x) >> 6);
+    const uint64_t *__restrict__ sorted_h0, const uint4 *__restrict__ table, uint32_t E,
+    const ClassInfo *__restrict__ classes, uint32_t n_classes, uint64_t m, uint32_t m_k64, uint32_t ec,
+    uint32_t n_chunks, uint32_t *__restrict__ item_counter, uint4 *__restrict__ partial, uint64_t part_stride) {
+    // per-wave double-buffered staging of 64 table entries (1 KiB) in LDS:
+    // one coalesced 16-B load per lane fetches the next chunk while the
+    // current one is consumed through broadcast ds_read_b128.
+    __shared__ uint4 stage[4][2][64];
+    const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63;
-    if (wave >= *n_units) return;
-    const uint4 u = units[wave];
-    const uint32_t L = __builtin_amdgcn_readfirstlane(u.x);
-    const uint32_t start = __builtin_amdgcn_readfirstlane(u.y);
-    const uint32_t cnt = __builtin_amdgcn_readfirstlane(u.z);
     const uint32_t m32 = (uint32_t)m;
+    const uint32_t mv = vgpr(m32);
+    const uint32_t n_items = *n_units * n_chunks;
+    uint32_t slot = 0;
 
-    uint64_t h0[U];
-    uint32_t acc[U], sum_lo[U], sum_hi[U];
-    uint64_t key[U];
-#pragma unroll
-    for (int r = 0; r < U; ++r) {
-        const uint32_t j = lane + 64 * r;
-        h0[r] = (j < cnt) ? sorted_h0[start + j] : 0;
-        acc[r] = 0;
-        sum_lo[r] = 0;
-        sum_hi[r] = 0;
-        key[r] = 0;
-    }
-    const uint4 *__restrict__ row = table + (uint64_t)L * E;
+    for (;;) {
+        uint32_t item = 0;
+        if (lane == 0) item = atomicAdd(item_counter, 1u);
+        item = __builtin_amdgcn_readfirstlane(__shfl(item, 0, 64));
+        if (item >= n_items) break;
+        const uint32_t unit = item / n_chunks, chunk = item - unit * n_chunks;
+        const uint4 u = units[unit];
+        const uint32_t L = __builtin_amdgcn_readfirstlane(u.x);
+        const uint32_t start = __builtin_amdgcn_readfirstlane(u.y);
+        const uint32_t cnt = __builtin_amdgcn_readfirstlane(u.z);
+        const uint32_t e0 = chunk * ec, e1 = min(E, e0 + ec);
 
-    for (uint32_t c = 0; c < n_classes; ++c) {
-        const ClassInfo ci = classes[c];
-        uint64_t nH[U];
-        uint32_t Hm[U], Hm2[U];
+        uint64_t h0[U];
+        uint32_t sum_lo[U], sum_hi[U], klo[U], khi[U];  // key = max of (t << 32 | ~e); 0 = none
 #pragma unroll
         for (int r = 0; r < U; ++r) {
-            const uint64_t H = h0[r] * ci.pn;
-            nH[r] = ~H;
-            Hm[r] = (uint32_t)(H % m);
-            Hm2[r] = reduce3m(Hm[r] + m_k64, m32);
+            const uint32_t j = lane + 64 * r;
+            h0[r] = (j < cnt) ? sorted_h0[start + j] : 0;
+            sum_lo[r] = 0;
+            sum_hi[r] = 0;
+            klo[r] = 0;
+            khi[r] = 0;
         }
-        const uint4 *__restrict__ q = row + ci.start;
-        uint32_t i = 0;
-        // 4 events per step: each partial sum of 4 delays (< 2^30 each) fits u32
-        for (; i + 4 <= ci.count; i += 4) {
-            uint4 qq[4];
+        const uint4 *__restrict__ row = table + (uint64_t)L * E;
+
+        // class containing e0 (few classes: scalar scan)
+        uint32_t cc = 0;
+        ClassInfo ci = classes[0];
+        while (ci.start + ci.count <= e0) ci = classes[++cc];
+        uint32_t pos = e0;  // next event (sorted order) to stage
+        uint32_t hi_c = min(e1, ci.start + ci.count);
+        uint4 pre = (pos + lane < hi_c) ? row[pos + lane] : make_uint4(0, 0, 0, 0);
+        uint32_t Hlo[U], Hhi[U], Hm[U], Hm2[U];
+        bool fresh = true;
+        while (pos < e1) {
+            if (fresh) {
 #pragma unroll
-            for (int t = 0; t < 4; ++t) qq[t] = q[i + t];
-#pragma unroll
-            for (int r = 0; r < U; ++r) {
-                uint32_t part = 0;
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const uint64_t C = ((uint64_t)qq[t].y << 32) | qq[t].x;
-                    const uint32_t base = (C > nH[r]) ? Hm2[r] : Hm[r];
-                    const uint32_t d = reduce3m(base + qq[t].z, m32);
-                    part += d;
-                    const uint64_t k = ((uint64_t)d << 32) | qq[t].w;
-                    key[r] = k > key[r] ? k : key[r];
+                for (int r = 0; r < U; ++r) {
+                    const uint64_t H = h0[r] * ci.pn;
+                    Hlo[r] = (uint32_t)H;
+                    Hhi[r] = (uint32_t)(H >> 32);
+                    Hm[r] = (uint32_t)(H % m);
+                    const uint32_t t2 = Hm[r] + m_k64;
+                    Hm2[r] = min(t2, t2 - m32);
                 }
-                const uint32_t lo = sum_lo[r] + part;
-                sum_hi[r] += (lo < part);
-                sum_lo[r] = lo;
+                fresh = false;
+            }
+            const uint32_t n = min(64u, hi_c - pos);
+            stage[wv][slot][lane] = pre;
+            // prefetch the next staged chunk (possibly in the next class)
+            uint32_t npos = pos + n, nhi = hi_c;
+            ClassInfo nci = ci;
+            bool nfresh = false;
+            if (npos == hi_c && npos < e1) {
+                nci = classes[cc + 1];
+                nhi = min(e1, nci.start + nci.count);
+                nfresh = true;
+            }
+            if (npos < e1) pre = (npos + lane < nhi) ? row[npos + lane] : make_uint4(0, 0, 0, 0);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint4 *__restrict__ sq = stage[wv][slot];
+            const uint32_t n4 = n & ~3u;
+            for (uint32_t i = 0; i < n4; i += 4) {
+                uint4 qq[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) qq[t] = sq[i + t];
+#pragma unroll
+                for (int r = 0; r < U; ++r) {
+                    uint32_t part = 0;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        decide_fast(Hlo[r], Hhi[r], Hm[r], Hm2[r], qq[t].x, qq[t].y, qq[t].z, qq[t].w, mv, klo[r],
+                                    khi[r], part);
+                    const uint32_t lo = sum_lo[r] + part;
+                    sum_hi[r] += (lo < part);
+                    sum_lo[r] = lo;
+                }
+            }
+            for (uint32_t i = n4; i < n; ++i) {  // class / item tail (< 4 events)
+                const uint4 q1 = sq[i];
+#pragma unroll
+                for (int r = 0; r < U; ++r) {
+                    uint32_t part = 0;
+                    decide_fast(Hlo[r], Hhi[r], Hm[r], Hm2[r], q1.x, q1.y, q1.z, q1.w, mv, klo[r], khi[r], part);
+                    const uint32_t lo = sum_lo[r] + part;
+                    sum_hi[r] += (lo < part);
+                    sum_lo[r] = lo;
+                }
+            }
+            slot ^= 1;
+            pos = npos;
+            if (nfresh) {
+                ci = nci;
+                ++cc;
+                hi_c = nhi;
+                fresh = true;
             }
         }
-        for (; i < ci.count; ++i) {
-            const uint4 qq = q[i];
-            const uint64_t C = ((uint64_t)qq.y << 32) | qq.x;
+        uint4 *__restrict__ out = partial + (uint64_t)chunk * part_stride + (uint64_t)unit * (64 * U);
 #pragma unroll
-            for (int r = 0; r < U; ++r) {
-                const uint32_t base = (C > nH[r]) ? Hm2[r] : Hm[r];
-                const uint32_t d = reduce3m(base + qq.z, m32);
-                const uint32_t lo = sum_lo[r] + d;
-                sum_hi[r] += (lo < d);
-                sum_lo[r] = lo;
-                const uint64_t k = ((uint64_t)d << 32) | qq.w;
-                key[r] = k > key[r] ? k : key[r];
-            }
-        }
+        for (int r = 0; r < U; ++r) out[lane + 64 * r] = make_uint4(sum_lo[r], sum_hi[r], klo[r], khi[r]);
     }
-    (void)acc;
-#pragma unroll
-    for (int r = 0; r < U; ++r) {
-        const uint32_t j = lane + 64 * r;
-        if (j < cnt) {
-            nmz_sched_stats st;
-            st.sum_delay_ns = ((uint64_t)sum_hi[r] << 32) | sum_lo[r];
-            st.max_delay_ns = (int64_t)(key[r] >> 32);
-            st.argmax_event = ~(uint32_t)key[r];
-            st.n_fault = 0;
-            st.first_fault = NMZ_NONE;
-            st.flags = 0;
-            stats[sorted_idx[start + j]] = st;
-        }
+}
+
+// combine the per-chunk partials of every seed and scatter to the original index
+template <int U>
+__global__ __launch_bounds__(256) void k_replayable_merge(const uint4 *__restrict__ units,
+                                                          const uint32_t *__restrict__ n_units,
+                                                          const uint32_t *__restrict__ sorted_idx,
+                                                          const uint4 *__restrict__ partial, uint64_t part_stride,
+                                                          uint32_t n_chunks, nmz_sched_stats *__restrict__ stats) {
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t unit = g / (64 * U);
+    const uint32_t j = (uint32_t)(g - unit * (64 * U));
+    if (unit >= *n_units) return;
+    const uint4 u = units[unit];
+    if (j >= u.z) return;
+    uint64_t sum = 0, key = 0;
+    for (uint32_t c = 0; c < n_chunks; ++c) {
+        const uint4 p = partial[(uint64_t)c * part_stride + g];
+        sum += ((uint64_t)p.y << 32) | p.x;
+        const uint64_t k = ((uint64_t)p.w << 32) | p.z;
+        key = k > key ? k : key;
     }
+    nmz_sched_stats st;
+    st.sum_delay_ns = sum;
+    st.max_delay_ns = (int64_t)(key >> 32);
+    st.argmax_event = ~(uint32_t)key;
+    st.n_fault = 0;
+    st.first_fault = NMZ_NONE;
+    st.flags = 0;
+    stats[sorted_idx[u.y + j]] = st;
 }
 
 // general modulus (m >= 2^30, including uint64(negative duration)): one seed per lane
@@ -263,15 +382,33 @@ __global__ __launch_bounds__(256) void k_replayable_dump(const uint32_t *__restr
     out[idx] = m ? (int64_t)(h % m) : 0;
 }
 
+constexpr uint32_t REPLAY_EC = 1024;  // events per work item
+
+static uint32_t replay_ec() {
+    static uint32_t ec = [] {
+        const char *e = getenv("NMZ_REPLAY_EC");
+        uint32_t v = e ? (uint32_t)atoi(e) : REPLAY_EC;
+        return (v >= 64 && v % 64 == 0) ? v : REPLAY_EC;
+    }();
+    return ec;
+}
+
 static size_t seed_scratch_bytes(uint64_t S) {
-    uint64_t max_units = S / REPLAY_SEEDS_PER_UNIT + 257;
+    uint64_t max_units = S / REPLAY_SEEDS_PER_UNIT_MIN + 257;
     return Carve::bytes_for(S, 8) * 2 + Carve::bytes_for(S, 4) + Carve::bytes_for(1024, 4) +
-           Carve::bytes_for(max_units, 16);
+           Carve::bytes_for(max_units, 16) + Carve::bytes_for(4, 4);
+}
+
+static size_t partial_bytes(uint64_t S, uint32_t E, int U, uint32_t ec) {
+    const uint64_t units = S / (64 * (uint64_t)U) + 257;
+    const uint64_t chunks = (E + ec - 1) / ec;
+    return Carve::bytes_for(units * 64 * U * chunks, 16);
 }
 
 struct SeedScratch {
     uint64_t *h0;
     Buckets b;
+    uint32_t *counter;
 };
 
 static SeedScratch carve_seed_scratch(void *p, uint64_t S) {
@@ -285,7 +422,8 @@ static SeedScratch carve_seed_scratch(void *p, uint64_t S) {
     s.b.offset = small + 256;
     s.b.cursor = small + 256 + 260;
     s.b.n_units = small + 256 + 260 + 256;
-    s.b.units = cv.take<uint4>(S / REPLAY_SEEDS_PER_UNIT + 257);
+    s.b.units = cv.take<uint4>(S / REPLAY_SEEDS_PER_UNIT_MIN + 257);
+    s.counter = cv.take<uint32_t>(4);
     return s;
 }
 
@@ -302,14 +440,38 @@ static int replayable_run(nmz_replayable_plan *p, hipStream_t st, const uint32_t
     NMZ_CHECK(S <= p->max_seeds, "more seeds than the plan was created for");
     SeedScratch sc = carve_seed_scratch(p->seed_scratch.ptr, p->max_seeds);
     hipLaunchKernelGGL(k_seed_prefix, dim3(ceil_div(S, 256)), dim3(256), 0, st, d_soff, d_sbytes, S, sc.h0);
-    const uint64_t max_units = S / REPLAY_SEEDS_PER_UNIT + 256;
-    NMZ_TRY(bucket_seeds(st, sc.h0, S, p->mod.kind == MOD_FAST ? REPLAY_SEEDS_PER_UNIT : 64, max_units, sc.b));
-    KernelTimer kt(p->ctx, st, "replayable_sweep");
+    const int U = replay_u();
+    const uint32_t per_unit = 64u * (uint32_t)U;
+    const uint64_t max_units = S / per_unit + 256;
+    NMZ_TRY(bucket_seeds(st, sc.h0, S, p->mod.kind == MOD_FAST ? per_unit : 64, max_units, sc.b));
     if (p->mod.kind == MOD_FAST) {
-        hipLaunchKernelGGL(k_replayable_sweep_fast<REPLAY_U>, dim3(ceil_div(max_units, 4)), dim3(256), 0, st,
-                           sc.b.units, sc.b.n_units, sc.b.sorted_h0, sc.b.sorted_idx, p->d_table, E,
-                           p->d_classes, p->n_classes, p->mod.m, p->mod.m_k64, d_stats);
+        const uint32_t ec = replay_ec();
+        const uint32_t n_chunks = (E + ec - 1) / ec;
+        NMZ_TRY(p->partial.ensure(partial_bytes(p->max_seeds, E, U, ec)));
+        const uint64_t stride = (p->max_seeds / per_unit + 257) * (uint64_t)per_unit;
+        NMZ_HIP(hipMemsetAsync(sc.counter, 0, 4, st));
+        const unsigned grid = (unsigned)std::min<uint64_t>(p->ctx->n_cu * 8ull, ceil_div(max_units * n_chunks, 4));
+        {
+            KernelTimer kt(p->ctx, st, "replayable_sweep");
+#define NMZ_K1(UU)                                                                                                   \
+    hipLaunchKernelGGL(k_replayable_sweep_fast<UU>, dim3(grid), dim3(256), 0, st, sc.b.units, sc.b.n_units,          \
+                       sc.b.sorted_h0, p->d_table, E, p->d_classes, p->n_classes, p->mod.m, p->mod.m_k64, ec,        \
+                       n_chunks, sc.counter, p->partial.as<uint4>(), stride)
+            if (U == 2) NMZ_K1(2); else if (U == 8) NMZ_K1(8); else NMZ_K1(4);
+#undef NMZ_K1
+        }
+        const unsigned mgrid = ceil_div(max_units * per_unit, 256);
+        if (U == 2)
+            hipLaunchKernelGGL(k_replayable_merge<2>, dim3(mgrid), dim3(256), 0, st, sc.b.units, sc.b.n_units,
+                               sc.b.sorted_idx, p->partial.as<uint4>(), stride, n_chunks, d_stats);
+        else if (U == 8)
+            hipLaunchKernelGGL(k_replayable_merge<8>, dim3(mgrid), dim3(256), 0, st, sc.b.units, sc.b.n_units,
+                               sc.b.sorted_idx, p->partial.as<uint4>(), stride, n_chunks, d_stats);
+        else
+            hipLaunchKernelGGL(k_replayable_merge<4>, dim3(mgrid), dim3(256), 0, st, sc.b.units, sc.b.n_units,
+                               sc.b.sorted_idx, p->partial.as<uint4>(), stride, n_chunks, d_stats);
     } else {
+        KernelTimer kt(p->ctx, st, "replayable_sweep");
         const uint64_t units64 = S / 64 + 256;
         hipLaunchKernelGGL(k_replayable_sweep_general, dim3(ceil_div(units64, 4)), dim3(256), 0, st,
                            sc.b.units, sc.b.n_units, sc.b.sorted_h0, sc.b.sorted_idx, p->d_table, E,
@@ -373,6 +535,7 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
     auto cleanup = [&](int code) {
         p->plan_mem.release();
         p->seed_scratch.release();
+        p->partial.release();
         delete p;
         return code;
     };
@@ -414,6 +577,7 @@ int nmz_replayable_plan_destroy(nmz_replayable_plan *plan) {
         CtxGuard g(plan->ctx);
         plan->plan_mem.release();
         plan->seed_scratch.release();
+        plan->partial.release();
     }
     delete plan;
     return NMZ_OK;
@@ -446,6 +610,7 @@ int nmz_replayable_sweep(nmz_ctx *ctx, const uint32_t *seed_off, const uint8_t *
         ~PlanGuard() {
             p->plan_mem.release();
             p->seed_scratch.release();
+            p->partial.release();
             delete p;
         }
     } pg{plan};
