@@ -170,7 +170,8 @@ int nmz_random_plan_destroy(nmz_random_plan *plan);
 int nmz_random_sweep_dev(nmz_random_plan *plan, uint64_t seed0, uint64_t n_seeds,
                          nmz_sched_stats *d_stats, void *stream);
 
-/* Top-k selection over device-resident stats (seed value = seed0 + index). */
+/* Top-k selection over device-resident stats (seed value = seed0 + index).
+ * k <= 256 (here and for the sweeps' topk outputs); NMZ_EINVAL otherwise. */
 int nmz_topk_select_dev(nmz_ctx *ctx, const nmz_sched_stats *d_stats, uint64_t n, uint64_t seed0,
                         uint32_t k, nmz_topk_entry *d_out, void *stream);
 

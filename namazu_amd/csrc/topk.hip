@@ -1,7 +1,8 @@
 // Failure-schedule candidate selection: top-k seeds by
 // (n_fault desc, sum_delay desc (int64), seed asc).
-// Two-level selection: each 256-thread block bitonic-sorts a 2048-entry chunk
-// in LDS and keeps its best k; levels repeat until one chunk remains.
+// Multi-level selection: each 256-thread block reduces a 2048-entry chunk to
+// its best k (threshold filter + bitonic sort of the survivors in LDS); levels
+// repeat until one chunk remains.
 #include "nmz_common.h"
 #include "nmz_internal.h"
 
@@ -24,12 +25,12 @@ __device__ inline nmz_topk_entry topk_sentinel() {
     return e;
 }
 
-// sort `s` (TOPK_CHUNK entries in LDS) best-first
-__device__ void bitonic_sort_chunk(nmz_topk_entry *s) {
-    for (uint32_t size = 2; size <= TOPK_CHUNK; size <<= 1) {
+// bitonic sort (best first) of the first `n` entries of s (n a power of two)
+__device__ void bitonic_sort_n(nmz_topk_entry *s, uint32_t n) {
+    for (uint32_t size = 2; size <= n; size <<= 1) {
         for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
             __syncthreads();
-            for (uint32_t t = threadIdx.x; t < TOPK_CHUNK / 2; t += blockDim.x) {
+            for (uint32_t t = threadIdx.x; t < n / 2; t += blockDim.x) {
                 uint32_t i = 2 * t - (t & (stride - 1));
                 uint32_t j = i + stride;
                 bool best_first = ((i & size) == 0);
@@ -45,39 +46,58 @@ __device__ void bitonic_sort_chunk(nmz_topk_entry *s) {
     __syncthreads();
 }
 
-// level 0: from stats (seed value = seed0 + index)
-__global__ __launch_bounds__(256) void k_topk_from_stats(const nmz_sched_stats *__restrict__ stats,
-                                                         uint64_t n, uint64_t seed0, uint32_t k,
-                                                         nmz_topk_entry *__restrict__ out) {
-    __shared__ nmz_topk_entry s[TOPK_CHUNK];
-    uint64_t base = (uint64_t)blockIdx.x * TOPK_CHUNK;
-    for (uint32_t t = threadIdx.x; t < TOPK_CHUNK; t += blockDim.x) {
-        uint64_t i = base + t;
-        nmz_topk_entry e = topk_sentinel();
-        if (i < n) {
-            const nmz_sched_stats st = stats[i];
-            e.seed = seed0 + i;
-            e.sum_delay_ns = (int64_t)st.sum_delay_ns;
-            e.n_fault = st.n_fault;
-            e.first_fault = st.first_fault;
-        }
-        s[t] = e;
-    }
-    bitonic_sort_chunk(s);
-    for (uint32_t t = threadIdx.x; t < k; t += blockDim.x) out[(uint64_t)blockIdx.x * k + t] = s[t];
-}
+constexpr uint32_t TOPK_THREADS = 256;
+constexpr uint32_t TOPK_PER_THREAD = TOPK_CHUNK / TOPK_THREADS;
 
-// level >= 1: from candidate entries
-__global__ __launch_bounds__(256) void k_topk_merge(const nmz_topk_entry *__restrict__ in, uint64_t n,
-                                                    uint32_t k, nmz_topk_entry *__restrict__ out) {
-    __shared__ nmz_topk_entry s[TOPK_CHUNK];
-    uint64_t base = (uint64_t)blockIdx.x * TOPK_CHUNK;
-    for (uint32_t t = threadIdx.x; t < TOPK_CHUNK; t += blockDim.x) {
-        uint64_t i = base + t;
-        s[t] = (i < n) ? in[i] : topk_sentinel();
+// Chunk top-k by threshold filtering. Each thread's best entry is a "winner";
+// the k-th best winner T is a lower bound of the chunk's k-th best entry (k
+// distinct entries are >= T), so only entries >= T can be in the chunk's
+// top-k. The survivors (typically ~k) are compacted in LDS and sorted.
+template <bool FROM_STATS>
+__global__ __launch_bounds__(TOPK_THREADS) void k_topk_chunk(const void *__restrict__ src, uint64_t n,
+                                                              uint64_t seed0, uint32_t k,
+                                                              nmz_topk_entry *__restrict__ out) {
+    __shared__ nmz_topk_entry cand[TOPK_CHUNK];
+    __shared__ nmz_topk_entry win[TOPK_THREADS];
+    __shared__ uint32_t ncand;
+    const uint32_t t = threadIdx.x;
+    const uint64_t base = (uint64_t)blockIdx.x * TOPK_CHUNK;
+    nmz_topk_entry e[TOPK_PER_THREAD];
+    nmz_topk_entry best = topk_sentinel();
+#pragma unroll
+    for (uint32_t r = 0; r < TOPK_PER_THREAD; ++r) {
+        const uint64_t i = base + (uint64_t)r * TOPK_THREADS + t;
+        nmz_topk_entry x = topk_sentinel();
+        if (i < n) {
+            if (FROM_STATS) {
+                const nmz_sched_stats st = static_cast<const nmz_sched_stats *>(src)[i];
+                x.seed = seed0 + i;
+                x.sum_delay_ns = (int64_t)st.sum_delay_ns;
+                x.n_fault = st.n_fault;
+                x.first_fault = st.first_fault;
+            } else {
+                x = static_cast<const nmz_topk_entry *>(src)[i];
+            }
+        }
+        e[r] = x;
+        if (topk_better(x, best)) best = x;
     }
-    bitonic_sort_chunk(s);
-    for (uint32_t t = threadIdx.x; t < k; t += blockDim.x) out[(uint64_t)blockIdx.x * k + t] = s[t];
+    win[t] = best;
+    if (t == 0) ncand = 0;
+    bitonic_sort_n(win, TOPK_THREADS);
+    const nmz_topk_entry T = win[k - 1];
+#pragma unroll
+    for (uint32_t r = 0; r < TOPK_PER_THREAD; ++r) {
+        if (!topk_better(T, e[r])) cand[atomicAdd(&ncand, 1u)] = e[r];  // e >= T
+    }
+    __syncthreads();
+    const uint32_t c = ncand;
+    uint32_t np = 2;
+    while (np < c) np <<= 1;
+    for (uint32_t i = c + t; i < np; i += TOPK_THREADS) cand[i] = topk_sentinel();
+    bitonic_sort_n(cand, np);
+    for (uint32_t i = t; i < k; i += TOPK_THREADS)
+        out[(uint64_t)blockIdx.x * k + i] = i < c ? cand[i] : topk_sentinel();
 }
 
 uint64_t topk_scratch_entries(uint64_t n, uint32_t k) {
@@ -92,16 +112,16 @@ uint64_t topk_scratch_entries(uint64_t n, uint32_t k) {
 int topk_select(hipStream_t st, const nmz_sched_stats *d_stats, uint64_t n, uint64_t seed0, uint32_t k,
                 nmz_topk_entry *d_scratch, nmz_topk_entry *d_out) {
     if (k == 0) return NMZ_OK;
-    NMZ_CHECK(k <= TOPK_CHUNK / 2, "top-k supports k <= 1024");
+    NMZ_CHECK(k <= TOPK_THREADS, "top-k supports k <= 256");
     uint64_t blocks = (n + TOPK_CHUNK - 1) / TOPK_CHUNK;
     if (blocks == 0) blocks = 1;
     nmz_topk_entry *a = d_scratch, *b = d_scratch + blocks * k;
-    hipLaunchKernelGGL(k_topk_from_stats, dim3((unsigned)blocks), dim3(256), 0, st, d_stats, n, seed0, k,
+    hipLaunchKernelGGL(k_topk_chunk<true>, dim3((unsigned)blocks), dim3(TOPK_THREADS), 0, st, d_stats, n, seed0, k,
                        blocks == 1 ? d_out : a);
     uint64_t cur = blocks * k;
     while (blocks > 1) {
         blocks = (cur + TOPK_CHUNK - 1) / TOPK_CHUNK;
-        hipLaunchKernelGGL(k_topk_merge, dim3((unsigned)blocks), dim3(256), 0, st, a, cur, k,
+        hipLaunchKernelGGL(k_topk_chunk<false>, dim3((unsigned)blocks), dim3(TOPK_THREADS), 0, st, a, cur, 0, k,
                            blocks == 1 ? d_out : b);
         cur = blocks * k;
         nmz_topk_entry *tmp = a;

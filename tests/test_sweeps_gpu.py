@@ -232,3 +232,43 @@ def test_random_config4_scale_sampled(ctx):
         assert np.array_equal(st[s:s + 1], ost)
     best = st[r.topk["seed"][0] - 1000]
     assert best["n_fault"] == st["n_fault"].max()
+
+
+# ---------------------------------------------------------------- top-k
+def _topk_dev(ctx, st, seed0, k):
+    import torch
+    L = _lib.load()
+    d_st = torch.from_numpy(np.frombuffer(st.tobytes(), np.uint8).copy()).cuda()
+    d_tk = torch.empty(max(k, 1) * 24, dtype=torch.uint8, device="cuda")
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(L.nmz_topk_select_dev(ctx.handle, ctypes.c_void_p(d_st.data_ptr()), len(st), seed0, k,
+                                     ctypes.c_void_p(d_tk.data_ptr()), stream))
+    torch.cuda.synchronize()
+    return np.frombuffer(d_tk.cpu().numpy().tobytes(), dtype=_lib.TOPK_DTYPE)[:k]
+
+
+@pytest.mark.parametrize("n,k,mode", [
+    (1, 1, "rand"), (5, 16, "rand"), (2047, 64, "rand"), (2048, 256, "rand"), (2049, 1, "rand"),
+    (300_001, 64, "rand"), (300_001, 256, "rand"), (100_000, 64, "ties"), (70_000, 64, "const"),
+    (70_000, 128, "sorted"), (70_000, 64, "faults")])
+def test_topk_select_dev(ctx, n, k, mode):
+    """Threshold-filter top-k vs the oracle: random keys, heavy ties (every
+    entry a survivor), ascending keys (worst case for per-thread winners),
+    n_fault-dominated order, sizes around the 2048-entry chunk."""
+    rng = np.random.default_rng(n * 7 + k)
+    st = np.zeros(n, O.SCHED_STATS_DTYPE)
+    if mode == "rand":
+        st["sum_delay_ns"] = rng.integers(0, 2**62, n, dtype=np.uint64)
+    elif mode == "ties":
+        st["sum_delay_ns"] = rng.integers(0, 4, n, dtype=np.uint64)
+    elif mode == "const":
+        st["sum_delay_ns"] = 77
+    elif mode == "sorted":
+        st["sum_delay_ns"] = np.arange(n, dtype=np.uint64)
+    else:
+        st["n_fault"] = rng.integers(0, 3, n, dtype=np.uint32)
+        st["sum_delay_ns"] = rng.integers(0, 1000, n, dtype=np.uint64)
+    st["first_fault"] = rng.integers(0, 2**32, n, dtype=np.uint32)
+    got = _topk_dev(ctx, st, 12345, k)
+    exp = O.topk_from_stats(st, 12345, k)
+    assert got.tolist() == exp[:k].tolist()
