@@ -11,13 +11,16 @@
 //     so every lane of a wave reads the same table row: table reads are
 //     wave-uniform scalar loads.
 //  3. Events are grouped by hint length; per (seed, length class) the lane
-//     precomputes H = h0*P^len, Hm = H mod m and ~H. Per decision:
+//     precomputes H = h0*P^len, Hm = H mod m and Hm' = (Hm + 2^64 mod m) mod m:
 //         h = H + C (mod 2^64),  carry = C > ~H
-//         h mod m = (Hm + (C mod m) + carry*((-2^64) mod m)) mod m
-//     i.e. one 64-bit compare, a select, an add and two min-reductions.
-//  4. Per-seed statistics (sum, max with first-index argmax) accumulate in
+//         h mod m = (carry ? Hm' : Hm) + (C mod m)   (one conditional -m)
+//  4. Within every (row L, class) segment the table is sorted by C, so the
+//     carry is monotone in the position: carry <=> pos >= k(seed), with k
+//     found by one binary search per (seed, segment). Per decision the carry
+//     is a single compare of a running position counter -- no 64-bit add.
+//  5. Per-seed statistics (sum, max with first-index argmax) accumulate in
 //     registers; the argmax tie-break uses the key (t << 32 | ~e) so the
-//     class-sorted event order still yields the first original index.
+//     sorted event order still yields the first original index.
 #include <algorithm>
 #include <cstdlib>
 #include <numeric>
@@ -43,9 +46,9 @@ struct nmz_replayable_plan {
     nmz::ModParams mod{};
     uint32_t n_classes = 0;
     nmz::ClassInfo *d_classes = nullptr;
-    uint4 *d_table = nullptr;          // [256][E] {C lo, C hi, C mod m, ~e}
-    uint32_t *d_pos_of_event = nullptr; // original e -> sorted position
-    uint64_t *d_pn_of_event = nullptr;  // original e -> P^len
+    uint4 *d_table = nullptr;          // [256][E] {C lo, C hi, C mod m, ~e}, C-sorted per class segment
+    uint32_t *d_hoff = nullptr;        // hint CSR on the device (dump path)
+    uint8_t *d_hbytes = nullptr;
     uint64_t max_seeds = 0;
     nmz::DevBuf seed_scratch;           // h0, buckets, sorted seeds
     nmz::DevBuf partial;                // per-chunk partial (sum, key) per seed
@@ -84,6 +87,45 @@ __global__ __launch_bounds__(256) void k_replayable_table(const uint32_t *__rest
     table[(uint64_t)L * E + pos] = make_uint4((uint32_t)C, (uint32_t)(C >> 32), cm, ~e);
 }
 
+// Sort every (row L, class) segment of the table by C (ascending, ties by
+// position): rank by counting over the segment through LDS tiles, then
+// scatter. O(n_class^2) per row -- ~1e10 compares at E = 4096, well under a ms.
+__global__ __launch_bounds__(256) void k_replayable_table_sort(const uint4 *__restrict__ tmp,
+                                                               const ClassInfo *__restrict__ classes,
+                                                               uint32_t n_classes, uint32_t E,
+                                                               uint4 *__restrict__ table) {
+    __shared__ uint2 tile[256];
+    const uint32_t L = blockIdx.y;
+    const uint32_t p0 = blockIdx.x * 256;
+    const uint32_t p = p0 + threadIdx.x;
+    const uint4 *__restrict__ row = tmp + (uint64_t)L * E;
+    uint32_t cs = 0, ce = 0, lo = UINT32_MAX, hi = 0;
+    for (uint32_t c = 0; c < n_classes; ++c) {
+        const uint32_t a = classes[c].start, b = a + classes[c].count;
+        if (p >= a && p < b) cs = a, ce = b;
+        // union of the classes this block touches
+        if (b > p0 && a < min(E, p0 + 256)) lo = min(lo, a), hi = max(hi, b);
+    }
+    const uint4 x = p < E ? row[p] : make_uint4(0, 0, 0, 0);
+    const uint64_t cx = ((uint64_t)x.y << 32) | x.x;
+    uint32_t rank = 0;
+    for (uint32_t j0 = lo; j0 < hi; j0 += 256) {
+        __syncthreads();
+        if (j0 + threadIdx.x < hi) {
+            const uint4 y = row[j0 + threadIdx.x];
+            tile[threadIdx.x] = make_uint2(y.x, y.y);
+        }
+        __syncthreads();
+        const uint32_t jn = min(256u, hi - j0);
+        for (uint32_t jj = 0; jj < jn; ++jj) {
+            const uint32_t j = j0 + jj;
+            const uint64_t cj = ((uint64_t)tile[jj].y << 32) | tile[jj].x;
+            rank += (j >= cs && j < ce && (cj < cx || (cj == cx && j < p))) ? 1u : 0u;
+        }
+    }
+    if (p < E) table[(uint64_t)L * E + cs + rank] = x;
+}
+
 // ---------------------------------------------------------------------------
 // seed prefix: h0 = FNV(seed bytes)
 // ---------------------------------------------------------------------------
@@ -98,40 +140,35 @@ __global__ __launch_bounds__(256) void k_seed_prefix(const uint32_t *__restrict_
 }
 
 // ---------------------------------------------------------------------------
-// the sweep (MOD_FAST): one wave per work unit of up to 64*U seeds that share
-// the FNV low byte L; U seeds per lane.
-//
-// Per decision (m < 2^30):
-//   carry = C > ~H                       v_cmp_gt_u64      (one 64-bit compare)
-//   s     = (carry ? Hm' : Hm) + (C % m)  v_cndmask, v_add  (s < 2m)
-//   t     = min(s, s - m)                v_sub, v_min_u32
-//   max   : 64-bit key (t << 32 | ~e) max -- first original index wins ties
-//           even though events run class-sorted; straight-line, no SALU masks
-//   sum   : u32 partial over 4 events (< 2^32 since t < 2^30), folded into u64
+// the sweep (MOD_FAST): persistent waves take work items of up to 64*U seeds
+// (U per lane) that share the FNV low byte L, times a chunk of events.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t vgpr(uint32_t x) {
-    // keep a launch constant in a VGPR: VGPR-only v_sub_u32 issues at full rate,
-    // the SGPR-operand form at half rate on gfx950
+    // keep a launch constant in a VGPR: VGPR-only VOP2 issues at full rate,
+    // the SGPR / literal operand forms at half rate on gfx950
     uint32_t v;
     asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(x));
     return v;
 }
 
+__device__ __forceinline__ void vsub(uint32_t &d, uint32_t x) {
+    asm("v_sub_u32 %0, %0, %1" : "+v"(d) : "v"(x));
+}
+
 // One decision, VOP2 carry/borrow chains only (the forms gfx950 issues at
-// ~2.25 cycles; v_cmp_* and v_min/max_u32 take ~4.1, cmp64+2 selects ~5.8 --
-// tools/ubench/valu_patterns.hip):
-//   vcc = carry(H + C)            v_add_co / v_addc_co      (sums discarded)
-//   s   = (vcc ? Hm2 : Hm) + Cm   v_cndmask, v_add
+// ~2.25 cycles; v_cmp_*, v_min/max_u32 and v_addc/v_subb take ~4.1 --
+// tools/ubench/valu_patterns.hip, decide_block.hip):
+//   vcc = T_t < d                 v_sub_co     (before the seed's carry switch)
+//   s   = (vcc ? Hm : Hm2) + Cm   v_cndmask, v_add
 //   t   = s < m ? s : s - m       v_sub_co (borrow), v_cndmask
 //   key = max(key, t:~e)          v_sub_co / v_subb_co (64-bit borrow), 2 x v_cndmask
 //   part += t                     v_add
-__device__ __forceinline__ void decide_fast(uint32_t Hlo, uint32_t Hhi, uint32_t Hm, uint32_t Hm2, uint32_t Clo,
-                                            uint32_t Chi, uint32_t Cm, uint32_t ne, uint32_t mv, uint32_t &klo,
-                                            uint32_t &khi, uint32_t &part) {
+__device__ __forceinline__ void decide_pos(uint32_t Tt, uint32_t d, uint32_t Hm, uint32_t Hm2, uint32_t Cm,
+                                           uint32_t ne, uint32_t mv, uint32_t &klo, uint32_t &khi,
+                                           uint32_t &part) {
     uint32_t t0, t1, sv, cv;
-    asm("v_add_co_u32 %[t0], vcc, %[Clo], %[Hlo]\n\t"
-        "v_addc_co_u32 %[t1], vcc, %[Chi], %[Hhi], vcc\n\t"
-        "v_cndmask_b32 %[sv], %[Hm], %[Hm2], vcc\n\t"
+    asm("v_sub_co_u32 %[t0], vcc, %[Tt], %[d]\n\t"
+        "v_cndmask_b32 %[sv], %[Hm2], %[Hm], vcc\n\t"
         "v_add_u32 %[sv], %[Cm], %[sv]\n\t"
         "v_sub_co_u32 %[cv], vcc, %[sv], %[mv]\n\t"
         "v_cndmask_b32 %[sv], %[cv], %[sv], vcc\n\t"
@@ -142,30 +179,46 @@ __device__ __forceinline__ void decide_fast(uint32_t Hlo, uint32_t Hhi, uint32_t
         "v_add_u32 %[part], %[part], %[sv]"
         : [t0] "=&v"(t0), [t1] "=&v"(t1), [sv] "=&v"(sv), [cv] "=&v"(cv), [klo] "+v"(klo), [khi] "+v"(khi),
           [part] "+v"(part)
-        : [Hlo] "v"(Hlo), [Hhi] "v"(Hhi), [Hm] "v"(Hm), [Hm2] "v"(Hm2), [Clo] "v"(Clo), [Chi] "v"(Chi),
-          [Cm] "v"(Cm), [ne] "v"(ne), [mv] "v"(mv)
+        : [Tt] "v"(Tt), [d] "v"(d), [Hm] "v"(Hm), [Hm2] "v"(Hm2), [Cm] "v"(Cm), [ne] "v"(ne), [mv] "v"(mv)
         : "vcc");
 }
 
+// number of entries in the C-sorted range row[lo, lo+n) with C <= x
+__device__ __forceinline__ uint32_t count_le(const uint4 *__restrict__ row, uint32_t lo, uint32_t n, uint64_t x) {
+    uint32_t k = 0;
+    for (uint32_t s = n ? 1u << (31 - __builtin_clz(n)) : 0u; s; s >>= 1) {
+        if (k + s <= n) {
+            const uint2 c = *reinterpret_cast<const uint2 *>(row + lo + k + s - 1);
+            if ((((uint64_t)c.y << 32) | c.x) <= x) k += s;
+        }
+    }
+    return k;
+}
+
+constexpr uint32_t POS_BIAS = 0x40000000u;  // keeps d = BIAS + k - i positive
+
 // Work item = (seed group of <= 64*U seeds sharing the low byte L, chunk of
-// `ec` events in the length-sorted order). Items are handed out dynamically
-// (one global atomic per item) to a persistent grid, so the last round is
-// never a half-empty second pass of whole seed groups; each item writes its
-// partial (sum, key) per seed and k_replayable_merge combines the chunks.
+// `ec` events in the table order). Items are handed out dynamically (one
+// global atomic per item) to a persistent grid, so the last round is never a
+// half-empty second pass; each item writes its partial (sum, key) per seed
+// and k_replayable_merge combines the chunks.
 template <int U>
 __global__ __launch_bounds__(256) void k_replayable_sweep_fast(
     const uint4 *__restrict__ units, const uint32_t *__restrict__ n_units,
     const uint64_t *__restrict__ sorted_h0, const uint4 *__restrict__ table, uint32_t E,
     const ClassInfo *__restrict__ classes, uint32_t n_classes, uint64_t m, uint32_t m_k64, uint32_t ec,
-    uint32_t n_chunks, uint32_t *__restrict__ item_counter, uint4 *__restrict__ partial, uint64_t part_stride) {
+    uint32_t n_chunks, uint32_t fold_mask, uint32_t *__restrict__ item_counter, uint4 *__restrict__ partial,
+    uint64_t part_stride) {
     // per-wave double-buffered staging of 64 table entries (1 KiB) in LDS:
     // one coalesced 16-B load per lane fetches the next chunk while the
-    // current one is consumed through broadcast ds_read_b128.
+    // current one is consumed through broadcast LDS reads.
     __shared__ uint4 stage[4][2][64];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t m32 = (uint32_t)m;
     const uint32_t mv = vgpr(m32);
+    const uint32_t T0 = vgpr(POS_BIAS), T1 = vgpr(POS_BIAS + 1), T2 = vgpr(POS_BIAS + 2), T3 = vgpr(POS_BIAS + 3);
+    const uint32_t V4 = vgpr(4u), V1 = vgpr(1u);
     const uint32_t n_items = *n_units * n_chunks;
     uint32_t slot = 0;
 
@@ -198,21 +251,21 @@ __global__ __launch_bounds__(256) void k_replayable_sweep_fast(
         uint32_t cc = 0;
         ClassInfo ci = classes[0];
         while (ci.start + ci.count <= e0) ci = classes[++cc];
-        uint32_t pos = e0;  // next event (sorted order) to stage
+        uint32_t pos = e0;  // next event (table order) to stage
         uint32_t hi_c = min(e1, ci.start + ci.count);
         uint4 pre = (pos + lane < hi_c) ? row[pos + lane] : make_uint4(0, 0, 0, 0);
-        uint32_t Hlo[U], Hhi[U], Hm[U], Hm2[U];
+        uint32_t Hm[U], Hm2[U], d[U];
         bool fresh = true;
         while (pos < e1) {
             if (fresh) {
 #pragma unroll
                 for (int r = 0; r < U; ++r) {
                     const uint64_t H = h0[r] * ci.pn;
-                    Hlo[r] = (uint32_t)H;
-                    Hhi[r] = (uint32_t)(H >> 32);
                     Hm[r] = (uint32_t)(H % m);
                     const uint32_t t2 = Hm[r] + m_k64;
                     Hm2[r] = min(t2, t2 - m32);
+                    // carry(H + C) <=> C > ~H <=> position >= pos + count(C <= ~H)
+                    d[r] = POS_BIAS + count_le(row, pos, hi_c - pos, ~H);
                 }
                 fresh = false;
             }
@@ -233,32 +286,47 @@ __global__ __launch_bounds__(256) void k_replayable_sweep_fast(
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const uint4 *__restrict__ sq = stage[wv][slot];
             const uint32_t n4 = n & ~3u;
-            for (uint32_t i = 0; i < n4; i += 4) {
-                uint4 qq[4];
+            // part[r] holds up to 4 << fold_shift delays (< 2^32 since t < m) between folds
+            uint32_t part[U];
 #pragma unroll
-                for (int t = 0; t < 4; ++t) qq[t] = sq[i + t];
+            for (int r = 0; r < U; ++r) part[r] = 0;
+            for (uint32_t i = 0, g = 1; i < n4; i += 4, ++g) {
+                uint2 qq[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) qq[t] = make_uint2(sq[i + t].z, sq[i + t].w);
 #pragma unroll
                 for (int r = 0; r < U; ++r) {
-                    uint32_t part = 0;
+                    decide_pos(T0, d[r], Hm[r], Hm2[r], qq[0].x, qq[0].y, mv, klo[r], khi[r], part[r]);
+                    decide_pos(T1, d[r], Hm[r], Hm2[r], qq[1].x, qq[1].y, mv, klo[r], khi[r], part[r]);
+                    decide_pos(T2, d[r], Hm[r], Hm2[r], qq[2].x, qq[2].y, mv, klo[r], khi[r], part[r]);
+                    decide_pos(T3, d[r], Hm[r], Hm2[r], qq[3].x, qq[3].y, mv, klo[r], khi[r], part[r]);
+                    vsub(d[r], V4);
+                }
+                if ((g & fold_mask) == 0) {
 #pragma unroll
-                    for (int t = 0; t < 4; ++t)
-                        decide_fast(Hlo[r], Hhi[r], Hm[r], Hm2[r], qq[t].x, qq[t].y, qq[t].z, qq[t].w, mv, klo[r],
-                                    khi[r], part);
-                    const uint32_t lo = sum_lo[r] + part;
-                    sum_hi[r] += (lo < part);
-                    sum_lo[r] = lo;
+                    for (int r = 0; r < U; ++r) {
+                        const uint32_t lo = sum_lo[r] + part[r];
+                        sum_hi[r] += (lo < part[r]);
+                        sum_lo[r] = lo;
+                        part[r] = 0;
+                    }
                 }
             }
             for (uint32_t i = n4; i < n; ++i) {  // class / item tail (< 4 events)
                 const uint4 q1 = sq[i];
 #pragma unroll
                 for (int r = 0; r < U; ++r) {
-                    uint32_t part = 0;
-                    decide_fast(Hlo[r], Hhi[r], Hm[r], Hm2[r], q1.x, q1.y, q1.z, q1.w, mv, klo[r], khi[r], part);
-                    const uint32_t lo = sum_lo[r] + part;
-                    sum_hi[r] += (lo < part);
-                    sum_lo[r] = lo;
+                    decide_pos(T0, d[r], Hm[r], Hm2[r], q1.z, q1.w, mv, klo[r], khi[r], part[r]);
+                    vsub(d[r], V1);
                 }
+            }
+            // here part holds <= fold_mask groups since the last fold plus the tail
+            // (< 4 events): fewer than 4 * (fold_mask + 1) delays, so no overflow
+#pragma unroll
+            for (int r = 0; r < U; ++r) {
+                const uint32_t lo = sum_lo[r] + part[r];
+                sum_hi[r] += (lo < part[r]);
+                sum_lo[r] = lo;
             }
             slot ^= 1;
             pos = npos;
@@ -364,21 +432,20 @@ __global__ __launch_bounds__(256) void k_stats_constant(uint64_t n, uint32_t E,
     stats[s] = st;
 }
 
-// full per-decision dump for the first n_dump seeds (parity / debugging path)
+// full per-decision dump for the first n_dump seeds (parity / debugging path):
+// plain FNV over seed bytes || hint bytes, independent of the table
 __global__ __launch_bounds__(256) void k_replayable_dump(const uint32_t *__restrict__ soff,
                                                          const uint8_t *__restrict__ sbytes,
-                                                         uint64_t n_dump, const uint4 *__restrict__ table,
-                                                         uint32_t E, const uint32_t *__restrict__ pos_of,
-                                                         const uint64_t *__restrict__ pn_of, uint64_t m,
-                                                         int64_t *__restrict__ out) {
+                                                         uint64_t n_dump, const uint32_t *__restrict__ hoff,
+                                                         const uint8_t *__restrict__ hbytes, uint32_t E,
+                                                         uint64_t m, int64_t *__restrict__ out) {
     uint64_t idx = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (idx >= n_dump * E) return;
     const uint64_t s = idx / E;
     const uint32_t e = (uint32_t)(idx % E);
     uint64_t h = FNV_OFFSET;
     for (uint32_t i = soff[s], end = soff[s + 1]; i < end; ++i) h = fnv_step(h, sbytes[i]);
-    const uint4 q = table[(uint64_t)(h & 0xff) * E + pos_of[e]];
-    h = h * pn_of[e] + (((uint64_t)q.y << 32) | q.x);
+    for (uint32_t i = hoff[e], end = hoff[e + 1]; i < end; ++i) h = fnv_step(h, hbytes[i]);
     out[idx] = m ? (int64_t)(h % m) : 0;
 }
 
@@ -450,13 +517,17 @@ static int replayable_run(nmz_replayable_plan *p, hipStream_t st, const uint32_t
         NMZ_TRY(p->partial.ensure(partial_bytes(p->max_seeds, E, U, ec)));
         const uint64_t stride = (p->max_seeds / per_unit + 257) * (uint64_t)per_unit;
         NMZ_HIP(hipMemsetAsync(sc.counter, 0, 4, st));
+        // fold the u32 partial sums every 2^f groups of 4 events, (4 << f)(m - 1) + 3(m - 1) < 2^32
+        uint32_t fold_mask = 0;
+        while (fold_mask < 15 && ((uint64_t)(4 * (fold_mask + 1) * 2 + 3)) * (p->mod.m - 1) < (1ull << 32))
+            fold_mask = fold_mask * 2 + 1;
         const unsigned grid = (unsigned)std::min<uint64_t>(p->ctx->n_cu * 8ull, ceil_div(max_units * n_chunks, 4));
         {
             KernelTimer kt(p->ctx, st, "replayable_sweep");
 #define NMZ_K1(UU)                                                                                                   \
     hipLaunchKernelGGL(k_replayable_sweep_fast<UU>, dim3(grid), dim3(256), 0, st, sc.b.units, sc.b.n_units,          \
                        sc.b.sorted_h0, p->d_table, E, p->d_classes, p->n_classes, p->mod.m, p->mod.m_k64, ec,        \
-                       n_chunks, sc.counter, p->partial.as<uint4>(), stride)
+                       n_chunks, fold_mask, sc.counter, p->partial.as<uint4>(), stride)
             if (U == 2) NMZ_K1(2); else if (U == 8) NMZ_K1(8); else NMZ_K1(4);
 #undef NMZ_K1
         }
@@ -495,18 +566,15 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
     hipStream_t st = ctx->stream;
 
     // length classes (stable, so original order is kept inside a class)
-    std::vector<uint32_t> perm(E), pos_of(E);
+    std::vector<uint32_t> perm(E);
     std::iota(perm.begin(), perm.end(), 0u);
     std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) {
         return hint_off[a + 1] - hint_off[a] < hint_off[b + 1] - hint_off[b];
     });
     std::vector<ClassInfo> cls;
-    std::vector<uint64_t> pn_of(E);
     for (uint32_t i = 0; i < E; ++i) {
         const uint32_t e = perm[i];
-        pos_of[e] = i;
         const uint32_t len = hint_off[e + 1] - hint_off[e];
-        pn_of[e] = fnv_pow(len);
         if (cls.empty() || fnv_pow(len) != cls.back().pn ||
             len != hint_off[perm[cls.back().start] + 1] - hint_off[perm[cls.back().start]])
             cls.push_back(ClassInfo{fnv_pow(len), i, 0});
@@ -516,7 +584,7 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
     const uint64_t nbytes = E ? hint_off[E] : 0;
 
     size_t need = Carve::bytes_for(cls.size() + 1, sizeof(ClassInfo)) + Carve::bytes_for((size_t)256 * E + 1, 16) +
-                  Carve::bytes_for(E + 1, 4) * 3 + Carve::bytes_for(E + 1, 8) + Carve::bytes_for(nbytes + 1, 1);
+                  Carve::bytes_for(E + 1, 4) * 2 + Carve::bytes_for(nbytes + 1, 1);
     int rc = p->plan_mem.ensure(need);
     if (rc == NMZ_OK && E && p->mod.kind != MOD_ZERO) rc = p->seed_scratch.ensure(seed_scratch_bytes(max_seeds));
     if (rc != NMZ_OK) {
@@ -527,11 +595,9 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
     Carve cv(p->plan_mem.ptr);
     p->d_classes = cv.take<ClassInfo>(cls.size() + 1);
     p->d_table = cv.take<uint4>((size_t)256 * E + 1);
-    p->d_pos_of_event = cv.take<uint32_t>(E + 1);
     uint32_t *d_perm = cv.take<uint32_t>(E + 1);
-    uint32_t *d_hoff = cv.take<uint32_t>(E + 1);
-    p->d_pn_of_event = cv.take<uint64_t>(E + 1);
-    uint8_t *d_hbytes = cv.take<uint8_t>(nbytes + 1);
+    uint32_t *d_hoff = p->d_hoff = cv.take<uint32_t>(E + 1);
+    uint8_t *d_hbytes = p->d_hbytes = cv.take<uint8_t>(nbytes + 1);
     auto cleanup = [&](int code) {
         p->plan_mem.release();
         p->seed_scratch.release();
@@ -541,15 +607,42 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
     };
     if (E) {
         if (hipMemcpyAsync(p->d_classes, cls.data(), cls.size() * sizeof(ClassInfo), hipMemcpyHostToDevice, st) ||
-            hipMemcpyAsync(p->d_pos_of_event, pos_of.data(), E * 4, hipMemcpyHostToDevice, st) ||
             hipMemcpyAsync(d_perm, perm.data(), E * 4, hipMemcpyHostToDevice, st) ||
             hipMemcpyAsync(d_hoff, hint_off, (E + 1) * 4, hipMemcpyHostToDevice, st) ||
-            hipMemcpyAsync(p->d_pn_of_event, pn_of.data(), E * 8, hipMemcpyHostToDevice, st) ||
             (nbytes && hipMemcpyAsync(d_hbytes, hint_bytes, nbytes, hipMemcpyHostToDevice, st)))
             return cleanup(fail(NMZ_EHIP, "plan upload failed"));
+        // unsorted table into scratch, then the per-(L, class) C sort into place
+        DevBuf tmp;
+        if (tmp.ensure((size_t)256 * E * sizeof(uint4)) != NMZ_OK) return cleanup(NMZ_ENOMEM);
         hipLaunchKernelGGL(k_replayable_table, dim3(E), dim3(256), 0, st, d_hoff, d_hbytes, d_perm, E, p->mod.m,
-                           p->mod.kind == MOD_FAST ? 1 : 0, p->d_table);
-        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+                           p->mod.kind == MOD_FAST ? 1 : 0, tmp.as<uint4>());
+        uint32_t max_class = 0;
+        for (const ClassInfo &c : cls) max_class = std::max(max_class, c.count);
+        bool bad = false;
+        if (max_class <= 16384) {  // O(n^2) rank sort on the device
+            hipLaunchKernelGGL(k_replayable_table_sort, dim3(ceil_div(E, 256), 256), dim3(256), 0, st,
+                               tmp.as<uint4>(), p->d_classes, p->n_classes, E, p->d_table);
+            bad = hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess;
+        } else {  // very large classes: sort the segments on the host
+            std::vector<uint4> h((size_t)256 * E);
+            bad = hipGetLastError() != hipSuccess ||
+                  hipMemcpyAsync(h.data(), tmp.ptr, h.size() * sizeof(uint4), hipMemcpyDeviceToHost, st) !=
+                      hipSuccess ||
+                  hipStreamSynchronize(st) != hipSuccess;
+            if (!bad) {
+                auto key = [](const uint4 &q) { return ((uint64_t)q.y << 32) | q.x; };
+                for (uint32_t L = 0; L < 256; ++L)
+                    for (const ClassInfo &c : cls)
+                        std::stable_sort(h.begin() + (size_t)L * E + c.start,
+                                         h.begin() + (size_t)L * E + c.start + c.count,
+                                         [&](const uint4 &a, const uint4 &b) { return key(a) < key(b); });
+                bad = hipMemcpyAsync(p->d_table, h.data(), h.size() * sizeof(uint4), hipMemcpyHostToDevice, st) !=
+                          hipSuccess ||
+                      hipStreamSynchronize(st) != hipSuccess;
+            }
+        }
+        tmp.release();
+        if (bad)
             return cleanup(fail(NMZ_EHIP, "plan table kernel failed"));
     }
     *out = p;
@@ -634,8 +727,7 @@ int nmz_replayable_sweep(nmz_ctx *ctx, const uint32_t *seed_off, const uint8_t *
     NMZ_TRY(replayable_run(plan, st, d_soff, d_sb, n_seeds, d_stats));
     if (n_dump_seeds && n_events) {
         hipLaunchKernelGGL(k_replayable_dump, dim3(ceil_div(n_dump_seeds * n_events, 256)), dim3(256), 0, st, d_soff,
-                           d_sb, n_dump_seeds, plan->d_table, n_events, plan->d_pos_of_event, plan->d_pn_of_event,
-                           plan->mod.m, d_dump);
+                           d_sb, n_dump_seeds, plan->d_hoff, plan->d_hbytes, n_events, plan->mod.m, d_dump);
         NMZ_HIP(hipGetLastError());
     }
     if (k) NMZ_TRY(topk_select(st, d_stats, n_seeds, 0, k, d_tk, d_tk + tk_entries));
