@@ -34,10 +34,11 @@ sys.path.insert(0, HERE)
 PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 78.6 T int32 lane-ops/s (2 cyc/wave64 instr/SIMD)
 PEAK_HBM_GBS = 8000.0
 MAX_INTERVAL_NS = 100_000_000
-# VALU instructions per decision in k_replayable_sweep_fast's steady-state loop
-# (4 events x 4 seeds per iteration; counted from the gfx950 ISA, cross-checked
-# with rocprofv3 SQ_INSTS_VALU in profiles/).
-REPLAY_VALU_PER_DEC = 13.0
+# VALU wave-instructions per wave-decision (64 decisions) of k_replayable_sweep_fast:
+# rocprofv3 SQ_INSTS_VALU / (S*E/64) = 738.4M / 67.1M = 11.0 (profiles/r01c_summary.json);
+# the gfx950 ISA of the steady-state loop has 82 per 8 decisions = 10.25, the rest is
+# the per-segment binary search, staging and folds.
+REPLAY_VALU_PER_DEC = 11.0
 RANDOM_VALU_PER_DEC = 170.0  # SURVEY 8(d) declared model for the random decision
 
 
