@@ -341,6 +341,11 @@ struct nmz_ed_plan {
     nmz_ctx *ctx = nullptr;
     uint32_t n = 0, band = 0, G = 0;
     bool fast = false;
+    bool bv = false;               // bit-parallel kernel (k_ed_bv) usable
+    uint32_t ndw = 0, lds_dw = 0;  // bv: dwords per Peq row per query, LDS dwords per workgroup
+    uint64_t n_chunks = 0;         // bv: total chunks (64-query block row x 4 candidate groups)
+    uint16_t *d_bsym = nullptr;
+    uint64_t *d_boff = nullptr, *d_chunk_start = nullptr;
     nmz::DevBuf mem;
     uint16_t *d_qsym = nullptr, *d_csym = nullptr;
     uint64_t *d_qoff = nullptr, *d_coff = nullptr;
@@ -390,7 +395,64 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         delete p;
         return code;
     };
-    if (fast) {
+    // bit-parallel path: per-query Peq rows for every symbol of the alphabet must fit in LDS
+    uint32_t n_sym = 0;
+    if (fast && ed_bv_supported(band)) {
+        std::vector<uint8_t> seen(65536, 0);
+        for (uint64_t t = 0; t < total; ++t)
+            if (!seen[ids[t]]) { seen[ids[t]] = 1; ++n_sym; }
+        const uint32_t KF = (2 * band + 31) / 32;
+        uint32_t ndw = (maxlen + 31) / 32 + KF + 2;
+        ndw |= 1;  // odd row stride: rows of distinct symbols start on distinct bank pairs
+        const uint64_t lds_bytes = (uint64_t)(n_sym + 1) * ndw * 8;
+        if (lds_bytes <= 65536) {
+            p->bv = true;
+            p->ndw = ndw;
+            p->lds_dw = (uint32_t)(((lds_bytes + 15) / 16) * 4);
+        }
+    }
+    if (fast && p->bv) {
+        const uint32_t G = (N + 63) / 64;
+        p->G = G;
+        const uint32_t ndw = p->ndw;
+        const uint32_t zero_row = n_sym * ndw * 8;
+        std::vector<uint32_t> len(N + 1, 0);
+        std::vector<uint64_t> boff(G + 1, 0), chunk_start(G + 1, 0);
+        std::vector<uint32_t> gmax(G, 0);
+        for (uint32_t i = 0; i < N; ++i) {
+            len[i] = (uint32_t)(off[i + 1] - off[i]);
+            gmax[i / 64] = std::max(gmax[i / 64], len[i]);
+        }
+        // each group's stream: ceil(gmax/32) blocks of 32 positions + 1 spare (prefetch)
+        for (uint32_t g = 0; g < G; ++g) boff[g + 1] = boff[g] + ((uint64_t)(gmax[g] + 31) / 32 + 1) * 32 * 64;
+        for (uint32_t b = 0; b < G; ++b) chunk_start[b + 1] = chunk_start[b] + (G - b + 3) / 4;
+        p->n_chunks = chunk_start[G];
+        std::vector<uint16_t> bs(boff[G], (uint16_t)zero_row);
+        for (uint32_t i = 0; i < N; ++i) {
+            uint16_t *gb = bs.data() + boff[i / 64] + (uint64_t)(i % 64) * 8;
+            for (uint32_t t = 0; t < len[i]; ++t)
+                gb[(uint64_t)(t / 8) * 512 + (t % 8)] = (uint16_t)(ids[off[i] + t] * ndw * 8);
+        }
+        size_t need = Carve::bytes_for(total + 1, 2) + Carve::bytes_for(bs.size() + 1, 2) +
+                      Carve::bytes_for(N + 1, 8) + Carve::bytes_for(G + 1, 8) * 2 + Carve::bytes_for(N + 1, 4);
+        int rc = p->mem.ensure(need);
+        if (rc != NMZ_OK) return cleanup(rc);
+        Carve cv(p->mem.ptr);
+        p->d_qsym = cv.take<uint16_t>(total + 1);
+        p->d_bsym = cv.take<uint16_t>(bs.size() + 1);
+        p->d_qoff = cv.take<uint64_t>(N + 1);
+        p->d_boff = cv.take<uint64_t>(G + 1);
+        p->d_chunk_start = cv.take<uint64_t>(G + 1);
+        p->d_len = cv.take<uint32_t>(N + 1);
+        if ((total && hipMemcpyAsync(p->d_qsym, ids.data(), total * 2, hipMemcpyHostToDevice, st)) ||
+            hipMemcpyAsync(p->d_bsym, bs.data(), bs.size() * 2, hipMemcpyHostToDevice, st) ||
+            hipMemcpyAsync(p->d_qoff, off, (N + 1) * 8, hipMemcpyHostToDevice, st) ||
+            hipMemcpyAsync(p->d_boff, boff.data(), (G + 1) * 8, hipMemcpyHostToDevice, st) ||
+            hipMemcpyAsync(p->d_chunk_start, chunk_start.data(), (G + 1) * 8, hipMemcpyHostToDevice, st) ||
+            hipMemcpyAsync(p->d_len, len.data(), (N + 1) * 4, hipMemcpyHostToDevice, st) ||
+            hipStreamSynchronize(st))
+            return cleanup(fail(NMZ_EHIP, "ED plan upload failed"));
+    } else if (fast) {
         const uint32_t G = (N + 63) / 64;
         p->G = G;
         std::vector<uint32_t> gmax(G + 1, 0), len(N + 1, 0);
@@ -446,6 +508,30 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
     const uint32_t N = p->n;
     if (N == 0 || k == 0) return NMZ_OK;
     hipLaunchKernelGGL(k_knn_init, dim3(ceil_div((uint64_t)N * k, 256)), dim3(256), 0, st, d_knn, (uint64_t)N * k);
+    if (p->bv) {
+        EdBvArgs A;
+        A.qsym = p->d_qsym;
+        A.qoff = p->d_qoff;
+        A.len = p->d_len;
+        A.bsym = p->d_bsym;
+        A.boff = p->d_boff;
+        A.chunk_start = p->d_chunk_start;
+        A.knn = d_knn;
+        A.N = N;
+        A.G = p->G;
+        A.k = k;
+        A.ndw = p->ndw;
+        A.lds_dw = p->lds_dw;
+        A.shard = shard;
+        A.n_shards = n_shards;
+        A.n_chunks = shard < p->n_chunks ? (p->n_chunks - shard + n_shards - 1) / n_shards : 0;
+        if (A.n_chunks == 0) return NMZ_OK;
+        uint64_t blocks = A.n_chunks * 32;
+        blocks = (blocks + 7) / 8 * 8;  // multiple of 8 for the XCD remap
+        NMZ_CHECK(blocks < (1ULL << 31), "too many traces for one launch");
+        KernelTimer kt(p->ctx, st, "ed_bv");
+        return ed_bv_launch(A, p->band, blocks, st);
+    }
     if (p->fast) {
         EdArgs A;
         A.qsym = p->d_qsym;
@@ -522,7 +608,7 @@ int nmz_ed_plan_destroy(nmz_ed_plan *plan) {
     return NMZ_OK;
 }
 
-int nmz_ed_plan_is_fast(const nmz_ed_plan *plan) { return plan && plan->fast ? 1 : 0; }
+int nmz_ed_plan_is_fast(const nmz_ed_plan *plan) { return plan ? (plan->bv ? 2 : (plan->fast ? 1 : 0)) : 0; }
 
 int nmz_ed_allpairs_knn_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys, void *stream) {
     return nmz_ed_allpairs_knn_shard_dev(plan, k, 0, 1, d_knn_keys, stream);

@@ -1,0 +1,343 @@
+// K3b -- bit-parallel banded Levenshtein (Myers 1999 / Hyyro 2003, diagonal
+// band) for the all-pairs k-NN search over event-hash traces.
+//
+// ED_w(a,b) = min(D_band(n,m), w+1) exactly as k_ed_tile / the oracle define
+// it.  Any DP whose boundary values are upper bounds of
+// the true Levenshtein values and finite outside the band gives a D' with
+// Lev <= D' <= D_band on the band; both ends agree once clamped at w+1, so
+// the band edges here carry +1 deltas (an upper bound) instead of +inf.
+//
+// Layout of one wave: 64 candidate traces b (one per lane) x 2 query traces
+// a1, a2 (shared by the wave, held in LDS).  The query is the bit-vector
+// "pattern": rows = query positions, columns = candidate positions.  Per
+// column j a lane keeps the vertical deltas of the 2w+1 band rows
+// r_j .. r_j+2w (r_j = j-w) as two bit-vectors P (+1) and M (-1) of KF
+// 32-bit words; bit k <-> row r_j+k.  One column step is ~13 VALU ops per
+// word instead of ~3 ops per DP cell: for w = 32 one step covers 65 cells.
+//
+//   Eq  = Peq_a[b_j] bits r_j..r_j+2w      (LDS; per-query match bitmaps)
+//   Xv  = Eq | M
+//   Xh  = (((Eq & P) + P) ^ P) | Eq
+//   Ph  = M | ~(Xh | P)         Mh = P & Xh          (horizontal deltas)
+//   Xs  = Xv >> 1                                    (band slides one row down)
+//   P'  = Mh | ~(Xs | Ph)       M' = Ph & Xs         (+1 inserted at bit 2w)
+//
+// Query rows <= 0 are virtual rows with D(i,j) = j - i, a fixed point of the
+// recurrence that reproduces row 0 (D(0,j) = j) and the +1 top boundary, so
+// every column runs the same code.  The value of the band's top cell
+// T_j = D(r_j, j) advances by vdelta + hdelta = 1 - ((M | Xh) & 1); the bits
+// are shifted into an accumulator and popcounted once per 32 columns.
+// Cut-off: D is non-decreasing along diagonals, so min(band at column j)
+// never decreases; T_j - popcount(M) is a lower bound of it, and once it
+// exceeds w the pair's result is w+1.
+//
+// Peq tables: per query, one bit row per symbol of the plan's alphabet
+// (dense ids), 2 queries interleaved per dword ([symbol][dword][query]) so
+// one ds_read_b64 returns a dword of both queries.  Candidate symbols are
+// stored as that row's LDS byte offset (u16), [group][pos/8][lane][8].
+#include "nmz_common.h"
+#include "nmz_internal.h"
+
+namespace nmz {
+
+__device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
+    return __builtin_amdgcn_alignbit(hi, lo, s);
+}
+
+__device__ __forceinline__ void bv_knn_insert(uint64_t *list, uint32_t k, uint64_t key) {
+    if (key >= __hip_atomic_load(&list[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    for (uint32_t s = 0; s < k; ++s) {
+        const uint64_t old = atomicMin((unsigned long long *)&list[s], (unsigned long long)key);
+        if (old == UINT64_MAX) return;
+        key = old > key ? old : key;
+    }
+}
+
+__device__ __forceinline__ void bv_knn_insert_wave(uint64_t *list, uint32_t k, uint64_t key, uint32_t lane) {
+    for (uint32_t r = 0; r < k; ++r) {
+        uint64_t best = key;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const uint64_t o = __shfl_xor(best, off, 64);
+            best = o < best ? o : best;
+        }
+        if (best == UINT64_MAX) return;
+        if (best >= __hip_atomic_load(&list[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+        if (lane == (uint32_t)__builtin_amdgcn_readfirstlane(__ffsll(__ballot(key == best)) - 1))
+            bv_knn_insert(list, k, best);
+        if (key == best) key = UINT64_MAX;
+    }
+}
+
+template <int W>
+struct BvShape {
+    static constexpr int KF = (2 * W + 31) / 32;           // words holding band bits 0..2w-1
+    static constexpr bool ELIDE = (2 * W == 32 * KF);       // insertion bit 2w in a word of its own
+    static constexpr int ND = KF + 1;                       // dwords fetched per query per column
+    static constexpr int OFF = W + 31;                      // Peq bit of query row i = i + OFF
+    static constexpr uint32_t TOPMASK = ELIDE ? 0xffffffffu : ((1u << ((2 * W) & 31)) - 1);
+};
+
+// one query's column state
+template <int KF>
+struct BvState {
+    uint32_t P[KF], M[KF];
+    uint32_t acc;  // bit per column: (M | Xh) & 1  (= 1 - increment of T)
+    uint32_t T;    // T at the start of the current 32-column block
+};
+
+template <int W, int t>
+__device__ __forceinline__ void bv_column(BvState<BvShape<W>::KF> &S, const uint32_t (&d)[BvShape<W>::ND]) {
+    using SH = BvShape<W>;
+    constexpr int KF = SH::KF;
+    uint32_t Eq[KF], Xv[KF], Xh[KF], Ph[KF], Mh[KF];
+#pragma unroll
+    for (int k = 0; k < KF; ++k) Eq[k] = t == 0 ? d[k] : alignbit(d[k + 1], d[k], t);
+#pragma unroll
+    for (int k = 0; k < KF; ++k) Xv[k] = Eq[k] | S.M[k];
+    // X = (Eq & P) + P over KF words
+    if constexpr (KF == 1) {
+        const uint32_t X = (Eq[0] & S.P[0]) + S.P[0];
+        Xh[0] = (X ^ S.P[0]) | Eq[0];
+    } else {
+        static_assert(KF == 2, "KF <= 2 (w <= 32)");
+        const uint64_t p = ((uint64_t)S.P[1] << 32) | S.P[0];
+        const uint64_t e = ((uint64_t)(Eq[1] & S.P[1]) << 32) | (Eq[0] & S.P[0]);
+        const uint64_t X = e + p;
+        Xh[0] = ((uint32_t)X ^ S.P[0]) | Eq[0];
+        Xh[1] = ((uint32_t)(X >> 32) ^ S.P[1]) | Eq[1];
+    }
+#pragma unroll
+    for (int k = 0; k < KF; ++k) {
+        Ph[k] = S.M[k] | ~(Xh[k] | S.P[k]);
+        Mh[k] = S.P[k] & Xh[k];
+    }
+    S.acc = alignbit(S.M[0] | Xh[0], S.acc, 1);
+    uint32_t Xs[KF];
+#pragma unroll
+    for (int k = 0; k + 1 < KF; ++k) Xs[k] = alignbit(Xv[k + 1], Xv[k], 1);
+    if constexpr (SH::ELIDE) {
+        // bit 2w-1 of Xs = Xv bit 2w = Eq bit 2w (M bit 2w is 0: inserted +1)
+        Xs[KF - 1] = alignbit(d[KF] >> t, Xv[KF - 1], 1);
+    } else {
+        Xs[KF - 1] = Xv[KF - 1] >> 1;
+    }
+#pragma unroll
+    for (int k = 0; k < KF; ++k) {
+        S.P[k] = Mh[k] | ~(Xs[k] | Ph[k]);
+        S.M[k] = Ph[k] & Xs[k];
+    }
+    if constexpr (!SH::ELIDE) {
+        constexpr uint32_t ins = 1u << ((2 * W) & 31);
+        S.P[KF - 1] |= ins;
+        S.M[KF - 1] &= ~ins;
+    }
+}
+
+// D(n, m) once column m = j is done: T_j + sum of the first k' vertical deltas
+template <int W>
+__device__ __forceinline__ uint32_t bv_extract(const BvState<BvShape<W>::KF> &S, uint32_t Tj, uint32_t kp) {
+    int32_t v = (int32_t)Tj;
+#pragma unroll
+    for (int k = 0; k < BvShape<W>::KF; ++k) {
+        const int32_t lo = (int32_t)kp - 32 * k;
+        const uint32_t mask = lo >= 32 ? 0xffffffffu : (lo <= 0 ? 0u : ((1u << lo) - 1));
+        v += __builtin_popcount(S.P[k] & mask) - __builtin_popcount(S.M[k] & mask);
+    }
+    return (uint32_t)v;
+}
+
+template <int W>
+__device__ __forceinline__ void bv_init(BvState<BvShape<W>::KF> &S) {
+    // column 0: rows r_1+k (r_1 = 1-w): k < w are rows <= 0 (delta -1), k >= w rows >= 1 (+1)
+#pragma unroll
+    for (int k = 0; k < BvShape<W>::KF; ++k) {
+        uint32_t mm = 0, pp = 0;
+        for (int b = 0; b < 32; ++b) {
+            const int bit = 32 * k + b;
+            if (bit < W) mm |= 1u << b;
+            else if (bit <= 2 * W) pp |= 1u << b;
+        }
+        S.M[k] = mm;
+        S.P[k] = pp;
+    }
+    S.acc = 0;
+    S.T = W;
+}
+
+template <int W>
+__device__ __forceinline__ uint32_t bv_lower_bound(const BvState<BvShape<W>::KF> &S, uint32_t Tj) {
+    int32_t v = (int32_t)Tj;
+#pragma unroll
+    for (int k = 0; k < BvShape<W>::KF; ++k)
+        v -= __builtin_popcount(k == BvShape<W>::KF - 1 ? (S.M[k] & BvShape<W>::TOPMASK) : S.M[k]);
+    return (uint32_t)(v < 0 ? 0 : v);
+}
+
+template <int W, int t, bool SLOW>
+__device__ __forceinline__ void bv_step2(BvState<BvShape<W>::KF> &S1, BvState<BvShape<W>::KF> &S2,
+                                         const uint32_t *peq_bytes, uint32_t addr, uint32_t j, uint32_t m,
+                                         uint32_t n1, uint32_t n2, bool &run1, bool &run2, uint32_t &r1,
+                                         uint32_t &r2) {
+    using SH = BvShape<W>;
+    const uint2 *pp = (const uint2 *)((const char *)peq_bytes + addr);
+    uint32_t d1[SH::ND], d2[SH::ND];
+#pragma unroll
+    for (int k = 0; k < SH::ND; ++k) {
+        const uint2 x = pp[k];
+        d1[k] = x.x;
+        d2[k] = x.y;
+    }
+    bv_column<W, t>(S1, d1);
+    bv_column<W, t>(S2, d2);
+    if constexpr (SLOW) {
+        if (j == m) {
+            if (run1) {
+                const uint32_t Tj = S1.T + (t + 1) - __builtin_popcount(S1.acc >> (31 - t));
+                r1 = min(bv_extract<W>(S1, Tj, n1 + W - m), (uint32_t)W + 1);
+                run1 = false;
+            }
+            if (run2) {
+                const uint32_t Tj = S2.T + (t + 1) - __builtin_popcount(S2.acc >> (31 - t));
+                r2 = min(bv_extract<W>(S2, Tj, n2 + W - m), (uint32_t)W + 1);
+                run2 = false;
+            }
+        }
+    }
+}
+
+template <int W, bool SLOW, int t = 0>
+__device__ __forceinline__ void bv_block(BvState<BvShape<W>::KF> &S1, BvState<BvShape<W>::KF> &S2,
+                                         const uint32_t *peq, const uint32_t (&sym)[16], uint32_t base,
+                                         uint32_t j0, uint32_t m, uint32_t n1, uint32_t n2, bool &run1, bool &run2,
+                                         uint32_t &r1, uint32_t &r2) {
+    if constexpr (t < 32) {
+        const uint32_t w = sym[t / 2];
+        const uint32_t addr = ((t & 1) ? (w >> 16) : (w & 0xffffu)) + base;
+        bv_step2<W, t, SLOW>(S1, S2, peq, addr, j0 + t + 1, m, n1, n2, run1, run2, r1, r2);
+        bv_block<W, SLOW, t + 1>(S1, S2, peq, sym, base, j0, m, n1, n2, run1, run2, r1, r2);
+    }
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void k_ed_bv(EdBvArgs A) {
+    using SH = BvShape<W>;
+    extern __shared__ uint32_t peq[];
+    // XCD-aware: hardware block h runs on XCD h % 8; each XCD gets a
+    // contiguous range of logical blocks, so the 32 blocks of one chunk
+    // (same candidate groups, 64 query traces) share that XCD's L2.
+    const uint32_t nblk = gridDim.x, per_xcd = nblk / 8;
+    const uint32_t lb = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
+    const uint64_t lchunk = lb / 32;
+    if (lchunk >= A.n_chunks) return;  // whole workgroup: no barrier reached yet
+    const uint64_t chunk = lchunk * A.n_shards + A.shard;
+    // block row b: largest b with chunk_start[b] <= chunk
+    uint32_t lo = 0, hi = A.G;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (A.chunk_start[mid] <= chunk) lo = mid; else hi = mid;
+    }
+    const uint32_t b = lo;
+    const uint32_t gq = (uint32_t)(chunk - A.chunk_start[b]);
+    const uint32_t q1 = 64 * b + 2 * (lb % 32), q2 = q1 + 1;
+    const uint32_t n1 = q1 < A.N ? A.len[q1] : 0, n2 = q2 < A.N ? A.len[q2] : 0;
+
+    // ---- per-query match bitmaps (both queries of this workgroup) ----
+    {
+        uint4 *p4 = (uint4 *)peq;
+        for (uint32_t i = threadIdx.x; i < A.lds_dw / 4; i += 256) p4[i] = make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    {
+        const uint16_t *a1 = A.qsym + (q1 < A.N ? A.qoff[q1] : 0);
+        const uint16_t *a2 = A.qsym + (q2 < A.N ? A.qoff[q2] : 0);
+        for (uint32_t i = threadIdx.x; i < n1; i += 256) {
+            const uint32_t p = i + 1 + SH::OFF;
+            atomicOr(&peq[((uint32_t)a1[i] * A.ndw + (p >> 5)) * 2 + 0], 1u << (p & 31));
+        }
+        for (uint32_t i = threadIdx.x; i < n2; i += 256) {
+            const uint32_t p = i + 1 + SH::OFF;
+            atomicOr(&peq[((uint32_t)a2[i] * A.ndw + (p >> 5)) * 2 + 1], 1u << (p & 31));
+        }
+    }
+    __syncthreads();
+
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t g = b + 4 * gq + wave;
+    if (g >= A.G) return;
+    const uint32_t j = 64 * g + lane;
+    const bool v1 = q1 < A.N && j < A.N && j > q1;
+    const bool v2 = q2 < A.N && j < A.N && j > q2;
+    const uint32_t m = j < A.N ? A.len[j] : 0;
+    uint32_t r1 = W + 1, r2 = W + 1;
+    const int32_t dd1 = (int32_t)m - (int32_t)n1, dd2 = (int32_t)m - (int32_t)n2;
+    bool run1 = v1 && dd1 <= W && dd1 >= -W;
+    bool run2 = v2 && dd2 <= W && dd2 >= -W;
+    // empty traces: D = the other length (<= w here)
+    if (run1 && (n1 == 0 || m == 0)) { r1 = n1 + m; run1 = false; }
+    if (run2 && (n2 == 0 || m == 0)) { r2 = n2 + m; run2 = false; }
+
+    uint32_t jmax = (run1 || run2) ? m : 0;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) jmax = max(jmax, (uint32_t)__shfl_xor((int)jmax, off, 64));
+    jmax = __builtin_amdgcn_readfirstlane(jmax);
+
+    if (jmax > 0) {
+        BvState<SH::KF> S1, S2;
+        bv_init<W>(S1);
+        bv_init<W>(S2);
+        const uint4 *cs = (const uint4 *)(A.bsym + A.boff[g]) + lane;  // [pos/8][lane] uint4
+        uint32_t cur[16], nxt[16];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint4 v = cs[r * 64];
+            cur[4 * r] = v.x; cur[4 * r + 1] = v.y; cur[4 * r + 2] = v.z; cur[4 * r + 3] = v.w;
+        }
+        for (uint32_t kb = 0; 32 * kb < jmax; ++kb) {
+            // prefetch the next 32 candidate symbols (streams carry one spare block)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint4 v = cs[(4 * (kb + 1) + r) * 64];
+                nxt[4 * r] = v.x; nxt[4 * r + 1] = v.y; nxt[4 * r + 2] = v.z; nxt[4 * r + 3] = v.w;
+            }
+            const uint32_t j0 = 32 * kb;
+            const uint32_t base = (kb + 1) * 8;  // dword (kb+1) of each row, 2 queries x 4 B
+            const bool here = (run1 || run2) && m > j0 && m <= j0 + 32;
+            if (__any(here)) {
+                bv_block<W, true>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2);
+            } else {
+                bv_block<W, false>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2);
+            }
+            S1.T += 32 - __builtin_popcount(S1.acc);
+            S2.T += 32 - __builtin_popcount(S2.acc);
+            if (run1 && bv_lower_bound<W>(S1, S1.T) > W) run1 = false;
+            if (run2 && bv_lower_bound<W>(S2, S2.T) > W) run2 = false;
+            if (!__any(run1 || run2)) break;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) cur[r] = nxt[r];
+        }
+    }
+    // publish: candidate lists (per lane) and query lists (wave-reduced)
+    const uint64_t key1 = v1 ? (((uint64_t)r1 << 32) | j) : UINT64_MAX;
+    const uint64_t key2 = v2 ? (((uint64_t)r2 << 32) | j) : UINT64_MAX;
+    if (v1) bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, ((uint64_t)r1 << 32) | q1);
+    if (v2) bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, ((uint64_t)r2 << 32) | q2);
+    if (q1 < A.N) bv_knn_insert_wave(A.knn + (uint64_t)q1 * A.k, A.k, key1, lane);
+    if (q2 < A.N) bv_knn_insert_wave(A.knn + (uint64_t)q2 * A.k, A.k, key2, lane);
+}
+
+bool ed_bv_supported(uint32_t band) { return band == 8 || band == 16 || band == 32; }
+
+int ed_bv_launch(const EdBvArgs &A, uint32_t band, uint64_t blocks, hipStream_t st) {
+    const size_t lds = (size_t)A.lds_dw * 4;
+    switch (band) {
+        case 8: hipLaunchKernelGGL(k_ed_bv<8>, dim3((unsigned)blocks), dim3(256), lds, st, A); break;
+        case 16: hipLaunchKernelGGL(k_ed_bv<16>, dim3((unsigned)blocks), dim3(256), lds, st, A); break;
+        case 32: hipLaunchKernelGGL(k_ed_bv<32>, dim3((unsigned)blocks), dim3(256), lds, st, A); break;
+        default: return fail(NMZ_EINVAL, "internal: band has no bit-parallel kernel");
+    }
+    NMZ_HIP(hipGetLastError());
+    return NMZ_OK;
+}
+
+}  // namespace nmz

@@ -22,4 +22,19 @@ struct Carve {
     static size_t bytes_for(size_t count, size_t elem) { return (count * elem + 255) & ~size_t(255); }
 };
 
+// bit-parallel banded edit distance (ed_bv.hip)
+struct EdBvArgs {
+    const uint16_t *qsym;         // query symbols (dense ids), CSR order
+    const uint64_t *qoff;         // [N+1]
+    const uint32_t *len;          // [N]
+    const uint16_t *bsym;         // candidate Peq-row byte offsets, [group][pos/8][lane][8]
+    const uint64_t *boff;         // [G] element offset of each group's stream
+    const uint64_t *chunk_start;  // [G+1] first chunk of each 64-query block row
+    uint64_t *knn;                // [N][k]
+    uint64_t n_chunks;            // chunks of this shard
+    uint32_t N, G, k, ndw, lds_dw, shard, n_shards;
+};
+bool ed_bv_supported(uint32_t band);
+int ed_bv_launch(const EdBvArgs &A, uint32_t band, uint64_t blocks, hipStream_t st);
+
 }  // namespace nmz

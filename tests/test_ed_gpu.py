@@ -124,7 +124,7 @@ def test_knn_device_plan_api(ctx):
     ts = make_traces(300, 150, 200, 0.03)
     plan = ctypes.c_void_p()
     _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), len(ts), 32, ctypes.byref(plan)))
-    assert L.nmz_ed_plan_is_fast(plan) == 1
+    assert L.nmz_ed_plan_is_fast(plan) == 2  # bit-parallel kernel
     k = 8
     d_keys = torch.empty(len(ts) * k, dtype=torch.int64, device="cuda")
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -149,3 +149,45 @@ def test_knn_config3_shape_sampled(ctx):
         order = np.lexsort((pairs[:, 1], d))[:8]
         assert ds[q].tolist() == d[order].tolist()
         assert ids[q].tolist() == pairs[order, 1].tolist()
+
+
+@pytest.mark.parametrize("w", [8, 16, 32])
+def test_knn_tile_kernel_mid_alphabet(ctx, w):
+    """Alphabet too large for the bit-parallel LDS tables -> packed-u16 tile kernel."""
+    ts = make_traces(150, 280, 400, 0.03, alphabet=3000, rng=np.random.default_rng(w))
+    from namazu_amd import _lib as L
+    plan = ctypes.c_void_p()
+    L.check(L.load().nmz_ed_plan_create(ctx.handle, L.ptr(ts.off), L.ptr(ts.sym), len(ts), w, ctypes.byref(plan)))
+    kind = L.load().nmz_ed_plan_is_fast(plan)
+    L.load().nmz_ed_plan_destroy(plan)
+    assert kind == 1
+    ids, ds = knn(ctx, ts, w, 6)
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, w, 6)
+    assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+
+
+@pytest.mark.parametrize("n,lmin,lmax,w,mut,alphabet", [
+    (300, 0, 300, 32, 0.02, 48), (257, 60, 64, 32, 0.0, 5), (200, 31, 97, 16, 0.04, 20),
+    (129, 1, 40, 8, 0.1, 3), (190, 500, 560, 32, 0.01, 100)])
+def test_knn_bitparallel_kernel(ctx, n, lmin, lmax, w, mut, alphabet):
+    ts = make_traces(n, lmin, lmax, mut, alphabet=alphabet, rng=np.random.default_rng(n + w))
+    from namazu_amd import _lib as L
+    plan = ctypes.c_void_p()
+    L.check(L.load().nmz_ed_plan_create(ctx.handle, L.ptr(ts.off), L.ptr(ts.sym), len(ts), w, ctypes.byref(plan)))
+    kind = L.load().nmz_ed_plan_is_fast(plan)
+    L.load().nmz_ed_plan_destroy(plan)
+    assert kind == 2
+    ids, ds = knn(ctx, ts, w, 8)
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, w, 8)
+    assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+
+
+def test_knn_config3_near_duplicates(ctx):
+    """L = 2048, w = 32 with low mutation rates, so most distances land inside
+    the band (exercises the end-of-trace extraction after 64 column blocks)."""
+    from namazu_amd.synth import synth_traces
+    ts = synth_traces(192, 2048, seed=11, p_transpose=0.002, p_subst=0.001)
+    ids, ds = knn(ctx, ts, 32, 8)
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, 32, 8, nthreads=16)
+    assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+    assert (od[:, 0] <= 32).all()
