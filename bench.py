@@ -227,6 +227,86 @@ def bench_random_secondary(args, torch, D, ctx, L, stream):
     return out
 
 
+ED_LEN = 2048
+ED_BAND = 32
+ED_K = 8
+
+
+def bench_ed_secondary(args, torch, D, ctx, L, stream):
+    """configs[2]: historystorage all-pairs search, N traces x 2048 events, band 32, top-8 per trace.
+    Total work is fixed (strong scaling): rank r runs shard r of N(N-1)/2 pairs; the partial k-NN key
+    lists are all_gathered over RCCL and merged on the device (nmz_knn_merge_dev) inside the step."""
+    from namazu_amd import _lib
+    from namazu_amd.synth import synth_traces
+    N, k = args.ed_traces, ED_K
+    t0 = time.time()
+    ts = synth_traces(N, ED_LEN)
+    synth_s = time.time() - t0
+    plan = ctypes.c_void_p()
+    t0 = time.time()
+    _lib.check(L.nmz_ed_plan_create(ctx.handle, host_ptr(ts.off), host_ptr(ts.sym), N, ED_BAND, ctypes.byref(plan)))
+    plan_ms = (time.time() - t0) * 1e3
+    kind = {2: "k_ed_bv", 1: "k_ed_tile", 0: "k_ed_generic"}[L.nmz_ed_plan_is_fast(plan)]
+    dev = torch.device("cuda", D.local_rank)
+    d_knn = torch.empty(N * k, dtype=torch.int64, device=dev)
+    d_parts = torch.empty(D.world * N * k, dtype=torch.int64, device=dev) if D.world > 1 else None
+    d_out = torch.empty(N * k, dtype=torch.int64, device=dev) if D.world > 1 else d_knn
+
+    def step():
+        _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, D.rank, D.world, ctypes.c_void_p(d_knn.data_ptr()),
+                                                   stream))
+        if D.pg:
+            D.pg.all_gather_into_tensor(d_parts, d_knn)
+            _lib.check(L.nmz_knn_merge_dev(ctx.handle, ctypes.c_void_p(d_parts.data_ptr()), D.world, N, k,
+                                           ctypes.c_void_p(d_out.data_ptr()), stream))
+
+    step()
+    torch.cuda.synchronize()
+    tname = kind[2:].encode()
+    _lib.check(L.nmz_timing_enable(ctx.handle, 1))
+    tot, cnt = ctypes.c_double(), ctypes.c_uint64()
+    L.nmz_timing_read(ctx.handle, tname, ctypes.byref(tot), ctypes.byref(cnt), 1)
+    steps = args.ed_steps
+    D.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    D.barrier()
+    el = D.max(torch, time.perf_counter() - t0)
+    _lib.check(L.nmz_timing_read(ctx.handle, tname, ctypes.byref(tot), ctypes.byref(cnt), 1))
+    _lib.check(L.nmz_timing_enable(ctx.handle, 0))
+    L.nmz_ed_plan_destroy(plan)
+    pairs = N * (N - 1) // 2
+    cells_per_pair = ED_LEN * (2 * ED_BAND + 1) - ED_BAND * (ED_BAND + 1)
+    kern_ms = tot.value / max(cnt.value, 1)
+    out = dict(metric="trace-pair edit distances/s (banded, all-pairs k-NN)", value=pairs * steps / el,
+               unit="pairs/s", n_gpus=D.world, steps=steps, ms_per_step=el / steps * 1e3, scaling="strong",
+               config={"workload": "configs[2] historystorage all-pairs search", "traces": N, "events": ED_LEN,
+                       "band": ED_BAND, "k": k, "parallelism": f"pair-tile shards x{D.world}" +
+                       (" + RCCL all_gather k-NN merge" if D.world > 1 else "")},
+               kernel=kind, kernel_ms=kern_ms, plan_ms=plan_ms, synth_s=round(synth_s, 2),
+               band_cells_per_s=pairs * cells_per_pair * steps / el)
+    keys = d_out.cpu().numpy().view(np.uint64).reshape(N, k)
+    if D.rank == 0 and args.cpu_baseline and D.world == 1:
+        from oracle import oracle as O
+        threads = min(16, os.cpu_count() or 1)
+        q = 0
+        cand = np.array([c for c in range(N) if c != q], np.uint32)
+        pairs_s = np.stack([np.full(len(cand), q, np.uint32), cand], 1)
+        t0 = time.perf_counter()
+        dist = O.ed_pairs(ts.off, ts.sym, pairs_s, ED_BAND, nthreads=threads)
+        dt = time.perf_counter() - t0
+        order = np.lexsort((cand, dist))[:k]
+        ok = (keys[q] >> np.uint64(32)).astype(np.uint32).tolist() == dist[order].tolist() and \
+            (keys[q] & np.uint64(0xFFFFFFFF)).astype(np.uint32).tolist() == cand[order].tolist()
+        out["cpu_baseline"] = dict(value=len(cand) / dt, unit="pairs/s", cores=threads, kind="port",
+                                   sample=f"trace 0 vs all {len(cand)} others (oracle/nmz_oracle.c full-band DP, "
+                                          f"no cut-off)", seconds=round(dt, 3), parity_with_gpu=bool(ok))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -237,6 +317,8 @@ def main():
     ap.add_argument("--cpu-seeds", type=int, default=1 << 18)
     ap.add_argument("--random-seeds", type=int, default=1 << 20)
     ap.add_argument("--cpu-random-seeds", type=int, default=256)
+    ap.add_argument("--ed-traces", type=int, default=100_000)
+    ap.add_argument("--ed-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     ap.add_argument("--no-secondary", dest="secondary", action="store_false")
     args = ap.parse_args()
@@ -294,8 +376,8 @@ def main():
     if D.rank == 0 and D.world == 1 and args.cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_replayable(r, args)
     if args.secondary:
-        sec = bench_random_secondary(args, torch, D, ctx, L, stream)
-        line["secondary"] = [sec]
+        line["secondary"] = [bench_random_secondary(args, torch, D, ctx, L, stream),
+                             bench_ed_secondary(args, torch, D, ctx, L, stream)]
     if D.rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()

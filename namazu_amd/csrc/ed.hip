@@ -342,6 +342,9 @@ struct nmz_ed_plan {
     uint32_t n = 0, band = 0, G = 0;
     bool fast = false;
     bool bv = false;               // bit-parallel kernel (k_ed_bv) usable
+    bool wide = false;             // wide-band bit-parallel kernel (k_ed_wide) usable
+    uint32_t n_sym = 0;
+    uint32_t *d_peq = nullptr;     // wide: [N][n_sym][ndw] match bitmaps
     uint32_t ndw = 0, lds_dw = 0;  // bv: dwords per Peq row per query, LDS dwords per workgroup
     uint64_t n_chunks = 0;         // bv: total chunks (64-query block row x 4 candidate groups)
     uint16_t *d_bsym = nullptr;
@@ -371,7 +374,8 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
     for (uint32_t i = 0; i < N; ++i) maxlen = std::max<uint32_t>(maxlen, (uint32_t)(off[i + 1] - off[i]));
     // dense symbol ids (exact remap: a == b <=> id(a) == id(b))
     std::vector<uint16_t> ids;
-    bool fast = (band == 8 || band == 16 || band == 32) && maxlen + band < MAX_FAST_LEN;
+    const bool want_wide = ed_wide_supported(band);
+    bool fast = ((band == 8 || band == 16 || band == 32) && maxlen + band < MAX_FAST_LEN) || want_wide;
     if (fast) {
         std::unordered_map<uint64_t, uint32_t> dict;
         dict.reserve(1024);
@@ -389,7 +393,6 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
             ids[t] = (uint16_t)id;
         }
     }
-    p->fast = fast;
     auto cleanup = [&](int code) {
         p->mem.release();
         delete p;
@@ -411,7 +414,38 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
             p->lds_dw = (uint32_t)(((lds_bytes + 15) / 16) * 4);
         }
     }
-    if (fast && p->bv) {
+    if (fast && want_wide) {
+        std::vector<uint8_t> seen(65536, 0);
+        for (uint64_t t = 0; t < total; ++t)
+            if (!seen[ids[t]]) { seen[ids[t]] = 1; ++n_sym; }
+        const uint32_t ndw = ed_wide_ndw(band, maxlen);
+        const uint64_t peq_bytes = (uint64_t)N * std::max(n_sym, 1u) * ndw * 4;
+        if (peq_bytes <= (16ULL << 30)) {
+            p->wide = true;
+            p->ndw = ndw;
+            p->n_sym = std::max(n_sym, 1u);
+        } else {
+            fast = false;
+        }
+    }
+    p->fast = fast;
+    if (fast && p->wide) {
+        size_t need = Carve::bytes_for(total + 64, 2) + Carve::bytes_for(N + 1, 8) +
+                      Carve::bytes_for((uint64_t)N * p->n_sym * p->ndw, 4);
+        int rc = p->mem.ensure(need);
+        if (rc != NMZ_OK) return cleanup(rc);
+        Carve cv(p->mem.ptr);
+        p->d_qsym = cv.take<uint16_t>(total + 64);
+        p->d_qoff = cv.take<uint64_t>(N + 1);
+        p->d_peq = cv.take<uint32_t>((uint64_t)N * p->n_sym * p->ndw);
+        if (hipMemsetAsync(p->d_qsym, 0, (total + 64) * 2, st) ||
+            (total && hipMemcpyAsync(p->d_qsym, ids.data(), total * 2, hipMemcpyHostToDevice, st)) ||
+            hipMemcpyAsync(p->d_qoff, off, (N + 1) * 8, hipMemcpyHostToDevice, st))
+            return cleanup(fail(NMZ_EHIP, "ED plan upload failed"));
+        rc = ed_wide_build_peq(p->d_qsym, p->d_qoff, N, p->n_sym, p->ndw, band, p->d_peq, st);
+        if (rc != NMZ_OK) return cleanup(rc);
+        if (hipStreamSynchronize(st)) return cleanup(fail(NMZ_EHIP, "ED plan build failed"));
+    } else if (fast && p->bv) {
         const uint32_t G = (N + 63) / 64;
         p->G = G;
         const uint32_t ndw = p->ndw;
@@ -508,6 +542,25 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
     const uint32_t N = p->n;
     if (N == 0 || k == 0) return NMZ_OK;
     hipLaunchKernelGGL(k_knn_init, dim3(ceil_div((uint64_t)N * k, 256)), dim3(256), 0, st, d_knn, (uint64_t)N * k);
+    if (p->wide) {
+        EdWideArgs A;
+        A.sym = p->d_qsym;
+        A.off = p->d_qoff;
+        A.peq = p->d_peq;
+        A.knn = d_knn;
+        A.n_pairs = (uint64_t)N * (N - 1) / 2;
+        const uint64_t chunks = (A.n_pairs + 31) / 32;
+        A.n_waves = (shard < chunks ? (chunks - shard + n_shards - 1) / n_shards : 0) * 32;
+        A.N = N;
+        A.k = k;
+        A.n_sym = p->n_sym;
+        A.ndw = p->ndw;
+        A.shard = shard;
+        A.n_shards = n_shards;
+        if (A.n_waves == 0) return NMZ_OK;
+        KernelTimer kt(p->ctx, st, "ed_wide");
+        return ed_wide_launch(A, p->band, st);
+    }
     if (p->bv) {
         EdBvArgs A;
         A.qsym = p->d_qsym;
@@ -608,7 +661,10 @@ int nmz_ed_plan_destroy(nmz_ed_plan *plan) {
     return NMZ_OK;
 }
 
-int nmz_ed_plan_is_fast(const nmz_ed_plan *plan) { return plan ? (plan->bv ? 2 : (plan->fast ? 1 : 0)) : 0; }
+int nmz_ed_plan_is_fast(const nmz_ed_plan *plan) {
+    if (!plan) return 0;
+    return plan->wide ? 3 : (plan->bv ? 2 : (plan->fast ? 1 : 0));
+}
 
 int nmz_ed_allpairs_knn_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys, void *stream) {
     return nmz_ed_allpairs_knn_shard_dev(plan, k, 0, 1, d_knn_keys, stream);

@@ -35,6 +35,22 @@ struct EdBvArgs {
     uint32_t N, G, k, ndw, lds_dw, shard, n_shards;
 };
 bool ed_bv_supported(uint32_t band);
+
+// wide-band bit-parallel edit distance (ed_wide.hip): one pair per wave
+struct EdWideArgs {
+    const uint16_t *sym;   // dense symbol ids, CSR order (padded with 64 zeros)
+    const uint64_t *off;   // [N+1]
+    const uint32_t *peq;   // [N][n_sym][ndw] match bitmaps
+    uint64_t *knn;         // [N][k]
+    uint64_t n_pairs;      // N(N-1)/2
+    uint64_t n_waves;      // waves of this shard (chunks of 32 pairs dealt round-robin)
+    uint32_t N, k, n_sym, ndw, shard, n_shards;
+};
+bool ed_wide_supported(uint32_t band);
+uint32_t ed_wide_ndw(uint32_t band, uint32_t max_len);
+int ed_wide_build_peq(const uint16_t *d_sym, const uint64_t *d_off, uint32_t N, uint32_t n_sym, uint32_t ndw,
+                      uint32_t band, uint32_t *d_peq, hipStream_t st);
+int ed_wide_launch(const EdWideArgs &A, uint32_t band, hipStream_t st);
 int ed_bv_launch(const EdBvArgs &A, uint32_t band, uint64_t blocks, hipStream_t st);
 
 }  // namespace nmz

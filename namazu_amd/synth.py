@@ -2,6 +2,9 @@
 
 * zk_hints: replay hints in pynmz's format (misc/pynmz/inspector/zookeeper.py:113,
   str(hash(frozenset(...))) = decimal signed int64), from SplitMix64.
+* etcd_traces: configs[4] long traces -- 64 event symbols (etcd raft
+  messages x members), transpositions 1%, substitutions 0.3%, so pair
+  distances (~0.046 per event, ~3000 at 65,536 events) stay inside w = 4096.
 * synth_traces: SURVEY 8(d) config 3 -- a ZooKeeper-style Markov base sequence
   over 48 event symbols (the stored example traces hold 38 distinct events),
   each trace = base + adjacent transpositions at 2% + substitutions at 0.5%,
@@ -60,3 +63,8 @@ def synth_traces(n, length, seed=0x5EED, n_symbols=48, p_transpose=0.02, p_subst
         ids[c0:c0 + c] = t
     ts.sym = sym_hash[ids.reshape(-1)]
     return ts
+
+
+def etcd_traces(n, length, seed=0xE7CD):
+    """configs[4]: n etcd-style traces of `length` events (see module docstring)."""
+    return synth_traces(n, length, seed=seed, n_symbols=64, p_transpose=0.01, p_subst=0.003)

@@ -191,3 +191,34 @@ def test_knn_config3_near_duplicates(ctx):
     oi, od = O.ed_allpairs_knn(ts.off, ts.sym, 32, 8, nthreads=16)
     assert np.array_equal(ids, oi) and np.array_equal(ds, od)
     assert (od[:, 0] <= 32).all()
+
+
+@pytest.mark.parametrize("n,lmin,lmax,w,mut,alphabet", [
+    (12, 2500, 2600, 1024, 0.05, 30),      # distances inside the band, ragged lengths
+    (9, 1500, 3400, 1024, 0.02, 8),        # |n - m| > w for some pairs
+    (10, 4000, 4100, 2048, 0.3, 20),       # distances past the band: cut-off path
+    (7, 9000, 9050, 4096, 0.1, 64),        # configs[4] band, lengths not multiples of 32
+    (5, 0, 40, 1024, 0.5, 4),              # short and empty traces
+])
+def test_knn_wide_kernel(ctx, n, lmin, lmax, w, mut, alphabet):
+    ts = make_traces(n, lmin, lmax, mut, alphabet=alphabet, rng=np.random.default_rng(n * 7 + w))
+    plan = ctypes.c_void_p()
+    L = _lib.load()
+    _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), len(ts), w, ctypes.byref(plan)))
+    kind = L.nmz_ed_plan_is_fast(plan)
+    L.nmz_ed_plan_destroy(plan)
+    assert kind == 3
+    k = min(4, max(n - 1, 1))
+    ids, ds = knn(ctx, ts, w, k)
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, w, k, nthreads=16)
+    assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+
+
+def test_knn_wide_etcd_shape(ctx):
+    """configs[4] trace model (etcd-style, w = 4096) at 16k events, 6 traces."""
+    from namazu_amd.synth import etcd_traces
+    ts = etcd_traces(6, 16384, seed=3)
+    ids, ds = knn(ctx, ts, 4096, 3)
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, 4096, 3, nthreads=16)
+    assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+    assert (od[:, 0] < 4096).all()

@@ -20,9 +20,9 @@ def main():
     reps = int(sys.argv[5]) if len(sys.argv) > 5 else 3
     import torch
     from namazu_amd import _lib
-    from namazu_amd.synth import synth_traces
+    from namazu_amd.synth import etcd_traces, synth_traces
     t0 = time.time()
-    ts = synth_traces(N, L)
+    ts = etcd_traces(N, L) if (len(sys.argv) > 6 and sys.argv[6] == "etcd") else synth_traces(N, L)
     print(f"synth {time.time() - t0:.1f}s", flush=True)
     Lb = _lib.load()
     ctx = _lib.Context(0)
@@ -43,12 +43,12 @@ def main():
         pairs = N * (N - 1) / 2
         print(f"rep {r}: {el * 1e3:.2f} ms  {pairs / el:.3e} pairs/s  "
               f"{pairs * (L * (2 * W + 1) - W * (W + 1)) / el:.3e} band-cells/s", flush=True)
-    kname = b"ed_bv" if Lb.nmz_ed_plan_is_fast(plan) == 2 else b"ed_tile"
+    kname = {3: b"ed_wide", 2: b"ed_bv", 1: b"ed_tile"}.get(Lb.nmz_ed_plan_is_fast(plan), b"none")
     _lib.check(Lb.nmz_timing_read(ctx.handle, kname, ctypes.byref(tot), ctypes.byref(cnt), 1))
     print(f"kernel avg {tot.value / max(cnt.value, 1):.3f} ms over {cnt.value}")
     keys = d_knn.cpu().numpy().view(np.uint64).reshape(N, k)
     d = (keys >> np.uint64(32)).astype(np.int64)
-    print("knn dist histogram (first col):", np.bincount(np.minimum(d[:, 0], W + 1))[-5:])
+    print("knn first-col dist: min", d[:, 0].min(), "median", int(np.median(d[:, 0])), "max", d[:, 0].max())
     Lb.nmz_ed_plan_destroy(plan)
     ctx.close()
 
