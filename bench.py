@@ -39,7 +39,23 @@ MAX_INTERVAL_NS = 100_000_000
 # the gfx950 ISA of the steady-state loop has 82 per 8 decisions = 10.25, the rest is
 # the per-segment binary search, staging and folds.
 REPLAY_VALU_PER_DEC = 11.0
-RANDOM_VALU_PER_DEC = 170.0  # SURVEY 8(d) declared model for the random decision
+# k_random_sweep: SQ_INSTS_VALU 2.949e10 per launch of 2^20 seeds x 10^4 events (profiles/r01d_summary.json)
+# -> 180.0 lane-instructions per decision (SURVEY 8(d) declared model: ~170)
+RANDOM_VALU_PER_DEC = 2.949e10 * 64 / (2**20 * 10**4)
+# k_ed_bv<32> on configs[2] (100k x 2048, w=32): SQ_INSTS_VALU 1.3585e12 per launch of 4,999,950,000 pairs
+# (profiles/r01d_summary.json) -> lane-instructions per pair; the cut-off makes it input-dependent, so it
+# is valid for this synthetic workload only
+ED_BV_VALU_PER_PAIR = 1.3585e12 * 64 / 4_999_950_000
+# k_ed_wide<4> on configs[4] (256 x 65536, w=4096): SQ_INSTS_VALU 1.218e11 per launch of 32,640 pairs
+# (profiles/r01e_summary.json) = 56.9 per wave-column (ISA: 56.6); no cut-off, etcd-style distances stay in band
+ED_WIDE_VALU_PER_PAIR = 1.21801e11 * 64 / 32640
+
+
+def roofline_valu(kernel, ops_per_unit, units, kernel_ms, source):
+    achieved = ops_per_unit * units / (kernel_ms * 1e-3) / 1e12
+    return {"bound": "valu", "achieved": achieved, "peak": PEAK_VALU_TOPS, "unit": "Tops/s",
+            "frac": achieved / PEAK_VALU_TOPS, "traffic": None, "kernel": kernel, "kernel_ms": kernel_ms,
+            "ops_per_unit": ops_per_unit, "units_per_launch": units, "ops_source": source}
 
 
 def splitmix64(state, n):
@@ -211,7 +227,9 @@ def bench_random_secondary(args, torch, D, ctx, L, stream):
     out = dict(metric="random-policy fault-sweep decisions/s", value=dec / el, unit="decisions/s",
                config={"workload": "configs[3] share", "seeds_per_gpu": S, "events": E, "entities": 16,
                        "prioritized": 4, "fault_probability": 0.1},
-               ms_per_step=el / steps * 1e3, kernel_ms=kern_ms)
+               ms_per_step=el / steps * 1e3, kernel_ms=kern_ms,
+               roofline=roofline_valu("k_random_sweep", RANDOM_VALU_PER_DEC, S * E, kern_ms,
+                                      "SQ_INSTS_VALU per launch, profiles/r01d_summary.json"))
     stats = np.frombuffer(d_stats.cpu().numpy().tobytes(), dtype=_lib.SCHED_STATS_DTYPE)
     if D.rank == 0 and args.cpu_baseline and D.world == 1:
         from oracle import oracle as O
@@ -227,26 +245,21 @@ def bench_random_secondary(args, torch, D, ctx, L, stream):
     return out
 
 
-ED_LEN = 2048
-ED_BAND = 32
-ED_K = 8
-
-
-def bench_ed_secondary(args, torch, D, ctx, L, stream):
-    """configs[2]: historystorage all-pairs search, N traces x 2048 events, band 32, top-8 per trace.
+def bench_ed_secondary(args, torch, D, ctx, L, stream, spec):
+    """All-pairs banded edit-distance k-NN (configs[2] and configs[4]).
     Total work is fixed (strong scaling): rank r runs shard r of N(N-1)/2 pairs; the partial k-NN key
     lists are all_gathered over RCCL and merged on the device (nmz_knn_merge_dev) inside the step."""
     from namazu_amd import _lib
-    from namazu_amd.synth import synth_traces
-    N, k = args.ed_traces, ED_K
+    from namazu_amd import synth
+    N, k, ED_LEN, ED_BAND = spec["traces"], spec["k"], spec["events"], spec["band"]
     t0 = time.time()
-    ts = synth_traces(N, ED_LEN)
+    ts = getattr(synth, spec["generator"])(N, ED_LEN)
     synth_s = time.time() - t0
     plan = ctypes.c_void_p()
     t0 = time.time()
     _lib.check(L.nmz_ed_plan_create(ctx.handle, host_ptr(ts.off), host_ptr(ts.sym), N, ED_BAND, ctypes.byref(plan)))
     plan_ms = (time.time() - t0) * 1e3
-    kind = {2: "k_ed_bv", 1: "k_ed_tile", 0: "k_ed_generic"}[L.nmz_ed_plan_is_fast(plan)]
+    kind = {3: "k_ed_wide", 2: "k_ed_bv", 1: "k_ed_tile", 0: "k_ed_generic"}[L.nmz_ed_plan_is_fast(plan)]
     dev = torch.device("cuda", D.local_rank)
     d_knn = torch.empty(N * k, dtype=torch.int64, device=dev)
     d_parts = torch.empty(D.world * N * k, dtype=torch.int64, device=dev) if D.world > 1 else None
@@ -266,7 +279,7 @@ def bench_ed_secondary(args, torch, D, ctx, L, stream):
     _lib.check(L.nmz_timing_enable(ctx.handle, 1))
     tot, cnt = ctypes.c_double(), ctypes.c_uint64()
     L.nmz_timing_read(ctx.handle, tname, ctypes.byref(tot), ctypes.byref(cnt), 1)
-    steps = args.ed_steps
+    steps = spec["steps"]
     D.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -283,10 +296,12 @@ def bench_ed_secondary(args, torch, D, ctx, L, stream):
     kern_ms = tot.value / max(cnt.value, 1)
     out = dict(metric="trace-pair edit distances/s (banded, all-pairs k-NN)", value=pairs * steps / el,
                unit="pairs/s", n_gpus=D.world, steps=steps, ms_per_step=el / steps * 1e3, scaling="strong",
-               config={"workload": "configs[2] historystorage all-pairs search", "traces": N, "events": ED_LEN,
+               config={"workload": spec["workload"], "traces": N, "events": ED_LEN, "generator": spec["generator"],
                        "band": ED_BAND, "k": k, "parallelism": f"pair-tile shards x{D.world}" +
                        (" + RCCL all_gather k-NN merge" if D.world > 1 else "")},
                kernel=kind, kernel_ms=kern_ms, plan_ms=plan_ms, synth_s=round(synth_s, 2),
+               roofline=roofline_valu(kind, spec["valu_per_pair"], (pairs + D.world - 1) // D.world, kern_ms,
+                                      spec["valu_source"]) if spec.get("valu_per_pair") else None,
                band_cells_per_s=pairs * cells_per_pair * steps / el)
     keys = d_out.cpu().numpy().view(np.uint64).reshape(N, k)
     if D.rank == 0 and args.cpu_baseline and D.world == 1:
@@ -376,8 +391,15 @@ def main():
     if D.rank == 0 and D.world == 1 and args.cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_replayable(r, args)
     if args.secondary:
+        ed3 = dict(workload="configs[2] historystorage all-pairs search", traces=args.ed_traces, events=2048,
+                   band=32, k=8, generator="synth_traces", steps=args.ed_steps, valu_per_pair=ED_BV_VALU_PER_PAIR,
+                   valu_source="SQ_INSTS_VALU per launch, profiles/r01d_summary.json")
+        ed5 = dict(workload="configs[4] long-trace stress, wide band", traces=256, events=65536, band=4096, k=8,
+                   generator="etcd_traces", steps=args.ed_steps, valu_per_pair=ED_WIDE_VALU_PER_PAIR,
+                   valu_source="SQ_INSTS_VALU per launch, profiles/r01e_summary.json")
         line["secondary"] = [bench_random_secondary(args, torch, D, ctx, L, stream),
-                             bench_ed_secondary(args, torch, D, ctx, L, stream)]
+                             bench_ed_secondary(args, torch, D, ctx, L, stream, ed3),
+                             bench_ed_secondary(args, torch, D, ctx, L, stream, ed5)]
     if D.rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()
