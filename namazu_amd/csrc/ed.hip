@@ -342,13 +342,15 @@ struct nmz_ed_plan {
     uint32_t n = 0, band = 0, G = 0;
     bool fast = false;
     bool bv = false;               // bit-parallel kernel (k_ed_bv) usable
+    uint64_t *d_soff = nullptr;    // bv: per-trace stream offsets
+    uint32_t pool = 0;
     bool wide = false;             // wide-band bit-parallel kernel (k_ed_wide) usable
     uint32_t n_sym = 0;
     uint32_t *d_peq = nullptr;     // wide: [N][n_sym][ndw] match bitmaps
     uint32_t ndw = 0, lds_dw = 0;  // bv: dwords per Peq row per query, LDS dwords per workgroup
-    uint64_t n_chunks = 0;         // bv: total chunks (64-query block row x 4 candidate groups)
+    uint64_t n_chunks = 0;         // bv: total chunks (64-query block row x ED_BV_POOL candidates)
     uint16_t *d_bsym = nullptr;
-    uint64_t *d_boff = nullptr, *d_chunk_start = nullptr;
+    uint64_t *d_chunk_start = nullptr;
     nmz::DevBuf mem;
     uint16_t *d_qsym = nullptr, *d_csym = nullptr;
     uint64_t *d_qoff = nullptr, *d_coff = nullptr;
@@ -451,37 +453,31 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         const uint32_t ndw = p->ndw;
         const uint32_t zero_row = n_sym * ndw * 8;
         std::vector<uint32_t> len(N + 1, 0);
-        std::vector<uint64_t> boff(G + 1, 0), chunk_start(G + 1, 0);
-        std::vector<uint32_t> gmax(G, 0);
+        std::vector<uint64_t> soff(N + 1, 0), chunk_start(G + 1, 0);
         for (uint32_t i = 0; i < N; ++i) {
             len[i] = (uint32_t)(off[i + 1] - off[i]);
-            gmax[i / 64] = std::max(gmax[i / 64], len[i]);
+            soff[i + 1] = soff[i] + ((uint64_t)(len[i] + 31) / 32 + 1) * 32;  // whole blocks + 1 spare
         }
-        // each group's stream: ceil(gmax/32) blocks of 32 positions + 1 spare (prefetch)
-        for (uint32_t g = 0; g < G; ++g) boff[g + 1] = boff[g] + ((uint64_t)(gmax[g] + 31) / 32 + 1) * 32 * 64;
-        for (uint32_t b = 0; b < G; ++b) chunk_start[b + 1] = chunk_start[b] + (G - b + 3) / 4;
+        p->pool = ED_BV_POOL;
+        for (uint32_t b = 0; b < G; ++b)
+            chunk_start[b + 1] = chunk_start[b] + (N - 64 * b + p->pool - 1) / p->pool;
         p->n_chunks = chunk_start[G];
-        std::vector<uint16_t> bs(boff[G], (uint16_t)zero_row);
-        for (uint32_t i = 0; i < N; ++i) {
-            uint16_t *gb = bs.data() + boff[i / 64] + (uint64_t)(i % 64) * 8;
-            for (uint32_t t = 0; t < len[i]; ++t)
-                gb[(uint64_t)(t / 8) * 512 + (t % 8)] = (uint16_t)(ids[off[i] + t] * ndw * 8);
-        }
-        size_t need = Carve::bytes_for(total + 1, 2) + Carve::bytes_for(bs.size() + 1, 2) +
-                      Carve::bytes_for(N + 1, 8) + Carve::bytes_for(G + 1, 8) * 2 + Carve::bytes_for(N + 1, 4);
+        std::vector<uint16_t> bs(soff[N] + 64, (uint16_t)zero_row);  // + 2 spare blocks at the end
+        for (uint32_t i = 0; i < N; ++i)
+            for (uint32_t t = 0; t < len[i]; ++t) bs[soff[i] + t] = (uint16_t)(ids[off[i] + t] * ndw * 8);
+        size_t need = Carve::bytes_for(bs.size(), 2) + Carve::bytes_for(N + 1, 8) * 2 +
+                      Carve::bytes_for(G + 1, 8) + Carve::bytes_for(N + 1, 4);
         int rc = p->mem.ensure(need);
         if (rc != NMZ_OK) return cleanup(rc);
         Carve cv(p->mem.ptr);
-        p->d_qsym = cv.take<uint16_t>(total + 1);
-        p->d_bsym = cv.take<uint16_t>(bs.size() + 1);
+        p->d_bsym = cv.take<uint16_t>(bs.size());
+        p->d_soff = cv.take<uint64_t>(N + 1);
         p->d_qoff = cv.take<uint64_t>(N + 1);
-        p->d_boff = cv.take<uint64_t>(G + 1);
         p->d_chunk_start = cv.take<uint64_t>(G + 1);
         p->d_len = cv.take<uint32_t>(N + 1);
-        if ((total && hipMemcpyAsync(p->d_qsym, ids.data(), total * 2, hipMemcpyHostToDevice, st)) ||
-            hipMemcpyAsync(p->d_bsym, bs.data(), bs.size() * 2, hipMemcpyHostToDevice, st) ||
+        if (hipMemcpyAsync(p->d_bsym, bs.data(), bs.size() * 2, hipMemcpyHostToDevice, st) ||
+            hipMemcpyAsync(p->d_soff, soff.data(), (N + 1) * 8, hipMemcpyHostToDevice, st) ||
             hipMemcpyAsync(p->d_qoff, off, (N + 1) * 8, hipMemcpyHostToDevice, st) ||
-            hipMemcpyAsync(p->d_boff, boff.data(), (G + 1) * 8, hipMemcpyHostToDevice, st) ||
             hipMemcpyAsync(p->d_chunk_start, chunk_start.data(), (G + 1) * 8, hipMemcpyHostToDevice, st) ||
             hipMemcpyAsync(p->d_len, len.data(), (N + 1) * 4, hipMemcpyHostToDevice, st) ||
             hipStreamSynchronize(st))
@@ -563,24 +559,22 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
     }
     if (p->bv) {
         EdBvArgs A;
-        A.qsym = p->d_qsym;
-        A.qoff = p->d_qoff;
-        A.len = p->d_len;
         A.bsym = p->d_bsym;
-        A.boff = p->d_boff;
+        A.soff = p->d_soff;
+        A.len = p->d_len;
         A.chunk_start = p->d_chunk_start;
         A.knn = d_knn;
         A.N = N;
         A.G = p->G;
         A.k = k;
-        A.ndw = p->ndw;
         A.lds_dw = p->lds_dw;
+        A.pool = p->pool;
         A.shard = shard;
         A.n_shards = n_shards;
         A.n_chunks = shard < p->n_chunks ? (p->n_chunks - shard + n_shards - 1) / n_shards : 0;
         if (A.n_chunks == 0) return NMZ_OK;
         uint64_t blocks = A.n_chunks * 32;
-        blocks = (blocks + 7) / 8 * 8;  // multiple of 8 for the XCD remap
+        blocks = (blocks + 7) / 8 * 8;
         NMZ_CHECK(blocks < (1ULL << 31), "too many traces for one launch");
         KernelTimer kt(p->ctx, st, "ed_bv");
         return ed_bv_launch(A, p->band, blocks, st);

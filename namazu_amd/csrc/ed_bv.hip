@@ -34,7 +34,7 @@
 // Peq tables: per query, one bit row per symbol of the plan's alphabet
 // (dense ids), 2 queries interleaved per dword ([symbol][dword][query]) so
 // one ds_read_b64 returns a dword of both queries.  Candidate symbols are
-// stored as that row's LDS byte offset (u16), [group][pos/8][lane][8].
+// stored as that row's LDS byte offset (u16), one stream per trace.
 #include "nmz_common.h"
 #include "nmz_internal.h"
 
@@ -219,117 +219,183 @@ __device__ __forceinline__ void bv_block(BvState<BvShape<W>::KF> &S1, BvState<Bv
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_ed_bv: the column step above with lane refill.  A workgroup owns 2 query
+// traces and a pool of up to ED_BV_POOL candidate traces; each lane works
+// on one candidate at a time and, when both of its pairs are finished
+// (extracted or cut off), publishes them and takes the next candidate from
+// the workgroup's LDS counter, restarting at column 1 in the next 32-column
+// block (lanes may be at different columns; the in-block shift t stays
+// wave-uniform because restarts happen on block boundaries).  A wave stops
+// when the pool is empty and its lanes are idle, so its cost follows the
+// mean cut-off column of its pairs instead of the maximum over 64 of them.
+// Candidate streams are per trace ([pos] u16 Peq-row byte offsets, padded to
+// whole 32-position blocks plus one spare block); the query's Peq rows are
+// built from the same streams.
+// ---------------------------------------------------------------------------
+// publish the pairs of the lanes with `fin` set: candidate lists per lane
+// (distinct lists), query lists wave-reduced (the 2 query lists are shared by
+// every lane of the workgroup; per-lane atomics on them serialize in L2)
+__device__ __forceinline__ void bv_publish(const EdBvArgs &A, bool fin, uint32_t j, uint32_t q1, uint32_t q2,
+                                            bool v2, uint32_t r1, uint32_t r2, uint32_t lane) {
+    if (fin) {
+        bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, ((uint64_t)r1 << 32) | q1);
+        if (v2) bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, ((uint64_t)r2 << 32) | q2);
+    }
+    const uint64_t k1 = fin ? (((uint64_t)r1 << 32) | j) : UINT64_MAX;
+    const uint64_t k2 = (fin && v2) ? (((uint64_t)r2 << 32) | j) : UINT64_MAX;
+    bv_knn_insert_wave(A.knn + (uint64_t)q1 * A.k, A.k, k1, lane);
+    if (q2 < A.N) bv_knn_insert_wave(A.knn + (uint64_t)q2 * A.k, A.k, k2, lane);
+}
+
+__device__ __forceinline__ void bv_load_block(uint32_t (&dst)[16], const uint16_t *stream, uint32_t blk) {
+    const uint4 *p = (const uint4 *)(stream + (uint64_t)blk * 32);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint4 v = p[r];
+        dst[4 * r] = v.x; dst[4 * r + 1] = v.y; dst[4 * r + 2] = v.z; dst[4 * r + 3] = v.w;
+    }
+}
+
 template <int W>
 __global__ __launch_bounds__(256) void k_ed_bv(EdBvArgs A) {
     using SH = BvShape<W>;
     extern __shared__ uint32_t peq[];
-    // XCD-aware: hardware block h runs on XCD h % 8; each XCD gets a
-    // contiguous range of logical blocks, so the 32 blocks of one chunk
-    // (same candidate groups, 64 query traces) share that XCD's L2.
+    // pool counter lives after the Peq tables (a static __shared__ variable
+    // would shift the dynamic region off 8-byte alignment: misaligned ds_read_b64)
+    uint32_t &pool_next = peq[A.lds_dw];
     const uint32_t nblk = gridDim.x, per_xcd = nblk / 8;
     const uint32_t lb = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
     const uint64_t lchunk = lb / 32;
-    if (lchunk >= A.n_chunks) return;  // whole workgroup: no barrier reached yet
+    if (lchunk >= A.n_chunks) return;
     const uint64_t chunk = lchunk * A.n_shards + A.shard;
-    // block row b: largest b with chunk_start[b] <= chunk
     uint32_t lo = 0, hi = A.G;
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) / 2;
         if (A.chunk_start[mid] <= chunk) lo = mid; else hi = mid;
     }
     const uint32_t b = lo;
-    const uint32_t gq = (uint32_t)(chunk - A.chunk_start[b]);
+    const uint32_t cr = (uint32_t)(chunk - A.chunk_start[b]);
     const uint32_t q1 = 64 * b + 2 * (lb % 32), q2 = q1 + 1;
-    const uint32_t n1 = q1 < A.N ? A.len[q1] : 0, n2 = q2 < A.N ? A.len[q2] : 0;
+    if (q1 >= A.N) return;  // whole workgroup
+    const bool has2 = q2 < A.N;
+    const uint32_t n1 = A.len[q1], n2 = has2 ? A.len[q2] : 0;
+    const uint32_t c0 = 64 * b + A.pool * cr;
+    const uint32_t c1 = min(c0 + A.pool, A.N);
+    const uint32_t pool_lo = max(c0, q1 + 1);
+    const uint32_t pool_n = c1 > pool_lo ? c1 - pool_lo : 0;
 
-    // ---- per-query match bitmaps (both queries of this workgroup) ----
     {
         uint4 *p4 = (uint4 *)peq;
         for (uint32_t i = threadIdx.x; i < A.lds_dw / 4; i += 256) p4[i] = make_uint4(0, 0, 0, 0);
+        if (threadIdx.x == 0) pool_next = 256;
     }
     __syncthreads();
     {
-        const uint16_t *a1 = A.qsym + (q1 < A.N ? A.qoff[q1] : 0);
-        const uint16_t *a2 = A.qsym + (q2 < A.N ? A.qoff[q2] : 0);
+        const uint16_t *a1 = A.bsym + A.soff[q1];
         for (uint32_t i = threadIdx.x; i < n1; i += 256) {
             const uint32_t p = i + 1 + SH::OFF;
-            atomicOr(&peq[((uint32_t)a1[i] * A.ndw + (p >> 5)) * 2 + 0], 1u << (p & 31));
+            atomicOr(&peq[(uint32_t)a1[i] / 4 + (p >> 5) * 2 + 0], 1u << (p & 31));
         }
-        for (uint32_t i = threadIdx.x; i < n2; i += 256) {
-            const uint32_t p = i + 1 + SH::OFF;
-            atomicOr(&peq[((uint32_t)a2[i] * A.ndw + (p >> 5)) * 2 + 1], 1u << (p & 31));
+        if (has2) {
+            const uint16_t *a2 = A.bsym + A.soff[q2];
+            for (uint32_t i = threadIdx.x; i < n2; i += 256) {
+                const uint32_t p = i + 1 + SH::OFF;
+                atomicOr(&peq[(uint32_t)a2[i] / 4 + (p >> 5) * 2 + 1], 1u << (p & 31));
+            }
         }
     }
     __syncthreads();
+    if (pool_n == 0) return;
 
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t g = b + 4 * gq + wave;
-    if (g >= A.G) return;
-    const uint32_t j = 64 * g + lane;
-    const bool v1 = q1 < A.N && j < A.N && j > q1;
-    const bool v2 = q2 < A.N && j < A.N && j > q2;
-    const uint32_t m = j < A.N ? A.len[j] : 0;
-    uint32_t r1 = W + 1, r2 = W + 1;
-    const int32_t dd1 = (int32_t)m - (int32_t)n1, dd2 = (int32_t)m - (int32_t)n2;
-    bool run1 = v1 && dd1 <= W && dd1 >= -W;
-    bool run2 = v2 && dd2 <= W && dd2 >= -W;
-    // empty traces: D = the other length (<= w here)
-    if (run1 && (n1 == 0 || m == 0)) { r1 = n1 + m; run1 = false; }
-    if (run2 && (n2 == 0 || m == 0)) { r2 = n2 + m; run2 = false; }
-
-    uint32_t jmax = (run1 || run2) ? m : 0;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) jmax = max(jmax, (uint32_t)__shfl_xor((int)jmax, off, 64));
-    jmax = __builtin_amdgcn_readfirstlane(jmax);
-
-    if (jmax > 0) {
-        BvState<SH::KF> S1, S2;
-        bv_init<W>(S1);
-        bv_init<W>(S2);
-        const uint4 *cs = (const uint4 *)(A.bsym + A.boff[g]) + lane;  // [pos/8][lane] uint4
-        uint32_t cur[16], nxt[16];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const uint4 v = cs[r * 64];
-            cur[4 * r] = v.x; cur[4 * r + 1] = v.y; cur[4 * r + 2] = v.z; cur[4 * r + 3] = v.w;
+    const uint32_t lane = threadIdx.x & 63;
+    // lane state
+    uint32_t j = 0, m = 0, r1 = W + 1, r2 = W + 1, kb0 = 0;
+    bool run1 = false, run2 = false, active = false, v2 = false;
+    const uint16_t *stream = A.bsym;
+    BvState<SH::KF> S1, S2;
+    uint32_t cur[16], nxt[16];
+    uint32_t idx = threadIdx.x;  // first 256 candidates are pre-assigned
+    uint32_t kb = 0;
+    bool need = true;
+    bool first = true;
+    while (true) {
+        // ---- (re)assign candidates to lanes that need one ----
+        while (true) {
+            const uint64_t want = __ballot(need);
+            if (want == 0) break;
+            if (!first) {
+                const uint32_t cnt = __popcll(want);
+                uint32_t base_idx = 0;
+                if (lane == (uint32_t)(__ffsll((unsigned long long)want) - 1)) base_idx = atomicAdd(&pool_next, cnt);
+                base_idx = __shfl(base_idx, __ffsll((unsigned long long)want) - 1, 64);
+                if (need) idx = base_idx + __popcll(want & ((1ull << lane) - 1));
+            }
+            first = false;
+            if (need) {
+                if (idx >= pool_n) {
+                    need = false;
+                    active = false;
+                    stream = A.bsym;  // idle lanes keep reading a valid stream (results unused)
+                    bv_load_block(cur, stream, 0);
+                } else {
+                    j = pool_lo + idx;
+                    m = A.len[j];
+                    stream = A.bsym + A.soff[j];
+                    v2 = has2 && j > q2;
+                    r1 = W + 1;
+                    r2 = W + 1;
+                    const int32_t dd1 = (int32_t)m - (int32_t)n1, dd2 = (int32_t)m - (int32_t)n2;
+                    run1 = dd1 <= W && dd1 >= -W;
+                    run2 = v2 && dd2 <= W && dd2 >= -W;
+                    if (run1 && (n1 == 0 || m == 0)) { r1 = n1 + m; run1 = false; }
+                    if (run2 && (n2 == 0 || m == 0)) { r2 = n2 + m; run2 = false; }
+                    if (run1 || run2) {
+                        need = false;
+                        active = true;
+                        kb0 = kb;
+                        bv_init<W>(S1);
+                        bv_init<W>(S2);
+                        bv_load_block(cur, stream, 0);
+                    }
+                }
+            }
+            // candidates decided without a DP (|n - m| > w, empty traces): publish, draw again
+            const bool fin = need && !active && idx < pool_n;
+            if (__any(fin)) bv_publish(A, fin, j, q1, q2, v2, r1, r2, lane);
         }
-        for (uint32_t kb = 0; 32 * kb < jmax; ++kb) {
-            // prefetch the next 32 candidate symbols (streams carry one spare block)
+        if (!__any(active)) break;
+        // ---- one 32-column block ----
+        const uint32_t lkb = active ? kb - kb0 : 0;
+        bv_load_block(nxt, stream, lkb + 1);  // streams carry one spare block
+        const uint32_t j0 = 32 * lkb;
+        const uint32_t base = (lkb + 1) * 8;
+        const bool here = active && (run1 || run2) && m > j0 && m <= j0 + 32;
+        if (__any(here)) {
+            bv_block<W, true>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2);
+        } else {
+            bv_block<W, false>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2);
+        }
+        S1.T += 32 - __builtin_popcount(S1.acc);
+        S2.T += 32 - __builtin_popcount(S2.acc);
+        if (run1 && bv_lower_bound<W>(S1, S1.T) > W) run1 = false;
+        if (run2 && bv_lower_bound<W>(S2, S2.T) > W) run2 = false;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const uint4 v = cs[(4 * (kb + 1) + r) * 64];
-                nxt[4 * r] = v.x; nxt[4 * r + 1] = v.y; nxt[4 * r + 2] = v.z; nxt[4 * r + 3] = v.w;
-            }
-            const uint32_t j0 = 32 * kb;
-            const uint32_t base = (kb + 1) * 8;  // dword (kb+1) of each row, 2 queries x 4 B
-            const bool here = (run1 || run2) && m > j0 && m <= j0 + 32;
-            if (__any(here)) {
-                bv_block<W, true>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2);
-            } else {
-                bv_block<W, false>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2);
-            }
-            S1.T += 32 - __builtin_popcount(S1.acc);
-            S2.T += 32 - __builtin_popcount(S2.acc);
-            if (run1 && bv_lower_bound<W>(S1, S1.T) > W) run1 = false;
-            if (run2 && bv_lower_bound<W>(S2, S2.T) > W) run2 = false;
-            if (!__any(run1 || run2)) break;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) cur[r] = nxt[r];
+        for (int r = 0; r < 16; ++r) cur[r] = nxt[r];
+        ++kb;
+        const bool fin = active && !run1 && !run2;
+        if (__any(fin)) bv_publish(A, fin, j, q1, q2, v2, r1, r2, lane);
+        if (fin) {
+            active = false;
+            need = true;
         }
     }
-    // publish: candidate lists (per lane) and query lists (wave-reduced)
-    const uint64_t key1 = v1 ? (((uint64_t)r1 << 32) | j) : UINT64_MAX;
-    const uint64_t key2 = v2 ? (((uint64_t)r2 << 32) | j) : UINT64_MAX;
-    if (v1) bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, ((uint64_t)r1 << 32) | q1);
-    if (v2) bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, ((uint64_t)r2 << 32) | q2);
-    if (q1 < A.N) bv_knn_insert_wave(A.knn + (uint64_t)q1 * A.k, A.k, key1, lane);
-    if (q2 < A.N) bv_knn_insert_wave(A.knn + (uint64_t)q2 * A.k, A.k, key2, lane);
 }
 
 bool ed_bv_supported(uint32_t band) { return band == 8 || band == 16 || band == 32; }
 
 int ed_bv_launch(const EdBvArgs &A, uint32_t band, uint64_t blocks, hipStream_t st) {
-    const size_t lds = (size_t)A.lds_dw * 4;
+    const size_t lds = (size_t)A.lds_dw * 4 + 16;  // + pool counter
     switch (band) {
         case 8: hipLaunchKernelGGL(k_ed_bv<8>, dim3((unsigned)blocks), dim3(256), lds, st, A); break;
         case 16: hipLaunchKernelGGL(k_ed_bv<16>, dim3((unsigned)blocks), dim3(256), lds, st, A); break;

@@ -22,19 +22,20 @@ struct Carve {
     static size_t bytes_for(size_t count, size_t elem) { return (count * elem + 255) & ~size_t(255); }
 };
 
-// bit-parallel banded edit distance (ed_bv.hip)
+bool ed_bv_supported(uint32_t band);
+
+// bit-parallel banded edit distance (ed_bv.hip): 2 queries x a pool of ED_BV_POOL candidates per workgroup
+constexpr uint32_t ED_BV_POOL = 1024;
 struct EdBvArgs {
-    const uint16_t *qsym;         // query symbols (dense ids), CSR order
-    const uint64_t *qoff;         // [N+1]
+    const uint16_t *bsym;         // per-trace streams of Peq-row byte offsets (u16), padded to 32-blocks + 1
+    const uint64_t *soff;         // [N] element offset of each trace's stream
     const uint32_t *len;          // [N]
-    const uint16_t *bsym;         // candidate Peq-row byte offsets, [group][pos/8][lane][8]
-    const uint64_t *boff;         // [G] element offset of each group's stream
     const uint64_t *chunk_start;  // [G+1] first chunk of each 64-query block row
     uint64_t *knn;                // [N][k]
     uint64_t n_chunks;            // chunks of this shard
-    uint32_t N, G, k, ndw, lds_dw, shard, n_shards;
+    uint32_t N, G, k, lds_dw, shard, n_shards, pool;
 };
-bool ed_bv_supported(uint32_t band);
+int ed_bv_launch(const EdBvArgs &A, uint32_t band, uint64_t blocks, hipStream_t st);
 
 // wide-band bit-parallel edit distance (ed_wide.hip): one pair per wave
 struct EdWideArgs {
