@@ -42,10 +42,10 @@ REPLAY_VALU_PER_DEC = 11.0
 # k_random_sweep: SQ_INSTS_VALU 2.949e10 per launch of 2^20 seeds x 10^4 events (profiles/r01d_summary.json)
 # -> 180.0 lane-instructions per decision (SURVEY 8(d) declared model: ~170)
 RANDOM_VALU_PER_DEC = 2.949e10 * 64 / (2**20 * 10**4)
-# k_ed_bv<32> on configs[2] (100k x 2048, w=32): SQ_INSTS_VALU 1.3585e12 per launch of 4,999,950,000 pairs
-# (profiles/r01d_summary.json) -> lane-instructions per pair; the cut-off makes it input-dependent, so it
-# is valid for this synthetic workload only
-ED_BV_VALU_PER_PAIR = 1.3585e12 * 64 / 4_999_950_000
+# k_ed_bv<32> on configs[2] (100k x 2048, w=32): SQ_INSTS_VALU 1.22834e12 per launch of 4,999,950,000 pairs
+# (profiles/r01f_summary.json, lane-refill kernel) -> lane-instructions per pair; the cut-off makes it
+# input-dependent, so it is valid for this synthetic workload only
+ED_BV_VALU_PER_PAIR = 1.22834e12 * 64 / 4_999_950_000
 # k_ed_wide<4> on configs[4] (256 x 65536, w=4096): SQ_INSTS_VALU 1.218e11 per launch of 32,640 pairs
 # (profiles/r01e_summary.json) = 56.9 per wave-column (ISA: 56.6); no cut-off, etcd-style distances stay in band
 ED_WIDE_VALU_PER_PAIR = 1.21801e11 * 64 / 32640
@@ -393,7 +393,7 @@ def main():
     if args.secondary:
         ed3 = dict(workload="configs[2] historystorage all-pairs search", traces=args.ed_traces, events=2048,
                    band=32, k=8, generator="synth_traces", steps=args.ed_steps, valu_per_pair=ED_BV_VALU_PER_PAIR,
-                   valu_source="SQ_INSTS_VALU per launch, profiles/r01d_summary.json")
+                   valu_source="SQ_INSTS_VALU per launch, profiles/r01f_summary.json")
         ed5 = dict(workload="configs[4] long-trace stress, wide band", traces=256, events=65536, band=4096, k=8,
                    generator="etcd_traces", steps=args.ed_steps, valu_per_pair=ED_WIDE_VALU_PER_PAIR,
                    valu_source="SQ_INSTS_VALU per launch, profiles/r01e_summary.json")

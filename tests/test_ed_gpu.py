@@ -222,3 +222,35 @@ def test_knn_wide_etcd_shape(ctx):
     oi, od = O.ed_allpairs_knn(ts.off, ts.sym, 4096, 3, nthreads=16)
     assert np.array_equal(ids, oi) and np.array_equal(ds, od)
     assert (od[:, 0] < 4096).all()
+
+
+@pytest.mark.parametrize("w,alphabet,lmin,lmax,n,kind", [
+    (32, 20, 150, 260, 400, 2),     # k_ed_bv
+    (16, 3000, 100, 140, 200, 1),   # k_ed_tile
+    (1024, 16, 1500, 1700, 12, 3),  # k_ed_wide
+    (5, 12, 10, 60, 90, 0),         # k_ed_generic
+])
+def test_knn_shards_merge_to_full(ctx, w, alphabet, lmin, lmax, n, kind):
+    """The multi-GPU path on one device: shard s of 3 into separate partial lists,
+    merged by nmz_knn_merge_dev, equals the oracle's all-pairs k-NN."""
+    import torch
+    L = _lib.load()
+    ts = make_traces(n, lmin, lmax, 0.05, alphabet=alphabet, rng=np.random.default_rng(w + n))
+    plan = ctypes.c_void_p()
+    _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), n, w, ctypes.byref(plan)))
+    assert L.nmz_ed_plan_is_fast(plan) == kind
+    k, S = 6, 3
+    parts = torch.empty(S * n * k, dtype=torch.int64, device="cuda")
+    out = torch.empty(n * k, dtype=torch.int64, device="cuda")
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for s in range(S):
+        _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, s, S, ctypes.c_void_p(parts.data_ptr() + s * n * k * 8),
+                                                   stream))
+    _lib.check(L.nmz_knn_merge_dev(ctx.handle, ctypes.c_void_p(parts.data_ptr()), S, n, k,
+                                   ctypes.c_void_p(out.data_ptr()), stream))
+    torch.cuda.synchronize()
+    L.nmz_ed_plan_destroy(plan)
+    keys = out.cpu().numpy().view(np.uint64).reshape(n, k)
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, w, k, nthreads=16)
+    assert np.array_equal((keys >> np.uint64(32)).astype(np.uint32), od)
+    assert np.array_equal((keys & np.uint64(0xFFFFFFFF)).astype(np.uint32), oi)
