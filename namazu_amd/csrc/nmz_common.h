@@ -167,19 +167,34 @@ __host__ __device__ inline void stats_empty(nmz_sched_stats &s) {
 inline unsigned ceil_div(uint64_t a, uint64_t b) { return (unsigned)((a + b - 1) / b); }
 
 // seed bucketing by FNV low byte (shared by both sweeps)
+// The 256 global bucket counters and cursors take device-scope atomics from
+// every block; one counter per 128-byte line (stride BUCKET_STRIDE) spreads
+// them over the L2 channels instead of serialising them on 8 lines.
+constexpr uint32_t BUCKET_STRIDE = 32;
+constexpr size_t BUCKET_SMALL_U32 = 2 * 256 * BUCKET_STRIDE + 260 + 4;  // count, cursor, offset, n_units
 struct Buckets {
-    uint32_t *count;       // [256]
+    uint32_t *count;       // [256 * BUCKET_STRIDE]
     uint32_t *offset;      // [257]
-    uint32_t *cursor;      // [256]
+    uint32_t *cursor;      // [256 * BUCKET_STRIDE]
     uint32_t *n_units;     // [1]
     uint4 *units;          // [max_units] {L, start, count, 0}
     uint64_t *sorted_h0;   // [S]
     uint32_t *sorted_idx;  // [S]
 };
 
-int bucket_seeds(hipStream_t st, const uint64_t *d_h0, uint64_t n_seeds, uint32_t seeds_per_unit,
-                 uint64_t max_units, Buckets &b);
+inline void buckets_small(uint32_t *small, Buckets &b) {
+    b.count = small;
+    b.cursor = small + 256 * BUCKET_STRIDE;
+    b.offset = small + 2 * 256 * BUCKET_STRIDE;
+    b.n_units = b.offset + 260;
+}
 
-__global__ void k_bucket_hist(const uint64_t *h0, uint64_t n, uint32_t *count);
+// b.count must already hold the 256 bucket counts (filled by the caller's prefix kernel)
+int bucket_seeds_counted(hipStream_t st, const uint64_t *d_h0, uint64_t n_seeds, uint32_t seeds_per_unit,
+                         Buckets &b);
+// seeds per thread in the prefix + histogram kernels and in the scatter (tuning: NMZ_PREFIX_PT, NMZ_SCATTER_PT)
+uint32_t prefix_per_thread();
+uint32_t scatter_per_thread();
+
 
 }  // namespace nmz

@@ -1,3 +1,4 @@
+#include <cstdlib>
 // Context management, error plumbing, parameter resolution and the seed
 // bucketing pass shared by the replayable and random sweeps.
 #include <cstdio>
@@ -62,21 +63,11 @@ KernelTimer::~KernelTimer() {
 }
 
 // ---------------------------------------------------------------------------
-// Seed bucketing: counting sort of seeds by (FNV prefix state & 0xff), so a
+// Seed bucketing: counting sort of seeds by (FNV prefix state & 0xff; the
+// histogram is fused into the sweeps' prefix kernels), so a
 // wave's lanes share one row of the per-event tables and every table read in
 // the sweep loop is wave-uniform (scalar loads, no LDS, no gathers).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_bucket_hist(const uint64_t *__restrict__ h0, uint64_t n,
-                                                     uint32_t *__restrict__ count) {
-    __shared__ uint32_t hist[256];
-    hist[threadIdx.x] = 0;
-    __syncthreads();
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
-        atomicAdd(&hist[h0[i] & 0xff], 1u);
-    __syncthreads();
-    if (hist[threadIdx.x]) atomicAdd(&count[threadIdx.x], hist[threadIdx.x]);
-}
-
 // one block of 256 threads: exclusive scan of the 256 bucket counts and the
 // work-unit table (bucket, start, count) with units of `per_unit` seeds.
 __global__ __launch_bounds__(256) void k_bucket_scan(const uint32_t *__restrict__ count,
@@ -86,24 +77,33 @@ __global__ __launch_bounds__(256) void k_bucket_scan(const uint32_t *__restrict_
                                                      uint32_t *__restrict__ n_units) {
     __shared__ uint32_t off[257];
     __shared__ uint32_t uoff[257];
+    __shared__ uint2 wsum[4];
     const uint32_t t = threadIdx.x;
-    if (t == 0) {
-        uint32_t acc = 0, uacc = 0;
-        for (int i = 0; i < 256; ++i) {
-            off[i] = acc;
-            uoff[i] = uacc;
-            acc += count[i];
-            uacc += (count[i] + per_unit - 1) / per_unit;
-        }
-        off[256] = acc;
-        uoff[256] = uacc;
-        *n_units = uacc;
+    const uint32_t lane = t & 63, w = t >> 6;
+    const uint32_t c0 = count[t * BUCKET_STRIDE];
+    const uint32_t u0 = (c0 + per_unit - 1) / per_unit;
+    // inclusive wave scan of (count, units), then the 4 wave totals
+    uint32_t a = c0, b = u0;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t pa = __shfl_up(a, d, 64), pb = __shfl_up(b, d, 64);
+        if (lane >= d) a += pa, b += pb;
+    }
+    if (lane == 63) wsum[w] = make_uint2(a, b);
+    __syncthreads();
+    uint32_t ba = 0, bb = 0;
+    for (uint32_t i = 0; i < w; ++i) ba += wsum[i].x, bb += wsum[i].y;
+    off[t] = ba + a - c0;
+    uoff[t] = bb + b - u0;
+    if (t == 255) {
+        off[256] = ba + a;
+        uoff[256] = bb + b;
+        *n_units = bb + b;
     }
     __syncthreads();
     offset[t] = off[t];
     if (t == 0) offset[256] = off[256];
-    cursor[t] = 0;
-    const uint32_t c = count[t];
+    cursor[t * BUCKET_STRIDE] = 0;
+    const uint32_t c = c0;
     uint32_t u = uoff[t];
     for (uint32_t s = 0; s < c; s += per_unit, ++u)
         units[u] = make_uint4(t, off[t] + s, min(per_unit, c - s), 0);
@@ -113,8 +113,24 @@ __global__ __launch_bounds__(256) void k_bucket_scan(const uint32_t *__restrict_
 // (block, bucket) pair and one global atomic per non-empty pair reserves the
 // range, so the 256 global cursors see <= 256 atomics per block instead of one
 // per seed. Order inside a bucket is irrelevant: results go to the original index.
-constexpr uint32_t SCATTER_PER_THREAD = 16;
+static uint32_t env_pow2(const char *name, uint32_t dflt, uint32_t lo, uint32_t hi) {
+    const char *e = getenv(name);
+    const uint32_t v = e ? (uint32_t)atoi(e) : dflt;
+    return (v >= lo && v <= hi && (v & (v - 1)) == 0) ? v : dflt;
+}
 
+uint32_t prefix_per_thread() {
+    static const uint32_t v = env_pow2("NMZ_PREFIX_PT", 8, 1, 64);
+    return v;
+}
+
+uint32_t scatter_per_thread() {
+    static const uint32_t v = env_pow2("NMZ_SCATTER_PT", 16, 4, 16);
+    return v;
+}
+
+
+template <uint32_t SCATTER_PER_THREAD>
 __global__ __launch_bounds__(256) void k_bucket_scatter(const uint64_t *__restrict__ h0, uint64_t n,
                                                         const uint32_t *__restrict__ offset,
                                                         uint32_t *__restrict__ cursor,
@@ -134,7 +150,7 @@ __global__ __launch_bounds__(256) void k_bucket_scatter(const uint64_t *__restri
         rk[r] = i < n ? atomicAdd(&cnt[hv[r] & 0xff], 1u) : 0u;
     }
     __syncthreads();
-    if (cnt[t]) base[t] = offset[t] + atomicAdd(&cursor[t], cnt[t]);
+    if (cnt[t]) base[t] = offset[t] + atomicAdd(&cursor[t * BUCKET_STRIDE], cnt[t]);
     __syncthreads();
 #pragma unroll
     for (uint32_t r = 0; r < SCATTER_PER_THREAD; ++r) {
@@ -147,19 +163,16 @@ __global__ __launch_bounds__(256) void k_bucket_scatter(const uint64_t *__restri
     }
 }
 
-int bucket_seeds(hipStream_t st, const uint64_t *d_h0, uint64_t n_seeds, uint32_t per_unit,
-                 uint64_t max_units, Buckets &b) {
-    (void)max_units;
-    NMZ_HIP(hipMemsetAsync(b.count, 0, 256 * sizeof(uint32_t), st));
-    if (n_seeds) {
-        unsigned grid = ceil_div(n_seeds, 256 * 16);
-        hipLaunchKernelGGL(k_bucket_hist, dim3(grid), dim3(256), 0, st, d_h0, n_seeds, b.count);
-    }
+int bucket_seeds_counted(hipStream_t st, const uint64_t *d_h0, uint64_t n_seeds, uint32_t per_unit, Buckets &b) {
     hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(256), 0, st, b.count, b.offset, b.cursor, per_unit,
                        b.units, b.n_units);
     if (n_seeds)
-        hipLaunchKernelGGL(k_bucket_scatter, dim3(ceil_div(n_seeds, 256 * SCATTER_PER_THREAD)), dim3(256), 0, st,
-                           d_h0, n_seeds, b.offset, b.cursor, b.sorted_h0, b.sorted_idx);
+    {
+        const uint32_t pt = scatter_per_thread();
+        auto kern = pt == 4 ? k_bucket_scatter<4> : pt == 8 ? k_bucket_scatter<8> : k_bucket_scatter<16>;
+        hipLaunchKernelGGL(kern, dim3(ceil_div(n_seeds, 256 * pt)), dim3(256), 0, st, d_h0, n_seeds, b.offset,
+                           b.cursor, b.sorted_h0, b.sorted_idx);
+    }
     NMZ_HIP(hipGetLastError());
     return NMZ_OK;
 }

@@ -150,9 +150,23 @@ __device__ __forceinline__ uint64_t seed_prefix(uint64_t seed) {
     return h;
 }
 
-__global__ __launch_bounds__(256) void k_random_prefix(uint64_t seed0, uint64_t n, uint64_t *__restrict__ h0) {
-    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < n) h0[i] = seed_prefix(seed0 + i);
+__global__ __launch_bounds__(256) void k_random_prefix(uint64_t seed0, uint64_t n, uint64_t *__restrict__ h0,
+                                                       uint32_t *__restrict__ count, uint32_t ppt) {
+    // fused bucket histogram (low byte of h0), as in k_seed_prefix
+    __shared__ uint32_t hist[256];
+    hist[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t b0 = (uint64_t)blockIdx.x * 256 * ppt;
+    for (uint32_t r = 0; r < ppt; ++r) {
+        const uint64_t i = b0 + (uint64_t)r * 256 + threadIdx.x;
+        if (i < n) {
+            const uint64_t h = seed_prefix(seed0 + i);
+            h0[i] = h;
+            atomicAdd(&hist[h & 0xff], 1u);
+        }
+    }
+    __syncthreads();
+    if (hist[threadIdx.x]) atomicAdd(&count[threadIdx.x * BUCKET_STRIDE], hist[threadIdx.x]);
 }
 
 __global__ __launch_bounds__(256) void k_random_sweep(const uint4 *__restrict__ units,
@@ -260,7 +274,7 @@ static int make_kparams(const nmz_random_params *p, RandomKParams &kp) {
 }
 
 static size_t random_seed_scratch_bytes(uint64_t S) {
-    return Carve::bytes_for(S, 8) * 2 + Carve::bytes_for(S, 4) + Carve::bytes_for(1024, 4) +
+    return Carve::bytes_for(S, 8) * 2 + Carve::bytes_for(S, 4) + Carve::bytes_for(BUCKET_SMALL_U32, 4) +
            Carve::bytes_for(S / 64 + 257, 16);
 }
 
@@ -270,11 +284,7 @@ static Buckets carve_random(void *p, uint64_t S, uint64_t **h0) {
     Buckets b;
     b.sorted_h0 = cv.take<uint64_t>(S);
     b.sorted_idx = cv.take<uint32_t>(S);
-    uint32_t *small = cv.take<uint32_t>(1024);
-    b.count = small;
-    b.offset = small + 256;
-    b.cursor = small + 256 + 260;
-    b.n_units = small + 256 + 260 + 256;
+    buckets_small(cv.take<uint32_t>(BUCKET_SMALL_U32), b);
     b.units = cv.take<uint4>(S / 64 + 257);
     return b;
 }
@@ -326,9 +336,11 @@ static int random_run(nmz_random_plan *p, hipStream_t st, uint64_t seed0, uint64
     const uint32_t E = p->n_events;
     uint64_t *d_h0;
     Buckets b = carve_random(p->seed_scratch.ptr, p->max_seeds, &d_h0);
-    hipLaunchKernelGGL(k_random_prefix, dim3(ceil_div(S, 256)), dim3(256), 0, st, seed0, S, d_h0);
+    NMZ_HIP(hipMemsetAsync(b.count, 0, 256 * BUCKET_STRIDE * sizeof(uint32_t), st));
+    hipLaunchKernelGGL(k_random_prefix, dim3(ceil_div(S, 256 * prefix_per_thread())), dim3(256), 0, st, seed0, S, d_h0,
+                       b.count, prefix_per_thread());
     const uint64_t max_units = S / 64 + 256;
-    NMZ_TRY(bucket_seeds(st, d_h0, S, 64, max_units, b));
+    NMZ_TRY(bucket_seeds_counted(st, d_h0, S, 64, b));
     KernelTimer kt(p->ctx, st, "random_sweep");
     hipLaunchKernelGGL(k_random_sweep, dim3(ceil_div(max_units, 4)), dim3(256), 0, st, b.units, b.n_units,
                        b.sorted_h0, b.sorted_idx, p->d_table, E, p->kp, d_stats);

@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <numeric>
+#include <string>
 #include <vector>
 
 #include "nmz_common.h"
@@ -58,6 +59,17 @@ struct nmz_replayable_plan {
 namespace nmz {
 
 constexpr uint32_t REPLAY_SEEDS_PER_UNIT_MIN = 64 * 2;
+
+// argmax key mode: f64 bits + v_max_f64 (default) or a u64 compare chain (NMZ_REPLAY_KEY=u64).
+// Measured on configs[1]: 0.83 ms vs 0.96 ms per launch. (A strict-greater update on t with a
+// tie flag -- 11 full-rate VOP2 per decision, no v_subb / v_max -- measured 0.98 ms.)
+static int replay_key_mode() {
+    static int k = [] {
+        const char *e = getenv("NMZ_REPLAY_KEY");
+        return (e && std::string(e) == "u64") ? 0 : 1;
+    }();
+    return k;
+}
 
 // seeds per lane (default 2, the fastest measured; NMZ_REPLAY_U=2|4|8 for tuning)
 static int replay_u() {
@@ -131,12 +143,32 @@ __global__ __launch_bounds__(256) void k_replayable_table_sort(const uint4 *__re
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_seed_prefix(const uint32_t *__restrict__ soff,
                                                      const uint8_t *__restrict__ sbytes, uint64_t n,
-                                                     uint64_t *__restrict__ h0) {
-    uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (s >= n) return;
-    uint64_t h = FNV_OFFSET;
-    for (uint32_t i = soff[s], end = soff[s + 1]; i < end; ++i) h = fnv_step(h, sbytes[i]);
-    h0[s] = h;
+                                                     uint64_t *__restrict__ h0, uint32_t *__restrict__ count,
+                                                     uint32_t ppt) {
+    // fused bucket histogram (low byte of h0): LDS counts, one global atomic per (block, bucket)
+    __shared__ uint32_t hist[256];
+    hist[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t b0 = (uint64_t)blockIdx.x * 256 * ppt;
+    for (uint32_t r = 0; r < ppt; ++r) {
+        const uint64_t s = b0 + (uint64_t)r * 256 + threadIdx.x;
+        if (s < n) {
+            uint64_t h = FNV_OFFSET;
+            uint32_t i = soff[s];
+            const uint32_t end = soff[s + 1];
+            // bytes up to a 4-byte boundary, then whole dwords, then the tail
+            for (; i < end && (reinterpret_cast<uintptr_t>(sbytes + i) & 3); ++i) h = fnv_step(h, sbytes[i]);
+            for (; i + 4 <= end; i += 4) {
+                const uint32_t w = *reinterpret_cast<const uint32_t *>(sbytes + i);
+                h = fnv_step(fnv_step(fnv_step(fnv_step(h, w & 0xff), (w >> 8) & 0xff), (w >> 16) & 0xff), w >> 24);
+            }
+            for (; i < end; ++i) h = fnv_step(h, sbytes[i]);
+            h0[s] = h;
+            atomicAdd(&hist[h & 0xff], 1u);
+        }
+    }
+    __syncthreads();
+    if (hist[threadIdx.x]) atomicAdd(&count[threadIdx.x * BUCKET_STRIDE], hist[threadIdx.x]);
 }
 
 // ---------------------------------------------------------------------------
@@ -183,6 +215,30 @@ __device__ __forceinline__ void decide_pos(uint32_t Tt, uint32_t d, uint32_t Hm,
         : "vcc");
 }
 
+// The same decision with the argmax key kept as the bit pattern of an f64:
+// (t << 32 | ~e) with t < 2^30 is a non-negative finite double (bit 63 = 0,
+// exponent < 0x7ff; f64 denormals are preserved, the kernel default), whose
+// order equals the u64 order, so the 4-instruction u64 compare/select
+// becomes one v_max_f64.
+__device__ __forceinline__ void decide_f64(uint32_t Tt, uint32_t d, uint32_t Hm, uint32_t Hm2, uint2 q, uint32_t mv,
+                                           double &kmax, uint32_t &part) {
+    // q = {~e, C mod m}, this seed's own copy from LDS; t replaces C mod m in
+    // place, so {~e, t} is already the key's register pair (no v_mov)
+    uint32_t t0, tmp, cv;
+    uint32_t x = q.y;
+    asm("v_sub_co_u32 %[t0], vcc, %[Tt], %[d]\n\t"
+        "v_cndmask_b32 %[tmp], %[Hm2], %[Hm], vcc\n\t"
+        "v_add_u32 %[x], %[x], %[tmp]\n\t"
+        "v_sub_co_u32 %[cv], vcc, %[x], %[mv]\n\t"
+        "v_cndmask_b32 %[x], %[cv], %[x], vcc\n\t"
+        "v_add_u32 %[part], %[part], %[x]"
+        : [t0] "=&v"(t0), [tmp] "=&v"(tmp), [cv] "=&v"(cv), [x] "+v"(x), [part] "+v"(part)
+        : [Tt] "v"(Tt), [d] "v"(d), [Hm] "v"(Hm), [Hm2] "v"(Hm2), [mv] "v"(mv)
+        : "vcc");
+    const double key = __builtin_bit_cast(double, ((uint64_t)x << 32) | q.x);
+    asm("v_max_f64 %0, %0, %1" : "+v"(kmax) : "v"(key));
+}
+
 // number of entries in the C-sorted range row[lo, lo+n) with C <= x
 __device__ __forceinline__ uint32_t count_le(const uint4 *__restrict__ row, uint32_t lo, uint32_t n, uint64_t x) {
     uint32_t k = 0;
@@ -202,17 +258,20 @@ constexpr uint32_t POS_BIAS = 0x40000000u;  // keeps d = BIAS + k - i positive
 // global atomic per item) to a persistent grid, so the last round is never a
 // half-empty second pass; each item writes its partial (sum, key) per seed
 // and k_replayable_merge combines the chunks.
-template <int U>
+template <int U, int KM>  // KM: 0 = u64 compare chain, 1 = f64 max
 __global__ __launch_bounds__(256) void k_replayable_sweep_fast(
     const uint4 *__restrict__ units, const uint32_t *__restrict__ n_units,
     const uint64_t *__restrict__ sorted_h0, const uint4 *__restrict__ table, uint32_t E,
     const ClassInfo *__restrict__ classes, uint32_t n_classes, uint64_t m, uint32_t m_k64, uint32_t ec,
     uint32_t n_chunks, uint32_t fold_mask, uint32_t *__restrict__ item_counter, uint4 *__restrict__ partial,
     uint64_t part_stride) {
-    // per-wave double-buffered staging of 64 table entries (1 KiB) in LDS:
-    // one coalesced 16-B load per lane fetches the next chunk while the
-    // current one is consumed through broadcast LDS reads.
-    __shared__ uint4 stage[4][2][64];
+    // per-wave double-buffered staging of 64 table entries in LDS: one
+    // coalesced 16-B load per lane fetches the next chunk while the current
+    // one is consumed through broadcast LDS reads. An event's slot holds
+    // {~e, C mod m} x U: every seed r reads its own pair, and the decision
+    // overwrites C mod m with t, leaving the f64 key pair {~e, t} in place.
+    constexpr int STR = 2 * U;
+    __shared__ uint32_t stage[4][2][64 * STR];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t m32 = (uint32_t)m;
@@ -236,6 +295,7 @@ __global__ __launch_bounds__(256) void k_replayable_sweep_fast(
 
         uint64_t h0[U];
         uint32_t sum_lo[U], sum_hi[U], klo[U], khi[U];  // key = max of (t << 32 | ~e); 0 = none
+        double kf[U];                                   // the same key as f64 bits (KM 1)
 #pragma unroll
         for (int r = 0; r < U; ++r) {
             const uint32_t j = lane + 64 * r;
@@ -244,6 +304,7 @@ __global__ __launch_bounds__(256) void k_replayable_sweep_fast(
             sum_hi[r] = 0;
             klo[r] = 0;
             khi[r] = 0;
+            kf[r] = 0.0;
         }
         const uint4 *__restrict__ row = table + (uint64_t)L * E;
 
@@ -270,7 +331,14 @@ __global__ __launch_bounds__(256) void k_replayable_sweep_fast(
                 fresh = false;
             }
             const uint32_t n = min(64u, hi_c - pos);
-            stage[wv][slot][lane] = pre;
+            {
+                uint32_t *sw = &stage[wv][slot][lane * STR];
+#pragma unroll
+                for (int r = 0; r < U; ++r) {
+                    sw[2 * r] = pre.w;
+                    sw[2 * r + 1] = pre.z;
+                }
+            }
             // prefetch the next staged chunk (possibly in the next class)
             uint32_t npos = pos + n, nhi = hi_c;
             ClassInfo nci = ci;
@@ -284,22 +352,27 @@ __global__ __launch_bounds__(256) void k_replayable_sweep_fast(
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint4 *__restrict__ sq = stage[wv][slot];
+            const uint32_t *__restrict__ sq = stage[wv][slot];
             const uint32_t n4 = n & ~3u;
             // part[r] holds up to 4 << fold_shift delays (< 2^32 since t < m) between folds
             uint32_t part[U];
 #pragma unroll
             for (int r = 0; r < U; ++r) part[r] = 0;
             for (uint32_t i = 0, g = 1; i < n4; i += 4, ++g) {
-                uint2 qq[4];
-#pragma unroll
-                for (int t = 0; t < 4; ++t) qq[t] = make_uint2(sq[i + t].z, sq[i + t].w);
 #pragma unroll
                 for (int r = 0; r < U; ++r) {
-                    decide_pos(T0, d[r], Hm[r], Hm2[r], qq[0].x, qq[0].y, mv, klo[r], khi[r], part[r]);
-                    decide_pos(T1, d[r], Hm[r], Hm2[r], qq[1].x, qq[1].y, mv, klo[r], khi[r], part[r]);
-                    decide_pos(T2, d[r], Hm[r], Hm2[r], qq[2].x, qq[2].y, mv, klo[r], khi[r], part[r]);
-                    decide_pos(T3, d[r], Hm[r], Hm2[r], qq[3].x, qq[3].y, mv, klo[r], khi[r], part[r]);
+                    const uint2 *__restrict__ qr = reinterpret_cast<const uint2 *>(sq + i * STR + 2 * r);
+                    if constexpr (KM == 1) {
+                        decide_f64(T0, d[r], Hm[r], Hm2[r], qr[0], mv, kf[r], part[r]);
+                        decide_f64(T1, d[r], Hm[r], Hm2[r], qr[U], mv, kf[r], part[r]);
+                        decide_f64(T2, d[r], Hm[r], Hm2[r], qr[2 * U], mv, kf[r], part[r]);
+                        decide_f64(T3, d[r], Hm[r], Hm2[r], qr[3 * U], mv, kf[r], part[r]);
+                    } else {
+                        decide_pos(T0, d[r], Hm[r], Hm2[r], qr[0].y, qr[0].x, mv, klo[r], khi[r], part[r]);
+                        decide_pos(T1, d[r], Hm[r], Hm2[r], qr[U].y, qr[U].x, mv, klo[r], khi[r], part[r]);
+                        decide_pos(T2, d[r], Hm[r], Hm2[r], qr[2 * U].y, qr[2 * U].x, mv, klo[r], khi[r], part[r]);
+                        decide_pos(T3, d[r], Hm[r], Hm2[r], qr[3 * U].y, qr[3 * U].x, mv, klo[r], khi[r], part[r]);
+                    }
                     vsub(d[r], V4);
                 }
                 if ((g & fold_mask) == 0) {
@@ -313,10 +386,13 @@ __global__ __launch_bounds__(256) void k_replayable_sweep_fast(
                 }
             }
             for (uint32_t i = n4; i < n; ++i) {  // class / item tail (< 4 events)
-                const uint4 q1 = sq[i];
 #pragma unroll
                 for (int r = 0; r < U; ++r) {
-                    decide_pos(T0, d[r], Hm[r], Hm2[r], q1.z, q1.w, mv, klo[r], khi[r], part[r]);
+                    const uint2 q1 = *reinterpret_cast<const uint2 *>(sq + i * STR + 2 * r);
+                    if constexpr (KM == 1)
+                        decide_f64(T0, d[r], Hm[r], Hm2[r], q1, mv, kf[r], part[r]);
+                    else
+                        decide_pos(T0, d[r], Hm[r], Hm2[r], q1.y, q1.x, mv, klo[r], khi[r], part[r]);
                     vsub(d[r], V1);
                 }
             }
@@ -339,7 +415,14 @@ __global__ __launch_bounds__(256) void k_replayable_sweep_fast(
         }
         uint4 *__restrict__ out = partial + (uint64_t)chunk * part_stride + (uint64_t)unit * (64 * U);
 #pragma unroll
-        for (int r = 0; r < U; ++r) out[lane + 64 * r] = make_uint4(sum_lo[r], sum_hi[r], klo[r], khi[r]);
+        for (int r = 0; r < U; ++r) {
+            if constexpr (KM == 1) {
+                const uint64_t kb = __builtin_bit_cast(uint64_t, kf[r]);
+                klo[r] = (uint32_t)kb;
+                khi[r] = (uint32_t)(kb >> 32);
+            }
+            out[lane + 64 * r] = make_uint4(sum_lo[r], sum_hi[r], klo[r], khi[r]);
+        }
     }
 }
 
@@ -449,7 +532,7 @@ __global__ __launch_bounds__(256) void k_replayable_dump(const uint32_t *__restr
     out[idx] = m ? (int64_t)(h % m) : 0;
 }
 
-constexpr uint32_t REPLAY_EC = 1024;  // events per work item
+constexpr uint32_t REPLAY_EC = 2048;  // events per work item (2048 vs 1024: same sweep time, half the merge reads)
 
 static uint32_t replay_ec() {
     static uint32_t ec = [] {
@@ -462,7 +545,7 @@ static uint32_t replay_ec() {
 
 static size_t seed_scratch_bytes(uint64_t S) {
     uint64_t max_units = S / REPLAY_SEEDS_PER_UNIT_MIN + 257;
-    return Carve::bytes_for(S, 8) * 2 + Carve::bytes_for(S, 4) + Carve::bytes_for(1024, 4) +
+    return Carve::bytes_for(S, 8) * 2 + Carve::bytes_for(S, 4) + Carve::bytes_for(BUCKET_SMALL_U32, 4) +
            Carve::bytes_for(max_units, 16) + Carve::bytes_for(4, 4);
 }
 
@@ -484,11 +567,7 @@ static SeedScratch carve_seed_scratch(void *p, uint64_t S) {
     s.h0 = cv.take<uint64_t>(S);
     s.b.sorted_h0 = cv.take<uint64_t>(S);
     s.b.sorted_idx = cv.take<uint32_t>(S);
-    uint32_t *small = cv.take<uint32_t>(1024);
-    s.b.count = small;
-    s.b.offset = small + 256;
-    s.b.cursor = small + 256 + 260;
-    s.b.n_units = small + 256 + 260 + 256;
+    buckets_small(cv.take<uint32_t>(BUCKET_SMALL_U32), s.b);
     s.b.units = cv.take<uint4>(S / REPLAY_SEEDS_PER_UNIT_MIN + 257);
     s.counter = cv.take<uint32_t>(4);
     return s;
@@ -506,11 +585,13 @@ static int replayable_run(nmz_replayable_plan *p, hipStream_t st, const uint32_t
     }
     NMZ_CHECK(S <= p->max_seeds, "more seeds than the plan was created for");
     SeedScratch sc = carve_seed_scratch(p->seed_scratch.ptr, p->max_seeds);
-    hipLaunchKernelGGL(k_seed_prefix, dim3(ceil_div(S, 256)), dim3(256), 0, st, d_soff, d_sbytes, S, sc.h0);
+    NMZ_HIP(hipMemsetAsync(sc.b.count, 0, 256 * BUCKET_STRIDE * sizeof(uint32_t), st));
+    hipLaunchKernelGGL(k_seed_prefix, dim3(ceil_div(S, 256 * prefix_per_thread())), dim3(256), 0, st, d_soff, d_sbytes,
+                       S, sc.h0, sc.b.count, prefix_per_thread());
     const int U = replay_u();
     const uint32_t per_unit = 64u * (uint32_t)U;
     const uint64_t max_units = S / per_unit + 256;
-    NMZ_TRY(bucket_seeds(st, sc.h0, S, p->mod.kind == MOD_FAST ? per_unit : 64, max_units, sc.b));
+    NMZ_TRY(bucket_seeds_counted(st, sc.h0, S, p->mod.kind == MOD_FAST ? per_unit : 64, sc.b));
     if (p->mod.kind == MOD_FAST) {
         const uint32_t ec = replay_ec();
         const uint32_t n_chunks = (E + ec - 1) / ec;
@@ -525,7 +606,7 @@ static int replayable_run(nmz_replayable_plan *p, hipStream_t st, const uint32_t
         {
             KernelTimer kt(p->ctx, st, "replayable_sweep");
 #define NMZ_K1(UU)                                                                                                   \
-    hipLaunchKernelGGL(k_replayable_sweep_fast<UU>, dim3(grid), dim3(256), 0, st, sc.b.units, sc.b.n_units,          \
+    hipLaunchKernelGGL((replay_key_mode() == 1 ? k_replayable_sweep_fast<UU, 1> : k_replayable_sweep_fast<UU, 0>), dim3(grid), dim3(256), 0, st, sc.b.units, sc.b.n_units,          \
                        sc.b.sorted_h0, p->d_table, E, p->d_classes, p->n_classes, p->mod.m, p->mod.m_k64, ec,        \
                        n_chunks, fold_mask, sc.counter, p->partial.as<uint4>(), stride)
             if (U == 2) NMZ_K1(2); else if (U == 8) NMZ_K1(8); else NMZ_K1(4);

@@ -1,19 +1,40 @@
 // Failure-schedule candidate selection: top-k seeds by
 // (n_fault desc, sum_delay desc (int64), seed asc).
-// Multi-level selection: each 256-thread block reduces a 2048-entry chunk to
-// its best k (threshold filter + bitonic sort of the survivors in LDS); levels
-// repeat until one chunk remains.
+//
+// Two kernels, no full sorts:
+//  1. k_topk_chunk: a 256-thread block reduces a 2048-entry chunk of the
+//     stats to its best k, sorted. A 64-bit coarse key (monotone in the
+//     order, not strict) gives a threshold tau = the k-th largest per-thread
+//     maximum: at least k entries reach it, and every member of the chunk's
+//     top-k does. The survivors (typically ~k) are ranked exactly by counting
+//     and written to their slot.
+//  2. k_topk_merge: a block merges up to 32 sorted lists into one sorted list
+//     of k by a tree of bitonic merges in LDS (elementwise best of A[i] and
+//     B[kp-1-i] is a bitonic sequence holding the top kp of both; log2(kp)
+//     half-cleaner stages sort it). Levels repeat until one list remains.
 #include "nmz_common.h"
 #include "nmz_internal.h"
 
 namespace nmz {
 
 constexpr uint32_t TOPK_CHUNK = 2048;
+constexpr uint32_t TOPK_THREADS = 256;
+constexpr uint32_t TOPK_PER_THREAD = TOPK_CHUNK / TOPK_THREADS;
+constexpr uint32_t TOPK_RANK_MAX = 512;   // survivors ranked by counting; more -> bitonic sort
+constexpr uint32_t TOPK_MERGE_SLOTS = 4096;  // LDS entries per merge block (96 KiB)
 
 __device__ inline bool topk_better(const nmz_topk_entry &a, const nmz_topk_entry &b) {
     if (a.n_fault != b.n_fault) return a.n_fault > b.n_fault;
     if (a.sum_delay_ns != b.sum_delay_ns) return a.sum_delay_ns > b.sum_delay_ns;
     return a.seed < b.seed;
+}
+
+// strict total order: topk_better, then chunk position (equal entries: sentinels)
+__device__ inline bool topk_before(const nmz_topk_entry &a, uint32_t ia, const nmz_topk_entry &b, uint32_t ib) {
+    if (a.n_fault != b.n_fault) return a.n_fault > b.n_fault;
+    if (a.sum_delay_ns != b.sum_delay_ns) return a.sum_delay_ns > b.sum_delay_ns;
+    if (a.seed != b.seed) return a.seed < b.seed;
+    return ia < ib;
 }
 
 __device__ inline nmz_topk_entry topk_sentinel() {
@@ -23,6 +44,15 @@ __device__ inline nmz_topk_entry topk_sentinel() {
     e.n_fault = 0;
     e.first_fault = NMZ_NONE;
     return e;
+}
+
+// Coarse key: a better than b => coarse(a) >= coarse(b). n_fault in the top 16
+// bits (saturated: every entry with >= 0xffff faults maps to the maximum key),
+// then the top 48 bits of the order-preserving (sign-flipped) sum.
+__device__ inline uint64_t topk_coarse(const nmz_topk_entry &x) {
+    if (x.n_fault >= 0xffffu) return UINT64_MAX;
+    const uint64_t bs = (uint64_t)x.sum_delay_ns ^ (1ull << 63);
+    return ((uint64_t)x.n_fault << 48) | (bs >> 16);
 }
 
 // bitonic sort (best first) of the first `n` entries of s (n a power of two)
@@ -46,58 +76,123 @@ __device__ void bitonic_sort_n(nmz_topk_entry *s, uint32_t n) {
     __syncthreads();
 }
 
-constexpr uint32_t TOPK_THREADS = 256;
-constexpr uint32_t TOPK_PER_THREAD = TOPK_CHUNK / TOPK_THREADS;
-
-// Chunk top-k by threshold filtering. Each thread's best entry is a "winner";
-// the k-th best winner T is a lower bound of the chunk's k-th best entry (k
-// distinct entries are >= T), so only entries >= T can be in the chunk's
-// top-k. The survivors (typically ~k) are compacted in LDS and sorted.
-template <bool FROM_STATS>
-__global__ __launch_bounds__(TOPK_THREADS) void k_topk_chunk(const void *__restrict__ src, uint64_t n,
+__global__ __launch_bounds__(TOPK_THREADS) void k_topk_chunk(const nmz_sched_stats *__restrict__ stats, uint64_t n,
                                                               uint64_t seed0, uint32_t k,
                                                               nmz_topk_entry *__restrict__ out) {
     __shared__ nmz_topk_entry cand[TOPK_CHUNK];
-    __shared__ nmz_topk_entry win[TOPK_THREADS];
+    __shared__ uint32_t cidx[TOPK_CHUNK];
+    __shared__ uint64_t wkey[TOPK_THREADS];
+    __shared__ uint64_t tau_s;
     __shared__ uint32_t ncand;
     const uint32_t t = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * TOPK_CHUNK;
     nmz_topk_entry e[TOPK_PER_THREAD];
-    nmz_topk_entry best = topk_sentinel();
+    uint64_t ck[TOPK_PER_THREAD];
+    uint64_t wk = 0;
 #pragma unroll
     for (uint32_t r = 0; r < TOPK_PER_THREAD; ++r) {
         const uint64_t i = base + (uint64_t)r * TOPK_THREADS + t;
         nmz_topk_entry x = topk_sentinel();
         if (i < n) {
-            if (FROM_STATS) {
-                const nmz_sched_stats st = static_cast<const nmz_sched_stats *>(src)[i];
-                x.seed = seed0 + i;
-                x.sum_delay_ns = (int64_t)st.sum_delay_ns;
-                x.n_fault = st.n_fault;
-                x.first_fault = st.first_fault;
-            } else {
-                x = static_cast<const nmz_topk_entry *>(src)[i];
-            }
+            const nmz_sched_stats st = stats[i];
+            x.seed = seed0 + i;
+            x.sum_delay_ns = (int64_t)st.sum_delay_ns;
+            x.n_fault = st.n_fault;
+            x.first_fault = st.first_fault;
         }
         e[r] = x;
-        if (topk_better(x, best)) best = x;
+        ck[r] = topk_coarse(x);
+        wk = ck[r] > wk ? ck[r] : wk;
     }
-    win[t] = best;
+    wkey[t] = wk;
     if (t == 0) ncand = 0;
-    bitonic_sort_n(win, TOPK_THREADS);
-    const nmz_topk_entry T = win[k - 1];
+    __syncthreads();
+    // tau = k-th largest per-thread maximum (with multiplicity)
+    uint32_t gt = 0, ge = 0;
+#pragma unroll 8
+    for (uint32_t j = 0; j < TOPK_THREADS; ++j) {
+        const uint64_t w = wkey[j];
+        gt += w > wk ? 1u : 0u;
+        ge += w >= wk ? 1u : 0u;
+    }
+    if (gt < k && k <= ge) tau_s = wk;  // every writer writes the same value
+    __syncthreads();
+    const uint64_t tau = tau_s;
 #pragma unroll
     for (uint32_t r = 0; r < TOPK_PER_THREAD; ++r) {
-        if (!topk_better(T, e[r])) cand[atomicAdd(&ncand, 1u)] = e[r];  // e >= T
+        if (ck[r] >= tau) {
+            const uint32_t c = atomicAdd(&ncand, 1u);
+            cand[c] = e[r];
+            cidx[c] = r * TOPK_THREADS + t;
+        }
     }
     __syncthreads();
-    const uint32_t c = ncand;
+    const uint32_t c = ncand;  // >= k
+    nmz_topk_entry *__restrict__ o = out + (uint64_t)blockIdx.x * k;
+    if (c <= TOPK_RANK_MAX) {
+        for (uint32_t i = t; i < c; i += TOPK_THREADS) {
+            const nmz_topk_entry x = cand[i];
+            const uint32_t xi = cidx[i];
+            uint32_t rk = 0;
+            for (uint32_t j = 0; j < c; ++j) rk += topk_before(cand[j], cidx[j], x, xi) ? 1u : 0u;
+            if (rk < k) o[rk] = x;
+        }
+        return;
+    }
     uint32_t np = 2;
     while (np < c) np <<= 1;
     for (uint32_t i = c + t; i < np; i += TOPK_THREADS) cand[i] = topk_sentinel();
     bitonic_sort_n(cand, np);
-    for (uint32_t i = t; i < k; i += TOPK_THREADS)
-        out[(uint64_t)blockIdx.x * k + i] = i < c ? cand[i] : topk_sentinel();
+    for (uint32_t i = t; i < k; i += TOPK_THREADS) o[i] = cand[i];
+}
+
+// Merge `lpb` consecutive sorted lists of k entries (kp = next pow2 >= k,
+// lpb * kp <= TOPK_MERGE_SLOTS) into one sorted list of k. Lists past n_lists
+// are sentinels.
+__global__ __launch_bounds__(TOPK_THREADS) void k_topk_merge(const nmz_topk_entry *__restrict__ in,
+                                                              uint32_t n_lists, uint32_t k, uint32_t lkp,
+                                                              uint32_t lpb, nmz_topk_entry *__restrict__ out) {
+    // kp = 2^lkp: index math by shifts and masks (runtime divisions cost ~40 VALU each)
+    const uint32_t kp = 1u << lkp, kmask = kp - 1, lh = lkp ? lkp - 1 : 0, hmask = (kp >> 1) - 1;
+    __shared__ nmz_topk_entry s[TOPK_MERGE_SLOTS];
+    const uint32_t t = threadIdx.x;
+    const uint32_t l0 = blockIdx.x * lpb;
+    for (uint32_t i = t; i < lpb * kp; i += TOPK_THREADS) {
+        const uint32_t l = l0 + (i >> lkp), j = i & kmask;
+        s[i] = (l < n_lists && j < k) ? in[(uint64_t)l * k + j] : topk_sentinel();
+    }
+    for (uint32_t w = 1; w < lpb; w <<= 1) {  // merge list pairs (a, a + w), a % 2w == 0
+        const uint32_t pairs = lpb / (2 * w);
+        __syncthreads();
+        for (uint32_t i = t; i < pairs * kp; i += TOPK_THREADS) {
+            const uint32_t a = (i >> lkp) * 2 * w, j = i & kmask;
+            nmz_topk_entry &x = s[a * kp + j];
+            const nmz_topk_entry y = s[(a + w) * kp + (kp - 1 - j)];
+            if (topk_better(y, x)) x = y;
+        }
+        for (uint32_t stride = kp >> 1; stride > 0; stride >>= 1) {
+            __syncthreads();
+            for (uint32_t i = t; i < pairs * (kp >> 1); i += TOPK_THREADS) {
+                const uint32_t a = (i >> lh) * 2 * w, q = i & hmask;
+                const uint32_t p = 2 * q - (q & (stride - 1));
+                nmz_topk_entry &x = s[a * kp + p];
+                nmz_topk_entry &y = s[a * kp + p + stride];
+                if (topk_better(y, x)) {
+                    const nmz_topk_entry tmp = x;
+                    x = y;
+                    y = tmp;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = t; j < k; j += TOPK_THREADS) out[(uint64_t)blockIdx.x * k + j] = s[j];
+}
+
+static uint32_t pow2_at_least(uint32_t x) {
+    uint32_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
 }
 
 uint64_t topk_scratch_entries(uint64_t n, uint32_t k) {
@@ -113,17 +208,20 @@ int topk_select(hipStream_t st, const nmz_sched_stats *d_stats, uint64_t n, uint
                 nmz_topk_entry *d_scratch, nmz_topk_entry *d_out) {
     if (k == 0) return NMZ_OK;
     NMZ_CHECK(k <= TOPK_THREADS, "top-k supports k <= 256");
-    uint64_t blocks = (n + TOPK_CHUNK - 1) / TOPK_CHUNK;
-    if (blocks == 0) blocks = 1;
-    nmz_topk_entry *a = d_scratch, *b = d_scratch + blocks * k;
-    hipLaunchKernelGGL(k_topk_chunk<true>, dim3((unsigned)blocks), dim3(TOPK_THREADS), 0, st, d_stats, n, seed0, k,
-                       blocks == 1 ? d_out : a);
-    uint64_t cur = blocks * k;
-    while (blocks > 1) {
-        blocks = (cur + TOPK_CHUNK - 1) / TOPK_CHUNK;
-        hipLaunchKernelGGL(k_topk_chunk<false>, dim3((unsigned)blocks), dim3(TOPK_THREADS), 0, st, a, cur, 0, k,
-                           blocks == 1 ? d_out : b);
-        cur = blocks * k;
+    uint64_t lists = (n + TOPK_CHUNK - 1) / TOPK_CHUNK;
+    if (lists == 0) lists = 1;
+    NMZ_CHECK(lists < (1ull << 31), "too many seeds for one top-k selection");
+    nmz_topk_entry *a = d_scratch, *b = d_scratch + lists * k;
+    hipLaunchKernelGGL(k_topk_chunk, dim3((unsigned)lists), dim3(TOPK_THREADS), 0, st, d_stats, n, seed0, k,
+                       lists == 1 ? d_out : a);
+    const uint32_t kp = pow2_at_least(k);
+    const uint32_t lkp = (uint32_t)__builtin_ctz(kp);
+    const uint32_t lpb = std::min<uint32_t>(32, TOPK_MERGE_SLOTS / kp);
+    while (lists > 1) {
+        const uint64_t nb = (lists + lpb - 1) / lpb;
+        hipLaunchKernelGGL(k_topk_merge, dim3((unsigned)nb), dim3(TOPK_THREADS), 0, st, a, (uint32_t)lists, k, lkp,
+                           lpb, nb == 1 ? d_out : b);
+        lists = nb;
         nmz_topk_entry *tmp = a;
         a = b;
         b = tmp;

@@ -250,11 +250,14 @@ def _topk_dev(ctx, st, seed0, k):
 @pytest.mark.parametrize("n,k,mode", [
     (1, 1, "rand"), (5, 16, "rand"), (2047, 64, "rand"), (2048, 256, "rand"), (2049, 1, "rand"),
     (300_001, 64, "rand"), (300_001, 256, "rand"), (100_000, 64, "ties"), (70_000, 64, "const"),
-    (70_000, 128, "sorted"), (70_000, 64, "faults")])
+    (70_000, 128, "sorted"), (70_000, 64, "faults"), (90_001, 100, "neg"), (50_000, 37, "bigfault"),
+    (3, 100, "neg"), (200_000, 256, "sorted")])
 def test_topk_select_dev(ctx, n, k, mode):
-    """Threshold-filter top-k vs the oracle: random keys, heavy ties (every
-    entry a survivor), ascending keys (worst case for per-thread winners),
-    n_fault-dominated order, sizes around the 2048-entry chunk."""
+    """Threshold-filter top-k + list-merge tree vs the oracle: random keys,
+    heavy ties (every entry a survivor), ascending keys (worst case for
+    per-thread winners), n_fault-dominated order, negative int64 sums, fault
+    counts past the coarse key's 16-bit saturation, k not a power of two,
+    sizes around the 2048-entry chunk."""
     rng = np.random.default_rng(n * 7 + k)
     st = np.zeros(n, O.SCHED_STATS_DTYPE)
     if mode == "rand":
@@ -265,6 +268,12 @@ def test_topk_select_dev(ctx, n, k, mode):
         st["sum_delay_ns"] = 77
     elif mode == "sorted":
         st["sum_delay_ns"] = np.arange(n, dtype=np.uint64)
+    elif mode == "neg":
+        st["sum_delay_ns"] = rng.integers(-2**63, 2**63, n, dtype=np.int64).view(np.uint64)
+    elif mode == "bigfault":
+        st["n_fault"] = rng.integers(65530, 65540, n, dtype=np.uint32)
+        st["n_fault"][::97] = 2**32 - 1
+        st["sum_delay_ns"] = rng.integers(0, 2**40, n, dtype=np.uint64)
     else:
         st["n_fault"] = rng.integers(0, 3, n, dtype=np.uint32)
         st["sum_delay_ns"] = rng.integers(0, 1000, n, dtype=np.uint64)
