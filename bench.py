@@ -34,28 +34,34 @@ sys.path.insert(0, HERE)
 PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 78.6 T int32 lane-ops/s (2 cyc/wave64 instr/SIMD)
 PEAK_HBM_GBS = 8000.0
 MAX_INTERVAL_NS = 100_000_000
-# VALU wave-instructions per wave-decision (64 decisions) of k_replayable_sweep_fast:
-# rocprofv3 SQ_INSTS_VALU / (S*E/64) = 738.4M / 67.1M = 11.0 (profiles/r01c_summary.json);
-# the gfx950 ISA of the steady-state loop has 82 per 8 decisions = 10.25, the rest is
-# the per-segment binary search, staging and folds.
-REPLAY_VALU_PER_DEC = 11.0
-# k_random_sweep: SQ_INSTS_VALU 2.949e10 per launch of 2^20 seeds x 10^4 events (profiles/r01d_summary.json)
-# -> 180.0 lane-instructions per decision (SURVEY 8(d) declared model: ~170)
-RANDOM_VALU_PER_DEC = 2.949e10 * 64 / (2**20 * 10**4)
-# k_ed_bv<32> on configs[2] (100k x 2048, w=32): SQ_INSTS_VALU 1.22834e12 per launch of 4,999,950,000 pairs
-# (profiles/r01f_summary.json, lane-refill kernel) -> lane-instructions per pair; the cut-off makes it
-# input-dependent, so it is valid for this synthetic workload only
-ED_BV_VALU_PER_PAIR = 1.22834e12 * 64 / 4_999_950_000
-# k_ed_wide<4> on configs[4] (256 x 65536, w=4096): SQ_INSTS_VALU 1.218e11 per launch of 32,640 pairs
-# (profiles/r01e_summary.json) = 56.9 per wave-column (ISA: 56.6); no cut-off, etcd-style distances stay in band
-ED_WIDE_VALU_PER_PAIR = 1.21801e11 * 64 / 32640
+# VALU lane-instructions per unit (decision / trace pair) of each dominant kernel, measured by rocprofv3
+# (SQ_INSTS_VALU x 64 / units per launch) on this bench's own workloads: profiles/valu_per_unit.json,
+# written by tools/valu_per_unit.py from the latest profile summary. The ED kernels' counts depend on
+# the cut-off and so hold for these synthetic workloads only. HBM traffic = 2 x FETCH_SIZE + WRITE_SIZE
+# (MI355X_MICROARCH.md: gfx950 FETCH_SIZE counts half the bytes of wide coalesced reads).
+VALU_TABLE = os.path.join(HERE, "profiles", "valu_per_unit.json")
 
 
-def roofline_valu(kernel, ops_per_unit, units, kernel_ms, source):
-    achieved = ops_per_unit * units / (kernel_ms * 1e-3) / 1e12
+def valu_entry(kernel):
+    try:
+        return json.load(open(VALU_TABLE))[kernel]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def roofline_valu(kernel, units, kernel_ms):
+    """VALU issue roofline of `kernel`: measured lane-instructions per unit x units / kernel time."""
+    e = valu_entry(kernel)
+    if e is None:
+        return None
+    achieved = e["ops_per_unit"] * units / (kernel_ms * 1e-3) / 1e12
+    traffic = e.get("hbm_bytes_per_launch")
+    if traffic is not None and units != e["units_per_launch"]:
+        traffic = traffic * units / e["units_per_launch"]
     return {"bound": "valu", "achieved": achieved, "peak": PEAK_VALU_TOPS, "unit": "Tops/s",
-            "frac": achieved / PEAK_VALU_TOPS, "traffic": None, "kernel": kernel, "kernel_ms": kernel_ms,
-            "ops_per_unit": ops_per_unit, "units_per_launch": units, "ops_source": source}
+            "frac": achieved / PEAK_VALU_TOPS, "traffic": traffic, "traffic_unit": "bytes/launch (2 x FETCH_SIZE + WRITE_SIZE)",
+            "kernel": kernel, "kernel_ms": kernel_ms, "ops_per_unit": e["ops_per_unit"], "units_per_launch": units,
+            "ops_source": e["source"]}
 
 
 def splitmix64(state, n):
@@ -228,8 +234,7 @@ def bench_random_secondary(args, torch, D, ctx, L, stream):
                config={"workload": "configs[3] share", "seeds_per_gpu": S, "events": E, "entities": 16,
                        "prioritized": 4, "fault_probability": 0.1},
                ms_per_step=el / steps * 1e3, kernel_ms=kern_ms,
-               roofline=roofline_valu("k_random_sweep", RANDOM_VALU_PER_DEC, S * E, kern_ms,
-                                      "SQ_INSTS_VALU per launch, profiles/r01d_summary.json"))
+               roofline=roofline_valu("k_random_sweep", S * E, kern_ms))
     stats = np.frombuffer(d_stats.cpu().numpy().tobytes(), dtype=_lib.SCHED_STATS_DTYPE)
     if D.rank == 0 and args.cpu_baseline and D.world == 1:
         from oracle import oracle as O
@@ -300,8 +305,7 @@ def bench_ed_secondary(args, torch, D, ctx, L, stream, spec):
                        "band": ED_BAND, "k": k, "parallelism": f"pair-tile shards x{D.world}" +
                        (" + RCCL all_gather k-NN merge" if D.world > 1 else "")},
                kernel=kind, kernel_ms=kern_ms, plan_ms=plan_ms, synth_s=round(synth_s, 2),
-               roofline=roofline_valu(kind, spec["valu_per_pair"], (pairs + D.world - 1) // D.world, kern_ms,
-                                      spec["valu_source"]) if spec.get("valu_per_pair") else None,
+               roofline=roofline_valu(kind, (pairs + D.world - 1) // D.world, kern_ms),
                band_cells_per_s=pairs * cells_per_pair * steps / el)
     keys = d_out.cpu().numpy().view(np.uint64).reshape(N, k)
     if D.rank == 0 and args.cpu_baseline and D.world == 1:
@@ -350,9 +354,7 @@ def main():
     r = bench_replayable(args, torch, D, ctx, L, stream)
     decisions = D.world * r["S"] * r["E"] * args.steps
     value = decisions / r["elapsed"]
-    kern_s = r["kern_ms"] * 1e-3
     dec_launch = r["S"] * r["E"]
-    achieved = dec_launch * REPLAY_VALU_PER_DEC / kern_s / 1e12
     line = {
         "metric": "schedule decisions/sec + trace-pair edit distances/sec at 1/2/4/8 MI355X",
         "value": value,
@@ -369,34 +371,22 @@ def main():
         "config": {"workload": "configs[1] replayable seed sweep", "seeds_per_gpu": r["S"], "events": r["E"],
                    "max_interval_ns": MAX_INTERVAL_NS, "topk": 64,
                    "parallelism": f"seed-range x{D.world}" + (" + RCCL all_gather top-k" if D.world > 1 else "")},
-        "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_VALU_TOPS, "unit": "Tops/s",
-                     "frac": achieved / PEAK_VALU_TOPS, "traffic": None,
-                     "kernel": "k_replayable_sweep_fast", "kernel_ms": r["kern_ms"],
-                     "ops_per_unit": REPLAY_VALU_PER_DEC, "units_per_launch": dec_launch,
-                     "declared_model_ops_per_unit": None},
+        "roofline": roofline_valu("k_replayable_sweep_fast", dec_launch, r["kern_ms"]),
         "plan_ms": r["plan_ms"],
         "topk_head": [int(x) for x in r["topk"]["seed"][:4]],
     }
-    # survey 8(d) declared model: 6*len(hint)+18 ops per decision
+    # survey 8(d) declared model for the reference's byte-serial algorithm: 6*len(hint)+18 ops per decision
     hoff = r["hints"][0]
     mean_len = float(np.mean(np.diff(hoff.astype(np.int64))))
-    line["roofline"]["declared_model_ops_per_unit"] = 6 * mean_len + 18
-    prof = os.path.join(HERE, "profiles", "replayable_pmc.json")
-    if os.path.exists(prof):
-        try:
-            pm = json.load(open(prof))
-            line["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
-        except Exception:
-            pass
+    if line["roofline"]:
+        line["roofline"]["declared_model_ops_per_unit"] = 6 * mean_len + 18
     if D.rank == 0 and D.world == 1 and args.cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_replayable(r, args)
     if args.secondary:
         ed3 = dict(workload="configs[2] historystorage all-pairs search", traces=args.ed_traces, events=2048,
-                   band=32, k=8, generator="synth_traces", steps=args.ed_steps, valu_per_pair=ED_BV_VALU_PER_PAIR,
-                   valu_source="SQ_INSTS_VALU per launch, profiles/r01f_summary.json")
+                   band=32, k=8, generator="synth_traces", steps=args.ed_steps)
         ed5 = dict(workload="configs[4] long-trace stress, wide band", traces=256, events=65536, band=4096, k=8,
-                   generator="etcd_traces", steps=args.ed_steps, valu_per_pair=ED_WIDE_VALU_PER_PAIR,
-                   valu_source="SQ_INSTS_VALU per launch, profiles/r01e_summary.json")
+                   generator="etcd_traces", steps=args.ed_steps)
         line["secondary"] = [bench_random_secondary(args, torch, D, ctx, L, stream),
                              bench_ed_secondary(args, torch, D, ctx, L, stream, ed3),
                              bench_ed_secondary(args, torch, D, ctx, L, stream, ed5)]

@@ -13,4 +13,5 @@ timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES S
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- $B > $OUT/pmc_fetch.log 2>&1
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- $B > $OUT/pmc_write.log 2>&1
 python3 $R/tools/summarize_profile.py $OUT $OUT/summary.json > $OUT/summary.txt
+python3 $R/tools/valu_per_unit.py $OUT/summary.json $TAG > $OUT/valu_per_unit.txt
 echo done
