@@ -97,12 +97,20 @@ class Dist:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        if "NMZ_BENCH_DEVICE" in os.environ:
+            self.local_rank = int(os.environ["NMZ_BENCH_DEVICE"])
         self.pg = None
 
     def init(self, torch):
         if self.world > 1:
             import torch.distributed as dist
-            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local_rank))
+            # NMZ_BENCH_BACKEND=gloo + NMZ_BENCH_DEVICE=0 rehearse the N > 1 path with several ranks on one
+            # GPU (RCCL refuses two ranks per device); the driver's runs use the defaults (RCCL, rank i on GPU i)
+            backend = os.environ.get("NMZ_BENCH_BACKEND", "nccl")
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local_rank))
+            else:
+                dist.init_process_group(backend)
             self.pg = dist
 
     def barrier(self):
@@ -140,22 +148,38 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     d_sb = torch.from_numpy(sb).to(dev)
     d_stats = torch.empty(S * 32, dtype=torch.uint8, device=dev)
     K_TOP = 64
-    d_topk = torch.empty(K_TOP * 24, dtype=torch.uint8, device=dev)
-    gathered = [torch.empty_like(d_topk) for _ in range(D.world)] if D.world > 1 else None
+    # two top-k buffers: the RCCL all_gather of step i (async, on the process group's stream) overlaps
+    # the sweep of step i+1; a buffer is rewritten only after the gather that reads it has completed
+    d_topk = [torch.empty(K_TOP * 24, dtype=torch.uint8, device=dev) for _ in range(2)]
+    gathered = [[torch.empty_like(d_topk[0]) for _ in range(D.world)] for _ in range(2)] if D.world > 1 else None
+    pending = [None, None]
+    it = [0]
 
     def step():
+        b = it[0] & 1
+        it[0] += 1
+        if pending[b] is not None:
+            pending[b].wait()
+            pending[b] = None
         _lib.check(L.nmz_replayable_sweep_dev(plan, ctypes.c_void_p(d_soff.data_ptr()),
                                               ctypes.c_void_p(d_sb.data_ptr()), S,
                                               ctypes.c_void_p(d_stats.data_ptr()), stream))
         _lib.check(L.nmz_topk_select_dev(ctx.handle, ctypes.c_void_p(d_stats.data_ptr()), S, seed_lo, K_TOP,
-                                         ctypes.c_void_p(d_topk.data_ptr()), stream))
+                                         ctypes.c_void_p(d_topk[b].data_ptr()), stream))
         if D.pg:
-            D.pg.all_gather(gathered, d_topk)
-            return gathered
-        return [d_topk]
+            pending[b] = D.pg.all_gather(gathered[b], d_topk[b], async_op=True)
+            return gathered[b]
+        return [d_topk[b]]
+
+    def drain():
+        for b in range(2):
+            if pending[b] is not None:
+                pending[b].wait()
+                pending[b] = None
 
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     _lib.check(L.nmz_timing_enable(ctx.handle, 1))
     tot, cnt = ctypes.c_double(), ctypes.c_uint64()
@@ -165,6 +189,7 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         outs = step()
+    drain()
     torch.cuda.synchronize()
     D.barrier()
     el = time.perf_counter() - t0
