@@ -8,7 +8,10 @@
 //     maximum: at least k entries reach it, and every member of the chunk's
 //     top-k does. The survivors (typically ~k) are ranked exactly by counting
 //     and written to their slot.
-//  2. k_topk_merge: a block merges up to 32 sorted lists into one sorted list
+//  2. k_topk_merge_wave (k <= 64): a 1024-thread block merges 32 sorted lists,
+//     one list per wave in registers (lane l = entry l), pairwise bitonic merges
+//     with cross-lane shuffles and 4 barriers. k_topk_merge (k > 64): a block
+//     merges up to 32 sorted lists into one sorted list
 //     of k by a tree of bitonic merges in LDS (elementwise best of A[i] and
 //     B[kp-1-i] is a bitonic sequence holding the top kp of both; log2(kp)
 //     half-cleaner stages sort it). Levels repeat until one list remains.
@@ -189,6 +192,64 @@ __global__ __launch_bounds__(TOPK_THREADS) void k_topk_merge(const nmz_topk_entr
     for (uint32_t j = t; j < k; j += TOPK_THREADS) out[(uint64_t)blockIdx.x * k + j] = s[j];
 }
 
+// ---- k <= 64: list merges in registers, one list per wave (lane l holds entry l) ----
+__device__ __forceinline__ nmz_topk_entry shfl_xor_entry(const nmz_topk_entry &x, uint32_t s) {
+    nmz_topk_entry y;
+    y.seed = __shfl_xor(x.seed, s, 64);
+    y.sum_delay_ns = __shfl_xor(x.sum_delay_ns, s, 64);
+    y.n_fault = __shfl_xor(x.n_fault, s, 64);
+    y.first_fault = __shfl_xor(x.first_fault, s, 64);
+    return y;
+}
+
+// x: sorted list A (best first) over lanes 0..kp-1; yr: list B reversed (lane l holds B[kp-1-l]).
+// Elementwise best is a bitonic sequence holding the top kp of A u B; half-cleaners sort it.
+__device__ __forceinline__ void wave_merge(nmz_topk_entry &x, const nmz_topk_entry &yr, uint32_t kp, uint32_t lane) {
+    if (topk_better(yr, x)) x = yr;
+    for (uint32_t st = kp >> 1; st > 0; st >>= 1) {
+        const nmz_topk_entry p = shfl_xor_entry(x, st);
+        const bool lower = (lane & st) == 0;
+        if (lower ? topk_better(p, x) : topk_better(x, p)) x = p;
+    }
+}
+
+constexpr uint32_t TOPK_WAVE_LISTS = 32;  // lists merged per 1024-thread block
+
+// Merge up to 32 consecutive sorted lists of k (kp = pow2 >= k <= 64) into one: round 1 merges list
+// pairs straight from global memory (one pair per wave), later rounds through double-buffered LDS
+// slots; 5 rounds, 4 barriers, no LDS compare-exchange stages.
+__global__ __launch_bounds__(1024) void k_topk_merge_wave(const nmz_topk_entry *__restrict__ in, uint32_t n_lists,
+                                                          uint32_t k, uint32_t kp,
+                                                          nmz_topk_entry *__restrict__ out) {
+    __shared__ nmz_topk_entry slot[2][TOPK_WAVE_LISTS / 2][64];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t l0 = (uint64_t)blockIdx.x * TOPK_WAVE_LISTS;
+    auto load = [&](uint64_t l, uint32_t j) {
+        return (l < n_lists && j < k) ? in[l * k + j] : topk_sentinel();
+    };
+    nmz_topk_entry x = topk_sentinel();
+    // round 1: wave w merges lists 2w, 2w+1
+    {
+        const uint64_t la = l0 + 2 * w;
+        x = lane < kp ? load(la, lane) : topk_sentinel();
+        const nmz_topk_entry yr = lane < kp ? load(la + 1, kp - 1 - lane) : topk_sentinel();
+        wave_merge(x, yr, kp, lane);
+        slot[0][w][lane] = x;
+    }
+    uint32_t cur = 0;
+    for (uint32_t waves = TOPK_WAVE_LISTS / 4; waves >= 1; waves >>= 1) {
+        __syncthreads();
+        if (w < waves) {
+            x = slot[cur][2 * w][lane];
+            const nmz_topk_entry yr = lane < kp ? slot[cur][2 * w + 1][kp - 1 - lane] : topk_sentinel();
+            wave_merge(x, yr, kp, lane);
+            slot[cur ^ 1][w][lane] = x;
+        }
+        cur ^= 1;
+    }
+    if (w == 0 && lane < k) out[(uint64_t)blockIdx.x * k + lane] = x;
+}
+
 static uint32_t pow2_at_least(uint32_t x) {
     uint32_t p = 1;
     while (p < x) p <<= 1;
@@ -217,6 +278,15 @@ int topk_select(hipStream_t st, const nmz_sched_stats *d_stats, uint64_t n, uint
     const uint32_t kp = pow2_at_least(k);
     const uint32_t lkp = (uint32_t)__builtin_ctz(kp);
     const uint32_t lpb = std::min<uint32_t>(32, TOPK_MERGE_SLOTS / kp);
+    while (kp <= 64 && lists > 1) {
+        const uint64_t nb = (lists + TOPK_WAVE_LISTS - 1) / TOPK_WAVE_LISTS;
+        hipLaunchKernelGGL(k_topk_merge_wave, dim3((unsigned)nb), dim3(1024), 0, st, a, (uint32_t)lists, k, kp,
+                           nb == 1 ? d_out : b);
+        lists = nb;
+        nmz_topk_entry *tmp = a;
+        a = b;
+        b = tmp;
+    }
     while (lists > 1) {
         const uint64_t nb = (lists + lpb - 1) / lpb;
         hipLaunchKernelGGL(k_topk_merge, dim3((unsigned)nb), dim3(TOPK_THREADS), 0, st, a, (uint32_t)lists, k, lkp,
