@@ -189,9 +189,11 @@ inline void buckets_small(uint32_t *small, Buckets &b) {
     b.n_units = b.offset + 260;
 }
 
-// b.count must already hold the 256 bucket counts (filled by the caller's prefix kernel)
+// b.count must already hold the 256 bucket counts (filled by the caller's prefix kernel); the scan
+// re-zeroes them (and *zero_word, if given) for the next call, so the counters must be zeroed once
+// when the scratch is allocated
 int bucket_seeds_counted(hipStream_t st, const uint64_t *d_h0, uint64_t n_seeds, uint32_t seeds_per_unit,
-                         Buckets &b);
+                         Buckets &b, uint32_t *zero_word = nullptr);
 // seeds per thread in the prefix + histogram kernels and in the scatter (tuning: NMZ_PREFIX_PT, NMZ_SCATTER_PT)
 uint32_t prefix_per_thread();
 uint32_t scatter_per_thread();

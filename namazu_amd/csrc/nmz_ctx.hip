@@ -70,17 +70,22 @@ KernelTimer::~KernelTimer() {
 // ---------------------------------------------------------------------------
 // one block of 256 threads: exclusive scan of the 256 bucket counts and the
 // work-unit table (bucket, start, count) with units of `per_unit` seeds.
-__global__ __launch_bounds__(256) void k_bucket_scan(const uint32_t *__restrict__ count,
+__global__ __launch_bounds__(256) void k_bucket_scan(uint32_t *__restrict__ count,
                                                      uint32_t *__restrict__ offset,
                                                      uint32_t *__restrict__ cursor,
                                                      uint32_t per_unit, uint4 *__restrict__ units,
-                                                     uint32_t *__restrict__ n_units) {
+                                                     uint32_t *__restrict__ n_units,
+                                                     uint32_t *__restrict__ zero_word) {
     __shared__ uint32_t off[257];
     __shared__ uint32_t uoff[257];
     __shared__ uint2 wsum[4];
     const uint32_t t = threadIdx.x;
     const uint32_t lane = t & 63, w = t >> 6;
     const uint32_t c0 = count[t * BUCKET_STRIDE];
+    // leave the counters zeroed for the next sweep's prefix kernel (and the caller's work-item
+    // counter): no memset launches per step; plan creation zeroes them once
+    count[t * BUCKET_STRIDE] = 0;
+    if (zero_word && t == 0) *zero_word = 0;
     const uint32_t u0 = (c0 + per_unit - 1) / per_unit;
     // inclusive wave scan of (count, units), then the 4 wave totals
     uint32_t a = c0, b = u0;
@@ -163,9 +168,10 @@ __global__ __launch_bounds__(256) void k_bucket_scatter(const uint64_t *__restri
     }
 }
 
-int bucket_seeds_counted(hipStream_t st, const uint64_t *d_h0, uint64_t n_seeds, uint32_t per_unit, Buckets &b) {
+int bucket_seeds_counted(hipStream_t st, const uint64_t *d_h0, uint64_t n_seeds, uint32_t per_unit, Buckets &b,
+                         uint32_t *zero_word) {
     hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(256), 0, st, b.count, b.offset, b.cursor, per_unit,
-                       b.units, b.n_units);
+                       b.units, b.n_units, zero_word);
     if (n_seeds)
     {
         const uint32_t pt = scatter_per_thread();

@@ -313,6 +313,12 @@ static int random_plan_create(nmz_ctx *ctx, const uint64_t *evhash, const uint8_
     int rc = p->table_mem.ensure(Carve::bytes_for((size_t)256 * E + 1, 16) + Carve::bytes_for(E + 1, 8) +
                                  Carve::bytes_for(E + 1, 1));
     if (rc == NMZ_OK) rc = p->seed_scratch.ensure(random_seed_scratch_bytes(max_seeds));
+    if (rc == NMZ_OK) {  // bucket counters start at zero (k_bucket_scan re-zeroes them)
+        uint64_t *h0_unused;
+        Buckets b0 = carve_random(p->seed_scratch.ptr, max_seeds, &h0_unused);
+        if (hipMemsetAsync(b0.count, 0, 256 * BUCKET_STRIDE * sizeof(uint32_t), ctx->stream) != hipSuccess)
+            rc = fail(NMZ_EHIP, "hipMemsetAsync of the seed scratch failed");
+    }
     if (rc != NMZ_OK) return cleanup(rc);
     Carve cv(p->table_mem.ptr);
     p->d_table = cv.take<uint4>((size_t)256 * E + 1);
@@ -336,7 +342,6 @@ static int random_run(nmz_random_plan *p, hipStream_t st, uint64_t seed0, uint64
     const uint32_t E = p->n_events;
     uint64_t *d_h0;
     Buckets b = carve_random(p->seed_scratch.ptr, p->max_seeds, &d_h0);
-    NMZ_HIP(hipMemsetAsync(b.count, 0, 256 * BUCKET_STRIDE * sizeof(uint32_t), st));
     hipLaunchKernelGGL(k_random_prefix, dim3(ceil_div(S, 256 * prefix_per_thread())), dim3(256), 0, st, seed0, S, d_h0,
                        b.count, prefix_per_thread());
     const uint64_t max_units = S / 64 + 256;

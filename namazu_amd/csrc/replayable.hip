@@ -627,19 +627,17 @@ static int replayable_run(nmz_replayable_plan *p, hipStream_t st, const uint32_t
     }
     NMZ_CHECK(S <= p->max_seeds, "more seeds than the plan was created for");
     SeedScratch sc = carve_seed_scratch(p->seed_scratch.ptr, p->max_seeds);
-    NMZ_HIP(hipMemsetAsync(sc.b.count, 0, 256 * BUCKET_STRIDE * sizeof(uint32_t), st));
     hipLaunchKernelGGL(k_seed_prefix, dim3(ceil_div(S, 256 * prefix_per_thread())), dim3(256), 0, st, d_soff, d_sbytes,
                        S, sc.h0, sc.b.count, prefix_per_thread());
     const int U = replay_u();
     const uint32_t per_unit = 64u * (uint32_t)U;
     const uint64_t max_units = S / per_unit + 256;
-    NMZ_TRY(bucket_seeds_counted(st, sc.h0, S, p->mod.kind == MOD_FAST ? per_unit : 64, sc.b));
+    NMZ_TRY(bucket_seeds_counted(st, sc.h0, S, p->mod.kind == MOD_FAST ? per_unit : 64, sc.b, sc.counter));
     if (p->mod.kind == MOD_FAST) {
         const uint32_t ec = replay_ec();
         const uint32_t n_chunks = (E + ec - 1) / ec;
         NMZ_TRY(p->partial.ensure(partial_bytes(p->max_seeds, E, U, ec)));
         const uint64_t stride = (p->max_seeds / per_unit + 257) * (uint64_t)per_unit;
-        NMZ_HIP(hipMemsetAsync(sc.counter, 0, 4, st));
         // fold the u32 partial sums every 2^f groups of 4 events, (4 << f)(m - 1) + 3(m - 1) < 2^32
         uint32_t fold_mask = 0;
         while (fold_mask < 15 && ((uint64_t)(4 * (fold_mask + 1) * 2 + 3)) * (p->mod.m - 1) < (1ull << 32))
@@ -709,7 +707,15 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
     size_t need = Carve::bytes_for(cls.size() + 1, sizeof(ClassInfo)) + Carve::bytes_for((size_t)256 * E + 1, 16) +
                   Carve::bytes_for(E + 1, 4) * 2 + Carve::bytes_for(nbytes + 1, 1);
     int rc = p->plan_mem.ensure(need);
-    if (rc == NMZ_OK && E && p->mod.kind != MOD_ZERO) rc = p->seed_scratch.ensure(seed_scratch_bytes(max_seeds));
+    if (rc == NMZ_OK && E && p->mod.kind != MOD_ZERO) {
+        rc = p->seed_scratch.ensure(seed_scratch_bytes(max_seeds));
+        if (rc == NMZ_OK) {  // bucket counters and the work-item counter start at zero (k_bucket_scan re-zeroes)
+            SeedScratch sc0 = carve_seed_scratch(p->seed_scratch.ptr, max_seeds);
+            if (hipMemsetAsync(sc0.b.count, 0, 256 * BUCKET_STRIDE * sizeof(uint32_t), st) != hipSuccess ||
+                hipMemsetAsync(sc0.counter, 0, 4 * sizeof(uint32_t), st) != hipSuccess)
+                rc = fail(NMZ_EHIP, "hipMemsetAsync of the seed scratch failed");
+        }
+    }
     if (rc != NMZ_OK) {
         p->plan_mem.release();
         delete p;
