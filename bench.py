@@ -161,11 +161,11 @@ def bench_replayable(args, torch, D, ctx, L, stream):
         if pending[b] is not None:
             pending[b].wait()
             pending[b] = None
-        _lib.check(L.nmz_replayable_sweep_dev(plan, ctypes.c_void_p(d_soff.data_ptr()),
-                                              ctypes.c_void_p(d_sb.data_ptr()), S,
-                                              ctypes.c_void_p(d_stats.data_ptr()), stream))
-        _lib.check(L.nmz_topk_select_dev(ctx.handle, ctypes.c_void_p(d_stats.data_ptr()), S, seed_lo, K_TOP,
-                                         ctypes.c_void_p(d_topk[b].data_ptr()), stream))
+        # sweep + top-k in one call
+        _lib.check(L.nmz_replayable_sweep_topk_dev(plan, ctypes.c_void_p(d_soff.data_ptr()),
+                                                   ctypes.c_void_p(d_sb.data_ptr()), S, seed_lo, K_TOP,
+                                                   ctypes.c_void_p(d_stats.data_ptr()),
+                                                   ctypes.c_void_p(d_topk[b].data_ptr()), stream))
         if D.pg:
             pending[b] = D.pg.all_gather(gathered[b], d_topk[b], async_op=True)
             return gathered[b]

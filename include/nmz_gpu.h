@@ -144,6 +144,14 @@ int nmz_replayable_plan_destroy(nmz_replayable_plan *plan);
 int nmz_replayable_sweep_dev(nmz_replayable_plan *plan, const uint32_t *d_seed_off,
                              const uint8_t *d_seed_bytes, uint64_t n_seeds,
                              nmz_sched_stats *d_stats, void *stream);
+/* The same plus the top-k failure candidates (d_topk[k], k <= 256, by sum_delay desc then seed asc,
+ * .seed = seed0 + seed index), enqueued in one call. Results equal nmz_replayable_sweep_dev +
+ * nmz_topk_select_dev(seed0, k).
+ * Same reference path as nmz_replayable_sweep (replayablepolicy.go:100-114); top-k is SURVEY A7. */
+int nmz_replayable_sweep_topk_dev(nmz_replayable_plan *plan, const uint32_t *d_seed_off,
+                                  const uint8_t *d_seed_bytes, uint64_t n_seeds, uint64_t seed0,
+                                  uint32_t k, nmz_sched_stats *d_stats, nmz_topk_entry *d_topk,
+                                  void *stream);
 
 /* ---- random policy sweep ------------------------------------------------
  * Seeds are the integers seed0 .. seed0+n_seeds-1. For seed s and event e

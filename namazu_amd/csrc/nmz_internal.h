@@ -5,6 +5,8 @@
 namespace nmz {
 
 uint64_t topk_scratch_entries(uint64_t n, uint32_t k);
+int topk_merge_lists(hipStream_t st, nmz_topk_entry *a, nmz_topk_entry *b, uint64_t lists, uint32_t k,
+                     nmz_topk_entry *d_out);
 int topk_select(hipStream_t st, const nmz_sched_stats *d_stats, uint64_t n, uint64_t seed0, uint32_t k,
                 nmz_topk_entry *d_scratch, nmz_topk_entry *d_out);
 

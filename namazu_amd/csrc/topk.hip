@@ -17,84 +17,19 @@
 //     half-cleaner stages sort it). Levels repeat until one list remains.
 #include "nmz_common.h"
 #include "nmz_internal.h"
+#include "topk_dev.h"
 
 namespace nmz {
-
-constexpr uint32_t TOPK_CHUNK = 2048;
-constexpr uint32_t TOPK_THREADS = 256;
-constexpr uint32_t TOPK_PER_THREAD = TOPK_CHUNK / TOPK_THREADS;
-constexpr uint32_t TOPK_RANK_MAX = 512;   // survivors ranked by counting; more -> bitonic sort
-constexpr uint32_t TOPK_MERGE_SLOTS = 4096;  // LDS entries per merge block (96 KiB)
-
-__device__ inline bool topk_better(const nmz_topk_entry &a, const nmz_topk_entry &b) {
-    if (a.n_fault != b.n_fault) return a.n_fault > b.n_fault;
-    if (a.sum_delay_ns != b.sum_delay_ns) return a.sum_delay_ns > b.sum_delay_ns;
-    return a.seed < b.seed;
-}
-
-// strict total order: topk_better, then chunk position (equal entries: sentinels)
-__device__ inline bool topk_before(const nmz_topk_entry &a, uint32_t ia, const nmz_topk_entry &b, uint32_t ib) {
-    if (a.n_fault != b.n_fault) return a.n_fault > b.n_fault;
-    if (a.sum_delay_ns != b.sum_delay_ns) return a.sum_delay_ns > b.sum_delay_ns;
-    if (a.seed != b.seed) return a.seed < b.seed;
-    return ia < ib;
-}
-
-__device__ inline nmz_topk_entry topk_sentinel() {
-    nmz_topk_entry e;
-    e.seed = UINT64_MAX;
-    e.sum_delay_ns = INT64_MIN;
-    e.n_fault = 0;
-    e.first_fault = NMZ_NONE;
-    return e;
-}
-
-// Coarse key: a better than b => coarse(a) >= coarse(b). n_fault in the top 16
-// bits (saturated: every entry with >= 0xffff faults maps to the maximum key),
-// then the top 48 bits of the order-preserving (sign-flipped) sum.
-__device__ inline uint64_t topk_coarse(const nmz_topk_entry &x) {
-    if (x.n_fault >= 0xffffu) return UINT64_MAX;
-    const uint64_t bs = (uint64_t)x.sum_delay_ns ^ (1ull << 63);
-    return ((uint64_t)x.n_fault << 48) | (bs >> 16);
-}
-
-// bitonic sort (best first) of the first `n` entries of s (n a power of two)
-__device__ void bitonic_sort_n(nmz_topk_entry *s, uint32_t n) {
-    for (uint32_t size = 2; size <= n; size <<= 1) {
-        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-            __syncthreads();
-            for (uint32_t t = threadIdx.x; t < n / 2; t += blockDim.x) {
-                uint32_t i = 2 * t - (t & (stride - 1));
-                uint32_t j = i + stride;
-                bool best_first = ((i & size) == 0);
-                nmz_topk_entry a = s[i], b = s[j];
-                bool swap = best_first ? topk_better(b, a) : topk_better(a, b);
-                if (swap) {
-                    s[i] = b;
-                    s[j] = a;
-                }
-            }
-        }
-    }
-    __syncthreads();
-}
 
 __global__ __launch_bounds__(TOPK_THREADS) void k_topk_chunk(const nmz_sched_stats *__restrict__ stats, uint64_t n,
                                                               uint64_t seed0, uint32_t k,
                                                               nmz_topk_entry *__restrict__ out) {
-    __shared__ nmz_topk_entry cand[TOPK_CHUNK];
-    __shared__ uint32_t cidx[TOPK_CHUNK];
-    __shared__ uint64_t wkey[TOPK_THREADS];
-    __shared__ uint64_t tau_s;
-    __shared__ uint32_t ncand;
-    const uint32_t t = threadIdx.x;
+    __shared__ TopkShared sh;
     const uint64_t base = (uint64_t)blockIdx.x * TOPK_CHUNK;
     nmz_topk_entry e[TOPK_PER_THREAD];
-    uint64_t ck[TOPK_PER_THREAD];
-    uint64_t wk = 0;
 #pragma unroll
     for (uint32_t r = 0; r < TOPK_PER_THREAD; ++r) {
-        const uint64_t i = base + (uint64_t)r * TOPK_THREADS + t;
+        const uint64_t i = base + (uint64_t)r * TOPK_THREADS + threadIdx.x;
         nmz_topk_entry x = topk_sentinel();
         if (i < n) {
             const nmz_sched_stats st = stats[i];
@@ -104,49 +39,8 @@ __global__ __launch_bounds__(TOPK_THREADS) void k_topk_chunk(const nmz_sched_sta
             x.first_fault = st.first_fault;
         }
         e[r] = x;
-        ck[r] = topk_coarse(x);
-        wk = ck[r] > wk ? ck[r] : wk;
     }
-    wkey[t] = wk;
-    if (t == 0) ncand = 0;
-    __syncthreads();
-    // tau = k-th largest per-thread maximum (with multiplicity)
-    uint32_t gt = 0, ge = 0;
-#pragma unroll 8
-    for (uint32_t j = 0; j < TOPK_THREADS; ++j) {
-        const uint64_t w = wkey[j];
-        gt += w > wk ? 1u : 0u;
-        ge += w >= wk ? 1u : 0u;
-    }
-    if (gt < k && k <= ge) tau_s = wk;  // every writer writes the same value
-    __syncthreads();
-    const uint64_t tau = tau_s;
-#pragma unroll
-    for (uint32_t r = 0; r < TOPK_PER_THREAD; ++r) {
-        if (ck[r] >= tau) {
-            const uint32_t c = atomicAdd(&ncand, 1u);
-            cand[c] = e[r];
-            cidx[c] = r * TOPK_THREADS + t;
-        }
-    }
-    __syncthreads();
-    const uint32_t c = ncand;  // >= k
-    nmz_topk_entry *__restrict__ o = out + (uint64_t)blockIdx.x * k;
-    if (c <= TOPK_RANK_MAX) {
-        for (uint32_t i = t; i < c; i += TOPK_THREADS) {
-            const nmz_topk_entry x = cand[i];
-            const uint32_t xi = cidx[i];
-            uint32_t rk = 0;
-            for (uint32_t j = 0; j < c; ++j) rk += topk_before(cand[j], cidx[j], x, xi) ? 1u : 0u;
-            if (rk < k) o[rk] = x;
-        }
-        return;
-    }
-    uint32_t np = 2;
-    while (np < c) np <<= 1;
-    for (uint32_t i = c + t; i < np; i += TOPK_THREADS) cand[i] = topk_sentinel();
-    bitonic_sort_n(cand, np);
-    for (uint32_t i = t; i < k; i += TOPK_THREADS) o[i] = cand[i];
+    topk_block_select(e, k, out + (uint64_t)blockIdx.x * k, sh);
 }
 
 // Merge `lpb` consecutive sorted lists of k entries (kp = next pow2 >= k,
@@ -263,21 +157,17 @@ uint64_t topk_scratch_entries(uint64_t n, uint32_t k) {
     return 2 * blocks * k + 2 * TOPK_CHUNK;
 }
 
-// Writes the best k entries to d_out (device). scratch must hold
-// topk_scratch_entries(n, k) entries.
-int topk_select(hipStream_t st, const nmz_sched_stats *d_stats, uint64_t n, uint64_t seed0, uint32_t k,
-                nmz_topk_entry *d_scratch, nmz_topk_entry *d_out) {
-    if (k == 0) return NMZ_OK;
-    NMZ_CHECK(k <= TOPK_THREADS, "top-k supports k <= 256");
-    uint64_t lists = (n + TOPK_CHUNK - 1) / TOPK_CHUNK;
-    if (lists == 0) lists = 1;
-    NMZ_CHECK(lists < (1ull << 31), "too many seeds for one top-k selection");
-    nmz_topk_entry *a = d_scratch, *b = d_scratch + lists * k;
-    hipLaunchKernelGGL(k_topk_chunk, dim3((unsigned)lists), dim3(TOPK_THREADS), 0, st, d_stats, n, seed0, k,
-                       lists == 1 ? d_out : a);
+// Merges n_lists sorted lists of k entries (in `a`; `b` is scratch of the same size) into the best k,
+// written to d_out. Both buffers are overwritten.
+int topk_merge_lists(hipStream_t st, nmz_topk_entry *a, nmz_topk_entry *b, uint64_t lists, uint32_t k,
+                     nmz_topk_entry *d_out) {
     const uint32_t kp = pow2_at_least(k);
     const uint32_t lkp = (uint32_t)__builtin_ctz(kp);
     const uint32_t lpb = std::min<uint32_t>(32, TOPK_MERGE_SLOTS / kp);
+    if (lists == 1) {
+        NMZ_HIP(hipMemcpyAsync(d_out, a, (size_t)k * sizeof(nmz_topk_entry), hipMemcpyDeviceToDevice, st));
+        return NMZ_OK;
+    }
     while (kp <= 64 && lists > 1) {
         const uint64_t nb = (lists + TOPK_WAVE_LISTS - 1) / TOPK_WAVE_LISTS;
         hipLaunchKernelGGL(k_topk_merge_wave, dim3((unsigned)nb), dim3(1024), 0, st, a, (uint32_t)lists, k, kp,
@@ -298,6 +188,23 @@ int topk_select(hipStream_t st, const nmz_sched_stats *d_stats, uint64_t n, uint
     }
     NMZ_HIP(hipGetLastError());
     return NMZ_OK;
+}
+
+// Writes the best k entries to d_out (device). scratch must hold
+// topk_scratch_entries(n, k) entries.
+int topk_select(hipStream_t st, const nmz_sched_stats *d_stats, uint64_t n, uint64_t seed0, uint32_t k,
+                nmz_topk_entry *d_scratch, nmz_topk_entry *d_out) {
+    if (k == 0) return NMZ_OK;
+    NMZ_CHECK(k <= TOPK_THREADS, "top-k supports k <= 256");
+    uint64_t lists = (n + TOPK_CHUNK - 1) / TOPK_CHUNK;
+    if (lists == 0) lists = 1;
+    NMZ_CHECK(lists < (1ull << 31), "too many seeds for one top-k selection");
+    nmz_topk_entry *a = d_scratch, *b = d_scratch + lists * k;
+    hipLaunchKernelGGL(k_topk_chunk, dim3((unsigned)lists), dim3(TOPK_THREADS), 0, st, d_stats, n, seed0, k,
+                       lists == 1 ? d_out : a);
+    NMZ_HIP(hipGetLastError());
+    if (lists == 1) return NMZ_OK;
+    return topk_merge_lists(st, a, b, lists, k, d_out);
 }
 
 }  // namespace nmz

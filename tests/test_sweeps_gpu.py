@@ -147,6 +147,44 @@ def test_replayable_device_plan_api(ctx):
     L.nmz_replayable_plan_destroy(plan)
 
 
+@pytest.mark.parametrize("m,S,E,k,seed0", [
+    (100_000_000, 5000, 300, 64, 0),          # MOD_FAST: top-k fused into the merge, 3 lists
+    (100_000_000, 1500, 64, 100, 7),          # k not a power of two (LDS list-merge path)
+    (100_000_000, 200, 40, 16, 2**64 - 50),   # one list; seeds wrap past 2^64
+    (3_000_000_000, 2500, 50, 32, 5),         # MOD_GENERAL: separate selection
+    (0, 700, 20, 8, 0),                       # maxInterval 0: constant stats, all ties
+    (1_000_000, 0, 20, 8, 0),                 # no seeds: sentinels
+])
+def test_replayable_sweep_topk_dev_matches_separate_selection(ctx, m, S, E, k, seed0):
+    """nmz_replayable_sweep_topk_dev (merge + first top-k level fused) == sweep_dev + topk_select_dev
+    == oracle."""
+    import torch
+    L = _lib.load()
+    hints = zk_hints(E)
+    seeds = [str(i * 7919) for i in range(S)]
+    ho, hb = to_csr(hints)
+    so, sb = to_csr(seeds)
+    plan = ctypes.c_void_p()
+    _lib.check(L.nmz_replayable_plan_create(ctx.handle, _lib.ptr(ho), _lib.ptr(hb), E, m, max(S, 1),
+                                            ctypes.byref(plan)))
+    d_so = torch.from_numpy(so.view(np.int32)).cuda()
+    d_sb = torch.from_numpy(sb).cuda()
+    d_st = torch.zeros(max(S, 1) * 32, dtype=torch.uint8, device="cuda")
+    d_tk = torch.zeros(k * 24, dtype=torch.uint8, device="cuda")
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(L.nmz_replayable_sweep_topk_dev(plan, ctypes.c_void_p(d_so.data_ptr()),
+                                               ctypes.c_void_p(d_sb.data_ptr()), S, seed0, k,
+                                               ctypes.c_void_p(d_st.data_ptr()), ctypes.c_void_p(d_tk.data_ptr()),
+                                               stream))
+    torch.cuda.synchronize()
+    L.nmz_replayable_plan_destroy(plan)
+    got = np.frombuffer(d_st.cpu().numpy().tobytes(), dtype=_lib.SCHED_STATS_DTYPE)[:S]
+    tk = np.frombuffer(d_tk.cpu().numpy().tobytes(), dtype=_lib.TOPK_DTYPE)
+    st, _ = rep_oracle(seeds, hints, m) if S else (np.zeros(0, O.SCHED_STATS_DTYPE), None)
+    assert np.array_equal(got, st)
+    assert tk.tolist() == O.topk_from_stats(st, seed0, k).tolist()
+
+
 # ---------------------------------------------------------------- K2
 PARAMS = [(30_000_000, 100_000_000, 0.1), (5_000_000, 5_000_000, 0.5), (0, 1 << 20, 1.0),
           (80_000_000, 3_000_000_000, 0.999), (0, 0, 0.0), (-5_000_000, 5_000_000, 0.3), (7, 9, 0.25),
