@@ -10,7 +10,8 @@ import threading
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libnmz_gpu.so")
+# NMZ_LIB_PATH: an alternative in-tree build of the same library (tuning variants)
+LIB_PATH = os.environ.get("NMZ_LIB_PATH") or os.path.join(HERE, "libnmz_gpu.so")
 
 NMZ_OK = 0
 NMZ_EINVAL = -1

@@ -1,3 +1,4 @@
+#include <cstdlib>
 // K3 -- banded Levenshtein over event-hash sequences + all-pairs k-NN.
 //
 // ED_w(a,b) = min(D(n,m), w+1), D restricted to |i-j| <= w (outside = +inf).
@@ -458,7 +459,14 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
             len[i] = (uint32_t)(off[i + 1] - off[i]);
             soff[i + 1] = soff[i] + ((uint64_t)(len[i] + 31) / 32 + 1) * 32;  // whole blocks + 1 spare
         }
-        p->pool = ED_BV_POOL;
+        // candidates per workgroup: a larger pool amortises the Peq build and evens out the lanes' refill
+        // tail, a smaller one keeps enough workgroups for small N (configs[2]-shaped traces, 1 MI355X:
+        // N = 100k: 1024 -> 1.78 s, 4096 -> 1.64 s, 8192 -> 1.65 s; N = 8192: 1024 -> 14.5 ms, 4096 -> 19.6 ms)
+        p->pool = N >= 24576 ? 4 * ED_BV_POOL : (N >= 12288 ? 2 * ED_BV_POOL : ED_BV_POOL);
+        if (const char *e = getenv("NMZ_ED_POOL")) {  // tuning override (multiple of 256)
+            const uint32_t v = (uint32_t)atoi(e);
+            if (v >= 256 && v % 256 == 0) p->pool = v;
+        }
         for (uint32_t b = 0; b < G; ++b)
             chunk_start[b + 1] = chunk_start[b] + (N - 64 * b + p->pool - 1) / p->pool;
         p->n_chunks = chunk_start[G];

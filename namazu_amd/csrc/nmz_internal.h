@@ -27,7 +27,7 @@ struct Carve {
 bool ed_bv_supported(uint32_t band);
 
 // bit-parallel banded edit distance (ed_bv.hip): 2 queries x a pool of ED_BV_POOL candidates per workgroup
-constexpr uint32_t ED_BV_POOL = 1024;
+constexpr uint32_t ED_BV_POOL = 1024;  // base pool; the plan scales it up to 4x for large N (ed.hip)
 struct EdBvArgs {
     const uint16_t *bsym;         // per-trace streams of Peq-row byte offsets (u16), padded to 32-blocks + 1
     const uint64_t *soff;         // [N] element offset of each trace's stream

@@ -41,6 +41,17 @@ def test_knn_fast_kernel(ctx, n, lmin, lmax, w, mut, k):
     assert np.array_equal(ids, oi) and np.array_equal(ds, od)
 
 
+@pytest.mark.parametrize("pool", [256, 2048, 4096])
+def test_knn_bv_pool_sizes(ctx, monkeypatch, pool):
+    """k_ed_bv workgroups own pools of 256..4096 candidates (the plan picks 4096 for N >= 24576);
+    forced here on a smaller N with short ragged traces, vs the oracle."""
+    monkeypatch.setenv("NMZ_ED_POOL", str(pool))
+    ts = make_traces(1500, 100, 200, 0.04, alphabet=20, rng=np.random.default_rng(pool))
+    ids, ds = knn(ctx, ts, 32, 8)
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, 32, 8, nthreads=16)
+    assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+
+
 @pytest.mark.parametrize("w", [0, 1, 5, 31, 33, 100])
 def test_knn_generic_bands(ctx, w):
     ts = make_traces(60, 0, 60, 0.2)
