@@ -3,7 +3,9 @@
 
 Headline workload (BASELINE.json configs[1]): replayable-policy seed sweep,
 2^20 seeds x 4096-event ZooKeeper-style packet trace, maxInterval 100 ms, on
-each GPU (weak scaling: every rank sweeps its own 2^20 seeds). One step =
+each GPU (weak scaling: every rank sweeps its own 2^20 seeds per step; steps
+are pipelined over 3 plans / HIP streams, each slot with its own seed range,
+so one step's latency-bound kernels overlap the neighbouring steps). One step =
   seed prefix hashing + bucketing + the K1 sweep (stats for every seed)
   + per-rank top-64 selection (+ RCCL all_gather and merge when N > 1).
 Inputs are resident in HBM before the timed region; the per-trace plan
@@ -136,72 +138,96 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     hints = zk_hints(E)
     from namazu_amd.explorepolicy import to_csr
     hoff, hb = to_csr(hints)
-    seed_lo = D.rank * S
-    soff, sb = decimal_csr(seed_lo, S)
-    plan = ctypes.c_void_p()
+    # Consecutive steps are pipelined over NP plans and HIP streams (NMZ_BENCH_PIPELINE, default 3), each
+    # slot sweeping its own range of S seeds: the latency-bound kernels around one step's sweep (seed
+    # prefix, bucketing, merge, top-k) and the tail of its persistent sweep grid overlap the neighbouring
+    # steps. Every step does all of its work on its own batch.
+    NP = max(1, int(os.environ.get("NMZ_BENCH_PIPELINE", "3")))
+    seed_lo = [(D.rank * NP + sp) * S for sp in range(NP)]
+    csr = [decimal_csr(lo, S) for lo in seed_lo]
+    plans = []
     t0 = time.time()
-    _lib.check(L.nmz_replayable_plan_create(ctx.handle, host_ptr(hoff), host_ptr(hb), E, MAX_INTERVAL_NS, S,
-                                            ctypes.byref(plan)))
-    plan_ms = (time.time() - t0) * 1e3
+    for _ in range(NP):
+        plan = ctypes.c_void_p()
+        _lib.check(L.nmz_replayable_plan_create(ctx.handle, host_ptr(hoff), host_ptr(hb), E, MAX_INTERVAL_NS, S,
+                                                ctypes.byref(plan)))
+        plans.append(plan)
+    plan_ms = (time.time() - t0) * 1e3 / NP
     dev = torch.device("cuda", D.local_rank)
-    d_soff = torch.from_numpy(soff.view(np.int32)).to(dev)
-    d_sb = torch.from_numpy(sb).to(dev)
-    d_stats = torch.empty(S * 32, dtype=torch.uint8, device=dev)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(NP - 1)]
+    d_soff = [torch.from_numpy(so.view(np.int32)).to(dev) for so, _ in csr]
+    d_sb = [torch.from_numpy(sb).to(dev) for _, sb in csr]
+    d_stats = [torch.empty(S * 32, dtype=torch.uint8, device=dev) for _ in range(NP)]
     K_TOP = 64
-    # two top-k buffers: the RCCL all_gather of step i (async, on the process group's stream) overlaps
-    # the sweep of step i+1; a buffer is rewritten only after the gather that reads it has completed
-    d_topk = [torch.empty(K_TOP * 24, dtype=torch.uint8, device=dev) for _ in range(2)]
-    gathered = [[torch.empty_like(d_topk[0]) for _ in range(D.world)] for _ in range(2)] if D.world > 1 else None
-    pending = [None, None]
+    # per-slot top-k buffers: the RCCL all_gather of a step (async, on the process group's stream) overlaps
+    # the following steps; a slot is rewritten only after the gather that reads it has completed
+    d_topk = [torch.empty(K_TOP * 24, dtype=torch.uint8, device=dev) for _ in range(NP)]
+    gathered = [[torch.empty_like(d_topk[0]) for _ in range(D.world)] for _ in range(NP)] if D.world > 1 else None
+    pending = [None] * NP
     it = [0]
 
-    def step():
-        b = it[0] & 1
-        it[0] += 1
-        if pending[b] is not None:
-            pending[b].wait()
-            pending[b] = None
-        # sweep + top-k in one call
-        _lib.check(L.nmz_replayable_sweep_topk_dev(plan, ctypes.c_void_p(d_soff.data_ptr()),
-                                                   ctypes.c_void_p(d_sb.data_ptr()), S, seed_lo, K_TOP,
-                                                   ctypes.c_void_p(d_stats.data_ptr()),
-                                                   ctypes.c_void_p(d_topk[b].data_ptr()), stream))
-        if D.pg:
-            pending[b] = D.pg.all_gather(gathered[b], d_topk[b], async_op=True)
-            return gathered[b]
-        return [d_topk[b]]
+    def step(sp=None):
+        if sp is None:
+            sp = it[0] % NP
+            it[0] += 1
+        with torch.cuda.stream(streams[sp]):
+            if pending[sp] is not None:
+                pending[sp].wait()
+                pending[sp] = None
+            # sweep + top-k in one call
+            _lib.check(L.nmz_replayable_sweep_topk_dev(plans[sp], ctypes.c_void_p(d_soff[sp].data_ptr()),
+                                                       ctypes.c_void_p(d_sb[sp].data_ptr()), S, seed_lo[sp], K_TOP,
+                                                       ctypes.c_void_p(d_stats[sp].data_ptr()),
+                                                       ctypes.c_void_p(d_topk[sp].data_ptr()),
+                                                       ctypes.c_void_p(streams[sp].cuda_stream)))
+            if D.pg:
+                pending[sp] = D.pg.all_gather(gathered[sp], d_topk[sp], async_op=True)
 
     def drain():
-        for b in range(2):
-            if pending[b] is not None:
-                pending[b].wait()
-                pending[b] = None
+        for sp in range(NP):
+            if pending[sp] is not None:
+                with torch.cuda.stream(streams[sp]):
+                    pending[sp].wait()
+                pending[sp] = None
 
-    for _ in range(args.warmup):
+    def outputs():
+        if D.pg:
+            return [t for g in gathered for t in g]
+        return list(d_topk)
+
+    for _ in range(max(args.warmup, NP)):
         step()
     drain()
     torch.cuda.synchronize()
+    # the roofline's kernel time: K1 launches one at a time (HIP events on the launch stream), untimed
     _lib.check(L.nmz_timing_enable(ctx.handle, 1))
     tot, cnt = ctypes.c_double(), ctypes.c_uint64()
     L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
+    for _ in range(5):
+        step(0)
+        drain()
+    torch.cuda.synchronize()
+    _lib.check(L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
+    _lib.check(L.nmz_timing_enable(ctx.handle, 0))
+    kern_ms = tot.value / max(cnt.value, 1)
+    # the timed region: exactly args.steps pipelined steps
+    it[0] = 0
     D.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        outs = step()
+        step()
     drain()
     torch.cuda.synchronize()
     D.barrier()
     el = time.perf_counter() - t0
-    merged = merge_topk(b"".join(o.cpu().numpy().tobytes() for o in outs), K_TOP)
-    _lib.check(L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
-    _lib.check(L.nmz_timing_enable(ctx.handle, 0))
-    kern_ms = tot.value / max(cnt.value, 1)
+    merged = merge_topk(b"".join(o.cpu().numpy().tobytes() for o in outputs()), K_TOP)
     el_max = D.max(torch, el)
-    stats = np.frombuffer(d_stats.cpu().numpy().tobytes(), dtype=_lib.SCHED_STATS_DTYPE)
-    L.nmz_replayable_plan_destroy(plan)
-    return dict(S=S, E=E, hints=(hoff, hb), seeds=(soff, sb), elapsed=el_max, kern_ms=kern_ms, plan_ms=plan_ms,
-                stats=stats, topk=merged)
+    stats = np.frombuffer(d_stats[0].cpu().numpy().tobytes(), dtype=_lib.SCHED_STATS_DTYPE)
+    for plan in plans:
+        L.nmz_replayable_plan_destroy(plan)
+    return dict(S=S, E=E, hints=(hoff, hb), seeds=csr[0], elapsed=el_max, kern_ms=kern_ms, plan_ms=plan_ms,
+                stats=stats, topk=merged, pipeline=NP)
 
 
 def cpu_baseline_replayable(r, args):
@@ -394,7 +420,7 @@ def main():
         "dtype": "u64",
         "data": "synthetic (ZooKeeper-style hints: signed decimal SplitMix64, seed 0x5EED; decimal seeds)",
         "config": {"workload": "configs[1] replayable seed sweep", "seeds_per_gpu": r["S"], "events": r["E"],
-                   "max_interval_ns": MAX_INTERVAL_NS, "topk": 64,
+                   "max_interval_ns": MAX_INTERVAL_NS, "topk": 64, "pipeline_streams": r["pipeline"],
                    "parallelism": f"seed-range x{D.world}" + (" + RCCL all_gather top-k" if D.world > 1 else "")},
         "roofline": roofline_valu("k_replayable_sweep_fast", dec_launch, r["kern_ms"]),
         "plan_ms": r["plan_ms"],
