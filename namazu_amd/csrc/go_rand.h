@@ -71,6 +71,14 @@ __device__ __forceinline__ uint64_t vec_c(uint32_t s) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// high word of the seeded vec[I] (only x_{21+3I} and x_{22+3I} enter it)
+template <int I>
+__device__ __forceinline__ uint32_t vec_hi(uint32_t s) {
+    constexpr uint32_t ca = pow_a(21 + 3 * I), cb = pow_a(22 + 3 * I);
+    constexpr uint64_t ck = NMZ_GO_RNG_COOKED[I];
+    return (modmul(s, ca) << 8) ^ (modmul(s, cb) >> 12) ^ (uint32_t)(ck >> 32);
+}
+
 // outputs 0 and 1 after Seed (no state)
 __device__ __forceinline__ uint64_t out0(uint32_t s) { return vec_c<333>(s) + vec_c<606>(s); }
 __device__ __forceinline__ uint64_t out1(uint32_t s) { return vec_c<332>(s) + vec_c<605>(s); }

@@ -101,6 +101,18 @@ __device__ __forceinline__ Decision decide(uint32_t s, uint32_t cls, const Rando
         d.delay = cp.min;
     }
     if (cls & NMZ_EV_FAULTABLE) {
+        if (t == 1) {
+            // Intn(999) reads bits 32..62 of y1 = vec[332] + vec[605]: the high words' sum, plus the carry
+            // out of the low words. The carry changes v by one, which changes the outcome only when v
+            // sits next to the rejection bound or v % 999 next to thr - 1 / 998 (~2e-3 of draws); only
+            // then are the low words (two more modmuls) computed.
+            const uint32_t v0 = (gorand::vec_hi<332>(s) + gorand::vec_hi<605>(s)) & 0x7fffffffu;
+            const uint32_t r0 = v0 % INTN_N;
+            if (!(v0 >= INT31N_MAX || r0 == INTN_N - 1 || r0 + 1 == (uint32_t)P.fault_threshold)) {
+                d.fault = ((int32_t)r0 < P.fault_threshold) ? 1u : 0u;
+                return d;
+            }
+        }
         uint64_t y = (t == 0) ? gorand::out0(s) : (t == 1 ? gorand::out1(s) : go_output(s, t));
         ++t;
         uint32_t v = (uint32_t)(y >> 32) & 0x7fffffffu;
