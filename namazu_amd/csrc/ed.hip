@@ -348,6 +348,8 @@ struct nmz_ed_plan {
     bool wide = false;             // wide-band bit-parallel kernel (k_ed_wide) usable
     uint32_t n_sym = 0;
     uint32_t *d_peq = nullptr;     // wide: [N][n_sym][ndw] match bitmaps
+    uint32_t *d_rowb = nullptr;    // wide: per-position Peq row byte offsets (EdWideArgs::rowb)
+    uint64_t *d_rowb_off = nullptr;
     uint32_t ndw = 0, lds_dw = 0;  // bv: dwords per Peq row per query, LDS dwords per workgroup
     uint64_t n_chunks = 0;         // bv: total chunks (64-query block row x ED_BV_POOL candidates)
     uint16_t *d_bsym = nullptr;
@@ -423,7 +425,8 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
             if (!seen[ids[t]]) { seen[ids[t]] = 1; ++n_sym; }
         const uint32_t ndw = ed_wide_ndw(band, maxlen);
         const uint64_t peq_bytes = (uint64_t)N * std::max(n_sym, 1u) * ndw * 4;
-        if (peq_bytes <= (16ULL << 30)) {
+        // one query's table must be addressable by a 32-bit buffer offset
+        if (peq_bytes <= (16ULL << 30) && (uint64_t)std::max(n_sym, 1u) * ndw * 4 < (1ULL << 31)) {
             p->wide = true;
             p->ndw = ndw;
             p->n_sym = std::max(n_sym, 1u);
@@ -433,14 +436,26 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
     }
     p->fast = fast;
     if (fast && p->wide) {
+        // per-position Peq row byte offsets, each trace padded to whole 32-column blocks + 2 spare blocks
+        std::vector<uint64_t> roff(N + 1, 0);
+        for (uint32_t i = 0; i < N; ++i) roff[i + 1] = roff[i] + ((off[i + 1] - off[i] + 31) / 32 + 2) * 32;
+        std::vector<uint32_t> rowb(roff[N] + 1, 0);
+        for (uint32_t i = 0; i < N; ++i)
+            for (uint64_t t = off[i]; t < off[i + 1]; ++t) rowb[roff[i] + (t - off[i])] = ids[t] * p->ndw * 4;
         size_t need = Carve::bytes_for(total + 64, 2) + Carve::bytes_for(N + 1, 8) +
-                      Carve::bytes_for((uint64_t)N * p->n_sym * p->ndw, 4);
+                      Carve::bytes_for((uint64_t)N * p->n_sym * p->ndw, 4) + Carve::bytes_for(rowb.size(), 4) +
+                      Carve::bytes_for(N + 1, 8);
         int rc = p->mem.ensure(need);
         if (rc != NMZ_OK) return cleanup(rc);
         Carve cv(p->mem.ptr);
         p->d_qsym = cv.take<uint16_t>(total + 64);
         p->d_qoff = cv.take<uint64_t>(N + 1);
         p->d_peq = cv.take<uint32_t>((uint64_t)N * p->n_sym * p->ndw);
+        p->d_rowb = cv.take<uint32_t>(rowb.size());
+        p->d_rowb_off = cv.take<uint64_t>(N + 1);
+        if (hipMemcpyAsync(p->d_rowb, rowb.data(), rowb.size() * 4, hipMemcpyHostToDevice, st) ||
+            hipMemcpyAsync(p->d_rowb_off, roff.data(), (N + 1) * 8, hipMemcpyHostToDevice, st))
+            return cleanup(fail(NMZ_EHIP, "ED plan upload failed"));
         if (hipMemsetAsync(p->d_qsym, 0, (total + 64) * 2, st) ||
             (total && hipMemcpyAsync(p->d_qsym, ids.data(), total * 2, hipMemcpyHostToDevice, st)) ||
             hipMemcpyAsync(p->d_qoff, off, (N + 1) * 8, hipMemcpyHostToDevice, st))
@@ -550,6 +565,8 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
         EdWideArgs A;
         A.sym = p->d_qsym;
         A.off = p->d_qoff;
+        A.rowb = p->d_rowb;
+        A.rowb_off = p->d_rowb_off;
         A.peq = p->d_peq;
         A.knn = d_knn;
         A.n_pairs = (uint64_t)N * (N - 1) / 2;

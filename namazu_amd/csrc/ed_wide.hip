@@ -149,11 +149,17 @@ __global__ __launch_bounds__(256) void k_ed_wide(EdWideArgs A) {
             r = n + m;
         } else {
             const uint32_t *prow = A.peq + (uint64_t)i * A.n_sym * A.ndw;
-            // candidate symbols: wave-uniform, read through the scalar cache (constant address space)
+            // The query's match table through a buffer descriptor: per column the load's scalar offset
+            // is (row byte offset of the candidate's symbol) + (band dword) * 4, the lane's part a
+            // constant VGPR -- one s_add per column instead of a 64-bit address computation.
+            const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+                (void *)prow, (short)0, (int)(A.n_sym * A.ndw * 4), 0x00020000);
+            const uint32_t voff = KL * lane * 4;
+            // candidate's per-position row offsets: wave-uniform, read through the scalar cache
             typedef const uint32_t __attribute__((address_space(4))) *cptr;
-            const uint64_t sb = __builtin_amdgcn_readfirstlane((uint32_t)A.off[j]) |
-                                ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(A.off[j] >> 32)) << 32);
-            const cptr sym32 = (cptr)(const void *)A.sym;
+            const uint64_t rb = __builtin_amdgcn_readfirstlane((uint32_t)A.rowb_off[j]) |
+                                ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(A.rowb_off[j] >> 32)) << 32);
+            const cptr rowb = (cptr)(const void *)(A.rowb + rb);
             WideState<KL> S;
 #pragma unroll
             for (int k = 0; k < KL; ++k) {
@@ -163,26 +169,39 @@ __global__ __launch_bounds__(256) void k_ed_wide(EdWideArgs A) {
             S.acc = 0;
             uint32_t T = W;
             // Eq dwords of column jj (1-based): row b_{jj}, dword (jj+31)>>5 + KL*lane, shift (jj-1)&31
-            auto eq_ptr = [&](uint32_t jj) -> const uint32_t * {
-                const uint64_t e = sb + jj - 1;
-                const uint32_t c = (sym32[e >> 1] >> (16 * (uint32_t)(e & 1))) & 0xffffu;
-                return prow + (uint64_t)c * A.ndw + ((jj + 31) >> 5) + KL * lane;
+            auto load_col = [&](uint32_t (&d)[KL + 1], uint32_t row_bytes, uint32_t jj) {
+                const uint32_t so = row_bytes + ((jj + 31) >> 5) * 4;
+                if constexpr (KL == 4) {
+                    const u32x4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, so, 0);
+                    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+                    d[4] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + 16, so, 0);
+                } else {
+#pragma unroll
+                    for (int k = 0; k <= KL; ++k) d[k] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + 4 * k, so, 0);
+                }
             };
             constexpr int D = 8;
+            uint32_t cur[32], nxt[32];  // row offsets of this block's and the next block's columns
+#pragma unroll
+            for (int k = 0; k < 32; ++k) cur[k] = rowb[k];
             uint32_t ring[D][KL + 1];
 #pragma unroll
-            for (int u = 0; u < D; ++u) wide_load<KL>(ring[u], eq_ptr(1 + u));
+            for (int u = 0; u < D; ++u) load_col(ring[u], cur[u], 1 + u);
             bool done = false;
             uint32_t j0 = 0;
             for (; j0 + 32 <= m; j0 += 32) {
+#pragma unroll
+                for (int k = 0; k < 32; ++k) nxt[k] = rowb[j0 + 32 + k];  // streams carry 2 spare blocks
 #pragma unroll
                 for (int t = 0; t < 32; ++t) {
                     uint32_t dcur[KL + 1];
 #pragma unroll
                     for (int k = 0; k <= KL; ++k) dcur[k] = ring[t % D][k];
-                    wide_load<KL>(ring[t % D], eq_ptr(j0 + t + 1 + D));  // streams are padded past the end
+                    load_col(ring[t % D], t + D < 32 ? cur[t + D] : nxt[t + D - 32], j0 + t + 1 + D);
                     wide_column<KL>(S, dcur, t, lane);
                 }
+#pragma unroll
+                for (int k = 0; k < 32; ++k) cur[k] = nxt[k];
                 T += 32 - __builtin_popcount(__builtin_amdgcn_readfirstlane(S.acc));
                 if (j0 + 32 == m) {
                     r = min((uint32_t)((int32_t)T + wide_prefix<KL>(S, n + W - m, lane)), W + 1);
@@ -203,7 +222,7 @@ __global__ __launch_bounds__(256) void k_ed_wide(EdWideArgs A) {
                 const uint32_t tail = m - j0;
                 for (uint32_t t = 0; t < tail; ++t) {
                     uint32_t dcur[KL + 1];
-                    wide_load<KL>(dcur, eq_ptr(j0 + t + 1));
+                    load_col(dcur, rowb[j0 + t], j0 + t + 1);
                     wide_column<KL>(S, dcur, t, lane);
                 }
                 const uint32_t acc0 = __builtin_amdgcn_readfirstlane(S.acc);

@@ -43,6 +43,9 @@ int ed_bv_launch(const EdBvArgs &A, uint32_t band, uint64_t blocks, hipStream_t 
 struct EdWideArgs {
     const uint16_t *sym;   // dense symbol ids, CSR order (padded with 64 zeros)
     const uint64_t *off;   // [N+1]
+    const uint32_t *rowb;  // per trace, per position: byte offset of that symbol's Peq row (c * ndw * 4),
+                           // each trace starting at a multiple of 32 entries, padded by >= 64 zero entries
+    const uint64_t *rowb_off;  // [N]: first entry of trace j in rowb
     const uint32_t *peq;   // [N][n_sym][ndw] match bitmaps
     uint64_t *knn;         // [N][k]
     uint64_t n_pairs;      // N(N-1)/2
