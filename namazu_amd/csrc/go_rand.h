@@ -45,11 +45,19 @@ constexpr PowTable make_pow_table() {
     return t;
 }
 
-// a * b mod (2^31 - 1) for a, b < 2^31 (Mersenne folding)
-__device__ __forceinline__ uint32_t modmul(uint32_t a, uint32_t b) {
-    const uint64_t p = (uint64_t)a * b;
-    uint32_t r = ((uint32_t)p & M31) + (uint32_t)(p >> 31);
-    return min(r, r - M31);
+// a * b mod (2^31 - 1) for a, b < 2^31 (Mersenne folding). With a * b = Q * 2^31 + R (R < 2^31), the product
+// p = a * 2b is Q * 2^32 + 2R, so its high word is Q and its low word shifted right by one is R; Q + R < 2M
+// and Q + R = a * b (mod M). For a compile-time b this is v_mad_u64_u32 + lshr + add + a conditional
+// subtract: no mask with a literal and no v_alignbit (both half rate on gfx950). `nm` is -M (mod 2^32); a hot
+// loop passes it in a VGPR the compiler cannot see through, so that the subtract is a full-rate VGPR-VGPR add
+// instead of an add with a literal.
+constexpr uint32_t NEG_M31 = 0u - M31;
+__device__ __forceinline__ uint32_t modmul(uint32_t a, uint32_t b, uint32_t nm = NEG_M31) {
+    const uint64_t p = (uint64_t)a * (2u * b);
+    const uint32_t r = (uint32_t)(p >> 32) + ((uint32_t)p >> 1);
+    uint32_t t;
+    const bool borrow = __builtin_sub_overflow(r, 0u - nm, &t);
+    return borrow ? r : t;
 }
 
 // Go's `seed % int32max; if seed < 0 { seed += int32max }; if seed == 0 { seed = 89482311 }`
@@ -62,10 +70,10 @@ __host__ __device__ inline uint32_t seed_reduce(int64_t seed) {
 
 // seeded vec[i] for a compile-time index
 template <int I>
-__device__ __forceinline__ uint64_t vec_c(uint32_t s) {
+__device__ __forceinline__ uint64_t vec_c(uint32_t s, uint32_t nm = NEG_M31) {
     constexpr uint32_t ca = pow_a(21 + 3 * I), cb = pow_a(22 + 3 * I), cc = pow_a(23 + 3 * I);
     constexpr uint64_t ck = NMZ_GO_RNG_COOKED[I];
-    const uint32_t xa = modmul(s, ca), xb = modmul(s, cb), xc = modmul(s, cc);
+    const uint32_t xa = modmul(s, ca, nm), xb = modmul(s, cb, nm), xc = modmul(s, cc, nm);
     const uint32_t lo = (xb << 20) ^ xc ^ (uint32_t)ck;
     const uint32_t hi = (xa << 8) ^ (xb >> 12) ^ (uint32_t)(ck >> 32);
     return ((uint64_t)hi << 32) | lo;
@@ -73,15 +81,19 @@ __device__ __forceinline__ uint64_t vec_c(uint32_t s) {
 
 // high word of the seeded vec[I] (only x_{21+3I} and x_{22+3I} enter it)
 template <int I>
-__device__ __forceinline__ uint32_t vec_hi(uint32_t s) {
+__device__ __forceinline__ uint32_t vec_hi(uint32_t s, uint32_t nm = NEG_M31) {
     constexpr uint32_t ca = pow_a(21 + 3 * I), cb = pow_a(22 + 3 * I);
     constexpr uint64_t ck = NMZ_GO_RNG_COOKED[I];
-    return (modmul(s, ca) << 8) ^ (modmul(s, cb) >> 12) ^ (uint32_t)(ck >> 32);
+    return (modmul(s, ca, nm) << 8) ^ (modmul(s, cb, nm) >> 12) ^ (uint32_t)(ck >> 32);
 }
 
 // outputs 0 and 1 after Seed (no state)
-__device__ __forceinline__ uint64_t out0(uint32_t s) { return vec_c<333>(s) + vec_c<606>(s); }
-__device__ __forceinline__ uint64_t out1(uint32_t s) { return vec_c<332>(s) + vec_c<605>(s); }
+__device__ __forceinline__ uint64_t out0(uint32_t s, uint32_t nm = NEG_M31) {
+    return vec_c<333>(s, nm) + vec_c<606>(s, nm);
+}
+__device__ __forceinline__ uint64_t out1(uint32_t s, uint32_t nm = NEG_M31) {
+    return vec_c<332>(s, nm) + vec_c<605>(s, nm);
+}
 
 }  // namespace gorand
 }  // namespace nmz

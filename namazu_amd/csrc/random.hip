@@ -71,6 +71,20 @@ __device__ __forceinline__ uint64_t mod_barrett(uint64_t v, uint64_t n, uint64_t
     return r >= n ? r - n : r;
 }
 
+// Same for n < 2^31: r = v - q*n < 2n < 2^32, so only the low word of q = floor(v*mu / 2^64) is needed and
+// r = v_lo - q_lo*n (mod 2^32). With v*mu = X + (vh*mul + vl*muh)*2^32 + vh*muh*2^64 (X = vl*mul):
+// a = vh*mul + hi(X), b = vl*muh + lo(a), q = vh*muh + hi(a) + hi(b).
+__device__ __forceinline__ uint32_t mod_barrett31(uint64_t v, uint32_t n, uint64_t mu) {
+    const uint32_t vl = (uint32_t)v, vh = (uint32_t)(v >> 32);
+    const uint32_t mul = (uint32_t)mu, muh = (uint32_t)(mu >> 32);
+    const uint64_t a = (uint64_t)vh * mul + __umulhi(vl, mul);
+    const uint64_t b = (uint64_t)vl * muh + (uint32_t)a;
+    const uint32_t ql = vh * muh + (uint32_t)(a >> 32) + (uint32_t)(b >> 32);
+    const uint32_t r = vl - ql * n;
+    uint32_t t;
+    return __builtin_sub_overflow(r, n, &t) ? r : t;
+}
+
 struct Decision {
     int64_t delay;
     uint32_t fault;
@@ -78,12 +92,13 @@ struct Decision {
 };
 
 // One decision given the reduced Go seed s (1 <= s < 2^31-1) and uniform class bits.
-__device__ __forceinline__ Decision decide(uint32_t s, uint32_t cls, const RandomKParams &P) {
+__device__ __forceinline__ Decision decide(uint32_t s, uint32_t cls, const RandomKParams &P,
+                                           uint32_t nm = gorand::NEG_M31) {
     Decision d{0, 0, 0};
     const ClassParams &cp = P.cls[cls & NMZ_EV_PRIORITIZED];
     int t = 0;
     if (cp.n) {
-        uint64_t v = gorand::out0(s) & MASK63;
+        uint64_t v = gorand::out0(s, nm) & MASK63;
         t = 1;
         if (cp.mu) {
             while (v > cp.max_accept) {  // rare: re-draw
@@ -93,7 +108,8 @@ __device__ __forceinline__ Decision decide(uint32_t s, uint32_t cls, const Rando
                 }
                 v = go_output(s, t++) & MASK63;
             }
-            d.delay = (int64_t)mod_barrett(v, cp.n, cp.mu) + cp.min;
+            d.delay = (cp.n >> 31) == 0 ? (int64_t)mod_barrett31(v, (uint32_t)cp.n, cp.mu) + cp.min
+                                        : (int64_t)mod_barrett(v, cp.n, cp.mu) + cp.min;
         } else {
             d.delay = (int64_t)(v & (cp.n - 1)) + cp.min;
         }
@@ -106,14 +122,14 @@ __device__ __forceinline__ Decision decide(uint32_t s, uint32_t cls, const Rando
             // out of the low words. The carry changes v by one, which changes the outcome only when v
             // sits next to the rejection bound or v % 999 next to thr - 1 / 998 (~2e-3 of draws); only
             // then are the low words (two more modmuls) computed.
-            const uint32_t v0 = (gorand::vec_hi<332>(s) + gorand::vec_hi<605>(s)) & 0x7fffffffu;
+            const uint32_t v0 = (gorand::vec_hi<332>(s, nm) + gorand::vec_hi<605>(s, nm)) & 0x7fffffffu;
             const uint32_t r0 = v0 % INTN_N;
             if (!(v0 >= INT31N_MAX || r0 == INTN_N - 1 || r0 + 1 == (uint32_t)P.fault_threshold)) {
                 d.fault = ((int32_t)r0 < P.fault_threshold) ? 1u : 0u;
                 return d;
             }
         }
-        uint64_t y = (t == 0) ? gorand::out0(s) : (t == 1 ? gorand::out1(s) : go_output(s, t));
+        uint64_t y = (t == 0) ? gorand::out0(s, nm) : (t == 1 ? gorand::out1(s, nm) : go_output(s, t));
         ++t;
         uint32_t v = (uint32_t)(y >> 32) & 0x7fffffffu;
         while (v > INT31N_MAX) {  // rare: re-draw
@@ -199,17 +215,25 @@ __global__ __launch_bounds__(256) void k_random_sweep(const uint4 *__restrict__ 
     const uint64_t H = h0 * fnv_pow(8);
     const uint32_t Hm = (uint32_t)(H % gorand::M31);
     const uint4 *__restrict__ row = table + (uint64_t)L * E;
+    uint32_t nm = gorand::NEG_M31;  // -M in a VGPR (see gorand::modmul)
+    asm volatile("" : "+v"(nm));
 
     uint64_t sum = 0;
     int64_t best = INT64_MIN;
-    uint32_t arg = NMZ_NONE, nf = 0, ff = NMZ_NONE, ovf = 0;
+    // argmax = first maximum: starting at event 0 with best = INT64_MIN, a strict > reproduces it
+    uint32_t arg = E ? 0u : NMZ_NONE, nf = 0, ff = NMZ_NONE, ovf = 0;
     for (uint32_t e = 0; e < E; ++e) {
-        const uint4 q = row[e];
-        const uint32_t cls = __builtin_amdgcn_readfirstlane(q.w);
+        // the event index is wave-uniform; without the readfirstlane the compiler keeps it in a VGPR
+        // (divergent rejection loops below) and loads the entry per lane
+        const uint32_t eu = __builtin_amdgcn_readfirstlane(e);
+        const uint4 qv = row[eu];
+        const uint4 q = make_uint4(__builtin_amdgcn_readfirstlane(qv.x), __builtin_amdgcn_readfirstlane(qv.y),
+                                   __builtin_amdgcn_readfirstlane(qv.z), __builtin_amdgcn_readfirstlane(qv.w));
+        const uint32_t cls = q.w;
         const uint32_t s = go_seed_from_table(H, Hm, q);
-        const Decision d = decide(s, cls, P);
+        const Decision d = decide(s, cls, P, nm);
         sum += (uint64_t)d.delay;
-        if (d.delay > best || arg == NMZ_NONE) {
+        if (d.delay > best) {
             best = d.delay;
             arg = e;
         }

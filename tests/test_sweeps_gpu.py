@@ -188,7 +188,7 @@ def test_replayable_sweep_topk_dev_matches_separate_selection(ctx, m, S, E, k, s
 # ---------------------------------------------------------------- K2
 PARAMS = [(30_000_000, 100_000_000, 0.1), (5_000_000, 5_000_000, 0.5), (0, 1 << 20, 1.0),
           (80_000_000, 3_000_000_000, 0.999), (0, 0, 0.0), (-5_000_000, 5_000_000, 0.3), (7, 9, 0.25),
-          (1, 1 + (1 << 40), 0.05)]
+          (1, 1 + (1 << 40), 0.05), (0, (1 << 31) - 1, 0.2), (0, (1 << 31) + 1, 0.2), (3, 3 + (1 << 31), 0.7)]
 
 
 @pytest.mark.parametrize("mn,mx,p", PARAMS)
