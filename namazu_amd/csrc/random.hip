@@ -197,51 +197,64 @@ __global__ __launch_bounds__(256) void k_random_prefix(uint64_t seed0, uint64_t 
     if (hist[threadIdx.x]) atomicAdd(&count[threadIdx.x * BUCKET_STRIDE], hist[threadIdx.x]);
 }
 
-__global__ __launch_bounds__(256) void k_random_sweep(const uint4 *__restrict__ units,
+// Work item = (unit of <= 64 seeds sharing the low byte L, chunk of ec events), handed out by a global atomic
+// to a persistent grid. With one wave per unit over all events, 2^20 seeds make 16,640 units for 8,192 wave
+// slots: a third round of 256 lone waves took ~5 % of the launch. An item writes its seeds' partial stats
+// over [e0, e1) (or the final stats when there is one chunk); k_random_merge combines the chunks in order.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_random_sweep(const uint4 *__restrict__ units,
                                                       const uint32_t *__restrict__ n_units,
                                                       const uint64_t *__restrict__ sorted_h0,
                                                       const uint32_t *__restrict__ sorted_idx,
-                                                      const uint4 *__restrict__ table, uint32_t E,
-                                                      RandomKParams P, nmz_sched_stats *__restrict__ stats) {
-    const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * 256 + threadIdx.x) >> 6);
+                                                      const uint4 *__restrict__ table, uint32_t E, uint32_t ec,
+                                                      uint32_t n_chunks, RandomKParams P,
+                                                      uint32_t *__restrict__ item_counter,
+                                                      nmz_sched_stats *__restrict__ partial, uint64_t part_stride,
+                                                      nmz_sched_stats *__restrict__ stats) {
     const uint32_t lane = threadIdx.x & 63;
-    if (wave >= *n_units) return;
-    const uint4 u = units[wave];
-    const uint32_t L = __builtin_amdgcn_readfirstlane(u.x);
-    const uint32_t start = __builtin_amdgcn_readfirstlane(u.y);
-    const uint32_t cnt = __builtin_amdgcn_readfirstlane(u.z);
-    const bool active = lane < cnt;
-    const uint64_t h0 = active ? sorted_h0[start + lane] : 0;
-    const uint64_t H = h0 * fnv_pow(8);
-    const uint32_t Hm = (uint32_t)(H % gorand::M31);
-    const uint4 *__restrict__ row = table + (uint64_t)L * E;
     uint32_t nm = gorand::NEG_M31;  // -M in a VGPR (see gorand::modmul)
     asm volatile("" : "+v"(nm));
+    const uint32_t n_items = *n_units * n_chunks;
+    for (;;) {
+        uint32_t item = 0;
+        if (lane == 0) item = atomicAdd(item_counter, 1u);
+        item = __builtin_amdgcn_readfirstlane(__shfl(item, 0, 64));
+        if (item >= n_items) break;
+        const uint32_t unit = item / n_chunks, chunk = item - unit * n_chunks;
+        const uint4 u = units[unit];
+        const uint32_t L = __builtin_amdgcn_readfirstlane(u.x);
+        const uint32_t start = __builtin_amdgcn_readfirstlane(u.y);
+        const uint32_t cnt = __builtin_amdgcn_readfirstlane(u.z);
+        const uint32_t e0 = chunk * ec, e1 = min(E, e0 + ec);
+        const bool active = lane < cnt;
+        const uint64_t h0 = active ? sorted_h0[start + lane] : 0;
+        const uint64_t H = h0 * fnv_pow(8);
+        const uint32_t Hm = (uint32_t)(H % gorand::M31);
+        const uint4 *__restrict__ row = table + (uint64_t)L * E;
 
-    uint64_t sum = 0;
-    int64_t best = INT64_MIN;
-    // argmax = first maximum: starting at event 0 with best = INT64_MIN, a strict > reproduces it
-    uint32_t arg = E ? 0u : NMZ_NONE, nf = 0, ff = NMZ_NONE, ovf = 0;
-    for (uint32_t e = 0; e < E; ++e) {
-        // the event index is wave-uniform; without the readfirstlane the compiler keeps it in a VGPR
-        // (divergent rejection loops below) and loads the entry per lane
-        const uint32_t eu = __builtin_amdgcn_readfirstlane(e);
-        const uint4 qv = row[eu];
-        const uint4 q = make_uint4(__builtin_amdgcn_readfirstlane(qv.x), __builtin_amdgcn_readfirstlane(qv.y),
-                                   __builtin_amdgcn_readfirstlane(qv.z), __builtin_amdgcn_readfirstlane(qv.w));
-        const uint32_t cls = q.w;
-        const uint32_t s = go_seed_from_table(H, Hm, q);
-        const Decision d = decide(s, cls, P, nm);
-        sum += (uint64_t)d.delay;
-        if (d.delay > best) {
-            best = d.delay;
-            arg = e;
+        uint64_t sum = 0;
+        int64_t best = INT64_MIN;
+        // argmax = first maximum: starting at the chunk's first event with best = INT64_MIN, a strict >
+        // reproduces it (an empty chunk only when E = 0: argmax NMZ_NONE)
+        uint32_t arg = e0 < e1 ? e0 : NMZ_NONE, nf = 0, ff = NMZ_NONE, ovf = 0;
+        for (uint32_t e = e0; e < e1; ++e) {
+            // the event index is wave-uniform; without the readfirstlane the compiler keeps it in a VGPR
+            // (divergent rejection loops below) and loads the entry per lane
+            const uint32_t eu = __builtin_amdgcn_readfirstlane(e);
+            const uint4 qv = row[eu];
+            const uint4 q = make_uint4(__builtin_amdgcn_readfirstlane(qv.x), __builtin_amdgcn_readfirstlane(qv.y),
+                                       __builtin_amdgcn_readfirstlane(qv.z), __builtin_amdgcn_readfirstlane(qv.w));
+            const uint32_t cls = q.w;
+            const uint32_t s = go_seed_from_table(H, Hm, q);
+            const Decision d = decide(s, cls, P, nm);
+            sum += (uint64_t)d.delay;
+            if (d.delay > best) {
+                best = d.delay;
+                arg = e;
+            }
+            nf += d.fault;
+            ff = (d.fault && ff == NMZ_NONE) ? e : ff;
+            ovf |= d.overflow;
         }
-        nf += d.fault;
-        ff = (d.fault && ff == NMZ_NONE) ? e : ff;
-        ovf |= d.overflow;
-    }
-    if (active) {
         nmz_sched_stats st;
         st.sum_delay_ns = sum;
         st.max_delay_ns = best;
@@ -249,8 +262,40 @@ __global__ __launch_bounds__(256) void k_random_sweep(const uint4 *__restrict__ 
         st.n_fault = nf;
         st.first_fault = ff;
         st.flags = ovf ? NMZ_STAT_RNG_OVERFLOW : 0u;
-        stats[sorted_idx[start + lane]] = st;
+        if (n_chunks == 1) {
+            if (active) stats[sorted_idx[start + lane]] = st;
+        } else {
+            partial[(uint64_t)chunk * part_stride + (uint64_t)unit * 64 + lane] = st;
+        }
     }
+}
+
+// combine the per-chunk partial stats of every seed (in event order) and scatter to the seed's index
+__global__ __launch_bounds__(256) void k_random_merge(const uint4 *__restrict__ units,
+                                                      const uint32_t *__restrict__ n_units,
+                                                      const uint32_t *__restrict__ sorted_idx,
+                                                      const nmz_sched_stats *__restrict__ partial,
+                                                      uint64_t part_stride, uint32_t n_chunks,
+                                                      nmz_sched_stats *__restrict__ stats) {
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t unit = g / 64;
+    const uint32_t j = (uint32_t)(g & 63);
+    if (unit >= *n_units) return;
+    const uint4 u = units[unit];
+    if (j >= u.z) return;
+    nmz_sched_stats st = partial[g];
+    for (uint32_t c = 1; c < n_chunks; ++c) {
+        const nmz_sched_stats p = partial[(uint64_t)c * part_stride + g];
+        st.sum_delay_ns += p.sum_delay_ns;
+        if (p.max_delay_ns > st.max_delay_ns) {
+            st.max_delay_ns = p.max_delay_ns;
+            st.argmax_event = p.argmax_event;
+        }
+        st.n_fault += p.n_fault;
+        if (st.first_fault == NMZ_NONE) st.first_fault = p.first_fault;
+        st.flags |= p.flags;
+    }
+    stats[sorted_idx[u.y + j]] = st;
 }
 
 __global__ __launch_bounds__(256) void k_random_dump(uint64_t seed0, uint64_t n_dump, const uint4 *__restrict__ table,
@@ -282,6 +327,7 @@ struct nmz_random_plan {
     uint64_t max_seeds = 0;
     nmz::DevBuf table_mem;
     nmz::DevBuf seed_scratch;
+    nmz::DevBuf partial;  // per-chunk partial stats per seed slot (n_chunks > 1)
 };
 
 namespace nmz {
@@ -309,12 +355,23 @@ static int make_kparams(const nmz_random_params *p, RandomKParams &kp) {
     return NMZ_OK;
 }
 
-static size_t random_seed_scratch_bytes(uint64_t S) {
-    return Carve::bytes_for(S, 8) * 2 + Carve::bytes_for(S, 4) + Carve::bytes_for(BUCKET_SMALL_U32, 4) +
-           Carve::bytes_for(S / 64 + 257, 16);
+constexpr uint32_t RANDOM_EC = 1024;  // events per work item
+
+static uint32_t random_ec() {
+    static const uint32_t v = [] {
+        const char *e = getenv("NMZ_RANDOM_EC");
+        const uint32_t x = e ? (uint32_t)atoi(e) : RANDOM_EC;
+        return x >= 64 ? x : RANDOM_EC;
+    }();
+    return v;
 }
 
-static Buckets carve_random(void *p, uint64_t S, uint64_t **h0) {
+static size_t random_seed_scratch_bytes(uint64_t S) {
+    return Carve::bytes_for(S, 8) * 2 + Carve::bytes_for(S, 4) + Carve::bytes_for(BUCKET_SMALL_U32, 4) +
+           Carve::bytes_for(S / 64 + 257, 16) + Carve::bytes_for(4, 4);
+}
+
+static Buckets carve_random(void *p, uint64_t S, uint64_t **h0, uint32_t **counter) {
     Carve cv(p);
     *h0 = cv.take<uint64_t>(S);
     Buckets b;
@@ -322,6 +379,7 @@ static Buckets carve_random(void *p, uint64_t S, uint64_t **h0) {
     b.sorted_idx = cv.take<uint32_t>(S);
     buckets_small(cv.take<uint32_t>(BUCKET_SMALL_U32), b);
     b.units = cv.take<uint4>(S / 64 + 257);
+    *counter = cv.take<uint32_t>(4);
     return b;
 }
 
@@ -343,6 +401,7 @@ static int random_plan_create(nmz_ctx *ctx, const uint64_t *evhash, const uint8_
     auto cleanup = [&](int code) {
         p->table_mem.release();
         p->seed_scratch.release();
+        p->partial.release();
         delete p;
         return code;
     };
@@ -351,7 +410,8 @@ static int random_plan_create(nmz_ctx *ctx, const uint64_t *evhash, const uint8_
     if (rc == NMZ_OK) rc = p->seed_scratch.ensure(random_seed_scratch_bytes(max_seeds));
     if (rc == NMZ_OK) {  // bucket counters start at zero (k_bucket_scan re-zeroes them)
         uint64_t *h0_unused;
-        Buckets b0 = carve_random(p->seed_scratch.ptr, max_seeds, &h0_unused);
+        uint32_t *counter_unused;
+        Buckets b0 = carve_random(p->seed_scratch.ptr, max_seeds, &h0_unused, &counter_unused);
         if (hipMemsetAsync(b0.count, 0, 256 * BUCKET_STRIDE * sizeof(uint32_t), ctx->stream) != hipSuccess)
             rc = fail(NMZ_EHIP, "hipMemsetAsync of the seed scratch failed");
     }
@@ -377,14 +437,29 @@ static int random_run(nmz_random_plan *p, hipStream_t st, uint64_t seed0, uint64
     NMZ_CHECK(S <= p->max_seeds, "more seeds than the plan was created for");
     const uint32_t E = p->n_events;
     uint64_t *d_h0;
-    Buckets b = carve_random(p->seed_scratch.ptr, p->max_seeds, &d_h0);
+    uint32_t *d_counter;
+    Buckets b = carve_random(p->seed_scratch.ptr, p->max_seeds, &d_h0, &d_counter);
     hipLaunchKernelGGL(k_random_prefix, dim3(ceil_div(S, 256 * prefix_per_thread())), dim3(256), 0, st, seed0, S, d_h0,
                        b.count, prefix_per_thread());
     const uint64_t max_units = S / 64 + 256;
-    NMZ_TRY(bucket_seeds_counted(st, d_h0, S, 64, b));
-    KernelTimer kt(p->ctx, st, "random_sweep");
-    hipLaunchKernelGGL(k_random_sweep, dim3(ceil_div(max_units, 4)), dim3(256), 0, st, b.units, b.n_units,
-                       b.sorted_h0, b.sorted_idx, p->d_table, E, p->kp, d_stats);
+    NMZ_TRY(bucket_seeds_counted(st, d_h0, S, 64, b, d_counter));
+    const uint32_t ec = random_ec();
+    const uint32_t n_chunks = std::max<uint32_t>(1, (E + ec - 1) / ec);
+    const uint64_t stride = (p->max_seeds / 64 + 257) * 64;
+    nmz_sched_stats *part = nullptr;
+    if (n_chunks > 1) {
+        NMZ_TRY(p->partial.ensure(Carve::bytes_for(stride * n_chunks, sizeof(nmz_sched_stats))));
+        part = p->partial.as<nmz_sched_stats>();
+    }
+    const unsigned grid = (unsigned)std::min<uint64_t>(p->ctx->n_cu * 8ull, ceil_div(max_units * n_chunks, 4));
+    {
+        KernelTimer kt(p->ctx, st, "random_sweep");
+        hipLaunchKernelGGL(k_random_sweep, dim3(grid), dim3(256), 0, st, b.units, b.n_units, b.sorted_h0,
+                           b.sorted_idx, p->d_table, E, ec, n_chunks, p->kp, d_counter, part, stride, d_stats);
+    }
+    if (n_chunks > 1)
+        hipLaunchKernelGGL(k_random_merge, dim3(ceil_div(max_units * 64, 256)), dim3(256), 0, st, b.units,
+                           b.n_units, b.sorted_idx, part, stride, n_chunks, d_stats);
     NMZ_HIP(hipGetLastError());
     return NMZ_OK;
 }
@@ -410,6 +485,7 @@ int nmz_random_plan_destroy(nmz_random_plan *plan) {
         CtxGuard g(plan->ctx);
         plan->table_mem.release();
         plan->seed_scratch.release();
+        plan->partial.release();
     }
     delete plan;
     return NMZ_OK;
@@ -439,6 +515,7 @@ int nmz_random_sweep(nmz_ctx *ctx, uint64_t seed0, uint64_t n_seeds, const uint6
         ~PlanGuard() {
             p->table_mem.release();
             p->seed_scratch.release();
+            p->partial.release();
             delete p;
         }
     } pg{plan};

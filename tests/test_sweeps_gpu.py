@@ -253,6 +253,24 @@ def test_random_edge_cases(ctx):
     assert np.array_equal(r.stats, st)
 
 
+@pytest.mark.parametrize("E,mn,mx,p", [(3000, 30_000_000, 100_000_000, 0.001), (2048, 5_000_000, 5_000_000, 0.002),
+                                        (1025, 0, 1 << 20, 0.0), (4100, 7, 9, 0.0015)])
+def test_random_event_chunks(ctx, E, mn, mx, p):
+    """Traces longer than one work item (1,024 events): per-chunk partial stats merged in event order.
+    Rare faults put first_fault in later chunks; fixed or 2-valued delays make argmax ties across chunks."""
+    eh = RNG.integers(0, 2**64, size=E, dtype=np.uint64)
+    ec = RNG.integers(0, 4, size=E, dtype=np.uint8)
+    rp = Random()
+    rp.MinInterval, rp.MaxInterval, rp.FaultActionProbability = mn, mx, p
+    seed0 = int(RNG.integers(0, 2**63))
+    r = rp.Sweep(seed0, 1500, eh, ec, k=16, ctx=ctx)
+    st, _, _ = O.random_sweep(seed0, 1500, eh, ec, O.random_params(mn, mx, p))
+    assert np.array_equal(r.stats, st)
+    assert np.array_equal(r.topk, O.topk_from_stats(st, seed0, 16))
+    if p:
+        assert (st["first_fault"][st["n_fault"] > 0] >= 1024).any()
+
+
 def test_random_config4_scale_sampled(ctx):
     """configs[3] shape (16 entities, 10k events, p=0.1) at 2^18 seeds: sampled parity."""
     E, S = 10_000, 1 << 18
