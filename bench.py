@@ -392,6 +392,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     ap.add_argument("--no-secondary", dest="secondary", action="store_false")
     args = ap.parse_args()
+    # The JSON line is the only output on stdout: whatever the libraries write to fd 1 during the run
+    # (gloo's connection messages, HIP/RCCL diagnostics) goes to stderr instead.
+    sys.stdout.flush()
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
 
     import torch
     D = Dist()
@@ -442,7 +447,7 @@ def main():
                              bench_ed_secondary(args, torch, D, ctx, L, stream, ed3),
                              bench_ed_secondary(args, torch, D, ctx, L, stream, ed5)]
     if D.rank == 0:
-        print(json.dumps(line), flush=True)
+        os.write(out_fd, (json.dumps(line) + "\n").encode())
     ctx.close()
     if D.pg:
         D.pg.destroy_process_group()
