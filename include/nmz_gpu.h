@@ -135,7 +135,10 @@ int nmz_replayable_sweep(nmz_ctx *ctx, const uint32_t *seed_off, const uint8_t *
                          nmz_topk_entry *topk);
 
 /* Device-resident variant (all pointers are device pointers; hipStream_t as void*).
- * Requires a prior nmz_replayable_plan() for the same hint table. */
+ * The plan holds the per-event tables of one hint table and the scratch of one sweep
+ * for up to max_seeds seeds. Sweeps through one plan must be ordered (one stream at a
+ * time); concurrent sweeps on several streams take one plan each (bench.py pipelines
+ * three). */
 typedef struct nmz_replayable_plan nmz_replayable_plan;
 int nmz_replayable_plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hint_bytes,
                                uint32_t n_events, int64_t max_interval_ns,
@@ -169,7 +172,8 @@ int nmz_random_sweep(nmz_ctx *ctx, uint64_t seed0, uint64_t n_seeds, const uint6
                      uint64_t n_dump_seeds, uint32_t k, nmz_topk_entry *topk);
 
 /* Device-resident variant: per-event tables are built once in the plan; the
- * sweep enqueues on `stream` and writes d_stats[n_seeds] (device memory). */
+ * sweep enqueues on `stream` and writes d_stats[n_seeds] (device memory). As for
+ * replayable plans, one plan serves one stream at a time. */
 typedef struct nmz_random_plan nmz_random_plan;
 int nmz_random_plan_create(nmz_ctx *ctx, const uint64_t *evhash, const uint8_t *evclass,
                            uint32_t n_events, const nmz_random_params *params, uint64_t max_seeds,
