@@ -123,6 +123,7 @@ struct ModParams {
     uint32_t m32;
     uint32_t k64;   // 2^64 mod m (FAST only)
     uint32_t m_k64; // (m - k64) mod m, added when the 64-bit add carried
+    uint64_t mu;    // floor(2^64 / m) for mod_barrett_small (FAST only; 2^64 - 1 for m = 1)
     int kind;
 };
 
@@ -137,10 +138,25 @@ inline ModParams make_mod(uint64_t m) {
         uint64_t k = (uint64_t)(((unsigned __int128)1 << 64) % m);
         p.k64 = (uint32_t)k;
         p.m_k64 = (uint32_t)((m - k) % m);
+        p.mu = m == 1 ? ~0ULL : (uint64_t)(((unsigned __int128)1 << 64) / m);
     } else {
         p.kind = MOD_GENERAL;
     }
     return p;
+}
+
+// v mod m for any 64-bit v and m < 2^31, mu = floor(2^64 / m) (2^64 - 1 for m = 1): q = floor(v * mu / 2^64)
+// is floor(v / m) or one less, so r = v - q*m < 2m < 2^32 and only the low words are needed:
+// r = v_lo - q_lo * m (mod 2^32), with v*mu = vl*mul + (vh*mul + vl*muh) 2^32 + vh*muh 2^64.
+__device__ __forceinline__ uint32_t mod_barrett_small(uint64_t v, uint32_t m, uint64_t mu) {
+    const uint32_t vl = (uint32_t)v, vh = (uint32_t)(v >> 32);
+    const uint32_t mul = (uint32_t)mu, muh = (uint32_t)(mu >> 32);
+    const uint64_t a = (uint64_t)vh * mul + __umulhi(vl, mul);
+    const uint64_t b = (uint64_t)vl * muh + (uint32_t)a;
+    const uint32_t ql = vh * muh + (uint32_t)(a >> 32) + (uint32_t)(b >> 32);
+    const uint32_t r = vl - ql * m;
+    uint32_t t;
+    return __builtin_sub_overflow(r, m, &t) ? r : t;
 }
 
 // Reduce s in [0, 3m) to [0, m) for m < 2^30 with two branch-free min steps.

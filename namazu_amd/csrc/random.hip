@@ -71,20 +71,6 @@ __device__ __forceinline__ uint64_t mod_barrett(uint64_t v, uint64_t n, uint64_t
     return r >= n ? r - n : r;
 }
 
-// Same for n < 2^31: r = v - q*n < 2n < 2^32, so only the low word of q = floor(v*mu / 2^64) is needed and
-// r = v_lo - q_lo*n (mod 2^32). With v*mu = X + (vh*mul + vl*muh)*2^32 + vh*muh*2^64 (X = vl*mul):
-// a = vh*mul + hi(X), b = vl*muh + lo(a), q = vh*muh + hi(a) + hi(b).
-__device__ __forceinline__ uint32_t mod_barrett31(uint64_t v, uint32_t n, uint64_t mu) {
-    const uint32_t vl = (uint32_t)v, vh = (uint32_t)(v >> 32);
-    const uint32_t mul = (uint32_t)mu, muh = (uint32_t)(mu >> 32);
-    const uint64_t a = (uint64_t)vh * mul + __umulhi(vl, mul);
-    const uint64_t b = (uint64_t)vl * muh + (uint32_t)a;
-    const uint32_t ql = vh * muh + (uint32_t)(a >> 32) + (uint32_t)(b >> 32);
-    const uint32_t r = vl - ql * n;
-    uint32_t t;
-    return __builtin_sub_overflow(r, n, &t) ? r : t;
-}
-
 struct Decision {
     int64_t delay;
     uint32_t fault;
@@ -108,7 +94,7 @@ __device__ __forceinline__ Decision decide(uint32_t s, uint32_t cls, const Rando
                 }
                 v = go_output(s, t++) & MASK63;
             }
-            d.delay = (cp.n >> 31) == 0 ? (int64_t)mod_barrett31(v, (uint32_t)cp.n, cp.mu) + cp.min
+            d.delay = (cp.n >> 31) == 0 ? (int64_t)mod_barrett_small(v, (uint32_t)cp.n, cp.mu) + cp.min
                                         : (int64_t)mod_barrett(v, cp.n, cp.mu) + cp.min;
         } else {
             d.delay = (int64_t)(v & (cp.n - 1)) + cp.min;

@@ -297,7 +297,7 @@ template <int U, int KM>  // KM: 0 = u64 compare chain, 1 = f64 max
 __global__ __launch_bounds__(256) void k_replayable_sweep_fast(
     const uint4 *__restrict__ units, const uint32_t *__restrict__ n_units,
     const uint64_t *__restrict__ sorted_h0, const uint4 *__restrict__ table, uint32_t E,
-    const ClassInfo *__restrict__ classes, uint32_t n_classes, uint64_t m, uint32_t m_k64, uint32_t ec,
+    const ClassInfo *__restrict__ classes, uint32_t n_classes, uint64_t m, uint64_t m_mu, uint32_t m_k64, uint32_t ec,
     uint32_t n_chunks, uint32_t fold_mask, uint32_t *__restrict__ item_counter, uint4 *__restrict__ partial,
     uint64_t part_stride) {
     // per-wave double-buffered staging of 64 table entries in LDS: one
@@ -357,7 +357,7 @@ __global__ __launch_bounds__(256) void k_replayable_sweep_fast(
 #pragma unroll
                 for (int r = 0; r < U; ++r) {
                     const uint64_t H = h0[r] * ci.pn;
-                    Hm[r] = (uint32_t)(H % m);
+                    Hm[r] = mod_barrett_small(H, m32, m_mu);
                     const uint32_t t2 = Hm[r] + m_k64;
                     Hm2[r] = min(t2, t2 - m32);
                     // carry(H + C) <=> C > ~H <=> position >= pos + count(C <= ~H)
@@ -660,7 +660,7 @@ static int replayable_stats(nmz_replayable_plan *p, hipStream_t st, const uint32
             KernelTimer kt(p->ctx, st, "replayable_sweep");
 #define NMZ_K1(UU)                                                                                                   \
     hipLaunchKernelGGL((replay_key_mode() == 1 ? k_replayable_sweep_fast<UU, 1> : k_replayable_sweep_fast<UU, 0>), dim3(grid), dim3(256), 0, st, sc.b.units, sc.b.n_units,          \
-                       sc.b.sorted_h0, p->d_table, E, p->d_classes, p->n_classes, p->mod.m, p->mod.m_k64, ec,        \
+                       sc.b.sorted_h0, p->d_table, E, p->d_classes, p->n_classes, p->mod.m, p->mod.mu, p->mod.m_k64, ec,        \
                        n_chunks, fold_mask, sc.counter, p->partial.as<uint4>(), stride)
             if (U == 2) NMZ_K1(2); else if (U == 8) NMZ_K1(8); else NMZ_K1(4);
 #undef NMZ_K1
