@@ -286,6 +286,9 @@ __device__ __forceinline__ uint32_t count_le(const uint4 *__restrict__ row, uint
     return k;
 }
 
+// seed r's {~e, C mod m} pair from a 16-B staged read holding seeds 2k, 2k+1
+__device__ __forceinline__ uint2 half_of(uint4 v, int hi) { return hi ? make_uint2(v.z, v.w) : make_uint2(v.x, v.y); }
+
 constexpr uint32_t POS_BIAS = 0x40000000u;  // keeps d = BIAS + k - i positive
 
 // Work item = (seed group of <= 64*U seeds sharing the low byte L, chunk of
@@ -305,8 +308,9 @@ __global__ __launch_bounds__(256) void k_replayable_sweep_fast(
     // one is consumed through broadcast LDS reads. An event's slot holds
     // {~e, C mod m} x U: every seed r reads its own pair, and the decision
     // overwrites C mod m with t, leaving the f64 key pair {~e, t} in place.
+    static_assert(U % 2 == 0, "staged reads take seeds in pairs");
     constexpr int STR = 2 * U;
-    __shared__ uint32_t stage[4][2][64 * STR];
+    __shared__ __attribute__((aligned(16))) uint32_t stage[4][2][64 * STR];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t m32 = (uint32_t)m;
@@ -395,11 +399,22 @@ __global__ __launch_bounds__(256) void k_replayable_sweep_fast(
             for (int r = 0; r < U; ++r) part[r] = 0;
             for (uint32_t i = 0, g = 1; i < n4; i += 4, ++g) {
                 double kk[U][4];
+                // the 4 events' slots as 16-B reads (ds_read_b128: one LDS pass per 4 lane groups,
+                // half the LDS cycles of the ds_read2_b64 pairs that 8-B reads compile to)
+                uint4 qv[U / 2][4];
+                if constexpr (KM == 1) {
+#pragma unroll
+                    for (int rr = 0; rr < U / 2; ++rr)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            qv[rr][j] = *reinterpret_cast<const uint4 *>(sq + (i + j) * STR + 4 * rr);
+                }
 #pragma unroll
                 for (int r = 0; r < U; ++r) {
                     const uint2 *__restrict__ qr = reinterpret_cast<const uint2 *>(sq + i * STR + 2 * r);
                     if constexpr (KM == 1) {
-                        const uint2 q0 = qr[0], q1 = qr[U], q2 = qr[2 * U], q3 = qr[3 * U];
+                        const uint2 q0 = half_of(qv[r / 2][0], r & 1), q1 = half_of(qv[r / 2][1], r & 1);
+                        const uint2 q2 = half_of(qv[r / 2][2], r & 1), q3 = half_of(qv[r / 2][3], r & 1);
                         uint32_t x0 = q0.y, x1 = q1.y, x2 = q2.y, x3 = q3.y;
                         decide4(T0, T1, T2, T3, d[r], Hm[r], Hm2[r], mv, x0, x1, x2, x3, part[r]);
                         kk[r][0] = __builtin_bit_cast(double, ((uint64_t)x0 << 32) | q0.x);
