@@ -78,10 +78,11 @@ struct Decision {
 };
 
 // One decision given the reduced Go seed s (1 <= s < 2^31-1) and uniform class bits.
-__device__ __forceinline__ Decision decide(uint32_t s, uint32_t cls, const RandomKParams &P,
+// cp = P.cls[cls & NMZ_EV_PRIORITIZED], selected by the caller (the sweep keeps both classes in SGPRs
+// instead of indexing the kernel-argument struct, which costs a scalar load and wait per event)
+__device__ __forceinline__ Decision decide(uint32_t s, uint32_t cls, const ClassParams &cp, int32_t fault_threshold,
                                            uint32_t nm = gorand::NEG_M31) {
     Decision d{0, 0, 0};
-    const ClassParams &cp = P.cls[cls & NMZ_EV_PRIORITIZED];
     int t = 0;
     if (cp.n) {
         uint64_t v = gorand::out0(s, nm) & MASK63;
@@ -110,8 +111,8 @@ __device__ __forceinline__ Decision decide(uint32_t s, uint32_t cls, const Rando
             // then are the low words (two more modmuls) computed.
             const uint32_t v0 = (gorand::vec_hi<332>(s, nm) + gorand::vec_hi<605>(s, nm)) & 0x7fffffffu;
             const uint32_t r0 = v0 % INTN_N;
-            if (!(v0 >= INT31N_MAX || r0 == INTN_N - 1 || r0 + 1 == (uint32_t)P.fault_threshold)) {
-                d.fault = ((int32_t)r0 < P.fault_threshold) ? 1u : 0u;
+            if (!(v0 >= INT31N_MAX || r0 == INTN_N - 1 || r0 + 1 == (uint32_t)fault_threshold)) {
+                d.fault = ((int32_t)r0 < fault_threshold) ? 1u : 0u;
                 return d;
             }
         }
@@ -125,9 +126,14 @@ __device__ __forceinline__ Decision decide(uint32_t s, uint32_t cls, const Rando
             }
             v = (uint32_t)(go_output(s, t++) >> 32) & 0x7fffffffu;
         }
-        d.fault = ((int32_t)(v % INTN_N) < P.fault_threshold) ? 1u : 0u;
+        d.fault = ((int32_t)(v % INTN_N) < fault_threshold) ? 1u : 0u;
     }
     return d;
+}
+
+__device__ __forceinline__ uint4 uniform4(uint4 v) {
+    return make_uint4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
+                      __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
 }
 
 // Go seed for (prefix state h0 -> H = h0 * P^8, its residue Hm = H mod M31) and
@@ -200,6 +206,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     uint32_t nm = gorand::NEG_M31;  // -M in a VGPR (see gorand::modmul)
     asm volatile("" : "+v"(nm));
     const uint32_t n_items = *n_units * n_chunks;
+    const ClassParams c0 = P.cls[0], c1 = P.cls[1];
     for (;;) {
         uint32_t item = 0;
         if (lane == 0) item = atomicAdd(item_counter, 1u);
@@ -222,16 +229,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         // argmax = first maximum: starting at the chunk's first event with best = INT64_MIN, a strict >
         // reproduces it (an empty chunk only when E = 0: argmax NMZ_NONE)
         uint32_t arg = e0 < e1 ? e0 : NMZ_NONE, nf = 0, ff = NMZ_NONE, ovf = 0;
+        // the event index is wave-uniform; without the readfirstlane the compiler keeps it in a VGPR
+        // (divergent rejection loops below) and loads the entry per lane. The next event's entry is
+        // loaded one decision ahead, so its scalar-load latency hides behind the current decision.
+        uint4 qn = e0 < e1 ? uniform4(row[__builtin_amdgcn_readfirstlane(e0)]) : make_uint4(0, 0, 0, 0);
         for (uint32_t e = e0; e < e1; ++e) {
-            // the event index is wave-uniform; without the readfirstlane the compiler keeps it in a VGPR
-            // (divergent rejection loops below) and loads the entry per lane
-            const uint32_t eu = __builtin_amdgcn_readfirstlane(e);
-            const uint4 qv = row[eu];
-            const uint4 q = make_uint4(__builtin_amdgcn_readfirstlane(qv.x), __builtin_amdgcn_readfirstlane(qv.y),
-                                       __builtin_amdgcn_readfirstlane(qv.z), __builtin_amdgcn_readfirstlane(qv.w));
+            const uint4 q = qn;
+            const uint32_t en = __builtin_amdgcn_readfirstlane(min(e + 1, e1 - 1));
+            qn = uniform4(row[en]);
             const uint32_t cls = q.w;
             const uint32_t s = go_seed_from_table(H, Hm, q);
-            const Decision d = decide(s, cls, P, nm);
+            const Decision d = decide(s, cls, (cls & NMZ_EV_PRIORITIZED) ? c1 : c0, P.fault_threshold, nm);
             sum += (uint64_t)d.delay;
             if (d.delay > best) {
                 best = d.delay;
@@ -297,7 +305,7 @@ __global__ __launch_bounds__(256) void k_random_dump(uint64_t seed0, uint64_t n_
     // direct form: int64 seed, Go's reduction, no residue shortcut
     const uint64_t u = H + (((uint64_t)q.y << 32) | q.x);
     const uint32_t s = gorand::seed_reduce((int64_t)u);
-    const Decision d = decide(s, q.w, P);
+    const Decision d = decide(s, q.w, P.cls[q.w & NMZ_EV_PRIORITIZED], P.fault_threshold);
     delays[idx] = d.delay;
     faults[idx] = (uint8_t)d.fault;
     if (d.overflow) atomicOr(overflow, 1u);
