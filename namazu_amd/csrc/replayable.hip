@@ -387,7 +387,10 @@ __global__ __launch_bounds__(256) void k_replayable_sweep_fast(
                 nhi = min(e1, nci.start + nci.count);
                 nfresh = true;
             }
-            if (npos < e1) pre = (npos + lane < nhi) ? row[npos + lane] : make_uint4(0, 0, 0, 0);
+            // unconditional and clamped to the row: a guarded load became a divergent block whose result
+            // the compiler waited for (s_waitcnt vmcnt(0)) right after issuing it. Slots past the chunk's
+            // n events are never read, so the clamped lanes' values do not matter.
+            pre = row[min(npos + lane, E - 1)];
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
