@@ -33,7 +33,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
-PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 78.6 T int32 lane-ops/s (2 cyc/wave64 instr/SIMD)
+PEAK_CLOCK_GHZ = 2.4  # MI355X peak engine clock
+PEAK_VALU_TOPS = 256 * 4 * 32 * PEAK_CLOCK_GHZ * 1e9 / 1e12  # 78.6 T int32 lane-ops/s (2 cyc/wave64 instr/SIMD)
 PEAK_HBM_GBS = 8000.0
 MAX_INTERVAL_NS = 100_000_000
 # VALU lane-instructions per unit (decision / trace pair) of each dominant kernel, measured by rocprofv3
@@ -63,7 +64,12 @@ def roofline_valu(kernel, units, kernel_ms):
     return {"bound": "valu", "achieved": achieved, "peak": PEAK_VALU_TOPS, "unit": "Tops/s",
             "frac": achieved / PEAK_VALU_TOPS, "traffic": traffic, "traffic_unit": "bytes/launch (2 x FETCH_SIZE + WRITE_SIZE)",
             "kernel": kernel, "kernel_ms": kernel_ms, "ops_per_unit": e["ops_per_unit"], "units_per_launch": units,
-            "ops_source": e["source"]}
+            "ops_source": e["source"],
+            # the same lane-ops against the issue ceiling at the engine clock the chip held during this
+            # kernel's profile (GRBM_GUI_ACTIVE / duration), not the 2.4 GHz peak clock
+            "clock_ghz": e.get("clock_ghz"),
+            "frac_at_clock": (achieved / (PEAK_VALU_TOPS * e["clock_ghz"] / PEAK_CLOCK_GHZ)
+                              if e.get("clock_ghz") else None)}
 
 
 def splitmix64(state, n):

@@ -27,7 +27,8 @@ def main():
                 key = pre.split("::")[1].split("<")[0]
                 out[key] = {"ops_per_unit": e["SQ_INSTS_VALU"] * 64 / n, "unit": unit, "units_per_launch": n,
                             "kernel": name, "source": f"SQ_INSTS_VALU per launch, profiles/{tag}_summary.json",
-                            "hbm_bytes_per_launch": e.get("hbm_bytes_fetch_x2")}
+                            "hbm_bytes_per_launch": e.get("hbm_bytes_fetch_x2"),
+                            "clock_ghz": e.get("clock_ghz")}
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "valu_per_unit.json")
     json.dump(out, open(path, "w"), indent=1, sort_keys=True)
     for k, v in out.items():
