@@ -63,6 +63,20 @@ def test_replayable_many_length_classes_and_ties(ctx):
         assert np.array_equal(r.stats, st)
 
 
+@pytest.mark.parametrize("E", [1, 3, 63, 64, 65, 127, 2047, 2048, 2049, 4097])
+def test_replayable_event_counts_around_stage_and_chunk_edges(ctx, E):
+    """K1 stages 64 events at a time (the next chunk's load is clamped to the last event) and works in
+    2,048-event items: trace lengths on either side of both edges, vs the oracle."""
+    rng = np.random.default_rng(E)
+    hints = zk_hints(E, rng)
+    seeds = [str(i) for i in range(260)]
+    p = Replayable()
+    p.MaxInterval = 100_000_000
+    r = p.Sweep(seeds, hints, n_dump=3, ctx=ctx)
+    st, dl = rep_oracle(seeds, hints, 100_000_000, n_dump=3)
+    assert np.array_equal(r.stats, st) and np.array_equal(r.delays, dl)
+
+
 def test_replayable_empty_inputs(ctx):
     p = Replayable()
     p.MaxInterval = 10_000_000
