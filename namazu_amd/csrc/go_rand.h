@@ -60,6 +60,15 @@ __device__ __forceinline__ uint32_t modmul(uint32_t a, uint32_t b, uint32_t nm =
     return borrow ? r : t;
 }
 
+// (a * b mod (2^31 - 1)) << 8 for a, b in [1, 2^31 - 1): only the low 24 bits of the residue survive the shift.
+// r = Q + R (as in modmul) is never M, because a * b is not 0 mod the prime M; so the residue is r when r < 2^31
+// and r - M = r + 1 - 2^31 otherwise, and its low 24 bits are those of r + (r >> 31). No compare, no select.
+__device__ __forceinline__ uint32_t modmul_shl8(uint32_t a, uint32_t b) {
+    const uint64_t p = (uint64_t)a * (2u * b);
+    const uint32_t r = (uint32_t)(p >> 32) + ((uint32_t)p >> 1);
+    return (r + (r >> 31)) << 8;
+}
+
 // Go's `seed % int32max; if seed < 0 { seed += int32max }; if seed == 0 { seed = 89482311 }`
 __host__ __device__ inline uint32_t seed_reduce(int64_t seed) {
     int64_t s = seed % (int64_t)M31;
@@ -73,9 +82,9 @@ template <int I>
 __device__ __forceinline__ uint64_t vec_c(uint32_t s, uint32_t nm = NEG_M31) {
     constexpr uint32_t ca = pow_a(21 + 3 * I), cb = pow_a(22 + 3 * I), cc = pow_a(23 + 3 * I);
     constexpr uint64_t ck = NMZ_GO_RNG_COOKED[I];
-    const uint32_t xa = modmul(s, ca, nm), xb = modmul(s, cb, nm), xc = modmul(s, cc, nm);
+    const uint32_t xb = modmul(s, cb, nm), xc = modmul(s, cc, nm);
     const uint32_t lo = (xb << 20) ^ xc ^ (uint32_t)ck;
-    const uint32_t hi = (xa << 8) ^ (xb >> 12) ^ (uint32_t)(ck >> 32);
+    const uint32_t hi = modmul_shl8(s, ca) ^ (xb >> 12) ^ (uint32_t)(ck >> 32);
     return ((uint64_t)hi << 32) | lo;
 }
 
@@ -84,7 +93,7 @@ template <int I>
 __device__ __forceinline__ uint32_t vec_hi(uint32_t s, uint32_t nm = NEG_M31) {
     constexpr uint32_t ca = pow_a(21 + 3 * I), cb = pow_a(22 + 3 * I);
     constexpr uint64_t ck = NMZ_GO_RNG_COOKED[I];
-    return (modmul(s, ca, nm) << 8) ^ (modmul(s, cb, nm) >> 12) ^ (uint32_t)(ck >> 32);
+    return modmul_shl8(s, ca) ^ (modmul(s, cb, nm) >> 12) ^ (uint32_t)(ck >> 32);
 }
 
 // outputs 0 and 1 after Seed (no state)
