@@ -193,6 +193,11 @@ __global__ __launch_bounds__(256) void k_random_prefix(uint64_t seed0, uint64_t 
 // to a persistent grid. With one wave per unit over all events, 2^20 seeds make 16,640 units for 8,192 wave
 // slots: a third round of 256 lone waves took ~5 % of the launch. An item writes its seeds' partial stats
 // over [e0, e1) (or the final stats when there is one chunk); k_random_merge combines the chunks in order.
+// K32: every delay of both classes lies in [0, 0x7ff00000) ns (host-checked, random_k32), so the running maximum
+// is kept as K1 keeps it: the bit pattern of an f64 {lo = ~e, hi = delay}, a non-negative finite double (f64
+// denormals are preserved) whose order is (delay, then smaller e) -- the first maximum -- and is updated by one
+// v_max_f64 instead of a signed 64-bit compare and three selects; the delay's high word is never formed.
+template <bool K32>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_random_sweep(const uint4 *__restrict__ units,
                                                       const uint32_t *__restrict__ n_units,
                                                       const uint64_t *__restrict__ sorted_h0,
@@ -229,6 +234,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         // argmax = first maximum: starting at the chunk's first event with best = INT64_MIN, a strict >
         // reproduces it (an empty chunk only when E = 0: argmax NMZ_NONE)
         uint32_t arg = e0 < e1 ? e0 : NMZ_NONE, nf = 0, ff = NMZ_NONE, ovf = 0;
+        double kmax = 0.0;  // K32: below every real key ({~e, delay} with ~e > 0)
         // the event index is wave-uniform; without the readfirstlane the compiler keeps it in a VGPR
         // (divergent rejection loops below) and loads the entry per lane. The next event's entry is
         // loaded one decision ahead, so its scalar-load latency hides behind the current decision.
@@ -240,14 +246,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
             const uint32_t cls = q.w;
             const uint32_t s = go_seed_from_table(H, Hm, q);
             const Decision d = decide(s, cls, (cls & NMZ_EV_PRIORITIZED) ? c1 : c0, P.fault_threshold, nm);
-            sum += (uint64_t)d.delay;
-            if (d.delay > best) {
-                best = d.delay;
-                arg = e;
+            if constexpr (K32) {
+                const uint32_t d32 = (uint32_t)d.delay;
+                sum += d32;
+                const double key = __builtin_bit_cast(double, ((uint64_t)d32 << 32) | (uint32_t)~e);
+                asm("v_max_f64 %0, %0, %1" : "+v"(kmax) : "v"(key));
+            } else {
+                sum += (uint64_t)d.delay;
+                if (d.delay > best) {
+                    best = d.delay;
+                    arg = e;
+                }
             }
             nf += d.fault;
             ff = (d.fault && ff == NMZ_NONE) ? e : ff;
             ovf |= d.overflow;
+        }
+        if constexpr (K32) {
+            if (e0 < e1) {
+                const uint64_t kb = __builtin_bit_cast(uint64_t, kmax);
+                best = (int64_t)(kb >> 32);
+                arg = ~(uint32_t)kb;
+            }
         }
         nmz_sched_stats st;
         st.sum_delay_ns = sum;
@@ -262,6 +282,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
             partial[(uint64_t)chunk * part_stride + (uint64_t)unit * 64 + lane] = st;
         }
     }
+}
+
+// Whether k_random_sweep<true> applies: every delay min + [0, max(n, 1)) of both classes in [0, 0x7ff00000),
+// and fewer than 2^32 - 1 events per chunk (~e > 0). NMZ_RANDOM_K32=0 forces the general form.
+static bool random_k32(const RandomKParams &kp) {
+    static const int env = [] {
+        const char *e = getenv("NMZ_RANDOM_K32");
+        return e ? atoi(e) : 1;
+    }();
+    if (!env) return false;
+    for (const ClassParams &c : kp.cls) {
+        const uint64_t span = c.n ? c.n : 1;
+        if (c.min < 0 || (uint64_t)c.min + span > 0x7ff00000ull) return false;
+    }
+    return true;
 }
 
 // combine the per-chunk partial stats of every seed (in event order) and scatter to the seed's index
@@ -448,8 +483,13 @@ static int random_run(nmz_random_plan *p, hipStream_t st, uint64_t seed0, uint64
     const unsigned grid = (unsigned)std::min<uint64_t>(p->ctx->n_cu * 8ull, ceil_div(max_units * n_chunks, 4));
     {
         KernelTimer kt(p->ctx, st, "random_sweep");
-        hipLaunchKernelGGL(k_random_sweep, dim3(grid), dim3(256), 0, st, b.units, b.n_units, b.sorted_h0,
-                           b.sorted_idx, p->d_table, E, ec, n_chunks, p->kp, d_counter, part, stride, d_stats);
+        if (random_k32(p->kp))
+            hipLaunchKernelGGL(k_random_sweep<true>, dim3(grid), dim3(256), 0, st, b.units, b.n_units, b.sorted_h0,
+                               b.sorted_idx, p->d_table, E, ec, n_chunks, p->kp, d_counter, part, stride, d_stats);
+        else
+            hipLaunchKernelGGL(k_random_sweep<false>, dim3(grid), dim3(256), 0, st, b.units, b.n_units,
+                               b.sorted_h0, b.sorted_idx, p->d_table, E, ec, n_chunks, p->kp, d_counter, part,
+                               stride, d_stats);
     }
     if (n_chunks > 1)
         hipLaunchKernelGGL(k_random_merge, dim3(ceil_div(max_units * 64, 256)), dim3(256), 0, st, b.units,

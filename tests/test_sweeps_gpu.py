@@ -202,7 +202,9 @@ def test_replayable_sweep_topk_dev_matches_separate_selection(ctx, m, S, E, k, s
 # ---------------------------------------------------------------- K2
 PARAMS = [(30_000_000, 100_000_000, 0.1), (5_000_000, 5_000_000, 0.5), (0, 1 << 20, 1.0),
           (80_000_000, 3_000_000_000, 0.999), (0, 0, 0.0), (-5_000_000, 5_000_000, 0.3), (7, 9, 0.25),
-          (1, 1 + (1 << 40), 0.05), (0, (1 << 31) - 1, 0.2), (0, (1 << 31) + 1, 0.2), (3, 3 + (1 << 31), 0.7)]
+          (1, 1 + (1 << 40), 0.05), (0, (1 << 31) - 1, 0.2), (0, (1 << 31) + 1, 0.2), (3, 3 + (1 << 31), 0.7),
+          # the edge of k_random_sweep's 32-bit f64-key form (every delay < 0x7ff00000) and one past it
+          (0, 0x7ff00000, 0.2), (0, 0x7ff00001, 0.2), (0x7fe00000, 0x7ff00000, 0.4)]
 
 
 @pytest.mark.parametrize("mn,mx,p", PARAMS)
