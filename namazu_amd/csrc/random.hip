@@ -138,15 +138,19 @@ __device__ __forceinline__ uint4 uniform4(uint4 v) {
 
 // Go seed for (prefix state h0 -> H = h0 * P^8, its residue Hm = H mod M31) and
 // one table entry q = {C lo, C hi, C mod M31, class}
-__device__ __forceinline__ uint32_t go_seed_from_table(uint64_t H, uint32_t Hm, uint4 q) {
+// nm = -M31 and one = 1 arrive in VGPRs the compiler cannot see through, so that both conditional corrections are
+// a VOP2 borrow (v_sub_co) plus a VCC v_cndmask with VGPR operands (full rate) rather than an add of a literal and
+// a v_min_u32 (half rate), and the s == 0 test is a borrow out of s - 1 rather than a v_cmp.
+__device__ __forceinline__ uint32_t go_seed_from_table(uint64_t H, uint32_t Hm, uint4 q,
+                                                       uint32_t nm = gorand::NEG_M31, uint32_t one = 1u) {
     const uint64_t C = ((uint64_t)q.y << 32) | q.x;
     const uint64_t u = H + C;
     const uint32_t k = (uint32_t)(u < H) + (uint32_t)(u >> 63);  // wrap carry + sign
-    uint32_t s1 = Hm + q.z;                                      // < 2*M31
-    s1 = min(s1, s1 - gorand::M31);
-    const uint32_t dd = s1 - 4u * k;
-    uint32_t s = min(dd, dd + gorand::M31);
-    return s == 0 ? 89482311u : s;
+    uint32_t s1 = Hm + q.z, t;                                   // < 2*M31
+    s1 = __builtin_sub_overflow(s1, 0u - nm, &t) ? s1 : t;
+    uint32_t dd;
+    const uint32_t s = __builtin_sub_overflow(s1, 4u * k, &dd) ? dd - nm : dd;
+    return __builtin_sub_overflow(s, one, &t) ? 89482311u : s;
 }
 
 // per-event table: FNV correction for hint = le64(evhash), class bits
@@ -208,8 +212,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
                                                       nmz_sched_stats *__restrict__ partial, uint64_t part_stride,
                                                       nmz_sched_stats *__restrict__ stats) {
     const uint32_t lane = threadIdx.x & 63;
-    uint32_t nm = gorand::NEG_M31;  // -M in a VGPR (see gorand::modmul)
-    asm volatile("" : "+v"(nm));
+    uint32_t nm = gorand::NEG_M31, one = 1u;  // -M and 1 in VGPRs (see gorand::modmul, go_seed_from_table)
+    asm volatile("" : "+v"(nm), "+v"(one));
     const uint32_t n_items = *n_units * n_chunks;
     const ClassParams c0 = P.cls[0], c1 = P.cls[1];
     for (;;) {
@@ -244,7 +248,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
             const uint32_t en = __builtin_amdgcn_readfirstlane(min(e + 1, e1 - 1));
             qn = uniform4(row[en]);
             const uint32_t cls = q.w;
-            const uint32_t s = go_seed_from_table(H, Hm, q);
+            const uint32_t s = go_seed_from_table(H, Hm, q, nm, one);
             const Decision d = decide(s, cls, (cls & NMZ_EV_PRIORITIZED) ? c1 : c0, P.fault_threshold, nm);
             if constexpr (K32) {
                 const uint32_t d32 = (uint32_t)d.delay;
