@@ -12,6 +12,7 @@ import sys
 UNITS = {  # kernel name prefix -> (unit, units per launch of the bench workload)
     "void nmz::k_replayable_sweep_fast": ("decision", 2**20 * 4096),
     "nmz::k_random_sweep": ("decision", 2**20 * 10_000),
+    "void nmz::k_random_sweep<true>": ("decision", 2**20 * 10_000),
     "void nmz::k_ed_bv<32>": ("pair", 100_000 * 99_999 // 2),
     "void nmz::k_ed_wide<4>": ("pair", 256 * 255 // 2),
 }
