@@ -131,6 +131,45 @@ __device__ __forceinline__ Decision decide(uint32_t s, uint32_t cls, const Class
     return d;
 }
 
+// decide() for the sweep: the same decision with the draw count known per class (0 or 1 Go outputs before the
+// fault draw), so that nothing depends on a per-lane draw counter. A lane whose delay or fault draw is rejected
+// (probability ~1e-11 and ~3e-7 at the bench parameters) recomputes the whole decision with decide() in a
+// divergent branch; a lane whose fault outcome hangs on the low-word carry (~2e-3) computes output 1 in full.
+__device__ __forceinline__ Decision decide_sweep(uint32_t s, uint32_t cls, const ClassParams &cp,
+                                                 int32_t fault_threshold, uint32_t nm) {
+    Decision d{0, 0, 0};
+    bool slow = false;
+    if (cp.n) {
+        const uint64_t v = gorand::out0(s, nm) & MASK63;
+        if (cp.mu) {
+            slow = v > cp.max_accept;
+            d.delay = (cp.n >> 31) == 0 ? (int64_t)mod_barrett_small(v, (uint32_t)cp.n, cp.mu) + cp.min
+                                        : (int64_t)mod_barrett(v, cp.n, cp.mu) + cp.min;
+        } else {
+            d.delay = (int64_t)(v & (cp.n - 1)) + cp.min;
+        }
+        if (cls & NMZ_EV_FAULTABLE) {
+            const uint32_t v0 = (gorand::vec_hi<332>(s, nm) + gorand::vec_hi<605>(s, nm)) & 0x7fffffffu;
+            uint32_t r = v0 % INTN_N;
+            if (v0 >= INT31N_MAX || r == INTN_N - 1 || r + 1 == (uint32_t)fault_threshold) {
+                const uint32_t v1 = (uint32_t)(gorand::out1(s, nm) >> 32) & 0x7fffffffu;
+                slow |= v1 > INT31N_MAX;
+                r = v1 % INTN_N;
+            }
+            d.fault = ((int32_t)r < fault_threshold) ? 1u : 0u;
+        }
+    } else {
+        d.delay = cp.min;
+        if (cls & NMZ_EV_FAULTABLE) {
+            const uint32_t v = (uint32_t)(gorand::out0(s, nm) >> 32) & 0x7fffffffu;
+            slow = v > INT31N_MAX;
+            d.fault = ((int32_t)(v % INTN_N) < fault_threshold) ? 1u : 0u;
+        }
+    }
+    if (slow) d = decide(s, cls, cp, fault_threshold, nm);
+    return d;
+}
+
 __device__ __forceinline__ uint4 uniform4(uint4 v) {
     return make_uint4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
                       __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
@@ -249,7 +288,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
             qn = uniform4(row[en]);
             const uint32_t cls = q.w;
             const uint32_t s = go_seed_from_table(H, Hm, q, nm, one);
-            const Decision d = decide(s, cls, (cls & NMZ_EV_PRIORITIZED) ? c1 : c0, P.fault_threshold, nm);
+            const Decision d = decide_sweep(s, cls, (cls & NMZ_EV_PRIORITIZED) ? c1 : c0, P.fault_threshold, nm);
             if constexpr (K32) {
                 const uint32_t d32 = (uint32_t)d.delay;
                 sum += d32;
