@@ -136,7 +136,7 @@ __device__ __forceinline__ Decision decide(uint32_t s, uint32_t cls, const Class
 // (probability ~1e-11 and ~3e-7 at the bench parameters) recomputes the whole decision with decide() in a
 // divergent branch; a lane whose fault outcome hangs on the low-word carry (~2e-3) computes output 1 in full.
 __device__ __forceinline__ Decision decide_sweep(uint32_t s, uint32_t cls, const ClassParams &cp,
-                                                 int32_t fault_threshold, uint32_t nm) {
+                                                 int32_t fault_threshold, uint32_t nm, uint32_t &ovf) {
     Decision d{0, 0, 0};
     bool slow = false;
     if (cp.n) {
@@ -166,7 +166,10 @@ __device__ __forceinline__ Decision decide_sweep(uint32_t s, uint32_t cls, const
             d.fault = ((int32_t)(v % INTN_N) < fault_threshold) ? 1u : 0u;
         }
     }
-    if (slow) d = decide(s, cls, cp, fault_threshold, nm);
+    if (slow) {  // only here can the Go outputs run out (ovf is updated in this branch alone)
+        d = decide(s, cls, cp, fault_threshold, nm);
+        ovf |= d.overflow;
+    }
     return d;
 }
 
@@ -288,7 +291,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
             qn = uniform4(row[en]);
             const uint32_t cls = q.w;
             const uint32_t s = go_seed_from_table(H, Hm, q, nm, one);
-            const Decision d = decide_sweep(s, cls, (cls & NMZ_EV_PRIORITIZED) ? c1 : c0, P.fault_threshold, nm);
+            const Decision d = decide_sweep(s, cls, (cls & NMZ_EV_PRIORITIZED) ? c1 : c0, P.fault_threshold, nm, ovf);
             if constexpr (K32) {
                 const uint32_t d32 = (uint32_t)d.delay;
                 sum += d32;
@@ -302,8 +305,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
                 }
             }
             nf += d.fault;
-            ff = (d.fault && ff == NMZ_NONE) ? e : ff;
-            ovf |= d.overflow;
+            ff = min(ff, d.fault ? e : NMZ_NONE);  // events run in increasing order
         }
         if constexpr (K32) {
             if (e0 < e1) {
