@@ -272,7 +272,7 @@ def test_random_edge_cases(ctx):
 @pytest.mark.parametrize("E,mn,mx,p", [(3000, 30_000_000, 100_000_000, 0.001), (2048, 5_000_000, 5_000_000, 0.002),
                                         (1025, 0, 1 << 20, 0.0), (4100, 7, 9, 0.0015)])
 def test_random_event_chunks(ctx, E, mn, mx, p):
-    """Traces longer than one work item (1,024 events): per-chunk partial stats merged in event order.
+    """Traces longer than one work item (512 events): per-chunk partial stats merged in event order.
     Rare faults put first_fault in later chunks; fixed or 2-valued delays make argmax ties across chunks."""
     eh = RNG.integers(0, 2**64, size=E, dtype=np.uint64)
     ec = RNG.integers(0, 4, size=E, dtype=np.uint8)
