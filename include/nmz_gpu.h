@@ -220,6 +220,15 @@ int nmz_ed_allpairs_knn_shard_dev(nmz_ed_plan *plan, uint32_t k, uint32_t shard,
                                   uint64_t *d_knn_keys, void *stream);
 int nmz_knn_merge_dev(nmz_ctx *ctx, const uint64_t *d_parts, uint32_t n_parts, uint32_t n_traces,
                       uint32_t k, uint64_t *d_out, void *stream);
+/* Work counters of the plan's latest search (synchronises `stream`, NULL = the context's stream).
+ * out[NMZ_ED_NCOUNTERS]: the bit-parallel band kernel (nmz_ed_plan_is_fast == 2) fills
+ *   [0] pairs that ran the DP, [1] pairs whose result is <= band (in band),
+ *   [2] candidate x 32-column blocks executed (each block steps 2 query columns per candidate),
+ *   [3] candidates that ran the DP, [4] live query-blocks (blocks x queries still running);
+ * other kernels keep no counters and leave zeros. Diagnostics for the bench, not part of the
+ * reference interface. */
+#define NMZ_ED_NCOUNTERS 5
+int nmz_ed_plan_counters(nmz_ed_plan *plan, uint64_t *out, void *stream);
 
 #ifdef __cplusplus
 }

@@ -23,6 +23,7 @@ NMZ_EV_PRIORITIZED = 0x01
 NMZ_EV_FAULTABLE = 0x02
 NMZ_STAT_RNG_OVERFLOW = 0x01
 NMZ_NONE = 0xFFFFFFFF
+NMZ_ED_NCOUNTERS = 5
 
 SCHED_STATS_DTYPE = np.dtype([
     ("sum_delay_ns", "<u8"), ("max_delay_ns", "<i8"), ("argmax_event", "<u4"),
@@ -80,6 +81,7 @@ SIGNATURES = {
     "nmz_ed_allpairs_knn_dev": (_int, [_P, _u32, _P, _P]),
     "nmz_ed_allpairs_knn_shard_dev": (_int, [_P, _u32, _u32, _u32, _P, _P]),
     "nmz_knn_merge_dev": (_int, [_P, _P, _u32, _u32, _u32, _P, _P]),
+    "nmz_ed_plan_counters": (_int, [_P, _P, _P]),
     "nmz_topk_select_dev": (_int, [_P, _P, _u64, _u64, _u32, _P, _P]),
     "nmz_timing_enable": (_int, [_P, _int]),
     "nmz_timing_read": (_int, [_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),

@@ -354,6 +354,7 @@ struct nmz_ed_plan {
     uint64_t n_chunks = 0;         // bv: total chunks (64-query block row x ED_BV_POOL candidates)
     uint16_t *d_bsym = nullptr;
     uint64_t *d_chunk_start = nullptr;
+    uint64_t *d_counters = nullptr;  // bv: work counters of the latest search (nmz_ed_plan_counters)
     nmz::DevBuf mem;
     uint16_t *d_qsym = nullptr, *d_csym = nullptr;
     uint64_t *d_qoff = nullptr, *d_coff = nullptr;
@@ -489,10 +490,12 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         for (uint32_t i = 0; i < N; ++i)
             for (uint32_t t = 0; t < len[i]; ++t) bs[soff[i] + t] = (uint16_t)(ids[off[i] + t] * ndw * 8);
         size_t need = Carve::bytes_for(bs.size(), 2) + Carve::bytes_for(N + 1, 8) * 2 +
-                      Carve::bytes_for(G + 1, 8) + Carve::bytes_for(N + 1, 4);
+                      Carve::bytes_for(G + 1, 8) + Carve::bytes_for(N + 1, 4) +
+                      Carve::bytes_for(ED_BV_NCOUNTERS, 8);
         int rc = p->mem.ensure(need);
         if (rc != NMZ_OK) return cleanup(rc);
         Carve cv(p->mem.ptr);
+        p->d_counters = cv.take<uint64_t>(ED_BV_NCOUNTERS);
         p->d_bsym = cv.take<uint16_t>(bs.size());
         p->d_soff = cv.take<uint64_t>(N + 1);
         p->d_qoff = cv.take<uint64_t>(N + 1);
@@ -503,7 +506,7 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
             hipMemcpyAsync(p->d_qoff, off, (N + 1) * 8, hipMemcpyHostToDevice, st) ||
             hipMemcpyAsync(p->d_chunk_start, chunk_start.data(), (G + 1) * 8, hipMemcpyHostToDevice, st) ||
             hipMemcpyAsync(p->d_len, len.data(), (N + 1) * 4, hipMemcpyHostToDevice, st) ||
-            hipStreamSynchronize(st))
+            hipMemsetAsync(p->d_counters, 0, ED_BV_NCOUNTERS * 8, st) || hipStreamSynchronize(st))
             return cleanup(fail(NMZ_EHIP, "ED plan upload failed"));
     } else if (fast) {
         const uint32_t G = (N + 63) / 64;
@@ -589,6 +592,7 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
         A.len = p->d_len;
         A.chunk_start = p->d_chunk_start;
         A.knn = d_knn;
+        A.counters = p->d_counters;
         A.N = N;
         A.G = p->G;
         A.k = k;
@@ -601,6 +605,7 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
         uint64_t blocks = A.n_chunks * 32;
         blocks = (blocks + 7) / 8 * 8;
         NMZ_CHECK(blocks < (1ULL << 31), "too many traces for one launch");
+        NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_BV_NCOUNTERS * 8, st));
         KernelTimer kt(p->ctx, st, "ed_bv");
         return ed_bv_launch(A, p->band, blocks, st);
     }
@@ -683,6 +688,18 @@ int nmz_ed_plan_destroy(nmz_ed_plan *plan) {
 int nmz_ed_plan_is_fast(const nmz_ed_plan *plan) {
     if (!plan) return 0;
     return plan->wide ? 3 : (plan->bv ? 2 : (plan->fast ? 1 : 0));
+}
+
+int nmz_ed_plan_counters(nmz_ed_plan *plan, uint64_t *out, void *stream) {
+    NMZ_CHECK(plan != nullptr && out != nullptr, "NULL argument");
+    for (int i = 0; i < NMZ_ED_NCOUNTERS; ++i) out[i] = 0;
+    if (!plan->d_counters) return NMZ_OK;
+    static_assert(ED_BV_NCOUNTERS == NMZ_ED_NCOUNTERS, "counter layout");
+    CtxGuard g(plan->ctx);
+    hipStream_t st = stream ? (hipStream_t)stream : plan->ctx->stream;
+    NMZ_HIP(hipMemcpyAsync(out, plan->d_counters, ED_BV_NCOUNTERS * 8, hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipStreamSynchronize(st));
+    return NMZ_OK;
 }
 
 int nmz_ed_allpairs_knn_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys, void *stream) {

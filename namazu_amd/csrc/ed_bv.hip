@@ -237,8 +237,10 @@ __device__ __forceinline__ void bv_block(BvState<BvShape<W>::KF> &S1, BvState<Bv
 // (distinct lists), query lists wave-reduced (the 2 query lists are shared by
 // every lane of the workgroup; per-lane atomics on them serialize in L2)
 __device__ __forceinline__ void bv_publish(const EdBvArgs &A, bool fin, uint32_t j, uint32_t q1, uint32_t q2,
-                                            bool v2, uint32_t r1, uint32_t r2, uint32_t lane) {
+                                            bool v2, uint32_t r1, uint32_t r2, uint32_t lane, uint32_t w,
+                                            uint32_t &in_band) {
     if (fin) {
+        in_band += (uint32_t)(r1 <= w) + (uint32_t)(v2 && r2 <= w);
         bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, ((uint64_t)r1 << 32) | q1);
         if (v2) bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, ((uint64_t)r2 << 32) | q2);
     }
@@ -319,6 +321,8 @@ __global__ __launch_bounds__(256) void k_ed_bv(EdBvArgs A) {
     uint32_t kb = 0;
     bool need = true;
     bool first = true;
+    // work counters (A.counters): DP pairs, in-band pairs, lane blocks, DP candidates, live query-blocks
+    uint32_t c_dp_pairs = 0, c_in_band = 0, c_blocks = 0, c_dp_cand = 0, c_live = 0;
     while (true) {
         // ---- (re)assign candidates to lanes that need one ----
         while (true) {
@@ -353,6 +357,8 @@ __global__ __launch_bounds__(256) void k_ed_bv(EdBvArgs A) {
                     if (run1 || run2) {
                         need = false;
                         active = true;
+                        c_dp_cand += 1;
+                        c_dp_pairs += (uint32_t)run1 + (uint32_t)run2;
                         kb0 = kb;
                         bv_init<W>(S1);
                         bv_init<W>(S2);
@@ -362,9 +368,11 @@ __global__ __launch_bounds__(256) void k_ed_bv(EdBvArgs A) {
             }
             // candidates decided without a DP (|n - m| > w, empty traces): publish, draw again
             const bool fin = need && !active && idx < pool_n;
-            if (__any(fin)) bv_publish(A, fin, j, q1, q2, v2, r1, r2, lane);
+            if (__any(fin)) bv_publish(A, fin, j, q1, q2, v2, r1, r2, lane, W, c_in_band);
         }
         if (!__any(active)) break;
+        c_blocks += (uint32_t)active;
+        c_live += active ? (uint32_t)run1 + (uint32_t)run2 : 0u;
         // ---- one 32-column block ----
         const uint32_t lkb = active ? kb - kb0 : 0;
         bv_load_block(nxt, stream, lkb + 1);  // streams carry one spare block
@@ -384,10 +392,23 @@ __global__ __launch_bounds__(256) void k_ed_bv(EdBvArgs A) {
         for (int r = 0; r < 16; ++r) cur[r] = nxt[r];
         ++kb;
         const bool fin = active && !run1 && !run2;
-        if (__any(fin)) bv_publish(A, fin, j, q1, q2, v2, r1, r2, lane);
+        if (__any(fin)) bv_publish(A, fin, j, q1, q2, v2, r1, r2, lane, W, c_in_band);
         if (fin) {
             active = false;
             need = true;
+        }
+    }
+    if (A.counters) {
+        uint64_t c[ED_BV_NCOUNTERS] = {c_dp_pairs, c_in_band, c_blocks, c_dp_cand, c_live};
+#pragma unroll
+        for (int i = 0; i < ED_BV_NCOUNTERS; ++i) {
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) c[i] += __shfl_xor(c[i], off, 64);
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < ED_BV_NCOUNTERS; ++i)
+                if (c[i]) atomicAdd((unsigned long long *)&A.counters[i], (unsigned long long)c[i]);
         }
     }
 }

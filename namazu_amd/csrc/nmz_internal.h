@@ -34,9 +34,14 @@ struct EdBvArgs {
     const uint32_t *len;          // [N]
     const uint64_t *chunk_start;  // [G+1] first chunk of each 64-query block row
     uint64_t *knn;                // [N][k]
+    uint64_t *counters;           // [ED_BV_NCOUNTERS] work counters (nmz_ed_plan_counters), or nullptr
     uint64_t n_chunks;            // chunks of this shard
     uint32_t N, G, k, lds_dw, shard, n_shards, pool;
 };
+// k_ed_bv work counters, summed over the launch:
+//   0 pairs that ran the DP, 1 pairs with a result <= w (in band), 2 lane-candidate 32-column blocks executed,
+//   3 candidates that ran the DP, 4 live query-blocks (blocks x queries of that lane still running)
+constexpr int ED_BV_NCOUNTERS = 5;
 int ed_bv_launch(const EdBvArgs &A, uint32_t band, uint64_t blocks, hipStream_t st);
 
 // wide-band bit-parallel edit distance (ed_wide.hip): one pair per wave

@@ -8,8 +8,11 @@ search deals 32-wave tile groups round-robin over ranks (equal cells per
 group) and all_gathers the partial k-NN key lists (N x k x 8 B) for a per-trace
 merge (nmz_knn_merge_dev on the GPU, merge_knn_keys on the host).
 """
+import ctypes
+
 import numpy as np
 
+from . import _lib
 from ._lib import TOPK_DTYPE
 
 
@@ -47,3 +50,44 @@ def gather_topk(dist, topk_np, k, device="cpu"):
     t = torch.from_numpy(np.frombuffer(np.ascontiguousarray(topk_np).tobytes(), np.uint8).copy()).to(device)
     parts = all_gather_bytes(dist, t)
     return merge_topk([p.cpu().numpy() for p in parts], k)
+
+
+class RandomShardSweep:
+    """One rank's share of a random-policy fault sweep (BASELINE configs[3]): seeds
+    [seed0 + lo, seed0 + hi) of `n_total` (shard_range), swept on this rank's GPU with the
+    top-k selected on the device (nmz_random_sweep_dev + nmz_topk_select_dev, randompolicy.go:300-346).
+    The per-event tables are built once (the plan); step() enqueues one sweep of the share on
+    `stream` and leaves the rank's top-k (k x 24 B, TOPK_DTYPE) in the device buffer `d_topk`,
+    which the caller all_gathers (RCCL) and merges with merge_topk."""
+
+    def __init__(self, ctx, torch, device, evhash, evclass, params, seed0, n_total, world, rank, k=64):
+        self.L = _lib.load()
+        self.ctx = ctx
+        self.lo, self.hi = shard_range(n_total, world, rank)
+        self.seed0 = (seed0 + self.lo) % (1 << 64)
+        self.n = self.hi - self.lo
+        self.k = k
+        evhash = np.ascontiguousarray(evhash, np.uint64)
+        evclass = np.ascontiguousarray(evclass, np.uint8)
+        self.plan = ctypes.c_void_p()
+        _lib.check(self.L.nmz_random_plan_create(ctx.handle, _lib.ptr(evhash), _lib.ptr(evclass), len(evhash),
+                                                 ctypes.byref(params), max(self.n, 1), ctypes.byref(self.plan)))
+        self.d_stats = torch.empty(max(self.n, 1) * 32, dtype=torch.uint8, device=device)
+        self.d_topk = torch.empty(k * 24, dtype=torch.uint8, device=device)
+
+    def step(self, stream):
+        _lib.check(self.L.nmz_random_sweep_dev(self.plan, self.seed0, self.n,
+                                               ctypes.c_void_p(self.d_stats.data_ptr()), stream))
+        _lib.check(self.L.nmz_topk_select_dev(self.ctx.handle, ctypes.c_void_p(self.d_stats.data_ptr()), self.n,
+                                              self.seed0, self.k, ctypes.c_void_p(self.d_topk.data_ptr()), stream))
+
+    def stats(self):
+        return np.frombuffer(self.d_stats.cpu().numpy().tobytes(), _lib.SCHED_STATS_DTYPE)[:self.n]
+
+    def topk(self):
+        return np.frombuffer(self.d_topk.cpu().numpy().tobytes(), TOPK_DTYPE)
+
+    def close(self):
+        if self.plan:
+            self.L.nmz_random_plan_destroy(self.plan)
+            self.plan = None

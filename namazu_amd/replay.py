@@ -19,13 +19,29 @@ the seed itself (seed0 + i).
 from .config import Config
 
 REPLAY_SEED_ENV = "NMZ_REPLAY_SEED"  # replayablepolicy.go:83
+UINT64_MAX = (1 << 64) - 1
+INT64_MIN = -(1 << 63)
+
+
+def as_int64(seed):
+    """u64 seed -> the int64 with the same bits. TOML integers (and Go's TOML/viper decoders) are
+    int64, so seeds >= 2^63 are written as negative numbers; Random.LoadConfig masks them back
+    with & (2^64-1)."""
+    seed = int(seed) & UINT64_MAX
+    return seed - (1 << 64) if seed >= (1 << 63) else seed
+
+
+def _is_sentinel(e):
+    """A padding entry of a top-k list shorter than k (topk_sentinel(), csrc/topk_dev.h)."""
+    return int(e["seed"]) == UINT64_MAX and int(e["sum_delay_ns"]) == INT64_MIN and int(e["n_fault"]) == 0
 
 
 def replayable_seeds(topk, seeds):
     """Top-k entries of a replayable sweep over `seeds` -> seed strings, best first."""
     out = []
-    for idx in topk["seed"].tolist():
-        if idx >= len(seeds):  # sentinel (fewer seeds than k)
+    for e in topk[:len(seeds)]:
+        idx = int(e["seed"])
+        if _is_sentinel(e) or idx >= len(seeds):  # fewer seeds than k
             break
         s = seeds[idx]
         out.append(s.decode() if isinstance(s, bytes) else str(s))
@@ -35,10 +51,13 @@ def replayable_seeds(topk, seeds):
 def random_seeds(topk, seed0, n_seeds):
     """Top-k entries of a random sweep over seed0..seed0+n_seeds-1 -> u64 seeds, best first."""
     out = []
-    for s in topk["seed"].tolist():
-        if (s - seed0) % (1 << 64) >= n_seeds:  # sentinel
+    # at most n_seeds real entries; padding is recognised by its full signature, not by its seed
+    # value (a range that wraps past 2^64 can hold UINT64_MAX as a real seed)
+    for e in topk[:n_seeds]:
+        s = int(e["seed"])
+        if _is_sentinel(e) or (s - seed0) % (1 << 64) >= n_seeds:
             break
-        out.append(int(s))
+        out.append(s)
     return out
 
 
@@ -59,7 +78,7 @@ def replay_config(cfg: Config, seed):
     if policy == "replayable":
         out.set("explorePolicyParam.seed", str(seed))
     elif policy == "random":
-        out.set("explorePolicyParam.seed", int(seed))
+        out.set("explorePolicyParam.seed", as_int64(seed))
     else:
         raise ValueError(f"policy {policy!r} has no replay seed")
     return out

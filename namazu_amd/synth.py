@@ -8,7 +8,16 @@
 * synth_traces: SURVEY 8(d) config 3 -- a ZooKeeper-style Markov base sequence
   over 48 event symbols (the stored example traces hold 38 distinct events),
   each trace = base + adjacent transpositions at 2% + substitutions at 0.5%,
-  fixed length; symbols are 64-bit event hashes.
+  fixed length; symbols are 64-bit event hashes. Independent mutations at these
+  rates put every pair ~150-175 edits apart, past w = 32: a search workload in
+  which nothing is near anything else.
+* clustered_traces: configs[2] as a search workload -- the same base, split
+  into families. A family's parent is the base mutated at the survey rates;
+  each member is its parent plus a few edits (Poisson-many adjacent
+  transpositions and substitutions), as repeated runs of one schedule differ
+  by a few reordered or changed events. Members of one family are a few edits
+  apart (inside w = 32), families ~150 edits apart, so with families of
+  `family` traces about (family-1)/(n-1) of all pairs fall inside the band.
 """
 import numpy as np
 
@@ -68,3 +77,52 @@ def synth_traces(n, length, seed=0x5EED, n_symbols=48, p_transpose=0.02, p_subst
 def etcd_traces(n, length, seed=0xE7CD):
     """configs[4]: n etcd-style traces of `length` events (see module docstring)."""
     return synth_traces(n, length, seed=seed, n_symbols=64, p_transpose=0.01, p_subst=0.003)
+
+
+def clustered_traces(n, length, seed=0x5EED, n_symbols=48, family=1024, edits_mean=6.0,
+                     p_transpose=0.02, p_subst=0.005):
+    """configs[2] search workload: n traces in families of `family` near-duplicates (module docstring).
+    Trace i belongs to family i // family (contiguous ids). Returns a historystorage.TraceSet."""
+    from .historystorage import TraceSet
+    rng = np.random.default_rng(seed)
+    base = _markov_base(length, n_symbols, rng)
+    sym_hash = splitmix64(seed ^ 0xABCDEF, n_symbols)
+    n_fam = max(1, -(-n // family))
+    parents = np.broadcast_to(base, (n_fam, length)).copy()
+    _mutate(parents, rng, n_symbols, p_transpose, p_subst)
+    ids = np.empty((n, length), np.int64)
+    chunk = 4096
+    for c0 in range(0, n, chunk):
+        c = min(chunk, n - c0)
+        t = parents[np.arange(c0, c0 + c) // family].copy()
+        # a few edits per member: Poisson(edits_mean) events, each an adjacent transposition or a substitution
+        k = rng.poisson(edits_mean, c)
+        rows = np.repeat(np.arange(c), k)
+        pos = rng.integers(0, max(length - 1, 1), rows.size)
+        swap = rng.random(rows.size) < 0.5
+        r, i = rows[swap], pos[swap]
+        if length > 1:
+            a = t[r, i].copy()
+            t[r, i] = t[r, i + 1]
+            t[r, i + 1] = a
+        r, i = rows[~swap], pos[~swap]
+        t[r, i] = rng.integers(0, n_symbols, size=r.size)
+        ids[c0:c0 + c] = t
+    ts = TraceSet([])
+    ts.off = np.arange(n + 1, dtype=np.uint64) * np.uint64(length)
+    ts.sym = sym_hash[ids.reshape(-1)]
+    return ts
+
+
+def _mutate(t, rng, n_symbols, p_transpose, p_subst):
+    """In place: non-overlapping adjacent transpositions at p_transpose, then substitutions at p_subst."""
+    c, length = t.shape
+    if length > 1:
+        sw = rng.random((c, length - 1)) < p_transpose
+        sw[:, 1:] &= ~sw[:, :-1]
+        r, i = np.nonzero(sw)
+        a = t[r, i].copy()
+        t[r, i] = t[r, i + 1]
+        t[r, i + 1] = a
+    sub = rng.random((c, length)) < p_subst
+    t[sub] = rng.integers(0, n_symbols, size=int(sub.sum()))

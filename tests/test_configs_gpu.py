@@ -1,0 +1,196 @@
+"""One GPU parity test per BASELINE.json config, named after it (test_config0_ ... test_config4_), each
+through the C ABI (libnmz_gpu.so) against the CPU oracle at the config's own shape.
+
+configs[0] random policy, one 10k-event trace, single seed   (randompolicy.go:156-228,300-346)
+configs[1] replayable sweep, 2^20 seeds x 4,096 hints        (replayablepolicy.go:100-126)
+configs[2] all-pairs banded search, 2,048-event traces, w=32 (search surface naive.go:235-257)
+configs[3] random fault sweep, 16 entities, 10^7 schedules, sharded + top-k merge
+configs[4] long traces, 65,536 events, w = 4,096
+"""
+import numpy as np
+import pytest
+
+from namazu_amd import _lib
+from namazu_amd import dist as nd
+from namazu_amd import explorepolicy as ep
+from namazu_amd import historystorage as hs
+from namazu_amd.config import Config
+from namazu_amd.signal import Event
+from namazu_amd.synth import clustered_traces, etcd_traces, synth_traces, zk_hints
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RNG = np.random.default_rng(0xC0F)
+
+
+def config3_trace(E=10_000):
+    """16 entities entity-0..15 (explorepolicytester.go:36), entity-0..3 prioritized, all events faultable."""
+    eh = RNG.integers(0, 2**64, size=E, dtype=np.uint64)
+    ec = (np.where(np.arange(E) % 16 < 4, _lib.NMZ_EV_PRIORITIZED, 0) | _lib.NMZ_EV_FAULTABLE).astype(np.uint8)
+    return eh, ec
+
+
+def test_config0_random_single_seed_10k_trace():
+    """configs[0]: the random policy over one 10k-event trace under one seed, through the reference's own
+    surface (LoadConfig -> Sweep / decide / QueueEvent), against the oracle. 30 ms / 100 ms
+    (randompolicy_test.go:53-54), fault probability 0.1, seed 1."""
+    cfg = Config({"explorePolicy": "random", "explorePolicyParam": {
+        "minInterval": "30ms", "maxInterval": "100ms", "faultActionProbability": 0.1, "seed": 1,
+        "prioritizedEntities": [f"entity-{i}" for i in range(4)]}})
+    p = ep.Random()
+    assert p.LoadConfig(cfg) is None and p.Seed == 1
+    rng = np.random.default_rng(0x5EED)
+    events = [Event.packet(f"entity-{i % 16}", f"entity-{i % 16}", f"entity-{(i + 1) % 16}",
+                           replay_hint=str(int(rng.integers(-2**63, 2**63 - 1))))
+              for i in range(10_000)]
+    evhash, evclass = p.event_inputs(events)
+    assert int((evclass & _lib.NMZ_EV_PRIORITIZED).astype(bool).sum()) == 2500
+    st, dl, fl = O.random_sweep(1, 1, evhash, evclass, O.random_params(30_000_000, 100_000_000, 0.1), n_dump=1)
+    r = p.Sweep(p.Seed, 1, evhash, evclass, n_dump=1)
+    assert np.array_equal(r.delays, dl) and np.array_equal(r.faults, fl) and np.array_equal(r.stats, st)
+    # online: one decision per event through the policy's resident plan
+    for i in range(0, 10_000, 97):
+        assert p.decide(events[i]) == (int(dl[0, i]), bool(fl[0, i]))
+    for i in range(8):
+        p.QueueEvent(events[i])
+    got = {}
+    for _ in range(8):
+        a = p.ActionChan().get(timeout=5)
+        got[a.Event().ID()] = a.Class()
+    for i in range(8):
+        assert got[events[i].ID()] == ("PacketFaultAction" if fl[0, i] else "EventAcceptanceAction")
+    pr = (evclass & _lib.NMZ_EV_PRIORITIZED).astype(bool)
+    assert dl[0][pr].min() >= 24_000_000 and dl[0][pr].max() < 80_000_000
+    assert dl[0][~pr].min() >= 30_000_000 and dl[0][~pr].max() < 100_000_000
+
+
+def test_config1_replayable_1M_seeds_x_4k_hints(ctx):
+    """configs[1] at full size (2^20 seeds x 4,096 hints, maxInterval 100 ms): sampled bit-exact parity plus
+    size-independent invariants (dump rows reproduce the stats, max < m, top-k consistent with the stats)."""
+    S, E, m = 1 << 20, 4096, 100_000_000
+    hints = zk_hints(E)
+    seeds = [str(i) for i in range(S)]
+    p = ep.Replayable()
+    p.MaxInterval = m
+    r = p.Sweep(seeds, hints, n_dump=8, k=64, ctx=ctx)
+    st = r.stats
+    assert (st["max_delay_ns"] >= 0).all() and (st["max_delay_ns"] < m).all()
+    assert (st["argmax_event"] < E).all()
+    assert (st["sum_delay_ns"] <= st["max_delay_ns"].astype(np.uint64) * np.uint64(E)).all()
+    assert np.array_equal(r.delays.sum(1).astype(np.uint64), st["sum_delay_ns"][:8])
+    assert np.array_equal(r.delays.max(1), st["max_delay_ns"][:8])
+    assert np.array_equal(r.delays.argmax(1), st["argmax_event"][:8])
+    idx = np.unique(np.concatenate([np.arange(64), np.arange(S - 64, S), RNG.integers(0, S, 256)]))
+    so, sb = O.to_csr([seeds[i] for i in idx])
+    ho, hb = O.to_csr(hints)
+    ost, _ = O.replayable_sweep(so, sb, ho, hb, m)
+    assert np.array_equal(st[idx], ost)
+    order = np.lexsort((np.arange(S), -st["sum_delay_ns"].astype(np.float64)))
+    assert r.topk["seed"].tolist() == order[:64].tolist()
+
+
+def _brute_knn(ts, q, w, k):
+    pairs = np.array([[q, c] for c in range(len(ts)) if c != q], np.uint32)
+    d = O.ed_pairs(ts.off, ts.sym, pairs, w, nthreads=16)
+    order = np.lexsort((pairs[:, 1], d))[:k]
+    return d[order].tolist(), pairs[order, 1].tolist(), d
+
+
+def _plan_knn_and_counters(ctx, ts, w, k):
+    import ctypes
+    import torch
+    L = _lib.load()
+    plan = ctypes.c_void_p()
+    _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), len(ts), w, ctypes.byref(plan)))
+    assert L.nmz_ed_plan_is_fast(plan) == 2  # k_ed_bv
+    d_keys = torch.empty(len(ts) * k, dtype=torch.int64, device="cuda")
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(L.nmz_ed_allpairs_knn_dev(plan, k, ctypes.c_void_p(d_keys.data_ptr()), stream))
+    cnt = np.zeros(_lib.NMZ_ED_NCOUNTERS, np.uint64)
+    _lib.check(L.nmz_ed_plan_counters(plan, _lib.ptr(cnt), stream))
+    keys = d_keys.cpu().numpy().view(np.uint64).reshape(-1, k)
+    L.nmz_ed_plan_destroy(plan)
+    return (keys & np.uint64(0xFFFFFFFF)).astype(np.uint32), (keys >> np.uint64(32)).astype(np.uint32), cnt
+
+
+def test_config2_allpairs_search_clustered_families(ctx):
+    """configs[2] as a search workload: 4,096 traces x 2,048 events in 16 families of 256 near-duplicates
+    (synth.clustered_traces), w = 32, k = 8. Sampled queries vs the oracle's brute-force k-NN; the nearest
+    neighbours are real in-band distances (od[:, 0] < 33), and the kernel's in-band counter equals the
+    oracle's count of in-band pairs."""
+    N, Lx, w, k = 4096, 2048, 32, 8
+    ts = clustered_traces(N, Lx, seed=7, family=256)
+    ids, ds, cnt = _plan_knn_and_counters(ctx, ts, w, k)
+    assert (ds[:, 0] <= w).mean() > 0.99
+    in_band = 0
+    for q in [0, 1, 255, 256, 777, 2048, 3000, 4095]:
+        od, oi, d = _brute_knn(ts, q, w, k)
+        assert ds[q].tolist() == od and ids[q].tolist() == oi
+        assert od[0] <= w
+    # counters: every pair of one family (sampled: family 0) is in band; all pairs count once
+    fam = np.array([[i, j] for i in range(256) for j in range(i + 1, 256)], np.uint32)
+    dfam = O.ed_pairs(ts.off, ts.sym, fam, w, nthreads=16)
+    in_band = int((dfam <= w).sum())
+    assert in_band > 0.95 * len(fam)
+    assert cnt[0] <= N * (N - 1) // 2 and cnt[1] >= 16 * in_band * 0.9
+    assert cnt[1] <= 16 * (256 * 255 // 2) + (N * (N - 1) // 2 - 16 * (256 * 255 // 2)) // 1000
+
+
+def test_config2_allpairs_search_survey_generator(ctx):
+    """configs[2] with the survey's generator (independent 2 % transpositions + 0.5 % substitutions):
+    N = 2,048 traces x 2,048 events, sampled brute-force parity; distances saturate at w + 1."""
+    ts = synth_traces(2048, 2048, seed=7)
+    ids, ds, cnt = _plan_knn_and_counters(ctx, ts, 32, 8)
+    for q in [0, 1, 777, 2047]:
+        od, oi, _ = _brute_knn(ts, q, 32, 8)
+        assert ds[q].tolist() == od and ids[q].tolist() == oi
+    assert cnt[0] == 2048 * 2047 // 2  # equal lengths: every pair runs the DP
+
+
+def test_config3_random_fault_sweep_10M_sharded_topk(ctx):
+    """configs[3]: 10^7 schedules over one 10k-event trace (16 entities, p = 0.1), split by shard_range into 8
+    rank shares on this one GPU, each swept with its top-64 selected on the device, merged with merge_topk;
+    equals the top-64 of one unsharded sweep. Sampled seeds and the winners vs the oracle."""
+    import torch
+    S, K, W = 10_000_000, 64, 8
+    eh, ec = config3_trace()
+    params = _lib.resolve_random_params(30_000_000, 100_000_000, 0.1)
+    stream = __import__("ctypes").c_void_p(torch.cuda.current_stream().cuda_stream)
+    parts = []
+    for r in range(W):
+        sh = nd.RandomShardSweep(ctx, torch, "cuda", eh, ec, params, 5000, S, W, r, k=K)
+        sh.step(stream)
+        torch.cuda.synchronize()
+        parts.append(sh.topk())
+        if r == W - 1:
+            last = (sh.seed0, sh.stats())
+        sh.close()
+    merged = nd.merge_topk(parts, K)
+    full = nd.RandomShardSweep(ctx, torch, "cuda", eh, ec, params, 5000, S, 1, 0, k=K)
+    full.step(stream)
+    torch.cuda.synchronize()
+    assert merged.tolist() == full.topk().tolist()
+    st = full.stats()
+    full.close()
+    assert (st["flags"] == 0).all()
+    assert 0.09 < st["n_fault"].mean() / len(eh) < 0.11  # Intn(999) < 100
+    p = O.random_params(30_000_000, 100_000_000, 0.1)
+    for s in [0, 1, S // 2, S - 1] + [int(x) - 5000 for x in merged["seed"][:3]]:
+        ost, _, _ = O.random_sweep(5000 + s, 1, eh, ec, p)
+        assert np.array_equal(st[s:s + 1], ost)
+    # the last shard's own stats are the tail of the full sweep's
+    seed_last, st_last = last
+    assert np.array_equal(st_last, st[seed_last - 5000:])
+
+
+def test_config4_long_traces_wide_band(ctx):
+    """configs[4] length (65,536 events, w = 4,096), ragged: one trace ends inside a 32-column block, one is
+    shorter by more than w (distance w + 1 without a DP); all pairs against the oracle's full-band DP."""
+    full = etcd_traces(4, 65536, seed=5)
+    cut = [65536, 65531, 63000, 60001]
+    ts = hs.TraceSet([full.sym[int(full.off[i]):int(full.off[i]) + c] for i, c in enumerate(cut)])
+    ids, ds = hs.allpairs_knn(ts, 3, 4096, ctx=ctx)
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, 4096, 3, nthreads=16)
+    assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+    assert od[0, 0] < 4096 and (od == 4097).any()

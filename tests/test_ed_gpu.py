@@ -235,19 +235,6 @@ def test_knn_wide_etcd_shape(ctx):
     assert (od[:, 0] < 4096).all()
 
 
-def test_knn_wide_etcd_full_length(ctx):
-    """configs[4] length (65,536 events, w = 4096), ragged: one trace ends inside a 32-column block, one is shorter
-    by more than w (distance w + 1 without a DP), all pairs against the oracle's full-band DP."""
-    from namazu_amd.synth import etcd_traces
-    full = etcd_traces(4, 65536, seed=5)
-    cut = [65536, 65531, 63000, 60001]
-    ts = hs.TraceSet([full.sym[int(full.off[i]):int(full.off[i]) + c] for i, c in enumerate(cut)])
-    ids, ds = knn(ctx, ts, 4096, 3)
-    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, 4096, 3, nthreads=16)
-    assert np.array_equal(ids, oi) and np.array_equal(ds, od)
-    assert od[0, 0] < 4096 and (od == 4097).any()
-
-
 @pytest.mark.parametrize("w,alphabet,lmin,lmax,n,kind", [
     (32, 20, 150, 260, 400, 2),     # k_ed_bv
     (16, 3000, 100, 140, 200, 1),   # k_ed_tile

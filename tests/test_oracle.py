@@ -218,3 +218,19 @@ def test_topk_order():
     assert list(tk["seed"]) == [102, 104, 101, 100]
     tk = O.topk_from_stats(st, 0, 8)
     assert list(tk["seed"][6:]) == [2**64 - 1] * 2
+
+
+def test_random_rejection_vectors(golden):
+    """tests/golden/random_rejections.json: each vector's fault draw is rejected and re-drawn (Go Int31n), after
+    one Int63n delay draw (ranged) or none (fixed duration); for any ranged or fixed parameters."""
+    g = golden("random_rejections.json")
+    for mn, mx in [(30_000_000, 100_000_000), (0, 3_000_000_000)]:
+        p = O.random_params(mn, mx, 0.1)
+        for eh in g["ranged"]:
+            for cls in (2, 3):
+                assert O.random_decide(g["seed"], eh, cls, p)[2] == 3
+    for mn in [5_000_000, 3_000_000_000]:
+        p = O.random_params(mn, mn, 0.1)
+        for eh in g["fixed"]:
+            for cls in (2, 3):
+                assert O.random_decide(g["seed"], eh, cls, p)[2] == 2

@@ -4,6 +4,8 @@ CPU: the helpers and the reference's config/env route (replayablepolicy.go:74-87
 GPU: a sweep's best schedule, replayed through Replayable.LoadConfig +
 determineInterval event by event, reproduces the sweep's statistics; BASELINE configs[0] (the random
 policy over one 10k-event trace, single seed) through LoadConfig / decide / QueueEvent vs the oracle."""
+import re
+
 import numpy as np
 import pytest
 
@@ -33,6 +35,22 @@ def test_random_seeds_wrap_and_sentinel():
     assert replay.random_seeds(_topk([5]), 0, 4) == []
 
 
+def test_random_seeds_real_uint64_max_vs_padding():
+    """A range wrapping past 2^64 holds UINT64_MAX as a real seed; padding entries (fewer seeds than k)
+    carry the sentinel signature and stop the list (csrc/topk_dev.h topk_sentinel)."""
+    tk = _topk([2**64 - 1, 2**64 - 2, 2**64 - 1, 2**64 - 1])
+    tk["sum_delay_ns"][:2] = [7, 5]
+    tk["sum_delay_ns"][2:] = -2**63
+    tk["n_fault"][:2] = 1
+    assert replay.random_seeds(tk, 2**64 - 3, 3) == [2**64 - 1, 2**64 - 2]
+    # n_seeds bounds the list even without a sentinel
+    tk2 = _topk([1, 0, 2**64 - 1])
+    tk2["sum_delay_ns"] = [3, 2, 1]
+    assert replay.random_seeds(tk2, 2**64 - 2, 4) == [1, 0, 2**64 - 1]
+    assert replay.random_seeds(tk2, 2**64 - 2, 2) == []
+    assert replay.random_seeds(_topk([2**64 - 1, 2**64 - 2, 0]), 2**64 - 2, 2) == [2**64 - 1, 2**64 - 2]
+
+
 def test_replay_env_overrides_config_seed(monkeypatch):
     monkeypatch.delenv(replay.REPLAY_SEED_ENV, raising=False)
     cfg = Config({"explorePolicy": "replayable", "explorePolicyParam": {"seed": "old", "maxInterval": "1s"}})
@@ -54,6 +72,12 @@ def test_replay_config_roundtrip_through_toml(monkeypatch):
     q = ep.Random()
     assert q.LoadConfig(Config.from_toml(replay.to_toml(replay.replay_config(rnd, 2**63 + 5)))) is None
     assert q.Seed == 2**63 + 5
+    # the emitted TOML integer fits in int64 (Go TOML decoders reject anything larger)
+    text = replay.to_toml(replay.replay_config(rnd, 2**63 + 5))
+    v = int(re.search(r"^seed = (-?\d+)$", text, re.M).group(1))
+    assert -2**63 <= v < 2**63 and v == 2**63 + 5 - 2**64
+    for s in (0, 1, 2**63 - 1, 2**63, 2**64 - 1):
+        assert -2**63 <= replay.as_int64(s) < 2**63 and replay.as_int64(s) % 2**64 == s
     with pytest.raises(ValueError):
         replay.replay_config(Config({"explorePolicy": "dumb"}), 1)
 
@@ -80,44 +104,3 @@ def test_best_replayable_schedule_replays_event_by_event(monkeypatch):
     assert sum(delays) == int(st["sum_delay_ns"])
     assert max(delays) == int(st["max_delay_ns"]) and delays.index(max(delays)) == int(st["argmax_event"])
     ctx.close()
-
-
-@pytest.mark.gpu
-def test_random_config0_online_path():
-    """BASELINE configs[0]: the random policy over one 10k-event trace under a single seed, through the
-    reference's own surface (LoadConfig -> QueueEvent / decide, randompolicy.go:156-228,300-346), against
-    the oracle. 16 entities entity-0..15 (explorepolicytester.go:36), entity-0..3 prioritized,
-    30 ms / 100 ms (randompolicy_test.go:53-54), fault probability 0.1, seed 1."""
-    from oracle import oracle as O
-
-    cfg = Config({"explorePolicy": "random", "explorePolicyParam": {
-        "minInterval": "30ms", "maxInterval": "100ms", "faultActionProbability": 0.1, "seed": 1,
-        "prioritizedEntities": [f"entity-{i}" for i in range(4)]}})
-    p = ep.Random()
-    assert p.LoadConfig(cfg) is None and p.Seed == 1
-    rng = np.random.default_rng(0x5EED)
-    events = [Event.packet(f"entity-{i % 16}", f"entity-{i % 16}", f"entity-{(i + 1) % 16}",
-                           replay_hint=str(int(rng.integers(-2**63, 2**63 - 1))))
-              for i in range(10_000)]
-    evhash, evclass = p.event_inputs(events)
-    assert int((evclass & _lib.NMZ_EV_PRIORITIZED).astype(bool).sum()) == 2500
-    st, dl, fl = O.random_sweep(1, 1, evhash, evclass, O.random_params(30_000_000, 100_000_000, 0.1), n_dump=1)
-    # batched: the whole trace for the policy's seed in one call
-    r = p.Sweep(p.Seed, 1, evhash, evclass, n_dump=1)
-    assert np.array_equal(r.delays, dl) and np.array_equal(r.faults, fl) and np.array_equal(r.stats, st)
-    # online: one decision per QueueEvent-sized call, on a sample of the trace
-    for i in range(0, 10_000, 97):
-        assert p.decide(events[i]) == (int(dl[0, i]), bool(fl[0, i]))
-    # QueueEvent delivers the decided action after the decided delay (non-blocking)
-    for i in range(8):
-        p.QueueEvent(events[i])
-    got = {}
-    for _ in range(8):
-        a = p.ActionChan().get(timeout=5)
-        got[a.Event().ID()] = a.Class()
-    for i in range(8):
-        assert got[events[i].ID()] == ("PacketFaultAction" if fl[0, i] else "EventAcceptanceAction")
-    # delays lie in [0.8 min, max) and prioritized entities in [0.8 min, 0.8 max)
-    pr = (evclass & _lib.NMZ_EV_PRIORITIZED).astype(bool)
-    assert dl[0][pr].min() >= 24_000_000 and dl[0][pr].max() < 80_000_000
-    assert dl[0][~pr].min() >= 30_000_000 and dl[0][~pr].max() < 100_000_000

@@ -100,34 +100,6 @@ def test_replayable_bucket_boundaries(ctx):
         assert np.array_equal(r.stats, st), n
 
 
-def test_replayable_full_size_properties(ctx):
-    """BASELINE configs[1] size (2^20 seeds x 4096 events): sampled bit-exact
-    parity + size-independent invariants."""
-    S, E, m = 1 << 20, 4096, 100_000_000
-    hints = zk_hints(E, np.random.default_rng(0x5EED))
-    seeds = [str(i) for i in range(S)]
-    p = Replayable()
-    p.MaxInterval = m
-    r = p.Sweep(seeds, hints, n_dump=8, k=64, ctx=ctx)
-    st = r.stats
-    assert (st["max_delay_ns"] >= 0).all() and (st["max_delay_ns"] < m).all()
-    assert (st["argmax_event"] < E).all()
-    assert (st["sum_delay_ns"] <= st["max_delay_ns"].astype(np.uint64) * np.uint64(E)).all()
-    # dump rows agree with the stats of the same seeds
-    assert np.array_equal(r.delays.sum(1).astype(np.uint64), st["sum_delay_ns"][:8])
-    assert np.array_equal(r.delays.max(1), st["max_delay_ns"][:8])
-    assert np.array_equal(r.delays.argmax(1), st["argmax_event"][:8])
-    # sampled oracle parity (first, last and scattered seeds)
-    idx = np.unique(np.concatenate([np.arange(64), np.arange(S - 64, S), RNG.integers(0, S, 256)]))
-    so, sb = O.to_csr([seeds[i] for i in idx])
-    ho, hb = O.to_csr(hints)
-    ost, _ = O.replayable_sweep(so, sb, ho, hb, m)
-    assert np.array_equal(st[idx], ost)
-    # top-k is consistent with the stats it was selected from
-    order = np.lexsort((np.arange(S), -st["sum_delay_ns"].astype(np.float64)))
-    assert r.topk["seed"].tolist() == order[:64].tolist()
-
-
 def test_replayable_device_plan_api(ctx):
     """nmz_replayable_plan_create + nmz_replayable_sweep_dev on resident buffers."""
     import torch
@@ -249,6 +221,35 @@ def test_random_rejection_path(ctx):
     assert max(nouts) >= 3
 
 
+@pytest.mark.parametrize("kind,mn,mx", [("ranged", 30_000_000, 100_000_000),   # K32 sweep form
+                                         ("ranged", 0, 3_000_000_000),          # 64-bit max form
+                                         ("fixed", 5_000_000, 5_000_000),       # K32, no delay draw
+                                         ("fixed", 3_000_000_000, 3_000_000_000)])
+@pytest.mark.parametrize("p", [0.1, 0.3, 0.5, 0.7, 0.9])
+def test_random_sweep_rejected_fault_draw(ctx, golden, kind, mn, mx, p):
+    """decide_sweep's two rarely-taken re-draw branches (csrc/random.hip): a ranged delay accepted and the
+    Intn(999) fault draw rejected (`slow |= v1 > INT31N_MAX`), and the fixed-duration class with a rejected fault
+    draw (`slow = v > INT31N_MAX`). The vectors (tests/golden/random_rejections.json, searched with the oracle)
+    force them; sweep path only (no dump, which goes through decide()), stats vs the oracle for every seed
+    around the vectors' seed, both entity classes, several thresholds."""
+    g = golden("random_rejections.json")
+    hits = np.array(g[kind], np.uint64)
+    fill = RNG.integers(0, 2**64, size=23, dtype=np.uint64)
+    eh = np.concatenate([fill[:7], hits, fill[7:15], hits, fill[15:]])
+    ec = np.full(len(eh), 2, np.uint8)
+    ec[7 + len(hits) + 8:7 + 2 * len(hits) + 8] = 3  # second copy prioritized
+    rp = Random()
+    rp.MinInterval, rp.MaxInterval, rp.FaultActionProbability = mn, mx, p
+    seed0 = g["seed"] - 100
+    r = rp.Sweep(seed0, 201, eh, ec, k=8, ctx=ctx)
+    st, _, _ = O.random_sweep(seed0, 201, eh, ec, O.random_params(mn, mx, p))
+    assert np.array_equal(r.stats, st)
+    assert np.array_equal(r.topk, O.topk_from_stats(st, seed0, 8))
+    # the vectors do take the re-draw: the seed's decisions on them draw one more Go output than usual
+    pr = O.random_params(mn, mx, p)
+    assert all(O.random_decide(g["seed"], int(h), 2, pr)[2] == (3 if kind == "ranged" else 2) for h in hits)
+
+
 def test_random_edge_cases(ctx):
     rp = Random()
     rp.MinInterval, rp.MaxInterval, rp.FaultActionProbability = 30_000_000, 100_000_000, 0.1
@@ -285,25 +286,6 @@ def test_random_event_chunks(ctx, E, mn, mx, p):
     assert np.array_equal(r.topk, O.topk_from_stats(st, seed0, 16))
     if p:
         assert (st["first_fault"][st["n_fault"] > 0] >= 1024).any()
-
-
-def test_random_config4_scale_sampled(ctx):
-    """configs[3] shape (16 entities, 10k events, p=0.1) at 2^18 seeds: sampled parity."""
-    E, S = 10_000, 1 << 18
-    eh = RNG.integers(0, 2**64, size=E, dtype=np.uint64)
-    ec = (np.where(np.arange(E) % 16 < 4, 1, 0) | 2).astype(np.uint8)
-    rp = Random()
-    rp.MinInterval, rp.MaxInterval, rp.FaultActionProbability = 30_000_000, 100_000_000, 0.1
-    r = rp.Sweep(1000, S, eh, ec, k=64, ctx=ctx)
-    st = r.stats
-    assert (st["flags"] == 0).all()
-    frac = st["n_fault"].mean() / E
-    assert 0.09 < frac < 0.11  # Intn(999) < 100 -> p = 100/999
-    for s in [0, 1, S // 2, S - 1]:
-        ost, _, _ = O.random_sweep(1000 + s, 1, eh, ec, O.random_params(30_000_000, 100_000_000, 0.1))
-        assert np.array_equal(st[s:s + 1], ost)
-    best = st[r.topk["seed"][0] - 1000]
-    assert best["n_fault"] == st["n_fault"].max()
 
 
 # ---------------------------------------------------------------- top-k
