@@ -156,6 +156,13 @@ int nmz_replayable_sweep_topk_dev(nmz_replayable_plan *plan, const uint32_t *d_s
                                   uint32_t k, nmz_sched_stats *d_stats, nmz_topk_entry *d_topk,
                                   void *stream);
 
+/* Online decisions (Replayable.QueueEvent -> determineInterval, replayablepolicy.go:100-126):
+ * delays[e] = the interval of seed (seed_len bytes) for each of n_events pending events' hints
+ * (CSR hint_off[n_events+1] into hint_bytes). No plan or tables: a batch of the events queued
+ * since the last call, one thread per event. Synchronous; scratch is owned by the context. */
+int nmz_replayable_decide(nmz_ctx *ctx, const uint8_t *seed, uint32_t seed_len, const uint32_t *hint_off,
+                          const uint8_t *hint_bytes, uint32_t n_events, int64_t max_interval_ns, int64_t *delays);
+
 /* ---- random policy sweep ------------------------------------------------
  * Seeds are the integers seed0 .. seed0+n_seeds-1. For seed s and event e
  * (evhash[e], evclass[e] = NMZ_EV_* bits) the decision is made by a fresh
@@ -170,6 +177,12 @@ int nmz_random_sweep(nmz_ctx *ctx, uint64_t seed0, uint64_t n_seeds, const uint6
                      const uint8_t *evclass, uint32_t n_events, const nmz_random_params *params,
                      nmz_sched_stats *stats, int64_t *delays, uint8_t *faults,
                      uint64_t n_dump_seeds, uint32_t k, nmz_topk_entry *topk);
+
+/* Online decisions (Random.QueueEvent -> makeActionForEvent, randompolicy.go:300-346): the delay and
+ * fault choice of one seed for each of n_events pending events, the same decision as
+ * nmz_random_sweep makes for that seed and event. No plan; synchronous. */
+int nmz_random_decide(nmz_ctx *ctx, uint64_t seed, const uint64_t *evhash, const uint8_t *evclass,
+                      uint32_t n_events, const nmz_random_params *params, int64_t *delays, uint8_t *faults);
 
 /* Device-resident variant: per-event tables are built once in the plan; the
  * sweep enqueues on `stream` and writes d_stats[n_seeds] (device memory). As for
@@ -229,6 +242,30 @@ int nmz_knn_merge_dev(nmz_ctx *ctx, const uint64_t *d_parts, uint32_t n_parts, u
  * reference interface. */
 #define NMZ_ED_NCOUNTERS 5
 int nmz_ed_plan_counters(nmz_ed_plan *plan, uint64_t *out, void *stream);
+
+/* ---- trace equality classes (nmz tools visualize) ------------------------
+ * Replaces the O(n^2) loops of cli/tools/visualize.go:51-172 (gnuplot): trace i is a
+ * repeat iff an earlier trace equals it.
+ *   entity == NULL: exact mode (seenBefore, :51-60) -- sequence equality of sym[], i.e.
+ *       SingleTrace.Equals / AreActionsSliceEqual (util/signal/misc.go:22-35) when sym[] are
+ *       action symbols (namazu_amd/historystorage.py).
+ *   entity != NULL: partial-order mode, the reference default (-po-reduction=true, :42;
+ *       createTracesPerEntity / tracesEqualInPO :62-124): entity[t] is the element's entity
+ *       id, dense per trace (< 16384), NMZ_NONE for actions without an event (skipped);
+ *       sym[] are event symbols (Event.Equals). Traces are equal iff every entity's projected
+ *       subsequence is equal.
+ * sig[2*n_traces]: 128-bit signature per trace (equal traces -> equal signatures; distinct
+ * ones collide with probability ~2^-128). first_equal[i] = the smallest j with sig_j == sig_i
+ * (j <= i), so the unique-trace curve of visualize is the running count of first_equal[i] == i. */
+int nmz_trace_signatures(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, const uint32_t *entity,
+                         uint32_t n_traces, uint64_t *sig);
+int nmz_unique_traces(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, const uint32_t *entity,
+                      uint32_t n_traces, uint32_t *first_equal);
+/* Device-resident variant: d_entity may be NULL (exact mode); max_entities bounds the entity ids;
+ * d_sig[2*n_traces] receives the signatures. Enqueued on `stream` (NULL = the context's). */
+int nmz_unique_traces_dev(nmz_ctx *ctx, const uint64_t *d_off, const uint64_t *d_sym, const uint32_t *d_entity,
+                          uint32_t n_traces, uint32_t max_entities, uint64_t *d_sig, uint32_t *d_first_equal,
+                          void *stream);
 
 #ifdef __cplusplus
 }

@@ -69,6 +69,8 @@ SIGNATURES = {
     "nmz_replayable_plan_destroy": (_int, [_P]),
     "nmz_replayable_sweep_dev": (_int, [_P, _P, _P, _u64, _P, _P]),
     "nmz_replayable_sweep_topk_dev": (_int, [_P, _P, _P, _u64, _u64, _u32, _P, _P, _P]),
+    "nmz_replayable_decide": (_int, [_P, _P, _u32, _P, _P, _u32, _i64, _P]),
+    "nmz_random_decide": (_int, [_P, _u64, _P, _P, _u32, _P, _P, _P]),
     "nmz_random_sweep": (_int, [_P, _u64, _u64, _P, _P, _u32, _P, _P, _P, _P, _u64, _u32, _P]),
     "nmz_random_plan_create": (_int, [_P, _P, _P, _u32, _P, _u64, ctypes.POINTER(_P)]),
     "nmz_random_plan_destroy": (_int, [_P]),
@@ -82,6 +84,9 @@ SIGNATURES = {
     "nmz_ed_allpairs_knn_shard_dev": (_int, [_P, _u32, _u32, _u32, _P, _P]),
     "nmz_knn_merge_dev": (_int, [_P, _P, _u32, _u32, _u32, _P, _P]),
     "nmz_ed_plan_counters": (_int, [_P, _P, _P]),
+    "nmz_trace_signatures": (_int, [_P, _P, _P, _P, _u32, _P]),
+    "nmz_unique_traces": (_int, [_P, _P, _P, _P, _u32, _P]),
+    "nmz_unique_traces_dev": (_int, [_P, _P, _P, _P, _u32, _u32, _P, _P, _P]),
     "nmz_topk_select_dev": (_int, [_P, _P, _u64, _u64, _u32, _P, _P]),
     "nmz_timing_enable": (_int, [_P, _int]),
     "nmz_timing_read": (_int, [_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),

@@ -391,6 +391,26 @@ __global__ __launch_bounds__(256) void k_random_dump(uint64_t seed0, uint64_t n_
     if (d.overflow) atomicOr(overflow, 1u);
 }
 
+// online decisions for one seed (QueueEvent): one thread per pending event, the direct form of k_random_dump
+// without a table -- FNV over le64(seed) || le64(evhash), Go's seed reduction, decide()
+__global__ __launch_bounds__(256) void k_random_decide(uint64_t seed, const uint64_t *__restrict__ evhash,
+                                                       const uint8_t *__restrict__ evclass, uint32_t n,
+                                                       RandomKParams P, int64_t *__restrict__ delays,
+                                                       uint8_t *__restrict__ faults, uint32_t *__restrict__ overflow) {
+    const uint32_t e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= n) return;
+    uint64_t h = seed_prefix(seed);
+    const uint64_t eh = evhash[e];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h = fnv_step(h, (uint32_t)(eh >> (8 * i)) & 0xff);
+    const uint32_t s = gorand::seed_reduce((int64_t)h);
+    const uint32_t cls = evclass[e];
+    const Decision d = decide(s, cls, P.cls[cls & NMZ_EV_PRIORITIZED], P.fault_threshold);
+    delays[e] = d.delay;
+    faults[e] = (uint8_t)d.fault;
+    if (d.overflow) atomicOr(overflow, 1u);
+}
+
 }  // namespace nmz
 
 struct nmz_random_plan {
@@ -646,6 +666,44 @@ int nmz_random_sweep(nmz_ctx *ctx, uint64_t seed0, uint64_t n_seeds, const uint6
             }
         }
     }
+    return NMZ_OK;
+}
+
+// Online decisions for one seed (Random.QueueEvent -> makeActionForEvent, randompolicy.go:300-346 +
+// util/queue/impl.go:94-128, under the DESIGN.md section 2 contract): a batch of n pending events, no plan.
+int nmz_random_decide(nmz_ctx *ctx, uint64_t seed, const uint64_t *evhash, const uint8_t *evclass, uint32_t n_events,
+                      const nmz_random_params *params, int64_t *delays, uint8_t *faults) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    RandomKParams kp;
+    NMZ_TRY(make_kparams(params, kp));
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    if (n_events == 0) return NMZ_OK;
+    NMZ_CHECK(evhash && evclass && delays && faults, "NULL argument");
+    for (uint32_t e = 0; e < n_events; ++e)
+        NMZ_CHECK((evclass[e] & ~(NMZ_EV_PRIORITIZED | NMZ_EV_FAULTABLE)) == 0,
+                  "evclass has unknown bits (ProcSetEvent decisions are out of scope)");
+    hipStream_t st = ctx->stream;
+    NMZ_TRY(ctx->buf[9].ensure(Carve::bytes_for(n_events, 8) * 2 + Carve::bytes_for(n_events, 1) * 2 +
+                               Carve::bytes_for(4, 4)));
+    Carve cv(ctx->buf[9].ptr);
+    uint64_t *d_eh = cv.take<uint64_t>(n_events);
+    int64_t *d_del = cv.take<int64_t>(n_events);
+    uint8_t *d_ec = cv.take<uint8_t>(n_events);
+    uint8_t *d_flt = cv.take<uint8_t>(n_events);
+    uint32_t *d_ovf = cv.take<uint32_t>(4);
+    NMZ_HIP(hipMemsetAsync(d_ovf, 0, 4, st));
+    NMZ_HIP(hipMemcpyAsync(d_eh, evhash, (uint64_t)n_events * 8, hipMemcpyHostToDevice, st));
+    NMZ_HIP(hipMemcpyAsync(d_ec, evclass, n_events, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_random_decide, dim3(ceil_div(n_events, 256)), dim3(256), 0, st, seed, d_eh, d_ec, n_events,
+                       kp, d_del, d_flt, d_ovf);
+    NMZ_HIP(hipGetLastError());
+    uint32_t ovf = 0;
+    NMZ_HIP(hipMemcpyAsync(delays, d_del, (uint64_t)n_events * 8, hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipMemcpyAsync(faults, d_flt, n_events, hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipMemcpyAsync(&ovf, d_ovf, 4, hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipStreamSynchronize(st));
+    if (ovf) return fail(NMZ_ERANGE, "a decision needed more than 607 Go rng outputs");
     return NMZ_OK;
 }
 

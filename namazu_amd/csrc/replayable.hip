@@ -929,4 +929,44 @@ int nmz_replayable_sweep(nmz_ctx *ctx, const uint32_t *seed_off, const uint8_t *
     return NMZ_OK;
 }
 
+// Online decisions for one seed (Replayable.QueueEvent -> determineInterval, replayablepolicy.go:100-126): a batch
+// of n pending events, one thread per event (k_replayable_dump: plain FNV over seed || hint, then % m). No plan:
+// a batch of a few events needs no correction tables, only the launch.
+int nmz_replayable_decide(nmz_ctx *ctx, const uint8_t *seed, uint32_t seed_len, const uint32_t *hint_off,
+                          const uint8_t *hint_bytes, uint32_t n_events, int64_t max_interval_ns, int64_t *delays) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    if (n_events == 0) return NMZ_OK;
+    NMZ_CHECK(hint_off && delays && (seed_len == 0 || seed), "NULL argument");
+    if (max_interval_ns == 0) {  // :101-104
+        for (uint32_t e = 0; e < n_events; ++e) delays[e] = 0;
+        return NMZ_OK;
+    }
+    for (uint32_t e = 0; e < n_events; ++e) NMZ_CHECK(hint_off[e] <= hint_off[e + 1], "hint offsets must not decrease");
+    const uint32_t hbytes = hint_off[n_events];
+    NMZ_CHECK(hbytes == 0 || hint_bytes, "hint_bytes is NULL");
+    hipStream_t st = ctx->stream;
+    NMZ_TRY(ctx->buf[8].ensure(Carve::bytes_for(2, 4) + Carve::bytes_for(seed_len + 1, 1) +
+                               Carve::bytes_for(n_events + 1, 4) + Carve::bytes_for(hbytes + 1, 1) +
+                               Carve::bytes_for(n_events, 8) + 256));
+    Carve cv(ctx->buf[8].ptr);
+    uint32_t *d_soff = cv.take<uint32_t>(2);
+    uint8_t *d_sb = cv.take<uint8_t>(seed_len + 1);
+    uint32_t *d_hoff = cv.take<uint32_t>(n_events + 1);
+    uint8_t *d_hb = cv.take<uint8_t>(hbytes + 1);
+    int64_t *d_out = cv.take<int64_t>(n_events);
+    const uint32_t soff[2] = {0, seed_len};
+    NMZ_HIP(hipMemcpyAsync(d_soff, soff, 8, hipMemcpyHostToDevice, st));
+    if (seed_len) NMZ_HIP(hipMemcpyAsync(d_sb, seed, seed_len, hipMemcpyHostToDevice, st));
+    NMZ_HIP(hipMemcpyAsync(d_hoff, hint_off, (n_events + 1) * 4, hipMemcpyHostToDevice, st));
+    if (hbytes) NMZ_HIP(hipMemcpyAsync(d_hb, hint_bytes, hbytes, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_replayable_dump, dim3(ceil_div(n_events, 256)), dim3(256), 0, st, d_soff, d_sb, (uint64_t)1,
+                       d_hoff, d_hb, n_events, (uint64_t)max_interval_ns, d_out);
+    NMZ_HIP(hipGetLastError());
+    NMZ_HIP(hipMemcpyAsync(delays, d_out, (uint64_t)n_events * 8, hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipStreamSynchronize(st));
+    return NMZ_OK;
+}
+
 }  // extern "C"

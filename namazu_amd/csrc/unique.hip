@@ -1,0 +1,298 @@
+// Trace equality classes on the GPU: the `nmz tools visualize` unique-trace count
+// (cli/tools/visualize.go:51-172), exact and partial-order reduced.
+//
+//   exact (seenBefore, :51-60):  SingleTrace.Equals, element-wise equality of the
+//       action sequence (util/signal/misc.go:22-35).
+//   partial order (seenBeforePOR / tracesEqualInPO, :62-136): each trace is projected
+//       per entity (createTracesPerEntity: the events of its actions grouped by
+//       EntityID(), in trace order, actions without an event skipped); two traces
+//       are equal iff they hold the same entities and, per entity, element-wise
+//       equal event sequences (Event.Equals).
+//
+// Both are equivalence relations, and the reference's loop keeps a trace iff no
+// earlier trace equals it, so trace i is a repeat iff some j < i is equal to it.
+//
+// Signature: a trace is the multiset {(s_e, r_e)} of its symbols with their rank:
+// the position for exact mode, the index among the same entity's elements for PO
+// mode. The event symbol already holds the entity (the event JSON carries it), so
+// for PO mode the multiset determines every per-entity sequence and vice versa.
+// A multiset is hashed by summing a 64-bit mix of each pair mod 2^64 (an additive
+// multiset hash, Clarke et al. 2003) under two independent mixes, plus the element
+// count: 128 bits per trace, order independent, so lanes can add in any order.
+// Equal traces always give equal signatures; distinct ones collide with
+// probability ~2^-128 per pair (the symbols themselves are 64-bit FNV event
+// hashes).
+//
+// k_trace_sig: one wave per trace, 64 elements per step. PO ranks come from
+// per-wave LDS counters indexed by the element's entity id (dense per trace,
+// assigned by the host while it reads the trace): the lanes of one entity within
+// a step are found with a ballot per distinct entity, rank = counter + number of
+// lower lanes in that ballot. Classes: radix sort of (sig hi, sig lo) with the
+// trace index as payload (stable, so equal signatures keep index order), then
+// first_equal[i] = the index at the start of i's run (max-scan of run heads).
+#include <hipcub/hipcub.hpp>
+
+#include "nmz_common.h"
+#include "nmz_internal.h"
+
+namespace nmz {
+
+constexpr uint32_t SIG_WAVES = 4;             // waves (traces) per workgroup
+constexpr uint32_t SIG_MAX_ENT_LDS = 4096;    // entity counters per wave at 4 waves per workgroup (64 KiB)
+constexpr uint32_t SIG_MAX_ENT = 16384;       // one wave per workgroup beyond that
+
+__device__ __forceinline__ uint64_t fmix64(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ULL;
+    x ^= x >> 33;
+    return x;
+}
+
+__device__ __forceinline__ uint64_t mix_a(uint64_t s, uint32_t r) {
+    return fmix64(s ^ fmix64((uint64_t)r + 0x9e3779b97f4a7c15ULL));
+}
+
+__device__ __forceinline__ uint64_t mix_b(uint64_t s, uint32_t r) {
+    return fmix64((s + 0x632be59bd9b4e019ULL) * 0x94d049bb133111ebULL ^ ((uint64_t)r << 32 | (r ^ 0x5bd1e995u)));
+}
+
+template <bool PO>
+__global__ __launch_bounds__(256) void k_trace_sig(const uint64_t *__restrict__ off, const uint64_t *__restrict__ sym,
+                                                   const uint32_t *__restrict__ ent, uint32_t N, uint32_t max_ent,
+                                                   uint32_t waves_per_block, uint64_t *__restrict__ sig) {
+    extern __shared__ uint32_t cnt_all[];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t t = blockIdx.x * waves_per_block + wv;
+    if (wv >= waves_per_block || t >= N) return;  // whole waves only: no block-wide barrier below
+    // volatile: lanes read counters other lanes of the wave wrote (LDS ops of one wave execute in order)
+    volatile uint32_t *cnt = cnt_all + (size_t)wv * max_ent;
+    if (PO)
+        for (uint32_t i = lane; i < max_ent; i += 64) cnt[i] = 0;
+    const uint64_t base = off[t], n = off[t + 1] - base;
+    uint64_t acc1 = 0, acc2 = 0;
+    uint32_t counted = 0;
+    const uint64_t below = (1ULL << lane) - 1;
+    for (uint64_t c = 0; c < n; c += 64) {
+        const uint64_t i = c + lane;
+        const bool valid = i < n;
+        const uint64_t s = valid ? sym[base + i] : 0;
+        uint32_t rank = (uint32_t)i;
+        bool take = valid;
+        if (PO) {
+            const uint32_t e = valid ? ent[base + i] : NMZ_NONE;
+            take = valid && e != NMZ_NONE;
+            bool todo = take;
+            uint64_t m = __ballot(todo);
+            while (m) {
+                const int leader = __ffsll((unsigned long long)m) - 1;
+                const uint32_t e0 = __shfl(e, leader, 64);
+                const uint64_t grp = __ballot(todo && e == e0);
+                const uint32_t before = cnt[e0];
+                if (todo && e == e0) {
+                    rank = before + (uint32_t)__popcll(grp & below);
+                    todo = false;
+                }
+                if ((int)lane == leader) cnt[e0] = before + (uint32_t)__popcll(grp);
+                m &= ~grp;
+            }
+        }
+        if (take) {
+            acc1 += mix_a(s, rank);
+            acc2 += mix_b(s, rank);
+            counted += 1;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        acc1 += __shfl_xor(acc1, o, 64);
+        acc2 += __shfl_xor(acc2, o, 64);
+        counted += __shfl_xor(counted, o, 64);
+    }
+    if (lane == 0) {
+        sig[2 * (uint64_t)t] = acc1 + fmix64((uint64_t)counted + 1);
+        sig[2 * (uint64_t)t + 1] = acc2 ^ fmix64(((uint64_t)counted << 1) | 1);
+    }
+}
+
+__global__ void k_sig_split(const uint64_t *__restrict__ sig, uint32_t N, uint64_t *__restrict__ lo,
+                            uint64_t *__restrict__ hi, uint32_t *__restrict__ idx) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < N) {
+        lo[i] = sig[2 * (uint64_t)i];
+        hi[i] = sig[2 * (uint64_t)i + 1];
+        idx[i] = i;
+    }
+}
+
+__global__ void k_gather_u64(const uint64_t *__restrict__ src, const uint32_t *__restrict__ idx, uint32_t N,
+                             uint64_t *__restrict__ dst) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < N) dst[p] = src[idx[p]];
+}
+
+// heads of runs of equal (hi, lo) in sorted order: start[p] = p at a head, 0 elsewhere (max-scanned below)
+__global__ void k_sig_heads(const uint64_t *__restrict__ lo, const uint64_t *__restrict__ hi_sorted,
+                            const uint32_t *__restrict__ idx_sorted, uint32_t N, uint32_t *__restrict__ start) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= N) return;
+    bool head = p == 0;
+    if (!head) {
+        // lo halves of sorted neighbours, read through their trace indices
+        head = hi_sorted[p] != hi_sorted[p - 1] || lo[idx_sorted[p]] != lo[idx_sorted[p - 1]];
+    }
+    start[p] = head ? p : 0;
+}
+
+__global__ void k_sig_first(const uint32_t *__restrict__ idx_sorted, const uint32_t *__restrict__ start, uint32_t N,
+                            uint32_t *__restrict__ first_equal) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < N) first_equal[idx_sorted[p]] = idx_sorted[start[p]];
+}
+
+static int sig_launch(const uint64_t *d_off, const uint64_t *d_sym, const uint32_t *d_ent, uint32_t N,
+                      uint32_t max_ent, uint64_t *d_sig, hipStream_t st) {
+    if (N == 0) return NMZ_OK;
+    if (!d_ent) {
+        hipLaunchKernelGGL(k_trace_sig<false>, dim3(ceil_div(N, SIG_WAVES)), dim3(64 * SIG_WAVES), 0, st, d_off, d_sym,
+                           nullptr, N, 0u, SIG_WAVES, d_sig);
+    } else {
+        NMZ_CHECK(max_ent <= SIG_MAX_ENT, "more than 16384 distinct entities in one trace");
+        const uint32_t me = max_ent ? max_ent : 1;
+        const uint32_t wpb = me <= SIG_MAX_ENT_LDS ? SIG_WAVES : 1;
+        hipLaunchKernelGGL(k_trace_sig<true>, dim3(ceil_div(N, wpb)), dim3(64 * wpb), (size_t)wpb * me * 4, st, d_off,
+                           d_sym, d_ent, N, me, wpb, d_sig);
+    }
+    NMZ_HIP(hipGetLastError());
+    return NMZ_OK;
+}
+
+// equality classes from signatures: first_equal[i] = smallest j with sig_j == sig_i
+static int classes_launch(nmz_ctx *ctx, const uint64_t *d_sig, uint32_t N, uint32_t *d_first, hipStream_t st) {
+    if (N == 0) return NMZ_OK;
+    size_t sort_bytes = 0, scan_bytes = 0;
+    NMZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (uint64_t *)nullptr, (uint64_t *)nullptr,
+                                               (uint32_t *)nullptr, (uint32_t *)nullptr, (int)N, 0, 64, st));
+    NMZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, scan_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                              hipcub::Max(), (int)N, st));
+    DevBuf &scr = ctx->buf[6];
+    NMZ_TRY(scr.ensure(4 * Carve::bytes_for(N, 8) + 4 * Carve::bytes_for(N, 4) +
+                       Carve::bytes_for(std::max(sort_bytes, scan_bytes) + 1, 1)));
+    Carve cv(scr.ptr);
+    uint64_t *lo = cv.take<uint64_t>(N), *hi = cv.take<uint64_t>(N);
+    uint64_t *k1 = cv.take<uint64_t>(N), *k2 = cv.take<uint64_t>(N);
+    uint32_t *idx = cv.take<uint32_t>(N), *v1 = cv.take<uint32_t>(N), *v2 = cv.take<uint32_t>(N);
+    uint32_t *start = cv.take<uint32_t>(N);
+    void *tmp = cv.take<char>(std::max(sort_bytes, scan_bytes) + 1);
+    const unsigned g = ceil_div(N, 256);
+    hipLaunchKernelGGL(k_sig_split, dim3(g), dim3(256), 0, st, d_sig, N, lo, hi, idx);
+    NMZ_HIP(hipGetLastError());
+    // LSD: by lo, then (stable) by hi -> order (hi, lo, index)
+    size_t b = sort_bytes;
+    NMZ_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, b, lo, k1, idx, v1, (int)N, 0, 64, st));
+    // hi keys in lo-sorted order
+    hipLaunchKernelGGL(k_gather_u64, dim3(g), dim3(256), 0, st, hi, v1, N, k2);
+    NMZ_HIP(hipGetLastError());
+    b = sort_bytes;
+    NMZ_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, b, k2, hi, v1, v2, (int)N, 0, 64, st));
+    // hi now holds the sorted hi keys, v2 the trace indices in (hi, lo, index) order
+    hipLaunchKernelGGL(k_sig_heads, dim3(g), dim3(256), 0, st, lo, hi, v2, N, start);
+    NMZ_HIP(hipGetLastError());
+    b = scan_bytes;
+    NMZ_HIP(hipcub::DeviceScan::InclusiveScan(tmp, b, start, start, hipcub::Max(), (int)N, st));
+    hipLaunchKernelGGL(k_sig_first, dim3(g), dim3(256), 0, st, v2, start, N, d_first);
+    NMZ_HIP(hipGetLastError());
+    return NMZ_OK;
+}
+
+}  // namespace nmz
+
+using namespace nmz;
+
+extern "C" {
+
+int nmz_trace_signatures(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, const uint32_t *entity,
+                         uint32_t n_traces, uint64_t *sig) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    if (n_traces == 0) return NMZ_OK;
+    NMZ_CHECK(off && sig, "NULL argument");
+    const uint64_t total = off[n_traces];
+    NMZ_CHECK(total == 0 || sym, "sym is NULL");
+    uint32_t max_ent = 0;
+    if (entity)
+        for (uint64_t i = 0; i < total; ++i)
+            if (entity[i] != NMZ_NONE) max_ent = std::max(max_ent, entity[i] + 1);
+    hipStream_t st = ctx->stream;
+    NMZ_TRY(ctx->buf[7].ensure(Carve::bytes_for(n_traces + 1, 8) + Carve::bytes_for(total + 1, 8) +
+                               Carve::bytes_for(total + 1, 4) + Carve::bytes_for(2 * (uint64_t)n_traces, 8)));
+    Carve cv(ctx->buf[7].ptr);
+    uint64_t *d_off = cv.take<uint64_t>(n_traces + 1);
+    uint64_t *d_sym = cv.take<uint64_t>(total + 1);
+    uint32_t *d_ent = cv.take<uint32_t>(total + 1);
+    uint64_t *d_sig = cv.take<uint64_t>(2 * (uint64_t)n_traces);
+    NMZ_HIP(hipMemcpyAsync(d_off, off, (n_traces + 1) * 8, hipMemcpyHostToDevice, st));
+    if (total) NMZ_HIP(hipMemcpyAsync(d_sym, sym, total * 8, hipMemcpyHostToDevice, st));
+    if (total && entity) NMZ_HIP(hipMemcpyAsync(d_ent, entity, total * 4, hipMemcpyHostToDevice, st));
+    NMZ_TRY(sig_launch(d_off, d_sym, entity ? d_ent : nullptr, n_traces, max_ent, d_sig, st));
+    NMZ_HIP(hipMemcpyAsync(sig, d_sig, 2 * (uint64_t)n_traces * 8, hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipStreamSynchronize(st));
+    return NMZ_OK;
+}
+
+int nmz_unique_traces(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, const uint32_t *entity,
+                      uint32_t n_traces, uint32_t *first_equal) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    if (n_traces == 0) return NMZ_OK;
+    NMZ_CHECK(off && first_equal, "NULL argument");
+    const uint64_t total = off[n_traces];
+    NMZ_CHECK(total == 0 || sym, "sym is NULL");
+    for (uint32_t i = 0; i < n_traces; ++i) NMZ_CHECK(off[i] <= off[i + 1], "offsets must be non-decreasing");
+    uint32_t max_ent = 0;
+    if (entity)
+        for (uint64_t i = 0; i < total; ++i)
+            if (entity[i] != NMZ_NONE) max_ent = std::max(max_ent, entity[i] + 1);
+    hipStream_t st = ctx->stream;
+    NMZ_TRY(ctx->buf[7].ensure(Carve::bytes_for(n_traces + 1, 8) + Carve::bytes_for(total + 1, 8) +
+                               Carve::bytes_for(total + 1, 4) + Carve::bytes_for(2 * (uint64_t)n_traces, 8) +
+                               Carve::bytes_for(n_traces, 4)));
+    Carve cv(ctx->buf[7].ptr);
+    uint64_t *d_off = cv.take<uint64_t>(n_traces + 1);
+    uint64_t *d_sym = cv.take<uint64_t>(total + 1);
+    uint32_t *d_ent = cv.take<uint32_t>(total + 1);
+    uint64_t *d_sig = cv.take<uint64_t>(2 * (uint64_t)n_traces);
+    uint32_t *d_first = cv.take<uint32_t>(n_traces);
+    NMZ_HIP(hipMemcpyAsync(d_off, off, (n_traces + 1) * 8, hipMemcpyHostToDevice, st));
+    if (total) NMZ_HIP(hipMemcpyAsync(d_sym, sym, total * 8, hipMemcpyHostToDevice, st));
+    if (total && entity) NMZ_HIP(hipMemcpyAsync(d_ent, entity, total * 4, hipMemcpyHostToDevice, st));
+    NMZ_TRY(sig_launch(d_off, d_sym, entity ? d_ent : nullptr, n_traces, max_ent, d_sig, st));
+    {
+        KernelTimer kt(ctx, st, "unique_classes");
+        NMZ_TRY(classes_launch(ctx, d_sig, n_traces, d_first, st));
+    }
+    NMZ_HIP(hipMemcpyAsync(first_equal, d_first, (uint64_t)n_traces * 4, hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipStreamSynchronize(st));
+    return NMZ_OK;
+}
+
+int nmz_unique_traces_dev(nmz_ctx *ctx, const uint64_t *d_off, const uint64_t *d_sym, const uint32_t *d_entity,
+                          uint32_t n_traces, uint32_t max_entities, uint64_t *d_sig, uint32_t *d_first_equal,
+                          void *stream) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    if (n_traces == 0) return NMZ_OK;
+    NMZ_CHECK(d_off && d_sig && d_first_equal, "NULL argument");
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    {
+        KernelTimer kt(ctx, st, "trace_sig");
+        NMZ_TRY(sig_launch(d_off, d_sym, d_entity, n_traces, max_entities, d_sig, st));
+    }
+    return classes_launch(ctx, d_sig, n_traces, d_first_equal, st);
+}
+
+}  // extern "C"

@@ -9,14 +9,24 @@ Mirrors nmz/historystorage:
     the latest trace excluded)         naive/naive.go:235-257
 and adds the optional SimilaritySearcher interface: banded edit
 distance k-NN over event-hash sequences, plus the `nmz tools visualize`
-unique-trace count (cli/tools/visualize.go:51-60,138-172) as distance-0
-detection. The gob-encoded `history`/`SearchModeInfo` files are not read;
-the per-action JSON files carry the same events.
+unique-trace count (cli/tools/visualize.go:51-172), exact and partial-order
+reduced. The gob-encoded `history`/`SearchModeInfo` files are not read; the
+per-action JSON files (naive.go:65-80) carry the same actions and events.
 
-Trace symbols (build-defined): the FNV-1a 64 of the canonical
-JSON of each action's event without "uuid" (Event.Equals semantics); actions
-without an event file use their own JSON without "uuid"/"event_uuid".
-Every distance is computed by libnmz_gpu.so.
+Two symbol streams per stored trace (build-defined), each the FNV-1a
+64 of a canonical JSON (Go encoding/json form, namazu_amd/signal.py):
+  * action symbols: the action's map without "uuid" -- Action.Equals
+    (BasicSignal.EqualsSignal ignores only uuid and arrival time, signal.go:174-186),
+    so "event_uuid" counts wherever the layout puts it (top level since
+    action_accept_event.go:40; under "option" in the 2015 example traces).
+    Search / SearchWithConverter and the exact unique count compare these
+    (AreActionsSliceEqual, util/signal/misc.go:22-35). Actions of different runs
+    carry different event uuids, so -- as in the reference -- they never match.
+  * event symbols: the action's event without "uuid" -- Event.Equals. The
+    similarity search (SearchSimilar, AllPairsKNN) and the partial-order unique
+    count compare these; an action without an event file uses its action symbol
+    there, and has no entity (skipped by the PO projection, visualize.go:67-76).
+Every comparison runs in libnmz_gpu.so.
 """
 import ctypes
 import glob
@@ -34,24 +44,37 @@ STORAGE_TOML = "config.toml"  # historystorage.go:28
 
 
 class SingleTrace:
-    """util/trace.SingleTrace: the stored action sequence (events of each action)."""
+    """util/trace.SingleTrace: the stored action sequence.
 
-    def __init__(self, symbols, events=None):
+    symbols         event symbols (Event.Equals; SimilaritySearcher)
+    action_symbols  action symbols (Action.Equals; Equals, Search) -- default: symbols
+    entities        EntityID() of each action's event, None for an action without one
+    events          the events (signal.Event) or None"""
+
+    def __init__(self, symbols, events=None, action_symbols=None, entities=None):
         self.symbols = np.asarray(symbols, np.uint64)
         self.events = events or []
+        self.action_symbols = self.symbols if action_symbols is None else np.asarray(action_symbols, np.uint64)
+        self.entities = entities if entities is not None else [None] * len(self.symbols)
 
     def __len__(self):
         return len(self.symbols)
 
     def Equals(self, other):
-        return len(self) == len(other) and bool(np.array_equal(self.symbols, other.symbols))
+        """trace.go:29-31 -> AreActionsSliceEqual (misc.go:22-35): equal length, element-wise Action.Equals."""
+        return len(self.action_symbols) == len(other.action_symbols) and \
+            bool(np.array_equal(self.action_symbols, other.action_symbols))
 
 
-def _action_symbol(action_json):
-    m = {k: v for k, v in action_json.items() if k != "uuid"}
-    if isinstance(m.get("option"), dict):
-        m["option"] = {k: v for k, v in m["option"].items() if k != "event_uuid"}
-    return fnv1a64(go_json(m).encode())
+def action_symbol(action_json):
+    """Symbol of an action map: FNV-1a 64 of its canonical JSON without "uuid" (EqualsSignal keeps every
+    other key, including "event_uuid" at whichever level it is stored)."""
+    return fnv1a64(go_json({k: v for k, v in action_json.items() if k != "uuid"}).encode())
+
+
+def action_symbols(actions):
+    """[]Action (signal.Action objects or JSON maps) -> uint64 action symbols."""
+    return np.array([action_symbol(a.JSONMap() if hasattr(a, "JSONMap") else a) for a in actions], np.uint64)
 
 
 class TraceSet:
@@ -109,17 +132,23 @@ class Naive(HistoryStorage):
             return None, FileNotFoundError(adir)
         idx = sorted(int(m.group(1)) for f in os.listdir(adir)
                      if (m := re.fullmatch(r"(\d+)\.action\.json", f)))
-        syms, evs = [], []
+        syms, asyms, ents, evs = [], [], [], []
         for n in idx:
+            with open(os.path.join(adir, f"{n}.action.json")) as f:
+                asym = action_symbol(json.load(f))
+            asyms.append(asym)
             ep = os.path.join(adir, f"{n}.event.json")
-            if os.path.exists(ep):
-                ev = Event.from_json(open(ep).read())
+            if os.path.exists(ep):  # recordAction writes it iff act.Event() != nil (naive.go:72-79)
+                with open(ep) as f:
+                    ev = Event.from_json(f.read())
                 syms.append(ev.evhash())
+                ents.append(ev.EntityID())
                 evs.append(ev)
             else:
-                syms.append(_action_symbol(json.load(open(os.path.join(adir, f"{n}.action.json")))))
+                syms.append(asym)
+                ents.append(None)
                 evs.append(None)
-        return SingleTrace(syms, evs), None
+        return SingleTrace(syms, evs, action_symbols=asyms, entities=ents), None
 
     def IsSuccessful(self, i):
         try:
@@ -133,39 +162,58 @@ class Naive(HistoryStorage):
         except Exception as e:
             return 0, e
 
-    def load_all(self):
-        traces = []
+    def traces(self):
+        out = []
         for i in range(self.NrStoredHistories()):
             t, err = self.GetStoredHistory(i)
             if err is not None:
                 raise RuntimeError(f"failed to get history {i}: {err}")  # naive.go:241 panics
-            traces.append(t.symbols)
-        return TraceSet(traces)
+            out.append(t)
+        return out
+
+    def load_all(self):
+        """Event-symbol TraceSet of every stored trace (the SimilaritySearcher's input)."""
+        return TraceSet([t.symbols for t in self.traces()])
 
     # ---- search surface (GPU) ------------------------------------------------
     def SearchWithConverter(self, prefix, converter):
-        """naive.go:235-252: ids i < NrStoredHistories-1 whose converted trace equals prefix."""
+        """naive.go:235-252: ids i < NrStoredHistories-1 (the latest trace is excluded, :238) with
+        len(trace) >= len(prefix) whose converted trace equals `prefix` under AreActionsSliceEqual
+        (equal length, element-wise Action.Equals: action symbols). `prefix`: a SingleTrace, a list of
+        actions (signal.Action or JSON maps), or action symbols; `converter`: SingleTrace -> SingleTrace
+        (the reference's func([]Action) []Action)."""
         n = self.NrStoredHistories() - 1
         if n <= 0:
             return []
+        if isinstance(prefix, SingleTrace):
+            p = prefix.action_symbols
+        elif len(prefix) and (hasattr(prefix[0], "JSONMap") or isinstance(prefix[0], dict)):
+            p = action_symbols(prefix)
+        else:
+            p = np.asarray(prefix, np.uint64)
         cands = []
         for i in range(n):
             t, err = self.GetStoredHistory(i)
             if err is not None:
                 raise RuntimeError(f"failed to get history {i}: {err}")
-            if len(t) < len(prefix):
+            if len(t) < len(p):
                 continue
             cands.append((i, converter(t)))
         if not cands:
             return []
-        p = prefix.symbols if isinstance(prefix, SingleTrace) else np.asarray(prefix, np.uint64)
-        ts = TraceSet([p] + [c.symbols for _, c in cands])
+        ts = TraceSet([p] + [c.action_symbols for _, c in cands])
         pairs = np.array([[0, j + 1] for j in range(len(cands))], np.uint32)
-        d = ed_pairs(ts, pairs, band=0)
+        d = ed_pairs(ts, pairs, band=0)  # band 0: 0 iff equal length and element-wise equal
         return [cands[j][0] for j in range(len(cands)) if d[j] == 0]
 
     def Search(self, prefix):
+        """naive.go:254-257: SearchWithConverter with the identity converter."""
         return self.SearchWithConverter(prefix, lambda t: t)
+
+    def UniqueTraceCurve(self, po_reduction=True):
+        """`nmz tools visualize -mode gnuplot` (visualize.go:138-172): nrUniques after each stored trace;
+        po_reduction defaults to true as the flag does (:42)."""
+        return unique_trace_curve(self.traces(), po_reduction=po_reduction)
 
     # ---- SimilaritySearcher ----------------------------------------------------
     def SearchSimilar(self, trace, k, band):
@@ -224,14 +272,41 @@ def allpairs_knn(ts, k, band, ctx=None):
     return ids, ds
 
 
-def unique_trace_curve(ts, ctx=None):
-    """visualize.go gnuplot mode: after i+1 traces, how many distinct traces
-    (SingleTrace.Equals) have been seen. A trace is a repeat iff its nearest
-    neighbour is at distance 0 with a smaller id (kNN ties break by id)."""
+def po_inputs(traces):
+    """Partial-order projection inputs of SingleTraces: CSR of event symbols and per-element entity ids,
+    dense per trace in order of first appearance (the kernel needs per-trace counters only: an event
+    symbol already determines its entity), NMZ_NONE for actions without an event."""
+    ts = TraceSet([t.symbols for t in traces])
+    ent = np.full(max(int(ts.off[-1]), 1), _lib.NMZ_NONE, np.uint32)
+    pos = 0
+    for t in traces:
+        ids = {}
+        for e in t.entities:
+            if e is not None:
+                ent[pos] = ids.setdefault(e, len(ids))
+            pos += 1
+    return ts, ent
+
+
+def first_equal(traces, po_reduction=True, ctx=None):
+    """first_equal[i] = the smallest j with trace j equal to trace i (exact: Equals on action symbols;
+    PO: tracesEqualInPO on per-entity event sequences), computed by nmz_unique_traces."""
+    ctx = ctx or _lib.default_context()
+    if isinstance(traces, TraceSet):
+        ts, ent = traces, None
+    elif po_reduction:
+        ts, ent = po_inputs(traces)
+    else:
+        ts, ent = TraceSet([t.action_symbols for t in traces]), None
     n = len(ts)
-    if n == 0:
-        return []
-    ids, ds = allpairs_knn(ts, 1, 0, ctx=ctx) if n > 1 else (np.full((1, 1), _lib.NMZ_NONE),
-                                                              np.full((1, 1), _lib.NMZ_NONE))
-    seen_before = (ds[:, 0] == 0) & (ids[:, 0] < np.arange(n))
-    return list(np.cumsum(~seen_before).astype(int))
+    out = np.zeros(max(n, 1), np.uint32)
+    _lib.check(_lib.load().nmz_unique_traces(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), _lib.ptr(ent), n,
+                                             _lib.ptr(out)))
+    return out[:n]
+
+
+def unique_trace_curve(traces, po_reduction=True, ctx=None):
+    """visualize.go gnuplot mode (:138-172): after trace i, how many distinct traces have been seen.
+    traces: SingleTraces (exact or PO mode), or a TraceSet (exact mode over its symbols)."""
+    fe = first_equal(traces, po_reduction, ctx)
+    return list(np.cumsum(fe == np.arange(len(fe))).astype(int))

@@ -101,11 +101,17 @@ def go_json(v) -> str:
 
 
 class Action:
-    def __init__(self, cls, entity, event=None, option=None):
+    """Map-based action (BasicAction). The map follows the reference's constructors: InitSignal's keys
+    (signal.go:80-87) plus, for actions tied to an event (EventAcceptanceAction, PacketFaultAction,
+    FilesystemFaultAction: action_accept_event.go:40, action_fault_packet.go:43,
+    action_fault_filesystem.go:43), a top-level "event_uuid". NopAction keeps the event only as its
+    cause (action_nop.go:30-39), not in the map."""
+
+    def __init__(self, cls, entity, event=None, option=None, record_event_uuid=True):
         self.m = {"class": cls, "entity": entity, "type": "action",
                   "uuid": str(_uuid.uuid4()), "option": dict(option or {})}
-        if event is not None:
-            self.m["option"]["event_uuid"] = event.ID()
+        if event is not None and record_event_uuid:
+            self.m["event_uuid"] = event.ID()
         self._event = event
 
     def Class(self):
@@ -168,7 +174,7 @@ class Event:
     def DefaultAction(self):
         if self.Deferred():
             return Action("EventAcceptanceAction", self.EntityID(), self)
-        return Action("NopAction", self.EntityID(), self)
+        return Action("NopAction", self.EntityID(), self, record_event_uuid=False)
 
     def DefaultFaultAction(self):
         cls = FAULTABLE_CLASSES.get(self.Class())

@@ -258,3 +258,59 @@ def ed_allpairs_knn(off, sym, w, k, nthreads=0):
                                _p(np.ascontiguousarray(sym, np.uint64)), n, w, k, _p(ids),
                                _p(ds), nthreads)
     return ids, ds
+
+
+# ---------------------------------------------------------------- visualize uniqueness (pure Python, literal)
+def unique_curve_exact(traces):
+    """`nmz tools visualize` without PO reduction (cli/tools/visualize.go:51-60,138-172): for i in order,
+    seenBefore(uniqueTraces, trace_i) = any stored unique trace Equals it (SingleTrace.Equals ->
+    AreActionsSliceEqual: equal length + element-wise Action.Equals, util/signal/misc.go:22-35).
+    traces: sequences of action symbols (equal symbols <=> Action.Equals). Returns the printed
+    nrUniques column, one entry per trace."""
+    uniques, out = [], []
+    for t in traces:
+        t = [int(x) for x in t]
+        seen = False
+        for u in uniques:  # seenBefore
+            if len(u) == len(t) and all(a == b for a, b in zip(u, t)):
+                seen = True
+                break
+        if not seen:
+            uniques.append(t)
+        out.append(len(uniques))
+    return out
+
+
+def unique_curve_po(traces):
+    """`nmz tools visualize` with PO reduction, the default (visualize.go:42,62-136,158-159).
+    traces: sequences of (entity, event_symbol) per action, entity None for an action without an event
+    (act.Event() == nil: skipped by createTracesPerEntity). Equal event symbols <=> Event.Equals."""
+    def per_entity(t):  # createTracesPerEntity (:62-79)
+        m = {}
+        for ent, ev in t:
+            if ent is not None:
+                m.setdefault(ent, []).append(int(ev))
+        return m
+
+    def equal_in_po(a, b):  # tracesEqualInPO (:81-124)
+        ea, eb = sorted(a), sorted(b)
+        if len(ea) != len(eb):
+            return False
+        for x, y in zip(ea, eb):
+            if x != y:
+                return False
+        for ent in ea:
+            if len(a[ent]) != len(b[ent]):
+                return False
+            for x, y in zip(a[ent], b[ent]):
+                if x != y:
+                    return False
+        return True
+
+    uniques, out = [], []
+    for t in traces:
+        u = per_entity(t)
+        if not any(equal_in_po(v, u) for v in uniques):  # seenBeforePOR (:126-136)
+            uniques.append(u)
+        out.append(len(uniques))
+    return out

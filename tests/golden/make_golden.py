@@ -21,6 +21,10 @@ Provenance of each fixture:
                       oracle's all-pairs distances. Only the hashes are kept,
                       not the event files.
   ed_kat.json         textbook Levenshtein pairs
+  zk_store.json       the same 4 stored traces as data: every action map
+                      (N.action.json) and event map (N.event.json) in order,
+                      so tests can rebuild the naive store and check Search /
+                      visualize against the reference's map-equality rule
 """
 import glob
 import json
@@ -107,6 +111,20 @@ def main():
     dump("zk_traces.json", {"source": "reference example traces reduced to evhash sequences; distances from the "
                             "oracle", "traces": traces, "levenshtein": full, "banded": band,
                             "distinct_events": distinct})
+
+    store = []
+    for d in sorted(glob.glob(os.path.join(base, "0000000?"))):
+        files = glob.glob(os.path.join(d, "actions", "*.action.json"))
+        idx = sorted(int(re.match(r"(\d+)\.action\.json", os.path.basename(p)).group(1)) for p in files)
+        acts, evs = [], []
+        for i in idx:
+            with open(os.path.join(d, "actions", f"{i}.action.json")) as f:
+                acts.append(json.load(f))
+            ep = os.path.join(d, "actions", f"{i}.event.json")
+            evs.append(json.load(open(ep)) if os.path.exists(ep) else None)
+        store.append({"dir": os.path.relpath(d, REF), "actions": acts, "events": evs})
+    dump("zk_store.json", {"source": "reference example traces (data), action and event maps in order",
+                           "traces": store})
 
     kat = [("kitten", "sitting", 3), ("flaw", "lawn", 2), ("", "abc", 3), ("abc", "", 3), ("", "", 0),
            ("intention", "execution", 5), ("namazu", "namazu", 0), ("gumbo", "gambol", 2)]
