@@ -14,10 +14,22 @@ Error behaviour follows the Go code: LoadConfig *returns* an error value
 
 Every delay / fault decision -- batch sweeps and the online QueueEvent path --
 is computed by libnmz_gpu.so on the GPU. There is no CPU decision path.
+
+QueueEvent never blocks (randompolicy_test.go:112-118 asserts it): it appends the
+event to a pending list and returns. A decision thread takes every event queued
+since its last launch and decides the whole batch in one call
+(nmz_random_decide / nmz_replayable_decide); a delivery thread puts each action
+on ActionChan at its enqueue time + its delay, as the reference's per-event
+goroutine + time.After does (replayablepolicy.go:121-125, util/queue/impl.go:110-128).
 """
+import collections
+import ctypes
+import heapq
+import itertools
 import os
 import queue
 import threading
+import time
 
 import numpy as np
 
@@ -66,6 +78,92 @@ class SweepResult:
         self.topk = topk
 
 
+class OnlineDecider:
+    """The QueueEvent engine: pending events -> batched GPU decisions -> timed delivery.
+
+    decide_batch(events) -> [(delay_ns, action)] runs on the decision thread. latencies_ns holds the
+    enqueue-to-decided time of recent events (bench.py reports p50/p99); batch_sizes the sizes of recent
+    launches. A decision failure is kept and raised by the next submit(), where a Go policy would panic
+    (randompolicy.go:343, replayablepolicy.go:120)."""
+
+    def __init__(self, decide_batch, deliver, history=100_000):
+        self._decide_batch = decide_batch
+        self._deliver = deliver
+        self._pending = []
+        self._cv = threading.Condition()
+        self._heap = []
+        self._hcv = threading.Condition()
+        self._seq = itertools.count()
+        self.latencies_ns = collections.deque(maxlen=history)
+        self.batch_sizes = collections.deque(maxlen=history)
+        self.error = None
+        self._started = False
+        self._n_in = 0
+        self._n_decided = 0
+
+    def _start(self):
+        for fn in (self._decide_loop, self._deliver_loop):
+            threading.Thread(target=fn, daemon=True).start()
+        self._started = True
+
+    def submit(self, event):
+        if self.error is not None:
+            raise RuntimeError(f"explore policy decision failed: {self.error}") from self.error
+        with self._cv:
+            if not self._started:
+                self._start()
+            self._pending.append((time.monotonic_ns(), event))
+            self._n_in += 1
+            self._cv.notify()
+
+    def wait_decided(self, timeout=10.0):
+        """Block until every submitted event has been decided (tests and bench only)."""
+        end = time.monotonic() + timeout
+        with self._cv:
+            while self._n_decided < self._n_in and self.error is None:
+                if not self._cv.wait(max(end - time.monotonic(), 0)) and time.monotonic() >= end:
+                    return False
+        return self.error is None
+
+    def _decide_loop(self):
+        while True:
+            with self._cv:
+                while not self._pending:
+                    self._cv.wait()
+                batch, self._pending = self._pending, []
+            try:
+                out = self._decide_batch([e for _, e in batch])
+            except Exception as e:  # noqa: BLE001 -- surfaced by the next submit()
+                self.error = e
+                with self._cv:
+                    self._cv.notify_all()
+                return
+            now = time.monotonic_ns()
+            self.batch_sizes.append(len(batch))
+            with self._hcv:
+                for (t0, _), (delay, action) in zip(batch, out):
+                    self.latencies_ns.append(now - t0)
+                    heapq.heappush(self._heap, (t0 + max(int(delay), 0), next(self._seq), action))
+                self._hcv.notify()
+            with self._cv:
+                self._n_decided += len(batch)
+                self._cv.notify_all()
+
+    def _deliver_loop(self):
+        while True:
+            with self._hcv:
+                while True:
+                    if self._heap:
+                        wait = (self._heap[0][0] - time.monotonic_ns()) / 1e9
+                        if wait <= 0:
+                            _, _, action = heapq.heappop(self._heap)
+                            break
+                        self._hcv.wait(wait)
+                    else:
+                        self._hcv.wait()
+            self._deliver(action)
+
+
 class ExplorePolicy:
     """explorepolicy.ExplorePolicy."""
 
@@ -74,6 +172,7 @@ class ExplorePolicy:
     def __init__(self, device=0):
         self._device = device
         self._action_ch = queue.Queue()  # unbuffered Go channel -> thread-safe queue
+        self.online = OnlineDecider(self._decide_batch, self._action_ch.put)
 
     def Name(self):
         return self.NAME
@@ -88,16 +187,14 @@ class ExplorePolicy:
         return self._action_ch
 
     def QueueEvent(self, event):
+        """Non-blocking: the decision and the delayed delivery happen on the policy's threads."""
+        self.online.submit(event)
+
+    def _decide_batch(self, events):
         raise NotImplementedError
 
     def _ctx(self):
         return _lib.default_context(self._device)
-
-    def _deliver_after(self, delay_ns, action):
-        # goroutine + time.After(interval); QueueEvent never blocks
-        t = threading.Timer(max(delay_ns, 0) / 1e9, self._action_ch.put, args=(action,))
-        t.daemon = True
-        t.start()
 
 
 # ----------------------------------------------------------------- replayable
@@ -147,14 +244,24 @@ class Replayable(ExplorePolicy):
             int(self.MaxInterval), _lib.ptr(stats), _lib.ptr(delays), n_dump, k, _lib.ptr(topk)))
         return SweepResult(stats, delays=delays, topk=topk)
 
-    def determineInterval(self, event):
-        """Single decision, computed on the GPU."""
-        r = self.Sweep([self.Seed], [event.ReplayHint()], n_dump=1)
-        return int(r.delays[0, 0])
+    def decide_intervals(self, events, ctx=None):
+        """determineInterval for a batch of events under self.Seed (nmz_replayable_decide)."""
+        ctx = ctx or self._ctx()
+        hoff, hb = to_csr([e.ReplayHint() for e in events])
+        seed = self.Seed.encode() if isinstance(self.Seed, str) else bytes(self.Seed)
+        sb = np.frombuffer(seed, np.uint8).copy() if seed else np.zeros(1, np.uint8)
+        out = np.zeros(max(len(events), 1), np.int64)
+        _lib.check(_lib.load().nmz_replayable_decide(ctx.handle, _lib.ptr(sb), len(seed), _lib.ptr(hoff),
+                                                     _lib.ptr(hb), len(events), int(self.MaxInterval),
+                                                     _lib.ptr(out)))
+        return out[:len(events)]
 
-    def QueueEvent(self, event):
-        interval = self.determineInterval(event)
-        self._deliver_after(interval, event.DefaultAction())
+    def determineInterval(self, event):
+        """replayablepolicy.go:100-114, one decision on the GPU."""
+        return int(self.decide_intervals([event])[0])
+
+    def _decide_batch(self, events):
+        return list(zip(self.decide_intervals(events).tolist(), [e.DefaultAction() for e in events]))
 
 
 # ----------------------------------------------------------------- random
@@ -252,23 +359,33 @@ class Random(ExplorePolicy):
         delays = np.zeros((n_dump, e), np.int64) if n_dump else None
         faults = np.zeros((n_dump, e), np.uint8) if n_dump else None
         topk = np.zeros(k, _lib.TOPK_DTYPE) if k else None
-        import ctypes
         _lib.check(_lib.load().nmz_random_sweep(
             ctx.handle, int(seed0), int(n_seeds), _lib.ptr(evhash), _lib.ptr(evclass), e,
             ctypes.byref(p), _lib.ptr(stats), _lib.ptr(delays), _lib.ptr(faults), n_dump, k,
             _lib.ptr(topk)))
         return SweepResult(stats, delays=delays, faults=faults, topk=topk)
 
+    def decide_events(self, events, ctx=None):
+        """(delays int64[n], faults bool[n]) of a batch of events under self.Seed (nmz_random_decide)."""
+        ctx = ctx or self._ctx()
+        h, c = self.event_inputs(events)
+        n = len(events)
+        delays = np.zeros(max(n, 1), np.int64)
+        faults = np.zeros(max(n, 1), np.uint8)
+        p = self.params()
+        _lib.check(_lib.load().nmz_random_decide(ctx.handle, int(self.Seed), _lib.ptr(h), _lib.ptr(c), n,
+                                                 ctypes.byref(p), _lib.ptr(delays), _lib.ptr(faults)))
+        return delays[:n], faults[:n].astype(bool)
+
     def decide(self, event):
         """(delay_ns, fault) for one event under self.Seed, on the GPU."""
-        h, c = self.event_inputs([event])
-        r = self.Sweep(self.Seed, 1, h, c, n_dump=1)
-        return int(r.delays[0, 0]), bool(r.faults[0, 0])
+        d, f = self.decide_events([event])
+        return int(d[0]), bool(f[0])
 
-    def QueueEvent(self, event):
-        delay, fault = self.decide(event)
-        action = event.DefaultFaultAction() if fault else event.DefaultAction()
-        self._deliver_after(delay, action)
+    def _decide_batch(self, events):
+        d, f = self.decide_events(events)
+        return [(int(dl), e.DefaultFaultAction() if fl else e.DefaultAction())
+                for dl, fl, e in zip(d.tolist(), f.tolist(), events)]
 
 
 RegisterKnownExplorePolicies()

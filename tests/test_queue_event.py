@@ -1,0 +1,173 @@
+"""QueueEvent / ActionChan: the reference's send/receive harness (util/explorepolicytester/explorepolicytester.go:32-68,
+randompolicy_test.go:104-118, replayablepolicy_test.go:41-110) over the non-blocking online engine.
+
+CPU: OnlineDecider's host logic with a stand-in decision function (a slow one: QueueEvent must not wait for it),
+delivery order (delay, then FIFO), and failure propagation. GPU: the random and replayable policies through
+QueueEvent with the decisions made by nmz_random_decide / nmz_replayable_decide, against the oracle."""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from namazu_amd import explorepolicy as ep
+from namazu_amd.config import Config
+from namazu_amd.signal import Event
+
+
+def packet_event(i, entities):
+    """testutil.NewPacketEvent (util/test/testutil.go:33-38): entity-(i % entities), option {"n": i}."""
+    ent = f"entity-{i % entities}"
+    return Event.packet(ent, ent, f"entity-{(i + 1) % entities}", {"n": i}, replay_hint=f"hint-{ent}-{i}")
+
+
+def send_receive(policy, n, entities, concurrent, timeout=10.0):
+    """XTestPolicyWithPacketEvent: send n events (QueueEvent), receive n actions; returns
+    (events, actions, the longest QueueEvent call in seconds)."""
+    events = [packet_event(i, entities) for i in range(n)]
+    got, longest = [], [0.0]
+
+    def sender():
+        for ev in events:
+            t0 = time.perf_counter()
+            policy.QueueEvent(ev)
+            longest[0] = max(longest[0], time.perf_counter() - t0)
+
+    def receiver():
+        for _ in range(n):
+            got.append(policy.ActionChan().get(timeout=timeout))
+
+    if concurrent:
+        ts = [threading.Thread(target=sender), threading.Thread(target=receiver)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    else:
+        sender()
+        receiver()
+    assert len(got) == n
+    return events, got, longest[0]
+
+
+# ------------------------------------------------------------------ CPU: host logic
+class _Slow:
+    """Stand-in decision function: 50 ms per batch, delay = 5 ms x the event's "n" option."""
+
+    def __init__(self):
+        self.batches = []
+
+    def __call__(self, events):
+        self.batches.append(len(events))
+        time.sleep(0.05)
+        return [(5_000_000 * e.m["option"]["n"], e.DefaultAction()) for e in events]
+
+
+def test_queue_event_never_blocks_on_a_slow_decision():
+    out = []
+    slow = _Slow()
+    d = ep.OnlineDecider(slow, out.append)
+    events = [packet_event(i, 2) for i in range(20)]
+    t0 = time.perf_counter()
+    for ev in events:
+        d.submit(ev)
+    assert time.perf_counter() - t0 < 0.02  # 20 submits while the first 50 ms decision runs
+    assert d.wait_decided(5)
+    assert sum(slow.batches) == 20 and len(slow.batches) < 20  # later events were batched together
+    deadline = time.time() + 5
+    while len(out) < 20 and time.time() < deadline:
+        time.sleep(0.01)
+    # delivered by due time = enqueue + delay: here in event order (delays grow with n)
+    assert [a.Event().m["option"]["n"] for a in out] == list(range(20))
+    assert len(d.latencies_ns) == 20 and min(d.latencies_ns) > 0
+
+
+def test_equal_delays_deliver_fifo_and_failures_surface():
+    out = []
+    d = ep.OnlineDecider(lambda evs: [(0, e.DefaultAction()) for e in evs], out.append)
+    events = [packet_event(i, 3) for i in range(200)]
+    for ev in events:
+        d.submit(ev)
+    assert d.wait_decided(5)
+    deadline = time.time() + 5
+    while len(out) < 200 and time.time() < deadline:
+        time.sleep(0.01)
+    assert [a.Event().ID() for a in out] == [e.ID() for e in events]  # fixed duration: FIFO (impl.go:117-119)
+
+    def boom(evs):
+        raise ValueError("no device")
+    bad = ep.OnlineDecider(boom, out.append)
+    bad.submit(events[0])
+    assert not bad.wait_decided(5)
+    with pytest.raises(RuntimeError, match="no device"):
+        bad.submit(events[1])
+
+
+# ------------------------------------------------------------------ GPU
+def _random_policy():
+    p = ep.Random()
+    cfg = Config({"explorePolicy": "random", "explorePolicyParam": {
+        "minInterval": "0ms", "maxInterval": "30ms", "faultActionProbability": 0.3, "seed": 77,
+        "prioritizedEntities": ["entity-0"]}})
+    assert p.LoadConfig(cfg) is None
+    return p
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,entities,concurrent", [(10, 2, True), (10, 10, True), (10, 2, False), (10, 10, False),
+                                                   (500, 16, True), (500, 16, False)])
+def test_random_policy_with_packet_events(ctx, n, entities, concurrent):
+    """TestRandomPolicy{,ShouldNotBlock}WithPacketEvent_* (randompolicy_test.go:104-118) plus sizes that make
+    the decision thread batch: each action is the decision the oracle makes for (seed, event), delivered no
+    earlier than its delay after QueueEvent."""
+    from oracle import oracle as O
+    p = _random_policy()
+    t_start = time.monotonic_ns()
+    events, got, longest = send_receive(p, n, entities, concurrent)
+    assert longest < 0.05
+    eh, ec = p.event_inputs(events)
+    pr = O.random_params(p.MinInterval, p.MaxInterval, p.FaultActionProbability)
+    want = {}
+    for ev, h, c in zip(events, eh, ec):
+        d, f, _ = O.random_decide(p.Seed, int(h), int(c), pr)
+        want[ev.ID()] = (d, "PacketFaultAction" if f else "EventAcceptanceAction")
+    assert sorted(a.Event().ID() for a in got) == sorted(want)
+    for a in got:
+        assert a.Class() == want[a.Event().ID()][1]
+    assert p.online.wait_decided(5)
+    assert (time.monotonic_ns() - t_start) / 1e6 >= max(d for d, _ in want.values()) / 1e6 - 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,entities,concurrent", [(10, 2, True), (10, 10, False), (300, 5, True)])
+def test_replayable_policy_with_packet_events(ctx, n, entities, concurrent):
+    """replayablepolicy_test.go:41-110 (seed "foobar", maxInterval 1 s scaled to 20 ms, hints
+    hint-entity-%d-%d): actions are DefaultActions, and determineInterval equals the oracle's."""
+    from oracle import oracle as O
+    p = ep.Replayable()
+    cfg = Config({"explorePolicy": "replayable", "explorePolicyParam": {"maxInterval": "20ms", "seed": "foobar"}})
+    assert p.LoadConfig(cfg) is None
+    events, got, longest = send_receive(p, n, entities, concurrent)
+    assert longest < 0.05
+    assert sorted(a.Event().ID() for a in got) == sorted(e.ID() for e in events)
+    assert all(a.Class() == "EventAcceptanceAction" for a in got)
+    got_d = p.decide_intervals(events)
+    assert got_d.tolist() == [O.replayable_interval("foobar", e.ReplayHint(), 20_000_000) for e in events]
+    assert p.determineInterval(events[0]) == int(got_d[0])
+
+
+@pytest.mark.gpu
+def test_online_decisions_match_the_sweep(ctx):
+    """The online path (nmz_random_decide) and the batch sweep make the same decision for a seed and event."""
+    p = _random_policy()
+    rng = np.random.default_rng(4)
+    eh = rng.integers(0, 2**64, 3000, dtype=np.uint64)
+    ec = rng.integers(0, 4, 3000, dtype=np.uint8)
+    r = p.Sweep(p.Seed, 1, eh, ec, n_dump=1)
+
+    class _E:
+        def __init__(self, h, c):
+            self.h, self.c = h, c
+    p.event_inputs = lambda evs: (np.array([e.h for e in evs], np.uint64), np.array([e.c for e in evs], np.uint8))
+    d, f = p.decide_events([_E(h, c) for h, c in zip(eh, ec)])
+    assert np.array_equal(d, r.delays[0]) and np.array_equal(f, r.faults[0].astype(bool))
