@@ -72,23 +72,33 @@ def roofline_valu(kernel, units, kernel_ms):
                               if e.get("clock_ghz") else None)}
 
 
-def splitmix64(state, n):
-    out = np.zeros(n, np.uint64)
-    s = np.uint64(state)
-    with np.errstate(over="ignore"):
-        for i in range(n):
-            s = s + np.uint64(0x9E3779B97F4A7C15)
-            z = s
-            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-            out[i] = z ^ (z >> np.uint64(31))
-    return out
+def cpu_threads():
+    """Host threads for the CPU baselines: the cores this process may run on (on the GPU box the CPU share
+    set by OMP_NUM_THREADS, since nproc there counts the whole machine)."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def zk_hints(n_events, seed=0x5EED):
     """ZooKeeper-style replay hints: decimal signed int64 (pynmz zookeeper.py:113 format)."""
-    v = splitmix64(seed, n_events).view(np.int64)
-    return [str(int(x)) for x in v]
+    from namazu_amd.synth import splitmix64 as sm
+    return [str(int(x)) for x in sm(seed, n_events).view(np.int64)]
 
 
 def decimal_csr(lo, n):
@@ -140,9 +150,9 @@ def merge_topk(entries, k):
 
 def bench_replayable(args, torch, D, ctx, L, stream):
     from namazu_amd import _lib
+    from namazu_amd.explorepolicy import to_csr
     S, E = args.seeds, args.events
     hints = zk_hints(E)
-    from namazu_amd.explorepolicy import to_csr
     hoff, hb = to_csr(hints)
     # Consecutive steps are pipelined over NP plans and HIP streams (NMZ_BENCH_PIPELINE, default 3), each
     # slot sweeping its own range of S seeds: the latency-bound kernels around one step's sweep (seed
@@ -216,8 +226,11 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     _lib.check(L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
     _lib.check(L.nmz_timing_enable(ctx.handle, 0))
     kern_ms = tot.value / max(cnt.value, 1)
-    # the timed region: exactly args.steps pipelined steps
+    # the timed region: exactly args.steps pipelined steps; K1's launches are bracketed by HIP events on their
+    # own streams (nmz_timing_*), so the roofline's kernel time comes from these same launches
     it[0] = 0
+    _lib.check(L.nmz_timing_enable(ctx.handle, 1))
+    L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
     D.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -227,84 +240,211 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     torch.cuda.synchronize()
     D.barrier()
     el = time.perf_counter() - t0
+    _lib.check(L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
+    _lib.check(L.nmz_timing_enable(ctx.handle, 0))
+    kern_ms_timed = tot.value / max(cnt.value, 1)
     merged = merge_topk(b"".join(o.cpu().numpy().tobytes() for o in outputs()), K_TOP)
     el_max = D.max(torch, el)
     stats = np.frombuffer(d_stats[0].cpu().numpy().tobytes(), dtype=_lib.SCHED_STATS_DTYPE)
     for plan in plans:
         L.nmz_replayable_plan_destroy(plan)
-    return dict(S=S, E=E, hints=(hoff, hb), seeds=csr[0], elapsed=el_max, kern_ms=kern_ms, plan_ms=plan_ms,
-                stats=stats, topk=merged, pipeline=NP)
+    # configs[1] as stated, end to end: a new trace's plan (tables built and sorted from host hints) + one
+    # 2^20-seed sweep with top-k + the copy of the top-k to the host, per trace
+    e2e = []
+    e2e_hints = [to_csr(zk_hints(E, seed=0x5EED + 1 + i)) for i in range(args.e2e_traces)]
+    d_tk = torch.empty(K_TOP * 24, dtype=torch.uint8, device=dev)
+    for i, (ho, hbb) in enumerate(e2e_hints):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        plan = ctypes.c_void_p()
+        _lib.check(L.nmz_replayable_plan_create(ctx.handle, host_ptr(ho), host_ptr(hbb), E, MAX_INTERVAL_NS, S,
+                                                ctypes.byref(plan)))
+        _lib.check(L.nmz_replayable_sweep_topk_dev(plan, ctypes.c_void_p(d_soff[0].data_ptr()),
+                                                   ctypes.c_void_p(d_sb[0].data_ptr()), S, seed_lo[0], K_TOP,
+                                                   ctypes.c_void_p(d_stats[0].data_ptr()),
+                                                   ctypes.c_void_p(d_tk.data_ptr()), stream))
+        d_tk.cpu()
+        e2e.append(time.perf_counter() - t0)
+        L.nmz_replayable_plan_destroy(plan)
+    return dict(S=S, E=E, hints=(hoff, hb), seeds=csr[0], elapsed=el_max, kern_ms=kern_ms_timed,
+                kern_ms_isolated=kern_ms, plan_ms=plan_ms, stats=stats, topk=merged, pipeline=NP,
+                e2e_s=e2e)
 
 
 def cpu_baseline_replayable(r, args):
     from oracle import oracle as O
     n = min(args.cpu_seeds, r["S"])
     soff, sb = r["seeds"]
-    so = soff[: n + 1].copy()
     hoff, hb = r["hints"]
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     t0 = time.perf_counter()
-    st, _ = O.replayable_sweep(so, sb, hoff, hb, MAX_INTERVAL_NS, nthreads=threads)
+    st, _ = O.replayable_sweep(soff[: n + 1].copy(), sb, hoff, hb, MAX_INTERVAL_NS, nthreads=threads)
     dt = time.perf_counter() - t0
     parity = bool(np.array_equal(st, r["stats"][:n]))
+    n1 = max(n // 16, 1)  # single core, a sixteenth of the sample
+    t0 = time.perf_counter()
+    O.replayable_sweep(soff[: n1 + 1].copy(), sb, hoff, hb, MAX_INTERVAL_NS, nthreads=1)
+    dt1 = time.perf_counter() - t0
     return dict(value=n * r["E"] / dt, unit="decisions/s", cores=threads, kind="port",
                 sample=f"first {n} of {r['S']} seeds x {r['E']} events (oracle/nmz_oracle.c, OpenMP)",
-                parity_with_gpu=parity, seconds=round(dt, 3))
+                parity_with_gpu=parity, seconds=round(dt, 3), cpu_model=cpu_model(),
+                single_core=dict(value=n1 * r["E"] / dt1, sample=f"first {n1} seeds", seconds=round(dt1, 3)))
 
 
-def bench_random_secondary(args, torch, D, ctx, L, stream):
-    """configs[3] per-GPU share: 16 entities, 10k events, p=0.1, top-64."""
+def config3_trace(E=10_000):
+    """configs[3] / configs[0] trace: 16 entities entity-(i%16) (explorepolicytester.go:36), entity-0..3
+    prioritized, every event a deferred PacketEvent (faultable); event hashes SplitMix64(0x5EED1)."""
     from namazu_amd import _lib
-    S = args.random_seeds
-    E = 10_000
+    from namazu_amd.synth import splitmix64 as sm
     ent = np.arange(E) % 16
-    evhash = splitmix64(0x5EED1, E)
+    evhash = sm(0x5EED1, E)
     evclass = np.where(ent < 4, _lib.NMZ_EV_PRIORITIZED, 0).astype(np.uint8) | np.uint8(_lib.NMZ_EV_FAULTABLE)
+    return evhash, evclass
+
+
+def bench_random_fault_sweep(args, torch, D, ctx, L, stream):
+    """configs[3]: 10^7 schedules (seeds 0..10^7-1) over the 16-entity 10k-event trace, p = 0.1, split over the
+    ranks by shard_range (strong scaling: the job is fixed). One step = each rank's sweep of its share + its
+    device top-64 + (N > 1) RCCL all_gather of the ranks' top-64 lists + the deterministic merge."""
+    from namazu_amd import _lib
+    from namazu_amd import dist as nd
+    S_total, E, K = args.random_total, 10_000, 64
+    evhash, evclass = config3_trace(E)
     params = _lib.resolve_random_params(30_000_000, 100_000_000, 0.1)
-    plan = ctypes.c_void_p()
-    _lib.check(L.nmz_random_plan_create(ctx.handle, host_ptr(evhash), host_ptr(evclass), E, ctypes.byref(params), S,
-                                        ctypes.byref(plan)))
     dev = torch.device("cuda", D.local_rank)
-    d_stats = torch.empty(S * 32, dtype=torch.uint8, device=dev)
-    seed0 = D.rank * S
-    for _ in range(1):
-        _lib.check(L.nmz_random_sweep_dev(plan, seed0, S, ctypes.c_void_p(d_stats.data_ptr()), stream))
+    sh = nd.RandomShardSweep(ctx, torch, dev, evhash, evclass, params, 0, S_total, D.world, D.rank, k=K)
+    gathered = [torch.empty_like(sh.d_topk) for _ in range(D.world)] if D.world > 1 else None
+
+    def step():
+        sh.step(stream)
+        if D.pg:
+            D.pg.all_gather(gathered, sh.d_topk)
+
+    step()
     torch.cuda.synchronize()
-    _lib.check(L.nmz_timing_enable(ctx.handle, 1))
     tot, cnt = ctypes.c_double(), ctypes.c_uint64()
+    _lib.check(L.nmz_timing_enable(ctx.handle, 1))
     L.nmz_timing_read(ctx.handle, b"random_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
-    steps = 3
+    steps = args.random_steps
     D.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        _lib.check(L.nmz_random_sweep_dev(plan, seed0, S, ctypes.c_void_p(d_stats.data_ptr()), stream))
+        step()
     torch.cuda.synchronize()
     D.barrier()
     el = D.max(torch, time.perf_counter() - t0)
     _lib.check(L.nmz_timing_read(ctx.handle, b"random_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
     _lib.check(L.nmz_timing_enable(ctx.handle, 0))
-    L.nmz_random_plan_destroy(plan)
-    dec = D.world * S * E * steps
+    parts = [g.cpu().numpy() for g in gathered] if gathered else [sh.d_topk.cpu().numpy()]
+    merged = nd.merge_topk(parts, K)
     kern_ms = tot.value / max(cnt.value, 1)
-    out = dict(metric="random-policy fault-sweep decisions/s", value=dec / el, unit="decisions/s",
-               config={"workload": "configs[3] share", "seeds_per_gpu": S, "events": E, "entities": 16,
-                       "prioritized": 4, "fault_probability": 0.1},
-               ms_per_step=el / steps * 1e3, kernel_ms=kern_ms,
-               roofline=roofline_valu("k_random_sweep", S * E, kern_ms))
-    stats = np.frombuffer(d_stats.cpu().numpy().tobytes(), dtype=_lib.SCHED_STATS_DTYPE)
+    out = dict(metric="random-policy fault-sweep decisions/s", value=S_total * E * steps / el, unit="decisions/s",
+               n_gpus=D.world, steps=steps, ms_per_step=el / steps * 1e3, scaling="strong",
+               config={"workload": "configs[3] random fault sweep", "schedules": S_total, "events": E,
+                       "entities": 16, "prioritized": 4, "fault_probability": 0.1, "topk": K,
+                       "parallelism": f"seed-range x{D.world}" + (" + RCCL all_gather top-k" if D.world > 1 else "")},
+               kernel_ms=kern_ms,
+               roofline=roofline_valu("k_random_sweep", sh.n * E, kern_ms),
+               topk_head=[[int(x["seed"]), int(x["n_fault"]), int(x["sum_delay_ns"])] for x in merged[:4]])
     if D.rank == 0 and args.cpu_baseline and D.world == 1:
         from oracle import oracle as O
-        n = args.cpu_random_seeds
-        threads = min(16, os.cpu_count() or 1)
         p = O.random_params(30_000_000, 100_000_000, 0.1)
+        n = args.cpu_random_seeds
+        threads = cpu_threads()
         t0 = time.perf_counter()
-        st, _, _ = O.random_sweep(seed0, n, evhash, evclass, p, nthreads=threads)
+        st, _, _ = O.random_sweep(0, n, evhash, evclass, p, nthreads=threads)
         dt = time.perf_counter() - t0
+        n1 = max(n // 16, 1)
+        t0 = time.perf_counter()
+        O.random_sweep(0, n1, evhash, evclass, p, nthreads=1)
+        dt1 = time.perf_counter() - t0
+        # the winners' stats and the first seeds' stats vs the oracle
+        ok = bool(np.array_equal(st, sh.stats()[:n]))
+        for e in merged[:2]:
+            ost, _, _ = O.random_sweep(int(e["seed"]), 1, evhash, evclass, p)
+            ok = ok and int(ost["n_fault"][0]) == int(e["n_fault"]) and \
+                int(ost["sum_delay_ns"][0]) == int(e["sum_delay_ns"]) % (1 << 64)
         out["cpu_baseline"] = dict(value=n * E / dt, unit="decisions/s", cores=threads, kind="port",
-                                   sample=f"first {n} seeds x {E} events", seconds=round(dt, 3),
-                                   parity_with_gpu=bool(np.array_equal(st, stats[:n])))
+                                   sample=f"first {n} seeds x {E} events (oracle/nmz_oracle.c, full Go Seed per "
+                                          f"decision)", seconds=round(dt, 3), parity_with_gpu=ok,
+                                   cpu_model=cpu_model(),
+                                   single_core=dict(value=n1 * E / dt1, sample=f"first {n1} seeds",
+                                                    seconds=round(dt1, 3)))
+    sh.close()
     return out
+
+
+def bench_config0(args, torch, D, ctx, L):
+    """configs[0]: the random policy over one 10k-event trace under one seed, the reference's own CPU case.
+    Reported: the CPU restatement on one core (the reference decides on one goroutine per event, seeding Go's
+    rand per event: impl.go:39), the GPU decision of the whole trace in one nmz_random_decide call, and the
+    online path's per-event decision latency through QueueEvent (enqueue -> decided): events sent back to back
+    (the decision thread batches them) and one at a time (each waits for its own launch)."""
+    from namazu_amd.config import Config
+    from namazu_amd.explorepolicy import Random
+    from namazu_amd.signal import Event
+    from oracle import oracle as O
+    E = 10_000
+    evhash, evclass = config3_trace(E)
+    p = Random()
+    p.LoadConfig(Config({"explorePolicy": "random", "explorePolicyParam": {
+        "minInterval": "30ms", "maxInterval": "100ms", "faultActionProbability": 0.1, "seed": 1,
+        "prioritizedEntities": [f"entity-{i}" for i in range(4)]}}))
+    pr = O.random_params(30_000_000, 100_000_000, 0.1)
+    t0 = time.perf_counter()
+    st, dl, fl = O.random_sweep(1, 1, evhash, evclass, pr, n_dump=1, nthreads=1)
+    cpu_s = time.perf_counter() - t0
+
+    class _Ev:  # the trace's events as the kernel sees them (hash + class), for decide_events
+        def __init__(self, i):
+            self.i = i
+    p.event_inputs = lambda evs: (evhash[[e.i for e in evs]], evclass[[e.i for e in evs]])
+    evs = [_Ev(i) for i in range(E)]
+    p.decide_events(evs[:16])  # warm the launch path
+    times = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        d, f = p.decide_events(evs)
+        times.append(time.perf_counter() - t0)
+    parity = bool(np.array_equal(d, dl[0]) and np.array_equal(f, fl[0].astype(bool)))
+    # online: QueueEvent with real events (MaxInterval 0 ms delays would not matter: latency is enqueue -> decided)
+    q = Random()
+    q.LoadConfig(Config({"explorePolicy": "random", "explorePolicyParam": {
+        "minInterval": "1ms", "maxInterval": "2ms", "faultActionProbability": 0.1, "seed": 1}}))
+    events = [Event.packet(f"entity-{i % 16}", f"entity-{i % 16}", f"entity-{(i + 1) % 16}", {"n": i})
+              for i in range(2000)]
+    for ev in events[:50]:
+        q.QueueEvent(ev)
+    q.online.wait_decided(30)
+    q.online.latencies_ns.clear()
+    q.online.batch_sizes.clear()
+    for ev in events:
+        q.QueueEvent(ev)
+    q.online.wait_decided(60)
+    burst = np.array(q.online.latencies_ns, np.float64) / 1e3
+    batches = list(q.online.batch_sizes)
+    q.online.latencies_ns.clear()
+    for ev in events[:300]:
+        q.QueueEvent(ev)
+        q.online.wait_decided(10)
+    single = np.array(q.online.latencies_ns, np.float64) / 1e3
+    n_drain = 0
+    while n_drain < 2350:
+        q.ActionChan().get(timeout=10)
+        n_drain += 1
+    return dict(metric="configs[0] random policy, one seed over one 10k-event trace", unit="decisions/s",
+                cpu_1core=dict(value=E / cpu_s, seconds=round(cpu_s, 4), kind="port",
+                               note="oracle/nmz_oracle.c: full Go rand.Seed per decision, as the reference reseeds "
+                                    "per event (util/queue/impl.go:39)"),
+                gpu_batch=dict(value=E / min(times), ms=min(times) * 1e3,
+                               note="nmz_random_decide, the whole trace in one call (host arrays in and out)"),
+                parity_with_gpu=parity,
+                queue_event_latency_us=dict(
+                    burst=dict(events=len(burst), p50=float(np.percentile(burst, 50)),
+                               p99=float(np.percentile(burst, 99)), mean_batch=float(np.mean(batches))),
+                    one_at_a_time=dict(events=len(single), p50=float(np.percentile(single, 50)),
+                                       p99=float(np.percentile(single, 99)))))
 
 
 def bench_ed_secondary(args, torch, D, ctx, L, stream, spec):
@@ -315,7 +455,7 @@ def bench_ed_secondary(args, torch, D, ctx, L, stream, spec):
     from namazu_amd import synth
     N, k, ED_LEN, ED_BAND = spec["traces"], spec["k"], spec["events"], spec["band"]
     t0 = time.time()
-    ts = getattr(synth, spec["generator"])(N, ED_LEN)
+    ts = getattr(synth, spec["generator"])(N, ED_LEN, **spec.get("gen_kwargs", {}))
     synth_s = time.time() - t0
     plan = ctypes.c_void_p()
     t0 = time.time()
@@ -352,6 +492,8 @@ def bench_ed_secondary(args, torch, D, ctx, L, stream, spec):
     el = D.max(torch, time.perf_counter() - t0)
     _lib.check(L.nmz_timing_read(ctx.handle, tname, ctypes.byref(tot), ctypes.byref(cnt), 1))
     _lib.check(L.nmz_timing_enable(ctx.handle, 0))
+    counters = np.zeros(_lib.NMZ_ED_NCOUNTERS, np.uint64)
+    _lib.check(L.nmz_ed_plan_counters(plan, _lib.ptr(counters), stream))
     L.nmz_ed_plan_destroy(plan)
     pairs = N * (N - 1) // 2
     cells_per_pair = ED_LEN * (2 * ED_BAND + 1) - ED_BAND * (ED_BAND + 1)
@@ -363,7 +505,16 @@ def bench_ed_secondary(args, torch, D, ctx, L, stream, spec):
                        (" + RCCL all_gather k-NN merge" if D.world > 1 else "")},
                kernel=kind, kernel_ms=kern_ms, plan_ms=plan_ms, synth_s=round(synth_s, 2),
                roofline=roofline_valu(kind, (pairs + D.world - 1) // D.world, kern_ms),
-               band_cells_per_s=pairs * cells_per_pair * steps / el)
+               nominal_band_cells_per_s=pairs * cells_per_pair * steps / el)
+    if counters[3]:  # k_ed_bv work counters of the last step (this rank's shard)
+        c = [int(x) for x in counters]
+        out["search"] = dict(
+            dp_pairs=c[0], in_band_pairs=c[1], in_band_frac_of_shard_pairs=c[1] / max(c[0], 1),
+            mean_cutoff_column=32 * c[2] / c[3], full_columns=ED_LEN,
+            executed_cells_per_s=c[2] * 32 * 2 * (2 * ED_BAND + 1) * D.world / (el / steps),
+            live_cells_per_s=c[4] * 32 * (2 * ED_BAND + 1) * D.world / (el / steps),
+            note="cells = band cells (2w+1 per column); executed = every candidate x 32-column block a lane stepped "
+                 "(2 query columns each), live = the query columns still running in those blocks")
     keys = d_out.cpu().numpy().view(np.uint64).reshape(N, k)
     if D.rank == 0 and args.cpu_baseline and D.world == 1:
         from oracle import oracle as O
@@ -391,8 +542,10 @@ def main():
     ap.add_argument("--seeds", type=int, default=1 << 20)
     ap.add_argument("--events", type=int, default=4096)
     ap.add_argument("--cpu-seeds", type=int, default=1 << 18)
-    ap.add_argument("--random-seeds", type=int, default=1 << 20)
+    ap.add_argument("--random-total", type=int, default=10_000_000)
+    ap.add_argument("--random-steps", type=int, default=3)
     ap.add_argument("--cpu-random-seeds", type=int, default=256)
+    ap.add_argument("--e2e-traces", type=int, default=5)
     ap.add_argument("--ed-traces", type=int, default=100_000)
     ap.add_argument("--ed-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
@@ -436,7 +589,19 @@ def main():
         "roofline": roofline_valu("k_replayable_sweep_fast", dec_launch, r["kern_ms"]),
         "plan_ms": r["plan_ms"],
         "topk_head": [int(x) for x in r["topk"]["seed"][:4]],
+        "steady_state": "value re-sweeps one trace's resident plan each step (plan built once, before the timed "
+                        "region); end_to_end below builds a new trace's plan inside the timing",
+        "end_to_end": {"value": dec_launch / float(np.median(r["e2e_s"])), "unit": "decisions/s",
+                       "ms_median": float(np.median(r["e2e_s"])) * 1e3, "traces": len(r["e2e_s"]),
+                       "what": "per trace: nmz_replayable_plan_create from host hints (tables + segment sorts) + "
+                               "one 2^20-seed sweep with top-64 + top-64 copy to the host"},
     }
+    if line["roofline"]:
+        rf = line["roofline"]
+        rf["kernel_ms_source"] = "HIP events around every K1 launch of the timed region (on its stream)"
+        rf["kernel_ms_isolated"] = r["kern_ms_isolated"]
+        # the same lane-ops over the whole pipelined step (every kernel of the step on the clock)
+        rf["frac_of_step"] = rf["ops_per_unit"] * dec_launch / (line["ms_per_step"] * 1e-3) / 1e12 / PEAK_VALU_TOPS
     # survey 8(d) declared model for the reference's byte-serial algorithm: 6*len(hint)+18 ops per decision
     hoff = r["hints"][0]
     mean_len = float(np.mean(np.diff(hoff.astype(np.int64))))
@@ -445,13 +610,20 @@ def main():
     if D.rank == 0 and D.world == 1 and args.cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_replayable(r, args)
     if args.secondary:
-        ed3 = dict(workload="configs[2] historystorage all-pairs search", traces=args.ed_traces, events=2048,
-                   band=32, k=8, generator="synth_traces", steps=args.ed_steps)
+        ed3 = dict(workload="configs[2] historystorage all-pairs search, clustered (families of 1,024 "
+                            "near-duplicate runs)", traces=args.ed_traces, events=2048, band=32, k=8,
+                   generator="clustered_traces", gen_kwargs=dict(family=1024), steps=args.ed_steps)
+        ed3s = dict(workload="configs[2] historystorage all-pairs search, survey generator (independent "
+                             "mutations: every pair beyond the band)", traces=args.ed_traces, events=2048, band=32,
+                    k=8, generator="synth_traces", steps=args.ed_steps)
         ed5 = dict(workload="configs[4] long-trace stress, wide band", traces=256, events=65536, band=4096, k=8,
                    generator="etcd_traces", steps=args.ed_steps)
-        line["secondary"] = [bench_random_secondary(args, torch, D, ctx, L, stream),
+        line["secondary"] = [bench_random_fault_sweep(args, torch, D, ctx, L, stream),
                              bench_ed_secondary(args, torch, D, ctx, L, stream, ed3),
+                             bench_ed_secondary(args, torch, D, ctx, L, stream, ed3s),
                              bench_ed_secondary(args, torch, D, ctx, L, stream, ed5)]
+        if D.rank == 0 and D.world == 1 and args.cpu_baseline:
+            line["secondary"].append(bench_config0(args, torch, D, ctx, L))
     if D.rank == 0:
         os.write(out_fd, (json.dumps(line) + "\n").encode())
     ctx.close()

@@ -139,6 +139,56 @@ __global__ __launch_bounds__(256) void k_replayable_table_sort(const uint4 *__re
     if (p < E) table[(uint64_t)L * E + cs + rank] = x;
 }
 
+// Sort one (class, row L) segment per workgroup in LDS: bitonic sort of (C, position) pairs padded to a power of
+// two (the position makes keys distinct, so the order equals the stable C order of k_replayable_table_sort), then
+// a gather of the table entries in that order. Segments of up to SEG_SORT_MAX entries (48 KiB of LDS); larger
+// classes keep the counting kernel above.
+constexpr uint32_t SEG_SORT_MAX = 4096;
+
+__global__ __launch_bounds__(256) void k_replayable_table_segsort(const uint4 *__restrict__ tmp,
+                                                                  const ClassInfo *__restrict__ classes, uint32_t E,
+                                                                  uint4 *__restrict__ table) {
+    __shared__ uint64_t key[SEG_SORT_MAX];
+    __shared__ uint32_t pos[SEG_SORT_MAX];
+    const ClassInfo ci = classes[blockIdx.x];
+    const uint32_t L = blockIdx.y, n = ci.count;
+    if (n > SEG_SORT_MAX || n == 0) return;
+    uint32_t p2 = 1;
+    while (p2 < n) p2 <<= 1;
+    const uint4 *__restrict__ src = tmp + (uint64_t)L * E + ci.start;
+    for (uint32_t i = threadIdx.x; i < p2; i += 256) {
+        if (i < n) {
+            const uint4 q = src[i];
+            key[i] = ((uint64_t)q.y << 32) | q.x;
+        } else {
+            key[i] = UINT64_MAX;
+        }
+        pos[i] = i;
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= p2; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < p2; i += 256) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const uint64_t ki = key[i], kl = key[l];
+                    const uint32_t pi = pos[i], pl = pos[l];
+                    const bool gt = ki > kl || (ki == kl && pi > pl);
+                    if (((i & k) == 0) == gt) {  // ascending half: swap if i > l; descending half: if i < l
+                        key[i] = kl;
+                        key[l] = ki;
+                        pos[i] = pl;
+                        pos[l] = pi;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    uint4 *__restrict__ dst = table + (uint64_t)L * E + ci.start;
+    for (uint32_t i = threadIdx.x; i < n; i += 256) dst[i] = src[pos[i]];
+}
+
 // ---------------------------------------------------------------------------
 // seed prefix: h0 = FNV(seed bytes)
 // ---------------------------------------------------------------------------
@@ -788,15 +838,20 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
             hipMemcpyAsync(d_hoff, hint_off, (E + 1) * 4, hipMemcpyHostToDevice, st) ||
             (nbytes && hipMemcpyAsync(d_hbytes, hint_bytes, nbytes, hipMemcpyHostToDevice, st)))
             return cleanup(fail(NMZ_EHIP, "plan upload failed"));
-        // unsorted table into scratch, then the per-(L, class) C sort into place
-        DevBuf tmp;
+        // unsorted table into scratch (the context's, grow-only: no free, so no device sync), then the
+        // per-(L, class) C sort into place
+        DevBuf &tmp = ctx->buf[10];
         if (tmp.ensure((size_t)256 * E * sizeof(uint4)) != NMZ_OK) return cleanup(NMZ_ENOMEM);
         hipLaunchKernelGGL(k_replayable_table, dim3(E), dim3(256), 0, st, d_hoff, d_hbytes, d_perm, E, p->mod.m,
                            p->mod.kind == MOD_FAST ? 1 : 0, tmp.as<uint4>());
         uint32_t max_class = 0;
         for (const ClassInfo &c : cls) max_class = std::max(max_class, c.count);
         bool bad = false;
-        if (max_class <= 16384) {  // O(n^2) rank sort on the device
+        if (max_class <= SEG_SORT_MAX && !getenv("NMZ_REPLAY_RANKSORT")) {  // LDS bitonic sort per segment
+            hipLaunchKernelGGL(k_replayable_table_segsort, dim3(p->n_classes, 256), dim3(256), 0, st, tmp.as<uint4>(),
+                               p->d_classes, E, p->d_table);
+            bad = hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess;
+        } else if (max_class <= 16384) {  // O(n^2) rank sort on the device
             hipLaunchKernelGGL(k_replayable_table_sort, dim3(ceil_div(E, 256), 256), dim3(256), 0, st,
                                tmp.as<uint4>(), p->d_classes, p->n_classes, E, p->d_table);
             bad = hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess;
@@ -818,7 +873,6 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
                       hipStreamSynchronize(st) != hipSuccess;
             }
         }
-        tmp.release();
         if (bad)
             return cleanup(fail(NMZ_EHIP, "plan table kernel failed"));
     }
