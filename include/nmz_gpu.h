@@ -233,6 +233,15 @@ int nmz_ed_allpairs_knn_shard_dev(nmz_ed_plan *plan, uint32_t k, uint32_t shard,
                                   uint64_t *d_knn_keys, void *stream);
 int nmz_knn_merge_dev(nmz_ctx *ctx, const uint64_t *d_parts, uint32_t n_parts, uint32_t n_traces,
                       uint32_t k, uint64_t *d_out, void *stream);
+/* Single queries against a resident store (HistoryStorage similarity search; the reference's own
+ * search re-decodes every stored trace per query, naive.go:235-252 "FIXME: quite ineffective"):
+ * the plan's stored traces stay on the device; each of n_queries query traces (CSR q_off/q_sym,
+ * u64 event hashes, no longer than the longest stored trace) gets its k nearest stored traces by
+ * (ED_band asc, id asc), ED_band as in nmz_ed_pairs. knn_id/knn_dist are [n_queries * k], NMZ_NONE
+ * where fewer than k traces exist. Needs a bit-parallel plan (nmz_ed_plan_is_fast == 2: band 8, 16
+ * or 32); NMZ_EINVAL otherwise. Synchronous. */
+int nmz_ed_plan_query_knn(nmz_ed_plan *plan, const uint64_t *q_off, const uint64_t *q_sym, uint32_t n_queries,
+                          uint32_t k, uint32_t *knn_id, uint32_t *knn_dist);
 /* Work counters of the plan's latest search (synchronises `stream`, NULL = the context's stream).
  * out[NMZ_ED_NCOUNTERS]: the bit-parallel band kernel (nmz_ed_plan_is_fast == 2) fills
  *   [0] pairs that ran the DP, [1] pairs whose result is <= band (in band),

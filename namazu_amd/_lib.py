@@ -84,6 +84,7 @@ SIGNATURES = {
     "nmz_ed_allpairs_knn_shard_dev": (_int, [_P, _u32, _u32, _u32, _P, _P]),
     "nmz_knn_merge_dev": (_int, [_P, _P, _u32, _u32, _u32, _P, _P]),
     "nmz_ed_plan_counters": (_int, [_P, _P, _P]),
+    "nmz_ed_plan_query_knn": (_int, [_P, _P, _P, _u32, _u32, _P, _P]),
     "nmz_trace_signatures": (_int, [_P, _P, _P, _P, _u32, _P]),
     "nmz_unique_traces": (_int, [_P, _P, _P, _P, _u32, _P]),
     "nmz_unique_traces_dev": (_int, [_P, _P, _P, _P, _u32, _u32, _P, _P, _P]),

@@ -355,6 +355,8 @@ struct nmz_ed_plan {
     uint16_t *d_bsym = nullptr;
     uint64_t *d_chunk_start = nullptr;
     uint64_t *d_counters = nullptr;  // bv: work counters of the latest search (nmz_ed_plan_counters)
+    uint32_t maxlen = 0;
+    std::unordered_map<uint64_t, uint32_t> dict;  // bv: symbol -> dense id (single-query search)
     nmz::DevBuf mem;
     uint16_t *d_qsym = nullptr, *d_csym = nullptr;
     uint64_t *d_qoff = nullptr, *d_coff = nullptr;
@@ -382,8 +384,8 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
     std::vector<uint16_t> ids;
     const bool want_wide = ed_wide_supported(band);
     bool fast = ((band == 8 || band == 16 || band == 32) && maxlen + band < MAX_FAST_LEN) || want_wide;
+    std::unordered_map<uint64_t, uint32_t> dict;
     if (fast) {
-        std::unordered_map<uint64_t, uint32_t> dict;
         dict.reserve(1024);
         ids.resize(total);
         for (uint64_t t = 0; t < total && fast; ++t) {
@@ -467,6 +469,9 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
     } else if (fast && p->bv) {
         const uint32_t G = (N + 63) / 64;
         p->G = G;
+        p->maxlen = maxlen;
+        p->n_sym = n_sym;
+        p->dict = std::move(dict);
         const uint32_t ndw = p->ndw;
         const uint32_t zero_row = n_sym * ndw * 8;
         std::vector<uint32_t> len(N + 1, 0);
@@ -698,6 +703,71 @@ int nmz_ed_plan_counters(nmz_ed_plan *plan, uint64_t *out, void *stream) {
     CtxGuard g(plan->ctx);
     hipStream_t st = stream ? (hipStream_t)stream : plan->ctx->stream;
     NMZ_HIP(hipMemcpyAsync(out, plan->d_counters, ED_BV_NCOUNTERS * 8, hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipStreamSynchronize(st));
+    return NMZ_OK;
+}
+
+int nmz_ed_plan_query_knn(nmz_ed_plan *plan, const uint64_t *q_off, const uint64_t *q_sym, uint32_t n_queries,
+                          uint32_t k, uint32_t *knn_id, uint32_t *knn_dist) {
+    NMZ_CHECK(plan != nullptr, "plan is NULL");
+    NMZ_CHECK(k >= 1 && k <= 64, "k must be in [1, 64]");
+    NMZ_CHECK(plan->bv, "single-query search needs a bit-parallel plan (band 8, 16 or 32; alphabet within LDS)");
+    NMZ_CHECK(n_queries == 0 || (q_off && knn_id && knn_dist), "NULL argument");
+    CtxGuard g(plan->ctx);
+    NMZ_TRY(g.rc);
+    if (n_queries == 0) return NMZ_OK;
+    const uint64_t total = q_off[n_queries];
+    NMZ_CHECK(total == 0 || q_sym, "q_sym is NULL");
+    for (uint32_t q = 0; q < n_queries; ++q) {
+        NMZ_CHECK(q_off[q] <= q_off[q + 1], "query offsets must not decrease");
+        NMZ_CHECK(q_off[q + 1] - q_off[q] <= plan->maxlen, "query longer than the longest stored trace");
+    }
+    hipStream_t st = plan->ctx->stream;
+    const uint32_t N = plan->n;
+    // query streams in the plan's Peq-row offsets (unknown symbols: 0xffff), each padded by one 32-block
+    std::vector<uint64_t> qoff(n_queries + 1, 0);
+    for (uint32_t q = 0; q < n_queries; ++q) qoff[q + 1] = qoff[q] + (q_off[q + 1] - q_off[q] + 31) / 32 * 32 + 32;
+    std::vector<uint16_t> qs(qoff[n_queries] + 1, 0xffffu);
+    for (uint32_t q = 0; q < n_queries; ++q)
+        for (uint64_t t = q_off[q]; t < q_off[q + 1]; ++t) {
+            auto it = plan->dict.find(q_sym[t]);
+            if (it != plan->dict.end()) qs[qoff[q] + (t - q_off[q])] = (uint16_t)(it->second * plan->ndw * 8);
+        }
+    const uint64_t nk = (uint64_t)n_queries * k;
+    DevBuf &scr = plan->ctx->buf[11];
+    NMZ_TRY(scr.ensure(Carve::bytes_for(qs.size(), 2) + Carve::bytes_for(nk, 8) + 2 * Carve::bytes_for(nk, 4)));
+    Carve cv(scr.ptr);
+    uint16_t *d_qs = cv.take<uint16_t>(qs.size());
+    uint64_t *d_knn = cv.take<uint64_t>(nk);
+    uint32_t *d_id = cv.take<uint32_t>(nk), *d_ds = cv.take<uint32_t>(nk);
+    NMZ_HIP(hipMemcpyAsync(d_qs, qs.data(), qs.size() * 2, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_knn_init, dim3(ceil_div(nk, 256)), dim3(256), 0, st, d_knn, nk);
+    // a pool of 256 stored traces per workgroup: one pass of lanes, ~N/256 workgroups
+    const uint32_t pool = N >= 256u * 1024u ? 1024u : 256u;
+    for (uint32_t q = 0; q < n_queries && N; q += 2) {
+        EdBvQueryArgs A;
+        A.bsym = plan->d_bsym;
+        A.soff = plan->d_soff;
+        A.len = plan->d_len;
+        A.qs = d_qs;
+        A.n_queries = std::min(2u, n_queries - q);
+        for (uint32_t i = 0; i < 2; ++i) {
+            const uint32_t qq = std::min(q + i, n_queries - 1);
+            A.qoff[i] = qoff[qq];
+            A.nq[i] = (uint32_t)(q_off[qq + 1] - q_off[qq]);
+        }
+        A.knn = d_knn + (uint64_t)q * k;
+        A.N = N;
+        A.k = k;
+        A.lds_dw = plan->lds_dw;
+        A.pool = pool;
+        KernelTimer kt(plan->ctx, st, "ed_bv_query");
+        NMZ_TRY(ed_bv_query_launch(A, plan->band, ceil_div(N, pool), st));
+    }
+    hipLaunchKernelGGL(k_knn_final, dim3(ceil_div(nk, 256)), dim3(256), 0, st, d_knn, nk, d_id, d_ds);
+    NMZ_HIP(hipGetLastError());
+    NMZ_HIP(hipMemcpyAsync(knn_id, d_id, nk * 4, hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipMemcpyAsync(knn_dist, d_ds, nk * 4, hipMemcpyDeviceToHost, st));
     NMZ_HIP(hipStreamSynchronize(st));
     return NMZ_OK;
 }

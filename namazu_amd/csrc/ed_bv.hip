@@ -413,6 +413,134 @@ __global__ __launch_bounds__(256) void k_ed_bv(EdBvArgs A) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_ed_bv_query: one or two external query traces against every stored trace of a bit-parallel plan
+// (SearchSimilar on a resident store). The queries' Peq rows are built in LDS in the plan's layout
+// ([symbol][dword][query], row stride ndw * 8 bytes), so the stored traces' streams of Peq-row byte
+// offsets index them unchanged; query symbols the store has never seen carry 0xffff and set no bit (they
+// match no stored symbol). Each workgroup takes a pool of stored traces; lanes refill as in k_ed_bv.
+// Results go to the queries' k-NN lists only (keys dist << 32 | stored id).
+// ---------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(256) void k_ed_bv_query(EdBvQueryArgs A) {
+    using SH = BvShape<W>;
+    extern __shared__ uint32_t peq[];
+    uint32_t &pool_next = peq[A.lds_dw];
+    const uint32_t pool_lo = blockIdx.x * A.pool;
+    const uint32_t pool_n = min(A.pool, A.N - pool_lo);
+    const uint32_t n1 = A.nq[0], n2 = A.nq[1];
+    const bool has2 = A.n_queries > 1;
+    {
+        uint4 *p4 = (uint4 *)peq;
+        for (uint32_t i = threadIdx.x; i < A.lds_dw / 4; i += 256) p4[i] = make_uint4(0, 0, 0, 0);
+        if (threadIdx.x == 0) pool_next = 256;
+    }
+    __syncthreads();
+    for (uint32_t q = 0; q < A.n_queries; ++q) {
+        const uint16_t *a = A.qs + A.qoff[q];
+        for (uint32_t i = threadIdx.x; i < A.nq[q]; i += 256) {
+            if (a[i] == 0xffffu) continue;
+            const uint32_t p = i + 1 + SH::OFF;
+            atomicOr(&peq[(uint32_t)a[i] / 4 + (p >> 5) * 2 + q], 1u << (p & 31));
+        }
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t j = 0, m = 0, r1 = W + 1, r2 = W + 1, kb0 = 0;
+    bool run1 = false, run2 = false, active = false;
+    const uint16_t *stream = A.bsym;
+    BvState<SH::KF> S1, S2;
+    uint32_t cur[16], nxt[16];
+    uint32_t idx = threadIdx.x;
+    uint32_t kb = 0;
+    bool need = true, first = true;
+    auto publish = [&](bool fin) {
+        const uint64_t k1 = fin ? (((uint64_t)r1 << 32) | j) : UINT64_MAX;
+        const uint64_t k2 = (fin && has2) ? (((uint64_t)r2 << 32) | j) : UINT64_MAX;
+        bv_knn_insert_wave(A.knn, A.k, k1, lane);
+        if (has2) bv_knn_insert_wave(A.knn + A.k, A.k, k2, lane);
+    };
+    while (true) {
+        while (true) {
+            const uint64_t want = __ballot(need);
+            if (want == 0) break;
+            if (!first) {
+                const uint32_t cnt = __popcll(want);
+                uint32_t base_idx = 0;
+                if (lane == (uint32_t)(__ffsll((unsigned long long)want) - 1)) base_idx = atomicAdd(&pool_next, cnt);
+                base_idx = __shfl(base_idx, __ffsll((unsigned long long)want) - 1, 64);
+                if (need) idx = base_idx + __popcll(want & ((1ull << lane) - 1));
+            }
+            first = false;
+            if (need) {
+                if (idx >= pool_n) {
+                    need = false;
+                    active = false;
+                    stream = A.bsym;
+                    bv_load_block(cur, stream, 0);
+                } else {
+                    j = pool_lo + idx;
+                    m = A.len[j];
+                    stream = A.bsym + A.soff[j];
+                    r1 = W + 1;
+                    r2 = W + 1;
+                    const int32_t dd1 = (int32_t)m - (int32_t)n1, dd2 = (int32_t)m - (int32_t)n2;
+                    run1 = dd1 <= W && dd1 >= -W;
+                    run2 = has2 && dd2 <= W && dd2 >= -W;
+                    if (run1 && (n1 == 0 || m == 0)) { r1 = n1 + m; run1 = false; }
+                    if (run2 && (n2 == 0 || m == 0)) { r2 = n2 + m; run2 = false; }
+                    if (run1 || run2) {
+                        need = false;
+                        active = true;
+                        kb0 = kb;
+                        bv_init<W>(S1);
+                        bv_init<W>(S2);
+                        bv_load_block(cur, stream, 0);
+                    }
+                }
+            }
+            const bool fin = need && !active && idx < pool_n;
+            if (__any(fin)) publish(fin);
+        }
+        if (!__any(active)) break;
+        const uint32_t lkb = active ? kb - kb0 : 0;
+        bv_load_block(nxt, stream, lkb + 1);
+        const uint32_t j0 = 32 * lkb;
+        const uint32_t base = (lkb + 1) * 8;
+        const bool here = active && (run1 || run2) && m > j0 && m <= j0 + 32;
+        if (__any(here)) {
+            bv_block<W, true>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2);
+        } else {
+            bv_block<W, false>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2);
+        }
+        S1.T += 32 - __builtin_popcount(S1.acc);
+        S2.T += 32 - __builtin_popcount(S2.acc);
+        if (run1 && bv_lower_bound<W>(S1, S1.T) > W) run1 = false;
+        if (run2 && bv_lower_bound<W>(S2, S2.T) > W) run2 = false;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cur[r] = nxt[r];
+        ++kb;
+        const bool fin = active && !run1 && !run2;
+        if (__any(fin)) publish(fin);
+        if (fin) {
+            active = false;
+            need = true;
+        }
+    }
+}
+
+int ed_bv_query_launch(const EdBvQueryArgs &A, uint32_t band, uint32_t blocks, hipStream_t st) {
+    const size_t lds = (size_t)A.lds_dw * 4 + 16;
+    switch (band) {
+        case 8: hipLaunchKernelGGL(k_ed_bv_query<8>, dim3(blocks), dim3(256), lds, st, A); break;
+        case 16: hipLaunchKernelGGL(k_ed_bv_query<16>, dim3(blocks), dim3(256), lds, st, A); break;
+        case 32: hipLaunchKernelGGL(k_ed_bv_query<32>, dim3(blocks), dim3(256), lds, st, A); break;
+        default: return fail(NMZ_EINVAL, "internal: band has no bit-parallel kernel");
+    }
+    NMZ_HIP(hipGetLastError());
+    return NMZ_OK;
+}
+
 bool ed_bv_supported(uint32_t band) { return band == 8 || band == 16 || band == 32; }
 
 int ed_bv_launch(const EdBvArgs &A, uint32_t band, uint64_t blocks, hipStream_t st) {

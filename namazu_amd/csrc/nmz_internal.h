@@ -42,6 +42,18 @@ struct EdBvArgs {
 //   0 pairs that ran the DP, 1 pairs with a result <= w (in band), 2 lane-candidate 32-column blocks executed,
 //   3 candidates that ran the DP, 4 live query-blocks (blocks x queries of that lane still running)
 constexpr int ED_BV_NCOUNTERS = 5;
+// single-query search on a bit-parallel plan (ed_bv.hip k_ed_bv_query): 1-2 external queries vs every stored trace
+struct EdBvQueryArgs {
+    const uint16_t *bsym;  // the plan's stored streams
+    const uint64_t *soff;
+    const uint32_t *len;
+    const uint16_t *qs;    // query streams (plan's Peq-row byte offsets; 0xffff = symbol unknown to the store)
+    uint64_t qoff[2];
+    uint32_t nq[2];
+    uint64_t *knn;         // [n_queries][k]
+    uint32_t N, k, lds_dw, pool, n_queries;
+};
+int ed_bv_query_launch(const EdBvQueryArgs &A, uint32_t band, uint32_t blocks, hipStream_t st);
 int ed_bv_launch(const EdBvArgs &A, uint32_t band, uint64_t blocks, hipStream_t st);
 
 // wide-band bit-parallel edit distance (ed_wide.hip): one pair per wave

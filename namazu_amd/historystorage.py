@@ -217,14 +217,20 @@ class Naive(HistoryStorage):
 
     # ---- SimilaritySearcher ----------------------------------------------------
     def SearchSimilar(self, trace, k, band):
-        """k nearest stored traces to `trace` by (distance asc, id asc)."""
-        ts_all = self.load_all()
+        """k nearest stored traces to `trace` by (distance asc, id asc), as [(id, distance)].
+
+        The stored traces are read once and stay on the GPU (SimilarityIndex) until the storage holds a
+        different number of traces; each query is one launch against the resident store."""
         t = trace.symbols if isinstance(trace, SingleTrace) else np.asarray(trace, np.uint64)
-        ts = TraceSet([t] + [ts_all.trace(i) for i in range(len(ts_all))])
-        pairs = np.array([[0, j + 1] for j in range(len(ts_all))], np.uint32)
-        d = ed_pairs(ts, pairs, band)
-        order = np.lexsort((np.arange(len(d)), d))[:k]
-        return [(int(i), int(d[i])) for i in order]
+        n = self.NrStoredHistories()
+        key = (band, n)
+        if getattr(self, "_index_key", None) != key:
+            if getattr(self, "_index", None) is not None:
+                self._index.close()
+            self._index = SimilarityIndex(self.load_all(), band)
+            self._index_key = key
+        ids, ds = self._index.query([t], k)
+        return [(int(i), int(d)) for i, d in zip(ids[0], ds[0]) if i != _lib.NMZ_NONE]
 
     def AllPairsKNN(self, k, band):
         return allpairs_knn(self.load_all(), k, band)
@@ -260,6 +266,59 @@ def ed_pairs(ts, pairs, band, ctx=None):
     _lib.check(_lib.load().nmz_ed_pairs(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), len(ts),
                                         _lib.ptr(pairs), len(pairs), int(band), _lib.ptr(dist)))
     return dist
+
+
+class SimilarityIndex:
+    """A stored TraceSet resident on the GPU for single-query similarity search.
+
+    Band 8, 16 or 32 (the bit-parallel plan): each query() is one nmz_ed_plan_query_knn launch over the
+    resident traces. Other bands, alphabets too large for LDS, or queries longer than every stored trace go
+    through nmz_ed_pairs (the generic GPU kernel) against the same TraceSet."""
+
+    def __init__(self, ts, band, ctx=None):
+        import ctypes
+        self.ctx = ctx or _lib.default_context()
+        self.ts = ts
+        self.band = int(band)
+        self.plan = ctypes.c_void_p()
+        L = _lib.load()
+        _lib.check(L.nmz_ed_plan_create(self.ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), len(ts), self.band,
+                                        ctypes.byref(self.plan)))
+        self.bitparallel = L.nmz_ed_plan_is_fast(self.plan) == 2
+        self.maxlen = int(np.diff(ts.off.astype(np.int64)).max()) if len(ts) else 0
+
+    def query(self, queries, k):
+        """queries: event-symbol arrays -> (ids [n, k], dists [n, k]), NMZ_NONE padded."""
+        n, N = len(queries), len(self.ts)
+        ids = np.full((n, k), _lib.NMZ_NONE, np.uint32)
+        ds = np.full((n, k), _lib.NMZ_NONE, np.uint32)
+        if n == 0 or N == 0 or k == 0:
+            return ids, ds
+        qs = [np.asarray(q, np.uint64) for q in queries]
+        if self.bitparallel and k <= 64 and max(len(q) for q in qs) <= self.maxlen:
+            qset = TraceSet(qs)
+            _lib.check(_lib.load().nmz_ed_plan_query_knn(self.plan, _lib.ptr(qset.off), _lib.ptr(qset.sym), n, k,
+                                                          _lib.ptr(ids), _lib.ptr(ds)))
+            return ids, ds
+        for r, q in enumerate(qs):  # generic kernel, pairs (query, every stored trace)
+            both = TraceSet([q] + [self.ts.trace(i) for i in range(N)])
+            pairs = np.stack([np.zeros(N, np.uint32), np.arange(1, N + 1, dtype=np.uint32)], 1)
+            d = ed_pairs(both, pairs, self.band, ctx=self.ctx)
+            order = np.lexsort((np.arange(N), d))[:k]
+            ids[r, :len(order)] = order
+            ds[r, :len(order)] = d[order]
+        return ids, ds
+
+    def close(self):
+        if self.plan:
+            _lib.load().nmz_ed_plan_destroy(self.plan)
+            self.plan = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def allpairs_knn(ts, k, band, ctx=None):

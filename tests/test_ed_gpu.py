@@ -265,3 +265,55 @@ def test_knn_shards_merge_to_full(ctx, w, alphabet, lmin, lmax, n, kind):
     oi, od = O.ed_allpairs_knn(ts.off, ts.sym, w, k, nthreads=16)
     assert np.array_equal((keys >> np.uint64(32)).astype(np.uint32), od)
     assert np.array_equal((keys & np.uint64(0xFFFFFFFF)).astype(np.uint32), oi)
+
+
+@pytest.mark.parametrize("w,n,lmin,lmax,mut,alphabet,k", [
+    (32, 500, 100, 300, 0.03, 20, 8),     # ragged, most pairs in band
+    (16, 300, 0, 80, 0.2, 6, 5),          # short/empty traces, |n - m| > w
+    (8, 1200, 50, 60, 0.05, 40, 64),      # k = 64
+    (32, 100, 200, 200, 0.01, 48, 8),     # equal lengths, near duplicates
+])
+def test_similarity_index_queries_vs_oracle(ctx, w, n, lmin, lmax, mut, alphabet, k):
+    """SearchSimilar's resident store (nmz_ed_plan_query_knn / k_ed_bv_query): per query the oracle's
+    brute-force k-NN over the stored traces. Queries: stored traces themselves (distance 0 to their own id),
+    mutated copies, ones holding symbols the store never saw, an empty query."""
+    rng = np.random.default_rng(w * n)
+    ts = make_traces(n, lmin, lmax, mut, alphabet=alphabet, rng=rng)
+    idx = hs.SimilarityIndex(ts, w, ctx=ctx)
+    assert idx.bitparallel
+    qs = [ts.trace(3), ts.trace(n - 1)]
+    t = ts.trace(7).copy()
+    if len(t):
+        t[rng.random(len(t)) < 0.05] = np.uint64(12345)  # unseen symbol
+    qs.append(t)
+    t2 = ts.trace(11).copy()
+    mm = rng.random(len(t2)) < 0.03
+    t2[mm] = ts.sym[rng.integers(0, len(ts.sym), int(mm.sum()))]
+    qs.append(t2)
+    qs.append(np.zeros(0, np.uint64))
+    ids, ds = idx.query(qs, k)
+    for r, q in enumerate(qs):
+        both = hs.TraceSet([q] + [ts.trace(i) for i in range(n)])
+        pairs = np.stack([np.zeros(n, np.uint32), np.arange(1, n + 1, dtype=np.uint32)], 1)
+        d = O.ed_pairs(both.off, both.sym, pairs, w)
+        order = np.lexsort((np.arange(n), d))[:k]
+        assert ds[r, :len(order)].tolist() == d[order].tolist(), r
+        assert ids[r, :len(order)].tolist() == order.tolist(), r
+    assert ds[0, 0] == 0 and ids[0, 0] in np.nonzero(
+        [np.array_equal(ts.trace(i), ts.trace(3)) for i in range(n)])[0]
+    idx.close()
+
+
+def test_search_similar_on_storage_uses_resident_index(ctx, tmp_path):
+    from namazu_amd.signal import Event
+    from tests.test_host import _make_storage
+    evs = [Event.packet(f"entity-{i % 3}", "a", "b", {"n": i}) for i in range(40)]
+    runs = [evs[i:i + 30] for i in range(8)]
+    _make_storage(str(tmp_path), runs)
+    st = hs.LoadStorage(str(tmp_path))
+    t3, _ = st.GetStoredHistory(3)
+    near = st.SearchSimilar(t3, 3, 8)
+    assert near[0] == (3, 0) and [d for _, d in near] == sorted(d for _, d in near)
+    assert st._index.bitparallel
+    first = st._index
+    assert st.SearchSimilar(t3, 2, 8)[0] == (3, 0) and st._index is first  # reused, not rebuilt
