@@ -494,6 +494,33 @@ def bench_ed_secondary(args, torch, D, ctx, L, stream, spec):
     _lib.check(L.nmz_timing_enable(ctx.handle, 0))
     counters = np.zeros(_lib.NMZ_ED_NCOUNTERS, np.uint64)
     _lib.check(L.nmz_ed_plan_counters(plan, _lib.ptr(counters), stream))
+    single = None
+    if kind == "k_ed_bv" and D.rank == 0:
+        # single queries against the resident store (SearchSimilar): 8 stored traces as queries, one call
+        from namazu_amd.historystorage import TraceSet
+        qset = TraceSet([ts.trace(i) for i in range(8)])
+        kq = k + 1  # a stored trace queried finds itself too
+        qi = np.zeros(8 * kq, np.uint32)
+        qd = np.zeros(8 * kq, np.uint32)
+        reps = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            _lib.check(L.nmz_ed_plan_query_knn(plan, _lib.ptr(qset.off), _lib.ptr(qset.sym), 8, kq, _lib.ptr(qi),
+                                               _lib.ptr(qd)))
+            reps.append(time.perf_counter() - t0)
+        # the all-pairs k-NN lists of the same traces (self excluded) must agree with the single-query answers
+        agree = None
+        if D.world == 1:
+            keys8 = d_out.cpu().numpy().view(np.uint64).reshape(N, k)[:8]
+            agree = True
+            for i in range(8):
+                keep = qi.reshape(8, kq)[i] != i
+                ids_i, ds_i = qi.reshape(8, kq)[i][keep][:k], qd.reshape(8, kq)[i][keep][:k]
+                agree &= bool(np.array_equal((keys8[i] >> np.uint64(32)).astype(np.uint32), ds_i) and
+                              np.array_equal((keys8[i] & np.uint64(0xFFFFFFFF)).astype(np.uint32), ids_i))
+        single = dict(queries=8, ms_per_query=min(reps) * 1e3 / 8, pairs_per_s=8 * (N - 1) / min(reps),
+                      agrees_with_allpairs=agree,
+                      what="nmz_ed_plan_query_knn: 8 query traces vs the resident store, host arrays in and out")
     L.nmz_ed_plan_destroy(plan)
     pairs = N * (N - 1) // 2
     cells_per_pair = ED_LEN * (2 * ED_BAND + 1) - ED_BAND * (ED_BAND + 1)
@@ -504,8 +531,10 @@ def bench_ed_secondary(args, torch, D, ctx, L, stream, spec):
                        "band": ED_BAND, "k": k, "parallelism": f"pair-tile shards x{D.world}" +
                        (" + RCCL all_gather k-NN merge" if D.world > 1 else "")},
                kernel=kind, kernel_ms=kern_ms, plan_ms=plan_ms, synth_s=round(synth_s, 2),
-               roofline=roofline_valu(kind, (pairs + D.world - 1) // D.world, kern_ms),
+               roofline=roofline_valu(spec.get("valu_key", kind), (pairs + D.world - 1) // D.world, kern_ms),
                nominal_band_cells_per_s=pairs * cells_per_pair * steps / el)
+    if single:
+        out["single_query"] = single
     if counters[3]:  # k_ed_bv work counters of the last step (this rank's shard)
         c = [int(x) for x in counters]
         out["search"] = dict(
@@ -534,38 +563,8 @@ def bench_ed_secondary(args, torch, D, ctx, L, stream, spec):
     return out
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--seeds", type=int, default=1 << 20)
-    ap.add_argument("--events", type=int, default=4096)
-    ap.add_argument("--cpu-seeds", type=int, default=1 << 18)
-    ap.add_argument("--random-total", type=int, default=10_000_000)
-    ap.add_argument("--random-steps", type=int, default=3)
-    ap.add_argument("--cpu-random-seeds", type=int, default=256)
-    ap.add_argument("--e2e-traces", type=int, default=5)
-    ap.add_argument("--ed-traces", type=int, default=100_000)
-    ap.add_argument("--ed-steps", type=int, default=2)
-    ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
-    ap.add_argument("--no-secondary", dest="secondary", action="store_false")
-    args = ap.parse_args()
-    # The JSON line is the only output on stdout: whatever the libraries write to fd 1 during the run
-    # (gloo's connection messages, HIP/RCCL diagnostics) goes to stderr instead.
-    sys.stdout.flush()
-    out_fd = os.dup(1)
-    os.dup2(2, 1)
-
-    import torch
-    D = Dist()
-    torch.cuda.set_device(D.local_rank)
-    D.init(torch)
-    from namazu_amd import _lib
-    L = _lib.load()
-    ctx = _lib.Context(D.local_rank)
-    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-
+def headline_line(args, torch, D, ctx, L, stream):
+    """configs[1], the headline (see the module docstring)."""
     r = bench_replayable(args, torch, D, ctx, L, stream)
     decisions = D.world * r["S"] * r["E"] * args.steps
     value = decisions / r["elapsed"]
@@ -609,21 +608,67 @@ def main():
         line["roofline"]["declared_model_ops_per_unit"] = 6 * mean_len + 18
     if D.rank == 0 and D.world == 1 and args.cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_replayable(r, args)
+    return line
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--seeds", type=int, default=1 << 20)
+    ap.add_argument("--events", type=int, default=4096)
+    ap.add_argument("--cpu-seeds", type=int, default=1 << 18)
+    ap.add_argument("--random-total", type=int, default=10_000_000)
+    ap.add_argument("--random-steps", type=int, default=3)
+    ap.add_argument("--cpu-random-seeds", type=int, default=256)
+    ap.add_argument("--e2e-traces", type=int, default=5)
+    ap.add_argument("--ed-traces", type=int, default=100_000)
+    ap.add_argument("--ed-steps", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
+    ap.add_argument("--no-secondary", dest="secondary", action="store_false")
+    ap.add_argument("--legs", default="replayable,random,ed_clustered,ed_survey,ed_wide,config0",
+                    help="comma list of legs to run (profiling runs one leg at a time); the headline line "
+                         "needs 'replayable'")
+    args = ap.parse_args()
+    args.legs = set(args.legs.split(","))
+    # The JSON line is the only output on stdout: whatever the libraries write to fd 1 during the run
+    # (gloo's connection messages, HIP/RCCL diagnostics) goes to stderr instead.
+    sys.stdout.flush()
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
+
+    import torch
+    D = Dist()
+    torch.cuda.set_device(D.local_rank)
+    D.init(torch)
+    from namazu_amd import _lib
+    L = _lib.load()
+    ctx = _lib.Context(D.local_rank)
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    line = {}
+    if "replayable" in args.legs:
+        line = headline_line(args, torch, D, ctx, L, stream)
     if args.secondary:
         ed3 = dict(workload="configs[2] historystorage all-pairs search, clustered (families of 1,024 "
                             "near-duplicate runs)", traces=args.ed_traces, events=2048, band=32, k=8,
-                   generator="clustered_traces", gen_kwargs=dict(family=1024), steps=args.ed_steps)
+                   generator="clustered_traces", gen_kwargs=dict(family=1024), steps=args.ed_steps,
+                   valu_key="k_ed_bv:clustered")
         ed3s = dict(workload="configs[2] historystorage all-pairs search, survey generator (independent "
                              "mutations: every pair beyond the band)", traces=args.ed_traces, events=2048, band=32,
-                    k=8, generator="synth_traces", steps=args.ed_steps)
+                    k=8, generator="synth_traces", steps=args.ed_steps, valu_key="k_ed_bv:survey")
         ed5 = dict(workload="configs[4] long-trace stress, wide band", traces=256, events=65536, band=4096, k=8,
-                   generator="etcd_traces", steps=args.ed_steps)
-        line["secondary"] = [bench_random_fault_sweep(args, torch, D, ctx, L, stream),
-                             bench_ed_secondary(args, torch, D, ctx, L, stream, ed3),
-                             bench_ed_secondary(args, torch, D, ctx, L, stream, ed3s),
-                             bench_ed_secondary(args, torch, D, ctx, L, stream, ed5)]
-        if D.rank == 0 and D.world == 1 and args.cpu_baseline:
-            line["secondary"].append(bench_config0(args, torch, D, ctx, L))
+                   generator="etcd_traces", steps=args.ed_steps, valu_key="k_ed_wide")
+        sec = []
+        if "random" in args.legs:
+            sec.append(bench_random_fault_sweep(args, torch, D, ctx, L, stream))
+        for leg, spec in (("ed_clustered", ed3), ("ed_survey", ed3s), ("ed_wide", ed5)):
+            if leg in args.legs:
+                sec.append(bench_ed_secondary(args, torch, D, ctx, L, stream, spec))
+        if "config0" in args.legs and D.rank == 0 and D.world == 1 and args.cpu_baseline:
+            sec.append(bench_config0(args, torch, D, ctx, L))
+        line["secondary"] = sec
     if D.rank == 0:
         os.write(out_fd, (json.dumps(line) + "\n").encode())
     ctx.close()

@@ -1,39 +1,47 @@
 #!/usr/bin/env python3
-"""Per-unit VALU lane-instruction counts from a rocprofv3 summary (tools/summarize_profile.py output).
+"""Per-unit VALU lane-instruction counts from per-leg rocprofv3 summaries (tools/profile_r02.sh output).
 
-usage: valu_per_unit.py <summary.json> <tag>  -> writes profiles/valu_per_unit.json, which bench.py reads
-for each kernel's roofline (ops_per_unit = SQ_INSTS_VALU * 64 / units per launch). Units per launch are
-the bench workloads' (tools/profile.sh runs bench.py with its defaults).
+usage: valu_per_unit.py <profile dir with one sub-directory per bench leg> <tag>
+  -> profiles/valu_per_unit.json, which bench.py reads for each leg's roofline:
+     ops_per_unit = SQ_INSTS_VALU x 64 / units per launch of that leg's workload,
+     hbm_bytes_per_launch = 2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE correction),
+     clock_ghz = GRBM_GUI_ACTIVE / 8 XCDs / duration.
+The ED kernels' counts depend on the data through the cut-off, so each configs[2] generator has its own key.
 """
 import json
 import os
 import sys
 
-UNITS = {  # kernel name prefix -> (unit, units per launch of the bench workload)
-    "void nmz::k_replayable_sweep_fast": ("decision", 2**20 * 4096),
-    "nmz::k_random_sweep": ("decision", 2**20 * 10_000),
-    "void nmz::k_random_sweep<true>": ("decision", 2**20 * 10_000),
-    "void nmz::k_ed_bv<32>": ("pair", 100_000 * 99_999 // 2),
-    "void nmz::k_ed_wide<4>": ("pair", 256 * 255 // 2),
+# leg -> [(kernel name prefix, key, unit, units per launch of the leg's default workload)]
+LEGS = {
+    "replayable": [("void nmz::k_replayable_sweep_fast", "k_replayable_sweep_fast", "decision", 2**20 * 4096)],
+    "random": [("void nmz::k_random_sweep", "k_random_sweep", "decision", 10_000_000 * 10_000)],
+    "ed_clustered": [("void nmz::k_ed_bv<32>", "k_ed_bv:clustered", "pair", 100_000 * 99_999 // 2)],
+    "ed_survey": [("void nmz::k_ed_bv<32>", "k_ed_bv:survey", "pair", 100_000 * 99_999 // 2)],
+    "ed_wide": [("void nmz::k_ed_wide<4>", "k_ed_wide", "pair", 256 * 255 // 2)],
 }
 
 
 def main():
     src, tag = sys.argv[1], sys.argv[2]
-    summ = json.load(open(src))
-    out = {}
-    for name, e in summ.items():
-        for pre, (unit, n) in UNITS.items():
-            if name.startswith(pre) and "SQ_INSTS_VALU" in e:
-                key = pre.split("::")[1].split("<")[0]
-                out[key] = {"ops_per_unit": e["SQ_INSTS_VALU"] * 64 / n, "unit": unit, "units_per_launch": n,
-                            "kernel": name, "source": f"SQ_INSTS_VALU per launch, profiles/{tag}_summary.json",
-                            "hbm_bytes_per_launch": e.get("hbm_bytes_fetch_x2"),
-                            "clock_ghz": e.get("clock_ghz")}
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "valu_per_unit.json")
+    out = json.load(open(path)) if os.path.exists(path) else {}
+    for leg, kernels in LEGS.items():
+        f = os.path.join(src, leg, "summary.json")
+        if not os.path.exists(f):
+            continue
+        summ = json.load(open(f))
+        for name, e in summ.items():
+            for pre, key, unit, n in kernels:
+                if name.startswith(pre) and "SQ_INSTS_VALU" in e:
+                    out[key] = {"ops_per_unit": e["SQ_INSTS_VALU"] * 64 / n, "unit": unit, "units_per_launch": n,
+                                "kernel": name, "avg_ns": e["avg_ns"],
+                                "source": f"SQ_INSTS_VALU per launch, profiles/{tag}_{leg}_summary.json",
+                                "hbm_bytes_per_launch": e.get("hbm_bytes_fetch_x2"),
+                                "clock_ghz": e.get("clock_ghz")}
     json.dump(out, open(path, "w"), indent=1, sort_keys=True)
-    for k, v in out.items():
-        print(f"{k:24s} {v['ops_per_unit']:14.3f} VALU lane-instr / {v['unit']}")
+    for k, v in sorted(out.items()):
+        print(f"{k:26s} {v['ops_per_unit']:14.3f} VALU lane-instr / {v['unit']}  ({v['source']})")
 
 
 if __name__ == "__main__":
