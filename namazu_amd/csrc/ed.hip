@@ -27,6 +27,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <map>
+
 #include "nmz_common.h"
 #include "nmz_internal.h"
 
@@ -353,7 +355,10 @@ struct nmz_ed_plan {
     uint32_t ndw = 0, lds_dw = 0;  // bv: dwords per Peq row per query, LDS dwords per workgroup
     uint64_t n_chunks = 0;         // bv: total chunks (64-query block row x ED_BV_POOL candidates)
     uint16_t *d_bsym = nullptr;
-    uint64_t *d_chunk_start = nullptr;
+    uint64_t *d_chunk_start = nullptr;  // bv: [G+1] per-row chunk starts of the current shard (rewritten per call)
+    std::vector<uint64_t> row_chunks;    // bv: chunks per 64-query block row
+    std::map<uint64_t, std::vector<uint64_t>> shard_start;  // bv: per (shard, n_shards) row starts (host; kept, so
+                                                             // an async copy from it never sees it rewritten)
     uint64_t *d_counters = nullptr;  // bv: work counters of the latest search (nmz_ed_plan_counters)
     uint32_t maxlen = 0;
     std::unordered_map<uint64_t, uint32_t> dict;  // bv: symbol -> dense id (single-query search)
@@ -491,6 +496,8 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         for (uint32_t b = 0; b < G; ++b)
             chunk_start[b + 1] = chunk_start[b] + (N - 64 * b + p->pool - 1) / p->pool;
         p->n_chunks = chunk_start[G];
+        p->row_chunks.resize(G);
+        for (uint32_t b = 0; b < G; ++b) p->row_chunks[b] = chunk_start[b + 1] - chunk_start[b];
         std::vector<uint16_t> bs(soff[N] + 64, (uint16_t)zero_row);  // + 2 spare blocks at the end
         for (uint32_t i = 0; i < N; ++i)
             for (uint32_t t = 0; t < len[i]; ++t) bs[soff[i] + t] = (uint16_t)(ids[off[i] + t] * ndw * 8);
@@ -605,8 +612,18 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
         A.pool = p->pool;
         A.shard = shard;
         A.n_shards = n_shards;
-        A.n_chunks = shard < p->n_chunks ? (p->n_chunks - shard + n_shards - 1) / n_shards : 0;
+        // this shard's chunks per row: cr = ((shard - b) mod n_shards) + n_shards * t
+        std::vector<uint64_t> &ss = p->shard_start[((uint64_t)shard << 32) | n_shards];
+        if (ss.empty()) {
+            ss.assign(p->G + 1, 0);
+            for (uint32_t b = 0; b < p->G; ++b) {
+                const uint64_t nch = p->row_chunks[b], rot = (shard + n_shards - b % n_shards) % n_shards;
+                ss[b + 1] = ss[b] + (rot < nch ? (nch - rot + n_shards - 1) / n_shards : 0);
+            }
+        }
+        A.n_chunks = ss[p->G];
         if (A.n_chunks == 0) return NMZ_OK;
+        NMZ_HIP(hipMemcpyAsync(p->d_chunk_start, ss.data(), (p->G + 1) * 8, hipMemcpyHostToDevice, st));
         uint64_t blocks = A.n_chunks * 32;
         blocks = (blocks + 7) / 8 * 8;
         NMZ_CHECK(blocks < (1ULL << 31), "too many traces for one launch");

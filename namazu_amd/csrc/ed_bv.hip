@@ -270,14 +270,17 @@ __global__ __launch_bounds__(256) void k_ed_bv(EdBvArgs A) {
     const uint32_t lb = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
     const uint64_t lchunk = lb / 32;
     if (lchunk >= A.n_chunks) return;
-    const uint64_t chunk = lchunk * A.n_shards + A.shard;
+    // this shard's lchunk-th chunk: row b (binary search of the shard's per-row starts), then the row's
+    // chunks dealt round-robin starting at rank (b mod n_shards), so every rank gets every n_shards-th chunk
+    // of every row and the chunks next to the diagonal rotate over the ranks row by row
     uint32_t lo = 0, hi = A.G;
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) / 2;
-        if (A.chunk_start[mid] <= chunk) lo = mid; else hi = mid;
+        if (A.chunk_start[mid] <= lchunk) lo = mid; else hi = mid;
     }
     const uint32_t b = lo;
-    const uint32_t cr = (uint32_t)(chunk - A.chunk_start[b]);
+    const uint32_t rot = (A.shard + A.n_shards - b % A.n_shards) % A.n_shards;
+    const uint32_t cr = rot + A.n_shards * (uint32_t)(lchunk - A.chunk_start[b]);
     const uint32_t q1 = 64 * b + 2 * (lb % 32), q2 = q1 + 1;
     if (q1 >= A.N) return;  // whole workgroup
     const bool has2 = q2 < A.N;

@@ -32,7 +32,8 @@ struct EdBvArgs {
     const uint16_t *bsym;         // per-trace streams of Peq-row byte offsets (u16), padded to 32-blocks + 1
     const uint64_t *soff;         // [N] element offset of each trace's stream
     const uint32_t *len;          // [N]
-    const uint64_t *chunk_start;  // [G+1] first chunk of each 64-query block row
+    const uint64_t *chunk_start;  // [G+1] this shard's first chunk of each 64-query block row (row b's chunks
+                                  // cr = ((shard - b) mod n_shards) + n_shards * t, t = 0, 1, ...)
     uint64_t *knn;                // [N][k]
     uint64_t *counters;           // [ED_BV_NCOUNTERS] work counters (nmz_ed_plan_counters), or nullptr
     uint64_t n_chunks;            // chunks of this shard

@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Work balance of the all-pairs search's multi-GPU dealing, measured on one GPU.
+
+Runs each of n_shards shards of the configs[2] search (nmz_ed_allpairs_knn_shard_dev: every n_shards-th
+work chunk) one after the other on one device and records, per shard, the kernel time (HIP events) and
+k_ed_bv's executed-block counter. The job finishes when the slowest rank does, so max / mean of these is
+the dealing's loss at n_shards GPUs. usage: ed_shard_balance.py [generator] [n_shards] > out.json
+"""
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+
+def main():
+    gen = sys.argv[1] if len(sys.argv) > 1 else "clustered_traces"
+    S = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+    import torch
+    from namazu_amd import _lib, synth
+    L = _lib.load()
+    ctx = _lib.Context(0)
+    N, Lx, w, k = 100_000, 2048, 32, 8
+    ts = getattr(synth, gen)(N, Lx, **({"family": 1024} if gen == "clustered_traces" else {}))
+    plan = ctypes.c_void_p()
+    _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), N, w, ctypes.byref(plan)))
+    d = torch.empty(N * k, dtype=torch.int64, device="cuda")
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(L.nmz_timing_enable(ctx.handle, 1))
+    rows = []
+    cnt = np.zeros(_lib.NMZ_ED_NCOUNTERS, np.uint64)
+    for s in range(S):
+        tot, c = ctypes.c_double(), ctypes.c_uint64()
+        L.nmz_timing_read(ctx.handle, b"ed_bv", ctypes.byref(tot), ctypes.byref(c), 1)
+        _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, s, S, ctypes.c_void_p(d.data_ptr()), stream))
+        torch.cuda.synchronize()
+        _lib.check(L.nmz_timing_read(ctx.handle, b"ed_bv", ctypes.byref(tot), ctypes.byref(c), 1))
+        _lib.check(L.nmz_ed_plan_counters(plan, _lib.ptr(cnt), stream))
+        rows.append({"shard": s, "kernel_ms": tot.value, "dp_pairs": int(cnt[0]), "blocks": int(cnt[2]),
+                     "in_band": int(cnt[1])})
+    L.nmz_ed_plan_destroy(plan)
+    ms = np.array([r["kernel_ms"] for r in rows])
+    bl = np.array([r["blocks"] for r in rows], np.float64)
+    print(json.dumps({"generator": gen, "traces": N, "events": Lx, "band": w, "shards": S, "per_shard": rows,
+                      "time_max_over_mean": float(ms.max() / ms.mean()),
+                      "blocks_max_over_mean": float(bl.max() / bl.mean()),
+                      "sum_shard_ms": float(ms.sum())}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
