@@ -1,6 +1,8 @@
-"""CPU (gloo, world_size 2): the N>1 path -- seed-range sharding, all_gather of
-per-rank top-k and k-NN partial lists, deterministic merges -- checked against
-the single-process oracle result."""
+"""CPU (gloo, world_size 2): the N>1 host logic -- seed-range sharding (dist.shard_range), all_gather of per-rank
+top-k and k-NN partial lists (dist.gather_topk, dist.all_gather_bytes), deterministic merges (dist.merge_topk,
+dist.merge_knn_keys) -- checked against the single-process oracle result. There is no device here, so each rank's
+share is computed by the oracle; the same path with every rank on the device (the product's shard functions and
+the device merge) runs in tests/test_dist_gpu.py."""
 import os
 import socket
 
