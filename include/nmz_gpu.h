@@ -109,6 +109,10 @@ int nmz_device_count(int *count);
 int nmz_timing_enable(nmz_ctx *ctx, int on);
 int nmz_timing_read(nmz_ctx *ctx, const char *kernel, double *total_ms, uint64_t *count, int reset);
 
+/* FNV-1a 64 of each of n byte strings (CSR off[n+1] into bytes), one thread per string: the event
+ * identities of a batch of events (their canonical JSON; Go hash/fnv New64a). */
+int nmz_fnv1a64_batch(nmz_ctx *ctx, const uint64_t *off, const uint8_t *bytes, uint64_t n, uint64_t *out);
+
 /* ---- parameter resolution (host only, no device work) -------------------
  * min/max are time.Duration ns as parsed by LoadConfig; probability as float64.
  * Applies the prioritized x0.8 truncation in IEEE double exactly like

@@ -64,6 +64,7 @@ SIGNATURES = {
     "nmz_abi_version": (_int, []),
     "nmz_device_count": (_int, [ctypes.POINTER(_int)]),
     "nmz_random_params_resolve": (_int, [_i64, _i64, ctypes.c_double, _P]),
+    "nmz_fnv1a64_batch": (_int, [_P, _P, _P, _u64, _P]),
     "nmz_replayable_sweep": (_int, [_P, _P, _P, _u64, _P, _P, _u32, _i64, _P, _P, _u64, _u32, _P]),
     "nmz_replayable_plan_create": (_int, [_P, _P, _P, _u32, _i64, _u64, ctypes.POINTER(_P)]),
     "nmz_replayable_plan_destroy": (_int, [_P]),

@@ -372,6 +372,103 @@ struct nmz_ed_plan {
 
 namespace nmz {
 
+// stored streams of the bit-parallel plan from device symbols: one block per trace, each symbol's dense id is its
+// rank among the sorted distinct symbols (binary search), written as its Peq row's byte offset (id * ndw * 8)
+__global__ __launch_bounds__(256) void k_ed_bv_remap(const uint64_t *__restrict__ off, const uint64_t *__restrict__ sym,
+                                                     const uint64_t *__restrict__ uniq, uint32_t n_uniq,
+                                                     const uint64_t *__restrict__ soff, uint32_t row_bytes,
+                                                     uint16_t *__restrict__ bs) {
+    const uint32_t i = blockIdx.x;
+    const uint64_t b = off[i], n = off[i + 1] - b, so = soff[i];
+    for (uint64_t t = threadIdx.x; t < n; t += 256) {
+        const uint64_t x = sym[b + t];
+        uint32_t lo = 0, hi = n_uniq;  // first index with uniq[idx] >= x (x is present)
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (uniq[mid] < x) lo = mid + 1; else hi = mid;
+        }
+        bs[so + t] = (uint16_t)(lo * row_bytes);
+    }
+}
+
+constexpr uint64_t ED_DEVICE_REMAP_MIN = 1ULL << 20;  // symbols; smaller stores keep the host remap
+
+// The bit-parallel plan built on the device: upload the symbols, sort/unique them (dense ids = ranks), write the
+// candidate streams with a binary search per symbol. Returns 1 (not applicable: the alphabet does not fit the
+// bit-parallel LDS tables) so the caller falls back to the host build and the other kernels.
+static int ed_plan_build_bv_device(nmz_ed_plan *p, const uint64_t *off, const uint64_t *sym, uint32_t N,
+                                   uint32_t band, uint32_t maxlen) {
+    hipStream_t st = p->ctx->stream;
+    const uint64_t total = off[N];
+    NMZ_CHECK(total == 0 || sym, "sym is NULL");
+    DevBuf tmp;
+    struct Release {
+        DevBuf &b;
+        ~Release() { b.release(); }
+    } release_tmp{tmp};
+    NMZ_TRY(tmp.ensure(Carve::bytes_for(total, 8) * 2 + Carve::bytes_for(N + 1, 8)));
+    Carve tv(tmp.ptr);
+    uint64_t *d_sym = tv.take<uint64_t>(total), *d_uniq = tv.take<uint64_t>(total);
+    uint64_t *d_off = tv.take<uint64_t>(N + 1);
+    NMZ_HIP(hipMemcpyAsync(d_sym, sym, total * 8, hipMemcpyHostToDevice, st));
+    NMZ_HIP(hipMemcpyAsync(d_off, off, (N + 1) * 8, hipMemcpyHostToDevice, st));
+    uint64_t n_uniq = 0;
+    NMZ_TRY(device_unique_u64(d_sym, total, d_uniq, &n_uniq, st));
+    const uint32_t KF = (2 * band + 31) / 32;
+    const uint32_t ndw = ((maxlen + 31) / 32 + KF + 2) | 1;
+    if (n_uniq >= MAX_FAST_SYMBOLS || (n_uniq + 1) * ndw * 8 > 65536) return 1;
+    const uint32_t n_sym = (uint32_t)n_uniq, G = (N + 63) / 64;
+    p->bv = true;
+    p->fast = true;
+    p->ndw = ndw;
+    p->lds_dw = (uint32_t)((((uint64_t)(n_sym + 1) * ndw * 8 + 15) / 16) * 4);
+    p->G = G;
+    p->maxlen = maxlen;
+    p->n_sym = n_sym;
+    const uint32_t zero_row = n_sym * ndw * 8;
+    std::vector<uint32_t> len(N + 1, 0);
+    std::vector<uint64_t> soff(N + 1, 0), chunk_start(G + 1, 0);
+    for (uint32_t i = 0; i < N; ++i) {
+        len[i] = (uint32_t)(off[i + 1] - off[i]);
+        soff[i + 1] = soff[i] + ((uint64_t)(len[i] + 31) / 32 + 1) * 32;
+    }
+    p->pool = N >= 24576 ? 4 * ED_BV_POOL : (N >= 12288 ? 2 * ED_BV_POOL : ED_BV_POOL);
+    if (const char *e = getenv("NMZ_ED_POOL")) {
+        const uint32_t v = (uint32_t)atoi(e);
+        if (v >= 256 && v % 256 == 0) p->pool = v;
+    }
+    for (uint32_t b = 0; b < G; ++b) chunk_start[b + 1] = chunk_start[b] + (N - 64 * b + p->pool - 1) / p->pool;
+    p->n_chunks = chunk_start[G];
+    p->row_chunks.resize(G);
+    for (uint32_t b = 0; b < G; ++b) p->row_chunks[b] = chunk_start[b + 1] - chunk_start[b];
+    const uint64_t bs_n = soff[N] + 64;
+    NMZ_TRY(p->mem.ensure(Carve::bytes_for(bs_n, 2) + Carve::bytes_for(N + 1, 8) * 2 + Carve::bytes_for(G + 1, 8) +
+                          Carve::bytes_for(N + 1, 4) + Carve::bytes_for(ED_BV_NCOUNTERS, 8)));
+    Carve cv(p->mem.ptr);
+    p->d_counters = cv.take<uint64_t>(ED_BV_NCOUNTERS);
+    p->d_bsym = cv.take<uint16_t>(bs_n);
+    p->d_soff = cv.take<uint64_t>(N + 1);
+    p->d_qoff = cv.take<uint64_t>(N + 1);
+    p->d_chunk_start = cv.take<uint64_t>(G + 1);
+    p->d_len = cv.take<uint32_t>(N + 1);
+    NMZ_HIP(hipMemsetD16Async((hipDeviceptr_t)p->d_bsym, (unsigned short)zero_row, bs_n, st));
+    NMZ_HIP(hipMemcpyAsync(p->d_soff, soff.data(), (N + 1) * 8, hipMemcpyHostToDevice, st));
+    NMZ_HIP(hipMemcpyAsync(p->d_qoff, off, (N + 1) * 8, hipMemcpyHostToDevice, st));
+    NMZ_HIP(hipMemcpyAsync(p->d_chunk_start, chunk_start.data(), (G + 1) * 8, hipMemcpyHostToDevice, st));
+    NMZ_HIP(hipMemcpyAsync(p->d_len, len.data(), (N + 1) * 4, hipMemcpyHostToDevice, st));
+    NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_BV_NCOUNTERS * 8, st));
+    hipLaunchKernelGGL(k_ed_bv_remap, dim3(N), dim3(256), 0, st, d_off, d_sym, d_uniq, n_sym, p->d_soff, ndw * 8,
+                       p->d_bsym);
+    NMZ_HIP(hipGetLastError());
+    // the dictionary for single queries (nmz_ed_plan_query_knn): symbol -> rank
+    std::vector<uint64_t> uniq(n_sym);
+    NMZ_HIP(hipMemcpyAsync(uniq.data(), d_uniq, (uint64_t)n_sym * 8, hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipStreamSynchronize(st));
+    p->dict.reserve(n_sym * 2);
+    for (uint32_t i = 0; i < n_sym; ++i) p->dict.emplace(uniq[i], i);
+    return NMZ_OK;
+}
+
 static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, uint32_t N, uint32_t band,
                          nmz_ed_plan **out) {
     NMZ_CHECK(ctx && out, "NULL argument");
@@ -385,6 +482,22 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
     const uint64_t total = N ? off[N] : 0;
     uint32_t maxlen = 0;
     for (uint32_t i = 0; i < N; ++i) maxlen = std::max<uint32_t>(maxlen, (uint32_t)(off[i + 1] - off[i]));
+    if (ed_bv_supported(band) && maxlen + band < MAX_FAST_LEN && total >= ED_DEVICE_REMAP_MIN &&
+        total < (1ULL << 31) && !getenv("NMZ_ED_HOST_REMAP")) {
+        const int rc = ed_plan_build_bv_device(p, off, sym, N, band, maxlen);
+        if (rc == NMZ_OK) {
+            *out = p;
+            return NMZ_OK;
+        }
+        p->mem.release();
+        const bool not_applicable = rc == 1;
+        delete p;
+        if (!not_applicable) return rc;
+        p = new nmz_ed_plan();  // alphabet too large for the bit-parallel tables: host build below
+        p->ctx = ctx;
+        p->n = N;
+        p->band = band;
+    }
     // dense symbol ids (exact remap: a == b <=> id(a) == id(b))
     std::vector<uint16_t> ids;
     const bool want_wide = ed_wide_supported(band);

@@ -259,8 +259,20 @@ __device__ __forceinline__ void bv_load_block(uint32_t (&dst)[16], const uint16_
     }
 }
 
+// Occupancy: 5 waves/SIMD (<= 96 VGPRs; the compiler spills 6 VGPRs outside the 32-column block). configs[2]
+// clustered, 100k x 2,048: 1.509 s at the unconstrained 100 VGPRs (4 waves), 1.487 s at 5, 1.667 s at 6 (31
+// spills, some in the block refill path). NMZ_ED_BV_WAVES overrides for A/B builds.
+#ifndef NMZ_ED_BV_WAVES
+#define NMZ_ED_BV_WAVES 5
+#endif
+#if NMZ_ED_BV_WAVES > 0
+#define NMZ_ED_BV_ATTR __attribute__((amdgpu_waves_per_eu(NMZ_ED_BV_WAVES, NMZ_ED_BV_WAVES)))
+#else
+#define NMZ_ED_BV_ATTR
+#endif
+
 template <int W>
-__global__ __launch_bounds__(256) void k_ed_bv(EdBvArgs A) {
+__global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv(EdBvArgs A) {
     using SH = BvShape<W>;
     extern __shared__ uint32_t peq[];
     // pool counter lives after the Peq tables (a static __shared__ variable

@@ -6,6 +6,7 @@
 #include <new>
 
 #include "nmz_common.h"
+#include "nmz_internal.h"
 
 namespace nmz {
 
@@ -270,6 +271,45 @@ int nmz_timing_read(nmz_ctx *ctx, const char *kernel, double *total_ms, uint64_t
         }
         it->second.clear();
     }
+    return NMZ_OK;
+}
+
+}  // extern "C"
+
+namespace nmz {
+// one thread per string: FNV-1a 64 over its bytes (event identities)
+__global__ __launch_bounds__(256) void k_fnv_batch(const uint64_t *__restrict__ off, const uint8_t *__restrict__ bytes,
+                                                   uint64_t n, uint64_t *__restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint64_t h = FNV_OFFSET;
+    for (uint64_t b = off[i], e = off[i + 1]; b < e; ++b) h = fnv_step(h, bytes[b]);
+    out[i] = h;
+}
+}  // namespace nmz
+
+extern "C" {
+
+int nmz_fnv1a64_batch(nmz_ctx *ctx, const uint64_t *off, const uint8_t *bytes, uint64_t n, uint64_t *out) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    if (n == 0) return NMZ_OK;
+    NMZ_CHECK(off && out, "NULL argument");
+    for (uint64_t i = 0; i < n; ++i) NMZ_CHECK(off[i] <= off[i + 1], "offsets must not decrease");
+    const uint64_t nb = off[n];
+    NMZ_CHECK(nb == 0 || bytes, "bytes is NULL");
+    hipStream_t st = ctx->stream;
+    NMZ_TRY(ctx->buf[12].ensure(Carve::bytes_for(n + 1, 8) * 2 + Carve::bytes_for(nb + 1, 1)));
+    Carve cv(ctx->buf[12].ptr);
+    uint64_t *d_off = cv.take<uint64_t>(n + 1), *d_out = cv.take<uint64_t>(n + 1);
+    uint8_t *d_b = cv.take<uint8_t>(nb + 1);
+    NMZ_HIP(hipMemcpyAsync(d_off, off, (n + 1) * 8, hipMemcpyHostToDevice, st));
+    if (nb) NMZ_HIP(hipMemcpyAsync(d_b, bytes, nb, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_fnv_batch, dim3(ceil_div(n, 256)), dim3(256), 0, st, d_off, d_b, n, d_out);
+    NMZ_HIP(hipGetLastError());
+    NMZ_HIP(hipMemcpyAsync(out, d_out, n * 8, hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipStreamSynchronize(st));
     return NMZ_OK;
 }
 

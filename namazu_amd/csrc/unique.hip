@@ -206,6 +206,37 @@ static int classes_launch(nmz_ctx *ctx, const uint64_t *d_sig, uint32_t N, uint3
     return NMZ_OK;
 }
 
+// Sorted distinct values of d_sym[0..total) into d_uniq (capacity total), their count into *n_uniq (host).
+// Scratch: 2 x total x 8 B + hipcub's temporary storage, allocated here and released before returning.
+int device_unique_u64(const uint64_t *d_sym, uint64_t total, uint64_t *d_uniq, uint64_t *n_uniq, hipStream_t st) {
+    *n_uniq = 0;
+    if (total == 0) return NMZ_OK;
+    NMZ_CHECK(total < (1ULL << 31), "more than 2^31-1 symbols for the device remap");
+    size_t sort_bytes = 0, uniq_bytes = 0;
+    NMZ_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_bytes, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                                              (int)total, 0, 64, st));
+    NMZ_HIP(hipcub::DeviceSelect::Unique(nullptr, uniq_bytes, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                                         (uint64_t *)nullptr, (int)total, st));
+    DevBuf scr;
+    NMZ_TRY(scr.ensure(Carve::bytes_for(total, 8) + Carve::bytes_for(1, 8) +
+                       Carve::bytes_for(std::max(sort_bytes, uniq_bytes) + 1, 1)));
+    Carve cv(scr.ptr);
+    uint64_t *sorted = cv.take<uint64_t>(total);
+    uint64_t *d_n = cv.take<uint64_t>(1);
+    void *tmp = cv.take<char>(std::max(sort_bytes, uniq_bytes) + 1);
+    size_t b = sort_bytes;
+    int rc = NMZ_OK;
+    if (hipcub::DeviceRadixSort::SortKeys(tmp, b, d_sym, sorted, (int)total, 0, 64, st) != hipSuccess) rc = NMZ_EHIP;
+    b = uniq_bytes;
+    if (rc == NMZ_OK && hipcub::DeviceSelect::Unique(tmp, b, sorted, d_uniq, d_n, (int)total, st) != hipSuccess)
+        rc = NMZ_EHIP;
+    if (rc == NMZ_OK && (hipMemcpyAsync(n_uniq, d_n, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                         hipStreamSynchronize(st) != hipSuccess))
+        rc = NMZ_EHIP;
+    scr.release();
+    return rc == NMZ_OK ? NMZ_OK : fail(NMZ_EHIP, "device symbol sort/unique failed");
+}
+
 }  // namespace nmz
 
 using namespace nmz;

@@ -332,14 +332,19 @@ class Random(ExplorePolicy):
         return _lib.resolve_random_params(self.MinInterval, self.MaxInterval,
                                           self.FaultActionProbability)
 
-    def event_inputs(self, events):
-        """events -> (evhash uint64[E], evclass uint8[E]) as the kernel consumes them."""
+    def event_inputs(self, events, ctx=None):
+        """events -> (evhash uint64[E], evclass uint8[E]) as the kernel consumes them. The event hashes of a
+        batch are computed on the GPU (nmz_fnv1a64_batch over the events' canonical JSON)."""
         evhash = np.zeros(len(events), np.uint64)
         evclass = np.zeros(len(events), np.uint8)
+        if events:
+            off, data = to_csr([ev.canonical_json() for ev in events])
+            off64 = off.astype(np.uint64)
+            _lib.check(_lib.load().nmz_fnv1a64_batch((ctx or self._ctx()).handle, _lib.ptr(off64), _lib.ptr(data),
+                                                     len(events), _lib.ptr(evhash)))
         for i, ev in enumerate(events):
             if ev.Class() == "ProcSetEvent":
                 raise ValueError("ProcSetEvent decisions belong to procPolicy (out of scope)")
-            evhash[i] = ev.evhash()
             c = 0
             if ev.EntityID() in self.PrioritizedEntities:
                 c |= _lib.NMZ_EV_PRIORITIZED

@@ -17,6 +17,7 @@ Event.Equals modulo 64-bit collisions.
 """
 import json
 import math
+import re
 import uuid as _uuid
 
 FNV_OFFSET = 0xCBF29CE484222325
@@ -63,7 +64,12 @@ def _go_float(f: float) -> str:
     return r[:-2] if r.endswith(".0") else r
 
 
+_PLAIN = re.compile(r'[^"\\<>&\x00-\x1f\u2028\u2029]*\Z')
+
+
 def _go_string(s: str) -> str:
+    if _PLAIN.match(s):  # nothing to escape (the common case): Go writes the string as is
+        return '"' + s + '"'
     out = ['"']
     for ch in s:
         c = ord(ch)

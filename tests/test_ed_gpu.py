@@ -317,3 +317,25 @@ def test_search_similar_on_storage_uses_resident_index(ctx, tmp_path):
     assert st._index.bitparallel
     first = st._index
     assert st.SearchSimilar(t3, 2, 8)[0] == (3, 0) and st._index is first  # reused, not rebuilt
+
+
+def test_device_and_host_plan_builds_agree(ctx, monkeypatch):
+    """Stores of >= 2^20 symbols build the bit-parallel plan on the device (sort/unique + binary-search remap);
+    NMZ_ED_HOST_REMAP forces the host build. Both give the oracle's k-NN lists and the same single-query answers
+    (the query dictionary comes from the device's sorted symbols)."""
+    rng = np.random.default_rng(77)
+    ts = make_traces(600, 1700, 2000, 0.01, alphabet=40, rng=rng)
+    assert int(ts.off[-1]) >= 1 << 20
+    ids_d, ds_d = knn(ctx, ts, 32, 5)
+    qs = [ts.trace(5), ts.trace(9)[:1500]]
+    qi_d, qd_d = hs.SimilarityIndex(ts, 32, ctx=ctx).query(qs, 4)
+    monkeypatch.setenv("NMZ_ED_HOST_REMAP", "1")
+    ids_h, ds_h = knn(ctx, ts, 32, 5)
+    qi_h, qd_h = hs.SimilarityIndex(ts, 32, ctx=ctx).query(qs, 4)
+    assert np.array_equal(ids_d, ids_h) and np.array_equal(ds_d, ds_h)
+    assert np.array_equal(qi_d, qi_h) and np.array_equal(qd_d, qd_h)
+    for q in [0, 299, 599]:
+        pairs = np.array([[q, c] for c in range(len(ts)) if c != q], np.uint32)
+        d = O.ed_pairs(ts.off, ts.sym, pairs, 32, nthreads=16)
+        order = np.lexsort((pairs[:, 1], d))[:5]
+        assert ds_d[q].tolist() == d[order].tolist() and ids_d[q].tolist() == pairs[order, 1].tolist()

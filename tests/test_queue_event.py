@@ -171,3 +171,25 @@ def test_online_decisions_match_the_sweep(ctx):
     p.event_inputs = lambda evs: (np.array([e.h for e in evs], np.uint64), np.array([e.c for e in evs], np.uint8))
     d, f = p.decide_events([_E(h, c) for h, c in zip(eh, ec)])
     assert np.array_equal(d, r.delays[0]) and np.array_equal(f, r.faults[0].astype(bool))
+
+
+@pytest.mark.gpu
+def test_event_hashes_on_the_gpu_match_the_host_rule(ctx):
+    """nmz_fnv1a64_batch (event identities of a decision batch) == FNV-1a 64 of the canonical JSON on the host,
+    including empty strings and the published vectors."""
+    from namazu_amd import _lib
+    from namazu_amd.explorepolicy import to_csr
+    from namazu_amd.signal import fnv1a64
+    rng = np.random.default_rng(8)
+    strs = [b"", b"a", b"foobar"] + [bytes(rng.integers(0, 256, int(n), dtype=np.uint8))
+                                      for n in rng.integers(0, 600, 300)]
+    off, data = to_csr(strs)
+    off64 = off.astype(np.uint64)  # kept alive across the call
+    out = np.zeros(len(strs), np.uint64)
+    _lib.check(_lib.load().nmz_fnv1a64_batch(ctx.handle, _lib.ptr(off64), _lib.ptr(data), len(strs), _lib.ptr(out)))
+    assert out.tolist() == [fnv1a64(x) for x in strs]
+    assert int(out[0]) == 0xCBF29CE484222325 and int(out[2]) == 0x85944171F73967E8
+    p = _random_policy()
+    events = [packet_event(i, 5) for i in range(100)]
+    eh, _ = p.event_inputs(events)
+    assert eh.tolist() == [e.evhash() for e in events]

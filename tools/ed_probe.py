@@ -20,9 +20,11 @@ def main():
     reps = int(sys.argv[5]) if len(sys.argv) > 5 else 3
     import torch
     from namazu_amd import _lib
-    from namazu_amd.synth import etcd_traces, synth_traces
+    from namazu_amd.synth import clustered_traces, etcd_traces, synth_traces
     t0 = time.time()
-    ts = etcd_traces(N, L) if (len(sys.argv) > 6 and sys.argv[6] == "etcd") else synth_traces(N, L)
+    gen = sys.argv[6] if len(sys.argv) > 6 else ""
+    ts = etcd_traces(N, L) if gen == "etcd" else (clustered_traces(N, L, family=1024) if gen == "clustered"
+                                                  else synth_traces(N, L))
     print(f"synth {time.time() - t0:.1f}s", flush=True)
     Lb = _lib.load()
     ctx = _lib.Context(0)
