@@ -376,6 +376,78 @@ def bench_random_fault_sweep(args, torch, D, ctx, L, stream):
     return out
 
 
+def bench_visualize(args, torch, D, ctx, L, stream):
+    """`nmz tools visualize` over a 100k-run store (2,048 events, 16 entities; runs repeat earlier runs exactly or
+    re-interleaved across entities): the unique-trace curve in the reference's default partial-order mode and
+    in exact mode, one nmz_unique_traces_dev call each (signatures + radix-sort classes) on device-resident
+    traces. The reference compares every new run with every unique one so far (O(n^2) equality tests,
+    visualize.go:126-172); its CPU restatement runs on a sample."""
+    from namazu_amd import _lib
+    from namazu_amd import synth
+    N, Lx = args.vis_traces, 2048
+    t0 = time.time()
+    ts, ent, n_bases = synth.po_store(N, Lx)
+    synth_s = time.time() - t0
+    dev = torch.device("cuda", D.local_rank)
+    d_off = torch.from_numpy(ts.off.view(np.int64)).to(dev)
+    d_sym = torch.from_numpy(ts.sym.view(np.int64)).to(dev)
+    d_ent = torch.from_numpy(ent.view(np.int32)).to(dev)
+    d_sig = torch.empty(2 * N, dtype=torch.int64, device=dev)
+    d_first = torch.empty(N, dtype=torch.int32, device=dev)
+
+    def run(po):
+        _lib.check(L.nmz_unique_traces_dev(ctx.handle, ctypes.c_void_p(d_off.data_ptr()),
+                                           ctypes.c_void_p(d_sym.data_ptr()),
+                                           ctypes.c_void_p(d_ent.data_ptr()) if po else None, N, 16,
+                                           ctypes.c_void_p(d_sig.data_ptr()), ctypes.c_void_p(d_first.data_ptr()),
+                                           stream))
+
+    out = dict(metric="visualize unique-trace curve, traces/s", unit="traces/s",
+               config={"workload": "nmz tools visualize (gnuplot) over a stored-run set", "traces": N, "events": Lx,
+                       "entities": 16, "distinct_runs_by_construction": n_bases}, synth_s=round(synth_s, 2))
+    for po in (True, False):
+        run(po)
+        torch.cuda.synchronize()
+        tot, cnt = ctypes.c_double(), ctypes.c_uint64()
+        _lib.check(L.nmz_timing_enable(ctx.handle, 1))
+        L.nmz_timing_read(ctx.handle, b"trace_sig", ctypes.byref(tot), ctypes.byref(cnt), 1)
+        steps = 3
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            run(po)
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) / steps
+        _lib.check(L.nmz_timing_read(ctx.handle, b"trace_sig", ctypes.byref(tot), ctypes.byref(cnt), 1))
+        _lib.check(L.nmz_timing_enable(ctx.handle, 0))
+        first = d_first.cpu().numpy().view(np.uint32)
+        uniq = int((first == np.arange(N)).sum())
+        sig_ms = tot.value / max(cnt.value, 1)
+        out["po" if po else "exact"] = dict(
+            value=N / el, ms=el * 1e3, unique=uniq, sig_kernel_ms=sig_ms,
+            sig_hbm_gbs=ts.sym.nbytes * (1.5 if po else 1.0) / (sig_ms * 1e-3) / 1e9)
+    out["value"] = out["po"]["value"]
+    out["po"]["unique_matches_construction"] = out["po"]["unique"] == n_bases
+    if D.rank == 0 and args.cpu_baseline:
+        from oracle import oracle as O
+        n = args.vis_cpu_traces
+        raw = [list(zip(ent[i * Lx:(i + 1) * Lx].tolist(), ts.sym[i * Lx:(i + 1) * Lx].tolist())) for i in range(n)]
+        t0 = time.perf_counter()
+        curve = O.unique_curve_po(raw)
+        dt = time.perf_counter() - t0
+        from namazu_amd.historystorage import TraceSet
+        sub_ts = TraceSet([ts.sym[i * Lx:(i + 1) * Lx] for i in range(n)])
+        fe = np.zeros(n, np.uint32)
+        ent_sub = np.ascontiguousarray(ent[:n * Lx])
+        _lib.check(L.nmz_unique_traces(ctx.handle, _lib.ptr(sub_ts.off), _lib.ptr(sub_ts.sym), _lib.ptr(ent_sub), n,
+                                       _lib.ptr(fe)))
+        gpu_curve = np.cumsum(fe == np.arange(n)).tolist()
+        out["cpu_baseline"] = dict(value=n / dt, unit="traces/s", cores=1, kind="port",
+                                   sample=f"first {n} runs, oracle.unique_curve_po (the reference's loops, O(n^2) "
+                                          f"in runs: the rate falls as the store grows)",
+                                   seconds=round(dt, 3), parity_with_gpu=gpu_curve == curve)
+    return out
+
+
 def bench_config0(args, torch, D, ctx, L):
     """configs[0]: the random policy over one 10k-event trace under one seed, the reference's own CPU case.
     Reported: the CPU restatement on one core (the reference decides on one goroutine per event, seeding Go's
@@ -631,7 +703,9 @@ def main():
     ap.add_argument("--ed-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     ap.add_argument("--no-secondary", dest="secondary", action="store_false")
-    ap.add_argument("--legs", default="replayable,random,ed_clustered,ed_survey,ed_wide,config0",
+    ap.add_argument("--vis-traces", type=int, default=100_000)
+    ap.add_argument("--vis-cpu-traces", type=int, default=1000)
+    ap.add_argument("--legs", default="replayable,random,ed_clustered,ed_survey,ed_wide,visualize,config0",
                     help="comma list of legs to run (profiling runs one leg at a time); the headline line "
                          "needs 'replayable'")
     args = ap.parse_args()
@@ -670,6 +744,8 @@ def main():
         for leg, spec in (("ed_clustered", ed3), ("ed_survey", ed3s), ("ed_wide", ed5)):
             if leg in args.legs:
                 sec.append(bench_ed_secondary(args, torch, D, ctx, L, stream, spec))
+        if "visualize" in args.legs and D.rank == 0:
+            sec.append(bench_visualize(args, torch, D, ctx, L, stream))
         if "config0" in args.legs and D.rank == 0 and D.world == 1 and args.cpu_baseline:
             sec.append(bench_config0(args, torch, D, ctx, L))
         line["secondary"] = sec

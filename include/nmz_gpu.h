@@ -274,7 +274,8 @@ int nmz_trace_signatures(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
                          uint32_t n_traces, uint64_t *sig);
 int nmz_unique_traces(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, const uint32_t *entity,
                       uint32_t n_traces, uint32_t *first_equal);
-/* Device-resident variant: d_entity may be NULL (exact mode); max_entities bounds the entity ids;
+/* Device-resident variant: d_entity may be NULL (exact mode); entity ids must be < max_entities (<= 16384;
+ * larger ids are skipped like NMZ_NONE, so the caller must pass the true bound);
  * d_sig[2*n_traces] receives the signatures. Enqueued on `stream` (NULL = the context's). */
 int nmz_unique_traces_dev(nmz_ctx *ctx, const uint64_t *d_off, const uint64_t *d_sym, const uint32_t *d_entity,
                           uint32_t n_traces, uint32_t max_entities, uint64_t *d_sig, uint32_t *d_first_equal,

@@ -26,8 +26,8 @@
 // k_trace_sig: one wave per trace, 64 elements per step. PO ranks come from
 // per-wave LDS counters indexed by the element's entity id (dense per trace,
 // assigned by the host while it reads the trace): the lanes of one entity within
-// a step are found with a ballot per distinct entity, rank = counter + number of
-// lower lanes in that ballot. Classes: radix sort of (sig hi, sig lo) with the
+// a step are the intersection of one ballot per bit of the id (ceil(log2 ids)
+// ballots), rank = counter + number of lower lanes in that set. Classes: radix sort of (sig hi, sig lo) with the
 // trace index as payload (stable, so equal signatures keep index order), then
 // first_equal[i] = the index at the start of i's run (max-scan of run heads).
 #include <hipcub/hipcub.hpp>
@@ -61,7 +61,8 @@ __device__ __forceinline__ uint64_t mix_b(uint64_t s, uint32_t r) {
 template <bool PO>
 __global__ __launch_bounds__(256) void k_trace_sig(const uint64_t *__restrict__ off, const uint64_t *__restrict__ sym,
                                                    const uint32_t *__restrict__ ent, uint32_t N, uint32_t max_ent,
-                                                   uint32_t waves_per_block, uint64_t *__restrict__ sig) {
+                                                   uint32_t kbits, uint32_t waves_per_block,
+                                                   uint64_t *__restrict__ sig) {
     extern __shared__ uint32_t cnt_all[];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t t = blockIdx.x * waves_per_block + wv;
@@ -81,21 +82,21 @@ __global__ __launch_bounds__(256) void k_trace_sig(const uint64_t *__restrict__ 
         uint32_t rank = (uint32_t)i;
         bool take = valid;
         if (PO) {
-            const uint32_t e = valid ? ent[base + i] : NMZ_NONE;
-            take = valid && e != NMZ_NONE;
-            bool todo = take;
-            uint64_t m = __ballot(todo);
-            while (m) {
-                const int leader = __ffsll((unsigned long long)m) - 1;
-                const uint32_t e0 = __shfl(e, leader, 64);
-                const uint64_t grp = __ballot(todo && e == e0);
-                const uint32_t before = cnt[e0];
-                if (todo && e == e0) {
-                    rank = before + (uint32_t)__popcll(grp & below);
-                    todo = false;
-                }
-                if ((int)lane == leader) cnt[e0] = before + (uint32_t)__popcll(grp);
-                m &= ~grp;
+            const uint32_t e0 = valid ? ent[base + i] : NMZ_NONE;
+            take = valid && e0 < max_ent;  // NMZ_NONE (no event) skipped; ids past the bound never index LDS
+            const uint32_t e = take ? e0 : 0u;
+            // lanes holding the same entity: intersect, bit by bit of the id, the ballot of lanes that agree
+            // on that bit (kbits ballots per 64 elements instead of one per distinct entity)
+            uint64_t same = __ballot(take);
+            for (uint32_t b = 0; b < kbits; ++b) {
+                const bool bit = (e >> b) & 1u;
+                const uint64_t B = __ballot(take && bit);
+                same &= bit ? B : ~B;
+            }
+            if (take) {
+                const uint32_t before = cnt[e];  // every lane reads before any lane of the wave writes
+                rank = before + (uint32_t)__popcll(same & below);
+                if ((same >> lane) == 1ull) cnt[e] = before + (uint32_t)__popcll(same);  // the group's last lane
             }
         }
         if (take) {
@@ -156,13 +157,15 @@ static int sig_launch(const uint64_t *d_off, const uint64_t *d_sym, const uint32
     if (N == 0) return NMZ_OK;
     if (!d_ent) {
         hipLaunchKernelGGL(k_trace_sig<false>, dim3(ceil_div(N, SIG_WAVES)), dim3(64 * SIG_WAVES), 0, st, d_off, d_sym,
-                           nullptr, N, 0u, SIG_WAVES, d_sig);
+                           nullptr, N, 0u, 0u, SIG_WAVES, d_sig);
     } else {
         NMZ_CHECK(max_ent <= SIG_MAX_ENT, "more than 16384 distinct entities in one trace");
         const uint32_t me = max_ent ? max_ent : 1;
         const uint32_t wpb = me <= SIG_MAX_ENT_LDS ? SIG_WAVES : 1;
+        uint32_t kbits = 0;
+        while ((1u << kbits) < me) ++kbits;
         hipLaunchKernelGGL(k_trace_sig<true>, dim3(ceil_div(N, wpb)), dim3(64 * wpb), (size_t)wpb * me * 4, st, d_off,
-                           d_sym, d_ent, N, me, wpb, d_sig);
+                           d_sym, d_ent, N, me, kbits, wpb, d_sig);
     }
     NMZ_HIP(hipGetLastError());
     return NMZ_OK;

@@ -126,3 +126,42 @@ def _mutate(t, rng, n_symbols, p_transpose, p_subst):
         t[r, i + 1] = a
     sub = rng.random((c, length)) < p_subst
     t[sub] = rng.integers(0, n_symbols, size=int(sub.sum()))
+
+
+def po_store(n, length, n_entities=16, p_reorder=0.5, p_new=0.3, seed=0x5EED):
+    """`nmz tools visualize` workload: n stored runs of `length` events over `n_entities` entities (each entity
+    `length // n_entities` events).
+
+    A run is either new (probability p_new: fresh per-entity event sequences) or a repeat of an earlier run's
+    per-entity sequences, re-interleaved across entities with probability p_reorder (partial-order equal,
+    not exactly equal) or in the same interleaving (exactly equal). Returns (TraceSet of event symbols,
+    entity ids uint32 per element (dense per trace), number of distinct runs by construction)."""
+    from .historystorage import TraceSet
+    rng = np.random.default_rng(seed)
+    per = length // n_entities
+    length = per * n_entities
+    ent_of = np.repeat(np.arange(n_entities, dtype=np.uint16), per)
+    base_of = np.empty(n, np.int64)
+    orders = np.empty((n, length), np.int64)
+    n_bases = 0
+    first_order = {}
+    for i in range(n):
+        if n_bases == 0 or rng.random() < p_new:
+            base_of[i] = n_bases
+            n_bases += 1
+            orders[i] = rng.permutation(length)
+            first_order[int(base_of[i])] = i
+        else:
+            base_of[i] = rng.integers(n_bases)
+            orders[i] = rng.permutation(length) if rng.random() < p_reorder else orders[first_order[int(base_of[i])]]
+    ev = rng.integers(0, 64, (n_bases, n_entities, per)).astype(np.uint64)
+    slot_ent = ent_of[orders].astype(np.uint16)                 # (n, length) entity of each slot
+    srt = np.argsort(slot_ent, axis=1, kind="stable")           # slots grouped by entity, in slot order (radix)
+    rank = np.empty_like(srt)
+    np.put_along_axis(rank, srt, np.tile(np.arange(length) % per, (n, 1)), axis=1)
+    sym = ev[base_of[:, None], slot_ent, rank] * np.uint64(0x9E3779B97F4A7C15) + \
+        slot_ent.astype(np.uint64) * np.uint64(0xBF58476D1CE4E5B9) + np.uint64(1)
+    ts = TraceSet([])
+    ts.off = np.arange(n + 1, dtype=np.uint64) * np.uint64(length)
+    ts.sym = sym.reshape(-1)
+    return ts, slot_ent.astype(np.uint32).reshape(-1), n_bases
