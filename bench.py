@@ -422,10 +422,19 @@ def bench_visualize(args, torch, D, ctx, L, stream):
         first = d_first.cpu().numpy().view(np.uint32)
         uniq = int((first == np.arange(N)).sum())
         sig_ms = tot.value / max(cnt.value, 1)
+        algo_bytes = ts.sym.nbytes + (ent.nbytes if po else 0) + 16 * N  # symbols (+ entity ids) read, sig written
+        key = "k_trace_sig:" + ("po" if po else "exact")
+        prof = valu_entry(key) or {}
+        achieved = algo_bytes / (sig_ms * 1e-3) / 1e9
         out["po" if po else "exact"] = dict(
             value=N / el, ms=el * 1e3, unique=uniq, sig_kernel_ms=sig_ms,
-            sig_hbm_gbs=ts.sym.nbytes * (1.5 if po else 1.0) / (sig_ms * 1e-3) / 1e9)
+            roofline={"bound": "hbm", "kernel": "k_trace_sig", "achieved": achieved, "peak": PEAK_HBM_GBS,
+                      "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "algorithmic_bytes": algo_bytes,
+                      "traffic": prof.get("hbm_bytes_per_launch"),
+                      "traffic_unit": "bytes/launch (2 x FETCH_SIZE + WRITE_SIZE)",
+                      "ops_per_unit": prof.get("ops_per_unit"), "ops_unit": "VALU lane-instr per trace"})
     out["value"] = out["po"]["value"]
+    out["roofline"] = out["po"]["roofline"]
     out["po"]["unique_matches_construction"] = out["po"]["unique"] == n_bases
     if D.rank == 0 and args.cpu_baseline:
         from oracle import oracle as O

@@ -4,12 +4,12 @@
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-prof}; shift || true
-LEGS=${*:-replayable random ed_clustered ed_survey ed_wide}
+LEGS=${*:-replayable random ed_clustered ed_survey ed_wide visualize}
 cd /tmp && export TMPDIR=/tmp
 for leg in $LEGS; do
   OUT=$R/gpurun_out/$TAG/$leg
   mkdir -p $OUT
-  B="python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline --ed-steps 1 --random-steps 1 --e2e-traces 1 --legs $leg"
+  B="python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline --ed-steps 1 --random-steps 1 --e2e-traces 1 --vis-traces 100000 --legs $leg"
   echo "== $leg"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B > $OUT/trace.log 2>&1
   timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_valu -o run -- $B > $OUT/pmc_valu.log 2>&1

@@ -19,6 +19,10 @@ LEGS = {
     "ed_clustered": [("void nmz::k_ed_bv<32>", "k_ed_bv:clustered", "pair", 100_000 * 99_999 // 2)],
     "ed_survey": [("void nmz::k_ed_bv<32>", "k_ed_bv:survey", "pair", 100_000 * 99_999 // 2)],
     "ed_wide": [("void nmz::k_ed_wide<4>", "k_ed_wide", "pair", 256 * 255 // 2)],
+    # one launch per mode per step (PO first, then exact): the profile's average mixes both modes, so the
+    # per-mode figures come from the two kernel instantiations
+    "visualize": [("void nmz::k_trace_sig<true>", "k_trace_sig:po", "trace", 100_000),
+                  ("void nmz::k_trace_sig<false>", "k_trace_sig:exact", "trace", 100_000)],
 }
 
 
