@@ -17,8 +17,9 @@
 // mode. The event symbol already holds the entity (the event JSON carries it), so
 // for PO mode the multiset determines every per-entity sequence and vice versa.
 // A multiset is hashed by summing a 64-bit mix of each pair mod 2^64 (an additive
-// multiset hash, Clarke et al. 2003) under two independent mixes, plus the element
+// multiset hash, Clarke et al. 2003) under two different mixes, plus the element
 // count: 128 bits per trace, order independent, so lanes can add in any order.
+// The rank's part of each mix comes from a per-context table (65,536 ranks).
 // Equal traces always give equal signatures; distinct ones collide with
 // probability ~2^-128 per pair (the symbols themselves are 64-bit FNV event
 // hashes).
@@ -50,19 +51,35 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t x) {
     return x;
 }
 
-__device__ __forceinline__ uint64_t mix_a(uint64_t s, uint32_t r) {
-    return fmix64(s ^ fmix64((uint64_t)r + 0x9e3779b97f4a7c15ULL));
+// per-rank keys: RANK_KEYS ranks in a table (computed once per context), larger ranks inline
+constexpr uint32_t RANK_KEYS = 65536;
+
+__device__ __forceinline__ uint64_t rank_key_a(uint32_t r) { return fmix64((uint64_t)r + 0x9e3779b97f4a7c15ULL); }
+__device__ __forceinline__ uint64_t rank_key_b(uint32_t r) {
+    return fmix64(((uint64_t)r << 32 | (r ^ 0x5bd1e995u)) + 0x632be59bd9b4e019ULL);
 }
 
-__device__ __forceinline__ uint64_t mix_b(uint64_t s, uint32_t r) {
-    return fmix64((s + 0x632be59bd9b4e019ULL) * 0x94d049bb133111ebULL ^ ((uint64_t)r << 32 | (r ^ 0x5bd1e995u)));
+__global__ void k_rank_keys(ulonglong2 *__restrict__ keys) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < RANK_KEYS) keys[r] = make_ulonglong2(rank_key_a(r), rank_key_b(r));
+}
+
+// the pair (symbol s, rank r) -> two 64-bit summands: t = fmix64(s ^ ka(r)) and a second, different nonlinear
+// function of t and kb(r) (one more 64-bit multiply instead of another fmix64)
+__device__ __forceinline__ void mix2(uint64_t s, uint32_t r, const ulonglong2 *__restrict__ keys, uint64_t &a,
+                                     uint64_t &b) {
+    const ulonglong2 k = r < RANK_KEYS ? keys[r] : make_ulonglong2(rank_key_a(r), rank_key_b(r));
+    const uint64_t t = fmix64(s ^ k.x);
+    a = t;
+    const uint64_t u = (t ^ k.y) * 0x94d049bb133111ebULL;
+    b = u ^ (u >> 29);
 }
 
 template <bool PO>
 __global__ __launch_bounds__(256) void k_trace_sig(const uint64_t *__restrict__ off, const uint64_t *__restrict__ sym,
                                                    const uint32_t *__restrict__ ent, uint32_t N, uint32_t max_ent,
                                                    uint32_t kbits, uint32_t waves_per_block,
-                                                   uint64_t *__restrict__ sig) {
+                                                   const ulonglong2 *__restrict__ keys, uint64_t *__restrict__ sig) {
     extern __shared__ uint32_t cnt_all[];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t t = blockIdx.x * waves_per_block + wv;
@@ -100,8 +117,10 @@ __global__ __launch_bounds__(256) void k_trace_sig(const uint64_t *__restrict__ 
             }
         }
         if (take) {
-            acc1 += mix_a(s, rank);
-            acc2 += mix_b(s, rank);
+            uint64_t a, b;
+            mix2(s, rank, keys, a, b);
+            acc1 += a;
+            acc2 += b;
             counted += 1;
         }
     }
@@ -152,12 +171,21 @@ __global__ void k_sig_first(const uint32_t *__restrict__ idx_sorted, const uint3
     if (p < N) first_equal[idx_sorted[p]] = idx_sorted[start[p]];
 }
 
-static int sig_launch(const uint64_t *d_off, const uint64_t *d_sym, const uint32_t *d_ent, uint32_t N,
+static int sig_launch(nmz_ctx *ctx, const uint64_t *d_off, const uint64_t *d_sym, const uint32_t *d_ent, uint32_t N,
                       uint32_t max_ent, uint64_t *d_sig, hipStream_t st) {
     if (N == 0) return NMZ_OK;
+    DevBuf &kb = ctx->buf[14];  // rank keys, built once per context
+    if (!kb.ptr) {
+        NMZ_TRY(kb.ensure((size_t)RANK_KEYS * sizeof(ulonglong2)));
+        // on the context's stream, waited for once: later launches on any stream see the finished table
+        hipLaunchKernelGGL(k_rank_keys, dim3(RANK_KEYS / 256), dim3(256), 0, ctx->stream, kb.as<ulonglong2>());
+        NMZ_HIP(hipGetLastError());
+        NMZ_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    const ulonglong2 *keys = kb.as<ulonglong2>();
     if (!d_ent) {
         hipLaunchKernelGGL(k_trace_sig<false>, dim3(ceil_div(N, SIG_WAVES)), dim3(64 * SIG_WAVES), 0, st, d_off, d_sym,
-                           nullptr, N, 0u, 0u, SIG_WAVES, d_sig);
+                           nullptr, N, 0u, 0u, SIG_WAVES, keys, d_sig);
     } else {
         NMZ_CHECK(max_ent <= SIG_MAX_ENT, "more than 16384 distinct entities in one trace");
         const uint32_t me = max_ent ? max_ent : 1;
@@ -165,7 +193,7 @@ static int sig_launch(const uint64_t *d_off, const uint64_t *d_sym, const uint32
         uint32_t kbits = 0;
         while ((1u << kbits) < me) ++kbits;
         hipLaunchKernelGGL(k_trace_sig<true>, dim3(ceil_div(N, wpb)), dim3(64 * wpb), (size_t)wpb * me * 4, st, d_off,
-                           d_sym, d_ent, N, me, kbits, wpb, d_sig);
+                           d_sym, d_ent, N, me, kbits, wpb, keys, d_sig);
     }
     NMZ_HIP(hipGetLastError());
     return NMZ_OK;
@@ -270,7 +298,7 @@ int nmz_trace_signatures(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
     NMZ_HIP(hipMemcpyAsync(d_off, off, (n_traces + 1) * 8, hipMemcpyHostToDevice, st));
     if (total) NMZ_HIP(hipMemcpyAsync(d_sym, sym, total * 8, hipMemcpyHostToDevice, st));
     if (total && entity) NMZ_HIP(hipMemcpyAsync(d_ent, entity, total * 4, hipMemcpyHostToDevice, st));
-    NMZ_TRY(sig_launch(d_off, d_sym, entity ? d_ent : nullptr, n_traces, max_ent, d_sig, st));
+    NMZ_TRY(sig_launch(ctx, d_off, d_sym, entity ? d_ent : nullptr, n_traces, max_ent, d_sig, st));
     NMZ_HIP(hipMemcpyAsync(sig, d_sig, 2 * (uint64_t)n_traces * 8, hipMemcpyDeviceToHost, st));
     NMZ_HIP(hipStreamSynchronize(st));
     return NMZ_OK;
@@ -303,7 +331,7 @@ int nmz_unique_traces(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, co
     NMZ_HIP(hipMemcpyAsync(d_off, off, (n_traces + 1) * 8, hipMemcpyHostToDevice, st));
     if (total) NMZ_HIP(hipMemcpyAsync(d_sym, sym, total * 8, hipMemcpyHostToDevice, st));
     if (total && entity) NMZ_HIP(hipMemcpyAsync(d_ent, entity, total * 4, hipMemcpyHostToDevice, st));
-    NMZ_TRY(sig_launch(d_off, d_sym, entity ? d_ent : nullptr, n_traces, max_ent, d_sig, st));
+    NMZ_TRY(sig_launch(ctx, d_off, d_sym, entity ? d_ent : nullptr, n_traces, max_ent, d_sig, st));
     {
         KernelTimer kt(ctx, st, "unique_classes");
         NMZ_TRY(classes_launch(ctx, d_sig, n_traces, d_first, st));
@@ -324,7 +352,7 @@ int nmz_unique_traces_dev(nmz_ctx *ctx, const uint64_t *d_off, const uint64_t *d
     hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
     {
         KernelTimer kt(ctx, st, "trace_sig");
-        NMZ_TRY(sig_launch(d_off, d_sym, d_entity, n_traces, max_entities, d_sig, st));
+        NMZ_TRY(sig_launch(ctx, d_off, d_sym, d_entity, n_traces, max_entities, d_sig, st));
     }
     return classes_launch(ctx, d_sig, n_traces, d_first_equal, st);
 }
