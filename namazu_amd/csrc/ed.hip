@@ -360,6 +360,7 @@ struct nmz_ed_plan {
     std::map<uint64_t, std::vector<uint64_t>> shard_start;  // bv: per (shard, n_shards) row starts (host; kept, so
                                                              // an async copy from it never sees it rewritten)
     uint64_t *d_counters = nullptr;  // bv: work counters of the latest search (nmz_ed_plan_counters)
+    uint32_t rq = 64;                // bv: queries per block row
     uint32_t maxlen = 0;
     std::unordered_map<uint64_t, uint32_t> dict;  // bv: symbol -> dense id (single-query search)
     nmz::DevBuf mem;
@@ -391,7 +392,17 @@ __global__ __launch_bounds__(256) void k_ed_bv_remap(const uint64_t *__restrict_
     }
 }
 
-constexpr uint64_t ED_DEVICE_REMAP_MIN = 1ULL << 20;  // symbols; smaller stores keep the host remap
+constexpr uint64_t ED_DEVICE_REMAP_MIN = 1ULL << 20;
+
+// queries per block row of the bit-parallel search (NMZ_ED_RW overrides the multiple of 64 for A/B runs)
+static uint32_t ed_bv_row_queries() {
+    static const uint32_t rq = [] {
+        const char *e = getenv("NMZ_ED_RW");
+        const int v = e ? atoi(e) : (int)ED_BV_RW;
+        return 64u * (uint32_t)((v >= 1 && v <= 32) ? v : (int)ED_BV_RW);
+    }();
+    return rq;
+}  // symbols; smaller stores keep the host remap
 
 // The bit-parallel plan built on the device: upload the symbols, sort/unique them (dense ids = ranks), write the
 // candidate streams with a binary search per symbol. Returns 1 (not applicable: the alphabet does not fit the
@@ -417,12 +428,14 @@ static int ed_plan_build_bv_device(nmz_ed_plan *p, const uint64_t *off, const ui
     const uint32_t KF = (2 * band + 31) / 32;
     const uint32_t ndw = ((maxlen + 31) / 32 + KF + 2) | 1;
     if (n_uniq >= MAX_FAST_SYMBOLS || (n_uniq + 1) * ndw * 8 > 65536) return 1;
-    const uint32_t n_sym = (uint32_t)n_uniq, G = (N + 63) / 64;
+    const uint32_t rq = ed_bv_row_queries();
+    const uint32_t n_sym = (uint32_t)n_uniq, G = (N + rq - 1) / rq;
     p->bv = true;
     p->fast = true;
     p->ndw = ndw;
     p->lds_dw = (uint32_t)((((uint64_t)(n_sym + 1) * ndw * 8 + 15) / 16) * 4);
     p->G = G;
+    p->rq = rq;
     p->maxlen = maxlen;
     p->n_sym = n_sym;
     const uint32_t zero_row = n_sym * ndw * 8;
@@ -437,7 +450,7 @@ static int ed_plan_build_bv_device(nmz_ed_plan *p, const uint64_t *off, const ui
         const uint32_t v = (uint32_t)atoi(e);
         if (v >= 256 && v % 256 == 0) p->pool = v;
     }
-    for (uint32_t b = 0; b < G; ++b) chunk_start[b + 1] = chunk_start[b] + (N - 64 * b + p->pool - 1) / p->pool;
+    for (uint32_t b = 0; b < G; ++b) chunk_start[b + 1] = chunk_start[b] + (N - rq * b + p->pool - 1) / p->pool;
     p->n_chunks = chunk_start[G];
     p->row_chunks.resize(G);
     for (uint32_t b = 0; b < G; ++b) p->row_chunks[b] = chunk_start[b + 1] - chunk_start[b];
@@ -585,8 +598,10 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         if (rc != NMZ_OK) return cleanup(rc);
         if (hipStreamSynchronize(st)) return cleanup(fail(NMZ_EHIP, "ED plan build failed"));
     } else if (fast && p->bv) {
-        const uint32_t G = (N + 63) / 64;
+        const uint32_t rq = ed_bv_row_queries();
+        const uint32_t G = (N + rq - 1) / rq;
         p->G = G;
+        p->rq = rq;
         p->maxlen = maxlen;
         p->n_sym = n_sym;
         p->dict = std::move(dict);
@@ -607,7 +622,7 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
             if (v >= 256 && v % 256 == 0) p->pool = v;
         }
         for (uint32_t b = 0; b < G; ++b)
-            chunk_start[b + 1] = chunk_start[b] + (N - 64 * b + p->pool - 1) / p->pool;
+            chunk_start[b + 1] = chunk_start[b] + (N - rq * b + p->pool - 1) / p->pool;
         p->n_chunks = chunk_start[G];
         p->row_chunks.resize(G);
         for (uint32_t b = 0; b < G; ++b) p->row_chunks[b] = chunk_start[b + 1] - chunk_start[b];
@@ -737,7 +752,8 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
         A.n_chunks = ss[p->G];
         if (A.n_chunks == 0) return NMZ_OK;
         NMZ_HIP(hipMemcpyAsync(p->d_chunk_start, ss.data(), (p->G + 1) * 8, hipMemcpyHostToDevice, st));
-        uint64_t blocks = A.n_chunks * 32;
+        A.rq = p->rq;
+        uint64_t blocks = A.n_chunks * (p->rq / 2);
         blocks = (blocks + 7) / 8 * 8;
         NMZ_CHECK(blocks < (1ULL << 31), "too many traces for one launch");
         NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_BV_NCOUNTERS * 8, st));

@@ -280,7 +280,8 @@ __global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv(EdBvArgs A) {
     uint32_t &pool_next = peq[A.lds_dw];
     const uint32_t nblk = gridDim.x, per_xcd = nblk / 8;
     const uint32_t lb = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
-    const uint64_t lchunk = lb / 32;
+    const uint32_t wpc = A.rq / 2;  // workgroups per chunk
+    const uint64_t lchunk = lb / wpc;
     if (lchunk >= A.n_chunks) return;
     // this shard's lchunk-th chunk: row b (binary search of the shard's per-row starts), then the row's
     // chunks dealt round-robin starting at rank (b mod n_shards), so every rank gets every n_shards-th chunk
@@ -293,11 +294,11 @@ __global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv(EdBvArgs A) {
     const uint32_t b = lo;
     const uint32_t rot = (A.shard + A.n_shards - b % A.n_shards) % A.n_shards;
     const uint32_t cr = rot + A.n_shards * (uint32_t)(lchunk - A.chunk_start[b]);
-    const uint32_t q1 = 64 * b + 2 * (lb % 32), q2 = q1 + 1;
+    const uint32_t q1 = A.rq * b + 2 * (lb % wpc), q2 = q1 + 1;
     if (q1 >= A.N) return;  // whole workgroup
     const bool has2 = q2 < A.N;
     const uint32_t n1 = A.len[q1], n2 = has2 ? A.len[q2] : 0;
-    const uint32_t c0 = 64 * b + A.pool * cr;
+    const uint32_t c0 = A.rq * b + A.pool * cr;
     const uint32_t c1 = min(c0 + A.pool, A.N);
     const uint32_t pool_lo = max(c0, q1 + 1);
     const uint32_t pool_n = c1 > pool_lo ? c1 - pool_lo : 0;

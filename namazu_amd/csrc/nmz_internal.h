@@ -38,7 +38,12 @@ struct EdBvArgs {
     uint64_t *counters;           // [ED_BV_NCOUNTERS] work counters (nmz_ed_plan_counters), or nullptr
     uint64_t n_chunks;            // chunks of this shard
     uint32_t N, G, k, lds_dw, shard, n_shards, pool;
+    uint32_t rq;                  // queries per block row (64 x ED_BV_ROW_WAVES64); rq / 2 workgroups share a chunk
 };
+// Block rows of the bit-parallel search: rq = 64 * ED_BV_RW queries; the rq / 2 workgroups of one chunk (one query
+// pair each, the same pool of candidates) are consecutive in the XCD-remapped order, so they run together on one
+// XCD and read the pool's candidate streams from its L2. 5 x 32 = 160 workgroups = one XCD's 32 CUs x 5.
+constexpr uint32_t ED_BV_RW = 5;
 // k_ed_bv work counters, summed over the launch:
 //   0 pairs that ran the DP, 1 pairs with a result <= w (in band), 2 lane-candidate 32-column blocks executed,
 //   3 candidates that ran the DP, 4 live query-blocks (blocks x queries of that lane still running)
