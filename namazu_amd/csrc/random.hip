@@ -449,15 +449,21 @@ static int make_kparams(const nmz_random_params *p, RandomKParams &kp) {
     return NMZ_OK;
 }
 
-constexpr uint32_t RANDOM_EC = 512;  // events per work item (1,024: 26.2 ms, 512: 26.0, 2,048: 26.5 per 2^20 x 10^4)
+// Events per work item. 2^20 seeds x 10^4 events: 512 -> 26.0 ms, 1,024 -> 26.2, 2,048 -> 26.5 (the last round of
+// work items is shorter with small items). 10^7 seeds: 512 / 1,024 / 2,048 all 245-246 ms, but each chunk adds a
+// 32-byte partial row per seed (written by the sweep, read by k_random_merge): 2,048 keeps that to 5 rows per seed
+// (8.1 -> ~2 GB per launch). NMZ_RANDOM_EC overrides.
+constexpr uint32_t RANDOM_EC = 512;
+constexpr uint32_t RANDOM_EC_LARGE = 2048;        // from RANDOM_EC_LARGE_SEEDS seeds per launch
+constexpr uint64_t RANDOM_EC_LARGE_SEEDS = 1ULL << 22;
 
-static uint32_t random_ec() {
-    static const uint32_t v = [] {
+static uint32_t random_ec(uint64_t S) {
+    static const uint32_t env = [] {
         const char *e = getenv("NMZ_RANDOM_EC");
-        const uint32_t x = e ? (uint32_t)atoi(e) : RANDOM_EC;
-        return x >= 64 ? x : RANDOM_EC;
+        const uint32_t x = e ? (uint32_t)atoi(e) : 0u;
+        return x >= 64 ? x : 0u;
     }();
-    return v;
+    return env ? env : (S >= RANDOM_EC_LARGE_SEEDS ? RANDOM_EC_LARGE : RANDOM_EC);
 }
 
 static size_t random_seed_scratch_bytes(uint64_t S) {
@@ -537,7 +543,7 @@ static int random_run(nmz_random_plan *p, hipStream_t st, uint64_t seed0, uint64
                        b.count, prefix_per_thread());
     const uint64_t max_units = S / 64 + 256;
     NMZ_TRY(bucket_seeds_counted(st, d_h0, S, 64, b, d_counter));
-    const uint32_t ec = random_ec();
+    const uint32_t ec = random_ec(S);
     const uint32_t n_chunks = std::max<uint32_t>(1, (E + ec - 1) / ec);
     const uint64_t stride = (p->max_seeds / 64 + 257) * 64;
     nmz_sched_stats *part = nullptr;
