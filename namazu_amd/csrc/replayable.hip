@@ -72,6 +72,16 @@ static int replay_key_mode() {
     return k;
 }
 
+// persistent workgroups (4 waves each) per CU: 8 = 8 waves/SIMD (NMZ_REPLAY_WG for A/B runs)
+static uint32_t replay_wg_per_cu() {
+    static const uint32_t w = [] {
+        const char *e = getenv("NMZ_REPLAY_WG");
+        const int v = e ? atoi(e) : 8;
+        return (uint32_t)((v >= 1 && v <= 16) ? v : 8);
+    }();
+    return w;
+}
+
 // seeds per lane (default 2, the fastest measured; NMZ_REPLAY_U=2|4|8 for tuning)
 static int replay_u() {
     static int u = [] {
@@ -723,7 +733,8 @@ static int replayable_stats(nmz_replayable_plan *p, hipStream_t st, const uint32
         uint32_t fold_mask = 0;
         while (fold_mask < 15 && ((uint64_t)(4 * (fold_mask + 1) * 2 + 3)) * (p->mod.m - 1) < (1ull << 32))
             fold_mask = fold_mask * 2 + 1;
-        const unsigned grid = (unsigned)std::min<uint64_t>(p->ctx->n_cu * 8ull, ceil_div(max_units * n_chunks, 4));
+        const unsigned grid = (unsigned)std::min<uint64_t>(p->ctx->n_cu * (uint64_t)replay_wg_per_cu(),
+                                                           ceil_div(max_units * n_chunks, 4));
         {
             KernelTimer kt(p->ctx, st, "replayable_sweep");
 #define NMZ_K1(UU)                                                                                                   \

@@ -193,3 +193,38 @@ def test_event_hashes_on_the_gpu_match_the_host_rule(ctx):
     events = [packet_event(i, 5) for i in range(100)]
     eh, _ = p.event_inputs(events)
     assert eh.tolist() == [e.evhash() for e in events]
+
+
+@pytest.mark.gpu
+def test_online_decide_edge_cases(ctx):
+    """nmz_replayable_decide: maxInterval 0 -> 0 (replayablepolicy.go:101-104), uint64 of a negative duration,
+    empty seed and hints, no events; nmz_random_decide: unknown class bits and min > max are errors, no events is a
+    no-op."""
+    import ctypes
+    from namazu_amd import _lib
+    from namazu_amd.explorepolicy import to_csr
+    from oracle import oracle as O
+    L = _lib.load()
+    hints = ["", "a", "hint-entity-0-1", "-9223372036854775808"]
+    ho, hb = to_csr(hints)
+    for seed in [b"", b"foobar"]:
+        sb = np.frombuffer(seed, np.uint8).copy() if seed else np.zeros(1, np.uint8)
+        for m in [0, 1, 100_000_000, -5_000_000, -1, 2**63 - 1]:
+            out = np.zeros(len(hints), np.int64)
+            _lib.check(L.nmz_replayable_decide(ctx.handle, _lib.ptr(sb), len(seed), _lib.ptr(ho), _lib.ptr(hb),
+                                               len(hints), m, _lib.ptr(out)))
+            assert out.tolist() == [O.replayable_interval(seed.decode(), h, m) for h in hints]
+    assert L.nmz_replayable_decide(ctx.handle, None, 0, None, None, 0, 10, None) == _lib.NMZ_OK
+    p = _lib.resolve_random_params(1, 5, 0.5)
+    eh = np.array([1, 2], np.uint64)
+    d = np.zeros(2, np.int64)
+    f = np.zeros(2, np.uint8)
+    bad = np.array([0, 4], np.uint8)
+    assert L.nmz_random_decide(ctx.handle, 1, _lib.ptr(eh), _lib.ptr(bad), 2, ctypes.byref(p), _lib.ptr(d),
+                               _lib.ptr(f)) == _lib.NMZ_EINVAL
+    q = _lib.RandomParams()
+    q.min_ns[0], q.max_ns[0], q.min_ns[1], q.max_ns[1] = 10, 5, 0, 0
+    ok = np.zeros(2, np.uint8)
+    assert L.nmz_random_decide(ctx.handle, 1, _lib.ptr(eh), _lib.ptr(ok), 2, ctypes.byref(q), _lib.ptr(d),
+                               _lib.ptr(f)) == _lib.NMZ_EINVAL
+    assert L.nmz_random_decide(ctx.handle, 1, None, None, 0, ctypes.byref(p), None, None) == _lib.NMZ_OK

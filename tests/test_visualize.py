@@ -240,3 +240,36 @@ def test_unique_first_equal_and_signatures(ctx):
     assert _lib.load().nmz_unique_traces(ctx.handle, None, None, None, 0, None) == 0
     assert _lib.load().nmz_unique_traces(None, None, None, None, 1, None) == _lib.NMZ_EINVAL
     del ctypes
+
+
+@pytest.mark.gpu
+def test_unique_traces_dev_entity_bound_and_errors(ctx):
+    """nmz_unique_traces_dev with the caller's entity bound: the same classes as the host entry point; more than
+    16,384 entities is an error, not an LDS overrun."""
+    import ctypes
+    import torch
+    from namazu_amd import _lib
+    rng = np.random.default_rng(3)
+    raw = _random_po_traces(rng, 120, 7, 0, 150, 60, 0.05, dup=0.5)
+    traces = [_to_single(t) for t in raw]
+    ts, ent = hs.po_inputs(traces)
+    fe = hs.first_equal(traces, po_reduction=True, ctx=ctx)
+    d_off = torch.from_numpy(ts.off.view(np.int64)).cuda()
+    d_sym = torch.from_numpy(ts.sym.view(np.int64)).cuda()
+    d_ent = torch.from_numpy(ent.view(np.int32)).cuda()
+    d_sig = torch.empty(2 * len(ts), dtype=torch.int64, device="cuda")
+    d_fe = torch.empty(len(ts), dtype=torch.int32, device="cuda")
+    L = _lib.load()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    _lib.check(L.nmz_unique_traces_dev(ctx.handle, P(d_off), P(d_sym), P(d_ent), len(ts), 7, P(d_sig), P(d_fe), st))
+    torch.cuda.synchronize()
+    assert d_fe.cpu().numpy().view(np.uint32).tolist() == fe.tolist()
+    assert L.nmz_unique_traces_dev(ctx.handle, P(d_off), P(d_sym), P(d_ent), len(ts), 20000, P(d_sig), P(d_fe),
+                                   st) == _lib.NMZ_EINVAL
+    big = np.arange(20000, dtype=np.uint32)
+    off = np.array([0, 20000], np.uint64)
+    sym = np.arange(20000, dtype=np.uint64)
+    out = np.zeros(1, np.uint32)
+    assert L.nmz_unique_traces(ctx.handle, _lib.ptr(off), _lib.ptr(sym), _lib.ptr(big), 1, _lib.ptr(out)) == \
+        _lib.NMZ_EINVAL
