@@ -556,6 +556,7 @@ def bench_ed_secondary(args, torch, D, ctx, L, stream, spec):
             D.pg.all_gather_into_tensor(d_parts, d_knn)
             _lib.check(L.nmz_knn_merge_dev(ctx.handle, ctypes.c_void_p(d_parts.data_ptr()), D.world, N, k,
                                            ctypes.c_void_p(d_out.data_ptr()), stream))
+            _lib.check(L.nmz_ed_knn_fill_dev(plan, k, ctypes.c_void_p(d_out.data_ptr()), stream))
 
     step()
     torch.cuda.synchronize()
@@ -619,13 +620,17 @@ def bench_ed_secondary(args, torch, D, ctx, L, stream, spec):
         out["single_query"] = single
     if counters[3]:  # k_ed_bv work counters of the last step (this rank's shard)
         c = [int(x) for x in counters]
+        shard_pairs = (pairs + D.world - 1) // D.world
         out["search"] = dict(
-            dp_pairs=c[0], in_band_pairs=c[1], in_band_frac_of_shard_pairs=c[1] / max(c[0], 1),
+            shard_pairs=shard_pairs, dp_pairs=c[0], qgram_settled_pairs=c[5],
+            length_band_settled_pairs=shard_pairs - c[0] - c[5], in_band_pairs=c[1],
+            in_band_frac_of_shard_pairs=c[1] / shard_pairs, dp_frac_of_shard_pairs=c[0] / shard_pairs,
             mean_cutoff_column=32 * c[2] / c[3], full_columns=ED_LEN,
             executed_cells_per_s=c[2] * 32 * 2 * (2 * ED_BAND + 1) * D.world / (el / steps),
             live_cells_per_s=c[4] * 32 * (2 * ED_BAND + 1) * D.world / (el / steps),
             note="cells = band cells (2w+1 per column); executed = every candidate x 32-column block a lane stepped "
-                 "(2 query columns each), live = the query columns still running in those blocks")
+                 "(2 query columns each), live = the query columns still running in those blocks; q-gram settled = "
+                 "pairs whose bigram profiles are > 4w apart, so ED > w is proven without a DP (result w + 1, exact)")
     keys = d_out.cpu().numpy().view(np.uint64).reshape(N, k)
     if D.rank == 0 and args.cpu_baseline and D.world == 1:
         from oracle import oracle as O

@@ -229,14 +229,19 @@ int nmz_ed_plan_create(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, u
 int nmz_ed_plan_destroy(nmz_ed_plan *plan);
 int nmz_ed_plan_is_fast(const nmz_ed_plan *plan);
 int nmz_ed_allpairs_knn_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys, void *stream);
-/* Multi-GPU: shard `shard` of `n_shards` processes every n_shards-th group of
- * 32 waves (one candidate group each, equal cells per group for equal-length
- * traces); its keys are partial lists. nmz_knn_merge_dev merges n_parts
- * partial lists ([n_parts][n_traces][k], e.g. after an RCCL all_gather). */
+/* Multi-GPU: shard `shard` of `n_shards` processes every n_shards-th work chunk;
+ * its keys are partial lists. nmz_knn_merge_dev merges n_parts partial lists
+ * ([n_parts][n_traces][k], e.g. after an RCCL all_gather), and nmz_ed_knn_fill_dev
+ * then completes the merged lists: on a bit-parallel plan (nmz_ed_plan_is_fast == 2) a
+ * shard lists only its pairs within the band, and every other pair's result is band + 1,
+ * so the merged lists take (band + 1, id) for the smallest ids not listed (not the trace
+ * itself), in increasing id, up to k. On other plans the fill leaves complete lists
+ * unchanged. (nmz_ed_allpairs_knn[_dev] fill by themselves.) */
 int nmz_ed_allpairs_knn_shard_dev(nmz_ed_plan *plan, uint32_t k, uint32_t shard, uint32_t n_shards,
                                   uint64_t *d_knn_keys, void *stream);
 int nmz_knn_merge_dev(nmz_ctx *ctx, const uint64_t *d_parts, uint32_t n_parts, uint32_t n_traces,
                       uint32_t k, uint64_t *d_out, void *stream);
+int nmz_ed_knn_fill_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys, void *stream);
 /* Single queries against a resident store (HistoryStorage similarity search; the reference's own
  * search re-decodes every stored trace per query, naive.go:235-252 "FIXME: quite ineffective"):
  * the plan's stored traces stay on the device; each of n_queries query traces (CSR q_off/q_sym,
@@ -250,10 +255,12 @@ int nmz_ed_plan_query_knn(nmz_ed_plan *plan, const uint64_t *q_off, const uint64
  * out[NMZ_ED_NCOUNTERS]: the bit-parallel band kernel (nmz_ed_plan_is_fast == 2) fills
  *   [0] pairs that ran the DP, [1] pairs whose result is <= band (in band),
  *   [2] candidate x 32-column blocks executed (each block steps 2 query columns per candidate),
- *   [3] candidates that ran the DP, [4] live query-blocks (blocks x queries still running);
+ *   [3] candidates that ran the DP, [4] live query-blocks (blocks x queries still running),
+ *   [5] pairs inside the length band whose result the q-gram lower bound settled at band + 1
+ *       without a DP;
  * other kernels keep no counters and leave zeros. Diagnostics for the bench, not part of the
  * reference interface. */
-#define NMZ_ED_NCOUNTERS 5
+#define NMZ_ED_NCOUNTERS 6
 int nmz_ed_plan_counters(nmz_ed_plan *plan, uint64_t *out, void *stream);
 
 /* ---- trace equality classes (nmz tools visualize) ------------------------

@@ -23,7 +23,7 @@ NMZ_EV_PRIORITIZED = 0x01
 NMZ_EV_FAULTABLE = 0x02
 NMZ_STAT_RNG_OVERFLOW = 0x01
 NMZ_NONE = 0xFFFFFFFF
-NMZ_ED_NCOUNTERS = 5
+NMZ_ED_NCOUNTERS = 6
 
 SCHED_STATS_DTYPE = np.dtype([
     ("sum_delay_ns", "<u8"), ("max_delay_ns", "<i8"), ("argmax_event", "<u4"),
@@ -84,6 +84,7 @@ SIGNATURES = {
     "nmz_ed_allpairs_knn_dev": (_int, [_P, _u32, _P, _P]),
     "nmz_ed_allpairs_knn_shard_dev": (_int, [_P, _u32, _u32, _u32, _P, _P]),
     "nmz_knn_merge_dev": (_int, [_P, _P, _u32, _u32, _u32, _P, _P]),
+    "nmz_ed_knn_fill_dev": (_int, [_P, _u32, _P, _P]),
     "nmz_ed_plan_counters": (_int, [_P, _P, _P]),
     "nmz_ed_plan_query_knn": (_int, [_P, _P, _P, _u32, _u32, _P, _P]),
     "nmz_trace_signatures": (_int, [_P, _P, _P, _P, _u32, _P]),

@@ -29,6 +29,8 @@
 
 #include <map>
 
+#include <hipcub/hipcub.hpp>
+
 #include "nmz_common.h"
 #include "nmz_internal.h"
 
@@ -309,6 +311,31 @@ __global__ void k_knn_final(const uint64_t *__restrict__ knn, uint64_t n, uint32
     ds[i] = key == UINT64_MAX ? NMZ_NONE : (uint32_t)(key >> 32);
 }
 
+// Complete k-NN lists whose listed keys are the results within the band (dist < fill_d): every pair not listed has
+// the result fill_d = band + 1, so list i takes (fill_d, j) for the smallest ids j < n_cand not listed (j != i when
+// self_exclude), in increasing j, until it holds k keys (UINT64_MAX where fewer candidates exist). Keys at or
+// above fill_d already in the list (kernels that list every pair) are recomputed to the same values.
+__global__ void k_knn_fill(uint64_t *knn, uint32_t n_lists, uint32_t k, uint32_t n_cand, uint32_t fill_d,
+                           int self_exclude) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_lists) return;
+    uint64_t *L = knn + (uint64_t)i * k;
+    uint32_t c = 0;
+    while (c < k && L[c] != UINT64_MAX && (uint32_t)(L[c] >> 32) < fill_d) ++c;
+    uint32_t j = 0;
+    for (uint32_t s = c; s < k; ++s) {
+        for (;; ++j) {
+            if (j >= n_cand) break;
+            if (self_exclude && j == i) continue;
+            bool listed = false;
+            for (uint32_t t = 0; t < c; ++t) listed |= (uint32_t)L[t] == j;
+            if (!listed) break;
+        }
+        L[s] = j < n_cand ? (((uint64_t)fill_d << 32) | j) : UINT64_MAX;
+        ++j;
+    }
+}
+
 // all-pairs via the generic kernel (fallback): pair list = upper triangle
 __global__ void k_pairs_upper(uint32_t N, uint64_t start, uint64_t count, uint32_t *pairs) {
     uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -360,10 +387,14 @@ struct nmz_ed_plan {
     std::map<uint64_t, std::vector<uint64_t>> shard_start;  // bv: per (shard, n_shards) row starts (host; kept, so
                                                              // an async copy from it never sees it rewritten)
     uint64_t *d_counters = nullptr;  // bv: work counters of the latest search (nmz_ed_plan_counters)
+    uint32_t *d_prof = nullptr;      // bv: [N][ED_QG_DW] q-gram profiles (ed_qgram_profiles)
     uint32_t rq = 64;                // bv: queries per block row
     uint32_t maxlen = 0;
     std::unordered_map<uint64_t, uint32_t> dict;  // bv: symbol -> dense id (single-query search)
     nmz::DevBuf mem;
+    // bv, two-phase search: per-(shard, n_shards) tile starts (host, kept), scratch and the entry lists
+    std::map<uint64_t, std::vector<uint64_t>> tile_start;
+    nmz::DevBuf tp_mem, tp_ent;
     uint16_t *d_qsym = nullptr, *d_csym = nullptr;
     uint64_t *d_qoff = nullptr, *d_coff = nullptr;
     uint32_t *d_gmax = nullptr, *d_len = nullptr;
@@ -393,6 +424,19 @@ __global__ __launch_bounds__(256) void k_ed_bv_remap(const uint64_t *__restrict_
 }
 
 constexpr uint64_t ED_DEVICE_REMAP_MIN = 1ULL << 20;
+
+// the q-gram lower-bound filter of the bit-parallel kernels (ed_bv.hip); NMZ_ED_QGRAM=0 turns it off for A/B runs
+// the two-phase search (filter tiles, then DP work items) when the q-gram filter is on; NMZ_ED_TWO_PHASE=0 keeps
+// the single-kernel search with its in-workgroup pre-filter (A/B runs)
+static bool ed_two_phase_enabled() {
+    const char *e = getenv("NMZ_ED_TWO_PHASE");
+    return !(e && atoi(e) == 0);
+}
+
+static bool ed_qgram_enabled() {
+    const char *e = getenv("NMZ_ED_QGRAM");
+    return !(e && atoi(e) == 0);
+}
 
 // queries per block row of the bit-parallel search (NMZ_ED_RW overrides the multiple of 64 for A/B runs)
 static uint32_t ed_bv_row_queries() {
@@ -448,7 +492,7 @@ static int ed_plan_build_bv_device(nmz_ed_plan *p, const uint64_t *off, const ui
     p->pool = N >= 24576 ? 4 * ED_BV_POOL : (N >= 12288 ? 2 * ED_BV_POOL : ED_BV_POOL);
     if (const char *e = getenv("NMZ_ED_POOL")) {
         const uint32_t v = (uint32_t)atoi(e);
-        if (v >= 256 && v % 256 == 0) p->pool = v;
+        if (v >= 256 && v % 256 == 0 && v <= 16384) p->pool = v;
     }
     for (uint32_t b = 0; b < G; ++b) chunk_start[b + 1] = chunk_start[b] + (N - rq * b + p->pool - 1) / p->pool;
     p->n_chunks = chunk_start[G];
@@ -456,9 +500,11 @@ static int ed_plan_build_bv_device(nmz_ed_plan *p, const uint64_t *off, const ui
     for (uint32_t b = 0; b < G; ++b) p->row_chunks[b] = chunk_start[b + 1] - chunk_start[b];
     const uint64_t bs_n = soff[N] + 64;
     NMZ_TRY(p->mem.ensure(Carve::bytes_for(bs_n, 2) + Carve::bytes_for(N + 1, 8) * 2 + Carve::bytes_for(G + 1, 8) +
-                          Carve::bytes_for(N + 1, 4) + Carve::bytes_for(ED_BV_NCOUNTERS, 8)));
+                          Carve::bytes_for(N + 1, 4) + Carve::bytes_for(ED_BV_NCOUNTERS, 8) +
+                          Carve::bytes_for((uint64_t)N * ED_QG_DW, 4)));
     Carve cv(p->mem.ptr);
     p->d_counters = cv.take<uint64_t>(ED_BV_NCOUNTERS);
+    p->d_prof = cv.take<uint32_t>((uint64_t)N * ED_QG_DW);
     p->d_bsym = cv.take<uint16_t>(bs_n);
     p->d_soff = cv.take<uint64_t>(N + 1);
     p->d_qoff = cv.take<uint64_t>(N + 1);
@@ -473,6 +519,7 @@ static int ed_plan_build_bv_device(nmz_ed_plan *p, const uint64_t *off, const ui
     hipLaunchKernelGGL(k_ed_bv_remap, dim3(N), dim3(256), 0, st, d_off, d_sym, d_uniq, n_sym, p->d_soff, ndw * 8,
                        p->d_bsym);
     NMZ_HIP(hipGetLastError());
+    NMZ_TRY(ed_qgram_profiles(p->d_bsym, p->d_soff, p->d_len, N, p->d_prof, st));
     // the dictionary for single queries (nmz_ed_plan_query_knn): symbol -> rank
     std::vector<uint64_t> uniq(n_sym);
     NMZ_HIP(hipMemcpyAsync(uniq.data(), d_uniq, (uint64_t)n_sym * 8, hipMemcpyDeviceToHost, st));
@@ -619,7 +666,7 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         p->pool = N >= 24576 ? 4 * ED_BV_POOL : (N >= 12288 ? 2 * ED_BV_POOL : ED_BV_POOL);
         if (const char *e = getenv("NMZ_ED_POOL")) {  // tuning override (multiple of 256)
             const uint32_t v = (uint32_t)atoi(e);
-            if (v >= 256 && v % 256 == 0) p->pool = v;
+            if (v >= 256 && v % 256 == 0 && v <= 16384) p->pool = v;
         }
         for (uint32_t b = 0; b < G; ++b)
             chunk_start[b + 1] = chunk_start[b] + (N - rq * b + p->pool - 1) / p->pool;
@@ -631,11 +678,12 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
             for (uint32_t t = 0; t < len[i]; ++t) bs[soff[i] + t] = (uint16_t)(ids[off[i] + t] * ndw * 8);
         size_t need = Carve::bytes_for(bs.size(), 2) + Carve::bytes_for(N + 1, 8) * 2 +
                       Carve::bytes_for(G + 1, 8) + Carve::bytes_for(N + 1, 4) +
-                      Carve::bytes_for(ED_BV_NCOUNTERS, 8);
+                      Carve::bytes_for(ED_BV_NCOUNTERS, 8) + Carve::bytes_for((uint64_t)N * ED_QG_DW, 4);
         int rc = p->mem.ensure(need);
         if (rc != NMZ_OK) return cleanup(rc);
         Carve cv(p->mem.ptr);
         p->d_counters = cv.take<uint64_t>(ED_BV_NCOUNTERS);
+        p->d_prof = cv.take<uint32_t>((uint64_t)N * ED_QG_DW);
         p->d_bsym = cv.take<uint16_t>(bs.size());
         p->d_soff = cv.take<uint64_t>(N + 1);
         p->d_qoff = cv.take<uint64_t>(N + 1);
@@ -646,8 +694,11 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
             hipMemcpyAsync(p->d_qoff, off, (N + 1) * 8, hipMemcpyHostToDevice, st) ||
             hipMemcpyAsync(p->d_chunk_start, chunk_start.data(), (G + 1) * 8, hipMemcpyHostToDevice, st) ||
             hipMemcpyAsync(p->d_len, len.data(), (N + 1) * 4, hipMemcpyHostToDevice, st) ||
-            hipMemsetAsync(p->d_counters, 0, ED_BV_NCOUNTERS * 8, st) || hipStreamSynchronize(st))
+            hipMemsetAsync(p->d_counters, 0, ED_BV_NCOUNTERS * 8, st))
             return cleanup(fail(NMZ_EHIP, "ED plan upload failed"));
+        rc = ed_qgram_profiles(p->d_bsym, p->d_soff, p->d_len, N, p->d_prof, st);
+        if (rc != NMZ_OK) return cleanup(rc);
+        if (hipStreamSynchronize(st)) return cleanup(fail(NMZ_EHIP, "ED plan build failed"));
     } else if (fast) {
         const uint32_t G = (N + 63) / 64;
         p->G = G;
@@ -699,6 +750,82 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
     return NMZ_OK;
 }
 
+// work items per query pair: ceil(entries / ED_BV_ITEM) (items[n_pairs] = 0 closes the scan)
+__global__ void k_bv_items(const uint32_t *__restrict__ cnt, uint32_t n, uint32_t *__restrict__ items) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= n) items[i] = i < n ? (cnt[i] + ED_BV_ITEM - 1) / ED_BV_ITEM : 0u;
+}
+
+// The two-phase bit-parallel search of one shard (nmz_internal.h EdQgArgs): filter count pass, scans (entry and
+// work-item offsets; the two totals come back to the host to size the entry lists and the DP grid), write pass,
+// DP over the work items. Returns 1 when the entry lists would exceed ED_TP_MAX_ENTRIES (caller falls back to
+// the single-kernel search).
+constexpr uint64_t ED_TP_MAX_ENTRIES = 1ULL << 30;  // 4 GiB of entries
+static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A) {
+    const uint32_t N = p->n, n_pairs = (N + 1) / 2, QB = (N + 63) / 64, NCB = (N + 255) / 256;
+    const uint32_t shard = A.shard, n_shards = A.n_shards;
+    if (N >= (1u << 30)) return 1;  // entries carry j in 30 bits
+    std::vector<uint64_t> &ts = p->tile_start[((uint64_t)shard << 32) | n_shards];
+    if (ts.empty()) {
+        ts.assign(QB + 1, 0);
+        for (uint32_t qb = 0; qb < QB; ++qb) {
+            const uint64_t nt = NCB - qb / 4, rot = (shard + n_shards - qb % n_shards) % n_shards;
+            ts[qb + 1] = ts[qb] + (rot < nt ? (nt - rot + n_shards - 1) / n_shards : 0);
+        }
+    }
+    size_t scan_bytes = 0;
+    NMZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                             (int)n_pairs + 1, st));
+    NMZ_TRY(p->tp_mem.ensure(Carve::bytes_for(QB + 1, 8) + 5 * Carve::bytes_for(n_pairs + 1, 4) +
+                             Carve::bytes_for(scan_bytes, 1) + Carve::bytes_for(4, 4)));
+    Carve cv(p->tp_mem.ptr);
+    uint64_t *d_ts = cv.take<uint64_t>(QB + 1);
+    uint32_t *d_cnt = cv.take<uint32_t>(n_pairs + 1), *d_poff = cv.take<uint32_t>(n_pairs + 1);
+    uint32_t *d_items = cv.take<uint32_t>(n_pairs + 1), *d_ioff = cv.take<uint32_t>(n_pairs + 1);
+    uint32_t *d_cur = cv.take<uint32_t>(n_pairs + 1);
+    void *d_scan = cv.take<char>(scan_bytes);
+    EdQgArgs Q;
+    Q.prof = A.prof;
+    Q.len = A.len;
+    Q.knn = A.knn;
+    Q.counters = A.counters;
+    Q.tile_start = d_ts;
+    Q.cnt = d_cnt;
+    Q.cur = d_cur;
+    Q.ent = nullptr;
+    Q.n_tiles = ts[QB];
+    Q.N = N;
+    Q.k = A.k;
+    Q.QB = QB;
+    Q.NCB = NCB;
+    Q.shard = shard;
+    Q.n_shards = n_shards;
+    NMZ_HIP(hipMemcpyAsync(d_ts, ts.data(), (QB + 1) * 8, hipMemcpyHostToDevice, st));
+    NMZ_HIP(hipMemsetAsync(d_cnt, 0, (n_pairs + 1) * 4, st));
+    {
+        KernelTimer kt(p->ctx, st, "ed_qg_filter");
+        NMZ_TRY(ed_qg_filter_launch(Q, p->band, true, st));
+    }
+    NMZ_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_cnt, d_poff, (int)n_pairs + 1, st));
+    hipLaunchKernelGGL(k_bv_items, dim3(ceil_div(n_pairs + 1, 256)), dim3(256), 0, st, d_cnt, n_pairs, d_items);
+    NMZ_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_items, d_ioff, (int)n_pairs + 1, st));
+    uint32_t tot[2] = {0, 0};
+    NMZ_HIP(hipMemcpyAsync(&tot[0], d_poff + n_pairs, 4, hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipMemcpyAsync(&tot[1], d_ioff + n_pairs, 4, hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipStreamSynchronize(st));
+    const uint64_t n_ent = tot[0], n_items = tot[1];
+    if (n_ent > ED_TP_MAX_ENTRIES) return 1;
+    NMZ_TRY(p->tp_ent.ensure(Carve::bytes_for(n_ent + 1, 4)));
+    Q.ent = p->tp_ent.as<uint32_t>();
+    NMZ_HIP(hipMemcpyAsync(d_cur, d_poff, (uint64_t)n_pairs * 4, hipMemcpyDeviceToDevice, st));
+    {
+        KernelTimer kt(p->ctx, st, "ed_qg_filter");
+        NMZ_TRY(ed_qg_filter_launch(Q, p->band, false, st));
+    }
+    KernelTimer kt(p->ctx, st, "ed_bv_dp");
+    return ed_bv_dp_launch(A, d_ioff, d_poff, Q.ent, n_pairs, (uint32_t)n_items, p->band, st);
+}
+
 static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_knn, uint32_t shard = 0,
                       uint32_t n_shards = 1) {
     const uint32_t N = p->n;
@@ -733,6 +860,7 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
         A.chunk_start = p->d_chunk_start;
         A.knn = d_knn;
         A.counters = p->d_counters;
+        A.prof = ed_qgram_enabled() ? (const uint4 *)p->d_prof : nullptr;
         A.N = N;
         A.G = p->G;
         A.k = k;
@@ -740,25 +868,42 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
         A.pool = p->pool;
         A.shard = shard;
         A.n_shards = n_shards;
-        // this shard's chunks per row: cr = ((shard - b) mod n_shards) + n_shards * t
-        std::vector<uint64_t> &ss = p->shard_start[((uint64_t)shard << 32) | n_shards];
-        if (ss.empty()) {
-            ss.assign(p->G + 1, 0);
-            for (uint32_t b = 0; b < p->G; ++b) {
-                const uint64_t nch = p->row_chunks[b], rot = (shard + n_shards - b % n_shards) % n_shards;
-                ss[b + 1] = ss[b] + (rot < nch ? (nch - rot + n_shards - 1) / n_shards : 0);
+        NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_BV_NCOUNTERS * 8, st));
+        int rc = 1;
+        if (A.prof && ed_two_phase_enabled()) {  // filter tiles + DP work items (the search's "ed_bv" time)
+            KernelTimer kt(p->ctx, st, "ed_bv");
+            rc = ed_bv_two_phase(p, st, A);
+            if (rc < 0) return rc;
+        }
+        if (rc == 1) {  // the single-kernel search (no q-gram filter, or entry lists beyond ED_TP_MAX_ENTRIES)
+            // this shard's chunks per row: cr = ((shard - b) mod n_shards) + n_shards * t
+            std::vector<uint64_t> &ss = p->shard_start[((uint64_t)shard << 32) | n_shards];
+            if (ss.empty()) {
+                ss.assign(p->G + 1, 0);
+                for (uint32_t b = 0; b < p->G; ++b) {
+                    const uint64_t nch = p->row_chunks[b], rot = (shard + n_shards - b % n_shards) % n_shards;
+                    ss[b + 1] = ss[b] + (rot < nch ? (nch - rot + n_shards - 1) / n_shards : 0);
+                }
+            }
+            A.n_chunks = ss[p->G];
+            if (A.n_chunks > 0) {
+                NMZ_HIP(hipMemcpyAsync(p->d_chunk_start, ss.data(), (p->G + 1) * 8, hipMemcpyHostToDevice, st));
+                A.rq = p->rq;
+                uint64_t blocks = A.n_chunks * (p->rq / 2);
+                blocks = (blocks + 7) / 8 * 8;
+                NMZ_CHECK(blocks < (1ULL << 31), "too many traces for one launch");
+                NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_BV_NCOUNTERS * 8, st));
+                KernelTimer kt(p->ctx, st, "ed_bv");
+                NMZ_TRY(ed_bv_launch(A, p->band, blocks, st));
             }
         }
-        A.n_chunks = ss[p->G];
-        if (A.n_chunks == 0) return NMZ_OK;
-        NMZ_HIP(hipMemcpyAsync(p->d_chunk_start, ss.data(), (p->G + 1) * 8, hipMemcpyHostToDevice, st));
-        A.rq = p->rq;
-        uint64_t blocks = A.n_chunks * (p->rq / 2);
-        blocks = (blocks + 7) / 8 * 8;
-        NMZ_CHECK(blocks < (1ULL << 31), "too many traces for one launch");
-        NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_BV_NCOUNTERS * 8, st));
-        KernelTimer kt(p->ctx, st, "ed_bv");
-        return ed_bv_launch(A, p->band, blocks, st);
+        // k_ed_bv lists in-band results only; a shard's partial lists are completed after the merge
+        // (nmz_ed_knn_fill_dev)
+        if (n_shards == 1) {
+            hipLaunchKernelGGL(k_knn_fill, dim3(ceil_div(N, 256)), dim3(256), 0, st, d_knn, N, k, N, p->band + 1, 1);
+            NMZ_HIP(hipGetLastError());
+        }
+        return NMZ_OK;
     }
     if (p->fast) {
         EdArgs A;
@@ -831,6 +976,8 @@ int nmz_ed_plan_destroy(nmz_ed_plan *plan) {
     {
         CtxGuard g(plan->ctx);
         plan->mem.release();
+        plan->tp_mem.release();
+        plan->tp_ent.release();
     }
     delete plan;
     return NMZ_OK;
@@ -903,6 +1050,7 @@ int nmz_ed_plan_query_knn(nmz_ed_plan *plan, const uint64_t *q_off, const uint64
             A.nq[i] = (uint32_t)(q_off[qq + 1] - q_off[qq]);
         }
         A.knn = d_knn + (uint64_t)q * k;
+        A.prof = ed_qgram_enabled() ? (const uint4 *)plan->d_prof : nullptr;
         A.N = N;
         A.k = k;
         A.lds_dw = plan->lds_dw;
@@ -910,6 +1058,9 @@ int nmz_ed_plan_query_knn(nmz_ed_plan *plan, const uint64_t *q_off, const uint64
         KernelTimer kt(plan->ctx, st, "ed_bv_query");
         NMZ_TRY(ed_bv_query_launch(A, plan->band, ceil_div(N, pool), st));
     }
+    // k_ed_bv_query lists in-band results only: every other stored trace is at band + 1
+    hipLaunchKernelGGL(k_knn_fill, dim3(ceil_div(n_queries, 256)), dim3(256), 0, st, d_knn, n_queries, k, N,
+                       plan->band + 1, 0);
     hipLaunchKernelGGL(k_knn_final, dim3(ceil_div(nk, 256)), dim3(256), 0, st, d_knn, nk, d_id, d_ds);
     NMZ_HIP(hipGetLastError());
     NMZ_HIP(hipMemcpyAsync(knn_id, d_id, nk * 4, hipMemcpyDeviceToHost, st));
@@ -966,6 +1117,20 @@ int nmz_knn_merge_dev(nmz_ctx *ctx, const uint64_t *d_parts, uint32_t n_parts, u
     return NMZ_OK;
 }
 
+int nmz_ed_knn_fill_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys, void *stream) {
+    NMZ_CHECK(plan != nullptr, "plan is NULL");
+    NMZ_CHECK(k >= 1 && k <= 64, "k must be in [1, 64]");
+    CtxGuard g(plan->ctx);
+    NMZ_TRY(g.rc);
+    if (plan->n == 0) return NMZ_OK;
+    NMZ_CHECK(d_knn_keys != nullptr, "d_knn_keys is NULL");
+    hipLaunchKernelGGL(k_knn_fill, dim3(ceil_div(plan->n, 256)), dim3(256), 0,
+                       stream ? (hipStream_t)stream : plan->ctx->stream, d_knn_keys, plan->n, k, plan->n,
+                       plan->band + 1, 1);
+    NMZ_HIP(hipGetLastError());
+    return NMZ_OK;
+}
+
 int nmz_ed_allpairs_knn(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, uint32_t n_traces, uint32_t band,
                         uint32_t k, uint32_t *knn_id, uint32_t *knn_dist) {
     NMZ_CHECK(ctx != nullptr, "ctx is NULL");
@@ -979,6 +1144,8 @@ int nmz_ed_allpairs_knn(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, 
         nmz_ed_plan *p;
         ~G() {
             p->mem.release();
+            p->tp_mem.release();
+            p->tp_ent.release();
             delete p;
         }
     } pg{plan};

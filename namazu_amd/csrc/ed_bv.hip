@@ -236,18 +236,18 @@ __device__ __forceinline__ void bv_block(BvState<BvShape<W>::KF> &S1, BvState<Bv
 // publish the pairs of the lanes with `fin` set: candidate lists per lane
 // (distinct lists), query lists wave-reduced (the 2 query lists are shared by
 // every lane of the workgroup; per-lane atomics on them serialize in L2)
+// Only results within the band are listed: every other pair's result is w + 1, and k_knn_fill completes the lists
+// with (w + 1, smallest ids not listed) after the search, so the bulk of the pairs (cut off, out of the length band
+// or settled by the q-gram bound) publish nothing and cost no global atomics.
 __device__ __forceinline__ void bv_publish(const EdBvArgs &A, bool fin, uint32_t j, uint32_t q1, uint32_t q2,
                                             bool v2, uint32_t r1, uint32_t r2, uint32_t lane, uint32_t w,
                                             uint32_t &in_band) {
-    if (fin) {
-        in_band += (uint32_t)(r1 <= w) + (uint32_t)(v2 && r2 <= w);
-        bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, ((uint64_t)r1 << 32) | q1);
-        if (v2) bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, ((uint64_t)r2 << 32) | q2);
-    }
-    const uint64_t k1 = fin ? (((uint64_t)r1 << 32) | j) : UINT64_MAX;
-    const uint64_t k2 = (fin && v2) ? (((uint64_t)r2 << 32) | j) : UINT64_MAX;
-    bv_knn_insert_wave(A.knn + (uint64_t)q1 * A.k, A.k, k1, lane);
-    if (q2 < A.N) bv_knn_insert_wave(A.knn + (uint64_t)q2 * A.k, A.k, k2, lane);
+    const bool b1 = fin && r1 <= w, b2 = fin && v2 && r2 <= w;
+    in_band += (uint32_t)b1 + (uint32_t)b2;
+    if (b1) bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, ((uint64_t)r1 << 32) | q1);
+    if (b2) bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, ((uint64_t)r2 << 32) | q2);
+    if (__any(b1)) bv_knn_insert_wave(A.knn + (uint64_t)q1 * A.k, A.k, b1 ? (((uint64_t)r1 << 32) | j) : UINT64_MAX, lane);
+    if (__any(b2)) bv_knn_insert_wave(A.knn + (uint64_t)q2 * A.k, A.k, b2 ? (((uint64_t)r2 << 32) | j) : UINT64_MAX, lane);
 }
 
 __device__ __forceinline__ void bv_load_block(uint32_t (&dst)[16], const uint16_t *stream, uint32_t blk) {
@@ -256,6 +256,66 @@ __device__ __forceinline__ void bv_load_block(uint32_t (&dst)[16], const uint16_
     for (int r = 0; r < 4; ++r) {
         const uint4 v = p[r];
         dst[4 * r] = v.x; dst[4 * r + 1] = v.y; dst[4 * r + 2] = v.z; dst[4 * r + 3] = v.w;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// q-gram filter (nmz_internal.h ED_QG_*): bucket of the adjacent pair (x, y) of stream values (Peq-row byte
+// offsets, i.e. dense symbol ids; 0xffff for a query symbol the store lacks, which merges such symbols -- a
+// valid coarsening). Profiles are built once per plan; a lane compares its candidate's profile with the
+// workgroup's query profiles by v_sad_u8 (|a - b| summed over 4 packed counts) before any DP.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t qg_bucket(uint32_t x, uint32_t y) {
+    uint32_t h = x * 0x9E3779B1u + y * 0x85EBCA77u;
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    return h >> (32 - 7);  // ED_QG_BUCKETS = 128
+}
+
+// one workgroup per trace: bigram counts in LDS, saturated at 255 and packed 4 per dword
+__global__ __launch_bounds__(256) void k_ed_qgram_profile(const uint16_t *__restrict__ bs,
+                                                          const uint64_t *__restrict__ soff,
+                                                          const uint32_t *__restrict__ len, uint32_t *__restrict__ prof) {
+    __shared__ uint32_t hist[ED_QG_BUCKETS];
+    const uint32_t i = blockIdx.x;
+    if (threadIdx.x < ED_QG_BUCKETS) hist[threadIdx.x] = 0;
+    __syncthreads();
+    const uint16_t *a = bs + soff[i];
+    const uint32_t n = len[i];
+    for (uint32_t t = threadIdx.x; t + 1 < n; t += 256) atomicAdd(&hist[qg_bucket(a[t], a[t + 1])], 1u);
+    __syncthreads();
+    if (threadIdx.x < ED_QG_DW) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) w |= min(hist[4 * threadIdx.x + b], 255u) << (8 * b);
+        prof[(uint64_t)i * ED_QG_DW + threadIdx.x] = w;
+    }
+}
+
+int ed_qgram_profiles(const uint16_t *bs, const uint64_t *soff, const uint32_t *len, uint32_t N, uint32_t *prof,
+                      hipStream_t st) {
+    if (N == 0) return NMZ_OK;
+    hipLaunchKernelGGL(k_ed_qgram_profile, dim3(N), dim3(256), 0, st, bs, soff, len, prof);
+    NMZ_HIP(hipGetLastError());
+    return NMZ_OK;
+}
+
+// L1 distance of a candidate's profile (global) to the two query profiles (LDS, 16-byte aligned)
+__device__ __forceinline__ void qg_l1x2(const uint4 *__restrict__ cp, const uint4 *qp1, const uint4 *qp2,
+                                        uint32_t &s1, uint32_t &s2) {
+    s1 = 0;
+    s2 = 0;
+#pragma unroll
+    for (int r = 0; r < (int)ED_QG_DW / 4; ++r) {
+        const uint4 c = cp[r], a = qp1[r], b = qp2[r];
+        s1 = __builtin_amdgcn_sad_u8(c.x, a.x, s1);
+        s1 = __builtin_amdgcn_sad_u8(c.y, a.y, s1);
+        s1 = __builtin_amdgcn_sad_u8(c.z, a.z, s1);
+        s1 = __builtin_amdgcn_sad_u8(c.w, a.w, s1);
+        s2 = __builtin_amdgcn_sad_u8(c.x, b.x, s2);
+        s2 = __builtin_amdgcn_sad_u8(c.y, b.y, s2);
+        s2 = __builtin_amdgcn_sad_u8(c.z, b.z, s2);
+        s2 = __builtin_amdgcn_sad_u8(c.w, b.w, s2);
     }
 }
 
@@ -270,6 +330,109 @@ __device__ __forceinline__ void bv_load_block(uint32_t (&dst)[16], const uint16_
 #else
 #define NMZ_ED_BV_ATTR
 #endif
+
+// wave-reduce the work counters and add them to counters[] (nmz_ed_plan_counters), if counting
+__device__ __forceinline__ void bv_flush_counters(uint64_t *counters, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                                  uint32_t c4, uint32_t c5) {
+    if (!counters) return;
+    uint64_t c[ED_BV_NCOUNTERS] = {c0, c1, c2, c3, c4, c5};
+#pragma unroll
+    for (int i = 0; i < ED_BV_NCOUNTERS; ++i) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) c[i] += __shfl_xor(c[i], off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int i = 0; i < ED_BV_NCOUNTERS; ++i)
+            if (c[i]) atomicAdd((unsigned long long *)&counters[i], (unsigned long long)c[i]);
+    }
+}
+
+// The DP loop of a workgroup whose 2 queries' Peq tables are in LDS: `ns` entries (candidate j, run1, run2 --
+// the pairs that need a DP, from fetch(idx, j, run1, run2)) drawn by the lanes through the LDS counter pool_next
+// (which must start at 256: entries 0..255 are pre-assigned), each run to extraction or cut-off, the in-band
+// results listed (bv_publish). Work counters are accumulated into the caller's registers.
+template <int W, class Fetch>
+__device__ __forceinline__ void bv_dp_run(const EdBvArgs &A, const uint32_t *peq, uint32_t &pool_next, uint32_t ns,
+                                          uint32_t q1, uint32_t q2, uint32_t n1, uint32_t n2, bool has2, Fetch fetch,
+                                          uint32_t &c_dp_pairs, uint32_t &c_in_band, uint32_t &c_blocks,
+                                          uint32_t &c_dp_cand, uint32_t &c_live) {
+    using SH = BvShape<W>;
+    const uint32_t lane = threadIdx.x & 63;
+    // lane state
+    uint32_t j = 0, m = 0, r1 = W + 1, r2 = W + 1, kb0 = 0;
+    bool run1 = false, run2 = false, active = false, v2 = false;
+    const uint16_t *stream = A.bsym;
+    BvState<SH::KF> S1, S2;
+    uint32_t cur[16], nxt[16];
+    uint32_t idx = threadIdx.x;  // the first 256 entries are pre-assigned
+    uint32_t kb = 0;
+    bool need = ns > 0;
+    bool first = true;
+    while (ns > 0) {
+        // ---- (re)assign survivors to lanes that need one ----
+        const uint64_t want = __ballot(need);
+        if (want != 0) {
+            if (!first) {
+                const uint32_t cnt = __popcll(want);
+                uint32_t base_idx = 0;
+                if (lane == (uint32_t)(__ffsll((unsigned long long)want) - 1)) base_idx = atomicAdd(&pool_next, cnt);
+                base_idx = __shfl(base_idx, __ffsll((unsigned long long)want) - 1, 64);
+                if (need) idx = base_idx + __popcll(want & ((1ull << lane) - 1));
+            }
+            first = false;
+            if (need) {
+                need = false;
+                if (idx >= ns) {
+                    active = false;
+                    stream = A.bsym;  // idle lanes keep reading a valid stream (results unused)
+                    bv_load_block(cur, stream, 0);
+                } else {
+                    fetch(idx, j, run1, run2);
+                    m = A.len[j];
+                    stream = A.bsym + A.soff[j];
+                    v2 = has2 && j > q2;
+                    r1 = W + 1;
+                    r2 = W + 1;
+                    active = true;
+                    c_dp_cand += 1;
+                    c_dp_pairs += (uint32_t)run1 + (uint32_t)run2;
+                    kb0 = kb;
+                    bv_init<W>(S1);
+                    bv_init<W>(S2);
+                    bv_load_block(cur, stream, 0);
+                }
+            }
+        }
+        if (!__any(active)) break;
+        c_blocks += (uint32_t)active;
+        c_live += active ? (uint32_t)run1 + (uint32_t)run2 : 0u;
+        // ---- one 32-column block ----
+        const uint32_t lkb = active ? kb - kb0 : 0;
+        bv_load_block(nxt, stream, lkb + 1);  // streams carry one spare block
+        const uint32_t j0 = 32 * lkb;
+        const uint32_t base = (lkb + 1) * 8;
+        const bool here = active && (run1 || run2) && m > j0 && m <= j0 + 32;
+        if (__any(here)) {
+            bv_block<W, true>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2);
+        } else {
+            bv_block<W, false>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2);
+        }
+        S1.T += 32 - __builtin_popcount(S1.acc);
+        S2.T += 32 - __builtin_popcount(S2.acc);
+        if (run1 && bv_lower_bound<W>(S1, S1.T) > W) run1 = false;
+        if (run2 && bv_lower_bound<W>(S2, S2.T) > W) run2 = false;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cur[r] = nxt[r];
+        ++kb;
+        const bool fin = active && !run1 && !run2;
+        if (__any(fin)) bv_publish(A, fin, j, q1, q2, v2, r1, r2, lane, W, c_in_band);
+        if (fin) {
+            active = false;
+            need = true;
+        }
+    }
+}
 
 template <int W>
 __global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv(EdBvArgs A) {
@@ -303,13 +466,75 @@ __global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv(EdBvArgs A) {
     const uint32_t pool_lo = max(c0, q1 + 1);
     const uint32_t pool_n = c1 > pool_lo ? c1 - pool_lo : 0;
 
-    {
-        uint4 *p4 = (uint4 *)peq;
-        for (uint32_t i = threadIdx.x; i < A.lds_dw / 4; i += 256) p4[i] = make_uint4(0, 0, 0, 0);
-        if (threadIdx.x == 0) pool_next = 256;
+    // after the pool counter and the survivor count (16-byte aligned: lds_dw is a multiple of 4): the two queries'
+    // q-gram profiles, then the pool's survivors (u16: pool index | run1 << 14 | run2 << 15)
+    uint32_t &n_surv = peq[A.lds_dw + 1];
+    uint32_t *qprof = peq + A.lds_dw + 4;
+    uint16_t *surv = (uint16_t *)(qprof + 2 * ED_QG_DW);
+    if (threadIdx.x == 0) {
+        pool_next = 256;
+        n_surv = 0;
+    }
+    if (A.prof && threadIdx.x < 2 * ED_QG_DW) {
+        const uint32_t q = threadIdx.x < ED_QG_DW ? q1 : q2, w = threadIdx.x % ED_QG_DW;
+        qprof[threadIdx.x] = (q < A.N) ? ((const uint32_t *)A.prof)[(uint64_t)q * ED_QG_DW + w] : 0u;
     }
     __syncthreads();
-    {
+    // work counters (A.counters): DP pairs, in-band pairs, lane blocks, DP candidates, live query-blocks, q-gram
+    uint32_t c_dp_pairs = 0, c_in_band = 0, c_blocks = 0, c_dp_cand = 0, c_live = 0, c_qgram = 0;
+    // ---- the pool's pairs that need a DP, decided for all candidates at once (all 256 threads) ----
+    // Out of the length band (|n - m| > w) or settled by the q-gram bound (L1 > 4w): w + 1, nothing to list
+    // (k_knn_fill). An empty trace within the length band: n + m <= w, listed here. The DP loop below then
+    // draws only survivors, so lanes never stall the wave on candidates that need no DP, and a workgroup whose
+    // pool has no survivor builds no Peq tables at all. Four candidates per thread per step keep their loads
+    // in flight together.
+    for (uint32_t c4 = 4 * threadIdx.x; c4 < pool_n; c4 += 4 * 256) {
+        uint32_t mm[4], l1[4], l2[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) mm[u] = c4 + u < pool_n ? A.len[pool_lo + c4 + u] : 0u;
+        if (A.prof) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                qg_l1x2(A.prof + (uint64_t)(pool_lo + min(c4 + u, pool_n - 1)) * (ED_QG_DW / 4), (const uint4 *)qprof,
+                        (const uint4 *)(qprof + ED_QG_DW), l1[u], l2[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t c = c4 + u;
+            if (c >= pool_n) break;
+            const uint32_t jj = pool_lo + c;
+            const bool vv2 = has2 && jj > q2;
+            const int32_t dd1 = (int32_t)mm[u] - (int32_t)n1, dd2 = (int32_t)mm[u] - (int32_t)n2;
+            bool a1 = dd1 <= W && dd1 >= -W, a2 = vv2 && dd2 <= W && dd2 >= -W;
+            if (a1 && (n1 == 0 || mm[u] == 0)) {
+                const uint64_t r = n1 + mm[u];
+                bv_knn_insert(A.knn + (uint64_t)jj * A.k, A.k, (r << 32) | q1);
+                bv_knn_insert(A.knn + (uint64_t)q1 * A.k, A.k, (r << 32) | jj);
+                c_in_band += 1;
+                a1 = false;
+            }
+            if (a2 && (n2 == 0 || mm[u] == 0)) {
+                const uint64_t r = n2 + mm[u];
+                bv_knn_insert(A.knn + (uint64_t)jj * A.k, A.k, (r << 32) | q2);
+                bv_knn_insert(A.knn + (uint64_t)q2 * A.k, A.k, (r << 32) | jj);
+                c_in_band += 1;
+                a2 = false;
+            }
+            if (A.prof) {  // q-gram bound: L1 > 4w => ED_w = w + 1, no DP
+                const bool f1 = a1 && l1[u] > 4 * W, f2 = a2 && l2[u] > 4 * W;
+                c_qgram += (uint32_t)f1 + (uint32_t)f2;
+                a1 = a1 && !f1;
+                a2 = a2 && !f2;
+            }
+            if (a1 || a2) surv[atomicAdd(&n_surv, 1u)] = (uint16_t)(c | ((uint32_t)a1 << 14) | ((uint32_t)a2 << 15));
+        }
+    }
+    __syncthreads();
+    const uint32_t ns = n_surv;
+    if (ns > 0) {  // the two queries' Peq tables (uniform branch: ns is read after the barrier)
+        uint4 *p4 = (uint4 *)peq;
+        for (uint32_t i = threadIdx.x; i < A.lds_dw / 4; i += 256) p4[i] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
         const uint16_t *a1 = A.bsym + A.soff[q1];
         for (uint32_t i = threadIdx.x; i < n1; i += 256) {
             const uint32_t p = i + 1 + SH::OFF;
@@ -322,111 +547,206 @@ __global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv(EdBvArgs A) {
                 atomicOr(&peq[(uint32_t)a2[i] / 4 + (p >> 5) * 2 + 1], 1u << (p & 31));
             }
         }
+        __syncthreads();
+    }
+
+    bv_dp_run<W>(A, peq, pool_next, ns, q1, q2, n1, n2, has2,
+                 [&](uint32_t i, uint32_t &jj, bool &a1, bool &a2) {
+                     const uint32_t e = surv[i];
+                     jj = pool_lo + (e & 0x3fffu);
+                     a1 = (e >> 14) & 1u;
+                     a2 = e >> 15;
+                 },
+                 c_dp_pairs, c_in_band, c_blocks, c_dp_cand, c_live);
+    bv_flush_counters(A.counters, c_dp_pairs, c_in_band, c_blocks, c_dp_cand, c_live, c_qgram);
+}
+
+// ---------------------------------------------------------------------------
+// Two-phase search (nmz_internal.h EdQgArgs): filter tiles, then DP work items.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t qg_l1_reg(const uint4 (&c)[ED_QG_DW / 4], const uint4 *q) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int r = 0; r < (int)ED_QG_DW / 4; ++r) {
+        const uint4 a = q[r];
+        s = __builtin_amdgcn_sad_u8(c[r].x, a.x, s);
+        s = __builtin_amdgcn_sad_u8(c[r].y, a.y, s);
+        s = __builtin_amdgcn_sad_u8(c[r].z, a.z, s);
+        s = __builtin_amdgcn_sad_u8(c[r].w, a.w, s);
+    }
+    return s;
+}
+
+// One tile: queries [64 qb, 64 qb + 64) x candidates [256 cb, 256 cb + 256), pairs j > q only. Tiles of a query
+// block are dealt to shards round-robin starting at shard (qb mod n_shards), as k_ed_bv deals its chunks.
+template <int W, bool COUNT>
+__global__ __launch_bounds__(256) void k_ed_qg_filter(EdQgArgs A) {
+    __shared__ uint4 qp[64][ED_QG_DW / 4];
+    __shared__ uint32_t qlen[64];
+    const uint64_t t = blockIdx.x;
+    if (t >= A.n_tiles) return;
+    uint32_t lo = 0, hi = A.QB;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (A.tile_start[mid] <= t) lo = mid; else hi = mid;
+    }
+    const uint32_t qb = lo;
+    const uint32_t rot = (A.shard + A.n_shards - qb % A.n_shards) % A.n_shards;
+    const uint32_t cb = qb / 4 + rot + A.n_shards * (uint32_t)(t - A.tile_start[qb]);
+    for (uint32_t i = threadIdx.x; i < 64 * (ED_QG_DW / 4); i += 256) {
+        const uint32_t q = 64 * qb + i / (ED_QG_DW / 4);
+        qp[i / (ED_QG_DW / 4)][i % (ED_QG_DW / 4)] =
+            q < A.N ? A.prof[(uint64_t)q * (ED_QG_DW / 4) + i % (ED_QG_DW / 4)] : make_uint4(0, 0, 0, 0);
+    }
+    if (threadIdx.x < 64) qlen[threadIdx.x] = 64 * qb + threadIdx.x < A.N ? A.len[64 * qb + threadIdx.x] : 0u;
+    __syncthreads();
+    const uint32_t j = 256 * cb + threadIdx.x, lane = threadIdx.x & 63;
+    const bool jv = j < A.N;
+    const uint32_t m = jv ? A.len[j] : 0u;
+    uint4 cp[ED_QG_DW / 4];
+#pragma unroll
+    for (int r = 0; r < (int)ED_QG_DW / 4; ++r)
+        cp[r] = jv ? A.prof[(uint64_t)j * (ED_QG_DW / 4) + r] : make_uint4(0, 0, 0, 0);
+    uint32_t c_qgram = 0, c_in_band = 0;
+    for (uint32_t pp = 0; pp < 32; ++pp) {
+        const uint32_t q1 = 64 * qb + 2 * pp, q2 = q1 + 1;
+        if (q1 >= A.N) break;
+        const uint32_t n1 = qlen[2 * pp], n2 = qlen[2 * pp + 1];
+        const int32_t dd1 = (int32_t)m - (int32_t)n1, dd2 = (int32_t)m - (int32_t)n2;
+        bool a1 = jv && j > q1 && dd1 <= W && dd1 >= -W;
+        bool a2 = jv && q2 < A.N && j > q2 && dd2 <= W && dd2 >= -W;
+        if (a1 && (n1 == 0 || m == 0)) {  // an empty trace: n + m <= w, listed once (count pass)
+            if (COUNT) {
+                const uint64_t r = n1 + m;
+                bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, (r << 32) | q1);
+                bv_knn_insert(A.knn + (uint64_t)q1 * A.k, A.k, (r << 32) | j);
+                c_in_band += 1;
+            }
+            a1 = false;
+        }
+        if (a2 && (n2 == 0 || m == 0)) {
+            if (COUNT) {
+                const uint64_t r = n2 + m;
+                bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, (r << 32) | q2);
+                bv_knn_insert(A.knn + (uint64_t)q2 * A.k, A.k, (r << 32) | j);
+                c_in_band += 1;
+            }
+            a2 = false;
+        }
+        if (a1 || a2) {  // q-gram bound: L1 > 4w => ED_w = w + 1, no DP
+            const bool f1 = a1 && qg_l1_reg(cp, qp[2 * pp]) > 4 * W;
+            const bool f2 = a2 && qg_l1_reg(cp, qp[2 * pp + 1]) > 4 * W;
+            c_qgram += (uint32_t)f1 + (uint32_t)f2;
+            a1 = a1 && !f1;
+            a2 = a2 && !f2;
+        }
+        const bool sv = a1 || a2;
+        const uint64_t mask = __ballot(sv);
+        if (mask) {
+            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)mask) - 1;
+            const uint32_t n = (uint32_t)__popcll(mask), p = q1 >> 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(COUNT ? &A.cnt[p] : &A.cur[p], n);
+            if (!COUNT) {
+                base = __shfl(base, leader, 64);
+                if (sv)
+                    A.ent[base + __popcll(mask & ((1ull << lane) - 1))] =
+                        j | ((uint32_t)a1 << 30) | ((uint32_t)a2 << 31);
+            }
+        }
+    }
+    if (COUNT) bv_flush_counters(A.counters, 0, c_in_band, 0, 0, 0, c_qgram);
+}
+
+int ed_qg_filter_launch(const EdQgArgs &A, uint32_t band, bool count, hipStream_t st) {
+    if (A.n_tiles == 0) return NMZ_OK;
+    NMZ_CHECK(A.n_tiles < (1ULL << 31), "too many traces for one launch");
+    const dim3 g((unsigned)A.n_tiles), b(256);
+#define NMZ_QG(Wv)                                                                          \
+    case Wv:                                                                                \
+        if (count) hipLaunchKernelGGL((k_ed_qg_filter<Wv, true>), g, b, 0, st, A);           \
+        else hipLaunchKernelGGL((k_ed_qg_filter<Wv, false>), g, b, 0, st, A);                \
+        break;
+    switch (band) {
+        NMZ_QG(8)
+        NMZ_QG(16)
+        NMZ_QG(32)
+        default: return fail(NMZ_EINVAL, "internal: band has no bit-parallel kernel");
+    }
+#undef NMZ_QG
+    NMZ_HIP(hipGetLastError());
+    return NMZ_OK;
+}
+
+// One work item: <= ED_BV_ITEM entries of query pair p (items dealt in XCD-remapped order, so a pair's items and
+// its neighbours' -- near-duplicates share candidates -- run on one XCD).
+template <int W>
+__global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv_dp(EdBvArgs A, const uint32_t *__restrict__ ioff,
+                                                                const uint32_t *__restrict__ poff,
+                                                                const uint32_t *__restrict__ ent, uint32_t n_pairs,
+                                                                uint32_t n_items) {
+    using SH = BvShape<W>;
+    extern __shared__ uint32_t peq[];
+    uint32_t &pool_next = peq[A.lds_dw];
+    const uint32_t nblk = gridDim.x, per_xcd = nblk / 8;
+    const uint32_t lb = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
+    if (lb >= n_items) return;
+    uint32_t lo = 0, hi = n_pairs;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (ioff[mid] <= lb) lo = mid; else hi = mid;
+    }
+    const uint32_t p = lo, ci = lb - ioff[p];
+    const uint32_t e0 = poff[p] + ci * ED_BV_ITEM, e1 = min(poff[p + 1], e0 + ED_BV_ITEM), ns = e1 - e0;
+    const uint32_t q1 = 2 * p, q2 = q1 + 1;
+    const bool has2 = q2 < A.N;
+    const uint32_t n1 = A.len[q1], n2 = has2 ? A.len[q2] : 0;
+    {
+        uint4 *p4 = (uint4 *)peq;
+        for (uint32_t i = threadIdx.x; i < A.lds_dw / 4; i += 256) p4[i] = make_uint4(0, 0, 0, 0);
+        if (threadIdx.x == 0) pool_next = 256;
     }
     __syncthreads();
-    if (pool_n == 0) return;
-
-    const uint32_t lane = threadIdx.x & 63;
-    // lane state
-    uint32_t j = 0, m = 0, r1 = W + 1, r2 = W + 1, kb0 = 0;
-    bool run1 = false, run2 = false, active = false, v2 = false;
-    const uint16_t *stream = A.bsym;
-    BvState<SH::KF> S1, S2;
-    uint32_t cur[16], nxt[16];
-    uint32_t idx = threadIdx.x;  // first 256 candidates are pre-assigned
-    uint32_t kb = 0;
-    bool need = true;
-    bool first = true;
-    // work counters (A.counters): DP pairs, in-band pairs, lane blocks, DP candidates, live query-blocks
+    {
+        const uint16_t *a1 = A.bsym + A.soff[q1];
+        for (uint32_t i = threadIdx.x; i < n1; i += 256) {
+            const uint32_t pos = i + 1 + SH::OFF;
+            atomicOr(&peq[(uint32_t)a1[i] / 4 + (pos >> 5) * 2 + 0], 1u << (pos & 31));
+        }
+        if (has2) {
+            const uint16_t *a2 = A.bsym + A.soff[q2];
+            for (uint32_t i = threadIdx.x; i < n2; i += 256) {
+                const uint32_t pos = i + 1 + SH::OFF;
+                atomicOr(&peq[(uint32_t)a2[i] / 4 + (pos >> 5) * 2 + 1], 1u << (pos & 31));
+            }
+        }
+    }
+    __syncthreads();
     uint32_t c_dp_pairs = 0, c_in_band = 0, c_blocks = 0, c_dp_cand = 0, c_live = 0;
-    while (true) {
-        // ---- (re)assign candidates to lanes that need one ----
-        while (true) {
-            const uint64_t want = __ballot(need);
-            if (want == 0) break;
-            if (!first) {
-                const uint32_t cnt = __popcll(want);
-                uint32_t base_idx = 0;
-                if (lane == (uint32_t)(__ffsll((unsigned long long)want) - 1)) base_idx = atomicAdd(&pool_next, cnt);
-                base_idx = __shfl(base_idx, __ffsll((unsigned long long)want) - 1, 64);
-                if (need) idx = base_idx + __popcll(want & ((1ull << lane) - 1));
-            }
-            first = false;
-            if (need) {
-                if (idx >= pool_n) {
-                    need = false;
-                    active = false;
-                    stream = A.bsym;  // idle lanes keep reading a valid stream (results unused)
-                    bv_load_block(cur, stream, 0);
-                } else {
-                    j = pool_lo + idx;
-                    m = A.len[j];
-                    stream = A.bsym + A.soff[j];
-                    v2 = has2 && j > q2;
-                    r1 = W + 1;
-                    r2 = W + 1;
-                    const int32_t dd1 = (int32_t)m - (int32_t)n1, dd2 = (int32_t)m - (int32_t)n2;
-                    run1 = dd1 <= W && dd1 >= -W;
-                    run2 = v2 && dd2 <= W && dd2 >= -W;
-                    if (run1 && (n1 == 0 || m == 0)) { r1 = n1 + m; run1 = false; }
-                    if (run2 && (n2 == 0 || m == 0)) { r2 = n2 + m; run2 = false; }
-                    if (run1 || run2) {
-                        need = false;
-                        active = true;
-                        c_dp_cand += 1;
-                        c_dp_pairs += (uint32_t)run1 + (uint32_t)run2;
-                        kb0 = kb;
-                        bv_init<W>(S1);
-                        bv_init<W>(S2);
-                        bv_load_block(cur, stream, 0);
-                    }
-                }
-            }
-            // candidates decided without a DP (|n - m| > w, empty traces): publish, draw again
-            const bool fin = need && !active && idx < pool_n;
-            if (__any(fin)) bv_publish(A, fin, j, q1, q2, v2, r1, r2, lane, W, c_in_band);
-        }
-        if (!__any(active)) break;
-        c_blocks += (uint32_t)active;
-        c_live += active ? (uint32_t)run1 + (uint32_t)run2 : 0u;
-        // ---- one 32-column block ----
-        const uint32_t lkb = active ? kb - kb0 : 0;
-        bv_load_block(nxt, stream, lkb + 1);  // streams carry one spare block
-        const uint32_t j0 = 32 * lkb;
-        const uint32_t base = (lkb + 1) * 8;
-        const bool here = active && (run1 || run2) && m > j0 && m <= j0 + 32;
-        if (__any(here)) {
-            bv_block<W, true>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2);
-        } else {
-            bv_block<W, false>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2);
-        }
-        S1.T += 32 - __builtin_popcount(S1.acc);
-        S2.T += 32 - __builtin_popcount(S2.acc);
-        if (run1 && bv_lower_bound<W>(S1, S1.T) > W) run1 = false;
-        if (run2 && bv_lower_bound<W>(S2, S2.T) > W) run2 = false;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) cur[r] = nxt[r];
-        ++kb;
-        const bool fin = active && !run1 && !run2;
-        if (__any(fin)) bv_publish(A, fin, j, q1, q2, v2, r1, r2, lane, W, c_in_band);
-        if (fin) {
-            active = false;
-            need = true;
-        }
+    bv_dp_run<W>(A, peq, pool_next, ns, q1, q2, n1, n2, has2,
+                 [&](uint32_t i, uint32_t &jj, bool &a1, bool &a2) {
+                     const uint32_t e = ent[e0 + i];
+                     jj = e & 0x3fffffffu;
+                     a1 = (e >> 30) & 1u;
+                     a2 = e >> 31;
+                 },
+                 c_dp_pairs, c_in_band, c_blocks, c_dp_cand, c_live);
+    bv_flush_counters(A.counters, c_dp_pairs, c_in_band, c_blocks, c_dp_cand, c_live, 0);
+}
+
+int ed_bv_dp_launch(const EdBvArgs &A, const uint32_t *ioff, const uint32_t *poff, const uint32_t *ent,
+                    uint32_t n_pairs, uint32_t n_items, uint32_t band, hipStream_t st) {
+    if (n_items == 0) return NMZ_OK;
+    const unsigned blocks = (n_items + 7) / 8 * 8;  // a multiple of 8 for the XCD remap
+    const size_t lds = (size_t)A.lds_dw * 4 + 16;
+    switch (band) {
+        case 8: hipLaunchKernelGGL(k_ed_bv_dp<8>, dim3(blocks), dim3(256), lds, st, A, ioff, poff, ent, n_pairs, n_items); break;
+        case 16: hipLaunchKernelGGL(k_ed_bv_dp<16>, dim3(blocks), dim3(256), lds, st, A, ioff, poff, ent, n_pairs, n_items); break;
+        case 32: hipLaunchKernelGGL(k_ed_bv_dp<32>, dim3(blocks), dim3(256), lds, st, A, ioff, poff, ent, n_pairs, n_items); break;
+        default: return fail(NMZ_EINVAL, "internal: band has no bit-parallel kernel");
     }
-    if (A.counters) {
-        uint64_t c[ED_BV_NCOUNTERS] = {c_dp_pairs, c_in_band, c_blocks, c_dp_cand, c_live};
-#pragma unroll
-        for (int i = 0; i < ED_BV_NCOUNTERS; ++i) {
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) c[i] += __shfl_xor(c[i], off, 64);
-        }
-        if (lane == 0) {
-#pragma unroll
-            for (int i = 0; i < ED_BV_NCOUNTERS; ++i)
-                if (c[i]) atomicAdd((unsigned long long *)&A.counters[i], (unsigned long long)c[i]);
-        }
-    }
+    NMZ_HIP(hipGetLastError());
+    return NMZ_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -446,19 +766,30 @@ __global__ __launch_bounds__(256) void k_ed_bv_query(EdBvQueryArgs A) {
     const uint32_t pool_n = min(A.pool, A.N - pool_lo);
     const uint32_t n1 = A.nq[0], n2 = A.nq[1];
     const bool has2 = A.n_queries > 1;
+    // query q-gram profiles (packed, after the pool counter) and their bucket counts (scratch)
+    uint32_t *qprof = peq + A.lds_dw + 4, *qhist = qprof + 2 * ED_QG_DW;
     {
         uint4 *p4 = (uint4 *)peq;
         for (uint32_t i = threadIdx.x; i < A.lds_dw / 4; i += 256) p4[i] = make_uint4(0, 0, 0, 0);
         if (threadIdx.x == 0) pool_next = 256;
+        for (uint32_t i = threadIdx.x; i < 2 * ED_QG_BUCKETS; i += 256) qhist[i] = 0;
     }
     __syncthreads();
     for (uint32_t q = 0; q < A.n_queries; ++q) {
         const uint16_t *a = A.qs + A.qoff[q];
         for (uint32_t i = threadIdx.x; i < A.nq[q]; i += 256) {
+            if (i + 1 < A.nq[q]) atomicAdd(&qhist[q * ED_QG_BUCKETS + qg_bucket(a[i], a[i + 1])], 1u);
             if (a[i] == 0xffffu) continue;
             const uint32_t p = i + 1 + SH::OFF;
             atomicOr(&peq[(uint32_t)a[i] / 4 + (p >> 5) * 2 + q], 1u << (p & 31));
         }
+    }
+    __syncthreads();
+    if (threadIdx.x < 2 * ED_QG_DW) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) w |= min(qhist[4 * threadIdx.x + b], 255u) << (8 * b);
+        qprof[threadIdx.x] = w;
     }
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
@@ -470,11 +801,10 @@ __global__ __launch_bounds__(256) void k_ed_bv_query(EdBvQueryArgs A) {
     uint32_t idx = threadIdx.x;
     uint32_t kb = 0;
     bool need = true, first = true;
-    auto publish = [&](bool fin) {
-        const uint64_t k1 = fin ? (((uint64_t)r1 << 32) | j) : UINT64_MAX;
-        const uint64_t k2 = (fin && has2) ? (((uint64_t)r2 << 32) | j) : UINT64_MAX;
-        bv_knn_insert_wave(A.knn, A.k, k1, lane);
-        if (has2) bv_knn_insert_wave(A.knn + A.k, A.k, k2, lane);
+    auto publish = [&](bool fin) {  // in-band results only (k_knn_fill completes the lists, as in k_ed_bv)
+        const bool b1 = fin && r1 <= W, b2 = fin && has2 && r2 <= W;
+        if (__any(b1)) bv_knn_insert_wave(A.knn, A.k, b1 ? (((uint64_t)r1 << 32) | j) : UINT64_MAX, lane);
+        if (__any(b2)) bv_knn_insert_wave(A.knn + A.k, A.k, b2 ? (((uint64_t)r2 << 32) | j) : UINT64_MAX, lane);
     };
     while (true) {
         while (true) {
@@ -505,6 +835,13 @@ __global__ __launch_bounds__(256) void k_ed_bv_query(EdBvQueryArgs A) {
                     run2 = has2 && dd2 <= W && dd2 >= -W;
                     if (run1 && (n1 == 0 || m == 0)) { r1 = n1 + m; run1 = false; }
                     if (run2 && (n2 == 0 || m == 0)) { r2 = n2 + m; run2 = false; }
+                    if (A.prof && (run1 || run2)) {  // q-gram bound, as in k_ed_bv
+                        uint32_t l1, l2;
+                        qg_l1x2(A.prof + (uint64_t)j * (ED_QG_DW / 4), (const uint4 *)qprof,
+                                (const uint4 *)(qprof + ED_QG_DW), l1, l2);
+                        run1 = run1 && l1 <= 4 * W;
+                        run2 = run2 && l2 <= 4 * W;
+                    }
                     if (run1 || run2) {
                         need = false;
                         active = true;
@@ -546,7 +883,7 @@ __global__ __launch_bounds__(256) void k_ed_bv_query(EdBvQueryArgs A) {
 }
 
 int ed_bv_query_launch(const EdBvQueryArgs &A, uint32_t band, uint32_t blocks, hipStream_t st) {
-    const size_t lds = (size_t)A.lds_dw * 4 + 16;
+    const size_t lds = (size_t)A.lds_dw * 4 + 16 + (2 * ED_QG_DW + 2 * ED_QG_BUCKETS) * 4;
     switch (band) {
         case 8: hipLaunchKernelGGL(k_ed_bv_query<8>, dim3(blocks), dim3(256), lds, st, A); break;
         case 16: hipLaunchKernelGGL(k_ed_bv_query<16>, dim3(blocks), dim3(256), lds, st, A); break;
@@ -560,7 +897,9 @@ int ed_bv_query_launch(const EdBvQueryArgs &A, uint32_t band, uint32_t blocks, h
 bool ed_bv_supported(uint32_t band) { return band == 8 || band == 16 || band == 32; }
 
 int ed_bv_launch(const EdBvArgs &A, uint32_t band, uint64_t blocks, hipStream_t st) {
-    const size_t lds = (size_t)A.lds_dw * 4 + 16;  // + pool counter
+    // + pool counters, query q-gram profiles, the pool's survivor list (u16, 14-bit pool index)
+    if (A.pool > (1u << 14)) return fail(NMZ_EINVAL, "internal: bit-parallel pool above 16384 candidates");
+    const size_t lds = (size_t)A.lds_dw * 4 + 16 + 2 * ED_QG_DW * 4 + ((size_t)A.pool * 2 + 15) / 16 * 16;
     switch (band) {
         case 8: hipLaunchKernelGGL(k_ed_bv<8>, dim3((unsigned)blocks), dim3(256), lds, st, A); break;
         case 16: hipLaunchKernelGGL(k_ed_bv<16>, dim3((unsigned)blocks), dim3(256), lds, st, A); break;

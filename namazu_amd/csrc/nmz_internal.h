@@ -36,6 +36,7 @@ struct EdBvArgs {
                                   // cr = ((shard - b) mod n_shards) + n_shards * t, t = 0, 1, ...)
     uint64_t *knn;                // [N][k]
     uint64_t *counters;           // [ED_BV_NCOUNTERS] work counters (nmz_ed_plan_counters), or nullptr
+    const uint4 *prof;            // [N][ED_QG_DW / 4] q-gram profiles (ed_qgram_profiles), or nullptr: no filter
     uint64_t n_chunks;            // chunks of this shard
     uint32_t N, G, k, lds_dw, shard, n_shards, pool;
     uint32_t rq;                  // queries per block row (64 x ED_BV_ROW_WAVES64); rq / 2 workgroups share a chunk
@@ -46,8 +47,36 @@ struct EdBvArgs {
 constexpr uint32_t ED_BV_RW = 5;
 // k_ed_bv work counters, summed over the launch:
 //   0 pairs that ran the DP, 1 pairs with a result <= w (in band), 2 lane-candidate 32-column blocks executed,
-//   3 candidates that ran the DP, 4 live query-blocks (blocks x queries of that lane still running)
-constexpr int ED_BV_NCOUNTERS = 5;
+//   3 candidates that ran the DP, 4 live query-blocks (blocks x queries of that lane still running),
+//   5 pairs inside the length band settled at w + 1 by the q-gram bound (no DP)
+constexpr int ED_BV_NCOUNTERS = 6;
+// q-gram (bigram) profiles: per trace, ED_QG_BUCKETS counts of hashed adjacent symbol pairs, saturated at 255 and
+// packed 4 per dword. One edit changes at most 4 bigram counts by one, so ED >= L1(profile_a, profile_b) / 4
+// (merging bigrams into buckets and saturating only lower the L1); L1 > 4w settles ED_w = w + 1 without a DP.
+constexpr uint32_t ED_QG_BUCKETS = 128, ED_QG_DW = ED_QG_BUCKETS / 4;
+int ed_qgram_profiles(const uint16_t *bs, const uint64_t *soff, const uint32_t *len, uint32_t N, uint32_t *prof,
+                      hipStream_t st);
+// Two-phase bit-parallel search (ed_bv.hip), used when the q-gram filter is on:
+//   1. k_ed_qg_filter over tiles of 64 queries x 256 candidates (a candidate's profile in registers against 64
+//      query profiles in LDS) decides every pair's length band and q-gram bound; a count pass sizes, and a write
+//      pass fills, per query pair (2p, 2p + 1) a list of entries j | run1 << 30 | run2 << 31 (pairs needing a DP);
+//   2. k_ed_bv_dp runs work items of <= ED_BV_ITEM entries of one query pair each (its Peq tables in LDS).
+constexpr uint32_t ED_BV_ITEM = 4096;
+struct EdQgArgs {
+    const uint4 *prof;           // [N][ED_QG_DW / 4] q-gram profiles
+    const uint32_t *len;         // [N]
+    uint64_t *knn;               // [N][k]: in-band results decided here (an empty trace in the length band)
+    uint64_t *counters;          // [ED_BV_NCOUNTERS] or nullptr (count pass only)
+    const uint64_t *tile_start;  // [QB+1] this shard's first tile of each 64-query block
+    uint32_t *cnt;               // count pass: [n_pairs] entries per query pair
+    uint32_t *cur;               // write pass: [n_pairs] cursors, starting at the pairs' entry offsets
+    uint32_t *ent;               // write pass: the entries
+    uint64_t n_tiles;
+    uint32_t N, k, QB, NCB, shard, n_shards;
+};
+int ed_qg_filter_launch(const EdQgArgs &A, uint32_t band, bool count, hipStream_t st);
+int ed_bv_dp_launch(const EdBvArgs &A, const uint32_t *ioff, const uint32_t *poff, const uint32_t *ent,
+                    uint32_t n_pairs, uint32_t n_items, uint32_t band, hipStream_t st);
 // single-query search on a bit-parallel plan (ed_bv.hip k_ed_bv_query): 1-2 external queries vs every stored trace
 struct EdBvQueryArgs {
     const uint16_t *bsym;  // the plan's stored streams
@@ -57,6 +86,7 @@ struct EdBvQueryArgs {
     uint64_t qoff[2];
     uint32_t nq[2];
     uint64_t *knn;         // [n_queries][k]
+    const uint4 *prof;     // the stored traces' q-gram profiles, or nullptr: no filter
     uint32_t N, k, lds_dw, pool, n_queries;
 };
 int ed_bv_query_launch(const EdBvQueryArgs &A, uint32_t band, uint32_t blocks, hipStream_t st);

@@ -4,9 +4,12 @@ Seed sweeps shard by contiguous seed range with no data-path collective; the
 only exchange is the failure-candidate merge: each rank's top-k (k x 24 B) is
 all_gathered (RCCL over xGMI with backend "nccl", gloo on CPU) and merged
 deterministically by (n_fault desc, sum_delay desc, seed asc). The all-pairs
-search deals 32-wave tile groups round-robin over ranks (equal cells per
-group) and all_gathers the partial k-NN key lists (N x k x 8 B) for a per-trace
-merge (nmz_knn_merge_dev on the GPU, merge_knn_keys on the host).
+search deals its work chunks round-robin over ranks and
+all_gathers the partial k-NN key lists (N x k x 8 B) for a per-trace merge
+(nmz_knn_merge_dev on the GPU, merge_knn_keys on the host). On a bit-parallel
+plan a shard lists only its pairs within the band; the merged lists are then
+completed with (band + 1, smallest unlisted ids) (nmz_ed_knn_fill_dev on the
+GPU, fill_knn_keys on the host).
 """
 import ctypes
 
@@ -35,6 +38,24 @@ def merge_knn_keys(parts, k):
     p = np.asarray(parts, np.uint64)
     allk = np.concatenate(list(p), axis=1)
     return np.sort(allk, axis=1)[:, :k]
+
+
+def fill_knn_keys(keys, n_cand, fill_d, self_exclude=True):
+    """Host restatement of nmz_ed_knn_fill_dev (csrc/ed.hip k_knn_fill): keep each list's keys with distance
+    < fill_d, then append (fill_d, j) for the smallest ids j < n_cand not listed (j != i), up to k keys."""
+    keys = np.array(keys, np.uint64, copy=True)
+    none = np.iinfo(np.uint64).max
+    for i, row in enumerate(keys):
+        kept = [int(x) for x in row if x != none and (int(x) >> 32) < fill_d]
+        listed = {x & 0xFFFFFFFF for x in kept}
+        out, j = list(kept), 0
+        while len(out) < len(row):
+            while j < n_cand and ((self_exclude and j == i) or j in listed):
+                j += 1
+            out.append((fill_d << 32) | j if j < n_cand else none)
+            j += 1
+        keys[i] = np.array(out, np.uint64)
+    return keys
 
 
 def all_gather_bytes(dist, tensor):

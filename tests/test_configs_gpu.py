@@ -133,7 +133,8 @@ def test_config2_allpairs_search_clustered_families(ctx):
     dfam = O.ed_pairs(ts.off, ts.sym, fam, w, nthreads=16)
     in_band = int((dfam <= w).sum())
     assert in_band > 0.95 * len(fam)
-    assert cnt[0] <= N * (N - 1) // 2 and cnt[1] >= 16 * in_band * 0.9
+    assert cnt[0] + cnt[5] == N * (N - 1) // 2 and cnt[1] >= 16 * in_band * 0.9
+    assert cnt[5] > 0.9 * (N * (N - 1) // 2 - 16 * (256 * 255 // 2))  # the q-gram bound settles most cross-family pairs
     assert cnt[1] <= 16 * (256 * 255 // 2) + (N * (N - 1) // 2 - 16 * (256 * 255 // 2)) // 1000
 
 
@@ -145,7 +146,10 @@ def test_config2_allpairs_search_survey_generator(ctx):
     for q in [0, 1, 777, 2047]:
         od, oi, _ = _brute_knn(ts, q, 32, 8)
         assert ds[q].tolist() == od and ids[q].tolist() == oi
-    assert cnt[0] == 2048 * 2047 // 2  # equal lengths: every pair runs the DP
+    # equal lengths: every pair is in the length band and either runs the DP or is settled by the q-gram bound;
+    # the survey's independent transpositions put nearly every pair's bigram profiles > 4w apart
+    assert cnt[0] + cnt[5] == 2048 * 2047 // 2
+    assert cnt[5] > 0.9 * (2048 * 2047 // 2)
 
 
 def test_config3_random_fault_sweep_10M_sharded_topk(ctx):

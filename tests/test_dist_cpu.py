@@ -48,14 +48,18 @@ def _worker(rank, world, port, q):
         mine = pairs[rank::world]
         d = O.ed_pairs(off, sym, mine, w)
         keys = np.full((N, k), np.iinfo(np.uint64).max, np.uint64)
+        # as a bit-parallel shard lists them: in-band results only; the merge is completed by fill_knn_keys
         for (i, j), dd in zip(mine, d):
+            if dd > w:
+                continue
             for a, b in ((i, j), (j, i)):
                 row = np.append(keys[a], np.uint64((int(dd) << 32) | int(b)))
                 keys[a] = np.sort(row)[:k]
         import torch
         t = torch.from_numpy(keys.view(np.uint8).reshape(-1).copy())
         parts = nd.all_gather_bytes(dist, t)
-        merged_knn = nd.merge_knn_keys([pp.numpy().view(np.uint64).reshape(N, k) for pp in parts], k)
+        merged_knn = nd.fill_knn_keys(nd.merge_knn_keys([pp.numpy().view(np.uint64).reshape(N, k) for pp in parts], k),
+                                      N, w + 1)
         q.put((rank, merged.tobytes(), merged_knn.tobytes()))
     finally:
         dist.destroy_process_group()

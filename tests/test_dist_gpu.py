@@ -63,6 +63,7 @@ def _worker(rank, world, port, q):
         out = torch.empty(N * k, dtype=torch.int64, device="cuda")
         _lib.check(L.nmz_knn_merge_dev(ctx.handle, ctypes.c_void_p(d_parts.data_ptr()), world, N, k,
                                        ctypes.c_void_p(out.data_ptr()), stream))
+        _lib.check(L.nmz_ed_knn_fill_dev(plan, k, ctypes.c_void_p(out.data_ptr()), stream))
         torch.cuda.synchronize()
         L.nmz_ed_plan_destroy(plan)
         q.put((rank, merged.tobytes(), out.cpu().numpy().tobytes()))

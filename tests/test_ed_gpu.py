@@ -243,7 +243,8 @@ def test_knn_wide_etcd_shape(ctx):
 ])
 def test_knn_shards_merge_to_full(ctx, w, alphabet, lmin, lmax, n, kind):
     """The multi-GPU path on one device: shard s of 3 into separate partial lists,
-    merged by nmz_knn_merge_dev, equals the oracle's all-pairs k-NN."""
+    merged by nmz_knn_merge_dev and completed by nmz_ed_knn_fill_dev, equals the oracle's all-pairs k-NN
+    (the bit-parallel shards list in-band pairs only; the fill leaves the other kernels' complete lists as they are)."""
     import torch
     L = _lib.load()
     ts = make_traces(n, lmin, lmax, 0.05, alphabet=alphabet, rng=np.random.default_rng(w + n))
@@ -259,6 +260,7 @@ def test_knn_shards_merge_to_full(ctx, w, alphabet, lmin, lmax, n, kind):
                                                    stream))
     _lib.check(L.nmz_knn_merge_dev(ctx.handle, ctypes.c_void_p(parts.data_ptr()), S, n, k,
                                    ctypes.c_void_p(out.data_ptr()), stream))
+    _lib.check(L.nmz_ed_knn_fill_dev(plan, k, ctypes.c_void_p(out.data_ptr()), stream))
     torch.cuda.synchronize()
     L.nmz_ed_plan_destroy(plan)
     keys = out.cpu().numpy().view(np.uint64).reshape(n, k)
@@ -339,3 +341,70 @@ def test_device_and_host_plan_builds_agree(ctx, monkeypatch):
         d = O.ed_pairs(ts.off, ts.sym, pairs, 32, nthreads=16)
         order = np.lexsort((pairs[:, 1], d))[:5]
         assert ds_d[q].tolist() == d[order].tolist() and ids_d[q].tolist() == pairs[order, 1].tolist()
+
+
+def _edited_family(n, length, alphabet, max_edits, rng):
+    """Traces = one base with 0..max_edits random edits each (adjacent transpositions, substitutions,
+    insertions, deletions), so pair distances spread across the band edge and the q-gram bound's edge."""
+    base = rng.integers(0, alphabet, size=length)
+    out = []
+    for _ in range(n):
+        t = list(base)
+        for _ in range(int(rng.integers(0, max_edits + 1))):
+            op, p = int(rng.integers(0, 4)), int(rng.integers(0, max(len(t) - 1, 1)))
+            if op == 0 and len(t) > 1:
+                t[p], t[p + 1] = t[p + 1], t[p]
+            elif op == 1:
+                t[p] = int(rng.integers(0, alphabet))
+            elif op == 2:
+                t.insert(p, int(rng.integers(0, alphabet)))
+            elif len(t) > 1:
+                del t[p]
+        out.append(np.array(t, np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(11))
+    return hs.TraceSet(out)
+
+
+@pytest.mark.parametrize("w,alphabet,max_edits", [(32, 48, 90), (16, 6, 40), (8, 200, 25)])
+def test_knn_qgram_filter_exact(ctx, monkeypatch, w, alphabet, max_edits):
+    """The q-gram lower bound (bigram profiles > 4w apart => ED_w = w + 1 without a DP) and the in-band-only
+    publishing + k_knn_fill: the all-pairs k-NN equals the oracle's and the run with the filter off, the counters
+    show pairs settled by the bound and pairs that ran the DP, and the shard path (merge + fill) agrees too."""
+    import torch
+    L = _lib.load()
+    rng = np.random.default_rng(w * 1000 + alphabet)
+    ts = _edited_family(400, 300, alphabet, max_edits, rng)
+    n, k = len(ts), 8
+    plan = ctypes.c_void_p()
+    _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), n, w, ctypes.byref(plan)))
+    assert L.nmz_ed_plan_is_fast(plan) == 2
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def run(qgram):
+        monkeypatch.setenv("NMZ_ED_QGRAM", "1" if qgram else "0")
+        d = torch.empty(n * k, dtype=torch.int64, device="cuda")
+        _lib.check(L.nmz_ed_allpairs_knn_dev(plan, k, ctypes.c_void_p(d.data_ptr()), stream))
+        cnt = np.zeros(_lib.NMZ_ED_NCOUNTERS, np.uint64)
+        _lib.check(L.nmz_ed_plan_counters(plan, _lib.ptr(cnt), stream))
+        return d.cpu().numpy().view(np.uint64).reshape(n, k), cnt
+
+    on, c_on = run(True)
+    off, c_off = run(False)
+    S = 3
+    parts = torch.empty(S * n * k, dtype=torch.int64, device="cuda")
+    out = torch.empty(n * k, dtype=torch.int64, device="cuda")
+    monkeypatch.setenv("NMZ_ED_QGRAM", "1")
+    for s in range(S):
+        _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, s, S, ctypes.c_void_p(parts.data_ptr() + s * n * k * 8),
+                                                   stream))
+    _lib.check(L.nmz_knn_merge_dev(ctx.handle, ctypes.c_void_p(parts.data_ptr()), S, n, k,
+                                   ctypes.c_void_p(out.data_ptr()), stream))
+    _lib.check(L.nmz_ed_knn_fill_dev(plan, k, ctypes.c_void_p(out.data_ptr()), stream))
+    torch.cuda.synchronize()  # the default torch stream is NULL here: the calls ran on the context's stream
+    sharded = out.cpu().numpy().view(np.uint64).reshape(n, k)
+    L.nmz_ed_plan_destroy(plan)
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, w, k, nthreads=16)
+    ref = (od.astype(np.uint64) << np.uint64(32)) | oi.astype(np.uint64)
+    assert np.array_equal(on, ref) and np.array_equal(off, ref) and np.array_equal(sharded, ref)
+    assert c_on[5] > 0 and c_on[0] > 0 and c_off[5] == 0
+    assert c_on[1] == c_off[1]  # the same in-band pairs
+    assert c_on[0] + c_on[5] == c_off[0]  # every pair the bound settles would have run the DP
