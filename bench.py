@@ -564,6 +564,10 @@ def bench_ed_secondary(args, torch, D, ctx, L, stream, spec):
     _lib.check(L.nmz_timing_enable(ctx.handle, 1))
     tot, cnt = ctypes.c_double(), ctypes.c_uint64()
     L.nmz_timing_read(ctx.handle, tname, ctypes.byref(tot), ctypes.byref(cnt), 1)
+    # the two-phase bit-parallel search's kernels (csrc/ed.hip ed_bv_two_phase): filter passes and DP work items
+    phase_t = {n: (ctypes.c_double(), ctypes.c_uint64()) for n in (b"ed_qg_filter", b"ed_bv_dp")}
+    for n, (a, b) in phase_t.items():
+        L.nmz_timing_read(ctx.handle, n, ctypes.byref(a), ctypes.byref(b), 1)
     steps = spec["steps"]
     D.barrier()
     torch.cuda.synchronize()
@@ -574,6 +578,9 @@ def bench_ed_secondary(args, torch, D, ctx, L, stream, spec):
     D.barrier()
     el = D.max(torch, time.perf_counter() - t0)
     _lib.check(L.nmz_timing_read(ctx.handle, tname, ctypes.byref(tot), ctypes.byref(cnt), 1))
+    for n, (a, b) in phase_t.items():
+        _lib.check(L.nmz_timing_read(ctx.handle, n, ctypes.byref(a), ctypes.byref(b), 1))
+    phase_ms = {n.decode(): a.value / steps for n, (a, b) in phase_t.items() if b.value}  # per search
     _lib.check(L.nmz_timing_enable(ctx.handle, 0))
     counters = np.zeros(_lib.NMZ_ED_NCOUNTERS, np.uint64)
     _lib.check(L.nmz_ed_plan_counters(plan, _lib.ptr(counters), stream))
@@ -618,6 +625,17 @@ def bench_ed_secondary(args, torch, D, ctx, L, stream, spec):
                nominal_band_cells_per_s=pairs * cells_per_pair * steps / el)
     if single:
         out["single_query"] = single
+    if phase_ms:
+        # two-phase search: the roofline belongs to the dominant kernel -- the DP over the pairs the filter kept
+        # (unit: DP pair, counted by the kernel) or, when nearly every pair is settled by the filter, the filter
+        # passes (unit: pair; both passes per search)
+        dp_ms, f_ms = phase_ms.get("ed_bv_dp", 0.0), phase_ms.get("ed_qg_filter", 0.0)
+        gen = spec.get("valu_key", kind).split(":")[-1]
+        out["phases_ms"] = {"filter_count_plus_write": f_ms, "dp": dp_ms, "rest": kern_ms - f_ms - dp_ms}
+        if dp_ms >= f_ms and counters[0]:
+            out["roofline"] = roofline_valu(f"k_ed_bv_dp:{gen}", int(counters[0]), dp_ms)
+        else:
+            out["roofline"] = roofline_valu(f"k_ed_qg_filter:{gen}", (pairs + D.world - 1) // D.world, f_ms)
     if counters[3]:  # k_ed_bv work counters of the last step (this rank's shard)
         c = [int(x) for x in counters]
         shard_pairs = (pairs + D.world - 1) // D.world

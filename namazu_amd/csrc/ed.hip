@@ -500,10 +500,10 @@ static int ed_plan_build_bv_device(nmz_ed_plan *p, const uint64_t *off, const ui
     for (uint32_t b = 0; b < G; ++b) p->row_chunks[b] = chunk_start[b + 1] - chunk_start[b];
     const uint64_t bs_n = soff[N] + 64;
     NMZ_TRY(p->mem.ensure(Carve::bytes_for(bs_n, 2) + Carve::bytes_for(N + 1, 8) * 2 + Carve::bytes_for(G + 1, 8) +
-                          Carve::bytes_for(N + 1, 4) + Carve::bytes_for(ED_BV_NCOUNTERS, 8) +
+                          Carve::bytes_for(N + 1, 4) + Carve::bytes_for(ED_CNT_WORDS, 8) +
                           Carve::bytes_for((uint64_t)N * ED_QG_DW, 4)));
     Carve cv(p->mem.ptr);
-    p->d_counters = cv.take<uint64_t>(ED_BV_NCOUNTERS);
+    p->d_counters = cv.take<uint64_t>(ED_CNT_WORDS);
     p->d_prof = cv.take<uint32_t>((uint64_t)N * ED_QG_DW);
     p->d_bsym = cv.take<uint16_t>(bs_n);
     p->d_soff = cv.take<uint64_t>(N + 1);
@@ -515,7 +515,7 @@ static int ed_plan_build_bv_device(nmz_ed_plan *p, const uint64_t *off, const ui
     NMZ_HIP(hipMemcpyAsync(p->d_qoff, off, (N + 1) * 8, hipMemcpyHostToDevice, st));
     NMZ_HIP(hipMemcpyAsync(p->d_chunk_start, chunk_start.data(), (G + 1) * 8, hipMemcpyHostToDevice, st));
     NMZ_HIP(hipMemcpyAsync(p->d_len, len.data(), (N + 1) * 4, hipMemcpyHostToDevice, st));
-    NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_BV_NCOUNTERS * 8, st));
+    NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_CNT_WORDS * 8, st));
     hipLaunchKernelGGL(k_ed_bv_remap, dim3(N), dim3(256), 0, st, d_off, d_sym, d_uniq, n_sym, p->d_soff, ndw * 8,
                        p->d_bsym);
     NMZ_HIP(hipGetLastError());
@@ -678,11 +678,11 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
             for (uint32_t t = 0; t < len[i]; ++t) bs[soff[i] + t] = (uint16_t)(ids[off[i] + t] * ndw * 8);
         size_t need = Carve::bytes_for(bs.size(), 2) + Carve::bytes_for(N + 1, 8) * 2 +
                       Carve::bytes_for(G + 1, 8) + Carve::bytes_for(N + 1, 4) +
-                      Carve::bytes_for(ED_BV_NCOUNTERS, 8) + Carve::bytes_for((uint64_t)N * ED_QG_DW, 4);
+                      Carve::bytes_for(ED_CNT_WORDS, 8) + Carve::bytes_for((uint64_t)N * ED_QG_DW, 4);
         int rc = p->mem.ensure(need);
         if (rc != NMZ_OK) return cleanup(rc);
         Carve cv(p->mem.ptr);
-        p->d_counters = cv.take<uint64_t>(ED_BV_NCOUNTERS);
+        p->d_counters = cv.take<uint64_t>(ED_CNT_WORDS);
         p->d_prof = cv.take<uint32_t>((uint64_t)N * ED_QG_DW);
         p->d_bsym = cv.take<uint16_t>(bs.size());
         p->d_soff = cv.take<uint64_t>(N + 1);
@@ -694,7 +694,7 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
             hipMemcpyAsync(p->d_qoff, off, (N + 1) * 8, hipMemcpyHostToDevice, st) ||
             hipMemcpyAsync(p->d_chunk_start, chunk_start.data(), (G + 1) * 8, hipMemcpyHostToDevice, st) ||
             hipMemcpyAsync(p->d_len, len.data(), (N + 1) * 4, hipMemcpyHostToDevice, st) ||
-            hipMemsetAsync(p->d_counters, 0, ED_BV_NCOUNTERS * 8, st))
+            hipMemsetAsync(p->d_counters, 0, ED_CNT_WORDS * 8, st))
             return cleanup(fail(NMZ_EHIP, "ED plan upload failed"));
         rc = ed_qgram_profiles(p->d_bsym, p->d_soff, p->d_len, N, p->d_prof, st);
         if (rc != NMZ_OK) return cleanup(rc);
@@ -868,7 +868,7 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
         A.pool = p->pool;
         A.shard = shard;
         A.n_shards = n_shards;
-        NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_BV_NCOUNTERS * 8, st));
+        NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_CNT_WORDS * 8, st));
         int rc = 1;
         if (A.prof && ed_two_phase_enabled()) {  // filter tiles + DP work items (the search's "ed_bv" time)
             KernelTimer kt(p->ctx, st, "ed_bv");
@@ -892,7 +892,7 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
                 uint64_t blocks = A.n_chunks * (p->rq / 2);
                 blocks = (blocks + 7) / 8 * 8;
                 NMZ_CHECK(blocks < (1ULL << 31), "too many traces for one launch");
-                NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_BV_NCOUNTERS * 8, st));
+                NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_CNT_WORDS * 8, st));
                 KernelTimer kt(p->ctx, st, "ed_bv");
                 NMZ_TRY(ed_bv_launch(A, p->band, blocks, st));
             }
@@ -995,8 +995,11 @@ int nmz_ed_plan_counters(nmz_ed_plan *plan, uint64_t *out, void *stream) {
     static_assert(ED_BV_NCOUNTERS == NMZ_ED_NCOUNTERS, "counter layout");
     CtxGuard g(plan->ctx);
     hipStream_t st = stream ? (hipStream_t)stream : plan->ctx->stream;
-    NMZ_HIP(hipMemcpyAsync(out, plan->d_counters, ED_BV_NCOUNTERS * 8, hipMemcpyDeviceToHost, st));
+    std::vector<uint64_t> lines(ED_CNT_WORDS);
+    NMZ_HIP(hipMemcpyAsync(lines.data(), plan->d_counters, ED_CNT_WORDS * 8, hipMemcpyDeviceToHost, st));
     NMZ_HIP(hipStreamSynchronize(st));
+    for (uint32_t sidx = 0; sidx < ED_CNT_STRIPES; ++sidx)
+        for (int i = 0; i < ED_BV_NCOUNTERS; ++i) out[i] += lines[sidx * ED_CNT_LINE + i];
     return NMZ_OK;
 }
 

@@ -331,7 +331,7 @@ __device__ __forceinline__ void qg_l1x2(const uint4 *__restrict__ cp, const uint
 #define NMZ_ED_BV_ATTR
 #endif
 
-// wave-reduce the work counters and add them to counters[] (nmz_ed_plan_counters), if counting
+// wave-reduce the work counters and add them to this workgroup's stripe of counters[] (nmz_ed_plan_counters)
 __device__ __forceinline__ void bv_flush_counters(uint64_t *counters, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                                   uint32_t c4, uint32_t c5) {
     if (!counters) return;
@@ -342,9 +342,10 @@ __device__ __forceinline__ void bv_flush_counters(uint64_t *counters, uint32_t c
         for (int off = 32; off >= 1; off >>= 1) c[i] += __shfl_xor(c[i], off, 64);
     }
     if ((threadIdx.x & 63) == 0) {
+        uint64_t *line = counters + (blockIdx.x % ED_CNT_STRIPES) * ED_CNT_LINE;
 #pragma unroll
         for (int i = 0; i < ED_BV_NCOUNTERS; ++i)
-            if (c[i]) atomicAdd((unsigned long long *)&counters[i], (unsigned long long)c[i]);
+            if (c[i]) atomicAdd((unsigned long long *)&line[i], (unsigned long long)c[i]);
     }
 }
 

@@ -50,6 +50,10 @@ constexpr uint32_t ED_BV_RW = 5;
 //   3 candidates that ran the DP, 4 live query-blocks (blocks x queries of that lane still running),
 //   5 pairs inside the length band settled at w + 1 by the q-gram bound (no DP)
 constexpr int ED_BV_NCOUNTERS = 6;
+// the counters live in ED_CNT_STRIPES stripes of 16 u64 (one 128-byte line each); a wave adds to stripe
+// (blockIdx mod ED_CNT_STRIPES) and nmz_ed_plan_counters sums the stripes (one address for the whole grid
+// serialised ~10^6 same-address atomics: 10 ms of a 16 ms filter pass)
+constexpr uint32_t ED_CNT_STRIPES = 64, ED_CNT_LINE = 16, ED_CNT_WORDS = ED_CNT_STRIPES * ED_CNT_LINE;
 // q-gram (bigram) profiles: per trace, ED_QG_BUCKETS counts of hashed adjacent symbol pairs, saturated at 255 and
 // packed 4 per dword. One edit changes at most 4 bigram counts by one, so ED >= L1(profile_a, profile_b) / 4
 // (merging bigrams into buckets and saturating only lower the L1); L1 > 4w settles ED_w = w + 1 without a DP.

@@ -16,8 +16,12 @@ import sys
 LEGS = {
     "replayable": [("void nmz::k_replayable_sweep_fast", "k_replayable_sweep_fast", "decision", 2**20 * 4096)],
     "random": [("void nmz::k_random_sweep", "k_random_sweep", "decision", 10_000_000 * 10_000)],
-    "ed_clustered": [("void nmz::k_ed_bv<32>", "k_ed_bv:clustered", "pair", 100_000 * 99_999 // 2)],
-    "ed_survey": [("void nmz::k_ed_bv<32>", "k_ed_bv:survey", "pair", 100_000 * 99_999 // 2)],
+    # two-phase search: the DP kernel per pair that ran the DP (the k_ed_bv counters of the bench workload:
+    # 51,032,886 clustered, 306,187 survey), the filter passes (count + write, one key) per pair of the search
+    "ed_clustered": [("void nmz::k_ed_bv_dp<32>", "k_ed_bv_dp:clustered", "DP pair", 51_032_886),
+                     ("void nmz::k_ed_qg_filter<32", "k_ed_qg_filter:clustered", "pair", 100_000 * 99_999 // 2)],
+    "ed_survey": [("void nmz::k_ed_bv_dp<32>", "k_ed_bv_dp:survey", "DP pair", 306_187),
+                  ("void nmz::k_ed_qg_filter<32", "k_ed_qg_filter:survey", "pair", 100_000 * 99_999 // 2)],
     "ed_wide": [("void nmz::k_ed_wide<4>", "k_ed_wide", "pair", 256 * 255 // 2)],
     # one launch per mode per step (PO first, then exact): the profile's average mixes both modes, so the
     # per-mode figures come from the two kernel instantiations
@@ -35,9 +39,19 @@ def main():
         if not os.path.exists(f):
             continue
         summ = json.load(open(f))
+        seen = set()
         for name, e in summ.items():
             for pre, key, unit, n in kernels:
                 if name.startswith(pre) and "SQ_INSTS_VALU" in e:
+                    if key in seen:  # several kernels under one key (the filter's count and write passes): sum
+                        o = out[key]
+                        o["ops_per_unit"] += e["SQ_INSTS_VALU"] * 64 / n
+                        o["avg_ns"] += e["avg_ns"]
+                        o["kernel"] += " + " + name
+                        if o.get("hbm_bytes_per_launch") is not None and e.get("hbm_bytes_fetch_x2") is not None:
+                            o["hbm_bytes_per_launch"] += e["hbm_bytes_fetch_x2"]
+                        continue
+                    seen.add(key)
                     out[key] = {"ops_per_unit": e["SQ_INSTS_VALU"] * 64 / n, "unit": unit, "units_per_launch": n,
                                 "kernel": name, "avg_ns": e["avg_ns"],
                                 "source": f"SQ_INSTS_VALU per launch, profiles/{tag}_{leg}_summary.json",
