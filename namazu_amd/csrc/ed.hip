@@ -393,7 +393,8 @@ struct nmz_ed_plan {
     std::unordered_map<uint64_t, uint32_t> dict;  // bv: symbol -> dense id (single-query search)
     nmz::DevBuf mem;
     // bv, two-phase search: per-(shard, n_shards) tile starts (host, kept), scratch and the entry lists
-    std::map<uint64_t, std::vector<uint64_t>> tile_start;
+    std::map<uint64_t, nmz::DevBuf> tile_list;      // per (shard, n_shards): the shard's tiles (qb << 32 | cb)
+    std::map<uint64_t, uint64_t> tile_count;
     nmz::DevBuf tp_mem, tp_ent;
     uint16_t *d_qsym = nullptr, *d_csym = nullptr;
     uint64_t *d_qoff = nullptr, *d_coff = nullptr;
@@ -761,25 +762,42 @@ __global__ void k_bv_items(const uint32_t *__restrict__ cnt, uint32_t n, uint32_
 // DP over the work items. Returns 1 when the entry lists would exceed ED_TP_MAX_ENTRIES (caller falls back to
 // the single-kernel search).
 constexpr uint64_t ED_TP_MAX_ENTRIES = 1ULL << 30;  // 4 GiB of entries
+
+// MurmurHash3's 64-bit finaliser (host): the shard of a filter tile
+static inline uint64_t tile_mix(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ULL;
+    return x ^ (x >> 33);
+}
 static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A) {
     const uint32_t N = p->n, n_pairs = (N + 1) / 2, QB = (N + 63) / 64, NCB = (N + 255) / 256;
     const uint32_t shard = A.shard, n_shards = A.n_shards;
     if (N >= (1u << 30)) return 1;  // entries carry j in 30 bits
-    std::vector<uint64_t> &ts = p->tile_start[((uint64_t)shard << 32) | n_shards];
-    if (ts.empty()) {
-        ts.assign(QB + 1, 0);
-        for (uint32_t qb = 0; qb < QB; ++qb) {
-            const uint64_t nt = NCB - qb / 4, rot = (shard + n_shards - qb % n_shards) % n_shards;
-            ts[qb + 1] = ts[qb] + (rot < nt ? (nt - rot + n_shards - 1) / n_shards : 0);
-        }
+    // this shard's tiles (qb << 32 | cb), built and uploaded once per (shard, n_shards): a tile belongs to shard
+    // tile_mix(qb << 32 | cb) mod n_shards. The DP work is data-dependent and clustered (the clustered workload's
+    // families put it in the few tiles next to the diagonal, with a period of 16 query blocks); a hash breaks
+    // that periodicity, where a round-robin deal aligned with it (8 shards: max/mean shard time 1.27)
+    const uint64_t key = ((uint64_t)shard << 32) | n_shards;
+    DevBuf &tl = p->tile_list[key];
+    if (!p->tile_count.count(key)) {
+        std::vector<uint64_t> tiles;
+        for (uint32_t qb = 0; qb < QB; ++qb)
+            for (uint32_t cb = qb / 4; cb < NCB; ++cb) {
+                const uint64_t id = ((uint64_t)qb << 32) | cb;
+                if (n_shards == 1 || tile_mix(id) % n_shards == shard) tiles.push_back(id);
+            }
+        NMZ_TRY(tl.ensure(Carve::bytes_for(tiles.size() + 1, 8)));
+        if (!tiles.empty()) NMZ_HIP(hipMemcpy(tl.ptr, tiles.data(), tiles.size() * 8, hipMemcpyHostToDevice));
+        p->tile_count[key] = tiles.size();
     }
     size_t scan_bytes = 0;
     NMZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
                                              (int)n_pairs + 1, st));
-    NMZ_TRY(p->tp_mem.ensure(Carve::bytes_for(QB + 1, 8) + 5 * Carve::bytes_for(n_pairs + 1, 4) +
-                             Carve::bytes_for(scan_bytes, 1) + Carve::bytes_for(4, 4)));
+    NMZ_TRY(p->tp_mem.ensure(5 * Carve::bytes_for(n_pairs + 1, 4) + Carve::bytes_for(scan_bytes, 1) +
+                             Carve::bytes_for(4, 4)));
     Carve cv(p->tp_mem.ptr);
-    uint64_t *d_ts = cv.take<uint64_t>(QB + 1);
     uint32_t *d_cnt = cv.take<uint32_t>(n_pairs + 1), *d_poff = cv.take<uint32_t>(n_pairs + 1);
     uint32_t *d_items = cv.take<uint32_t>(n_pairs + 1), *d_ioff = cv.take<uint32_t>(n_pairs + 1);
     uint32_t *d_cur = cv.take<uint32_t>(n_pairs + 1);
@@ -789,18 +807,17 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A) {
     Q.len = A.len;
     Q.knn = A.knn;
     Q.counters = A.counters;
-    Q.tile_start = d_ts;
+    Q.tiles = tl.as<uint64_t>();
     Q.cnt = d_cnt;
     Q.cur = d_cur;
     Q.ent = nullptr;
-    Q.n_tiles = ts[QB];
+    Q.n_tiles = p->tile_count[key];
     Q.N = N;
     Q.k = A.k;
     Q.QB = QB;
     Q.NCB = NCB;
     Q.shard = shard;
     Q.n_shards = n_shards;
-    NMZ_HIP(hipMemcpyAsync(d_ts, ts.data(), (QB + 1) * 8, hipMemcpyHostToDevice, st));
     NMZ_HIP(hipMemsetAsync(d_cnt, 0, (n_pairs + 1) * 4, st));
     {
         KernelTimer kt(p->ctx, st, "ed_qg_filter");
@@ -978,6 +995,7 @@ int nmz_ed_plan_destroy(nmz_ed_plan *plan) {
         plan->mem.release();
         plan->tp_mem.release();
         plan->tp_ent.release();
+        for (auto &kv : plan->tile_list) kv.second.release();
     }
     delete plan;
     return NMZ_OK;
@@ -1149,6 +1167,7 @@ int nmz_ed_allpairs_knn(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, 
             p->mem.release();
             p->tp_mem.release();
             p->tp_ent.release();
+            for (auto &kv : p->tile_list) kv.second.release();
             delete p;
         }
     } pg{plan};

@@ -578,22 +578,16 @@ __device__ __forceinline__ uint32_t qg_l1_reg(const uint4 (&c)[ED_QG_DW / 4], co
     return s;
 }
 
-// One tile: queries [64 qb, 64 qb + 64) x candidates [256 cb, 256 cb + 256), pairs j > q only. Tiles of a query
-// block are dealt to shards round-robin starting at shard (qb mod n_shards), as k_ed_bv deals its chunks.
+// One tile: queries [64 qb, 64 qb + 64) x candidates [256 cb, 256 cb + 256), pairs j > q only (the shard's tile
+// list: csrc/ed.hip ed_bv_two_phase).
 template <int W, bool COUNT>
 __global__ __launch_bounds__(256) void k_ed_qg_filter(EdQgArgs A) {
     __shared__ uint4 qp[64][ED_QG_DW / 4];
     __shared__ uint32_t qlen[64];
     const uint64_t t = blockIdx.x;
     if (t >= A.n_tiles) return;
-    uint32_t lo = 0, hi = A.QB;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) / 2;
-        if (A.tile_start[mid] <= t) lo = mid; else hi = mid;
-    }
-    const uint32_t qb = lo;
-    const uint32_t rot = (A.shard + A.n_shards - qb % A.n_shards) % A.n_shards;
-    const uint32_t cb = qb / 4 + rot + A.n_shards * (uint32_t)(t - A.tile_start[qb]);
+    const uint64_t tq = A.tiles[t];
+    const uint32_t qb = (uint32_t)(tq >> 32), cb = (uint32_t)tq;
     for (uint32_t i = threadIdx.x; i < 64 * (ED_QG_DW / 4); i += 256) {
         const uint32_t q = 64 * qb + i / (ED_QG_DW / 4);
         qp[i / (ED_QG_DW / 4)][i % (ED_QG_DW / 4)] =

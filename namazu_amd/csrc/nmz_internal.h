@@ -71,7 +71,7 @@ struct EdQgArgs {
     const uint32_t *len;         // [N]
     uint64_t *knn;               // [N][k]: in-band results decided here (an empty trace in the length band)
     uint64_t *counters;          // [ED_BV_NCOUNTERS] or nullptr (count pass only)
-    const uint64_t *tile_start;  // [QB+1] this shard's first tile of each 64-query block
+    const uint64_t *tiles;       // [n_tiles] this shard's tiles, qb << 32 | cb
     uint32_t *cnt;               // count pass: [n_pairs] entries per query pair
     uint32_t *cur;               // write pass: [n_pairs] cursors, starting at the pairs' entry offsets
     uint32_t *ent;               // write pass: the entries
