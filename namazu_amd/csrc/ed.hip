@@ -395,7 +395,7 @@ struct nmz_ed_plan {
     // bv, two-phase search: per-(shard, n_shards) tile starts (host, kept), scratch and the entry lists
     std::map<uint64_t, nmz::DevBuf> tile_list;      // per (shard, n_shards): the shard's tiles (qb << 32 | cb)
     std::map<uint64_t, uint64_t> tile_count;
-    nmz::DevBuf tp_mem, tp_ent;
+    nmz::DevBuf tp_mem, tp_ent, tp_mask;
     uint16_t *d_qsym = nullptr, *d_csym = nullptr;
     uint64_t *d_qoff = nullptr, *d_coff = nullptr;
     uint32_t *d_gmax = nullptr, *d_len = nullptr;
@@ -762,6 +762,7 @@ __global__ void k_bv_items(const uint32_t *__restrict__ cnt, uint32_t n, uint32_
 // DP over the work items. Returns 1 when the entry lists would exceed ED_TP_MAX_ENTRIES (caller falls back to
 // the single-kernel search).
 constexpr uint64_t ED_TP_MAX_ENTRIES = 1ULL << 30;  // 4 GiB of entries
+constexpr uint64_t ED_TP_MAX_MASK_BYTES = 4ULL << 30;
 
 // MurmurHash3's 64-bit finaliser (host): the shard of a filter tile
 static inline uint64_t tile_mix(uint64_t x) {
@@ -812,6 +813,10 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A) {
     Q.cur = d_cur;
     Q.ent = nullptr;
     Q.n_tiles = p->tile_count[key];
+    // the count pass's survivor ballots (2 KiB per tile) let the write pass scatter without recomputing the filter
+    Q.masks = nullptr;
+    if (Q.n_tiles * 2048 <= ED_TP_MAX_MASK_BYTES && p->tp_mask.ensure(Carve::bytes_for(Q.n_tiles * 2048, 1)) == NMZ_OK)
+        Q.masks = p->tp_mask.as<uint64_t>();
     Q.N = N;
     Q.k = A.k;
     Q.QB = QB;
@@ -837,7 +842,8 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A) {
     NMZ_HIP(hipMemcpyAsync(d_cur, d_poff, (uint64_t)n_pairs * 4, hipMemcpyDeviceToDevice, st));
     {
         KernelTimer kt(p->ctx, st, "ed_qg_filter");
-        NMZ_TRY(ed_qg_filter_launch(Q, p->band, false, st));
+        if (Q.masks) NMZ_TRY(ed_qg_scatter_launch(Q, st));
+        else NMZ_TRY(ed_qg_filter_launch(Q, p->band, false, st));
     }
     KernelTimer kt(p->ctx, st, "ed_bv_dp");
     return ed_bv_dp_launch(A, d_ioff, d_poff, Q.ent, n_pairs, (uint32_t)n_items, p->band, st);
@@ -995,6 +1001,7 @@ int nmz_ed_plan_destroy(nmz_ed_plan *plan) {
         plan->mem.release();
         plan->tp_mem.release();
         plan->tp_ent.release();
+        plan->tp_mask.release();
         for (auto &kv : plan->tile_list) kv.second.release();
     }
     delete plan;
@@ -1167,6 +1174,7 @@ int nmz_ed_allpairs_knn(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, 
             p->mem.release();
             p->tp_mem.release();
             p->tp_ent.release();
+            p->tp_mask.release();
             for (auto &kv : p->tile_list) kv.second.release();
             delete p;
         }

@@ -35,6 +35,8 @@
 // (dense ids), 2 queries interleaved per dword ([symbol][dword][query]) so
 // one ds_read_b64 returns a dword of both queries.  Candidate symbols are
 // stored as that row's LDS byte offset (u16), one stream per trace.
+#include <type_traits>
+
 #include "nmz_common.h"
 #include "nmz_internal.h"
 
@@ -595,48 +597,59 @@ __global__ __launch_bounds__(256) void k_ed_qg_filter(EdQgArgs A) {
     }
     if (threadIdx.x < 64) qlen[threadIdx.x] = 64 * qb + threadIdx.x < A.N ? A.len[64 * qb + threadIdx.x] : 0u;
     __syncthreads();
-    const uint32_t j = 256 * cb + threadIdx.x, lane = threadIdx.x & 63;
+    const uint32_t j = 256 * cb + threadIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const bool jv = j < A.N;
     const uint32_t m = jv ? A.len[j] : 0u;
     uint4 cp[ED_QG_DW / 4];
 #pragma unroll
     for (int r = 0; r < (int)ED_QG_DW / 4; ++r)
         cp[r] = jv ? A.prof[(uint64_t)j * (ED_QG_DW / 4) + r] : make_uint4(0, 0, 0, 0);
+    // empty traces (n + m <= w results, listed here) are rare: a tile without one runs the loop without that path
+    const bool any_empty =
+        __syncthreads_or((jv && m == 0) || (threadIdx.x < 64 && 64 * qb + threadIdx.x < A.N && qlen[threadIdx.x] == 0));
     uint32_t c_qgram = 0, c_in_band = 0;
-    for (uint32_t pp = 0; pp < 32; ++pp) {
+    auto body = [&](uint32_t pp, auto empty_tag) {
+        constexpr bool EMPTY = decltype(empty_tag)::value;
         const uint32_t q1 = 64 * qb + 2 * pp, q2 = q1 + 1;
-        if (q1 >= A.N) break;
         const uint32_t n1 = qlen[2 * pp], n2 = qlen[2 * pp + 1];
         const int32_t dd1 = (int32_t)m - (int32_t)n1, dd2 = (int32_t)m - (int32_t)n2;
         bool a1 = jv && j > q1 && dd1 <= W && dd1 >= -W;
         bool a2 = jv && q2 < A.N && j > q2 && dd2 <= W && dd2 >= -W;
-        if (a1 && (n1 == 0 || m == 0)) {  // an empty trace: n + m <= w, listed once (count pass)
-            if (COUNT) {
-                const uint64_t r = n1 + m;
-                bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, (r << 32) | q1);
-                bv_knn_insert(A.knn + (uint64_t)q1 * A.k, A.k, (r << 32) | j);
-                c_in_band += 1;
+        if constexpr (EMPTY) {
+            if (a1 && (n1 == 0 || m == 0)) {  // an empty trace: n + m <= w, listed once (count pass)
+                if (COUNT) {
+                    const uint64_t r = n1 + m;
+                    bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, (r << 32) | q1);
+                    bv_knn_insert(A.knn + (uint64_t)q1 * A.k, A.k, (r << 32) | j);
+                    c_in_band += 1;
+                }
+                a1 = false;
             }
-            a1 = false;
-        }
-        if (a2 && (n2 == 0 || m == 0)) {
-            if (COUNT) {
-                const uint64_t r = n2 + m;
-                bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, (r << 32) | q2);
-                bv_knn_insert(A.knn + (uint64_t)q2 * A.k, A.k, (r << 32) | j);
-                c_in_band += 1;
+            if (a2 && (n2 == 0 || m == 0)) {
+                if (COUNT) {
+                    const uint64_t r = n2 + m;
+                    bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, (r << 32) | q2);
+                    bv_knn_insert(A.knn + (uint64_t)q2 * A.k, A.k, (r << 32) | j);
+                    c_in_band += 1;
+                }
+                a2 = false;
             }
-            a2 = false;
         }
-        if (a1 || a2) {  // q-gram bound: L1 > 4w => ED_w = w + 1, no DP
-            const bool f1 = a1 && qg_l1_reg(cp, qp[2 * pp]) > 4 * W;
-            const bool f2 = a2 && qg_l1_reg(cp, qp[2 * pp + 1]) > 4 * W;
-            c_qgram += (uint32_t)f1 + (uint32_t)f2;
-            a1 = a1 && !f1;
-            a2 = a2 && !f2;
-        }
+        // q-gram bound: L1 > 4w => ED_w = w + 1, no DP
+        const bool f1 = a1 && qg_l1_reg(cp, qp[2 * pp]) > 4 * W;
+        const bool f2 = a2 && qg_l1_reg(cp, qp[2 * pp + 1]) > 4 * W;
+        c_qgram += (uint32_t)f1 + (uint32_t)f2;
+        a1 = a1 && !f1;
+        a2 = a2 && !f2;
         const bool sv = a1 || a2;
         const uint64_t mask = __ballot(sv);
+        if (COUNT && A.masks) {  // the survivors for the scatter pass: two ballots per (wave, pair)
+            const uint64_t m1 = __ballot(a1), m2 = __ballot(a2);
+            if (lane == 0) {
+                ulonglong2 *mk = (ulonglong2 *)A.masks + ((uint64_t)t * 4 + wave) * 32 + pp;
+                *mk = make_ulonglong2(m1, m2);
+            }
+        }
         if (mask) {
             const uint32_t leader = (uint32_t)__ffsll((unsigned long long)mask) - 1;
             const uint32_t n = (uint32_t)__popcll(mask), p = q1 >> 1;
@@ -649,8 +662,46 @@ __global__ __launch_bounds__(256) void k_ed_qg_filter(EdQgArgs A) {
                         j | ((uint32_t)a1 << 30) | ((uint32_t)a2 << 31);
             }
         }
+    };
+    const uint32_t np = min(32u, (A.N - 64 * qb + 1) / 2);  // query pairs of this block
+    if (any_empty) {
+        for (uint32_t pp = 0; pp < np; ++pp) body(pp, std::true_type{});
+    } else {
+        for (uint32_t pp = 0; pp < np; ++pp) body(pp, std::false_type{});
     }
     if (COUNT) bv_flush_counters(A.counters, 0, c_in_band, 0, 0, 0, c_qgram);
+}
+
+// The write pass from the count pass's ballots (EdQgArgs::masks): per (wave, pair) with survivors, one cursor
+// atomic and the entries -- no profile loads, no L1s.
+__global__ __launch_bounds__(256) void k_ed_qg_scatter(EdQgArgs A) {
+    const uint64_t t = blockIdx.x;
+    if (t >= A.n_tiles) return;
+    const uint64_t tq = A.tiles[t];
+    const uint32_t qb = (uint32_t)(tq >> 32), cb = (uint32_t)tq;
+    const uint32_t j = 256 * cb + threadIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t np = min(32u, (A.N - 64 * qb + 1) / 2);
+    const ulonglong2 *mk = (const ulonglong2 *)A.masks + ((uint64_t)t * 4 + wave) * 32;
+    for (uint32_t pp = 0; pp < np; ++pp) {
+        const ulonglong2 mm = mk[pp];
+        const uint64_t mask = mm.x | mm.y;
+        if (!mask) continue;
+        const uint32_t p = (64 * qb + 2 * pp) >> 1;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&A.cur[p], (uint32_t)__popcll(mask));
+        base = __shfl(base, 0, 64);
+        const uint64_t bit = 1ull << lane;
+        if (mask & bit)
+            A.ent[base + __popcll(mask & (bit - 1))] =
+                j | ((uint32_t)((mm.x & bit) != 0) << 30) | ((uint32_t)((mm.y & bit) != 0) << 31);
+    }
+}
+
+int ed_qg_scatter_launch(const EdQgArgs &A, hipStream_t st) {
+    if (A.n_tiles == 0) return NMZ_OK;
+    hipLaunchKernelGGL(k_ed_qg_scatter, dim3((unsigned)A.n_tiles), dim3(256), 0, st, A);
+    NMZ_HIP(hipGetLastError());
+    return NMZ_OK;
 }
 
 int ed_qg_filter_launch(const EdQgArgs &A, uint32_t band, bool count, hipStream_t st) {

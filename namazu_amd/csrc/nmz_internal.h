@@ -75,10 +75,13 @@ struct EdQgArgs {
     uint32_t *cnt;               // count pass: [n_pairs] entries per query pair
     uint32_t *cur;               // write pass: [n_pairs] cursors, starting at the pairs' entry offsets
     uint32_t *ent;               // write pass: the entries
+    uint64_t *masks;             // count pass: [n_tiles][4 waves][32 pairs] 2 ballots (run1, run2) for the
+                                 // scatter pass, or nullptr (the write pass recomputes the filter)
     uint64_t n_tiles;
     uint32_t N, k, QB, NCB, shard, n_shards;
 };
 int ed_qg_filter_launch(const EdQgArgs &A, uint32_t band, bool count, hipStream_t st);
+int ed_qg_scatter_launch(const EdQgArgs &A, hipStream_t st);
 int ed_bv_dp_launch(const EdBvArgs &A, const uint32_t *ioff, const uint32_t *poff, const uint32_t *ent,
                     uint32_t n_pairs, uint32_t n_items, uint32_t band, hipStream_t st);
 // single-query search on a bit-parallel plan (ed_bv.hip k_ed_bv_query): 1-2 external queries vs every stored trace

@@ -12,7 +12,7 @@ f = glob.glob(sys.argv[1] + "/**/run_kernel_trace.csv", recursive=True)[0]
 d = collections.defaultdict(list)
 for r in csv.DictReader(open(f)):
     n = r["Kernel_Name"]
-    if any(k in n for k in ("qg_filter", "bv_dp", "k_ed_bv<", "qgram_profile")):
+    if any(k in n for k in ("qg_filter", "qg_scatter", "bv_dp", "k_ed_bv<", "qgram_profile")):
         d[n.split("(")[0]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 for n, v in d.items():
     print(sys.argv[1].split("/")[-1], n, ["%.0f us" % x for x in v])
