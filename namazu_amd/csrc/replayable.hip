@@ -55,6 +55,13 @@ struct nmz_replayable_plan {
     nmz::DevBuf partial;                // per-chunk partial (sum, key) per seed
     nmz::DevBuf topk_lists;             // top-k selection scratch (nmz_replayable_sweep_topk_dev)
     nmz::DevBuf plan_mem;
+    // order-query statistics (k_replayable_sweep_oq): per-row blobs staged whole into LDS
+    bool oq = false;
+    uint32_t oq_ep = 0, oq_rb16 = 0;    // E padded to a multiple of 8; blob bytes / 16 per row
+    uint4 *d_oq_blob = nullptr;         // [256][rb16] {cm[3][EP] u32, e[3][EP] u16, samp[NS] u64}
+    uint64_t *d_oq_rowsum = nullptr;    // [256] sum of C mod m over the row
+    uint32_t *d_oq_samp_off = nullptr;  // [n_classes] first sample of each class
+    nmz::DevBuf oq_mem;
 };
 
 namespace nmz {
@@ -588,6 +595,233 @@ __global__ __launch_bounds__(256) void k_replayable_merge(const uint4 *__restric
     if (merge_slot<U>(g, units, *n_units, sorted_idx, partial, part_stride, n_chunks, st, idx)) stats[idx] = st;
 }
 
+// ---------------------------------------------------------------------------
+// Order-query statistics (MOD_FAST): the per-seed sum, max and first argmax of
+// every decision of a (row L, class) segment without deciding event by event.
+//
+// Inside a segment (C-sorted) every decision is t = (base + Cm) mod m with
+// base = Hm on the carry-free prefix [0, d) and Hm2 on [d, n). For a set of
+// events with one base b:
+//   sum t = |set| b + sum Cm - m #{Cm >= m - b}       (each t wraps at most once)
+//   max t = b + max{Cm < m - b}   if that set is non-empty (those t lie in [b, m),
+//           b + max Cm - m        otherwise              the wrapped ones in [0, b))
+// so a block of events sorted by (Cm, e desc) answers both with one binary
+// search for m - b: the count gives the wraps, the entry just below gives the
+// maximum and its smallest e. The prefix/suffix split at d is covered by
+// aligned blocks of three levels (512, 64, 8 events; each block sorted within
+// itself), the 8-event block holding d is decided event by event (which also
+// counts d exactly). Per (seed, segment of n events): n/512 + 16 block searches
+// instead of n decisions. Segments of <= OQ_BRUTE events are decided event by
+// event with wave-uniform table reads. The sum over all segments needs only the
+// carry-free counts d and the wrap count W:
+//   sum = sum_segments (d Hm + (n - d) Hm2) + sum_row Cm - m W.
+// ---------------------------------------------------------------------------
+constexpr uint32_t OQ_S0 = 512, OQ_S1 = 64, OQ_S2 = 8;
+constexpr uint32_t OQ_BRUTE = 24;   // segments of at most this many events: per-event decisions
+constexpr uint32_t OQ_WG = 1024;    // seeds per workgroup (16 waves share one staged row)
+constexpr uint32_t OQ_LDS_MAX = 160 * 1024;
+
+// plan: one workgroup per (top block, row L): the top block's entries (C order) sorted by (Cm, ~e) with a
+// bitonic network whose runs all end ascending after every stage (the first step of stage k compares an
+// element with its mirror in the k-run), so the 8-, 64- and 512-runs are snapshots of the three levels.
+// Also writes the 8-event samples of C and adds the block's C mod m to the row sum.
+__global__ __launch_bounds__(256) void k_replayable_oq_levels(const uint4 *__restrict__ table, uint32_t E,
+                                                              const uint4 *__restrict__ tb_list, uint32_t EP,
+                                                              uint32_t rb16, uint4 *__restrict__ blob,
+                                                              unsigned long long *__restrict__ rowsum) {
+    __shared__ uint64_t key[OQ_S0];
+    __shared__ unsigned long long part[4];
+    const uint4 tb = tb_list[blockIdx.x];  // {segment start, block start in the segment, size, first sample}
+    const uint32_t L = blockIdx.y;
+    const uint4 *__restrict__ row = table + (uint64_t)L * E + tb.x + tb.y;
+    uint32_t *cm = reinterpret_cast<uint32_t *>(blob + (uint64_t)L * rb16);
+    uint16_t *ev = reinterpret_cast<uint16_t *>(cm + 3 * EP);
+    uint64_t *samp = reinterpret_cast<uint64_t *>(cm + 3 * EP + 3 * EP / 2);
+    uint64_t s = 0;
+    for (uint32_t i = threadIdx.x; i < OQ_S0; i += 256) {
+        if (i < tb.z) {
+            const uint4 q = row[i];
+            key[i] = ((uint64_t)q.z << 32) | q.w;
+            s += q.z;
+            if ((i & 7) == 0) samp[tb.w + (tb.y + i) / 8] = ((uint64_t)q.y << 32) | q.x;
+        } else {
+            key[i] = UINT64_MAX;
+        }
+    }
+    for (int o = 32; o; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(rowsum + L, part[0] + part[1] + part[2] + part[3]);
+    const uint32_t p = threadIdx.x;  // one compare-exchange pair per thread
+    for (uint32_t k = 2; k <= OQ_S0; k <<= 1) {
+        for (uint32_t j = k >> 1; j; j >>= 1) {
+            uint32_t i, l;
+            if (j == k >> 1) {  // mirror step
+                i = (p / j) * k + (p % j);
+                l = (p / j) * k + (k - 1 - (p % j));
+            } else {
+                i = (p / j) * 2 * j + (p % j);
+                l = i + j;
+            }
+            const uint64_t a = key[i], b = key[l];
+            if (a > b) {
+                key[i] = b;
+                key[l] = a;
+            }
+            __syncthreads();
+        }
+        const int lv = k == OQ_S2 ? 2 : k == OQ_S1 ? 1 : k == OQ_S0 ? 0 : -1;
+        if (lv >= 0) {
+            for (uint32_t i = threadIdx.x; i < tb.z; i += 256) {
+                const uint64_t q = key[i];
+                cm[lv * EP + tb.x + tb.y + i] = (uint32_t)(q >> 32);
+                ev[lv * EP + tb.x + tb.y + i] = (uint16_t)~(uint32_t)q;
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// one decision from a table entry {C lo, C hi, Cm, ~e}: counts carry-free events (d) and wraps (W)
+__device__ __forceinline__ void oq_decide(uint4 q, uint64_t nH, uint32_t Hm, uint32_t Hm2, uint32_t m, uint32_t &d,
+                                          uint32_t &W, uint64_t &key) {
+    const bool nc = (((uint64_t)q.y << 32) | q.x) <= nH;
+    const uint32_t s = (nc ? Hm : Hm2) + q.z;
+    const bool wrap = s >= m;
+    const uint32_t t = wrap ? s - m : s;
+    d += nc;
+    W += wrap;
+    const uint64_t k = ((uint64_t)t << 32) | q.w;
+    key = k > key ? k : key;
+}
+
+// one sorted block cm[p0, p0 + size) (size >= 1, S = the level's block size) with base b: wraps and the
+// block's best key (t << 32 | ~e)
+template <uint32_t S>
+__device__ __forceinline__ void oq_block(const uint32_t *__restrict__ cm, const uint16_t *__restrict__ ev,
+                                         uint32_t p0, uint32_t size, uint32_t b, uint32_t m, uint32_t &W,
+                                         uint64_t &key) {
+    const uint32_t X = m - b;  // Cm < X <=> no wrap
+    uint32_t idx = 0;          // #{Cm < X}
+#pragma unroll
+    for (uint32_t step = S >> 1; step; step >>= 1) {
+        const uint32_t j = idx + step;
+        const uint32_t v = cm[p0 + min(j, size) - 1];
+        idx = (j <= size && v < X) ? j : idx;
+    }
+    {
+        const uint32_t v = cm[p0 + min(idx, size - 1)];
+        idx += (idx < size && v < X) ? 1u : 0u;
+    }
+    W += size - idx;
+    const uint32_t pos = p0 + (idx ? idx - 1 : size - 1);
+    const uint32_t t = b + cm[pos] - (idx ? 0u : m);
+    const uint64_t k = ((uint64_t)t << 32) | (uint32_t)~(uint32_t)ev[pos];
+    key = k > key ? k : key;
+}
+
+__global__ __launch_bounds__(OQ_WG, 8) void k_replayable_sweep_oq(
+    const uint4 *__restrict__ units, const uint32_t *__restrict__ n_units, const uint64_t *__restrict__ sorted_h0,
+    const uint32_t *__restrict__ sorted_idx, const uint4 *__restrict__ table, uint32_t E,
+    const uint4 *__restrict__ blob, uint32_t EP, uint32_t rb16, const unsigned long long *__restrict__ rowsum,
+    const ClassInfo *__restrict__ classes, const uint32_t *__restrict__ samp_off, uint32_t n_classes, uint32_t m,
+    uint64_t mu, uint32_t m_k64, nmz_sched_stats *__restrict__ stats) {
+    extern __shared__ uint4 oq_lds[];
+    if (blockIdx.x >= *n_units) return;
+    const uint4 u = units[blockIdx.x];
+    const uint32_t L = __builtin_amdgcn_readfirstlane(u.x);
+    const uint32_t start = __builtin_amdgcn_readfirstlane(u.y);
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(u.z);
+    {
+        const uint4 *__restrict__ src = blob + (uint64_t)L * rb16;
+        for (uint32_t i = threadIdx.x; i < rb16; i += OQ_WG) oq_lds[i] = src[i];
+    }
+    __syncthreads();
+    const uint32_t wv = threadIdx.x >> 6;
+    if (wv * 64 >= cnt) return;
+    const uint32_t j = threadIdx.x;
+    const bool live = j < cnt;
+    const uint64_t h0 = sorted_h0[start + min(j, cnt - 1)];
+    const uint32_t *cm0 = reinterpret_cast<const uint32_t *>(oq_lds);
+    const uint32_t *cm1 = cm0 + EP, *cm2 = cm0 + 2 * EP;
+    const uint16_t *e0 = reinterpret_cast<const uint16_t *>(cm0 + 3 * EP);
+    const uint16_t *e1 = e0 + EP, *e2 = e0 + 2 * EP;
+    const uint64_t *samp = reinterpret_cast<const uint64_t *>(cm0 + 3 * EP + 3 * EP / 2);
+    const uint4 *__restrict__ row = table + (uint64_t)L * E;
+
+    uint64_t sum = 0, key = 0;
+    uint32_t W = 0;
+    for (uint32_t c = 0; c < n_classes; ++c) {
+        const ClassInfo ci = classes[c];
+        const uint32_t n = ci.count, cs = ci.start;
+        const uint64_t H = h0 * ci.pn;
+        const uint64_t nH = ~H;
+        const uint32_t Hm = mod_barrett_small(H, m, mu);
+        const uint32_t t2 = Hm + m_k64;
+        const uint32_t Hm2 = min(t2, t2 - m);
+        uint32_t d = 0;
+        if (n <= OQ_BRUTE) {
+            for (uint32_t i = 0; i < n; ++i) oq_decide(row[cs + i], nH, Hm, Hm2, m, d, W, key);
+        } else {
+            // 8-event blocks whose first C is <= ~H are carry-free up to that entry
+            const uint32_t so = samp_off[c], ns = (n + 7) >> 3;
+            uint32_t k = 0;
+            for (uint32_t st = 1u << (31 - __builtin_clz(ns)); st; st >>= 1) {
+                const uint32_t jj = k + st;
+                const uint64_t v = samp[so + min(jj, ns) - 1];
+                k = (jj <= ns && v <= nH) ? jj : k;
+            }
+            const uint32_t b8 = k ? 8 * (k - 1) : 0;  // the 8-block holding the carry boundary
+            const uint32_t be = b8 + 8;
+            {
+                const uint32_t nb = min(8u, n - b8);
+#pragma unroll
+                for (uint32_t i = 0; i < 8; ++i) {
+                    const uint4 q = row[cs + b8 + min(i, nb - 1)];
+                    uint32_t dd = 0, ww = 0;
+                    uint64_t kk = 0;
+                    oq_decide(q, nH, Hm, Hm2, m, dd, ww, kk);
+                    if (i < nb) {
+                        d += dd;
+                        W += ww;
+                        key = kk > key ? kk : key;
+                    }
+                }
+            }
+            d += b8;
+            for (uint32_t lo = 0; lo < n; lo += OQ_S0) {
+                const uint32_t hi = min(lo + OQ_S0, n);
+                if (hi <= b8 || lo >= be) oq_block<OQ_S0>(cm0, e0, cs + lo, hi - lo, hi <= b8 ? Hm : Hm2, m, W, key);
+            }
+            const uint32_t lt = b8 & ~(OQ_S0 - 1);
+#pragma unroll 2
+            for (uint32_t q = 0; q < OQ_S0 / OQ_S1; ++q) {
+                const uint32_t lo = lt + q * OQ_S1, hi = min(lo + OQ_S1, n);
+                if (lo < n && (hi <= b8 || lo >= be))
+                    oq_block<OQ_S1>(cm1, e1, cs + lo, hi - lo, hi <= b8 ? Hm : Hm2, m, W, key);
+            }
+            const uint32_t lm = b8 & ~(OQ_S1 - 1);
+#pragma unroll 2
+            for (uint32_t q = 0; q < OQ_S1 / OQ_S2; ++q) {
+                const uint32_t lo = lm + q * OQ_S2, hi = min(lo + OQ_S2, n);
+                if (lo < n && lo != b8) oq_block<OQ_S2>(cm2, e2, cs + lo, hi - lo, lo < b8 ? Hm : Hm2, m, W, key);
+            }
+        }
+        sum += (uint64_t)d * Hm + (uint64_t)(n - d) * Hm2;
+    }
+    sum += rowsum[L] - (uint64_t)W * m;
+    if (live) {
+        nmz_sched_stats st;
+        st.sum_delay_ns = sum;
+        st.max_delay_ns = (int64_t)(key >> 32);
+        st.argmax_event = ~(uint32_t)key;
+        st.n_fault = 0;
+        st.first_fault = NMZ_NONE;
+        st.flags = 0;
+        stats[sorted_idx[start + j]] = st;
+    }
+}
+
 // general modulus (m >= 2^30, including uint64(negative duration)): one seed per lane
 __global__ __launch_bounds__(256) void k_replayable_sweep_general(
     const uint4 *__restrict__ units, const uint32_t *__restrict__ n_units,
@@ -675,6 +909,62 @@ static uint32_t replay_ec() {
     return ec;
 }
 
+// order-query statistics (default) or the per-decision sweep (NMZ_REPLAY_OQ=0, for A/B runs and as the path
+// for rows too large for LDS)
+static bool replay_oq_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("NMZ_REPLAY_OQ");
+        return !(e && std::string(e) == "0");
+    }();
+    return on;
+}
+
+// Build the order-query blobs after the C sort (MOD_FAST, E < 2^16, a row blob that fits one workgroup's LDS).
+static int oq_build(nmz_replayable_plan *p, const std::vector<ClassInfo> &cls, hipStream_t st) {
+    const uint32_t E = p->n_events;
+    p->oq = false;
+    if (p->mod.kind != MOD_FAST || E == 0 || E >= 65536) return NMZ_OK;
+    const uint32_t EP = (E + 7) & ~7u;
+    std::vector<uint32_t> samp_off;
+    std::vector<uint4> tbl;
+    uint32_t ns = 0;
+    for (const ClassInfo &c : cls) {
+        samp_off.push_back(ns);
+        for (uint32_t lo = 0; lo < c.count; lo += OQ_S0)
+            tbl.push_back(make_uint4(c.start, lo, std::min(OQ_S0, c.count - lo), ns));
+        ns += (c.count + 7) / 8;
+    }
+    const uint64_t rb = ((uint64_t)18 * EP + 8ull * ns + 15) & ~15ull;
+    if (rb > OQ_LDS_MAX) return NMZ_OK;
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_replayable_sweep_oq),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)OQ_LDS_MAX) != hipSuccess)
+            return NMZ_OK;  // keep the per-decision sweep
+        attr = true;
+    }
+    const size_t need = Carve::bytes_for(256 * rb / 16, 16) + Carve::bytes_for(256, 8) +
+                        Carve::bytes_for(samp_off.size(), 4) + Carve::bytes_for(tbl.size(), 16);
+    NMZ_TRY(p->oq_mem.ensure(need));
+    Carve cv(p->oq_mem.ptr);
+    p->d_oq_blob = cv.take<uint4>(256 * rb / 16);
+    p->d_oq_rowsum = cv.take<uint64_t>(256);
+    p->d_oq_samp_off = cv.take<uint32_t>(samp_off.size());
+    uint4 *d_tbl = cv.take<uint4>(tbl.size());
+    p->oq_ep = EP;
+    p->oq_rb16 = (uint32_t)(rb / 16);
+    NMZ_HIP(hipMemsetAsync(p->d_oq_blob, 0, 256 * rb, st));
+    NMZ_HIP(hipMemsetAsync(p->d_oq_rowsum, 0, 256 * 8, st));
+    NMZ_HIP(hipMemcpyAsync(p->d_oq_samp_off, samp_off.data(), samp_off.size() * 4, hipMemcpyHostToDevice, st));
+    NMZ_HIP(hipMemcpyAsync(d_tbl, tbl.data(), tbl.size() * 16, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_replayable_oq_levels, dim3((unsigned)tbl.size(), 256), dim3(256), 0, st, p->d_table, E, d_tbl,
+                       EP, p->oq_rb16, p->d_oq_blob, reinterpret_cast<unsigned long long *>(p->d_oq_rowsum));
+    NMZ_HIP(hipGetLastError());
+    NMZ_HIP(hipStreamSynchronize(st));  // the host vectors above are pageable
+    p->oq = true;
+    return NMZ_OK;
+}
+
 static size_t seed_scratch_bytes(uint64_t S) {
     uint64_t max_units = S / REPLAY_SEEDS_PER_UNIT_MIN + 257;
     return Carve::bytes_for(S, 8) * 2 + Carve::bytes_for(S, 4) + Carve::bytes_for(BUCKET_SMALL_U32, 4) +
@@ -723,6 +1013,17 @@ static int replayable_stats(nmz_replayable_plan *p, hipStream_t st, const uint32
     const int U = replay_u();
     const uint32_t per_unit = 64u * (uint32_t)U;
     const uint64_t max_units = S / per_unit + 256;
+    if (p->oq && replay_oq_enabled()) {
+        NMZ_TRY(bucket_seeds_counted(st, sc.h0, S, OQ_WG, sc.b, sc.counter));
+        const uint64_t units = S / OQ_WG + 256;
+        KernelTimer kt(p->ctx, st, "replayable_sweep");
+        hipLaunchKernelGGL(k_replayable_sweep_oq, dim3((unsigned)units), dim3(OQ_WG), p->oq_rb16 * 16u, st, sc.b.units,
+                           sc.b.n_units, sc.b.sorted_h0, sc.b.sorted_idx, p->d_table, E, p->d_oq_blob, p->oq_ep,
+                           p->oq_rb16, reinterpret_cast<const unsigned long long *>(p->d_oq_rowsum), p->d_classes,
+                           p->d_oq_samp_off, p->n_classes, p->mod.m32, p->mod.mu, p->mod.m_k64, d_stats);
+        NMZ_HIP(hipGetLastError());
+        return NMZ_OK;
+    }
     NMZ_TRY(bucket_seeds_counted(st, sc.h0, S, p->mod.kind == MOD_FAST ? per_unit : 64, sc.b, sc.counter));
     if (p->mod.kind == MOD_FAST) {
         const uint32_t ec = replay_ec();
@@ -840,6 +1141,7 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
         p->seed_scratch.release();
         p->partial.release();
         p->topk_lists.release();
+        p->oq_mem.release();
         delete p;
         return code;
     };
@@ -886,6 +1188,8 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
         }
         if (bad)
             return cleanup(fail(NMZ_EHIP, "plan table kernel failed"));
+        const int orc = oq_build(p, cls, st);
+        if (orc != NMZ_OK) return cleanup(orc);
     }
     *out = p;
     return NMZ_OK;
@@ -914,6 +1218,7 @@ int nmz_replayable_plan_destroy(nmz_replayable_plan *plan) {
         plan->seed_scratch.release();
         plan->partial.release();
         plan->topk_lists.release();
+        plan->oq_mem.release();
     }
     delete plan;
     return NMZ_OK;
@@ -958,6 +1263,7 @@ int nmz_replayable_sweep(nmz_ctx *ctx, const uint32_t *seed_off, const uint8_t *
             p->seed_scratch.release();
             p->partial.release();
             p->topk_lists.release();
+            p->oq_mem.release();
             delete p;
         }
     } pg{plan};

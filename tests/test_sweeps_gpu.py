@@ -63,7 +63,26 @@ def test_replayable_many_length_classes_and_ties(ctx):
         assert np.array_equal(r.stats, st)
 
 
-@pytest.mark.parametrize("E", [1, 3, 63, 64, 65, 127, 2047, 2048, 2049, 4097])
+@pytest.mark.parametrize("m", [1, 2, 3, 7, 1000, 100_000_000, 2**30 - 1])
+def test_replayable_order_query_block_edges(ctx, m):
+    """K1's order-query statistics (k_replayable_sweep_oq): length classes whose sizes sit on both sides of the
+    8-, 64- and 512-event block edges and of the per-event threshold (24), shuffled so the original event order
+    mixes the classes; tiny moduli make most maxima ties, which must resolve to the first original event."""
+    rng = np.random.default_rng(m)
+    sizes = [25, 64, 511, 512, 513, 1025, 8, 24, 1, 65, 1600]
+    hints = []
+    for c, n in enumerate(sizes):
+        hints += ["".join(rng.choice(list("0123456789-"), size=3 + c)) for _ in range(n)]
+    hints = [hints[i] for i in rng.permutation(len(hints))]
+    seeds = [str(i) for i in range(700)] + ["", "foobar"]
+    p = Replayable()
+    p.MaxInterval = m
+    r = p.Sweep(seeds, hints, n_dump=2, ctx=ctx)
+    st, dl = rep_oracle(seeds, hints, m, n_dump=2)
+    assert np.array_equal(r.stats, st) and np.array_equal(r.delays, dl)
+
+
+@pytest.mark.parametrize("E", [1, 3, 63, 64, 65, 127, 2047, 2048, 2049, 4097, 9000])
 def test_replayable_event_counts_around_stage_and_chunk_edges(ctx, E):
     """K1 stages 64 events at a time (the next chunk's load is clamped to the last event) and works in
     2,048-event items: trace lengths on either side of both edges, vs the oracle."""
