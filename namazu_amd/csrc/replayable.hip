@@ -38,6 +38,8 @@ struct ClassInfo {
     uint32_t count;
 };
 
+struct OqClass;
+
 }  // namespace nmz
 
 struct nmz_replayable_plan {
@@ -57,10 +59,10 @@ struct nmz_replayable_plan {
     nmz::DevBuf plan_mem;
     // order-query statistics (k_replayable_sweep_oq): per-row blobs staged whole into LDS
     bool oq = false;
-    uint32_t oq_ep = 0, oq_rb16 = 0;    // E padded to a multiple of 8; blob bytes / 16 per row
-    uint4 *d_oq_blob = nullptr;         // [256][rb16] {cm[3][EP] u32, e[3][EP] u16, samp[NS] u64}
+    uint32_t oq_rb16 = 0;               // row image bytes / 16
+    uint4 *d_oq_blob = nullptr;         // [256][rb16] row images (level arrays {Cm, ~e} + samples of C)
     uint64_t *d_oq_rowsum = nullptr;    // [256] sum of C mod m over the row
-    uint32_t *d_oq_samp_off = nullptr;  // [n_classes] first sample of each class
+    nmz::OqClass *d_oq_classes = nullptr;
     nmz::DevBuf oq_mem;
 };
 
@@ -615,43 +617,64 @@ __global__ __launch_bounds__(256) void k_replayable_merge(const uint4 *__restric
 // event with wave-uniform table reads. The sum over all segments needs only the
 // carry-free counts d and the wrap count W:
 //   sum = sum_segments (d Hm + (n - d) Hm2) + sum_row Cm - m W.
+//
+// LDS image of a row (uint2 units): the three level arrays {Cm, ~e} and the 8-event samples of C, each
+// segment's arrays skewed (logical entry i at base + i + i/32) so that the power-of-two strides of a
+// binary search land on distinct banks; a block that the segment end cuts short is padded with copies of
+// its last (largest) entry, so every search runs over a whole block with immediate-offset reads.
 // ---------------------------------------------------------------------------
 constexpr uint32_t OQ_S0 = 512, OQ_S1 = 64, OQ_S2 = 8;
-constexpr uint32_t OQ_BRUTE = 24;   // segments of at most this many events: per-event decisions
+constexpr uint32_t OQ_BRUTE = 64;   // segments of at most this many events: per-event decisions
 constexpr uint32_t OQ_WG = 1024;    // seeds per workgroup (16 waves share one staged row)
 constexpr uint32_t OQ_LDS_MAX = 160 * 1024;
+
+__host__ __device__ constexpr uint32_t oq_skew(uint32_t i) { return i + (i >> 5); }
+__host__ __device__ constexpr uint32_t oq_round(uint32_t n, uint32_t s) { return (n + s - 1) / s * s; }
+
+struct OqClass {
+    uint64_t pn;            // P^len
+    uint32_t start, count;  // table segment (C order)
+    uint32_t lv[3];         // level-array bases in the row image (uint2 units)
+    uint32_t samp, samp_p2; // sample base; sample slots (a power of two >= ceil(n / 8))
+    uint32_t pad[3];
+};
 
 // plan: one workgroup per (top block, row L): the top block's entries (C order) sorted by (Cm, ~e) with a
 // bitonic network whose runs all end ascending after every stage (the first step of stage k compares an
 // element with its mirror in the k-run), so the 8-, 64- and 512-runs are snapshots of the three levels.
 // Also writes the 8-event samples of C and adds the block's C mod m to the row sum.
 __global__ __launch_bounds__(256) void k_replayable_oq_levels(const uint4 *__restrict__ table, uint32_t E,
-                                                              const uint4 *__restrict__ tb_list, uint32_t EP,
-                                                              uint32_t rb16, uint4 *__restrict__ blob,
+                                                              const uint4 *__restrict__ tb_list,
+                                                              const OqClass *__restrict__ classes, uint32_t rb16,
+                                                              uint4 *__restrict__ blob,
                                                               unsigned long long *__restrict__ rowsum) {
     __shared__ uint64_t key[OQ_S0];
     __shared__ unsigned long long part[4];
-    const uint4 tb = tb_list[blockIdx.x];  // {segment start, block start in the segment, size, first sample}
-    const uint32_t L = blockIdx.y;
-    const uint4 *__restrict__ row = table + (uint64_t)L * E + tb.x + tb.y;
-    uint32_t *cm = reinterpret_cast<uint32_t *>(blob + (uint64_t)L * rb16);
-    uint16_t *ev = reinterpret_cast<uint16_t *>(cm + 3 * EP);
-    uint64_t *samp = reinterpret_cast<uint64_t *>(cm + 3 * EP + 3 * EP / 2);
+    const uint4 tb = tb_list[blockIdx.x];  // {class, block start in the segment, size, 0}
+    const OqClass ci = classes[tb.x];
+    const uint32_t L = blockIdx.y, lo = tb.y, size = tb.z, n = ci.count;
+    const bool levels = n > OQ_BRUTE;
+    const uint4 *__restrict__ row = table + (uint64_t)L * E + ci.start + lo;
+    uint2 *img = reinterpret_cast<uint2 *>(blob + (uint64_t)L * rb16);
     uint64_t s = 0;
     for (uint32_t i = threadIdx.x; i < OQ_S0; i += 256) {
-        if (i < tb.z) {
+        if (i < size) {
             const uint4 q = row[i];
             key[i] = ((uint64_t)q.z << 32) | q.w;
             s += q.z;
-            if ((i & 7) == 0) samp[tb.w + (tb.y + i) / 8] = ((uint64_t)q.y << 32) | q.x;
+            if (levels && (i & 7) == 0) img[ci.samp + oq_skew((lo + i) / 8)] = make_uint2(q.x, q.y);
         } else {
             key[i] = UINT64_MAX;
         }
     }
+    if (levels && lo == 0)  // sample padding: above every ~H but ~0 (H = 0), where the count is clamped to ns
+        for (uint32_t k = (n + 7) / 8 + threadIdx.x; k < ci.samp_p2; k += 256)
+            img[ci.samp + oq_skew(k)] = make_uint2(~0u, ~0u);
     for (int o = 32; o; o >>= 1) s += __shfl_xor(s, o, 64);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
     __syncthreads();
     if (threadIdx.x == 0) atomicAdd(rowsum + L, part[0] + part[1] + part[2] + part[3]);
+    if (!levels) return;
     const uint32_t p = threadIdx.x;  // one compare-exchange pair per thread
     for (uint32_t k = 2; k <= OQ_S0; k <<= 1) {
         for (uint32_t j = k >> 1; j; j >>= 1) {
@@ -672,10 +695,13 @@ __global__ __launch_bounds__(256) void k_replayable_oq_levels(const uint4 *__res
         }
         const int lv = k == OQ_S2 ? 2 : k == OQ_S1 ? 1 : k == OQ_S0 ? 0 : -1;
         if (lv >= 0) {
-            for (uint32_t i = threadIdx.x; i < tb.z; i += 256) {
-                const uint64_t q = key[i];
-                cm[lv * EP + tb.x + tb.y + i] = (uint32_t)(q >> 32);
-                ev[lv * EP + tb.x + tb.y + i] = (uint16_t)~(uint32_t)q;
+            // the level's storage covers the segment rounded up to 512 (level 0) or 64 events
+            const uint32_t padlen = oq_round(n, lv == 0 ? OQ_S0 : OQ_S1);
+            for (uint32_t i = threadIdx.x; i < OQ_S0 && lo + i < padlen; i += 256) {
+                const uint32_t b0 = i & ~(k - 1);
+                const uint32_t last = b0 < size ? min(b0 + k, size) - 1 : size - 1;
+                const uint64_t q = key[i < size ? i : last];
+                img[ci.lv[lv] + oq_skew(lo + i)] = make_uint2((uint32_t)(q >> 32), (uint32_t)q);
             }
             __syncthreads();
         }
@@ -695,64 +721,108 @@ __device__ __forceinline__ void oq_decide(uint4 q, uint64_t nH, uint32_t Hm, uin
     key = k > key ? k : key;
 }
 
-// one sorted block cm[p0, p0 + size) (size >= 1, S = the level's block size) with base b: wraps and the
-// block's best key (t << 32 | ~e)
-template <uint32_t S>
-__device__ __forceinline__ void oq_block(const uint32_t *__restrict__ cm, const uint16_t *__restrict__ ev,
-                                         uint32_t p0, uint32_t size, uint32_t b, uint32_t m, uint32_t &W,
-                                         uint64_t &key) {
-    const uint32_t X = m - b;  // Cm < X <=> no wrap
-    uint32_t idx = 0;          // #{Cm < X}
+// phys offset (from phys(idx)) of element idx + s - 1 in a skewed block, idx a multiple of 2s; and the step
+// of phys(idx) when idx grows by s
+__host__ __device__ constexpr uint32_t oq_off(uint32_t s) { return s >= 32 ? s - 2 + s / 32 : s - 1; }
+__host__ __device__ constexpr uint32_t oq_inc(uint32_t s) { return s >= 32 ? s + s / 32 : s; }
+
+// Interleaved searches over whole sorted blocks (skewed, padded with copies of the block's largest entry):
+// chains [0, N0) over 512-blocks, [N0, N0 + N1) over 64-blocks, the rest over 8-blocks, stepped together
+// so that every chain ends in the same round (9 dependent rounds of independent LDS reads). Per chain:
+// cnt = #{Cm < X} (0..S), cand = the entry just below X, or the block's largest entry when none is below X
+// (wrap). pb = phys index of the block's first entry.
+template <int N0, int N1, int N2>
+__device__ __forceinline__ void oq_search(const uint2 *__restrict__ img, const uint32_t (&pb)[N0 + N1 + N2],
+                                          const uint32_t (&X)[N0 + N1 + N2], uint32_t (&cnt)[N0 + N1 + N2],
+                                          uint2 (&cand)[N0 + N1 + N2], bool (&wrap)[N0 + N1 + N2]) {
+    constexpr int NC = N0 + N1 + N2;
+    // byte addresses, so every step is one ds_read_b32 with an immediate offset
+    const char *__restrict__ base = reinterpret_cast<const char *>(img);
+    uint32_t Q[NC];
 #pragma unroll
-    for (uint32_t step = S >> 1; step; step >>= 1) {
-        const uint32_t j = idx + step;
-        const uint32_t v = cm[p0 + min(j, size) - 1];
-        idx = (j <= size && v < X) ? j : idx;
+    for (int k = 0; k < NC; ++k) Q[k] = pb[k] * 8u;
+#pragma unroll
+    for (uint32_t r = 0; r < 9; ++r) {
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+            const uint32_t lg = k < N0 ? 8 : k < N0 + N1 ? 5 : 2;  // log2(S) - 1
+            if (r + lg >= 8) {
+                const uint32_t st = 1u << (8 - r);
+                const uint32_t v = *reinterpret_cast<const uint32_t *>(base + Q[k] + 8u * oq_off(st));
+                Q[k] = v < X[k] ? Q[k] + 8u * oq_inc(st) : Q[k];
+            }
+        }
     }
-    {
-        const uint32_t v = cm[p0 + min(idx, size - 1)];
-        idx += (idx < size && v < X) ? 1u : 0u;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+        const uint32_t S = k < N0 ? OQ_S0 : k < N0 + N1 ? OQ_S1 : OQ_S2;
+        const uint2 first = *reinterpret_cast<const uint2 *>(base + pb[k] * 8u + 8u * oq_skew(S - 1));
+        const uint32_t q = (Q[k] >> 3) - pb[k];
+        const uint32_t idx = q - ((q * 993u) >> 15);  // phys -> logical (q = idx + idx/32 < 33 * 32)
+        const uint2 c = *reinterpret_cast<const uint2 *>(base + Q[k] - (idx ? 8u + ((idx & 31) == 0 ? 8u : 0u) : 0u));
+        const bool all = first.x < X[k];
+        cnt[k] = all ? S : idx;
+        wrap[k] = !all && idx == 0;
+        cand[k] = (all || idx == 0) ? first : c;
+        // finish four chains at a time: the compiler would otherwise issue every chain's two final reads
+        // at once and spill
+        if ((k & 3) == 3) asm volatile("" ::: "memory");
     }
-    W += size - idx;
-    const uint32_t pos = p0 + (idx ? idx - 1 : size - 1);
-    const uint32_t t = b + cm[pos] - (idx ? 0u : m);
-    const uint64_t k = ((uint64_t)t << 32) | (uint32_t)~(uint32_t)ev[pos];
+}
+
+// fold one block result into the seed's statistics; side 0 = not this lane's block, 1 = carry-free (Hm),
+// 2 = carry (Hm2); rs = the block's real size
+__device__ __forceinline__ void oq_accum(int side, uint32_t rs, uint32_t cnt, uint2 cand, bool wrap, uint32_t Hm,
+                                         uint32_t Hm2, uint32_t m, uint32_t &W, uint64_t &key) {
+    const uint32_t b = side == 2 ? Hm2 : Hm;
+    const uint32_t t = b + cand.x - (wrap ? m : 0u);
+    const uint64_t k = side ? (((uint64_t)t << 32) | cand.y) : 0ull;
+    W += side ? rs - min(cnt, rs) : 0u;
     key = k > key ? k : key;
 }
 
-__global__ __launch_bounds__(OQ_WG, 8) void k_replayable_sweep_oq(
-    const uint4 *__restrict__ units, const uint32_t *__restrict__ n_units, const uint64_t *__restrict__ sorted_h0,
+// One workgroup per row L (256 workgroups, one per CU): the row image is staged into LDS once, then the 16
+// waves take the row's seeds 64 at a time (all seeds of a bucket share the row).
+__global__ __launch_bounds__(OQ_WG) void k_replayable_sweep_oq(
+    const uint32_t *__restrict__ bucket_off, const uint64_t *__restrict__ sorted_h0,
     const uint32_t *__restrict__ sorted_idx, const uint4 *__restrict__ table, uint32_t E,
-    const uint4 *__restrict__ blob, uint32_t EP, uint32_t rb16, const unsigned long long *__restrict__ rowsum,
-    const ClassInfo *__restrict__ classes, const uint32_t *__restrict__ samp_off, uint32_t n_classes, uint32_t m,
-    uint64_t mu, uint32_t m_k64, nmz_sched_stats *__restrict__ stats) {
+    const uint4 *__restrict__ blob, uint32_t rb16, const unsigned long long *__restrict__ rowsum,
+    const OqClass *__restrict__ classes, uint32_t n_classes, uint32_t m, uint64_t mu, uint32_t m_k64,
+    nmz_sched_stats *__restrict__ stats) {
     extern __shared__ uint4 oq_lds[];
-    if (blockIdx.x >= *n_units) return;
-    const uint4 u = units[blockIdx.x];
-    const uint32_t L = __builtin_amdgcn_readfirstlane(u.x);
-    const uint32_t start = __builtin_amdgcn_readfirstlane(u.y);
-    const uint32_t cnt = __builtin_amdgcn_readfirstlane(u.z);
+    const uint32_t L = blockIdx.x;
+    const uint32_t s0 = bucket_off[L], s1 = bucket_off[L + 1];
+    if (s0 == s1) return;
     {
         const uint4 *__restrict__ src = blob + (uint64_t)L * rb16;
-        for (uint32_t i = threadIdx.x; i < rb16; i += OQ_WG) oq_lds[i] = src[i];
+        constexpr uint32_t B = 4;  // loads in flight per thread
+        for (uint32_t i0 = 0; i0 < rb16; i0 += B * OQ_WG) {
+            uint4 v[B];
+#pragma unroll
+            for (uint32_t k = 0; k < B; ++k) {
+                const uint32_t i = i0 + k * OQ_WG + threadIdx.x;
+                if (i < rb16) v[k] = src[i];
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < B; ++k) {
+                const uint32_t i = i0 + k * OQ_WG + threadIdx.x;
+                if (i < rb16) oq_lds[i] = v[k];
+            }
+        }
     }
     __syncthreads();
-    const uint32_t wv = threadIdx.x >> 6;
-    if (wv * 64 >= cnt) return;
-    const uint32_t j = threadIdx.x;
-    const bool live = j < cnt;
-    const uint64_t h0 = sorted_h0[start + min(j, cnt - 1)];
-    const uint32_t *cm0 = reinterpret_cast<const uint32_t *>(oq_lds);
-    const uint32_t *cm1 = cm0 + EP, *cm2 = cm0 + 2 * EP;
-    const uint16_t *e0 = reinterpret_cast<const uint16_t *>(cm0 + 3 * EP);
-    const uint16_t *e1 = e0 + EP, *e2 = e0 + 2 * EP;
-    const uint64_t *samp = reinterpret_cast<const uint64_t *>(cm0 + 3 * EP + 3 * EP / 2);
+    const uint2 *img = reinterpret_cast<const uint2 *>(oq_lds);
     const uint4 *__restrict__ row = table + (uint64_t)L * E;
+    const uint64_t rsum = rowsum[L];
+    for (uint32_t g = s0 + (threadIdx.x & ~63u); g < s1; g += OQ_WG) {
+    const uint32_t j = g + (threadIdx.x & 63);
+    const bool live = j < s1;
+    const uint64_t h0 = sorted_h0[min(j, s1 - 1)];
 
     uint64_t sum = 0, key = 0;
     uint32_t W = 0;
     for (uint32_t c = 0; c < n_classes; ++c) {
-        const ClassInfo ci = classes[c];
+        const OqClass ci = classes[c];
         const uint32_t n = ci.count, cs = ci.start;
         const uint64_t H = h0 * ci.pn;
         const uint64_t nH = ~H;
@@ -763,24 +833,32 @@ __global__ __launch_bounds__(OQ_WG, 8) void k_replayable_sweep_oq(
         if (n <= OQ_BRUTE) {
             for (uint32_t i = 0; i < n; ++i) oq_decide(row[cs + i], nH, Hm, Hm2, m, d, W, key);
         } else {
-            // 8-event blocks whose first C is <= ~H are carry-free up to that entry
-            const uint32_t so = samp_off[c], ns = (n + 7) >> 3;
-            uint32_t k = 0;
-            for (uint32_t st = 1u << (31 - __builtin_clz(ns)); st; st >>= 1) {
-                const uint32_t jj = k + st;
-                const uint64_t v = samp[so + min(jj, ns) - 1];
-                k = (jj <= ns && v <= nH) ? jj : k;
+            const uint32_t XA = m - Hm, XB = m - Hm2;
+            const uint32_t ns = (n + 7) >> 3, nt = (n + OQ_S0 - 1) / OQ_S0;
+            // 8-event blocks whose first C is <= ~H are carry-free up to that entry: binary search over the
+            // samples (the C of every 8th entry, ascending; slots past ns hold whatever, so the count is clamped)
+            uint32_t ks;
+            {
+                const uint32_t sb = ci.samp;
+                uint32_t Q = sb;
+                for (uint32_t st = ci.samp_p2 >> 1; st; st >>= 1) {
+                    const uint2 v = img[Q + oq_off(st)];
+                    Q = ((((uint64_t)v.y) << 32) | v.x) <= nH ? Q + oq_inc(st) : Q;
+                }
+                const uint32_t q = Q - sb;
+                const uint32_t k0 = q - ((q * 993u) >> 15);
+                const uint2 v = img[Q];  // the last slot the lifting cannot reach
+                ks = min(k0 + (((((uint64_t)v.y) << 32) | v.x) <= nH ? 1u : 0u), ns);
             }
-            const uint32_t b8 = k ? 8 * (k - 1) : 0;  // the 8-block holding the carry boundary
+            const uint32_t b8 = ks ? 8 * (ks - 1) : 0;  // the 8-block holding the carry boundary
             const uint32_t be = b8 + 8;
             {
                 const uint32_t nb = min(8u, n - b8);
 #pragma unroll
-                for (uint32_t i = 0; i < 8; ++i) {
-                    const uint4 q = row[cs + b8 + min(i, nb - 1)];
+                for (uint32_t i = 0; i < 8; ++i) {  // decided event by event
                     uint32_t dd = 0, ww = 0;
                     uint64_t kk = 0;
-                    oq_decide(q, nH, Hm, Hm2, m, dd, ww, kk);
+                    oq_decide(row[cs + b8 + min(i, nb - 1)], nH, Hm, Hm2, m, dd, ww, kk);
                     if (i < nb) {
                         d += dd;
                         W += ww;
@@ -789,27 +867,78 @@ __global__ __launch_bounds__(OQ_WG, 8) void k_replayable_sweep_oq(
                 }
             }
             d += b8;
-            for (uint32_t lo = 0; lo < n; lo += OQ_S0) {
-                const uint32_t hi = min(lo + OQ_S0, n);
-                if (hi <= b8 || lo >= be) oq_block<OQ_S0>(cm0, e0, cs + lo, hi - lo, hi <= b8 ? Hm : Hm2, m, W, key);
+            const uint32_t pad1 = oq_round(n, OQ_S1);
+            // level 0: every 512-block of the segment, two at a time (this lane's boundary block is searched
+            // and dropped)
+            for (uint32_t b = 0; b < nt; b += 2) {
+                uint32_t pb[2], X[2], cn[2];
+                uint2 cand[2];
+                bool wr[2];
+                int side[2];
+                uint32_t rs[2];
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const uint32_t lo = min(b + k, nt - 1) * OQ_S0, hi = min(lo + OQ_S0, n);
+                    side[k] = b + k >= nt ? 0 : hi <= b8 ? 1 : lo >= be ? 2 : 0;
+                    X[k] = side[k] == 2 ? XB : XA;
+                    pb[k] = ci.lv[0] + oq_skew(lo);
+                    rs[k] = hi - lo;
+                }
+                if (__builtin_amdgcn_ballot_w64(side[0] != 0 || side[1] != 0)) {  // n <= 512: boundary only
+                    oq_search<2, 0, 0>(img, pb, X, cn, cand, wr);
+#pragma unroll
+                    for (int k = 0; k < 2; ++k)
+                        oq_accum(side[k], rs[k], cn[k], cand[k], wr[k], Hm, Hm2, m, W, key);
+                }
             }
-            const uint32_t lt = b8 & ~(OQ_S0 - 1);
-#pragma unroll 2
-            for (uint32_t q = 0; q < OQ_S0 / OQ_S1; ++q) {
-                const uint32_t lo = lt + q * OQ_S1, hi = min(lo + OQ_S1, n);
-                if (lo < n && (hi <= b8 || lo >= be))
-                    oq_block<OQ_S1>(cm1, e1, cs + lo, hi - lo, hi <= b8 ? Hm : Hm2, m, W, key);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {  // level 1: the eight 64-blocks of the boundary 512-block, 4 at a time
+                const uint32_t lt = (b8 & ~(OQ_S0 - 1)) + h * 4 * OQ_S1;
+                uint32_t pb[4], X[4], cn[4], rs[4];
+                int side[4];
+                uint2 cand[4];
+                bool wr[4], any = false;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t lo = lt + k * OQ_S1, hi = min(lo + OQ_S1, n);
+                    side[k] = lo >= n ? 0 : hi <= b8 ? 1 : lo >= be ? 2 : 0;
+                    any |= side[k] != 0;
+                    X[k] = side[k] == 2 ? XB : XA;
+                    pb[k] = ci.lv[1] + oq_skew(min(lo, pad1 - OQ_S1));
+                    rs[k] = hi - lo;
+                }
+                if (__builtin_amdgcn_ballot_w64(any)) {
+                    oq_search<0, 4, 0>(img, pb, X, cn, cand, wr);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) oq_accum(side[k], rs[k], cn[k], cand[k], wr[k], Hm, Hm2, m, W, key);
+                }
             }
-            const uint32_t lm = b8 & ~(OQ_S1 - 1);
-#pragma unroll 2
-            for (uint32_t q = 0; q < OQ_S1 / OQ_S2; ++q) {
-                const uint32_t lo = lm + q * OQ_S2, hi = min(lo + OQ_S2, n);
-                if (lo < n && lo != b8) oq_block<OQ_S2>(cm2, e2, cs + lo, hi - lo, lo < b8 ? Hm : Hm2, m, W, key);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {  // level 2: the 8-blocks of the boundary 64-block, less the one decided above
+                const uint32_t lm = (b8 & ~(OQ_S1 - 1)) + h * 4 * OQ_S2;
+                uint32_t pb[4], X[4], cn[4], rs[4];
+                int side[4];
+                uint2 cand[4];
+                bool wr[4], any = false;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t lo = lm + k * OQ_S2, hi = min(lo + OQ_S2, n);
+                    side[k] = (lo >= n || lo == b8) ? 0 : lo < b8 ? 1 : 2;
+                    any |= side[k] != 0;
+                    X[k] = side[k] == 2 ? XB : XA;
+                    pb[k] = ci.lv[2] + oq_skew(min(lo, pad1 - OQ_S2));
+                    rs[k] = hi - lo;
+                }
+                if (__builtin_amdgcn_ballot_w64(any)) {
+                    oq_search<0, 0, 4>(img, pb, X, cn, cand, wr);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) oq_accum(side[k], rs[k], cn[k], cand[k], wr[k], Hm, Hm2, m, W, key);
+                }
             }
         }
         sum += (uint64_t)d * Hm + (uint64_t)(n - d) * Hm2;
     }
-    sum += rowsum[L] - (uint64_t)W * m;
+    sum += rsum - (uint64_t)W * m;
     if (live) {
         nmz_sched_stats st;
         st.sum_delay_ns = sum;
@@ -818,7 +947,8 @@ __global__ __launch_bounds__(OQ_WG, 8) void k_replayable_sweep_oq(
         st.n_fault = 0;
         st.first_fault = NMZ_NONE;
         st.flags = 0;
-        stats[sorted_idx[start + j]] = st;
+        stats[sorted_idx[j]] = st;
+    }
     }
 }
 
@@ -919,23 +1049,44 @@ static bool replay_oq_enabled() {
     return on;
 }
 
-// Build the order-query blobs after the C sort (MOD_FAST, E < 2^16, a row blob that fits one workgroup's LDS).
+// Build the order-query row images after the C sort (MOD_FAST, a row image that fits one workgroup's LDS).
 static int oq_build(nmz_replayable_plan *p, const std::vector<ClassInfo> &cls, hipStream_t st) {
     const uint32_t E = p->n_events;
     p->oq = false;
-    if (p->mod.kind != MOD_FAST || E == 0 || E >= 65536) return NMZ_OK;
-    const uint32_t EP = (E + 7) & ~7u;
-    std::vector<uint32_t> samp_off;
+    if (p->mod.kind != MOD_FAST || E == 0) return NMZ_OK;
+    std::vector<OqClass> oc(cls.size());
     std::vector<uint4> tbl;
-    uint32_t ns = 0;
-    for (const ClassInfo &c : cls) {
-        samp_off.push_back(ns);
-        for (uint32_t lo = 0; lo < c.count; lo += OQ_S0)
-            tbl.push_back(make_uint4(c.start, lo, std::min(OQ_S0, c.count - lo), ns));
-        ns += (c.count + 7) / 8;
+    uint64_t len[4] = {0, 0, 0, 0};  // level 0, 1, 2 and samples (uint2 units)
+    for (size_t c = 0; c < cls.size(); ++c) {
+        const uint32_t n = cls[c].count;
+        OqClass &o = oc[c];
+        o = OqClass{};
+        o.pn = cls[c].pn;
+        o.start = cls[c].start;
+        o.count = n;
+        if (n > OQ_BRUTE) {
+            o.lv[0] = (uint32_t)len[0];
+            len[0] += oq_skew(oq_round(n, OQ_S0));
+            o.lv[1] = (uint32_t)len[1];
+            o.lv[2] = (uint32_t)len[2];
+            len[1] += oq_skew(oq_round(n, OQ_S1));
+            len[2] += oq_skew(oq_round(n, OQ_S1));
+            o.samp = (uint32_t)len[3];
+            uint32_t p2 = 1;
+            while (p2 < (n + 7) / 8) p2 <<= 1;
+            o.samp_p2 = p2;
+            len[3] += oq_skew(p2);
+        }
+        for (uint32_t lo = 0; lo < n; lo += OQ_S0) tbl.push_back(make_uint4((uint32_t)c, lo, std::min(OQ_S0, n - lo), 0));
     }
-    const uint64_t rb = ((uint64_t)18 * EP + 8ull * ns + 15) & ~15ull;
+    const uint64_t total = len[0] + len[1] + len[2] + len[3];
+    const uint64_t rb = (total * 8 + 15) & ~15ull;
     if (rb > OQ_LDS_MAX) return NMZ_OK;
+    for (OqClass &o : oc) {  // regions: level 0 | level 1 | level 2 | samples
+        o.lv[1] += (uint32_t)len[0];
+        o.lv[2] += (uint32_t)(len[0] + len[1]);
+        o.samp += (uint32_t)(len[0] + len[1] + len[2]);
+    }
     static bool attr = false;
     if (!attr) {
         if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_replayable_sweep_oq),
@@ -944,21 +1095,21 @@ static int oq_build(nmz_replayable_plan *p, const std::vector<ClassInfo> &cls, h
         attr = true;
     }
     const size_t need = Carve::bytes_for(256 * rb / 16, 16) + Carve::bytes_for(256, 8) +
-                        Carve::bytes_for(samp_off.size(), 4) + Carve::bytes_for(tbl.size(), 16);
+                        Carve::bytes_for(oc.size(), sizeof(OqClass)) + Carve::bytes_for(tbl.size(), 16);
     NMZ_TRY(p->oq_mem.ensure(need));
     Carve cv(p->oq_mem.ptr);
     p->d_oq_blob = cv.take<uint4>(256 * rb / 16);
     p->d_oq_rowsum = cv.take<uint64_t>(256);
-    p->d_oq_samp_off = cv.take<uint32_t>(samp_off.size());
+    p->d_oq_classes = cv.take<OqClass>(oc.size());
     uint4 *d_tbl = cv.take<uint4>(tbl.size());
-    p->oq_ep = EP;
     p->oq_rb16 = (uint32_t)(rb / 16);
     NMZ_HIP(hipMemsetAsync(p->d_oq_blob, 0, 256 * rb, st));
     NMZ_HIP(hipMemsetAsync(p->d_oq_rowsum, 0, 256 * 8, st));
-    NMZ_HIP(hipMemcpyAsync(p->d_oq_samp_off, samp_off.data(), samp_off.size() * 4, hipMemcpyHostToDevice, st));
+    NMZ_HIP(hipMemcpyAsync(p->d_oq_classes, oc.data(), oc.size() * sizeof(OqClass), hipMemcpyHostToDevice, st));
     NMZ_HIP(hipMemcpyAsync(d_tbl, tbl.data(), tbl.size() * 16, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_replayable_oq_levels, dim3((unsigned)tbl.size(), 256), dim3(256), 0, st, p->d_table, E, d_tbl,
-                       EP, p->oq_rb16, p->d_oq_blob, reinterpret_cast<unsigned long long *>(p->d_oq_rowsum));
+                       p->d_oq_classes, p->oq_rb16, p->d_oq_blob,
+                       reinterpret_cast<unsigned long long *>(p->d_oq_rowsum));
     NMZ_HIP(hipGetLastError());
     NMZ_HIP(hipStreamSynchronize(st));  // the host vectors above are pageable
     p->oq = true;
@@ -1015,12 +1166,11 @@ static int replayable_stats(nmz_replayable_plan *p, hipStream_t st, const uint32
     const uint64_t max_units = S / per_unit + 256;
     if (p->oq && replay_oq_enabled()) {
         NMZ_TRY(bucket_seeds_counted(st, sc.h0, S, OQ_WG, sc.b, sc.counter));
-        const uint64_t units = S / OQ_WG + 256;
         KernelTimer kt(p->ctx, st, "replayable_sweep");
-        hipLaunchKernelGGL(k_replayable_sweep_oq, dim3((unsigned)units), dim3(OQ_WG), p->oq_rb16 * 16u, st, sc.b.units,
-                           sc.b.n_units, sc.b.sorted_h0, sc.b.sorted_idx, p->d_table, E, p->d_oq_blob, p->oq_ep,
-                           p->oq_rb16, reinterpret_cast<const unsigned long long *>(p->d_oq_rowsum), p->d_classes,
-                           p->d_oq_samp_off, p->n_classes, p->mod.m32, p->mod.mu, p->mod.m_k64, d_stats);
+        hipLaunchKernelGGL(k_replayable_sweep_oq, dim3(256), dim3(OQ_WG), p->oq_rb16 * 16u, st, sc.b.offset,
+                           sc.b.sorted_h0, sc.b.sorted_idx, p->d_table, E, p->d_oq_blob, p->oq_rb16,
+                           reinterpret_cast<const unsigned long long *>(p->d_oq_rowsum), p->d_oq_classes,
+                           p->n_classes, p->mod.m32, p->mod.mu, p->mod.m_k64, d_stats);
         NMZ_HIP(hipGetLastError());
         return NMZ_OK;
     }
