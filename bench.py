@@ -13,7 +13,7 @@ Inputs are resident in HBM before the timed region; the per-trace plan
 
 Metric: schedule decisions/s (seeds x events / s), whole job.
 Also reported (same JSON line): the roofline of the dominant kernel
-(k_replayable_sweep_fast, HIP events on its launch stream), a CPU baseline
+(k_replayable_sweep_oq, HIP events on its launch stream), a CPU baseline
 (the oracle's C restatement on the host cores, bounded sample) and
 secondary lines for the random-policy sweep (configs[3]) and the banded
 edit-distance all-pairs search (configs[2]), each on a per-GPU share.
@@ -43,6 +43,10 @@ MAX_INTERVAL_NS = 100_000_000
 # the cut-off and so hold for these synthetic workloads only. HBM traffic = 2 x FETCH_SIZE + WRITE_SIZE
 # (MI355X_MICROARCH.md: gfx950 FETCH_SIZE counts half the bytes of wide coalesced reads).
 VALU_TABLE = os.path.join(HERE, "profiles", "valu_per_unit.json")
+
+
+# the K1 kernel the product runs: order-query statistics unless NMZ_REPLAY_OQ=0 selects the per-decision sweep
+K1_KERNEL = "k_replayable_sweep_fast" if os.environ.get("NMZ_REPLAY_OQ") == "0" else "k_replayable_sweep_oq"
 
 
 def valu_entry(kernel):
@@ -690,7 +694,7 @@ def headline_line(args, torch, D, ctx, L, stream):
         "config": {"workload": "configs[1] replayable seed sweep", "seeds_per_gpu": r["S"], "events": r["E"],
                    "max_interval_ns": MAX_INTERVAL_NS, "topk": 64, "pipeline_streams": r["pipeline"],
                    "parallelism": f"seed-range x{D.world}" + (" + RCCL all_gather top-k" if D.world > 1 else "")},
-        "roofline": roofline_valu("k_replayable_sweep_fast", dec_launch, r["kern_ms"]),
+        "roofline": roofline_valu(K1_KERNEL, dec_launch, r["kern_ms"]),
         # a new trace's plan (tables + segment sorts + allocations), median over the end-to-end traces;
         # plan_ms_first_three includes the process's first launches (module load) when the bench starts
         "plan_ms": float(np.median(r["e2e_plan_s"])) * 1e3,
@@ -705,6 +709,18 @@ def headline_line(args, torch, D, ctx, L, stream):
     }
     if line["roofline"]:
         rf = line["roofline"]
+        if K1_KERNEL == "k_replayable_sweep_oq":
+            # the order-query kernel does not decide event by event: its lane-instructions per decision are the
+            # per-seed searches spread over the 4,096 decisions they settle. The per-decision kernel's own
+            # ceiling (issue peak / its measured lane-instructions per decision) is the rate an ideal
+            # event-by-event sweep could reach on this chip.
+            rf["algorithm"] = ("order-query statistics: per (seed, hint-length class) binary searches over "
+                               "C-mod-m-sorted blocks (DESIGN.md section 4); units = seed x event decisions covered")
+            pd = valu_entry("k_replayable_sweep_fast")
+            if pd:
+                ceil = PEAK_VALU_TOPS * 1e12 / pd["ops_per_unit"]
+                rf["per_decision_ceiling"] = ceil
+                rf["vs_per_decision_ceiling"] = line["value"] / ceil
         rf["kernel_ms_source"] = "HIP events around every K1 launch of the timed region (on its stream)"
         rf["kernel_ms_isolated"] = r["kern_ms_isolated"]
         # the same lane-ops over the whole pipelined step (every kernel of the step on the clock)
