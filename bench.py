@@ -235,6 +235,7 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     it[0] = 0
     _lib.check(L.nmz_timing_enable(ctx.handle, 1))
     L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
+    L.nmz_timing_read_span(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
     D.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -245,8 +246,12 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     D.barrier()
     el = time.perf_counter() - t0
     _lib.check(L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
-    _lib.check(L.nmz_timing_enable(ctx.handle, 0))
     kern_ms_timed = tot.value / max(cnt.value, 1)
+    # the same launches' execution spans as the order-query kernel records them (first workgroup start to last
+    # workgroup end): a pipelined launch's HIP events also time its wait for the CUs another stream's K1 holds
+    _lib.check(L.nmz_timing_read_span(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
+    kern_ms_span = tot.value / cnt.value if cnt.value else None
+    _lib.check(L.nmz_timing_enable(ctx.handle, 0))
     merged = merge_topk(b"".join(o.cpu().numpy().tobytes() for o in outputs()), K_TOP)
     el_max = D.max(torch, el)
     stats = np.frombuffer(d_stats[0].cpu().numpy().tobytes(), dtype=_lib.SCHED_STATS_DTYPE)
@@ -271,8 +276,9 @@ def bench_replayable(args, torch, D, ctx, L, stream):
         d_tk.cpu()
         e2e.append(time.perf_counter() - t0)
         L.nmz_replayable_plan_destroy(plan)
-    return dict(S=S, E=E, hints=(hoff, hb), seeds=csr[0], elapsed=el_max, kern_ms=kern_ms_timed,
-                kern_ms_isolated=kern_ms, plan_ms=plan_ms, stats=stats, topk=merged, pipeline=NP,
+    return dict(S=S, E=E, hints=(hoff, hb), seeds=csr[0], elapsed=el_max,
+                kern_ms=kern_ms_span if kern_ms_span is not None else kern_ms_timed, kern_ms_events=kern_ms_timed,
+                kern_ms_span=kern_ms_span, kern_ms_isolated=kern_ms, plan_ms=plan_ms, stats=stats, topk=merged, pipeline=NP,
                 e2e_s=e2e, e2e_plan_s=e2e_plan)
 
 
@@ -721,7 +727,12 @@ def headline_line(args, torch, D, ctx, L, stream):
                 ceil = PEAK_VALU_TOPS * 1e12 / pd["ops_per_unit"]
                 rf["per_decision_ceiling"] = ceil
                 rf["vs_per_decision_ceiling"] = line["value"] / ceil
-        rf["kernel_ms_source"] = "HIP events around every K1 launch of the timed region (on its stream)"
+        if r["kern_ms_span"] is not None:
+            rf["kernel_ms_source"] = ("in-kernel execution span of every K1 launch of the timed region (wall_clock64 "
+                                      "at the first workgroup start and the last wave end, nmz_timing_read_span)")
+        else:
+            rf["kernel_ms_source"] = "HIP events around every K1 launch of the timed region (on its stream)"
+        rf["kernel_ms_events"] = r["kern_ms_events"]  # includes the wait for CUs held by another stream's K1
         rf["kernel_ms_isolated"] = r["kern_ms_isolated"]
         # the same lane-ops over the whole pipelined step (every kernel of the step on the clock)
         rf["frac_of_step"] = rf["ops_per_unit"] * dec_launch / (line["ms_per_step"] * 1e-3) / 1e12 / PEAK_VALU_TOPS

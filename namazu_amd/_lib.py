@@ -94,6 +94,8 @@ SIGNATURES = {
     "nmz_timing_enable": (_int, [_P, _int]),
     "nmz_timing_read": (_int, [_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                 ctypes.POINTER(_u64), _int]),
+    "nmz_timing_read_span": (_int, [_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                                ctypes.POINTER(_u64), _int]),
 }
 
 _lib = None

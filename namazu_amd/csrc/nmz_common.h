@@ -54,7 +54,12 @@ struct NmzTiming {
     bool enabled = false;
     std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> events;
     std::vector<hipEvent_t> pool;
+    // in-kernel execution spans: slot = {max ~start, max end} of wall_clock64() over the launch's workgroups
+    unsigned long long *span_dev = nullptr;
+    uint32_t span_next = 0;
+    std::map<std::string, std::vector<uint32_t>> spans;
 };
+constexpr uint32_t NMZ_SPAN_SLOTS = 4096;
 
 struct nmz_ctx {
     int device = 0;
@@ -76,6 +81,8 @@ struct KernelTimer {
     hipEvent_t a = nullptr, b = nullptr;
     KernelTimer(nmz_ctx *c, hipStream_t s, const char *n);
     ~KernelTimer();
+    // a fresh span slot for a kernel that records its own execution span (nullptr when timing is off)
+    unsigned long long *span();
 };
 
 // RAII: bind the calling OS thread to the context's device (cgo threads migrate).

@@ -57,6 +57,22 @@ KernelTimer::KernelTimer(nmz_ctx *c, hipStream_t s, const char *n) : ctx(c), st(
     if (a) (void)hipEventRecord(a, st);
 }
 
+unsigned long long *KernelTimer::span() {
+    if (!a || !b) return nullptr;
+    NmzTiming &t = ctx->timing;
+    if (!t.span_dev) {
+        if (hipMalloc(&t.span_dev, NMZ_SPAN_SLOTS * 16) != hipSuccess) {
+            t.span_dev = nullptr;
+            return nullptr;
+        }
+        if (hipMemset(t.span_dev, 0, NMZ_SPAN_SLOTS * 16) != hipSuccess) return nullptr;
+    }
+    if (t.span_next >= NMZ_SPAN_SLOTS) return nullptr;  // full until the next read with reset
+    const uint32_t slot = t.span_next++;
+    t.spans[name].push_back(slot);
+    return t.span_dev + 2 * slot;
+}
+
 KernelTimer::~KernelTimer() {
     if (!a || !b) return;
     (void)hipEventRecord(b, st);
@@ -236,6 +252,7 @@ int nmz_close(nmz_ctx *ctx) {
                 (void)hipEventDestroy(ab.second);
             }
         for (auto e : ctx->timing.pool) (void)hipEventDestroy(e);
+        if (ctx->timing.span_dev) (void)hipFree(ctx->timing.span_dev);
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     }
     delete ctx;
@@ -270,6 +287,36 @@ int nmz_timing_read(nmz_ctx *ctx, const char *kernel, double *total_ms, uint64_t
             ctx->timing.pool.push_back(ab.second);
         }
         it->second.clear();
+    }
+    return NMZ_OK;
+}
+
+int nmz_timing_read_span(nmz_ctx *ctx, const char *kernel, double *total_ms, uint64_t *count, int reset) {
+    NMZ_CHECK(ctx && kernel && total_ms && count, "NULL argument");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    *total_ms = 0;
+    *count = 0;
+    NmzTiming &t = ctx->timing;
+    if (!t.span_dev) return NMZ_OK;
+    NMZ_HIP(hipDeviceSynchronize());
+    std::vector<unsigned long long> h((size_t)NMZ_SPAN_SLOTS * 2);
+    NMZ_HIP(hipMemcpy(h.data(), t.span_dev, h.size() * 8, hipMemcpyDeviceToHost));
+    int khz = 0;
+    NMZ_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device));
+    NMZ_CHECK(khz > 0, "no wall clock rate");
+    auto it = t.spans.find(kernel);
+    if (it != t.spans.end())
+        for (uint32_t slot : it->second) {
+            const unsigned long long st = ~h[2 * slot], en = h[2 * slot + 1];
+            if (h[2 * slot] == 0 || en < st) continue;  // the launch had no work
+            *total_ms += (double)(en - st) / khz;
+            *count += 1;
+        }
+    if (reset) {  // every kernel's slots: the ring restarts empty
+        NMZ_HIP(hipMemset(t.span_dev, 0, NMZ_SPAN_SLOTS * 16));
+        t.spans.clear();
+        t.span_next = 0;
     }
     return NMZ_OK;
 }

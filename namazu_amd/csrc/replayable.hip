@@ -788,11 +788,12 @@ __global__ __launch_bounds__(OQ_WG) void k_replayable_sweep_oq(
     const uint32_t *__restrict__ sorted_idx, const uint4 *__restrict__ table, uint32_t E,
     const uint4 *__restrict__ blob, uint32_t rb16, const unsigned long long *__restrict__ rowsum,
     const OqClass *__restrict__ classes, uint32_t n_classes, uint32_t m, uint64_t mu, uint32_t m_k64,
-    nmz_sched_stats *__restrict__ stats) {
+    nmz_sched_stats *__restrict__ stats, unsigned long long *__restrict__ span) {
     extern __shared__ uint4 oq_lds[];
     const uint32_t L = blockIdx.x;
     const uint32_t s0 = bucket_off[L], s1 = bucket_off[L + 1];
     if (s0 == s1) return;
+    if (span && threadIdx.x == 0) atomicMax(span, ~(unsigned long long)wall_clock64());
     {
         const uint4 *__restrict__ src = blob + (uint64_t)L * rb16;
         constexpr uint32_t B = 4;  // loads in flight per thread
@@ -950,6 +951,7 @@ __global__ __launch_bounds__(OQ_WG) void k_replayable_sweep_oq(
         stats[sorted_idx[j]] = st;
     }
     }
+    if (span && (threadIdx.x & 63) == 0) atomicMax(span + 1, (unsigned long long)wall_clock64());
 }
 
 // general modulus (m >= 2^30, including uint64(negative duration)): one seed per lane
@@ -1170,7 +1172,7 @@ static int replayable_stats(nmz_replayable_plan *p, hipStream_t st, const uint32
         hipLaunchKernelGGL(k_replayable_sweep_oq, dim3(256), dim3(OQ_WG), p->oq_rb16 * 16u, st, sc.b.offset,
                            sc.b.sorted_h0, sc.b.sorted_idx, p->d_table, E, p->d_oq_blob, p->oq_rb16,
                            reinterpret_cast<const unsigned long long *>(p->d_oq_rowsum), p->d_oq_classes,
-                           p->n_classes, p->mod.m32, p->mod.mu, p->mod.m_k64, d_stats);
+                           p->n_classes, p->mod.m32, p->mod.mu, p->mod.m_k64, d_stats, kt.span());
         NMZ_HIP(hipGetLastError());
         return NMZ_OK;
     }
