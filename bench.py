@@ -728,8 +728,9 @@ def headline_line(args, torch, D, ctx, L, stream):
                 rf["per_decision_ceiling"] = ceil
                 rf["vs_per_decision_ceiling"] = line["value"] / ceil
         if r["kern_ms_span"] is not None:
-            rf["kernel_ms_source"] = ("in-kernel execution span of every K1 launch of the timed region (wall_clock64 "
-                                      "at the first workgroup start and the last wave end, nmz_timing_read_span)")
+            rf["kernel_ms_source"] = ("in-kernel execution spans of the timed region's K1 launches (wall_clock64 at "
+                                      "the first workgroup start and the last wave end, nmz_timing_read_span): the "
+                                      "union of the spans / launches, so overlapping launches share their time")
         else:
             rf["kernel_ms_source"] = "HIP events around every K1 launch of the timed region (on its stream)"
         rf["kernel_ms_events"] = r["kern_ms_events"]  # includes the wait for CUs held by another stream's K1

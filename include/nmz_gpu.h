@@ -110,7 +110,8 @@ int nmz_timing_enable(nmz_ctx *ctx, int on);
 int nmz_timing_read(nmz_ctx *ctx, const char *kernel, double *total_ms, uint64_t *count, int reset);
 /* The same kernels' execution spans as the kernels record them (first workgroup start to last workgroup end,
  * wall_clock64()), so launches that wait on the stream for another stream's kernels are not charged the
- * wait ("replayable_sweep" on the order-query path). reset clears every kernel's spans. */
+ * wait ("replayable_sweep" on the order-query path): total_ms = the length of the union of the spans
+ * (launches that overlap share their common time), count = launches. reset clears every kernel's spans. */
 int nmz_timing_read_span(nmz_ctx *ctx, const char *kernel, double *total_ms, uint64_t *count, int reset);
 
 /* FNV-1a 64 of each of n byte strings (CSR off[n+1] into bytes), one thread per string: the event

@@ -1,3 +1,4 @@
+#include <algorithm>
 #include <cstdlib>
 // Context management, error plumbing, parameter resolution and the seed
 // bucketing pass shared by the replayable and random sweeps.
@@ -306,13 +307,29 @@ int nmz_timing_read_span(nmz_ctx *ctx, const char *kernel, double *total_ms, uin
     NMZ_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device));
     NMZ_CHECK(khz > 0, "no wall clock rate");
     auto it = t.spans.find(kernel);
-    if (it != t.spans.end())
+    if (it != t.spans.end()) {
+        std::vector<std::pair<unsigned long long, unsigned long long>> iv;
         for (uint32_t slot : it->second) {
             const unsigned long long st = ~h[2 * slot], en = h[2 * slot + 1];
             if (h[2 * slot] == 0 || en < st) continue;  // the launch had no work
-            *total_ms += (double)(en - st) / khz;
-            *count += 1;
+            iv.push_back({st, en});
         }
+        // the union of the spans: launches of several streams that overlap share their common time
+        std::sort(iv.begin(), iv.end());
+        unsigned long long cur_s = 0, cur_e = 0, ticks = 0;
+        for (size_t i = 0; i < iv.size(); ++i) {
+            if (i == 0 || iv[i].first > cur_e) {
+                ticks += cur_e - cur_s;
+                cur_s = iv[i].first;
+                cur_e = iv[i].second;
+            } else if (iv[i].second > cur_e) {
+                cur_e = iv[i].second;
+            }
+        }
+        ticks += cur_e - cur_s;
+        *total_ms = (double)ticks / khz;
+        *count = iv.size();
+    }
     if (reset) {  // every kernel's slots: the ring restarts empty
         NMZ_HIP(hipMemset(t.span_dev, 0, NMZ_SPAN_SLOTS * 16));
         t.spans.clear();

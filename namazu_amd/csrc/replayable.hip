@@ -701,7 +701,11 @@ __global__ __launch_bounds__(256) void k_replayable_oq_levels(const uint4 *__res
                 const uint32_t b0 = i & ~(k - 1);
                 const uint32_t last = b0 < size ? min(b0 + k, size) - 1 : size - 1;
                 const uint64_t q = key[i < size ? i : last];
-                img[ci.lv[lv] + oq_skew(lo + i)] = make_uint2((uint32_t)(q >> 32), (uint32_t)q);
+                const uint2 w = make_uint2((uint32_t)(q >> 32), (uint32_t)q);
+                img[ci.lv[lv] + oq_skew(lo + i)] = w;
+                // the skew slot after every 32 entries repeats the entry before it, so the entry below phys(idx)
+                // is always at phys(idx) - 1
+                if (((lo + i) & 31) == 31) img[ci.lv[lv] + oq_skew(lo + i) + 1] = w;
             }
             __syncthreads();
         }
@@ -759,7 +763,7 @@ __device__ __forceinline__ void oq_search(const uint2 *__restrict__ img, const u
         const uint2 first = *reinterpret_cast<const uint2 *>(base + pb[k] * 8u + 8u * oq_skew(S - 1));
         const uint32_t q = (Q[k] >> 3) - pb[k];
         const uint32_t idx = q - ((q * 993u) >> 15);  // phys -> logical (q = idx + idx/32 < 33 * 32)
-        const uint2 c = *reinterpret_cast<const uint2 *>(base + Q[k] - (idx ? 8u + ((idx & 31) == 0 ? 8u : 0u) : 0u));
+        const uint2 c = *reinterpret_cast<const uint2 *>(base + Q[k] - 8u);  // idx - 1 (pad slots repeat it)
         const bool all = first.x < X[k];
         cnt[k] = all ? S : idx;
         wrap[k] = !all && idx == 0;
@@ -1058,7 +1062,8 @@ static int oq_build(nmz_replayable_plan *p, const std::vector<ClassInfo> &cls, h
     if (p->mod.kind != MOD_FAST || E == 0) return NMZ_OK;
     std::vector<OqClass> oc(cls.size());
     std::vector<uint4> tbl;
-    uint64_t len[4] = {0, 0, 0, 0};  // level 0, 1, 2 and samples (uint2 units)
+    uint64_t len[4] = {1, 0, 0, 0};  // level 0, 1, 2 and samples (uint2 units); slot 0 stays free, so the read
+                                     // below a block (unused when the count is 0) never leaves the image
     for (size_t c = 0; c < cls.size(); ++c) {
         const uint32_t n = cls[c].count;
         OqClass &o = oc[c];
