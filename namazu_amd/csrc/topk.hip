@@ -109,37 +109,33 @@ __device__ __forceinline__ void wave_merge(nmz_topk_entry &x, const nmz_topk_ent
 
 constexpr uint32_t TOPK_WAVE_LISTS = 32;  // lists merged per 1024-thread block
 
-// Merge up to 32 consecutive sorted lists of k (kp = pow2 >= k <= 64) into one: round 1 merges list
-// pairs straight from global memory (one pair per wave), later rounds through double-buffered LDS
-// slots; 5 rounds, 4 barriers, no LDS compare-exchange stages.
+// Merge up to 32 consecutive sorted lists of k (kp = pow2 >= k <= 64) into one: round 1 merges list pairs
+// straight from global memory (one pair per wave), later rounds pair wave w with wave w + n through one LDS
+// slot per wave (24 KB, so a block fits beside a K1 order-query workgroup); 5 rounds, 4 barriers.
 __global__ __launch_bounds__(1024) void k_topk_merge_wave(const nmz_topk_entry *__restrict__ in, uint32_t n_lists,
                                                           uint32_t k, uint32_t kp,
                                                           nmz_topk_entry *__restrict__ out) {
-    __shared__ nmz_topk_entry slot[2][TOPK_WAVE_LISTS / 2][64];
+    __shared__ nmz_topk_entry slot[TOPK_WAVE_LISTS / 2][64];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t l0 = (uint64_t)blockIdx.x * TOPK_WAVE_LISTS;
     auto load = [&](uint64_t l, uint32_t j) {
         return (l < n_lists && j < k) ? in[l * k + j] : topk_sentinel();
     };
-    nmz_topk_entry x = topk_sentinel();
     // round 1: wave w merges lists 2w, 2w+1
+    nmz_topk_entry x = lane < kp ? load(l0 + 2 * w, lane) : topk_sentinel();
     {
-        const uint64_t la = l0 + 2 * w;
-        x = lane < kp ? load(la, lane) : topk_sentinel();
-        const nmz_topk_entry yr = lane < kp ? load(la + 1, kp - 1 - lane) : topk_sentinel();
+        const nmz_topk_entry yr = lane < kp ? load(l0 + 2 * w + 1, kp - 1 - lane) : topk_sentinel();
         wave_merge(x, yr, kp, lane);
-        slot[0][w][lane] = x;
+        slot[w][lane] = x;
     }
-    uint32_t cur = 0;
-    for (uint32_t waves = TOPK_WAVE_LISTS / 4; waves >= 1; waves >>= 1) {
+    // rounds 2..5: wave w < n merges wave w + n's list (slots >= n are not written in that round)
+    for (uint32_t n = TOPK_WAVE_LISTS / 4; n >= 1; n >>= 1) {
         __syncthreads();
-        if (w < waves) {
-            x = slot[cur][2 * w][lane];
-            const nmz_topk_entry yr = lane < kp ? slot[cur][2 * w + 1][kp - 1 - lane] : topk_sentinel();
+        if (w < n) {
+            const nmz_topk_entry yr = lane < kp ? slot[w + n][kp - 1 - lane] : topk_sentinel();
             wave_merge(x, yr, kp, lane);
-            slot[cur ^ 1][w][lane] = x;
+            slot[w][lane] = x;
         }
-        cur ^= 1;
     }
     if (w == 0 && lane < k) out[(uint64_t)blockIdx.x * k + lane] = x;
 }

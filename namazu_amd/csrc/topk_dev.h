@@ -8,7 +8,6 @@ namespace nmz {
 constexpr uint32_t TOPK_CHUNK = 2048;
 constexpr uint32_t TOPK_THREADS = 256;
 constexpr uint32_t TOPK_PER_THREAD = TOPK_CHUNK / TOPK_THREADS;
-constexpr uint32_t TOPK_RANK_MAX = 512;   // survivors ranked by counting; more -> bitonic sort
 constexpr uint32_t TOPK_MERGE_SLOTS = 4096;  // LDS entries per merge block (96 KiB)
 
 __device__ inline bool topk_better(const nmz_topk_entry &a, const nmz_topk_entry &b) {
@@ -47,33 +46,16 @@ __device__ inline uint64_t topk_coarse(const nmz_topk_entry &x) {
     return ((uint64_t)x.n_fault << 48) | (bs >> 16);
 }
 
-// bitonic sort (best first) of the first `n` entries of s (n a power of two)
-__device__ void bitonic_sort_n(nmz_topk_entry *s, uint32_t n) {
-    for (uint32_t size = 2; size <= n; size <<= 1) {
-        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-            __syncthreads();
-            for (uint32_t t = threadIdx.x; t < n / 2; t += blockDim.x) {
-                uint32_t i = 2 * t - (t & (stride - 1));
-                uint32_t j = i + stride;
-                bool best_first = ((i & size) == 0);
-                nmz_topk_entry a = s[i], b = s[j];
-                bool swap = best_first ? topk_better(b, a) : topk_better(a, b);
-                if (swap) {
-                    s[i] = b;
-                    s[j] = a;
-                }
-            }
-        }
-    }
-    __syncthreads();
-}
-
+// LDS of one selection block: candidates up to TOPK_LDS_CAND (the coarse threshold leaves ~k of them unless
+// many entries tie on the coarse key), so the block fits beside a K1 order-query workgroup (<= 45 KB left on a CU)
+constexpr uint32_t TOPK_LDS_CAND = 512;
 struct TopkShared {
-    nmz_topk_entry cand[TOPK_CHUNK];
-    uint32_t cidx[TOPK_CHUNK];
+    nmz_topk_entry cand[TOPK_LDS_CAND];
+    uint32_t cidx[TOPK_LDS_CAND];
     uint64_t wkey[TOPK_THREADS];
     uint64_t tau;
     uint32_t ncand;
+    uint32_t win;
 };
 
 // The block's best k of its TOPK_CHUNK entries, sorted, to o[0..k). Thread t holds entries e[r] at chunk
@@ -106,20 +88,22 @@ __device__ inline void topk_block_select(const nmz_topk_entry (&e)[TOPK_PER_THRE
     __syncthreads();
     const uint64_t tau = sh.tau;
     // Sentinels (padding) rank after every real entry, so they never compete: they are left out
-    // of the candidates and fill the slots past the real ones (a block of padding alone would
-    // otherwise send 2048 equal entries to the bitonic sort).
+    // of the candidates and fill the slots past the real ones. Candidates are counted in full but stored only
+    // while they fit the LDS list.
 #pragma unroll
     for (uint32_t r = 0; r < TOPK_PER_THREAD; ++r) {
         if (ck[r] >= tau && !topk_is_sentinel(e[r])) {
             const uint32_t c = atomicAdd(&sh.ncand, 1u);
-            sh.cand[c] = e[r];
-            sh.cidx[c] = r * TOPK_THREADS + t;
+            if (c < TOPK_LDS_CAND) {
+                sh.cand[c] = e[r];
+                sh.cidx[c] = r * TOPK_THREADS + t;
+            }
         }
     }
     __syncthreads();
     const uint32_t c = sh.ncand;  // >= k unless the block holds fewer than k real entries
     for (uint32_t i = c + t; i < k; i += TOPK_THREADS) o[i] = topk_sentinel();
-    if (c <= TOPK_RANK_MAX) {
+    if (c <= TOPK_LDS_CAND) {
         for (uint32_t i = t; i < c; i += TOPK_THREADS) {
             const nmz_topk_entry x = sh.cand[i];
             const uint32_t xi = sh.cidx[i];
@@ -129,11 +113,31 @@ __device__ inline void topk_block_select(const nmz_topk_entry (&e)[TOPK_PER_THRE
         }
         return;
     }
-    uint32_t np = 2;
-    while (np < c) np <<= 1;
-    for (uint32_t i = c + t; i < np; i += TOPK_THREADS) sh.cand[i] = topk_sentinel();
-    bitonic_sort_n(sh.cand, np);
-    for (uint32_t i = t; i < k && i < c; i += TOPK_THREADS) o[i] = sh.cand[i];
+    // Many entries tie on the coarse key (e.g. equal sums): take the best k one at a time, each round a block
+    // reduction over every thread's best unused candidate.
+    uint32_t used = 0;
+    for (uint32_t i = 0; i < k && i < c; ++i) {
+        int br = -1;
+#pragma unroll
+        for (uint32_t r = 0; r < TOPK_PER_THREAD; ++r)
+            if (!((used >> r) & 1u) && ck[r] >= tau && !topk_is_sentinel(e[r]) &&
+                (br < 0 || topk_before(e[r], r * TOPK_THREADS + t, e[br], (uint32_t)br * TOPK_THREADS + t)))
+                br = (int)r;
+        sh.cand[t] = br >= 0 ? e[br] : topk_sentinel();
+        sh.cidx[t] = br >= 0 ? (uint32_t)br * TOPK_THREADS + t : UINT32_MAX;
+        __syncthreads();
+        for (uint32_t st = TOPK_THREADS / 2; st; st >>= 1) {
+            if (t < st && topk_before(sh.cand[t + st], sh.cidx[t + st], sh.cand[t], sh.cidx[t])) {
+                sh.cand[t] = sh.cand[t + st];
+                sh.cidx[t] = sh.cidx[t + st];
+            }
+            __syncthreads();
+        }
+        const uint32_t win = sh.cidx[0];
+        if (t == 0) o[i] = sh.cand[0];
+        if (win % TOPK_THREADS == t) used |= 1u << (win / TOPK_THREADS);
+        __syncthreads();
+    }
 }
 
 }  // namespace nmz

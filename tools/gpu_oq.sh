@@ -2,7 +2,7 @@
 # statistics (default) and with the per-decision sweep (NMZ_REPLAY_OQ=0)
 tag=$1
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_sweeps_gpu.py tests/test_configs_gpu.py -k "replayable or config1" \
+timeout -k 10 300 python -u -m pytest tests/test_sweeps_gpu.py tests/test_configs_gpu.py -k "replayable or config1 or topk or random" \
   -x -v --timeout 120 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> gpurun_out/${tag}_tests.log
