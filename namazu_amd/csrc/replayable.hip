@@ -160,52 +160,52 @@ __global__ __launch_bounds__(256) void k_replayable_table_sort(const uint4 *__re
 
 // Sort one (class, row L) segment per workgroup in LDS: bitonic sort of (C, position) pairs padded to a power of
 // two (the position makes keys distinct, so the order equals the stable C order of k_replayable_table_sort), then
-// a gather of the table entries in that order. Segments of up to SEG_SORT_MAX entries (48 KiB of LDS); larger
-// classes keep the counting kernel above.
+// a gather of the table entries in that order. 1,024 threads, each compare-exchange pair computed directly from
+// the thread index (no idle iterations). Segments of up to SEG_SORT_MAX entries (40 KiB of LDS); larger classes
+// keep the counting kernel above.
 constexpr uint32_t SEG_SORT_MAX = 4096;
 
-__global__ __launch_bounds__(256) void k_replayable_table_segsort(const uint4 *__restrict__ tmp,
-                                                                  const ClassInfo *__restrict__ classes, uint32_t E,
-                                                                  uint4 *__restrict__ table) {
+__global__ __launch_bounds__(1024) void k_replayable_table_segsort(const uint4 *__restrict__ tmp,
+                                                                   const ClassInfo *__restrict__ classes, uint32_t E,
+                                                                   uint4 *__restrict__ table) {
     __shared__ uint64_t key[SEG_SORT_MAX];
-    __shared__ uint32_t pos[SEG_SORT_MAX];
+    __shared__ uint16_t pos[SEG_SORT_MAX];
     const ClassInfo ci = classes[blockIdx.x];
     const uint32_t L = blockIdx.y, n = ci.count;
     if (n > SEG_SORT_MAX || n == 0) return;
     uint32_t p2 = 1;
     while (p2 < n) p2 <<= 1;
     const uint4 *__restrict__ src = tmp + (uint64_t)L * E + ci.start;
-    for (uint32_t i = threadIdx.x; i < p2; i += 256) {
+    for (uint32_t i = threadIdx.x; i < p2; i += blockDim.x) {
         if (i < n) {
             const uint4 q = src[i];
             key[i] = ((uint64_t)q.y << 32) | q.x;
         } else {
             key[i] = UINT64_MAX;
         }
-        pos[i] = i;
+        pos[i] = (uint16_t)i;
     }
     __syncthreads();
     for (uint32_t k = 2; k <= p2; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = threadIdx.x; i < p2; i += 256) {
-                const uint32_t l = i ^ j;
-                if (l > i) {
-                    const uint64_t ki = key[i], kl = key[l];
-                    const uint32_t pi = pos[i], pl = pos[l];
-                    const bool gt = ki > kl || (ki == kl && pi > pl);
-                    if (((i & k) == 0) == gt) {  // ascending half: swap if i > l; descending half: if i < l
-                        key[i] = kl;
-                        key[l] = ki;
-                        pos[i] = pl;
-                        pos[l] = pi;
-                    }
+            const uint32_t lj = 31 - __builtin_clz(j);
+            for (uint32_t p = threadIdx.x; p < p2 / 2; p += blockDim.x) {
+                const uint32_t i = ((p >> lj) << (lj + 1)) | (p & (j - 1)), l = i + j;
+                const uint64_t ki = key[i], kl = key[l];
+                const uint32_t pi = pos[i], pl = pos[l];
+                const bool gt = ki > kl || (ki == kl && pi > pl);
+                if (((i & k) == 0) == gt) {  // ascending half: swap if i > l; descending half: if i < l
+                    key[i] = kl;
+                    key[l] = ki;
+                    pos[i] = (uint16_t)pl;
+                    pos[l] = (uint16_t)pi;
                 }
             }
             __syncthreads();
         }
     }
     uint4 *__restrict__ dst = table + (uint64_t)L * E + ci.start;
-    for (uint32_t i = threadIdx.x; i < n; i += 256) dst[i] = src[pos[i]];
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[pos[i]];
 }
 
 // ---------------------------------------------------------------------------
@@ -1318,7 +1318,7 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
         for (const ClassInfo &c : cls) max_class = std::max(max_class, c.count);
         bool bad = false;
         if (max_class <= SEG_SORT_MAX && !getenv("NMZ_REPLAY_RANKSORT")) {  // LDS bitonic sort per segment
-            hipLaunchKernelGGL(k_replayable_table_segsort, dim3(p->n_classes, 256), dim3(256), 0, st, tmp.as<uint4>(),
+            hipLaunchKernelGGL(k_replayable_table_segsort, dim3(p->n_classes, 256), dim3(1024), 0, st, tmp.as<uint4>(),
                                p->d_classes, E, p->d_table);
             bad = hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess;
         } else if (max_class <= 16384) {  // O(n^2) rank sort on the device
