@@ -37,10 +37,13 @@ int fail(int code, const std::string &msg);
         if (rc_ != NMZ_OK) return rc_;                                                  \
     } while (0)
 
-// Grow-only device scratch buffer owned by a context.
+// Grow-only device scratch buffer owned by a context. With a pool (a plan's buffers: the context's list of
+// free buffers), release() hands the memory back to the pool and ensure() reuses a pooled buffer before it
+// allocates, so creating and destroying plans does not hipMalloc / hipFree (hipFree synchronises the device).
 struct DevBuf {
     void *ptr = nullptr;
     size_t cap = 0;
+    std::vector<DevBuf> *pool = nullptr;
     int ensure(size_t bytes);
     void release();
     template <typename T>
@@ -68,6 +71,7 @@ struct nmz_ctx {
     int n_cu = 0;
     // scratch slots reused across calls (host-pointer entry points)
     nmz::DevBuf buf[16];
+    std::vector<nmz::DevBuf> pool;  // free plan buffers (DevBuf::pool), freed by nmz_close
     NmzTiming timing;
 };
 

@@ -22,10 +22,22 @@ int fail(int code, const std::string &msg) {
 
 int DevBuf::ensure(size_t bytes) {
     if (bytes <= cap) return NMZ_OK;
-    if (ptr) (void)hipFree(ptr);
-    ptr = nullptr;
-    cap = 0;
+    release();
     size_t want = bytes < 256 ? 256 : bytes;
+    if (pool) {  // best fit among the pooled buffers (at most 4x the request, so small plans leave large ones)
+        size_t best = pool->size();
+        for (size_t i = 0; i < pool->size(); ++i)
+            if ((*pool)[i].cap >= want && (*pool)[i].cap <= 4 * want &&
+                (best == pool->size() || (*pool)[i].cap < (*pool)[best].cap))
+                best = i;
+        if (best < pool->size()) {
+            ptr = (*pool)[best].ptr;
+            cap = (*pool)[best].cap;
+            (*pool)[best] = pool->back();
+            pool->pop_back();
+            return NMZ_OK;
+        }
+    }
     if (hipMalloc(&ptr, want) != hipSuccess) {
         ptr = nullptr;
         return fail(NMZ_ENOMEM, "hipMalloc of " + std::to_string(want) + " bytes failed");
@@ -35,7 +47,16 @@ int DevBuf::ensure(size_t bytes) {
 }
 
 void DevBuf::release() {
-    if (ptr) (void)hipFree(ptr);
+    if (ptr) {
+        if (pool) {
+            DevBuf b;
+            b.ptr = ptr;
+            b.cap = cap;
+            pool->push_back(b);
+        } else {
+            (void)hipFree(ptr);
+        }
+    }
     ptr = nullptr;
     cap = 0;
 }
@@ -247,6 +268,8 @@ int nmz_close(nmz_ctx *ctx) {
     {
         CtxGuard g(ctx);
         for (auto &b : ctx->buf) b.release();
+        for (auto &b : ctx->pool) (void)hipFree(b.ptr);
+        ctx->pool.clear();
         for (auto &kv : ctx->timing.events)
             for (auto &ab : kv.second) {
                 (void)hipEventDestroy(ab.first);

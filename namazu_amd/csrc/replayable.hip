@@ -1246,6 +1246,7 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
     *out = nullptr;
     auto *p = new nmz_replayable_plan();
     p->ctx = ctx;
+    for (DevBuf *b : {&p->seed_scratch, &p->partial, &p->topk_lists, &p->plan_mem, &p->oq_mem}) b->pool = &ctx->pool;
     p->n_events = E;
     p->max_interval = max_interval;
     p->mod = make_mod((uint64_t)max_interval);  // uint64(r.MaxInterval), replayablepolicy.go:110
@@ -1283,7 +1284,9 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
         }
     }
     if (rc != NMZ_OK) {
+        (void)hipStreamSynchronize(st);
         p->plan_mem.release();
+        p->seed_scratch.release();
         delete p;
         return rc;
     }
@@ -1294,6 +1297,7 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
     uint32_t *d_hoff = p->d_hoff = cv.take<uint32_t>(E + 1);
     uint8_t *d_hbytes = p->d_hbytes = cv.take<uint8_t>(nbytes + 1);
     auto cleanup = [&](int code) {
+        (void)hipStreamSynchronize(st);  // pooled buffers: no work may still use them
         p->plan_mem.release();
         p->seed_scratch.release();
         p->partial.release();
@@ -1371,6 +1375,9 @@ int nmz_replayable_plan_destroy(nmz_replayable_plan *plan) {
     if (!plan) return NMZ_OK;
     {
         CtxGuard g(plan->ctx);
+        // the buffers go back to the context's pool, where the next plan may write them at once: wait for the
+        // work still reading them (hipFree, which this replaces, synchronised the device as well)
+        (void)hipDeviceSynchronize();
         plan->plan_mem.release();
         plan->seed_scratch.release();
         plan->partial.release();
@@ -1416,6 +1423,7 @@ int nmz_replayable_sweep(nmz_ctx *ctx, const uint32_t *seed_off, const uint8_t *
     struct PlanGuard {
         nmz_replayable_plan *p;
         ~PlanGuard() {
+            (void)hipStreamSynchronize(p->ctx->stream);  // pooled buffers: no work may still use them
             p->plan_mem.release();
             p->seed_scratch.release();
             p->partial.release();
