@@ -158,54 +158,123 @@ __global__ __launch_bounds__(256) void k_replayable_table_sort(const uint4 *__re
     if (p < E) table[(uint64_t)L * E + cs + rank] = x;
 }
 
-// Sort one (class, row L) segment per workgroup in LDS: bitonic sort of (C, position) pairs padded to a power of
-// two (the position makes keys distinct, so the order equals the stable C order of k_replayable_table_sort), then
-// a gather of the table entries in that order. 1,024 threads, each compare-exchange pair computed directly from
-// the thread index (no idle iterations). Segments of up to SEG_SORT_MAX entries (40 KiB of LDS); larger classes
-// keep the counting kernel above.
+// Sort one (class, row L) segment per workgroup in LDS by (C, position) -- the stable C order of
+// k_replayable_table_sort -- then gather the table entries in that order. C is an FNV-derived 64-bit value, so a
+// counting sort on its top 12 bits leaves ~n/4096 entries per bucket; each bucket is finished by one thread
+// (insertion sort). A segment whose largest bucket exceeds SEG_BUCKET_MAX (adversarial C values) takes a bitonic
+// sort instead. Segments of up to SEG_SORT_MAX entries; larger classes keep the counting kernel above.
 constexpr uint32_t SEG_SORT_MAX = 4096;
+constexpr uint32_t SEG_BUCKETS = 4096;
+constexpr uint32_t SEG_BUCKET_MAX = 32;
 
 __global__ __launch_bounds__(1024) void k_replayable_table_segsort(const uint4 *__restrict__ tmp,
                                                                    const ClassInfo *__restrict__ classes, uint32_t E,
                                                                    uint4 *__restrict__ table) {
     __shared__ uint64_t key[SEG_SORT_MAX];
     __shared__ uint16_t pos[SEG_SORT_MAX];
+    __shared__ uint32_t cnt[SEG_BUCKETS];
+    __shared__ uint32_t wsum[16], maxb;
     const ClassInfo ci = classes[blockIdx.x];
-    const uint32_t L = blockIdx.y, n = ci.count;
+    const uint32_t L = blockIdx.y, n = ci.count, t = threadIdx.x;
     if (n > SEG_SORT_MAX || n == 0) return;
-    uint32_t p2 = 1;
-    while (p2 < n) p2 <<= 1;
     const uint4 *__restrict__ src = tmp + (uint64_t)L * E + ci.start;
-    for (uint32_t i = threadIdx.x; i < p2; i += blockDim.x) {
+    for (uint32_t i = t; i < SEG_BUCKETS; i += blockDim.x) cnt[i] = 0;
+    if (t == 0) maxb = 0;
+    __syncthreads();
+    uint64_t mine[SEG_SORT_MAX / 1024];
+#pragma unroll
+    for (uint32_t r = 0; r < SEG_SORT_MAX / 1024; ++r) {
+        const uint32_t i = r * 1024 + t;
+        mine[r] = 0;
         if (i < n) {
             const uint4 q = src[i];
-            key[i] = ((uint64_t)q.y << 32) | q.x;
-        } else {
-            key[i] = UINT64_MAX;
+            mine[r] = ((uint64_t)q.y << 32) | q.x;
+            atomicAdd(&cnt[mine[r] >> 52], 1u);
         }
-        pos[i] = (uint16_t)i;
     }
     __syncthreads();
-    for (uint32_t k = 2; k <= p2; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            const uint32_t lj = 31 - __builtin_clz(j);
-            for (uint32_t p = threadIdx.x; p < p2 / 2; p += blockDim.x) {
-                const uint32_t i = ((p >> lj) << (lj + 1)) | (p & (j - 1)), l = i + j;
-                const uint64_t ki = key[i], kl = key[l];
-                const uint32_t pi = pos[i], pl = pos[l];
-                const bool gt = ki > kl || (ki == kl && pi > pl);
-                if (((i & k) == 0) == gt) {  // ascending half: swap if i > l; descending half: if i < l
-                    key[i] = kl;
-                    key[l] = ki;
-                    pos[i] = (uint16_t)pl;
-                    pos[l] = (uint16_t)pi;
-                }
+    // exclusive scan of the 4096 counts: 4 per thread, wave scans, then the 16 wave totals
+    uint32_t c4[4], tot = 0, mx = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < 4; ++r) {
+        c4[r] = cnt[4 * t + r];
+        tot += c4[r];
+        mx = max(mx, c4[r]);
+    }
+    const uint32_t lane = t & 63, w = t >> 6;
+    uint32_t inc = tot;
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += v;
+    }
+    if (lane == 63) wsum[w] = inc;
+    atomicMax(&maxb, mx);
+    __syncthreads();
+    uint32_t base = inc - tot;
+    for (uint32_t j = 0; j < w; ++j) base += wsum[j];
+#pragma unroll
+    for (uint32_t r = 0; r < 4; ++r) {
+        cnt[4 * t + r] = base;  // bucket start, advanced by the scatter below
+        base += c4[r];
+    }
+    __syncthreads();
+    if (maxb <= SEG_BUCKET_MAX) {
+#pragma unroll
+        for (uint32_t r = 0; r < SEG_SORT_MAX / 1024; ++r) {
+            const uint32_t i = r * 1024 + t;
+            if (i < n) {
+                const uint32_t slot = atomicAdd(&cnt[mine[r] >> 52], 1u);
+                key[slot] = mine[r];
+                pos[slot] = (uint16_t)i;
             }
-            __syncthreads();
+        }
+        __syncthreads();
+        // cnt[b] is now the end of bucket b; one thread per bucket sorts its few entries by (C, position)
+        for (uint32_t b = t; b < SEG_BUCKETS; b += blockDim.x) {
+            const uint32_t e1 = cnt[b], e0 = b ? cnt[b - 1] : 0;
+            for (uint32_t i = e0 + 1; i < e1; ++i) {
+                const uint64_t k = key[i];
+                const uint16_t p = pos[i];
+                uint32_t j = i;
+                while (j > e0 && (key[j - 1] > k || (key[j - 1] == k && pos[j - 1] > p))) {
+                    key[j] = key[j - 1];
+                    pos[j] = pos[j - 1];
+                    --j;
+                }
+                key[j] = k;
+                pos[j] = p;
+            }
+        }
+        __syncthreads();
+    } else {  // bitonic sort of (C, position) padded to a power of two
+        uint32_t p2 = 1;
+        while (p2 < n) p2 <<= 1;
+        for (uint32_t i = t; i < p2; i += blockDim.x) {
+            key[i] = i < n ? (((uint64_t)src[i].y << 32) | src[i].x) : UINT64_MAX;
+            pos[i] = (uint16_t)i;
+        }
+        __syncthreads();
+        for (uint32_t k = 2; k <= p2; k <<= 1) {
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                const uint32_t lj = 31 - __builtin_clz(j);
+                for (uint32_t p = t; p < p2 / 2; p += blockDim.x) {
+                    const uint32_t i = ((p >> lj) << (lj + 1)) | (p & (j - 1)), l = i + j;
+                    const uint64_t ki = key[i], kl = key[l];
+                    const uint32_t pi = pos[i], pl = pos[l];
+                    const bool gt = ki > kl || (ki == kl && pi > pl);
+                    if (((i & k) == 0) == gt) {  // ascending half: swap if i > l; descending half: if i < l
+                        key[i] = kl;
+                        key[l] = ki;
+                        pos[i] = (uint16_t)pl;
+                        pos[l] = (uint16_t)pi;
+                    }
+                }
+                __syncthreads();
+            }
         }
     }
     uint4 *__restrict__ dst = table + (uint64_t)L * E + ci.start;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[pos[i]];
+    for (uint32_t i = t; i < n; i += blockDim.x) dst[i] = src[pos[i]];
 }
 
 // ---------------------------------------------------------------------------
@@ -1324,7 +1393,9 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
         if (max_class <= SEG_SORT_MAX && !getenv("NMZ_REPLAY_RANKSORT")) {  // LDS bitonic sort per segment
             hipLaunchKernelGGL(k_replayable_table_segsort, dim3(p->n_classes, 256), dim3(1024), 0, st, tmp.as<uint4>(),
                                p->d_classes, E, p->d_table);
-            bad = hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess;
+            // no sync when the order-query images follow: oq_build synchronises after its kernels
+            bad = hipGetLastError() != hipSuccess ||
+                  (p->mod.kind != MOD_FAST && hipStreamSynchronize(st) != hipSuccess);
         } else if (max_class <= 16384) {  // O(n^2) rank sort on the device
             hipLaunchKernelGGL(k_replayable_table_sort, dim3(ceil_div(E, 256), 256), dim3(256), 0, st,
                                tmp.as<uint4>(), p->d_classes, p->n_classes, E, p->d_table);
@@ -1351,6 +1422,8 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
             return cleanup(fail(NMZ_EHIP, "plan table kernel failed"));
         const int orc = oq_build(p, cls, st);
         if (orc != NMZ_OK) return cleanup(orc);
+        // the plan is complete before it is returned: sweeps may run on any stream
+        if (!p->oq && hipStreamSynchronize(st) != hipSuccess) return cleanup(fail(NMZ_EHIP, "plan build failed"));
     }
     *out = p;
     return NMZ_OK;
