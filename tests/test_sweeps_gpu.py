@@ -82,6 +82,22 @@ def test_replayable_order_query_block_edges(ctx, m):
     assert np.array_equal(r.stats, st) and np.array_equal(r.delays, dl)
 
 
+def test_replayable_repeated_hints_plan_sort_fallback(ctx):
+    """Many identical hints give identical C values in every table row, so one top-12-bit bucket of the plan's
+    segment sort overflows and the segment takes the bitonic sort; ties in C must keep the event order."""
+    rng = np.random.default_rng(7)
+    hints = ["1234567890123456789"] * 150 + zk_hints(60, rng) + ["-123456789012345678"] * 40
+    hints = [hints[i] for i in rng.permutation(len(hints))]
+    seeds = [str(i) for i in range(500)]
+    for m in [100_000_000, 7]:
+        p = Replayable()
+        p.MaxInterval = m
+        r = p.Sweep(seeds, hints, n_dump=2, k=8, ctx=ctx)
+        st, dl = rep_oracle(seeds, hints, m, n_dump=2)
+        assert np.array_equal(r.stats, st) and np.array_equal(r.delays, dl)
+        assert np.array_equal(r.topk, O.topk_from_stats(st, 0, 8))
+
+
 @pytest.mark.parametrize("E", [1, 3, 63, 64, 65, 127, 2047, 2048, 2049, 4097, 9000])
 def test_replayable_event_counts_around_stage_and_chunk_edges(ctx, E):
     """K1 stages 64 events at a time (the next chunk's load is clamped to the last event) and works in
