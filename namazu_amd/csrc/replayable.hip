@@ -854,8 +854,158 @@ __device__ __forceinline__ void oq_accum(int side, uint32_t rs, uint32_t cnt, ui
     key = k > key ? k : key;
 }
 
+// One seed's statistics over one class segment (replayablepolicy.go:100-114 restated per segment, see above):
+// adds d Hm + (n - d) Hm2 to sum, the segment's wraps to W, and folds its maximum key {t, ~e} into key.
+__device__ __forceinline__ void oq_seed_class(const OqClass &ci, const uint2 *__restrict__ img,
+                                              const uint4 *__restrict__ row, uint64_t h0, uint32_t m, uint64_t mu,
+                                              uint32_t m_k64, uint64_t &sum, uint32_t &W, uint64_t &key) {
+    const uint32_t n = ci.count, cs = ci.start;
+    const uint64_t H = h0 * ci.pn;
+    const uint64_t nH = ~H;
+    const uint32_t Hm = mod_barrett_small(H, m, mu);
+    const uint32_t t2 = Hm + m_k64;
+    const uint32_t Hm2 = min(t2, t2 - m);
+    uint32_t d = 0;
+    if (n <= OQ_BRUTE) {
+        for (uint32_t i = 0; i < n; ++i) oq_decide(row[cs + i], nH, Hm, Hm2, m, d, W, key);
+    } else {
+        const uint32_t XA = m - Hm, XB = m - Hm2;
+        const uint32_t ns = (n + 7) >> 3, nt = (n + OQ_S0 - 1) / OQ_S0;
+        // 8-event blocks whose first C is <= ~H are carry-free up to that entry: binary search over the
+        // samples (the C of every 8th entry, ascending; slots past ns hold whatever, so the count is clamped)
+        uint32_t ks;
+        {
+            const uint32_t sb = ci.samp;
+            uint32_t Q = sb;
+            for (uint32_t st = ci.samp_p2 >> 1; st; st >>= 1) {
+                const uint2 v = img[Q + oq_off(st)];
+                Q = ((((uint64_t)v.y) << 32) | v.x) <= nH ? Q + oq_inc(st) : Q;
+            }
+            const uint32_t q = Q - sb;
+            const uint32_t k0 = q - ((q * 993u) >> 15);
+            const uint2 v = img[Q];  // the last slot the lifting cannot reach
+            ks = min(k0 + (((((uint64_t)v.y) << 32) | v.x) <= nH ? 1u : 0u), ns);
+        }
+        const uint32_t b8 = ks ? 8 * (ks - 1) : 0;  // the 8-block holding the carry boundary
+        const uint32_t be = b8 + 8;
+        {
+            const uint32_t nb = min(8u, n - b8);
+            // decided event by event; the eight loads are issued together and the updates are selects (a
+            // guarded update had let the compiler sink each load into its own branch and wait for it there)
+            uint4 q[8];
+#pragma unroll
+            for (uint32_t i = 0; i < 8; ++i) q[i] = row[cs + b8 + min(i, nb - 1)];
+#pragma unroll
+            for (uint32_t i = 0; i < 8; ++i) {
+                uint32_t dd = 0, ww = 0;
+                uint64_t kk = 0;
+                oq_decide(q[i], nH, Hm, Hm2, m, dd, ww, kk);
+                const bool in = i < nb;
+                d += in ? dd : 0u;
+                W += in ? ww : 0u;
+                key = (in && kk > key) ? kk : key;
+            }
+        }
+        d += b8;
+        const uint32_t pad1 = oq_round(n, OQ_S1);
+        // level 0: every 512-block of the segment, two at a time (this lane's boundary block is searched
+        // and dropped)
+        for (uint32_t b = 0; b < nt; b += 2) {
+            uint32_t pb[2], X[2], cn[2];
+            uint2 cand[2];
+            bool wr[2];
+            int side[2];
+            uint32_t rs[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t lo = min(b + k, nt - 1) * OQ_S0, hi = min(lo + OQ_S0, n);
+                side[k] = b + k >= nt ? 0 : hi <= b8 ? 1 : lo >= be ? 2 : 0;
+                X[k] = side[k] == 2 ? XB : XA;
+                pb[k] = ci.lv[0] + oq_skew(lo);
+                rs[k] = hi - lo;
+            }
+            if (__builtin_amdgcn_ballot_w64(side[0] != 0 || side[1] != 0)) {  // n <= 512: boundary only
+                oq_search<2, 0, 0>(img, pb, X, cn, cand, wr);
+#pragma unroll
+                for (int k = 0; k < 2; ++k) oq_accum(side[k], rs[k], cn[k], cand[k], wr[k], Hm, Hm2, m, W, key);
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // level 1: the eight 64-blocks of the boundary 512-block, 4 at a time
+            const uint32_t lt = (b8 & ~(OQ_S0 - 1)) + h * 4 * OQ_S1;
+            uint32_t pb[4], X[4], cn[4], rs[4];
+            int side[4];
+            uint2 cand[4];
+            bool wr[4], any = false;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t lo = lt + k * OQ_S1, hi = min(lo + OQ_S1, n);
+                side[k] = lo >= n ? 0 : hi <= b8 ? 1 : lo >= be ? 2 : 0;
+                any |= side[k] != 0;
+                X[k] = side[k] == 2 ? XB : XA;
+                pb[k] = ci.lv[1] + oq_skew(min(lo, pad1 - OQ_S1));
+                rs[k] = hi - lo;
+            }
+            if (__builtin_amdgcn_ballot_w64(any)) {
+                oq_search<0, 4, 0>(img, pb, X, cn, cand, wr);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) oq_accum(side[k], rs[k], cn[k], cand[k], wr[k], Hm, Hm2, m, W, key);
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // level 2: the 8-blocks of the boundary 64-block, less the one decided above
+            const uint32_t lm = (b8 & ~(OQ_S1 - 1)) + h * 4 * OQ_S2;
+            uint32_t pb[4], X[4], cn[4], rs[4];
+            int side[4];
+            uint2 cand[4];
+            bool wr[4], any = false;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t lo = lm + k * OQ_S2, hi = min(lo + OQ_S2, n);
+                side[k] = (lo >= n || lo == b8) ? 0 : lo < b8 ? 1 : 2;
+                any |= side[k] != 0;
+                X[k] = side[k] == 2 ? XB : XA;
+                pb[k] = ci.lv[2] + oq_skew(min(lo, pad1 - OQ_S2));
+                rs[k] = hi - lo;
+            }
+            if (__builtin_amdgcn_ballot_w64(any)) {
+                oq_search<0, 0, 4>(img, pb, X, cn, cand, wr);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) oq_accum(side[k], rs[k], cn[k], cand[k], wr[k], Hm, Hm2, m, W, key);
+            }
+        }
+    }
+    sum += (uint64_t)d * Hm + (uint64_t)(n - d) * Hm2;
+}
+
+__device__ __forceinline__ void oq_store(nmz_sched_stats *__restrict__ stats, uint32_t idx, uint64_t sum,
+                                         uint64_t key) {
+    nmz_sched_stats st;
+    st.sum_delay_ns = sum;
+    st.max_delay_ns = (int64_t)(key >> 32);
+    st.argmax_event = ~(uint32_t)key;
+    st.n_fault = 0;
+    st.first_fault = NMZ_NONE;
+    st.flags = 0;
+    stats[idx] = st;
+}
+
+#ifdef OQ_TRACE
+// debug builds only (-DOQ_TRACE): wall_clock64 per (row, wave) at the kernel start [9], after staging [0], at the
+// end of each of up to 7 seed chunks [1..7] and after the cooperative tail [8]; read with nmz_debug_oq_trace
+__device__ unsigned long long g_oq_trace[256][16][10];
+#endif
+
 // One workgroup per row L (256 workgroups, one per CU): the row image is staged into LDS once, then the 16
-// waves take the row's seeds 64 at a time (all seeds of a bucket share the row).
+// waves take the row's seeds in chunks of 64 from an LDS counter. A chunk is a chain of dependent LDS searches
+// (~19 us for a wave alone, 20-45 us beside 15 others): with a fixed share of chunks per wave the row waited
+// for the waves the SIMD arbiter served last (a row of 4 chunks per wave ended at ~140 us with its median wave
+// done at ~110). The row's last partial chunk (ns % 64 seeds) is shared by the waves as they finish: each
+// takes a subset of its class segments, and the partial statistics meet in LDS (u64 add and max are
+// associative), so it costs about one class chain instead of a whole chunk.
+constexpr uint32_t OQ_TAIL = 64;
+constexpr uint32_t OQ_TAIL_LDS = OQ_TAIL * 16 + 16;  // {sum, key} per tail seed + the chunk counter
+
 __global__ __launch_bounds__(OQ_WG) void k_replayable_sweep_oq(
     const uint32_t *__restrict__ bucket_off, const uint64_t *__restrict__ sorted_h0,
     const uint32_t *__restrict__ sorted_idx, const uint4 *__restrict__ table, uint32_t E,
@@ -867,164 +1017,92 @@ __global__ __launch_bounds__(OQ_WG) void k_replayable_sweep_oq(
     const uint32_t s0 = bucket_off[L], s1 = bucket_off[L + 1];
     if (s0 == s1) return;
     if (span && threadIdx.x == 0) atomicMax(span, ~(unsigned long long)wall_clock64());
+#ifdef OQ_TRACE
+    if ((threadIdx.x & 63) == 0) {
+        for (int k = 0; k < 10; ++k) g_oq_trace[L][threadIdx.x >> 6][k] = 0;
+        g_oq_trace[L][threadIdx.x >> 6][9] = wall_clock64();
+    }
+#endif
+    const uint32_t ns_row = s1 - s0;
+    const uint32_t rem = ns_row % 64;
+    const uint32_t tail = rem;  // the partial chunk, shared by all waves
+    const uint32_t smain = s1 - tail, nch = (smain - s0) / 64;
+    unsigned long long *tacc = reinterpret_cast<unsigned long long *>(oq_lds + rb16);  // [OQ_TAIL][2]
+    uint32_t *ctr = reinterpret_cast<uint32_t *>(tacc + 2 * OQ_TAIL);
     {
         const uint4 *__restrict__ src = blob + (uint64_t)L * rb16;
-        constexpr uint32_t B = 4;  // loads in flight per thread
+        // every load of a pass in flight at once: loads and stores unconditional, indices clamped to the image
+        // (guarded loads had compiled to one wait per load plus scratch copies)
+        constexpr uint32_t B = 8;  // 128 KB per pass
         for (uint32_t i0 = 0; i0 < rb16; i0 += B * OQ_WG) {
             uint4 v[B];
 #pragma unroll
-            for (uint32_t k = 0; k < B; ++k) {
-                const uint32_t i = i0 + k * OQ_WG + threadIdx.x;
-                if (i < rb16) v[k] = src[i];
-            }
+            for (uint32_t k = 0; k < B; ++k) v[k] = src[min(i0 + k * OQ_WG + threadIdx.x, rb16 - 1)];
+            // the clamped slots all write the image's last entry to its own place
 #pragma unroll
-            for (uint32_t k = 0; k < B; ++k) {
-                const uint32_t i = i0 + k * OQ_WG + threadIdx.x;
-                if (i < rb16) oq_lds[i] = v[k];
-            }
+            for (uint32_t k = 0; k < B; ++k) oq_lds[min(i0 + k * OQ_WG + threadIdx.x, rb16 - 1)] = v[k];
         }
+        if (tail)
+            for (uint32_t i = threadIdx.x; i < 2 * OQ_TAIL; i += OQ_WG) tacc[i] = 0;
+        if (threadIdx.x == 0) *ctr = 0;
     }
     __syncthreads();
+#ifdef OQ_TRACE
+    uint32_t tr_n = 0;
+    if ((threadIdx.x & 63) == 0) g_oq_trace[L][threadIdx.x >> 6][tr_n] = wall_clock64();
+    ++tr_n;
+#endif
     const uint2 *img = reinterpret_cast<const uint2 *>(oq_lds);
     const uint4 *__restrict__ row = table + (uint64_t)L * E;
     const uint64_t rsum = rowsum[L];
-    for (uint32_t g = s0 + (threadIdx.x & ~63u); g < s1; g += OQ_WG) {
-    const uint32_t j = g + (threadIdx.x & 63);
-    const bool live = j < s1;
-    const uint64_t h0 = sorted_h0[min(j, s1 - 1)];
-
-    uint64_t sum = 0, key = 0;
-    uint32_t W = 0;
-    for (uint32_t c = 0; c < n_classes; ++c) {
-        const OqClass ci = classes[c];
-        const uint32_t n = ci.count, cs = ci.start;
-        const uint64_t H = h0 * ci.pn;
-        const uint64_t nH = ~H;
-        const uint32_t Hm = mod_barrett_small(H, m, mu);
-        const uint32_t t2 = Hm + m_k64;
-        const uint32_t Hm2 = min(t2, t2 - m);
-        uint32_t d = 0;
-        if (n <= OQ_BRUTE) {
-            for (uint32_t i = 0; i < n; ++i) oq_decide(row[cs + i], nH, Hm, Hm2, m, d, W, key);
-        } else {
-            const uint32_t XA = m - Hm, XB = m - Hm2;
-            const uint32_t ns = (n + 7) >> 3, nt = (n + OQ_S0 - 1) / OQ_S0;
-            // 8-event blocks whose first C is <= ~H are carry-free up to that entry: binary search over the
-            // samples (the C of every 8th entry, ascending; slots past ns hold whatever, so the count is clamped)
-            uint32_t ks;
-            {
-                const uint32_t sb = ci.samp;
-                uint32_t Q = sb;
-                for (uint32_t st = ci.samp_p2 >> 1; st; st >>= 1) {
-                    const uint2 v = img[Q + oq_off(st)];
-                    Q = ((((uint64_t)v.y) << 32) | v.x) <= nH ? Q + oq_inc(st) : Q;
-                }
-                const uint32_t q = Q - sb;
-                const uint32_t k0 = q - ((q * 993u) >> 15);
-                const uint2 v = img[Q];  // the last slot the lifting cannot reach
-                ks = min(k0 + (((((uint64_t)v.y) << 32) | v.x) <= nH ? 1u : 0u), ns);
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (;;) {
+        uint32_t ch = 0;
+        if (lane == 0) ch = atomicAdd(ctr, 1u);
+        ch = __builtin_amdgcn_readfirstlane(ch);
+        if (ch >= nch) break;
+        const uint32_t j = s0 + ch * 64 + lane;
+        const uint64_t h0 = sorted_h0[j];
+        uint64_t sum = 0, key = 0;
+        uint32_t W = 0;
+        for (uint32_t c = 0; c < n_classes; ++c) {
+            const OqClass ci = classes[c];
+            oq_seed_class(ci, img, row, h0, m, mu, m_k64, sum, W, key);
+        }
+        oq_store(stats, sorted_idx[j], sum + rsum - (uint64_t)W * m, key);
+#ifdef OQ_TRACE
+        if (lane == 0 && tr_n < 8) g_oq_trace[L][wave][tr_n] = wall_clock64();
+        ++tr_n;
+#endif
+    }
+    if (tail) {
+        // r chunks of <= 64 tail seeds; wave w takes chunk w % r and every P-th class segment from w / r
+        const uint32_t r = (tail + 63) >> 6, P = (OQ_WG / 64) / r;
+        if (wave < r * P) {
+            const uint32_t jj = (wave % r) * 64 + lane, part = wave / r;
+            const uint64_t h0 = sorted_h0[smain + min(jj, tail - 1)];
+            uint64_t sum = 0, key = 0;
+            uint32_t W = 0;
+            for (uint32_t c = part; c < n_classes; c += P) {
+                const OqClass ci = classes[c];
+                oq_seed_class(ci, img, row, h0, m, mu, m_k64, sum, W, key);
             }
-            const uint32_t b8 = ks ? 8 * (ks - 1) : 0;  // the 8-block holding the carry boundary
-            const uint32_t be = b8 + 8;
-            {
-                const uint32_t nb = min(8u, n - b8);
-#pragma unroll
-                for (uint32_t i = 0; i < 8; ++i) {  // decided event by event
-                    uint32_t dd = 0, ww = 0;
-                    uint64_t kk = 0;
-                    oq_decide(row[cs + b8 + min(i, nb - 1)], nH, Hm, Hm2, m, dd, ww, kk);
-                    if (i < nb) {
-                        d += dd;
-                        W += ww;
-                        key = kk > key ? kk : key;
-                    }
-                }
-            }
-            d += b8;
-            const uint32_t pad1 = oq_round(n, OQ_S1);
-            // level 0: every 512-block of the segment, two at a time (this lane's boundary block is searched
-            // and dropped)
-            for (uint32_t b = 0; b < nt; b += 2) {
-                uint32_t pb[2], X[2], cn[2];
-                uint2 cand[2];
-                bool wr[2];
-                int side[2];
-                uint32_t rs[2];
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const uint32_t lo = min(b + k, nt - 1) * OQ_S0, hi = min(lo + OQ_S0, n);
-                    side[k] = b + k >= nt ? 0 : hi <= b8 ? 1 : lo >= be ? 2 : 0;
-                    X[k] = side[k] == 2 ? XB : XA;
-                    pb[k] = ci.lv[0] + oq_skew(lo);
-                    rs[k] = hi - lo;
-                }
-                if (__builtin_amdgcn_ballot_w64(side[0] != 0 || side[1] != 0)) {  // n <= 512: boundary only
-                    oq_search<2, 0, 0>(img, pb, X, cn, cand, wr);
-#pragma unroll
-                    for (int k = 0; k < 2; ++k)
-                        oq_accum(side[k], rs[k], cn[k], cand[k], wr[k], Hm, Hm2, m, W, key);
-                }
-            }
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {  // level 1: the eight 64-blocks of the boundary 512-block, 4 at a time
-                const uint32_t lt = (b8 & ~(OQ_S0 - 1)) + h * 4 * OQ_S1;
-                uint32_t pb[4], X[4], cn[4], rs[4];
-                int side[4];
-                uint2 cand[4];
-                bool wr[4], any = false;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t lo = lt + k * OQ_S1, hi = min(lo + OQ_S1, n);
-                    side[k] = lo >= n ? 0 : hi <= b8 ? 1 : lo >= be ? 2 : 0;
-                    any |= side[k] != 0;
-                    X[k] = side[k] == 2 ? XB : XA;
-                    pb[k] = ci.lv[1] + oq_skew(min(lo, pad1 - OQ_S1));
-                    rs[k] = hi - lo;
-                }
-                if (__builtin_amdgcn_ballot_w64(any)) {
-                    oq_search<0, 4, 0>(img, pb, X, cn, cand, wr);
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) oq_accum(side[k], rs[k], cn[k], cand[k], wr[k], Hm, Hm2, m, W, key);
-                }
-            }
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {  // level 2: the 8-blocks of the boundary 64-block, less the one decided above
-                const uint32_t lm = (b8 & ~(OQ_S1 - 1)) + h * 4 * OQ_S2;
-                uint32_t pb[4], X[4], cn[4], rs[4];
-                int side[4];
-                uint2 cand[4];
-                bool wr[4], any = false;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t lo = lm + k * OQ_S2, hi = min(lo + OQ_S2, n);
-                    side[k] = (lo >= n || lo == b8) ? 0 : lo < b8 ? 1 : 2;
-                    any |= side[k] != 0;
-                    X[k] = side[k] == 2 ? XB : XA;
-                    pb[k] = ci.lv[2] + oq_skew(min(lo, pad1 - OQ_S2));
-                    rs[k] = hi - lo;
-                }
-                if (__builtin_amdgcn_ballot_w64(any)) {
-                    oq_search<0, 0, 4>(img, pb, X, cn, cand, wr);
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) oq_accum(side[k], rs[k], cn[k], cand[k], wr[k], Hm, Hm2, m, W, key);
-                }
+            if (jj < tail) {
+                atomicAdd(tacc + 2 * jj, (unsigned long long)(sum - (uint64_t)W * m));
+                atomicMax(tacc + 2 * jj + 1, (unsigned long long)key);
             }
         }
-        sum += (uint64_t)d * Hm + (uint64_t)(n - d) * Hm2;
+        __syncthreads();
+        if (threadIdx.x < tail)
+            oq_store(stats, sorted_idx[smain + threadIdx.x], tacc[2 * threadIdx.x] + rsum, tacc[2 * threadIdx.x + 1]);
+#ifdef OQ_TRACE
+        if (lane == 0) g_oq_trace[L][wave][8] = wall_clock64();
+#endif
     }
-    sum += rsum - (uint64_t)W * m;
-    if (live) {
-        nmz_sched_stats st;
-        st.sum_delay_ns = sum;
-        st.max_delay_ns = (int64_t)(key >> 32);
-        st.argmax_event = ~(uint32_t)key;
-        st.n_fault = 0;
-        st.first_fault = NMZ_NONE;
-        st.flags = 0;
-        stats[sorted_idx[j]] = st;
+    if (span) {  // one atomic per workgroup: 4,096 same-address atomics at once (one per wave) queue for ~35 us
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(span + 1, (unsigned long long)wall_clock64());
     }
-    }
-    if (span && (threadIdx.x & 63) == 0) atomicMax(span + 1, (unsigned long long)wall_clock64());
 }
 
 // general modulus (m >= 2^30, including uint64(negative duration)): one seed per lane
@@ -1157,7 +1235,7 @@ static int oq_build(nmz_replayable_plan *p, const std::vector<ClassInfo> &cls, h
     }
     const uint64_t total = len[0] + len[1] + len[2] + len[3];
     const uint64_t rb = (total * 8 + 15) & ~15ull;
-    if (rb > OQ_LDS_MAX) return NMZ_OK;
+    if (rb + OQ_TAIL_LDS > OQ_LDS_MAX) return NMZ_OK;
     for (OqClass &o : oc) {  // regions: level 0 | level 1 | level 2 | samples
         o.lv[1] += (uint32_t)len[0];
         o.lv[2] += (uint32_t)(len[0] + len[1]);
@@ -1243,7 +1321,7 @@ static int replayable_stats(nmz_replayable_plan *p, hipStream_t st, const uint32
     if (p->oq && replay_oq_enabled()) {
         NMZ_TRY(bucket_seeds_counted(st, sc.h0, S, OQ_WG, sc.b, sc.counter));
         KernelTimer kt(p->ctx, st, "replayable_sweep");
-        hipLaunchKernelGGL(k_replayable_sweep_oq, dim3(256), dim3(OQ_WG), p->oq_rb16 * 16u, st, sc.b.offset,
+        hipLaunchKernelGGL(k_replayable_sweep_oq, dim3(256), dim3(OQ_WG), p->oq_rb16 * 16u + OQ_TAIL_LDS, st, sc.b.offset,
                            sc.b.sorted_h0, sc.b.sorted_idx, p->d_table, E, p->d_oq_blob, p->oq_rb16,
                            reinterpret_cast<const unsigned long long *>(p->d_oq_rowsum), p->d_oq_classes,
                            p->n_classes, p->mod.m32, p->mod.mu, p->mod.m_k64, d_stats, kt.span());
@@ -1434,6 +1512,11 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
 using namespace nmz;
 
 extern "C" {
+#ifdef OQ_TRACE
+int nmz_debug_oq_trace(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(nmz::g_oq_trace), sizeof(nmz::g_oq_trace)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int nmz_replayable_plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hint_bytes,
                                uint32_t n_events, int64_t max_interval_ns, uint64_t max_seeds,
