@@ -112,6 +112,47 @@ def test_replayable_event_counts_around_stage_and_chunk_edges(ctx, E):
     assert np.array_equal(r.stats, st) and np.array_equal(r.delays, dl)
 
 
+def _seeds_in_one_row(row, n):
+    """n decimal seeds whose FNV-1a 64 has low byte `row`: they all share one table row, i.e. one K1 workgroup."""
+    off, prime = np.uint64(0xCBF29CE484222325), np.uint64(0x100000001B3)
+    strs = np.arange(0, 400 * n + 1000).astype(str)
+    lens = np.char.str_len(strs)
+    h = np.zeros(len(strs), np.uint64)
+    for ln in np.unique(lens):
+        sel = lens == ln
+        b = np.frombuffer("".join(strs[sel]).encode(), np.uint8).reshape(-1, ln)
+        x = np.full(b.shape[0], off, np.uint64)
+        with np.errstate(over="ignore"):
+            for k in range(ln):
+                x = (x ^ b[:, k].astype(np.uint64)) * prime
+        h[sel] = x
+    out = strs[(h & np.uint64(0xFF)) == np.uint64(row)][:n]
+    assert len(out) == n
+    return [str(x) for x in out]
+
+
+@pytest.mark.parametrize("n", [1, 37, 64, 960, 1024, 1064, 1088, 2100])
+def test_replayable_one_row_chunks_and_partial_chunk(ctx, n):
+    """K1 takes a row's seeds in 64-seed chunks from an LDS counter and shares the row's partial chunk (n mod 64
+    seeds) between its waves by class segment: all seeds in one row, counts on both sides of whole chunks and of
+    one chunk per wave (1,024), with 20 length classes (some per-event, some order-query) so a wave takes
+    several segments of the partial chunk; plus a few seeds of other rows. Stats vs the oracle."""
+    rng = np.random.default_rng(n)
+    sizes = [3, 70, 9, 130, 1, 600, 17, 64, 65, 200, 5, 513, 33, 90, 2, 300, 12, 48, 150, 7]
+    hints = []
+    for c, k in enumerate(sizes):
+        hints += ["".join(rng.choice(list("0123456789"), size=c + 1)) for _ in range(k)]
+    hints = [hints[i] for i in rng.permutation(len(hints))]
+    seeds = _seeds_in_one_row(0x2A, n) + ["x", "yy", "zzz"]
+    for m in [100_000_000, 7]:
+        p = Replayable()
+        p.MaxInterval = m
+        r = p.Sweep(seeds, hints, n_dump=2, k=16, ctx=ctx)
+        st, dl = rep_oracle(seeds, hints, m, n_dump=2)
+        assert np.array_equal(r.stats, st) and np.array_equal(r.delays, dl)
+        assert np.array_equal(r.topk, O.topk_from_stats(st, 0, 16))
+
+
 def test_replayable_empty_inputs(ctx):
     p = Replayable()
     p.MaxInterval = 10_000_000
