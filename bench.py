@@ -56,17 +56,42 @@ def valu_entry(kernel):
         return None
 
 
+_FPS = None
+
+
+def isa_state(e):
+    """Whether the kernels a valu_per_unit.json entry profiled are the kernels the shipped library runs:
+    (fresh, {kernel: [profiled fingerprint, current fingerprint]}) from tools/kernel_isa.py."""
+    global _FPS
+    sys.path.insert(0, os.path.join(HERE, "tools"))
+    import kernel_isa
+    if _FPS is None:
+        _FPS = kernel_isa.kernel_fingerprints(os.path.join(HERE, "namazu_amd", "libnmz_gpu.so"))
+    prof = e.get("isa") or {}
+    detail = {k: [v, kernel_isa.lookup(_FPS, k)] for k, v in prof.items()}
+    fresh = bool(detail) and all(a is not None and a == b for a, b in detail.values())
+    return fresh, detail
+
+
 def roofline_valu(kernel, units, kernel_ms):
-    """VALU issue roofline of `kernel`: measured lane-instructions per unit x units / kernel time."""
+    """VALU issue roofline of `kernel`: measured lane-instructions per unit x units / kernel time. The entry's
+    lane-instructions per unit hold only for the machine code that was profiled: when the shipped kernel's
+    fingerprint differs (or the entry has none) the roofline is marked stale and carries no frac."""
     e = valu_entry(kernel)
     if e is None:
         return None
+    fresh, isa = isa_state(e)
     achieved = e["ops_per_unit"] * units / (kernel_ms * 1e-3) / 1e12
     traffic = e.get("hbm_bytes_per_launch")
     if traffic is not None and units != e["units_per_launch"]:
         traffic = traffic * units / e["units_per_launch"]
-    return {"bound": "valu", "achieved": achieved, "peak": PEAK_VALU_TOPS, "unit": "Tops/s",
-            "frac": achieved / PEAK_VALU_TOPS, "traffic": traffic, "traffic_unit": "bytes/launch (2 x FETCH_SIZE + WRITE_SIZE)",
+    if not fresh:
+        return {"bound": "valu", "kernel": kernel, "kernel_ms": kernel_ms, "stale": True, "achieved": None,
+                "frac": None, "peak": PEAK_VALU_TOPS, "unit": "Tops/s", "traffic": None,
+                "frac_if_profile_held": achieved / PEAK_VALU_TOPS, "ops_source": e["source"], "isa": isa,
+                "why": "the profiled kernel's machine code differs from the shipped library's (tools/kernel_isa.py)"}
+    return {"bound": "valu", "achieved": achieved, "peak": PEAK_VALU_TOPS, "unit": "Tops/s", "stale": False,
+            "frac": achieved / PEAK_VALU_TOPS, "traffic": traffic, "isa": isa, "traffic_unit": "bytes/launch (2 x FETCH_SIZE + WRITE_SIZE)",
             "kernel": kernel, "kernel_ms": kernel_ms, "ops_per_unit": e["ops_per_unit"], "units_per_launch": units,
             "ops_source": e["source"],
             # the same lane-ops against the issue ceiling at the engine clock the chip held during this
@@ -435,12 +460,14 @@ def bench_visualize(args, torch, D, ctx, L, stream):
         algo_bytes = ts.sym.nbytes + (ent.nbytes if po else 0) + 16 * N  # symbols (+ entity ids) read, sig written
         key = "k_trace_sig:" + ("po" if po else "exact")
         prof = valu_entry(key) or {}
+        traffic_fresh = bool(prof) and isa_state(prof)[0]
         achieved = algo_bytes / (sig_ms * 1e-3) / 1e9
         out["po" if po else "exact"] = dict(
             value=N / el, ms=el * 1e3, unique=uniq, sig_kernel_ms=sig_ms,
             roofline={"bound": "hbm", "kernel": "k_trace_sig", "achieved": achieved, "peak": PEAK_HBM_GBS,
                       "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "algorithmic_bytes": algo_bytes,
-                      "traffic": prof.get("hbm_bytes_per_launch"),
+                      "traffic": prof.get("hbm_bytes_per_launch") if traffic_fresh else None,
+                      "traffic_stale": not traffic_fresh,
                       "traffic_unit": "bytes/launch (2 x FETCH_SIZE + WRITE_SIZE)",
                       "ops_per_unit": prof.get("ops_per_unit"), "ops_unit": "VALU lane-instr per trace"})
     out["value"] = out["po"]["value"]
@@ -716,6 +743,9 @@ def headline_line(args, torch, D, ctx, L, stream):
     if line["roofline"]:
         rf = line["roofline"]
         if K1_KERNEL == "k_replayable_sweep_oq":
+            # the kernel derives each seed's statistics (sum, max, argmax) from order queries, not one decision
+            # at a time: a unit is a decision whose effect on the statistics is covered, bit-exact vs the oracle
+            rf["unit_kind"] = "stats-equivalent decision"
             # the order-query kernel does not decide event by event: its lane-instructions per decision are the
             # per-seed searches spread over the 4,096 decisions they settle. The per-decision kernel's own
             # ceiling (issue peak / its measured lane-instructions per decision) is the rate an ideal
@@ -723,7 +753,7 @@ def headline_line(args, torch, D, ctx, L, stream):
             rf["algorithm"] = ("order-query statistics: per (seed, hint-length class) binary searches over "
                                "C-mod-m-sorted blocks (DESIGN.md section 4); units = seed x event decisions covered")
             pd = valu_entry("k_replayable_sweep_fast")
-            if pd:
+            if pd and isa_state(pd)[0]:
                 ceil = PEAK_VALU_TOPS * 1e12 / pd["ops_per_unit"]
                 rf["per_decision_ceiling"] = ceil
                 rf["vs_per_decision_ceiling"] = line["value"] / ceil
@@ -736,7 +766,9 @@ def headline_line(args, torch, D, ctx, L, stream):
         rf["kernel_ms_events"] = r["kern_ms_events"]  # includes the wait for CUs held by another stream's K1
         rf["kernel_ms_isolated"] = r["kern_ms_isolated"]
         # the same lane-ops over the whole pipelined step (every kernel of the step on the clock)
-        rf["frac_of_step"] = rf["ops_per_unit"] * dec_launch / (line["ms_per_step"] * 1e-3) / 1e12 / PEAK_VALU_TOPS
+        if not rf.get("stale"):
+            rf["frac_of_step"] = (rf["ops_per_unit"] * dec_launch / (line["ms_per_step"] * 1e-3) / 1e12 /
+                                  PEAK_VALU_TOPS)
     # survey 8(d) declared model for the reference's byte-serial algorithm: 6*len(hint)+18 ops per decision
     hoff = r["hints"][0]
     mean_len = float(np.mean(np.diff(hoff.astype(np.int64))))

@@ -165,6 +165,14 @@ int nmz_replayable_sweep_topk_dev(nmz_replayable_plan *plan, const uint32_t *d_s
                                   uint32_t k, nmz_sched_stats *d_stats, nmz_topk_entry *d_topk,
                                   void *stream);
 
+/* The same sweep for the seeds "seed_lo", "seed_lo+1", ... "seed_lo+n_seeds-1": the decimal strings of those
+ * uint64 integers (strconv.FormatUint, wrapping past 2^64), generated on the device, so a sweep over a range of
+ * integer seeds needs no seed CSR in memory. Top-k .seed = the seed's integer value (seed_lo + index). Results
+ * equal nmz_replayable_sweep_topk_dev over the CSR of those strings with seed0 = seed_lo. n_seeds <= max_seeds
+ * of the plan. Same reference path (replayablepolicy.go:74-87 seed string, :100-114 interval). */
+int nmz_replayable_sweep_decimal_topk_dev(nmz_replayable_plan *plan, uint64_t seed_lo, uint64_t n_seeds, uint32_t k,
+                                          nmz_sched_stats *d_stats, nmz_topk_entry *d_topk, void *stream);
+
 /* Online decisions (Replayable.QueueEvent -> determineInterval, replayablepolicy.go:100-126):
  * delays[e] = the interval of seed (seed_len bytes) for each of n_events pending events' hints
  * (CSR hint_off[n_events+1] into hint_bytes). No plan or tables: a batch of the events queued

@@ -772,6 +772,32 @@ static inline uint64_t tile_mix(uint64_t x) {
     x *= 0xc4ceb9fe1a85ec53ULL;
     return x ^ (x >> 33);
 }
+// the entry-list limit (NMZ_ED_TP_MAX_ENTRIES lowers it, so tests can force the single-kernel fallback)
+static uint64_t ed_tp_max_entries() {
+    if (const char *e = getenv("NMZ_ED_TP_MAX_ENTRIES")) {
+        const unsigned long long v = strtoull(e, nullptr, 10);
+        if (v < ED_TP_MAX_ENTRIES) return v;
+    }
+    return ED_TP_MAX_ENTRIES;
+}
+
+// one block: sum of n u32 counts in u64
+__global__ __launch_bounds__(1024) void k_sum_u32_u64(const uint32_t *__restrict__ cnt, uint32_t n,
+                                                      uint64_t *__restrict__ out) {
+    __shared__ uint64_t part[16];
+    uint64_t s = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += 1024) s += cnt[i];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (int w = 0; w < 16; ++w) t += part[w];
+        *out = t;
+    }
+}
+
 static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A) {
     const uint32_t N = p->n, n_pairs = (N + 1) / 2, QB = (N + 63) / 64, NCB = (N + 255) / 256;
     const uint32_t shard = A.shard, n_shards = A.n_shards;
@@ -797,8 +823,9 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A) {
     NMZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
                                              (int)n_pairs + 1, st));
     NMZ_TRY(p->tp_mem.ensure(5 * Carve::bytes_for(n_pairs + 1, 4) + Carve::bytes_for(scan_bytes, 1) +
-                             Carve::bytes_for(4, 4)));
+                             Carve::bytes_for(4, 4) + Carve::bytes_for(1, 8)));
     Carve cv(p->tp_mem.ptr);
+    uint64_t *d_tot64 = cv.take<uint64_t>(1);
     uint32_t *d_cnt = cv.take<uint32_t>(n_pairs + 1), *d_poff = cv.take<uint32_t>(n_pairs + 1);
     uint32_t *d_items = cv.take<uint32_t>(n_pairs + 1), *d_ioff = cv.take<uint32_t>(n_pairs + 1);
     uint32_t *d_cur = cv.take<uint32_t>(n_pairs + 1);
@@ -831,12 +858,17 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A) {
     NMZ_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_cnt, d_poff, (int)n_pairs + 1, st));
     hipLaunchKernelGGL(k_bv_items, dim3(ceil_div(n_pairs + 1, 256)), dim3(256), 0, st, d_cnt, n_pairs, d_items);
     NMZ_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_items, d_ioff, (int)n_pairs + 1, st));
-    uint32_t tot[2] = {0, 0};
-    NMZ_HIP(hipMemcpyAsync(&tot[0], d_poff + n_pairs, 4, hipMemcpyDeviceToHost, st));
-    NMZ_HIP(hipMemcpyAsync(&tot[1], d_ioff + n_pairs, 4, hipMemcpyDeviceToHost, st));
+    // the entry total in 64 bits: the u32 scans above wrap beyond 2^32 entries (about N^2 / 4 for a store of
+    // near-duplicates), so their totals are trusted only once this sum is within ED_TP_MAX_ENTRIES
+    hipLaunchKernelGGL(k_sum_u32_u64, dim3(1), dim3(1024), 0, st, d_cnt, n_pairs, d_tot64);
+    NMZ_HIP(hipGetLastError());
+    uint64_t tot64 = 0;
+    uint32_t tot_items = 0;
+    NMZ_HIP(hipMemcpyAsync(&tot64, d_tot64, 8, hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipMemcpyAsync(&tot_items, d_ioff + n_pairs, 4, hipMemcpyDeviceToHost, st));
     NMZ_HIP(hipStreamSynchronize(st));
-    const uint64_t n_ent = tot[0], n_items = tot[1];
-    if (n_ent > ED_TP_MAX_ENTRIES) return 1;
+    if (tot64 > ed_tp_max_entries()) return 1;
+    const uint64_t n_ent = tot64, n_items = tot_items;
     NMZ_TRY(p->tp_ent.ensure(Carve::bytes_for(n_ent + 1, 4)));
     Q.ent = p->tp_ent.as<uint32_t>();
     NMZ_HIP(hipMemcpyAsync(d_cur, d_poff, (uint64_t)n_pairs * 4, hipMemcpyDeviceToDevice, st));
@@ -899,6 +931,11 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
             if (rc < 0) return rc;
         }
         if (rc == 1) {  // the single-kernel search (no q-gram filter, or entry lists beyond ED_TP_MAX_ENTRIES)
+            // the two-phase count pass may already have listed pairs with an empty trace: start from empty
+            // lists, or the single kernel would list them a second time
+            if (A.prof && ed_two_phase_enabled())
+                hipLaunchKernelGGL(k_knn_init, dim3(ceil_div((uint64_t)N * k, 256)), dim3(256), 0, st, d_knn,
+                                   (uint64_t)N * k);
             // this shard's chunks per row: cr = ((shard - b) mod n_shards) + n_shards * t
             std::vector<uint64_t> &ss = p->shard_start[((uint64_t)shard << 32) | n_shards];
             if (ss.empty()) {

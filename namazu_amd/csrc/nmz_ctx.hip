@@ -22,6 +22,10 @@ int fail(int code, const std::string &msg) {
 
 int DevBuf::ensure(size_t bytes) {
     if (bytes <= cap) return NMZ_OK;
+    // a pooled buffer that grows goes back to the pool, where the next plan of this context may take it and
+    // memset / upload into it on another stream: kernels of earlier calls that still read it must be done
+    // (unpooled buffers are released with hipFree, which synchronises by itself)
+    if (ptr && pool && hipDeviceSynchronize() != hipSuccess) return fail(NMZ_EHIP, "hipDeviceSynchronize failed");
     release();
     size_t want = bytes < 256 ? 256 : bytes;
     if (pool) {  // best fit among the pooled buffers (at most 4x the request, so small plans leave large ones)

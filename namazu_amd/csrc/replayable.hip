@@ -310,6 +310,53 @@ __global__ __launch_bounds__(256) void k_seed_prefix(const uint32_t *__restrict_
     if (hist[threadIdx.x]) atomicAdd(&count[threadIdx.x * BUCKET_STRIDE], hist[threadIdx.x]);
 }
 
+// FNV over the 9 decimal digits of x (< 10^9), most significant first; leading zeros are hashed only once
+// `started` (a digit of a more significant part was nonzero)
+__device__ __forceinline__ uint64_t fnv_dec9(uint64_t h, uint32_t x, bool &started) {
+    constexpr uint32_t P10[9] = {1u, 10u, 100u, 1000u, 10000u, 100000u, 1000000u, 10000000u, 100000000u};
+#pragma unroll
+    for (int i = 8; i >= 0; --i) {
+        const uint32_t d = x / P10[i];  // constant divisor: multiply-high + shift
+        x -= d * P10[i];
+        started |= d != 0;
+        if (started) h = fnv_step(h, '0' + d);
+    }
+    return h;
+}
+
+// FNV(decimal string of v) from state h: strconv.FormatUint(v, 10) bytes
+__device__ __forceinline__ uint64_t fnv_decimal_u64(uint64_t h, uint64_t v) {
+    const uint64_t e18 = 1000000000000000000ull;
+    const uint32_t c2 = (uint32_t)(v / e18);
+    const uint64_t r = v - (uint64_t)c2 * e18;
+    const uint32_t c1 = (uint32_t)(r / 1000000000ull), c0 = (uint32_t)(r - (uint64_t)c1 * 1000000000ull);
+    bool started = false;
+    h = fnv_dec9(h, c2, started);
+    h = fnv_dec9(h, c1, started);
+    h = fnv_dec9(h, c0, started);
+    return started ? h : fnv_step(h, '0');
+}
+
+// seed prefix of the seeds "seed_lo" .. "seed_lo + n - 1" (decimal strings generated here: no seed CSR), with
+// the same fused bucket histogram as k_seed_prefix
+__global__ __launch_bounds__(256) void k_seed_prefix_decimal(uint64_t seed_lo, uint64_t n, uint64_t *__restrict__ h0,
+                                                             uint32_t *__restrict__ count, uint32_t ppt) {
+    __shared__ uint32_t hist[256];
+    hist[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t b0 = (uint64_t)blockIdx.x * 256 * ppt;
+    for (uint32_t r = 0; r < ppt; ++r) {
+        const uint64_t s = b0 + (uint64_t)r * 256 + threadIdx.x;
+        if (s < n) {
+            const uint64_t h = fnv_decimal_u64(FNV_OFFSET, seed_lo + s);
+            h0[s] = h;
+            atomicAdd(&hist[h & 0xff], 1u);
+        }
+    }
+    __syncthreads();
+    if (hist[threadIdx.x]) atomicAdd(&count[threadIdx.x * BUCKET_STRIDE], hist[threadIdx.x]);
+}
+
 // ---------------------------------------------------------------------------
 // the sweep (MOD_FAST): persistent waves take work items of up to 64*U seeds
 // (U per lane) that share the FNV low byte L, times a chunk of events.
@@ -1241,13 +1288,11 @@ static int oq_build(nmz_replayable_plan *p, const std::vector<ClassInfo> &cls, h
         o.lv[2] += (uint32_t)(len[0] + len[1]);
         o.samp += (uint32_t)(len[0] + len[1] + len[2]);
     }
-    static bool attr = false;
-    if (!attr) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_replayable_sweep_oq),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)OQ_LDS_MAX) != hipSuccess)
-            return NMZ_OK;  // keep the per-decision sweep
-        attr = true;
-    }
+    // function attributes are per device, and contexts on several devices (or threads) build plans
+    // concurrently: set it on every build (cheap) instead of behind a process-wide flag
+    if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_replayable_sweep_oq),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)OQ_LDS_MAX) != hipSuccess)
+        return NMZ_OK;  // keep the per-decision sweep
     const size_t need = Carve::bytes_for(256 * rb / 16, 16) + Carve::bytes_for(256, 8) +
                         Carve::bytes_for(oc.size(), sizeof(OqClass)) + Carve::bytes_for(tbl.size(), 16);
     NMZ_TRY(p->oq_mem.ensure(need));
@@ -1302,8 +1347,9 @@ static SeedScratch carve_seed_scratch(void *p, uint64_t S) {
 
 // enqueue the sweep for device-resident seeds
 // Stats for every seed.
+// Seeds: the CSR d_soff / d_sbytes, or (d_soff == nullptr) the decimal strings of dec_lo .. dec_lo + S - 1.
 static int replayable_stats(nmz_replayable_plan *p, hipStream_t st, const uint32_t *d_soff,
-                            const uint8_t *d_sbytes, uint64_t S, nmz_sched_stats *d_stats) {
+                            const uint8_t *d_sbytes, uint64_t S, nmz_sched_stats *d_stats, uint64_t dec_lo = 0) {
     if (S == 0) return NMZ_OK;
     const uint32_t E = p->n_events;
     if (E == 0 || p->mod.kind == MOD_ZERO) {
@@ -1313,8 +1359,12 @@ static int replayable_stats(nmz_replayable_plan *p, hipStream_t st, const uint32
     }
     NMZ_CHECK(S <= p->max_seeds, "more seeds than the plan was created for");
     SeedScratch sc = carve_seed_scratch(p->seed_scratch.ptr, p->max_seeds);
-    hipLaunchKernelGGL(k_seed_prefix, dim3(ceil_div(S, 256 * prefix_per_thread())), dim3(256), 0, st, d_soff, d_sbytes,
-                       S, sc.h0, sc.b.count, prefix_per_thread());
+    if (d_soff)
+        hipLaunchKernelGGL(k_seed_prefix, dim3(ceil_div(S, 256 * prefix_per_thread())), dim3(256), 0, st, d_soff,
+                           d_sbytes, S, sc.h0, sc.b.count, prefix_per_thread());
+    else
+        hipLaunchKernelGGL(k_seed_prefix_decimal, dim3(ceil_div(S, 256 * prefix_per_thread())), dim3(256), 0, st,
+                           dec_lo, S, sc.h0, sc.b.count, prefix_per_thread());
     const int U = replay_u();
     const uint32_t per_unit = 64u * (uint32_t)U;
     const uint64_t max_units = S / per_unit + 256;
@@ -1375,10 +1425,10 @@ static int replayable_stats(nmz_replayable_plan *p, hipStream_t st, const uint32
 // 21 + 29 us for k_replayable_merge + k_topk_chunk at 2^20 seeds, so the levels stay separate.)
 static int replayable_run(nmz_replayable_plan *p, hipStream_t st, const uint32_t *d_soff, const uint8_t *d_sbytes,
                           uint64_t S, nmz_sched_stats *d_stats, uint64_t seed0 = 0, uint32_t k = 0,
-                          nmz_topk_entry *d_topk = nullptr) {
+                          nmz_topk_entry *d_topk = nullptr, uint64_t dec_lo = 0) {
     NMZ_CHECK(k <= 256, "top-k supports k <= 256");
     NMZ_CHECK(k == 0 || d_topk, "d_topk is NULL");
-    NMZ_TRY(replayable_stats(p, st, d_soff, d_sbytes, S, d_stats));
+    NMZ_TRY(replayable_stats(p, st, d_soff, d_sbytes, S, d_stats, dec_lo));
     if (k) {
         NMZ_TRY(p->topk_lists.ensure(topk_scratch_entries(S, k) * sizeof(nmz_topk_entry)));
         NMZ_TRY(topk_select(st, d_stats, S, seed0, k, p->topk_lists.as<nmz_topk_entry>(), d_topk));
@@ -1561,6 +1611,16 @@ int nmz_replayable_sweep_topk_dev(nmz_replayable_plan *plan, const uint32_t *d_s
     NMZ_TRY(g.rc);
     hipStream_t st = stream ? (hipStream_t)stream : plan->ctx->stream;
     return replayable_run(plan, st, d_seed_off, d_seed_bytes, n_seeds, d_stats, seed0, k, d_topk);
+}
+
+int nmz_replayable_sweep_decimal_topk_dev(nmz_replayable_plan *plan, uint64_t seed_lo, uint64_t n_seeds, uint32_t k,
+                                          nmz_sched_stats *d_stats, nmz_topk_entry *d_topk, void *stream) {
+    NMZ_CHECK(plan != nullptr, "plan is NULL");
+    NMZ_CHECK(n_seeds < (1ULL << 32), "at most 2^32-1 seeds per call");
+    CtxGuard g(plan->ctx);
+    NMZ_TRY(g.rc);
+    hipStream_t st = stream ? (hipStream_t)stream : plan->ctx->stream;
+    return replayable_run(plan, st, nullptr, nullptr, n_seeds, d_stats, seed_lo, k, d_topk, seed_lo);
 }
 
 int nmz_replayable_sweep(nmz_ctx *ctx, const uint32_t *seed_off, const uint8_t *seed_bytes, uint64_t n_seeds,

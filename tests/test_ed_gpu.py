@@ -408,3 +408,43 @@ def test_knn_qgram_filter_exact(ctx, monkeypatch, w, alphabet, max_edits):
     assert c_on[5] > 0 and c_on[0] > 0 and c_off[5] == 0
     assert c_on[1] == c_off[1]  # the same in-band pairs
     assert c_on[0] + c_on[5] == c_off[0]  # every pair the bound settles would have run the DP
+
+
+@pytest.mark.parametrize("limit", [0, 1, 500])
+def test_knn_two_phase_entry_limit_fallback(ctx, monkeypatch, limit):
+    """Entry lists beyond the two-phase limit (2^30 entries; NMZ_ED_TP_MAX_ENTRIES lowers it) take the
+    single-kernel search after the count pass has run. The count pass lists pairs with an empty trace before the
+    total is known, so the fallback must start from empty lists: near-duplicates with empty traces in the store
+    (n + m <= w pairs), vs the oracle, through the one-shard and the 3-shard (merge + fill) paths."""
+    import torch
+    monkeypatch.setenv("NMZ_ED_TP_MAX_ENTRIES", str(limit))
+    L = _lib.load()
+    rng = np.random.default_rng(77 + limit)
+    ts0 = _edited_family(500, 120, 16, 30, rng)
+    trs = [ts0.trace(i) for i in range(len(ts0))]
+    for i in (3, 40, 41, 333):
+        trs[i] = np.zeros(0, np.uint64)
+    trs[100] = trs[100][:5]
+    ts = hs.TraceSet(trs)
+    n, k, w = len(ts), 8, 32
+    ids, ds = knn(ctx, ts, w, k)
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, w, k, nthreads=16)
+    assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+    plan = ctypes.c_void_p()
+    _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), n, w, ctypes.byref(plan)))
+    assert L.nmz_ed_plan_is_fast(plan) == 2
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    S = 3
+    parts = torch.empty(S * n * k, dtype=torch.int64, device="cuda")
+    out = torch.empty(n * k, dtype=torch.int64, device="cuda")
+    for s in range(S):
+        _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, s, S, ctypes.c_void_p(parts.data_ptr() + s * n * k * 8),
+                                                   stream))
+    _lib.check(L.nmz_knn_merge_dev(ctx.handle, ctypes.c_void_p(parts.data_ptr()), S, n, k,
+                                   ctypes.c_void_p(out.data_ptr()), stream))
+    _lib.check(L.nmz_ed_knn_fill_dev(plan, k, ctypes.c_void_p(out.data_ptr()), stream))
+    torch.cuda.synchronize()
+    sharded = out.cpu().numpy().view(np.uint64).reshape(n, k)
+    L.nmz_ed_plan_destroy(plan)
+    ref = (od.astype(np.uint64) << np.uint64(32)) | oi.astype(np.uint64)
+    assert np.array_equal(sharded, ref)

@@ -20,10 +20,13 @@ LEGS = {
     "random": [("void nmz::k_random_sweep", "k_random_sweep", "decision", 10_000_000 * 10_000)],
     # two-phase search: the DP kernel per pair that ran the DP (the k_ed_bv counters of the bench workload:
     # 51,032,886 clustered, 306,187 survey), the filter passes (count + write, one key) per pair of the search
+    # the filter phase is the count pass plus the scatter (write) pass: bench.py times both under one name
     "ed_clustered": [("void nmz::k_ed_bv_dp<32>", "k_ed_bv_dp:clustered", "DP pair", 51_032_886),
-                     ("void nmz::k_ed_qg_filter<32", "k_ed_qg_filter:clustered", "pair", 100_000 * 99_999 // 2)],
+                     ("void nmz::k_ed_qg_filter<32", "k_ed_qg_filter:clustered", "pair", 100_000 * 99_999 // 2),
+                     ("nmz::k_ed_qg_scatter", "k_ed_qg_filter:clustered", "pair", 100_000 * 99_999 // 2)],
     "ed_survey": [("void nmz::k_ed_bv_dp<32>", "k_ed_bv_dp:survey", "DP pair", 306_187),
-                  ("void nmz::k_ed_qg_filter<32", "k_ed_qg_filter:survey", "pair", 100_000 * 99_999 // 2)],
+                  ("void nmz::k_ed_qg_filter<32", "k_ed_qg_filter:survey", "pair", 100_000 * 99_999 // 2),
+                  ("nmz::k_ed_qg_scatter", "k_ed_qg_filter:survey", "pair", 100_000 * 99_999 // 2)],
     "ed_wide": [("void nmz::k_ed_wide<4>", "k_ed_wide", "pair", 256 * 255 // 2)],
     # one launch per mode per step (PO first, then exact): the profile's average mixes both modes, so the
     # per-mode figures come from the two kernel instantiations
@@ -32,24 +35,46 @@ LEGS = {
 }
 
 
+def dp_pairs_of_run(leg_dir):
+    """DP pairs of the profiled run's own search (bench JSON line on stdout: trace.json), or None."""
+    try:
+        line = json.loads(open(os.path.join(leg_dir, "trace.json")).read().strip().splitlines()[-1])
+    except (OSError, ValueError, IndexError):
+        return None
+    for sec in line.get("secondary", []):
+        if sec.get("search", {}).get("dp_pairs"):
+            return int(sec["search"]["dp_pairs"])
+    return None
+
+
 def main():
     src, tag = sys.argv[1], sys.argv[2]
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "valu_per_unit.json")
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    import kernel_isa
+    path = os.path.join(here, "..", "profiles", "valu_per_unit.json")
     out = json.load(open(path)) if os.path.exists(path) else {}
+    # machine-code fingerprints of the library the profile ran (written on the box by tools/profile_r03.sh)
+    isa_path = os.path.join(src, "isa.json")
+    fps = json.load(open(isa_path)) if os.path.exists(isa_path) else kernel_isa.kernel_fingerprints()
     for leg, kernels in LEGS.items():
         f = os.path.join(src, leg, "summary.json")
         if not os.path.exists(f):
             continue
         summ = json.load(open(f))
+        dp_run = dp_pairs_of_run(os.path.join(src, leg))
         seen = set()
-        for name, e in summ.items():
+        for name, e in sorted(summ.items()):
             for pre, key, unit, n in kernels:
+                if unit == "DP pair" and dp_run:
+                    n = dp_run
                 if name.startswith(pre) and "SQ_INSTS_VALU" in e:
                     if key in seen:  # several kernels under one key (the filter's count and write passes): sum
                         o = out[key]
                         o["ops_per_unit"] += e["SQ_INSTS_VALU"] * 64 / n
                         o["avg_ns"] += e["avg_ns"]
                         o["kernel"] += " + " + name
+                        o["isa"][name] = kernel_isa.lookup(fps, name)
                         if o.get("hbm_bytes_per_launch") is not None and e.get("hbm_bytes_fetch_x2") is not None:
                             o["hbm_bytes_per_launch"] += e["hbm_bytes_fetch_x2"]
                         continue
@@ -58,7 +83,10 @@ def main():
                                 "kernel": name, "avg_ns": e["avg_ns"],
                                 "source": f"SQ_INSTS_VALU per launch, profiles/{tag}_{leg}_summary.json",
                                 "hbm_bytes_per_launch": e.get("hbm_bytes_fetch_x2"),
-                                "clock_ghz": e.get("clock_ghz")}
+                                "clock_ghz": e.get("clock_ghz"),
+                                # fingerprints of the profiled kernels (tools/kernel_isa.py): bench.py marks the
+                                # entry stale when the shipped library's kernels differ
+                                "isa": {name: kernel_isa.lookup(fps, name)}}
     json.dump(out, open(path, "w"), indent=1, sort_keys=True)
     for k, v in sorted(out.items()):
         print(f"{k:26s} {v['ops_per_unit']:14.3f} VALU lane-instr / {v['unit']}  ({v['source']})")
