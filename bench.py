@@ -779,6 +779,88 @@ def headline_line(args, torch, D, ctx, L, stream):
     return line
 
 
+def bench_group(args, torch):
+    """--group: every leg through one device group (nmz_open_group over devices 0..N-1 in this one process:
+    a context + worker thread per device, one RCCL communicator; csrc/group.hip), as a Go host binding the C ABI
+    would drive N GPUs. configs[1]: per step N x 2^20 decimal seeds (generated on the devices) x 4,096 hints with
+    the merged top-64 on the host; configs[3]: 10^7 schedules split over the shards, merged top-64; configs[2]
+    (clustered): the all-pairs k-NN, lists merged over RCCL and returned to the host. Every call is synchronous
+    (host results), so this measures the C ABI's own multi-GPU path, not the pipelined torchrun path."""
+    from namazu_amd import _lib
+    from namazu_amd import group as G
+    from namazu_amd import synth
+    from namazu_amd.explorepolicy import to_csr
+    n_dev = args.gpus
+    n_shards = args.group_shards or n_dev
+    g = G.Group(tuple(range(n_dev)), n_shards=n_shards)
+    S, E = args.seeds, args.events
+    hoff, hb = to_csr(zk_hints(E))
+    t0 = time.perf_counter()
+    rp = G.ReplayableGroupPlan(g, hoff, hb, MAX_INTERVAL_NS, max_seeds_per_shard=(S * n_dev + n_shards - 1) // n_shards)
+    plan_ms = (time.perf_counter() - t0) * 1e3
+    total = S * n_dev
+    for i in range(args.warmup):
+        rp.sweep_decimal(i * total, total, k=64, stats=False)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        _, tk = rp.sweep_decimal((args.warmup + i) * total, total, k=64, stats=False)
+    el = time.perf_counter() - t0
+    rp.close()
+    line = {"metric": "schedule decisions/sec + trace-pair edit distances/sec at 1/2/4/8 MI355X",
+            "value": total * E * args.steps / el, "unit": "decisions/s", "n_gpus": n_dev, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic (ZooKeeper-style hints: signed decimal SplitMix64, seed 0x5EED; decimal seeds)",
+            "config": {"workload": "configs[1] replayable seed sweep through a device group (C ABI)",
+                       "seeds_per_gpu": S, "events": E, "max_interval_ns": MAX_INTERVAL_NS, "topk": 64,
+                       "shards": n_shards,
+                       "parallelism": f"nmz_open_group x{n_dev} (one process, RCCL all_gather top-k)"},
+            "plan_ms": plan_ms, "topk_head": [int(x) for x in tk["seed"][:4]],
+            "what": "per step: nmz_replayable_group_sweep_decimal -- every shard's sweep + device top-64, the "
+                    "per-rank merge, RCCL all_gather, the final merge and the copy to the host"}
+    sec = []
+    if "random" in args.legs:
+        evhash, evclass = config3_trace(10_000)
+        params = _lib.resolve_random_params(30_000_000, 100_000_000, 0.1)
+        n = args.random_total
+        rg = G.RandomGroupPlan(g, evhash, evclass, params, max_seeds_per_shard=(n + n_shards - 1) // n_shards)
+        rg.sweep(0, n, k=64, stats=False)
+        t0 = time.perf_counter()
+        for _ in range(args.random_steps):
+            _, tk = rg.sweep(0, n, k=64, stats=False)
+        el = time.perf_counter() - t0
+        rg.close()
+        sec.append(dict(metric="random-policy fault-sweep decisions/s", value=n * 10_000 * args.random_steps / el,
+                        unit="decisions/s", n_gpus=n_dev, steps=args.random_steps,
+                        ms_per_step=el / args.random_steps * 1e3, scaling="strong",
+                        config={"workload": "configs[3] random fault sweep through a device group (C ABI)",
+                                "schedules": n, "events": 10_000, "shards": n_shards},
+                        topk_head=[[int(x["seed"]), int(x["n_fault"]), int(x["sum_delay_ns"])] for x in tk[:4]]))
+    if "ed_clustered" in args.legs:
+        N = args.ed_traces
+        ts = synth.clustered_traces(N, 2048, family=1024)
+        t0 = time.perf_counter()
+        ep = G.EdGroupPlan(g, ts, 32)
+        eplan_ms = (time.perf_counter() - t0) * 1e3
+        ep.knn(8)
+        t0 = time.perf_counter()
+        for _ in range(args.ed_steps):
+            ids, ds = ep.knn(8)
+        el = time.perf_counter() - t0
+        ep.close()
+        pairs = N * (N - 1) // 2
+        sec.append(dict(metric="trace-pair edit distances/s (banded, all-pairs k-NN)", value=pairs * args.ed_steps / el,
+                        unit="pairs/s", n_gpus=n_dev, steps=args.ed_steps, ms_per_step=el / args.ed_steps * 1e3,
+                        scaling="strong", plan_ms=eplan_ms,
+                        config={"workload": "configs[2] clustered all-pairs search through a device group (C ABI)",
+                                "traces": N, "events": 2048, "band": 32, "k": 8, "shards": n_shards},
+                        what="per step: nmz_ed_group_allpairs_knn -- shards, per-rank merge, RCCL all_gather, merge, "
+                             "fill, ids and distances to the host"))
+    line["secondary"] = sec
+    g.close()
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -797,6 +879,10 @@ def main():
     ap.add_argument("--no-secondary", dest="secondary", action="store_false")
     ap.add_argument("--vis-traces", type=int, default=100_000)
     ap.add_argument("--vis-cpu-traces", type=int, default=1000)
+    ap.add_argument("--group", action="store_true",
+                    help="run the legs through one nmz_open_group over devices 0..N-1 in this process (C ABI "
+                         "multi-GPU path) instead of one process per GPU")
+    ap.add_argument("--group-shards", type=int, default=0, help="shards of the --group run (0: one per device)")
     ap.add_argument("--legs", default="replayable,random,ed_clustered,ed_survey,ed_wide,visualize,config0",
                     help="comma list of legs to run (profiling runs one leg at a time); the headline line "
                          "needs 'replayable'")
@@ -809,6 +895,10 @@ def main():
     os.dup2(2, 1)
 
     import torch
+    if args.group:
+        line = bench_group(args, torch)
+        os.write(out_fd, (json.dumps(line) + "\n").encode())
+        return
     D = Dist()
     torch.cuda.set_device(D.local_rank)
     D.init(torch)

@@ -301,6 +301,69 @@ int nmz_unique_traces_dev(nmz_ctx *ctx, const uint64_t *d_off, const uint64_t *d
                           uint32_t n_traces, uint32_t max_entities, uint64_t *d_sig, uint32_t *d_first_equal,
                           void *stream);
 
+/* ---- device groups: several GPUs behind one call (multi-GPU inside the C ABI) ----------------------------
+ * The reference's callers are single processes (cli/run.go:123-136 initPolicy; cli/tools/visualize.go:138-172),
+ * so one process must reach every GPU of a node. A group holds one context and one worker thread per device
+ * (bound to its device once, so a cgo caller may call from any OS thread) and one RCCL communicator over the
+ * devices, created once. Work is cut into n_shards shards (0 = one per rank; more than the ranks = "virtual"
+ * shards, so a single GPU runs the sharding and merge logic of any shard count); shard s runs on rank
+ * s mod n_ranks. Sweeps shard by contiguous seed range (sizes differ by <= 1), the all-pairs search by the
+ * plan's tile hash (nmz_ed_allpairs_knn_shard_dev). Each rank merges its shards on its device, one RCCL
+ * all_gather over xGMI exchanges the ranks' lists, and a deterministic merge -- (n_fault desc, sum_delay desc,
+ * seed asc) for top-k, (dist asc, id asc) for k-NN -- makes the result identical to one unsharded call.
+ * Group calls are synchronous and serialised per group; host buffers are borrowed for the call only. */
+typedef struct nmz_group nmz_group;
+#define NMZ_GROUP_ID_BYTES 128
+/* bit d of dev_mask = device d */
+int nmz_open_group(uint32_t dev_mask, uint32_t n_shards, nmz_group **out);
+/* One process per device (several hosts, or a launcher with a process per GPU): rank 0 makes the id
+ * (nmz_group_unique_id) and hands it to every rank out of band; each rank opens its device. Every rank receives
+ * the merged results. stats outputs hold the seeds of this rank's shards only. */
+int nmz_group_unique_id(uint8_t *id /* [NMZ_GROUP_ID_BYTES] */);
+int nmz_open_group_rank(const uint8_t *id, int n_ranks, int rank, int device, uint32_t n_shards, nmz_group **out);
+int nmz_close_group(nmz_group *g);
+int nmz_group_info(const nmz_group *g, int *n_ranks, int *n_local_devices, uint32_t *n_shards);
+
+/* replayable sweep over a group (replayablepolicy.go:100-114 per decision, as nmz_replayable_sweep): one plan
+ * per device, kept for repeated sweeps; stats[n_seeds] (may be NULL) and the merged topk[k] (k <= 256, .seed =
+ * seed index, or the seed's integer value for the decimal form) go to host memory. */
+typedef struct nmz_replayable_group_plan nmz_replayable_group_plan;
+int nmz_replayable_group_plan_create(nmz_group *g, const uint32_t *hint_off, const uint8_t *hint_bytes,
+                                     uint32_t n_events, int64_t max_interval_ns, uint64_t max_seeds_per_shard,
+                                     nmz_replayable_group_plan **out);
+int nmz_replayable_group_plan_destroy(nmz_replayable_group_plan *gp);
+int nmz_replayable_group_sweep(nmz_replayable_group_plan *gp, const uint32_t *seed_off, const uint8_t *seed_bytes,
+                               uint64_t n_seeds, uint32_t k, nmz_sched_stats *stats, nmz_topk_entry *topk);
+/* seeds = decimal strings of seed_lo .. seed_lo + n_seeds - 1 (nmz_replayable_sweep_decimal_topk_dev) */
+int nmz_replayable_group_sweep_decimal(nmz_replayable_group_plan *gp, uint64_t seed_lo, uint64_t n_seeds, uint32_t k,
+                                       nmz_sched_stats *stats, nmz_topk_entry *topk);
+/* one call: plan + sweep + merged top-k (the group form of nmz_replayable_sweep) */
+int nmz_replayable_sweep_topk_group(nmz_group *g, const uint32_t *seed_off, const uint8_t *seed_bytes,
+                                    uint64_t n_seeds, const uint32_t *hint_off, const uint8_t *hint_bytes,
+                                    uint32_t n_events, int64_t max_interval_ns, uint32_t k, nmz_sched_stats *stats,
+                                    nmz_topk_entry *topk);
+
+/* random-policy sweep over a group (randompolicy.go:300-346, as nmz_random_sweep): seeds seed0 .. seed0+n-1. */
+typedef struct nmz_random_group_plan nmz_random_group_plan;
+int nmz_random_group_plan_create(nmz_group *g, const uint64_t *evhash, const uint8_t *evclass, uint32_t n_events,
+                                 const nmz_random_params *params, uint64_t max_seeds_per_shard,
+                                 nmz_random_group_plan **out);
+int nmz_random_group_plan_destroy(nmz_random_group_plan *gp);
+int nmz_random_group_sweep(nmz_random_group_plan *gp, uint64_t seed0, uint64_t n_seeds, uint32_t k,
+                           nmz_sched_stats *stats, nmz_topk_entry *topk);
+int nmz_random_sweep_topk_group(nmz_group *g, uint64_t seed0, uint64_t n_seeds, const uint64_t *evhash,
+                                const uint8_t *evclass, uint32_t n_events, const nmz_random_params *params,
+                                uint32_t k, nmz_sched_stats *stats, nmz_topk_entry *topk);
+
+/* all-pairs banded edit-distance k-NN over a group (as nmz_ed_allpairs_knn): every device holds the store. */
+typedef struct nmz_ed_group_plan nmz_ed_group_plan;
+int nmz_ed_group_plan_create(nmz_group *g, const uint64_t *off, const uint64_t *sym, uint32_t n_traces,
+                             uint32_t band, nmz_ed_group_plan **out);
+int nmz_ed_group_plan_destroy(nmz_ed_group_plan *gp);
+int nmz_ed_group_allpairs_knn(nmz_ed_group_plan *gp, uint32_t k, uint32_t *knn_id, uint32_t *knn_dist);
+int nmz_ed_allpairs_knn_group(nmz_group *g, const uint64_t *off, const uint64_t *sym, uint32_t n_traces,
+                              uint32_t band, uint32_t k, uint32_t *knn_id, uint32_t *knn_dist);
+
 #ifdef __cplusplus
 }
 #endif

@@ -91,6 +91,26 @@ SIGNATURES = {
     "nmz_unique_traces": (_int, [_P, _P, _P, _P, _u32, _P]),
     "nmz_unique_traces_dev": (_int, [_P, _P, _P, _P, _u32, _u32, _P, _P, _P]),
     "nmz_topk_select_dev": (_int, [_P, _P, _u64, _u64, _u32, _P, _P]),
+    "nmz_replayable_sweep_decimal_topk_dev": (_int, [_P, _u64, _u64, _u32, _P, _P, _P]),
+    # device groups (multi-GPU inside the C ABI, csrc/group.hip)
+    "nmz_open_group": (_int, [_u32, _u32, ctypes.POINTER(_P)]),
+    "nmz_group_unique_id": (_int, [_P]),
+    "nmz_open_group_rank": (_int, [_P, _int, _int, _int, _u32, ctypes.POINTER(_P)]),
+    "nmz_close_group": (_int, [_P]),
+    "nmz_group_info": (_int, [_P, ctypes.POINTER(_int), ctypes.POINTER(_int), ctypes.POINTER(_u32)]),
+    "nmz_replayable_group_plan_create": (_int, [_P, _P, _P, _u32, _i64, _u64, ctypes.POINTER(_P)]),
+    "nmz_replayable_group_plan_destroy": (_int, [_P]),
+    "nmz_replayable_group_sweep": (_int, [_P, _P, _P, _u64, _u32, _P, _P]),
+    "nmz_replayable_group_sweep_decimal": (_int, [_P, _u64, _u64, _u32, _P, _P]),
+    "nmz_replayable_sweep_topk_group": (_int, [_P, _P, _P, _u64, _P, _P, _u32, _i64, _u32, _P, _P]),
+    "nmz_random_group_plan_create": (_int, [_P, _P, _P, _u32, _P, _u64, ctypes.POINTER(_P)]),
+    "nmz_random_group_plan_destroy": (_int, [_P]),
+    "nmz_random_group_sweep": (_int, [_P, _u64, _u64, _u32, _P, _P]),
+    "nmz_random_sweep_topk_group": (_int, [_P, _u64, _u64, _P, _P, _u32, _P, _u32, _P, _P]),
+    "nmz_ed_group_plan_create": (_int, [_P, _P, _P, _u32, _u32, ctypes.POINTER(_P)]),
+    "nmz_ed_group_plan_destroy": (_int, [_P]),
+    "nmz_ed_group_allpairs_knn": (_int, [_P, _u32, _P, _P]),
+    "nmz_ed_allpairs_knn_group": (_int, [_P, _P, _P, _u32, _u32, _u32, _P, _P]),
     "nmz_timing_enable": (_int, [_P, _int]),
     "nmz_timing_read": (_int, [_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                 ctypes.POINTER(_u64), _int]),

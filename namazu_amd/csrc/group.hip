@@ -1,0 +1,683 @@
+// Multi-GPU inside the C ABI: device groups (nmz_open_group / nmz_open_group_rank).
+//
+// The reference's callers are single Go processes (`nmz run`'s initPolicy, cli/run.go:123-136; `nmz tools
+// visualize`, cli/tools/visualize.go:138-172), so the drop-in has to reach every GPU of a node from one
+// process. A group holds
+//   - one context per device (nmz_open: its own stream and scratch),
+//   - one worker thread per device, bound to that device once (cgo migrates the caller's OS thread; the
+//     workers do not move, and the devices' host-side work -- plan builds, uploads -- runs in parallel),
+//   - one RCCL communicator over the devices, created once (ncclCommInitAll; ncclCommInitRank when each
+//     process owns one device, nmz_open_group_rank).
+// Work is split into n_shards shards (>= the number of ranks: "virtual" shards, so one GPU runs the sharding
+// and merge logic of any shard count); shard s runs on rank s mod n_ranks. The sweeps shard by contiguous
+// seed range (dist.py shard_range: sizes differ by <= 1), the all-pairs search by the plan's own tile hash
+// (nmz_ed_allpairs_knn_shard_dev). Each rank merges its shards' results on its device, one RCCL all_gather
+// over xGMI exchanges the ranks' lists (k x 24 B top-k, or N x k x 8 B k-NN keys), and a deterministic merge
+// -- (n_fault desc, sum_delay desc, seed asc) / (dist asc, id asc) -- gives every rank the same result.
+#include <rccl/rccl.h>
+
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <future>
+#include <memory>
+#include <thread>
+#include <utility>
+
+#include "nmz_common.h"
+#include "nmz_internal.h"
+
+namespace nmz {
+
+// One thread bound to one device, running submitted tasks in order.
+class DeviceWorker {
+  public:
+    explicit DeviceWorker(int device) : device_(device), th_([this] { loop(); }) {}
+    ~DeviceWorker() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_one();
+        th_.join();
+    }
+    // the task's status and, on failure, its thread-local error message
+    std::future<std::pair<int, std::string>> submit(std::function<int()> f) {
+        auto task = std::make_shared<std::packaged_task<std::pair<int, std::string>()>>([f = std::move(f)] {
+            const int rc = f();
+            return std::make_pair(rc, rc == NMZ_OK ? std::string() : std::string(nmz_last_error()));
+        });
+        auto fut = task->get_future();
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            q_.push_back([task] { (*task)(); });
+        }
+        cv_.notify_one();
+        return fut;
+    }
+
+  private:
+    void loop() {
+        (void)hipSetDevice(device_);
+        for (;;) {
+            std::function<void()> job;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+                if (q_.empty()) return;
+                job = std::move(q_.front());
+                q_.pop_front();
+            }
+            job();
+        }
+    }
+    int device_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+    bool stop_ = false;
+    std::thread th_;  // last: started after the members above exist
+};
+
+struct GroupMember {
+    nmz_ctx *ctx = nullptr;
+    int rank = 0;
+    ncclComm_t comm = nullptr;
+    std::unique_ptr<DeviceWorker> worker;
+    DevBuf buf[4];  // group scratch on this device: [0] exchange (send | recv), [1] merge scratch, [2] shard outputs
+};
+
+}  // namespace nmz
+
+struct nmz_group {
+    std::vector<nmz::GroupMember> m;  // the devices of this process
+    int n_ranks = 1;
+    uint32_t n_shards = 1;
+    bool multi_process = false;
+    std::mutex mu;  // group calls are serialised (their contexts and scratch are the group's own)
+};
+
+namespace nmz {
+
+#define NMZ_NCCL(call)                                                                                   \
+    do {                                                                                                 \
+        ncclResult_t r_ = (call);                                                                        \
+        if (r_ != ncclSuccess) return ::nmz::fail(NMZ_EHIP, std::string(#call) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+// run fn(member index) on every member's worker thread, wait for all; the first failure's status and message
+// become the caller's (thread-local error)
+static int run_all(nmz_group *g, const std::function<int(size_t)> &fn) {
+    std::vector<std::future<std::pair<int, std::string>>> fut;
+    for (size_t i = 0; i < g->m.size(); ++i) fut.push_back(g->m[i].worker->submit([&fn, i] { return fn(i); }));
+    int rc = NMZ_OK;
+    std::string msg;
+    for (auto &f : fut) {
+        auto r = f.get();
+        if (r.first != NMZ_OK && rc == NMZ_OK) {
+            rc = r.first;
+            msg = r.second;
+        }
+    }
+    if (rc != NMZ_OK) return fail(rc, msg);
+    return NMZ_OK;
+}
+
+// the shards of `rank`: rank, rank + n_ranks, ...
+static std::vector<uint32_t> shards_of(const nmz_group *g, int rank) {
+    std::vector<uint32_t> s;
+    for (uint32_t x = (uint32_t)rank; x < g->n_shards; x += (uint32_t)g->n_ranks) s.push_back(x);
+    return s;
+}
+
+// [lo, hi) of shard s of `total` units (sizes differ by <= 1; namazu_amd/dist.py shard_range)
+static std::pair<uint64_t, uint64_t> shard_range(uint64_t total, uint32_t n, uint32_t s) {
+    const uint64_t base = total / n, extra = total % n;
+    const uint64_t lo = s * base + std::min<uint64_t>(s, extra);
+    return {lo, lo + base + (s < extra ? 1 : 0)};
+}
+
+// All-gather `bytes` from every member's send buffer into its recv buffer ([n_ranks][bytes], rank order), on the
+// members' streams (ordered after the work that filled send). One RCCL group call covers every local device.
+static int group_allgather(nmz_group *g, const std::vector<void *> &send, const std::vector<void *> &recv,
+                           size_t bytes) {
+    NMZ_NCCL(ncclGroupStart());
+    for (size_t i = 0; i < g->m.size(); ++i) {
+        GroupMember &mb = g->m[i];
+        if (hipSetDevice(mb.ctx->device) != hipSuccess) {
+            (void)ncclGroupEnd();
+            return fail(NMZ_EHIP, "hipSetDevice failed");
+        }
+        const ncclResult_t r = ncclAllGather(send[i], recv[i], bytes, ncclUint8, mb.comm, mb.ctx->stream);
+        if (r != ncclSuccess) {
+            (void)ncclGroupEnd();
+            return fail(NMZ_EHIP, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+        }
+    }
+    NMZ_NCCL(ncclGroupEnd());
+    return NMZ_OK;
+}
+
+// the member whose copy of a merged result goes to the host: every rank of a multi-process group returns
+// its own (identical) copy; in one process, member 0's
+static bool reports(const nmz_group *g, size_t i) { return g->multi_process || i == 0; }
+
+static int group_init_member(nmz_group *g, int device, int rank) {
+    GroupMember mb;
+    NMZ_TRY(nmz_open(device, &mb.ctx));
+    mb.rank = rank;
+    mb.worker.reset(new DeviceWorker(device));
+    g->m.push_back(std::move(mb));
+    return NMZ_OK;
+}
+
+static void group_free(nmz_group *g) {
+    for (GroupMember &mb : g->m) {
+        if (mb.ctx) {
+            (void)hipSetDevice(mb.ctx->device);
+            (void)hipDeviceSynchronize();
+            for (DevBuf &b : mb.buf) b.release();
+        }
+        if (mb.comm) (void)ncclCommDestroy(mb.comm);
+        mb.worker.reset();
+        if (mb.ctx) (void)nmz_close(mb.ctx);
+    }
+    delete g;
+}
+
+// ---- top-k exchange shared by both sweeps -------------------------------------------------------------
+// Member i has written its shards' top-k lists ([n_local][k] at lists_i); merge them into one list, all_gather
+// the ranks' lists, merge those into the final k and copy it to `topk` (host).
+static int group_topk_exchange(nmz_group *g, uint32_t k, const std::vector<nmz_topk_entry *> &lists,
+                               const std::vector<uint32_t> &n_local, nmz_topk_entry *topk) {
+    const size_t R = (size_t)g->n_ranks;
+    std::vector<void *> send(g->m.size()), recv(g->m.size());
+    NMZ_TRY(run_all(g, [&](size_t i) {
+        GroupMember &mb = g->m[i];
+        const size_t lb = Carve::bytes_for(k, sizeof(nmz_topk_entry));
+        NMZ_TRY(mb.buf[0].ensure(lb + Carve::bytes_for(R * k, sizeof(nmz_topk_entry))));
+        NMZ_TRY(mb.buf[1].ensure(Carve::bytes_for(std::max<size_t>(R, n_local[i]) * k + k, sizeof(nmz_topk_entry))));
+        Carve cv(mb.buf[0].ptr);
+        nmz_topk_entry *s = cv.take<nmz_topk_entry>(k), *r = cv.take<nmz_topk_entry>(R * k);
+        send[i] = s;
+        recv[i] = r;
+        hipStream_t st = mb.ctx->stream;
+        if (n_local[i] == 0) {  // no shard on this rank: a list of sentinels
+            std::vector<nmz_topk_entry> sent(k);
+            for (auto &e : sent) e = nmz_topk_entry{UINT64_MAX, INT64_MIN, 0u, NMZ_NONE};
+            NMZ_HIP(hipMemcpyAsync(s, sent.data(), k * sizeof(nmz_topk_entry), hipMemcpyHostToDevice, st));
+            NMZ_HIP(hipStreamSynchronize(st));  // pageable source
+            return NMZ_OK;
+        }
+        return topk_merge_lists(st, lists[i], mb.buf[1].as<nmz_topk_entry>(), n_local[i], k, s);
+    }));
+    NMZ_TRY(group_allgather(g, send, recv, (size_t)k * sizeof(nmz_topk_entry)));
+    return run_all(g, [&](size_t i) {
+        if (!reports(g, i)) return NMZ_OK;
+        GroupMember &mb = g->m[i];
+        hipStream_t st = mb.ctx->stream;
+        nmz_topk_entry *fin = mb.buf[1].as<nmz_topk_entry>() + R * k;
+        // topk_merge_lists overwrites both of its buffers: merge from a copy of the gathered lists
+        nmz_topk_entry *a = (nmz_topk_entry *)recv[i];
+        NMZ_TRY(topk_merge_lists(st, a, mb.buf[1].as<nmz_topk_entry>(), R, k, fin));
+        NMZ_HIP(hipMemcpyAsync(topk, fin, k * sizeof(nmz_topk_entry), hipMemcpyDeviceToHost, st));
+        NMZ_HIP(hipStreamSynchronize(st));
+        return NMZ_OK;
+    });
+}
+
+}  // namespace nmz
+
+using namespace nmz;
+
+// ---- group plans -------------------------------------------------------------------------------------------
+struct nmz_replayable_group_plan {
+    nmz_group *g;
+    std::vector<nmz_replayable_plan *> p;  // per member
+    uint64_t max_seeds_per_shard;
+};
+struct nmz_random_group_plan {
+    nmz_group *g;
+    std::vector<nmz_random_plan *> p;
+    uint64_t max_seeds_per_shard;
+};
+struct nmz_ed_group_plan {
+    nmz_group *g;
+    std::vector<nmz_ed_plan *> p;
+    uint32_t n;
+};
+
+namespace nmz {
+
+// Per-member shard outputs: stats of the largest local shard and one top-k list per local shard.
+struct ShardOut {
+    nmz_sched_stats *stats;
+    nmz_topk_entry *lists;
+};
+static int shard_out(GroupMember &mb, uint64_t max_shard, uint32_t n_local, uint32_t k, ShardOut &o) {
+    NMZ_TRY(mb.buf[2].ensure(Carve::bytes_for(max_shard + 1, sizeof(nmz_sched_stats)) +
+                             Carve::bytes_for((uint64_t)std::max(n_local, 1u) * k + 1, sizeof(nmz_topk_entry))));
+    Carve cv(mb.buf[2].ptr);
+    o.stats = cv.take<nmz_sched_stats>(max_shard + 1);
+    o.lists = cv.take<nmz_topk_entry>((uint64_t)std::max(n_local, 1u) * k + 1);
+    return NMZ_OK;
+}
+
+// One sweep over the group: for every local shard, sweep(member, plan index, lo, n, d_stats, d_topk_list) on
+// the member's stream (and its stats to the host), then the top-k exchange.
+static int group_sweep(nmz_group *g, uint64_t n_seeds, uint32_t k, nmz_sched_stats *stats, nmz_topk_entry *topk,
+                       const std::function<int(size_t, uint64_t, uint64_t, nmz_sched_stats *, nmz_topk_entry *)> &sweep) {
+    NMZ_CHECK(k <= 256, "top-k supports k <= 256");
+    NMZ_CHECK(k == 0 || topk, "topk is NULL");
+    std::vector<nmz_topk_entry *> lists(g->m.size());
+    std::vector<uint32_t> n_local(g->m.size());
+    NMZ_TRY(run_all(g, [&](size_t i) {
+        GroupMember &mb = g->m[i];
+        const std::vector<uint32_t> mine = shards_of(g, mb.rank);
+        n_local[i] = (uint32_t)mine.size();
+        uint64_t mx = 0;
+        for (uint32_t s : mine) {
+            const auto r = shard_range(n_seeds, g->n_shards, s);
+            mx = std::max(mx, r.second - r.first);
+        }
+        ShardOut o;
+        NMZ_TRY(shard_out(mb, mx, n_local[i], std::max(k, 1u), o));
+        lists[i] = o.lists;
+        hipStream_t st = mb.ctx->stream;
+        for (size_t j = 0; j < mine.size(); ++j) {
+            const auto r = shard_range(n_seeds, g->n_shards, mine[j]);
+            const uint64_t n = r.second - r.first;
+            NMZ_TRY(sweep(i, r.first, n, o.stats, k ? o.lists + j * k : nullptr));
+            if (stats && n) {
+                NMZ_HIP(hipMemcpyAsync(stats + r.first, o.stats, n * sizeof(nmz_sched_stats), hipMemcpyDeviceToHost,
+                                       st));
+                NMZ_HIP(hipStreamSynchronize(st));  // o.stats is reused by the next shard
+            }
+        }
+        return NMZ_OK;
+    }));
+    if (k == 0) return NMZ_OK;
+    return group_topk_exchange(g, k, lists, n_local, topk);
+}
+
+static int group_merge_knn(GroupMember &mb, uint64_t *parts, uint32_t n_parts, uint32_t N, uint32_t k,
+                           uint64_t *out, uint64_t *tmp) {
+    // nmz_knn_merge_dev merges up to 8 lists: fold the parts 8 (then 7 + the running result) at a time
+    if (n_parts <= 8) return nmz_knn_merge_dev(mb.ctx, parts, n_parts, N, k, out, nullptr);
+    const uint64_t nk = (uint64_t)N * k;
+    NMZ_TRY(nmz_knn_merge_dev(mb.ctx, parts, 8, N, k, tmp, nullptr));
+    for (uint32_t p = 8; p < n_parts; p += 7) {
+        const uint32_t take = std::min(7u, n_parts - p);
+        // [running | next parts] must be consecutive: copy the running result in front of them
+        uint64_t *front = parts + (uint64_t)(p - 1) * nk;
+        NMZ_HIP(hipMemcpyAsync(front, tmp, nk * 8, hipMemcpyDeviceToDevice, mb.ctx->stream));
+        NMZ_TRY(nmz_knn_merge_dev(mb.ctx, front, take + 1, N, k, p + take >= n_parts ? out : tmp, nullptr));
+    }
+    return NMZ_OK;
+}
+
+}  // namespace nmz
+
+extern "C" {
+
+int nmz_open_group(uint32_t dev_mask, uint32_t n_shards, nmz_group **out) {
+    NMZ_CHECK(out != nullptr, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    NMZ_HIP(hipGetDeviceCount(&n));
+    std::vector<int> devs;
+    for (int d = 0; d < 32; ++d)
+        if (dev_mask & (1u << d)) {
+            NMZ_CHECK(d < n, "dev_mask names a device that does not exist");
+            devs.push_back(d);
+        }
+    NMZ_CHECK(!devs.empty(), "dev_mask is empty");
+    auto *g = new nmz_group();
+    g->n_ranks = (int)devs.size();
+    g->n_shards = n_shards ? n_shards : (uint32_t)devs.size();
+    if (g->n_shards < (uint32_t)devs.size()) {
+        delete g;
+        return fail(NMZ_EINVAL, "n_shards must be 0 or >= the number of devices");
+    }
+    for (size_t i = 0; i < devs.size(); ++i) {
+        const int rc = group_init_member(g, devs[i], (int)i);
+        if (rc != NMZ_OK) {
+            const std::string msg = nmz_last_error();
+            group_free(g);
+            return fail(rc, msg);
+        }
+    }
+    std::vector<ncclComm_t> comms(devs.size());
+    const ncclResult_t r = ncclCommInitAll(comms.data(), (int)devs.size(), devs.data());
+    if (r != ncclSuccess) {
+        group_free(g);
+        return fail(NMZ_EHIP, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+    }
+    for (size_t i = 0; i < devs.size(); ++i) g->m[i].comm = comms[i];
+    *out = g;
+    return NMZ_OK;
+}
+
+int nmz_group_unique_id(uint8_t *id) {
+    NMZ_CHECK(id != nullptr, "id is NULL");
+    ncclUniqueId u;
+    NMZ_NCCL(ncclGetUniqueId(&u));
+    std::memcpy(id, u.internal, NMZ_GROUP_ID_BYTES);
+    return NMZ_OK;
+}
+
+int nmz_open_group_rank(const uint8_t *id, int n_ranks, int rank, int device, uint32_t n_shards, nmz_group **out) {
+    NMZ_CHECK(out && id, "NULL argument");
+    *out = nullptr;
+    NMZ_CHECK(n_ranks >= 1 && rank >= 0 && rank < n_ranks, "bad rank");
+    auto *g = new nmz_group();
+    g->n_ranks = n_ranks;
+    g->multi_process = true;
+    g->n_shards = n_shards ? n_shards : (uint32_t)n_ranks;
+    if (g->n_shards < (uint32_t)n_ranks) {
+        delete g;
+        return fail(NMZ_EINVAL, "n_shards must be 0 or >= n_ranks");
+    }
+    int rc = group_init_member(g, device, rank);
+    if (rc != NMZ_OK) {
+        const std::string msg = nmz_last_error();
+        group_free(g);
+        return fail(rc, msg);
+    }
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, NMZ_GROUP_ID_BYTES);
+    (void)hipSetDevice(device);
+    const ncclResult_t r = ncclCommInitRank(&g->m[0].comm, n_ranks, u, rank);
+    if (r != ncclSuccess) {
+        group_free(g);
+        return fail(NMZ_EHIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    *out = g;
+    return NMZ_OK;
+}
+
+int nmz_close_group(nmz_group *g) {
+    if (!g) return NMZ_OK;
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+    }
+    group_free(g);
+    return NMZ_OK;
+}
+
+int nmz_group_info(const nmz_group *g, int *n_ranks, int *n_local_devices, uint32_t *n_shards) {
+    NMZ_CHECK(g != nullptr, "group is NULL");
+    if (n_ranks) *n_ranks = g->n_ranks;
+    if (n_local_devices) *n_local_devices = (int)g->m.size();
+    if (n_shards) *n_shards = g->n_shards;
+    return NMZ_OK;
+}
+
+// ---- replayable ---------------------------------------------------------------------------------------------
+int nmz_replayable_group_plan_create(nmz_group *g, const uint32_t *hint_off, const uint8_t *hint_bytes,
+                                     uint32_t n_events, int64_t max_interval_ns, uint64_t max_seeds_per_shard,
+                                     nmz_replayable_group_plan **out) {
+    NMZ_CHECK(g && out, "NULL argument");
+    *out = nullptr;
+    std::lock_guard<std::mutex> lk(g->mu);
+    auto *gp = new nmz_replayable_group_plan();
+    gp->g = g;
+    gp->p.assign(g->m.size(), nullptr);
+    gp->max_seeds_per_shard = max_seeds_per_shard;
+    const int rc = run_all(g, [&](size_t i) {
+        return nmz_replayable_plan_create(g->m[i].ctx, hint_off, hint_bytes, n_events, max_interval_ns,
+                                          max_seeds_per_shard, &gp->p[i]);
+    });
+    if (rc != NMZ_OK) {
+        const std::string msg = nmz_last_error();
+        for (auto *p : gp->p) (void)nmz_replayable_plan_destroy(p);
+        delete gp;
+        return fail(rc, msg);
+    }
+    *out = gp;
+    return NMZ_OK;
+}
+
+int nmz_replayable_group_plan_destroy(nmz_replayable_group_plan *gp) {
+    if (!gp) return NMZ_OK;
+    std::lock_guard<std::mutex> lk(gp->g->mu);
+    (void)run_all(gp->g, [&](size_t i) { return nmz_replayable_plan_destroy(gp->p[i]); });
+    delete gp;
+    return NMZ_OK;
+}
+
+int nmz_replayable_group_sweep(nmz_replayable_group_plan *gp, const uint32_t *seed_off, const uint8_t *seed_bytes,
+                               uint64_t n_seeds, uint32_t k, nmz_sched_stats *stats, nmz_topk_entry *topk) {
+    NMZ_CHECK(gp != nullptr, "plan is NULL");
+    NMZ_CHECK(n_seeds == 0 || seed_off, "seed_off is NULL");
+    nmz_group *g = gp->g;
+    std::lock_guard<std::mutex> lk(g->mu);
+    // per member: the seed CSR of the largest local shard
+    std::vector<DevBuf> seeds(g->m.size());
+    struct Release {
+        nmz_group *g;
+        std::vector<DevBuf> &b;
+        ~Release() {
+            for (size_t i = 0; i < b.size(); ++i) {
+                (void)hipSetDevice(g->m[i].ctx->device);
+                (void)hipStreamSynchronize(g->m[i].ctx->stream);
+                b[i].release();
+            }
+        }
+    } rel{g, seeds};
+    return group_sweep(g, n_seeds, k, stats, topk,
+                       [&](size_t i, uint64_t lo, uint64_t n, nmz_sched_stats *d_stats, nmz_topk_entry *d_topk) {
+                           if (n == 0) {  // an empty shard: its top-k list is all sentinels
+                               if (!k) return NMZ_OK;
+                               return nmz_replayable_sweep_topk_dev(gp->p[i], nullptr, nullptr, 0, lo, k, d_stats,
+                                                                    d_topk, nullptr);
+                           }
+                           NMZ_CHECK(n <= gp->max_seeds_per_shard, "a shard has more seeds than the plan allows");
+                           GroupMember &mb = g->m[i];
+                           hipStream_t st = mb.ctx->stream;
+                           const uint32_t b0 = seed_off[lo], b1 = seed_off[lo + n];
+                           std::vector<uint32_t> off(n + 1);
+                           for (uint64_t t = 0; t <= n; ++t) off[t] = seed_off[lo + t] - b0;
+                           NMZ_TRY(seeds[i].ensure(Carve::bytes_for(n + 1, 4) + Carve::bytes_for(b1 - b0 + 1, 1)));
+                           Carve cv(seeds[i].ptr);
+                           uint32_t *d_off = cv.take<uint32_t>(n + 1);
+                           uint8_t *d_b = cv.take<uint8_t>(b1 - b0 + 1);
+                           NMZ_HIP(hipMemcpyAsync(d_off, off.data(), (n + 1) * 4, hipMemcpyHostToDevice, st));
+                           if (b1 > b0)
+                               NMZ_HIP(hipMemcpyAsync(d_b, seed_bytes + b0, b1 - b0, hipMemcpyHostToDevice, st));
+                           if (k)
+                               NMZ_TRY(nmz_replayable_sweep_topk_dev(gp->p[i], d_off, d_b, n, lo, k, d_stats, d_topk,
+                                                                     nullptr));
+                           else
+                               NMZ_TRY(nmz_replayable_sweep_dev(gp->p[i], d_off, d_b, n, d_stats, nullptr));
+                           NMZ_HIP(hipStreamSynchronize(st));  // `off` is pageable and the CSR buffer is reused
+                           return NMZ_OK;
+                       });
+}
+
+int nmz_replayable_group_sweep_decimal(nmz_replayable_group_plan *gp, uint64_t seed_lo, uint64_t n_seeds, uint32_t k,
+                                       nmz_sched_stats *stats, nmz_topk_entry *topk) {
+    NMZ_CHECK(gp != nullptr, "plan is NULL");
+    nmz_group *g = gp->g;
+    std::lock_guard<std::mutex> lk(g->mu);
+    return group_sweep(g, n_seeds, k, stats, topk,
+                       [&](size_t i, uint64_t lo, uint64_t n, nmz_sched_stats *d_stats, nmz_topk_entry *d_topk) {
+                           NMZ_CHECK(n <= gp->max_seeds_per_shard, "a shard has more seeds than the plan allows");
+                           return nmz_replayable_sweep_decimal_topk_dev(gp->p[i], seed_lo + lo, n, k, d_stats, d_topk,
+                                                                        nullptr);
+                       });
+}
+
+int nmz_replayable_sweep_topk_group(nmz_group *g, const uint32_t *seed_off, const uint8_t *seed_bytes,
+                                    uint64_t n_seeds, const uint32_t *hint_off, const uint8_t *hint_bytes,
+                                    uint32_t n_events, int64_t max_interval_ns, uint32_t k, nmz_sched_stats *stats,
+                                    nmz_topk_entry *topk) {
+    NMZ_CHECK(g != nullptr, "group is NULL");
+    const uint64_t per = std::max<uint64_t>((n_seeds + g->n_shards - 1) / g->n_shards, 1);
+    nmz_replayable_group_plan *gp = nullptr;
+    NMZ_TRY(nmz_replayable_group_plan_create(g, hint_off, hint_bytes, n_events, max_interval_ns, per, &gp));
+    const int rc = nmz_replayable_group_sweep(gp, seed_off, seed_bytes, n_seeds, k, stats, topk);
+    const std::string msg = rc == NMZ_OK ? std::string() : std::string(nmz_last_error());
+    (void)nmz_replayable_group_plan_destroy(gp);
+    return rc == NMZ_OK ? NMZ_OK : fail(rc, msg);
+}
+
+// ---- random -------------------------------------------------------------------------------------------------
+int nmz_random_group_plan_create(nmz_group *g, const uint64_t *evhash, const uint8_t *evclass, uint32_t n_events,
+                                 const nmz_random_params *params, uint64_t max_seeds_per_shard,
+                                 nmz_random_group_plan **out) {
+    NMZ_CHECK(g && out, "NULL argument");
+    *out = nullptr;
+    std::lock_guard<std::mutex> lk(g->mu);
+    auto *gp = new nmz_random_group_plan();
+    gp->g = g;
+    gp->p.assign(g->m.size(), nullptr);
+    gp->max_seeds_per_shard = max_seeds_per_shard;
+    const int rc = run_all(g, [&](size_t i) {
+        return nmz_random_plan_create(g->m[i].ctx, evhash, evclass, n_events, params, std::max<uint64_t>(max_seeds_per_shard, 1),
+                                      &gp->p[i]);
+    });
+    if (rc != NMZ_OK) {
+        const std::string msg = nmz_last_error();
+        for (auto *p : gp->p) (void)nmz_random_plan_destroy(p);
+        delete gp;
+        return fail(rc, msg);
+    }
+    *out = gp;
+    return NMZ_OK;
+}
+
+int nmz_random_group_plan_destroy(nmz_random_group_plan *gp) {
+    if (!gp) return NMZ_OK;
+    std::lock_guard<std::mutex> lk(gp->g->mu);
+    (void)run_all(gp->g, [&](size_t i) { return nmz_random_plan_destroy(gp->p[i]); });
+    delete gp;
+    return NMZ_OK;
+}
+
+int nmz_random_group_sweep(nmz_random_group_plan *gp, uint64_t seed0, uint64_t n_seeds, uint32_t k,
+                           nmz_sched_stats *stats, nmz_topk_entry *topk) {
+    NMZ_CHECK(gp != nullptr, "plan is NULL");
+    nmz_group *g = gp->g;
+    std::lock_guard<std::mutex> lk(g->mu);
+    return group_sweep(g, n_seeds, k, stats, topk,
+                       [&](size_t i, uint64_t lo, uint64_t n, nmz_sched_stats *d_stats, nmz_topk_entry *d_topk) {
+                           NMZ_CHECK(n <= gp->max_seeds_per_shard, "a shard has more seeds than the plan allows");
+                           GroupMember &mb = g->m[i];
+                           NMZ_TRY(nmz_random_sweep_dev(gp->p[i], seed0 + lo, n, d_stats, nullptr));
+                           if (!k) return NMZ_OK;
+                           return nmz_topk_select_dev(mb.ctx, d_stats, n, seed0 + lo, k, d_topk, nullptr);
+                       });
+}
+
+int nmz_random_sweep_topk_group(nmz_group *g, uint64_t seed0, uint64_t n_seeds, const uint64_t *evhash,
+                                const uint8_t *evclass, uint32_t n_events, const nmz_random_params *params,
+                                uint32_t k, nmz_sched_stats *stats, nmz_topk_entry *topk) {
+    NMZ_CHECK(g != nullptr, "group is NULL");
+    const uint64_t per = std::max<uint64_t>((n_seeds + g->n_shards - 1) / g->n_shards, 1);
+    nmz_random_group_plan *gp = nullptr;
+    NMZ_TRY(nmz_random_group_plan_create(g, evhash, evclass, n_events, params, per, &gp));
+    const int rc = nmz_random_group_sweep(gp, seed0, n_seeds, k, stats, topk);
+    const std::string msg = rc == NMZ_OK ? std::string() : std::string(nmz_last_error());
+    (void)nmz_random_group_plan_destroy(gp);
+    return rc == NMZ_OK ? NMZ_OK : fail(rc, msg);
+}
+
+// ---- all-pairs banded edit distance k-NN ---------------------------------------------------------------------
+int nmz_ed_group_plan_create(nmz_group *g, const uint64_t *off, const uint64_t *sym, uint32_t n_traces,
+                             uint32_t band, nmz_ed_group_plan **out) {
+    NMZ_CHECK(g && out, "NULL argument");
+    *out = nullptr;
+    std::lock_guard<std::mutex> lk(g->mu);
+    auto *gp = new nmz_ed_group_plan();
+    gp->g = g;
+    gp->n = n_traces;
+    gp->p.assign(g->m.size(), nullptr);
+    // every device builds the same plan from the same host traces, concurrently on the workers
+    const int rc = run_all(g, [&](size_t i) { return nmz_ed_plan_create(g->m[i].ctx, off, sym, n_traces, band, &gp->p[i]); });
+    if (rc != NMZ_OK) {
+        const std::string msg = nmz_last_error();
+        for (auto *p : gp->p) (void)nmz_ed_plan_destroy(p);
+        delete gp;
+        return fail(rc, msg);
+    }
+    *out = gp;
+    return NMZ_OK;
+}
+
+int nmz_ed_group_plan_destroy(nmz_ed_group_plan *gp) {
+    if (!gp) return NMZ_OK;
+    std::lock_guard<std::mutex> lk(gp->g->mu);
+    (void)run_all(gp->g, [&](size_t i) { return nmz_ed_plan_destroy(gp->p[i]); });
+    delete gp;
+    return NMZ_OK;
+}
+
+int nmz_ed_group_allpairs_knn(nmz_ed_group_plan *gp, uint32_t k, uint32_t *knn_id, uint32_t *knn_dist) {
+    NMZ_CHECK(gp != nullptr, "plan is NULL");
+    NMZ_CHECK(k >= 1 && k <= 64, "k must be in [1, 64]");
+    nmz_group *g = gp->g;
+    std::lock_guard<std::mutex> lk(g->mu);
+    const uint32_t N = gp->n;
+    if (N == 0) return NMZ_OK;
+    const uint64_t nk = (uint64_t)N * k;
+    const size_t R = (size_t)g->n_ranks;
+    std::vector<void *> send(g->m.size()), recv(g->m.size());
+    std::vector<uint64_t *> tmp(g->m.size());
+    // 1. each rank's shards into partial lists, merged into its send list
+    NMZ_TRY(run_all(g, [&](size_t i) {
+        GroupMember &mb = g->m[i];
+        const std::vector<uint32_t> mine = shards_of(g, mb.rank);
+        const uint64_t nl = std::max<size_t>(mine.size(), 1);
+        NMZ_TRY(mb.buf[0].ensure(Carve::bytes_for(nk, 8) * (1 + R)));
+        NMZ_TRY(mb.buf[2].ensure(Carve::bytes_for(nk * nl, 8) + Carve::bytes_for(nk, 8) * 2));
+        Carve c0(mb.buf[0].ptr);
+        send[i] = c0.take<uint64_t>(nk);
+        recv[i] = c0.take<uint64_t>(nk * R);
+        Carve c2(mb.buf[2].ptr);
+        uint64_t *parts = c2.take<uint64_t>(nk * nl);
+        tmp[i] = c2.take<uint64_t>(nk);
+        hipStream_t st = mb.ctx->stream;
+        if (mine.empty()) {  // no shard here: empty lists
+            NMZ_HIP(hipMemsetAsync(send[i], 0xff, nk * 8, st));
+            return NMZ_OK;
+        }
+        for (size_t j = 0; j < mine.size(); ++j)
+            NMZ_TRY(nmz_ed_allpairs_knn_shard_dev(gp->p[i], k, mine[j], g->n_shards, parts + j * nk, nullptr));
+        return group_merge_knn(mb, parts, (uint32_t)mine.size(), N, k, (uint64_t *)send[i], tmp[i]);
+    }));
+    // 2. the ranks' lists to every rank (RCCL over xGMI)
+    NMZ_TRY(group_allgather(g, send, recv, nk * 8));
+    // 3. merge + complete (band + 1 for the pairs no shard listed) + split into ids and distances
+    return run_all(g, [&](size_t i) {
+        if (!reports(g, i)) return NMZ_OK;
+        GroupMember &mb = g->m[i];
+        hipStream_t st = mb.ctx->stream;
+        uint64_t *fin = (uint64_t *)send[i];  // the send list is no longer needed
+        NMZ_TRY(group_merge_knn(mb, (uint64_t *)recv[i], (uint32_t)R, N, k, fin, tmp[i]));
+        NMZ_TRY(nmz_ed_knn_fill_dev(gp->p[i], k, fin, nullptr));
+        std::vector<uint64_t> h(nk);
+        NMZ_HIP(hipMemcpyAsync(h.data(), fin, nk * 8, hipMemcpyDeviceToHost, st));
+        NMZ_HIP(hipStreamSynchronize(st));
+        for (uint64_t t = 0; t < nk; ++t) {
+            const bool none = h[t] == UINT64_MAX;
+            if (knn_id) knn_id[t] = none ? NMZ_NONE : (uint32_t)h[t];
+            if (knn_dist) knn_dist[t] = none ? NMZ_NONE : (uint32_t)(h[t] >> 32);
+        }
+        return NMZ_OK;
+    });
+}
+
+int nmz_ed_allpairs_knn_group(nmz_group *g, const uint64_t *off, const uint64_t *sym, uint32_t n_traces,
+                              uint32_t band, uint32_t k, uint32_t *knn_id, uint32_t *knn_dist) {
+    NMZ_CHECK(g != nullptr, "group is NULL");
+    nmz_ed_group_plan *gp = nullptr;
+    NMZ_TRY(nmz_ed_group_plan_create(g, off, sym, n_traces, band, &gp));
+    const int rc = nmz_ed_group_allpairs_knn(gp, k, knn_id, knn_dist);
+    const std::string msg = rc == NMZ_OK ? std::string() : std::string(nmz_last_error());
+    (void)nmz_ed_group_plan_destroy(gp);
+    return rc == NMZ_OK ? NMZ_OK : fail(rc, msg);
+}
+
+}  // extern "C"
