@@ -527,31 +527,34 @@ def bench_config0(args, torch, D, ctx, L):
         d, f = p.decide_events(evs)
         times.append(time.perf_counter() - t0)
     parity = bool(np.array_equal(d, dl[0]) and np.array_equal(f, fl[0].astype(bool)))
-    # online: QueueEvent with real events (MaxInterval 0 ms delays would not matter: latency is enqueue -> decided)
+    # online: QueueEvent with real events under configs[0]'s parameters (30-100 ms delays): each event is decided
+    # inside QueueEvent (the library's host decision path) and released by the native time-bounded queue at
+    # enqueue + delay; latency = enqueue -> decided, delivered-delay error = release - (enqueue + decided delay)
     q = Random()
     q.LoadConfig(Config({"explorePolicy": "random", "explorePolicyParam": {
-        "minInterval": "1ms", "maxInterval": "2ms", "faultActionProbability": 0.1, "seed": 1}}))
+        "minInterval": "30ms", "maxInterval": "100ms", "faultActionProbability": 0.1, "seed": 1,
+        "prioritizedEntities": [f"entity-{i}" for i in range(4)]}}))
     events = [Event.packet(f"entity-{i % 16}", f"entity-{i % 16}", f"entity-{(i + 1) % 16}", {"n": i})
               for i in range(2000)]
-    for ev in events[:50]:
-        q.QueueEvent(ev)
-    q.online.wait_decided(30)
-    q.online.latencies_ns.clear()
-    q.online.batch_sizes.clear()
-    for ev in events:
-        q.QueueEvent(ev)
-    q.online.wait_decided(60)
-    burst = np.array(q.online.latencies_ns, np.float64) / 1e3
-    batches = list(q.online.batch_sizes)
-    q.online.latencies_ns.clear()
-    for ev in events[:300]:
-        q.QueueEvent(ev)
-        q.online.wait_decided(10)
-    single = np.array(q.online.latencies_ns, np.float64) / 1e3
-    n_drain = 0
-    while n_drain < 2350:
-        q.ActionChan().get(timeout=10)
-        n_drain += 1
+
+    def run(evs, one_at_a_time):
+        q.online.latencies_ns.clear()
+        q.online.delivery_err_ns.clear()
+        for ev in evs:
+            q.QueueEvent(ev)
+            if one_at_a_time:
+                q.online.wait_decided(10)
+        q.online.wait_delivered(30)
+        for _ in evs:
+            q.ActionChan().get(timeout=10)
+        lat = np.array(q.online.latencies_ns, np.float64) / 1e3
+        err = np.array(q.online.delivery_err_ns, np.float64) / 1e3
+        return dict(events=len(lat), p50=float(np.percentile(lat, 50)), p99=float(np.percentile(lat, 99)),
+                    delivered_delay_error_us=dict(p50=float(np.percentile(err, 50)),
+                                                  p99=float(np.percentile(err, 99)), max=float(err.max())))
+    run(events[:50], False)  # warm-up
+    burst = run(events, False)
+    single = run(events[:300], True)
     return dict(metric="configs[0] random policy, one seed over one 10k-event trace", unit="decisions/s",
                 cpu_1core=dict(value=E / cpu_s, seconds=round(cpu_s, 4), kind="port",
                                note="oracle/nmz_oracle.c: full Go rand.Seed per decision, as the reference reseeds "
@@ -559,11 +562,10 @@ def bench_config0(args, torch, D, ctx, L):
                 gpu_batch=dict(value=E / min(times), ms=min(times) * 1e3,
                                note="nmz_random_decide, the whole trace in one call (host arrays in and out)"),
                 parity_with_gpu=parity,
-                queue_event_latency_us=dict(
-                    burst=dict(events=len(burst), p50=float(np.percentile(burst, 50)),
-                               p99=float(np.percentile(burst, 99)), mean_batch=float(np.mean(batches))),
-                    one_at_a_time=dict(events=len(single), p50=float(np.percentile(single, 50)),
-                                       p99=float(np.percentile(single, 99)))))
+                queue_event_latency_us=dict(mode=q.online.mode, burst=burst, one_at_a_time=single,
+                                            what="enqueue -> decided inside QueueEvent (nmz_random_decide_host: the "
+                                                 "kernels' closed forms on the host); delivered-delay error = "
+                                                 "native release time - (enqueue + decided delay)"))
 
 
 def bench_ed_secondary(args, torch, D, ctx, L, stream, spec):
@@ -655,6 +657,7 @@ def bench_ed_secondary(args, torch, D, ctx, L, stream, spec):
     out = dict(metric="trace-pair edit distances/s (banded, all-pairs k-NN)", value=pairs * steps / el,
                unit="pairs/s", n_gpus=D.world, steps=steps, ms_per_step=el / steps * 1e3, scaling="strong",
                config={"workload": spec["workload"], "traces": N, "events": ED_LEN, "generator": spec["generator"],
+                       "distinct_symbols": int(len(np.unique(ts.sym))),
                        "band": ED_BAND, "k": k, "parallelism": f"pair-tile shards x{D.world}" +
                        (" + RCCL all_gather k-NN merge" if D.world > 1 else "")},
                kernel=kind, kernel_ms=kern_ms, plan_ms=plan_ms, synth_s=round(synth_s, 2),
@@ -883,7 +886,7 @@ def main():
                     help="run the legs through one nmz_open_group over devices 0..N-1 in this process (C ABI "
                          "multi-GPU path) instead of one process per GPU")
     ap.add_argument("--group-shards", type=int, default=0, help="shards of the --group run (0: one per device)")
-    ap.add_argument("--legs", default="replayable,random,ed_clustered,ed_survey,ed_wide,visualize,config0",
+    ap.add_argument("--legs", default="replayable,random,ed_clustered,ed_survey,ed_alphabet,ed_wide,visualize,config0",
                     help="comma list of legs to run (profiling runs one leg at a time); the headline line "
                          "needs 'replayable'")
     args = ap.parse_args()
@@ -918,12 +921,18 @@ def main():
         ed3s = dict(workload="configs[2] historystorage all-pairs search, survey generator (independent "
                              "mutations: every pair beyond the band)", traces=args.ed_traces, events=2048, band=32,
                     k=8, generator="synth_traces", steps=args.ed_steps, valu_key="k_ed_bv:survey")
+        ed3a = dict(workload="configs[2] historystorage all-pairs search, clustered, store-wide alphabet of "
+                             "thousands of events (each family of 1,024 runs records its own 40 event maps out of "
+                             "20,000): compact bit-parallel tables", traces=args.ed_traces, events=2048, band=32, k=8,
+                    generator="clustered_traces",
+                    gen_kwargs=dict(family=1024, n_symbols=40, alphabet_total=20_000), steps=args.ed_steps,
+                    valu_key="k_ed_bv:alphabet")
         ed5 = dict(workload="configs[4] long-trace stress, wide band", traces=256, events=65536, band=4096, k=8,
                    generator="etcd_traces", steps=args.ed_steps, valu_key="k_ed_wide")
         sec = []
         if "random" in args.legs:
             sec.append(bench_random_fault_sweep(args, torch, D, ctx, L, stream))
-        for leg, spec in (("ed_clustered", ed3), ("ed_survey", ed3s), ("ed_wide", ed5)):
+        for leg, spec in (("ed_clustered", ed3), ("ed_survey", ed3s), ("ed_alphabet", ed3a), ("ed_wide", ed5)):
             if leg in args.legs:
                 sec.append(bench_ed_secondary(args, torch, D, ctx, L, stream, spec))
         if "visualize" in args.legs and D.rank == 0:

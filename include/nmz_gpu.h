@@ -55,6 +55,7 @@ extern "C" {
 #define NMZ_EHIP (-2)     /* HIP runtime error */
 #define NMZ_ENOMEM (-3)   /* device allocation failed */
 #define NMZ_ERANGE (-4)   /* a decision needed more Go rng outputs than the kernel's closed form covers */
+#define NMZ_EAGAIN (-5)   /* nothing became ready within the timeout (nmz_tbqueue_dequeue) */
 
 /* per-event class bits for the random policy (one uint8 per event) */
 #define NMZ_EV_PRIORITIZED 0x01u /* EntityID() in prioritizedEntities (randompolicy.go:335) */
@@ -117,6 +118,34 @@ int nmz_timing_read_span(nmz_ctx *ctx, const char *kernel, double *total_ms, uin
 /* FNV-1a 64 of each of n byte strings (CSR off[n+1] into bytes), one thread per string: the event
  * identities of a batch of events (their canonical JSON; Go hash/fnv New64a). */
 int nmz_fnv1a64_batch(nmz_ctx *ctx, const uint64_t *off, const uint8_t *bytes, uint64_t n, uint64_t *out);
+
+/* ---- online decisions on the calling host thread (no device work) ------------------------------------
+ * The reference decides at enqueue, in the caller's goroutine (util/queue/impl.go:35-46,110-128;
+ * replayablepolicy.go:116-126), and QueueEvent must not block (randompolicy_test.go:112-118): a GPU launch per
+ * event (~100 us) is longer than the decision itself, so the online path decides on the host with the same
+ * closed forms the kernels run (shared code: FNV, Go's seed reduction, the jump-ahead rngSource outputs,
+ * Int63n / Intn rejection). Results equal nmz_*_decide and the sweeps bit for bit. Batch work (sweeps,
+ * all-pairs search) stays on the GPU. */
+int nmz_random_decide_host(uint64_t seed, const uint64_t *evhash, const uint8_t *evclass, uint32_t n_events,
+                           const nmz_random_params *params, int64_t *delays, uint8_t *faults);
+int nmz_replayable_decide_host(const uint8_t *seed, uint32_t seed_len, const uint32_t *hint_off,
+                               const uint8_t *hint_bytes, uint32_t n_events, int64_t max_interval_ns,
+                               int64_t *delays);
+/* FNV-1a 64 of n byte strings (an event's canonical JSON -> its identity) */
+int nmz_fnv1a64_batch_host(const uint64_t *off, const uint8_t *bytes, uint64_t n, uint64_t *out);
+
+/* Time-bounded queue (util/queue/impl.go:64-128 BasicTBQueue; host only): items are released at their due time
+ * (CLOCK_MONOTONIC ns, nmz_monotonic_ns) by one timer thread, equal due times in enqueue order; consumers block in
+ * dequeue (the policy's ActionChan). A released item records its release time, so release - due is the
+ * delivered-delay error of the online path. */
+typedef struct nmz_tbqueue nmz_tbqueue;
+int nmz_tbqueue_create(nmz_tbqueue **out);
+int nmz_tbqueue_destroy(nmz_tbqueue *q);
+int64_t nmz_monotonic_ns(void);
+int nmz_tbqueue_enqueue(nmz_tbqueue *q, uint64_t id, int64_t due_ns);
+/* timeout_ns < 0: wait forever; NMZ_EAGAIN when nothing was released in time */
+int nmz_tbqueue_dequeue(nmz_tbqueue *q, int64_t timeout_ns, uint64_t *id, int64_t *due_ns, int64_t *released_ns);
+int nmz_tbqueue_stats(nmz_tbqueue *q, uint64_t *enqueued, uint64_t *released, uint64_t *dequeued);
 
 /* ---- parameter resolution (host only, no device work) -------------------
  * min/max are time.Duration ns as parsed by LoadConfig; probability as float64.

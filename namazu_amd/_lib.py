@@ -18,6 +18,7 @@ NMZ_EINVAL = -1
 NMZ_EHIP = -2
 NMZ_ENOMEM = -3
 NMZ_ERANGE = -4
+NMZ_EAGAIN = -5
 
 NMZ_EV_PRIORITIZED = 0x01
 NMZ_EV_FAULTABLE = 0x02
@@ -92,6 +93,15 @@ SIGNATURES = {
     "nmz_unique_traces_dev": (_int, [_P, _P, _P, _P, _u32, _u32, _P, _P, _P]),
     "nmz_topk_select_dev": (_int, [_P, _P, _u64, _u64, _u32, _P, _P]),
     "nmz_replayable_sweep_decimal_topk_dev": (_int, [_P, _u64, _u64, _u32, _P, _P, _P]),
+    "nmz_random_decide_host": (_int, [_u64, _P, _P, _u32, _P, _P, _P]),
+    "nmz_replayable_decide_host": (_int, [_P, _u32, _P, _P, _u32, _i64, _P]),
+    "nmz_fnv1a64_batch_host": (_int, [_P, _P, _u64, _P]),
+    "nmz_tbqueue_create": (_int, [ctypes.POINTER(_P)]),
+    "nmz_tbqueue_destroy": (_int, [_P]),
+    "nmz_monotonic_ns": (_i64, []),
+    "nmz_tbqueue_enqueue": (_int, [_P, _u64, _i64]),
+    "nmz_tbqueue_dequeue": (_int, [_P, _i64, ctypes.POINTER(_u64), ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
+    "nmz_tbqueue_stats": (_int, [_P, ctypes.POINTER(_u64), ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     # device groups (multi-GPU inside the C ABI, csrc/group.hip)
     "nmz_open_group": (_int, [_u32, _u32, ctypes.POINTER(_P)]),
     "nmz_group_unique_id": (_int, [_P]),

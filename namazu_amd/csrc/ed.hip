@@ -390,6 +390,10 @@ struct nmz_ed_plan {
     uint32_t *d_prof = nullptr;      // bv: [N][ED_QG_DW] q-gram profiles (ed_qgram_profiles)
     uint32_t rq = 64;                // bv: queries per block row
     uint32_t maxlen = 0;
+    uint32_t bw = 0;                 // bv: the kernels' template band W >= band (8, 16, 32, 64)
+    bool cmp = false;                // bv: compact tables (streams of symbol ids, per-workgroup rows; ed_bv.hip)
+    uint32_t rmap_dw = 0, claim_dw = 0, row_bytes = 0;  // bv, compact: LDS layout (EdBvArgs)
+    uint32_t ww = 0;                 // wide: the kernel's W (1024 * 2^k >= band)
     std::unordered_map<uint64_t, uint32_t> dict;  // bv: symbol -> dense id (single-query search)
     nmz::DevBuf mem;
     // bv, two-phase search: per-(shard, n_shards) tile starts (host, kept), scratch and the entry lists
@@ -406,7 +410,8 @@ struct nmz_ed_plan {
 namespace nmz {
 
 // stored streams of the bit-parallel plan from device symbols: one block per trace, each symbol's dense id is its
-// rank among the sorted distinct symbols (binary search), written as its Peq row's byte offset (id * ndw * 8)
+// rank among the sorted distinct symbols (binary search), written as its Peq row's byte offset (id * ndw * 8), or
+// as the id itself for compact tables (row_bytes = 1)
 __global__ __launch_bounds__(256) void k_ed_bv_remap(const uint64_t *__restrict__ off, const uint64_t *__restrict__ sym,
                                                      const uint64_t *__restrict__ uniq, uint32_t n_uniq,
                                                      const uint64_t *__restrict__ soff, uint32_t row_bytes,
@@ -422,6 +427,54 @@ __global__ __launch_bounds__(256) void k_ed_bv_remap(const uint64_t *__restrict_
         }
         bs[so + t] = (uint16_t)(lo * row_bytes);
     }
+}
+
+// per trace: the number of distinct stream values (symbol ids < n_ids), one workgroup per trace with an LDS bitmap
+__global__ __launch_bounds__(256) void k_trace_distinct(const uint16_t *__restrict__ bs, const uint64_t *__restrict__ soff,
+                                                        const uint32_t *__restrict__ len, uint32_t n_ids,
+                                                        uint32_t *__restrict__ out) {
+    extern __shared__ uint32_t bits[];
+    const uint32_t i = blockIdx.x, nw = (n_ids + 31) / 32;
+    for (uint32_t t = threadIdx.x; t < nw; t += 256) bits[t] = 0;
+    __syncthreads();
+    const uint16_t *a = bs + soff[i];
+    for (uint32_t t = threadIdx.x; t < len[i]; t += 256) atomicOr(&bits[a[t] >> 5], 1u << (a[t] & 31));
+    __syncthreads();
+    uint32_t c = 0;
+    for (uint32_t t = threadIdx.x; t < nw; t += 256) c += __builtin_popcount(bits[t]);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
+    __shared__ uint32_t part[4];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) out[i] = part[0] + part[1] + part[2] + part[3];
+}
+
+// LDS extras of the pool kernels beyond the tables: counters, two q-gram profiles, a pool's survivor list
+static size_t bv_pool_extras(uint32_t pool) { return 16 + 2 * ED_QG_DW * 4 + ((size_t)pool * 2 + 15) / 16 * 16; }
+
+// Compact bit-parallel tables (ed_bv.hip CMP): R rows for a workgroup's queries + the zero row, the map of
+// n_ids symbol ids (+ the padding id) to row byte offsets (u16), the claim bitmap. False when they do not fit
+// `limit` bytes with `extras` (or a row offset would not fit 16 bits).
+static bool bv_compact_layout(uint32_t n_ids, uint32_t R, uint32_t ndw, size_t extras, size_t limit, uint32_t &lds_dw,
+                              uint32_t &rmap_dw, uint32_t &claim_dw) {
+    const uint64_t rows_bytes = (uint64_t)(R + 1) * ndw * 8;
+    const uint64_t peq_dw = (rows_bytes / 4 + 3) / 4 * 4;
+    const uint64_t map_dw = ((n_ids + 2) / 2 + 3) / 4 * 4;
+    const uint64_t clm_dw = ((n_ids + 32) / 32 + 3) / 4 * 4;
+    const uint64_t total = peq_dw + map_dw + clm_dw;
+    if (rows_bytes > 65535 || total * 4 + extras > limit) return false;
+    lds_dw = (uint32_t)total;
+    rmap_dw = (uint32_t)peq_dw;
+    claim_dw = (uint32_t)(peq_dw + map_dw);
+    return true;
+}
+
+// the largest d(2p) + d(2p + 1) over the query pairs (the rows one workgroup's compact tables need)
+static uint32_t pair_rows_max(const std::vector<uint32_t> &d) {
+    uint32_t r = 0;
+    for (size_t i = 0; i < d.size(); i += 2) r = std::max(r, d[i] + (i + 1 < d.size() ? d[i + 1] : 0u));
+    return r;
 }
 
 constexpr uint64_t ED_DEVICE_REMAP_MIN = 1ULL << 20;
@@ -470,30 +523,40 @@ static int ed_plan_build_bv_device(nmz_ed_plan *p, const uint64_t *off, const ui
     NMZ_HIP(hipMemcpyAsync(d_off, off, (N + 1) * 8, hipMemcpyHostToDevice, st));
     uint64_t n_uniq = 0;
     NMZ_TRY(device_unique_u64(d_sym, total, d_uniq, &n_uniq, st));
-    const uint32_t KF = (2 * band + 31) / 32;
+    const uint32_t bw = ed_bv_template(band);
+    const uint32_t KF = (2 * bw + 31) / 32;
     const uint32_t ndw = ((maxlen + 31) / 32 + KF + 2) | 1;
-    if (n_uniq >= MAX_FAST_SYMBOLS || (n_uniq + 1) * ndw * 8 > 65536) return 1;
+    if (n_uniq >= MAX_FAST_SYMBOLS) return 1;
     const uint32_t rq = ed_bv_row_queries();
     const uint32_t n_sym = (uint32_t)n_uniq, G = (N + rq - 1) / rq;
+    p->pool = N >= 24576 ? 4 * ED_BV_POOL : (N >= 12288 ? 2 * ED_BV_POOL : ED_BV_POOL);
+    if (const char *e = getenv("NMZ_ED_POOL")) {
+        const uint32_t v = (uint32_t)atoi(e);
+        if (v >= 256 && v % 256 == 0 && v <= 16384) p->pool = v;
+    }
+    // direct tables (every symbol of the store has a row) when they fit beside the pool kernels' extras, else
+    // compact tables (decided after the streams exist: they need the traces' distinct counts)
+    const uint64_t direct_bytes = (((uint64_t)(n_sym + 1) * ndw * 8 + 15) / 16) * 16;
+    const bool cmp = direct_bytes + bv_pool_extras(p->pool) > 65536 || getenv("NMZ_ED_COMPACT") != nullptr;
+    if (cmp) p->pool = std::min(p->pool, ED_BV_POOL);  // the single kernel's survivor list leaves room for rows
     p->bv = true;
     p->fast = true;
+    p->bw = bw;
+    p->cmp = cmp;
     p->ndw = ndw;
-    p->lds_dw = (uint32_t)((((uint64_t)(n_sym + 1) * ndw * 8 + 15) / 16) * 4);
+    p->row_bytes = ndw * 8;
+    p->lds_dw = (uint32_t)(direct_bytes / 4);
     p->G = G;
     p->rq = rq;
     p->maxlen = maxlen;
     p->n_sym = n_sym;
-    const uint32_t zero_row = n_sym * ndw * 8;
+    // padding value: the zero row's offset (direct), or the id n_sym, which no workgroup ever gives a row (compact)
+    const uint32_t zero_row = cmp ? n_sym : n_sym * ndw * 8;
     std::vector<uint32_t> len(N + 1, 0);
     std::vector<uint64_t> soff(N + 1, 0), chunk_start(G + 1, 0);
     for (uint32_t i = 0; i < N; ++i) {
         len[i] = (uint32_t)(off[i + 1] - off[i]);
         soff[i + 1] = soff[i] + ((uint64_t)(len[i] + 31) / 32 + 1) * 32;
-    }
-    p->pool = N >= 24576 ? 4 * ED_BV_POOL : (N >= 12288 ? 2 * ED_BV_POOL : ED_BV_POOL);
-    if (const char *e = getenv("NMZ_ED_POOL")) {
-        const uint32_t v = (uint32_t)atoi(e);
-        if (v >= 256 && v % 256 == 0 && v <= 16384) p->pool = v;
     }
     for (uint32_t b = 0; b < G; ++b) chunk_start[b + 1] = chunk_start[b] + (N - rq * b + p->pool - 1) / p->pool;
     p->n_chunks = chunk_start[G];
@@ -517,9 +580,26 @@ static int ed_plan_build_bv_device(nmz_ed_plan *p, const uint64_t *off, const ui
     NMZ_HIP(hipMemcpyAsync(p->d_chunk_start, chunk_start.data(), (G + 1) * 8, hipMemcpyHostToDevice, st));
     NMZ_HIP(hipMemcpyAsync(p->d_len, len.data(), (N + 1) * 4, hipMemcpyHostToDevice, st));
     NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_CNT_WORDS * 8, st));
-    hipLaunchKernelGGL(k_ed_bv_remap, dim3(N), dim3(256), 0, st, d_off, d_sym, d_uniq, n_sym, p->d_soff, ndw * 8,
-                       p->d_bsym);
+    hipLaunchKernelGGL(k_ed_bv_remap, dim3(N), dim3(256), 0, st, d_off, d_sym, d_uniq, n_sym, p->d_soff,
+                       cmp ? 1u : ndw * 8, p->d_bsym);
     NMZ_HIP(hipGetLastError());
+    if (cmp) {  // the traces' distinct counts size the per-workgroup rows
+        DevBuf dbuf;
+        struct R2 {
+            DevBuf &b;
+            ~R2() { b.release(); }
+        } rel{dbuf};
+        NMZ_TRY(dbuf.ensure(Carve::bytes_for(N + 1, 4)));
+        hipLaunchKernelGGL(k_trace_distinct, dim3(N), dim3(256), ((n_sym + 32) / 32) * 4, st, p->d_bsym, p->d_soff,
+                           p->d_len, n_sym + 1, dbuf.as<uint32_t>());
+        NMZ_HIP(hipGetLastError());
+        std::vector<uint32_t> d(N);
+        NMZ_HIP(hipMemcpyAsync(d.data(), dbuf.ptr, (uint64_t)N * 4, hipMemcpyDeviceToHost, st));
+        NMZ_HIP(hipStreamSynchronize(st));
+        if (!bv_compact_layout(n_sym, pair_rows_max(d), ndw, bv_pool_extras(p->pool), 65536, p->lds_dw, p->rmap_dw,
+                               p->claim_dw))
+            return 1;  // even a query pair's own symbols do not fit: the host build's other kernels
+    }
     NMZ_TRY(ed_qgram_profiles(p->d_bsym, p->d_soff, p->d_len, N, p->d_prof, st));
     // the dictionary for single queries (nmz_ed_plan_query_knn): symbol -> rank
     std::vector<uint64_t> uniq(n_sym);
@@ -543,7 +623,7 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
     const uint64_t total = N ? off[N] : 0;
     uint32_t maxlen = 0;
     for (uint32_t i = 0; i < N; ++i) maxlen = std::max<uint32_t>(maxlen, (uint32_t)(off[i + 1] - off[i]));
-    if (ed_bv_supported(band) && maxlen + band < MAX_FAST_LEN && total >= ED_DEVICE_REMAP_MIN &&
+    if (ed_bv_supported(band) && maxlen + ed_bv_template(band) < MAX_FAST_LEN && total >= ED_DEVICE_REMAP_MIN &&
         total < (1ULL << 31) && !getenv("NMZ_ED_HOST_REMAP")) {
         const int rc = ed_plan_build_bv_device(p, off, sym, N, band, maxlen);
         if (rc == NMZ_OK) {
@@ -562,7 +642,9 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
     // dense symbol ids (exact remap: a == b <=> id(a) == id(b))
     std::vector<uint16_t> ids;
     const bool want_wide = ed_wide_supported(band);
-    bool fast = ((band == 8 || band == 16 || band == 32) && maxlen + band < MAX_FAST_LEN) || want_wide;
+    const bool want_bv = ed_bv_supported(band) && maxlen + ed_bv_template(band) < MAX_FAST_LEN;
+    const bool tile_band = band == 8 || band == 16 || band == 32;  // k_ed_tile computes exactly its W
+    bool fast = want_bv || want_wide;
     std::unordered_map<uint64_t, uint32_t> dict;
     if (fast) {
         dict.reserve(1024);
@@ -585,27 +667,49 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         delete p;
         return code;
     };
-    // bit-parallel path: per-query Peq rows for every symbol of the alphabet must fit in LDS
+    // bit-parallel path: per-query Peq rows for every symbol of the alphabet in LDS (direct tables), or for the
+    // symbols of one query pair only (compact tables)
     uint32_t n_sym = 0;
-    if (fast && ed_bv_supported(band)) {
-        std::vector<uint8_t> seen(65536, 0);
-        for (uint64_t t = 0; t < total; ++t)
-            if (!seen[ids[t]]) { seen[ids[t]] = 1; ++n_sym; }
-        const uint32_t KF = (2 * band + 31) / 32;
+    const uint32_t pool0 = [&] {
+        uint32_t pl = N >= 24576 ? 4 * ED_BV_POOL : (N >= 12288 ? 2 * ED_BV_POOL : ED_BV_POOL);
+        if (const char *e = getenv("NMZ_ED_POOL")) {
+            const uint32_t v = (uint32_t)atoi(e);
+            if (v >= 256 && v % 256 == 0 && v <= 16384) pl = v;
+        }
+        return pl;
+    }();
+    if (fast && want_bv) {
+        n_sym = (uint32_t)dict.size();
+        const uint32_t bw = ed_bv_template(band);
+        const uint32_t KF = (2 * bw + 31) / 32;
         uint32_t ndw = (maxlen + 31) / 32 + KF + 2;
         ndw |= 1;  // odd row stride: rows of distinct symbols start on distinct bank pairs
-        const uint64_t lds_bytes = (uint64_t)(n_sym + 1) * ndw * 8;
-        if (lds_bytes <= 65536) {
+        const uint64_t lds_bytes = (((uint64_t)(n_sym + 1) * ndw * 8 + 15) / 16) * 16;
+        p->bw = bw;
+        p->ndw = ndw;
+        p->row_bytes = ndw * 8;
+        if (lds_bytes + bv_pool_extras(pool0) <= 65536 && !getenv("NMZ_ED_COMPACT")) {
             p->bv = true;
-            p->ndw = ndw;
-            p->lds_dw = (uint32_t)(((lds_bytes + 15) / 16) * 4);
+            p->lds_dw = (uint32_t)(lds_bytes / 4);
+        } else {
+            std::vector<uint32_t> d(N, 0), stamp(n_sym + 1, UINT32_MAX);
+            for (uint32_t i = 0; i < N; ++i)
+                for (uint64_t t = off[i]; t < off[i + 1]; ++t)
+                    if (stamp[ids[t]] != i) {
+                        stamp[ids[t]] = i;
+                        ++d[i];
+                    }
+            if (bv_compact_layout(n_sym, pair_rows_max(d), ndw, bv_pool_extras(std::min(pool0, ED_BV_POOL)), 65536,
+                                  p->lds_dw, p->rmap_dw, p->claim_dw)) {
+                p->bv = true;
+                p->cmp = true;
+            }
         }
     }
     if (fast && want_wide) {
-        std::vector<uint8_t> seen(65536, 0);
-        for (uint64_t t = 0; t < total; ++t)
-            if (!seen[ids[t]]) { seen[ids[t]] = 1; ++n_sym; }
-        const uint32_t ndw = ed_wide_ndw(band, maxlen);
+        n_sym = (uint32_t)dict.size();
+        p->ww = ed_wide_template(band);
+        const uint32_t ndw = ed_wide_ndw(p->ww, maxlen);
         const uint64_t peq_bytes = (uint64_t)N * std::max(n_sym, 1u) * ndw * 4;
         // one query's table must be addressable by a 32-bit buffer offset
         if (peq_bytes <= (16ULL << 30) && (uint64_t)std::max(n_sym, 1u) * ndw * 4 < (1ULL << 31)) {
@@ -642,7 +746,7 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
             (total && hipMemcpyAsync(p->d_qsym, ids.data(), total * 2, hipMemcpyHostToDevice, st)) ||
             hipMemcpyAsync(p->d_qoff, off, (N + 1) * 8, hipMemcpyHostToDevice, st))
             return cleanup(fail(NMZ_EHIP, "ED plan upload failed"));
-        rc = ed_wide_build_peq(p->d_qsym, p->d_qoff, N, p->n_sym, p->ndw, band, p->d_peq, st);
+        rc = ed_wide_build_peq(p->d_qsym, p->d_qoff, N, p->n_sym, p->ndw, p->ww, p->d_peq, st);
         if (rc != NMZ_OK) return cleanup(rc);
         if (hipStreamSynchronize(st)) return cleanup(fail(NMZ_EHIP, "ED plan build failed"));
     } else if (fast && p->bv) {
@@ -654,7 +758,7 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         p->n_sym = n_sym;
         p->dict = std::move(dict);
         const uint32_t ndw = p->ndw;
-        const uint32_t zero_row = n_sym * ndw * 8;
+        const uint32_t zero_row = p->cmp ? n_sym : n_sym * ndw * 8;
         std::vector<uint32_t> len(N + 1, 0);
         std::vector<uint64_t> soff(N + 1, 0), chunk_start(G + 1, 0);
         for (uint32_t i = 0; i < N; ++i) {
@@ -664,11 +768,7 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         // candidates per workgroup: a larger pool amortises the Peq build and evens out the lanes' refill
         // tail, a smaller one keeps enough workgroups for small N (configs[2]-shaped traces, 1 MI355X:
         // N = 100k: 1024 -> 1.78 s, 4096 -> 1.64 s, 8192 -> 1.65 s; N = 8192: 1024 -> 14.5 ms, 4096 -> 19.6 ms)
-        p->pool = N >= 24576 ? 4 * ED_BV_POOL : (N >= 12288 ? 2 * ED_BV_POOL : ED_BV_POOL);
-        if (const char *e = getenv("NMZ_ED_POOL")) {  // tuning override (multiple of 256)
-            const uint32_t v = (uint32_t)atoi(e);
-            if (v >= 256 && v % 256 == 0 && v <= 16384) p->pool = v;
-        }
+        p->pool = p->cmp ? std::min(pool0, ED_BV_POOL) : pool0;
         for (uint32_t b = 0; b < G; ++b)
             chunk_start[b + 1] = chunk_start[b] + (N - rq * b + p->pool - 1) / p->pool;
         p->n_chunks = chunk_start[G];
@@ -676,7 +776,8 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         for (uint32_t b = 0; b < G; ++b) p->row_chunks[b] = chunk_start[b + 1] - chunk_start[b];
         std::vector<uint16_t> bs(soff[N] + 64, (uint16_t)zero_row);  // + 2 spare blocks at the end
         for (uint32_t i = 0; i < N; ++i)
-            for (uint32_t t = 0; t < len[i]; ++t) bs[soff[i] + t] = (uint16_t)(ids[off[i] + t] * ndw * 8);
+            for (uint32_t t = 0; t < len[i]; ++t)
+                bs[soff[i] + t] = (uint16_t)(p->cmp ? ids[off[i] + t] : ids[off[i] + t] * ndw * 8);
         size_t need = Carve::bytes_for(bs.size(), 2) + Carve::bytes_for(N + 1, 8) * 2 +
                       Carve::bytes_for(G + 1, 8) + Carve::bytes_for(N + 1, 4) +
                       Carve::bytes_for(ED_CNT_WORDS, 8) + Carve::bytes_for((uint64_t)N * ED_QG_DW, 4);
@@ -700,7 +801,7 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         rc = ed_qgram_profiles(p->d_bsym, p->d_soff, p->d_len, N, p->d_prof, st);
         if (rc != NMZ_OK) return cleanup(rc);
         if (hipStreamSynchronize(st)) return cleanup(fail(NMZ_EHIP, "ED plan build failed"));
-    } else if (fast) {
+    } else if (fast && tile_band && maxlen + band < MAX_FAST_LEN) {
         const uint32_t G = (N + 63) / 64;
         p->G = G;
         std::vector<uint32_t> gmax(G + 1, 0), len(N + 1, 0);
@@ -736,6 +837,9 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
             hipStreamSynchronize(st))
             return cleanup(fail(NMZ_EHIP, "ED plan upload failed"));
     } else {
+        p->fast = false;
+        p->bv = false;
+        p->cmp = false;
         size_t need = Carve::bytes_for(N + 1, 8) + Carve::bytes_for(total + 1, 8);
         int rc = p->mem.ensure(need);
         if (rc != NMZ_OK) return cleanup(rc);
@@ -850,10 +954,11 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A) {
     Q.NCB = NCB;
     Q.shard = shard;
     Q.n_shards = n_shards;
+    Q.w = p->band;
     NMZ_HIP(hipMemsetAsync(d_cnt, 0, (n_pairs + 1) * 4, st));
     {
         KernelTimer kt(p->ctx, st, "ed_qg_filter");
-        NMZ_TRY(ed_qg_filter_launch(Q, p->band, true, st));
+        NMZ_TRY(ed_qg_filter_launch(Q, true, st));
     }
     NMZ_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_cnt, d_poff, (int)n_pairs + 1, st));
     hipLaunchKernelGGL(k_bv_items, dim3(ceil_div(n_pairs + 1, 256)), dim3(256), 0, st, d_cnt, n_pairs, d_items);
@@ -875,10 +980,10 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A) {
     {
         KernelTimer kt(p->ctx, st, "ed_qg_filter");
         if (Q.masks) NMZ_TRY(ed_qg_scatter_launch(Q, st));
-        else NMZ_TRY(ed_qg_filter_launch(Q, p->band, false, st));
+        else NMZ_TRY(ed_qg_filter_launch(Q, false, st));
     }
     KernelTimer kt(p->ctx, st, "ed_bv_dp");
-    return ed_bv_dp_launch(A, d_ioff, d_poff, Q.ent, n_pairs, (uint32_t)n_items, p->band, st);
+    return ed_bv_dp_launch(A, d_ioff, d_poff, Q.ent, n_pairs, (uint32_t)n_items, p->bw, p->cmp, st);
 }
 
 static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_knn, uint32_t shard = 0,
@@ -903,9 +1008,10 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
         A.ndw = p->ndw;
         A.shard = shard;
         A.n_shards = n_shards;
+        A.w = p->band;
         if (A.n_waves == 0) return NMZ_OK;
         KernelTimer kt(p->ctx, st, "ed_wide");
-        return ed_wide_launch(A, p->band, st);
+        return ed_wide_launch(A, p->ww, st);
     }
     if (p->bv) {
         EdBvArgs A;
@@ -921,6 +1027,10 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
         A.k = k;
         A.lds_dw = p->lds_dw;
         A.pool = p->pool;
+        A.w = p->band;
+        A.rmap_dw = p->rmap_dw;
+        A.claim_dw = p->claim_dw;
+        A.row_bytes = p->row_bytes;
         A.shard = shard;
         A.n_shards = n_shards;
         NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_CNT_WORDS * 8, st));
@@ -954,7 +1064,7 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
                 NMZ_CHECK(blocks < (1ULL << 31), "too many traces for one launch");
                 NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_CNT_WORDS * 8, st));
                 KernelTimer kt(p->ctx, st, "ed_bv");
-                NMZ_TRY(ed_bv_launch(A, p->band, blocks, st));
+                NMZ_TRY(ed_bv_launch(A, p->bw, p->cmp, blocks, st));
             }
         }
         // k_ed_bv lists in-band results only; a shard's partial lists are completed after the merge
@@ -1069,7 +1179,7 @@ int nmz_ed_plan_query_knn(nmz_ed_plan *plan, const uint64_t *q_off, const uint64
                           uint32_t k, uint32_t *knn_id, uint32_t *knn_dist) {
     NMZ_CHECK(plan != nullptr, "plan is NULL");
     NMZ_CHECK(k >= 1 && k <= 64, "k must be in [1, 64]");
-    NMZ_CHECK(plan->bv, "single-query search needs a bit-parallel plan (band 8, 16 or 32; alphabet within LDS)");
+    NMZ_CHECK(plan->bv, "single-query search needs a bit-parallel plan (band <= 64, alphabet or query pairs within LDS)");
     NMZ_CHECK(n_queries == 0 || (q_off && knn_id && knn_dist), "NULL argument");
     CtxGuard g(plan->ctx);
     NMZ_TRY(g.rc);
@@ -1089,8 +1199,20 @@ int nmz_ed_plan_query_knn(nmz_ed_plan *plan, const uint64_t *q_off, const uint64
     for (uint32_t q = 0; q < n_queries; ++q)
         for (uint64_t t = q_off[q]; t < q_off[q + 1]; ++t) {
             auto it = plan->dict.find(q_sym[t]);
-            if (it != plan->dict.end()) qs[qoff[q] + (t - q_off[q])] = (uint16_t)(it->second * plan->ndw * 8);
+            if (it != plan->dict.end())
+                qs[qoff[q] + (t - q_off[q])] = (uint16_t)(plan->cmp ? it->second : it->second * plan->ndw * 8);
         }
+    // compact tables: each launch's rows = the two queries' distinct known symbols
+    std::vector<uint32_t> qd(n_queries, 0);
+    if (plan->cmp) {
+        std::vector<uint32_t> stamp(plan->n_sym + 1, UINT32_MAX);
+        for (uint32_t q = 0; q < n_queries; ++q)
+            for (uint64_t t = qoff[q]; t < qoff[q] + (q_off[q + 1] - q_off[q]); ++t)
+                if (qs[t] != 0xffffu && stamp[qs[t]] != q) {
+                    stamp[qs[t]] = q;
+                    ++qd[q];
+                }
+    }
     const uint64_t nk = (uint64_t)n_queries * k;
     DevBuf &scr = plan->ctx->buf[11];
     NMZ_TRY(scr.ensure(Carve::bytes_for(qs.size(), 2) + Carve::bytes_for(nk, 8) + 2 * Carve::bytes_for(nk, 4)));
@@ -1120,8 +1242,18 @@ int nmz_ed_plan_query_knn(nmz_ed_plan *plan, const uint64_t *q_off, const uint64
         A.k = k;
         A.lds_dw = plan->lds_dw;
         A.pool = pool;
+        A.w = plan->band;
+        A.rmap_dw = plan->rmap_dw;
+        A.claim_dw = plan->claim_dw;
+        A.row_bytes = plan->row_bytes;
+        if (plan->cmp) {
+            const uint32_t R = qd[q] + (A.n_queries > 1 ? qd[q + 1] : 0);
+            NMZ_CHECK(bv_compact_layout(plan->n_sym, R, plan->ndw, 16 + (2 * ED_QG_DW + 2 * ED_QG_BUCKETS) * 4,
+                                        ED_BV_LDS_MAX, A.lds_dw, A.rmap_dw, A.claim_dw),
+                      "the queries have too many distinct symbols for the bit-parallel search");
+        }
         KernelTimer kt(plan->ctx, st, "ed_bv_query");
-        NMZ_TRY(ed_bv_query_launch(A, plan->band, ceil_div(N, pool), st));
+        NMZ_TRY(ed_bv_query_launch(A, plan->bw, plan->cmp, ceil_div(N, pool), st));
     }
     // k_ed_bv_query lists in-band results only: every other stored trace is at band + 1
     hipLaunchKernelGGL(k_knn_fill, dim3(ceil_div(n_queries, 256)), dim3(256), 0, st, d_knn, n_queries, k, N,

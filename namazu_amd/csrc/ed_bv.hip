@@ -35,6 +35,16 @@
 // (dense ids), 2 queries interleaved per dword ([symbol][dword][query]) so
 // one ds_read_b64 returns a dword of both queries.  Candidate symbols are
 // stored as that row's LDS byte offset (u16), one stream per trace.
+// Compact tables (CMP, stores whose alphabet does not fit LDS): the streams
+// hold dense symbol ids; a workgroup gives a row only to the distinct symbols
+// of its two queries (row 0 = the zero row) and translates a candidate symbol
+// through an LDS map id -> row byte offset (u16), one extra ds_read_u16 per
+// column.  Exact: a symbol absent from both queries matches no query row.
+//
+// Band: the kernels compute the band of their template W (8, 16, 32, 64) and
+// apply the requested w <= W at run time (length band, q-gram bound, cut-off,
+// clamp): a path of cost c <= w never leaves the diagonals |i - j| <= c, so
+// min(D_W, w + 1) = min(D_w, w + 1) (= min(Lev, w + 1)).
 #include <type_traits>
 
 #include "nmz_common.h"
@@ -101,13 +111,23 @@ __device__ __forceinline__ void bv_column(BvState<BvShape<W>::KF> &S, const uint
     if constexpr (KF == 1) {
         const uint32_t X = (Eq[0] & S.P[0]) + S.P[0];
         Xh[0] = (X ^ S.P[0]) | Eq[0];
-    } else {
-        static_assert(KF == 2, "KF <= 2 (w <= 32)");
+    } else if constexpr (KF == 2) {
         const uint64_t p = ((uint64_t)S.P[1] << 32) | S.P[0];
         const uint64_t e = ((uint64_t)(Eq[1] & S.P[1]) << 32) | (Eq[0] & S.P[0]);
         const uint64_t X = e + p;
         Xh[0] = ((uint32_t)X ^ S.P[0]) | Eq[0];
         Xh[1] = ((uint32_t)(X >> 32) ^ S.P[1]) | Eq[1];
+    } else {
+        static_assert(KF == 4, "KF in {1, 2, 4} (w <= 64)");
+        const uint64_t p0 = ((uint64_t)S.P[1] << 32) | S.P[0], p1 = ((uint64_t)S.P[3] << 32) | S.P[2];
+        const uint64_t e0 = ((uint64_t)(Eq[1] & S.P[1]) << 32) | (Eq[0] & S.P[0]);
+        const uint64_t e1 = ((uint64_t)(Eq[3] & S.P[3]) << 32) | (Eq[2] & S.P[2]);
+        const uint64_t X0 = e0 + p0;
+        const uint64_t X1 = e1 + p1 + (uint64_t)(X0 < p0);
+        Xh[0] = ((uint32_t)X0 ^ S.P[0]) | Eq[0];
+        Xh[1] = ((uint32_t)(X0 >> 32) ^ S.P[1]) | Eq[1];
+        Xh[2] = ((uint32_t)X1 ^ S.P[2]) | Eq[2];
+        Xh[3] = ((uint32_t)(X1 >> 32) ^ S.P[3]) | Eq[3];
     }
 #pragma unroll
     for (int k = 0; k < KF; ++k) {
@@ -180,7 +200,7 @@ template <int W, int t, bool SLOW>
 __device__ __forceinline__ void bv_step2(BvState<BvShape<W>::KF> &S1, BvState<BvShape<W>::KF> &S2,
                                          const uint32_t *peq_bytes, uint32_t addr, uint32_t j, uint32_t m,
                                          uint32_t n1, uint32_t n2, bool &run1, bool &run2, uint32_t &r1,
-                                         uint32_t &r2) {
+                                         uint32_t &r2, uint32_t w1) {
     using SH = BvShape<W>;
     const uint2 *pp = (const uint2 *)((const char *)peq_bytes + addr);
     uint32_t d1[SH::ND], d2[SH::ND];
@@ -196,28 +216,68 @@ __device__ __forceinline__ void bv_step2(BvState<BvShape<W>::KF> &S1, BvState<Bv
         if (j == m) {
             if (run1) {
                 const uint32_t Tj = S1.T + (t + 1) - __builtin_popcount(S1.acc >> (31 - t));
-                r1 = min(bv_extract<W>(S1, Tj, n1 + W - m), (uint32_t)W + 1);
+                r1 = min(bv_extract<W>(S1, Tj, n1 + W - m), w1);
                 run1 = false;
             }
             if (run2) {
                 const uint32_t Tj = S2.T + (t + 1) - __builtin_popcount(S2.acc >> (31 - t));
-                r2 = min(bv_extract<W>(S2, Tj, n2 + W - m), (uint32_t)W + 1);
+                r2 = min(bv_extract<W>(S2, Tj, n2 + W - m), w1);
                 run2 = false;
             }
         }
     }
 }
 
-template <int W, bool SLOW, int t = 0>
+// rmap: the compact tables' map symbol id -> row byte offset (LDS, CMP only)
+template <int W, bool CMP, bool SLOW, int t = 0>
 __device__ __forceinline__ void bv_block(BvState<BvShape<W>::KF> &S1, BvState<BvShape<W>::KF> &S2,
-                                         const uint32_t *peq, const uint32_t (&sym)[16], uint32_t base,
-                                         uint32_t j0, uint32_t m, uint32_t n1, uint32_t n2, bool &run1, bool &run2,
-                                         uint32_t &r1, uint32_t &r2) {
+                                         const uint32_t *peq, const uint16_t *rmap, const uint32_t (&sym)[16],
+                                         uint32_t base, uint32_t j0, uint32_t m, uint32_t n1, uint32_t n2, bool &run1,
+                                         bool &run2, uint32_t &r1, uint32_t &r2, uint32_t w1) {
     if constexpr (t < 32) {
         const uint32_t w = sym[t / 2];
-        const uint32_t addr = ((t & 1) ? (w >> 16) : (w & 0xffffu)) + base;
-        bv_step2<W, t, SLOW>(S1, S2, peq, addr, j0 + t + 1, m, n1, n2, run1, run2, r1, r2);
-        bv_block<W, SLOW, t + 1>(S1, S2, peq, sym, base, j0, m, n1, n2, run1, run2, r1, r2);
+        const uint32_t s = (t & 1) ? (w >> 16) : (w & 0xffffu);
+        const uint32_t addr = (CMP ? (uint32_t)rmap[s] : s) + base;
+        bv_step2<W, t, SLOW>(S1, S2, peq, addr, j0 + t + 1, m, n1, n2, run1, run2, r1, r2, w1);
+        bv_block<W, CMP, SLOW, t + 1>(S1, S2, peq, rmap, sym, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
+    }
+}
+
+// The Peq rows of a workgroup's one or two queries (a1, n1 -> slot 0; a2, n2 -> slot 1) into the zeroed LDS
+// tables: bit (i + 1 + OFF) of the row of the query's symbol i. Stream value 0xffff (a query symbol the store
+// lacks) sets nothing. CMP: stream values are symbol ids; each distinct id first claims a row (atomicOr on a
+// claim bitmap, row 0 stays the zero row) and rmap[id] = its byte offset; otherwise the values are the rows'
+// byte offsets already.
+template <int W, bool CMP>
+__device__ __forceinline__ void bv_peq_build(uint32_t *peq, uint32_t rmap_dw, uint32_t claim_dw, uint32_t row_bytes,
+                                             uint32_t *rows, const uint16_t *a1, uint32_t n1, const uint16_t *a2,
+                                             uint32_t n2) {
+    using SH = BvShape<W>;
+    uint16_t *rmap = (uint16_t *)(peq + rmap_dw);
+    if constexpr (CMP) {
+        uint32_t *claim = peq + claim_dw;
+        for (uint32_t q = 0; q < 2; ++q) {
+            const uint16_t *a = q ? a2 : a1;
+            const uint32_t n = q ? n2 : n1;
+            for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+                const uint32_t s = a[i];
+                if (s == 0xffffu) continue;
+                const uint32_t bit = 1u << (s & 31);
+                if (!(atomicOr(&claim[s >> 5], bit) & bit)) rmap[s] = (uint16_t)((atomicAdd(rows, 1u) + 1u) * row_bytes);
+            }
+        }
+        __syncthreads();
+    }
+    for (uint32_t q = 0; q < 2; ++q) {
+        const uint16_t *a = q ? a2 : a1;
+        const uint32_t n = q ? n2 : n1;
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+            const uint32_t s = a[i];
+            if (s == 0xffffu) continue;
+            const uint32_t off = CMP ? (uint32_t)rmap[s] : s;
+            const uint32_t p = i + 1 + SH::OFF;
+            atomicOr(&peq[off / 4 + (p >> 5) * 2 + q], 1u << (p & 31));
+        }
     }
 }
 
@@ -327,8 +387,10 @@ __device__ __forceinline__ void qg_l1x2(const uint4 *__restrict__ cp, const uint
 #ifndef NMZ_ED_BV_WAVES
 #define NMZ_ED_BV_WAVES 5
 #endif
+// W = 64 (4 state words per query) at 4 waves/SIMD (128 VGPRs): at 5 it spilled 168 bytes per lane
 #if NMZ_ED_BV_WAVES > 0
-#define NMZ_ED_BV_ATTR __attribute__((amdgpu_waves_per_eu(NMZ_ED_BV_WAVES, NMZ_ED_BV_WAVES)))
+#define NMZ_ED_BV_ATTR \
+    __attribute__((amdgpu_waves_per_eu(W == 64 ? 4 : NMZ_ED_BV_WAVES, W == 64 ? 4 : NMZ_ED_BV_WAVES)))
 #else
 #define NMZ_ED_BV_ATTR
 #endif
@@ -355,15 +417,17 @@ __device__ __forceinline__ void bv_flush_counters(uint64_t *counters, uint32_t c
 // the pairs that need a DP, from fetch(idx, j, run1, run2)) drawn by the lanes through the LDS counter pool_next
 // (which must start at 256: entries 0..255 are pre-assigned), each run to extraction or cut-off, the in-band
 // results listed (bv_publish). Work counters are accumulated into the caller's registers.
-template <int W, class Fetch>
+template <int W, bool CMP, class Fetch>
 __device__ __forceinline__ void bv_dp_run(const EdBvArgs &A, const uint32_t *peq, uint32_t &pool_next, uint32_t ns,
                                           uint32_t q1, uint32_t q2, uint32_t n1, uint32_t n2, bool has2, Fetch fetch,
                                           uint32_t &c_dp_pairs, uint32_t &c_in_band, uint32_t &c_blocks,
                                           uint32_t &c_dp_cand, uint32_t &c_live) {
     using SH = BvShape<W>;
     const uint32_t lane = threadIdx.x & 63;
+    const uint32_t w = A.w, w1 = A.w + 1;
+    const uint16_t *rmap = (const uint16_t *)(peq + A.rmap_dw);
     // lane state
-    uint32_t j = 0, m = 0, r1 = W + 1, r2 = W + 1, kb0 = 0;
+    uint32_t j = 0, m = 0, r1 = w1, r2 = w1, kb0 = 0;
     bool run1 = false, run2 = false, active = false, v2 = false;
     const uint16_t *stream = A.bsym;
     BvState<SH::KF> S1, S2;
@@ -395,8 +459,8 @@ __device__ __forceinline__ void bv_dp_run(const EdBvArgs &A, const uint32_t *peq
                     m = A.len[j];
                     stream = A.bsym + A.soff[j];
                     v2 = has2 && j > q2;
-                    r1 = W + 1;
-                    r2 = W + 1;
+                    r1 = w1;
+                    r2 = w1;
                     active = true;
                     c_dp_cand += 1;
                     c_dp_pairs += (uint32_t)run1 + (uint32_t)run2;
@@ -417,19 +481,19 @@ __device__ __forceinline__ void bv_dp_run(const EdBvArgs &A, const uint32_t *peq
         const uint32_t base = (lkb + 1) * 8;
         const bool here = active && (run1 || run2) && m > j0 && m <= j0 + 32;
         if (__any(here)) {
-            bv_block<W, true>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2);
+            bv_block<W, CMP, true>(S1, S2, peq, rmap, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
         } else {
-            bv_block<W, false>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2);
+            bv_block<W, CMP, false>(S1, S2, peq, rmap, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
         }
         S1.T += 32 - __builtin_popcount(S1.acc);
         S2.T += 32 - __builtin_popcount(S2.acc);
-        if (run1 && bv_lower_bound<W>(S1, S1.T) > W) run1 = false;
-        if (run2 && bv_lower_bound<W>(S2, S2.T) > W) run2 = false;
+        if (run1 && bv_lower_bound<W>(S1, S1.T) > w) run1 = false;
+        if (run2 && bv_lower_bound<W>(S2, S2.T) > w) run2 = false;
 #pragma unroll
         for (int r = 0; r < 16; ++r) cur[r] = nxt[r];
         ++kb;
         const bool fin = active && !run1 && !run2;
-        if (__any(fin)) bv_publish(A, fin, j, q1, q2, v2, r1, r2, lane, W, c_in_band);
+        if (__any(fin)) bv_publish(A, fin, j, q1, q2, v2, r1, r2, lane, w, c_in_band);
         if (fin) {
             active = false;
             need = true;
@@ -437,9 +501,8 @@ __device__ __forceinline__ void bv_dp_run(const EdBvArgs &A, const uint32_t *peq
     }
 }
 
-template <int W>
+template <int W, bool CMP>
 __global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv(EdBvArgs A) {
-    using SH = BvShape<W>;
     extern __shared__ uint32_t peq[];
     // pool counter lives after the Peq tables (a static __shared__ variable
     // would shift the dynamic region off 8-byte alignment: misaligned ds_read_b64)
@@ -508,7 +571,8 @@ __global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv(EdBvArgs A) {
             const uint32_t jj = pool_lo + c;
             const bool vv2 = has2 && jj > q2;
             const int32_t dd1 = (int32_t)mm[u] - (int32_t)n1, dd2 = (int32_t)mm[u] - (int32_t)n2;
-            bool a1 = dd1 <= W && dd1 >= -W, a2 = vv2 && dd2 <= W && dd2 >= -W;
+            const int32_t w = (int32_t)A.w;
+            bool a1 = dd1 <= w && dd1 >= -w, a2 = vv2 && dd2 <= w && dd2 >= -w;
             if (a1 && (n1 == 0 || mm[u] == 0)) {
                 const uint64_t r = n1 + mm[u];
                 bv_knn_insert(A.knn + (uint64_t)jj * A.k, A.k, (r << 32) | q1);
@@ -524,7 +588,7 @@ __global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv(EdBvArgs A) {
                 a2 = false;
             }
             if (A.prof) {  // q-gram bound: L1 > 4w => ED_w = w + 1, no DP
-                const bool f1 = a1 && l1[u] > 4 * W, f2 = a2 && l2[u] > 4 * W;
+                const bool f1 = a1 && l1[u] > 4 * A.w, f2 = a2 && l2[u] > 4 * A.w;
                 c_qgram += (uint32_t)f1 + (uint32_t)f2;
                 a1 = a1 && !f1;
                 a2 = a2 && !f2;
@@ -537,23 +601,14 @@ __global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv(EdBvArgs A) {
     if (ns > 0) {  // the two queries' Peq tables (uniform branch: ns is read after the barrier)
         uint4 *p4 = (uint4 *)peq;
         for (uint32_t i = threadIdx.x; i < A.lds_dw / 4; i += 256) p4[i] = make_uint4(0, 0, 0, 0);
+        if (threadIdx.x == 0) peq[A.lds_dw + 3] = 0;  // compact tables: rows claimed
         __syncthreads();
-        const uint16_t *a1 = A.bsym + A.soff[q1];
-        for (uint32_t i = threadIdx.x; i < n1; i += 256) {
-            const uint32_t p = i + 1 + SH::OFF;
-            atomicOr(&peq[(uint32_t)a1[i] / 4 + (p >> 5) * 2 + 0], 1u << (p & 31));
-        }
-        if (has2) {
-            const uint16_t *a2 = A.bsym + A.soff[q2];
-            for (uint32_t i = threadIdx.x; i < n2; i += 256) {
-                const uint32_t p = i + 1 + SH::OFF;
-                atomicOr(&peq[(uint32_t)a2[i] / 4 + (p >> 5) * 2 + 1], 1u << (p & 31));
-            }
-        }
+        bv_peq_build<W, CMP>(peq, A.rmap_dw, A.claim_dw, A.row_bytes, &peq[A.lds_dw + 3], A.bsym + A.soff[q1], n1,
+                             has2 ? A.bsym + A.soff[q2] : nullptr, n2);
         __syncthreads();
     }
 
-    bv_dp_run<W>(A, peq, pool_next, ns, q1, q2, n1, n2, has2,
+    bv_dp_run<W, CMP>(A, peq, pool_next, ns, q1, q2, n1, n2, has2,
                  [&](uint32_t i, uint32_t &jj, bool &a1, bool &a2) {
                      const uint32_t e = surv[i];
                      jj = pool_lo + (e & 0x3fffu);
@@ -582,7 +637,7 @@ __device__ __forceinline__ uint32_t qg_l1_reg(const uint4 (&c)[ED_QG_DW / 4], co
 
 // One tile: queries [64 qb, 64 qb + 64) x candidates [256 cb, 256 cb + 256), pairs j > q only (the shard's tile
 // list: csrc/ed.hip ed_bv_two_phase).
-template <int W, bool COUNT>
+template <bool COUNT>
 __global__ __launch_bounds__(256) void k_ed_qg_filter(EdQgArgs A) {
     __shared__ uint4 qp[64][ED_QG_DW / 4];
     __shared__ uint32_t qlen[64];
@@ -612,7 +667,7 @@ __global__ __launch_bounds__(256) void k_ed_qg_filter(EdQgArgs A) {
         constexpr bool EMPTY = decltype(empty_tag)::value;
         const uint32_t q1 = 64 * qb + 2 * pp, q2 = q1 + 1;
         const uint32_t n1 = qlen[2 * pp], n2 = qlen[2 * pp + 1];
-        const int32_t dd1 = (int32_t)m - (int32_t)n1, dd2 = (int32_t)m - (int32_t)n2;
+        const int32_t dd1 = (int32_t)m - (int32_t)n1, dd2 = (int32_t)m - (int32_t)n2, W = (int32_t)A.w;
         bool a1 = jv && j > q1 && dd1 <= W && dd1 >= -W;
         bool a2 = jv && q2 < A.N && j > q2 && dd2 <= W && dd2 >= -W;
         if constexpr (EMPTY) {
@@ -636,8 +691,8 @@ __global__ __launch_bounds__(256) void k_ed_qg_filter(EdQgArgs A) {
             }
         }
         // q-gram bound: L1 > 4w => ED_w = w + 1, no DP
-        const bool f1 = a1 && qg_l1_reg(cp, qp[2 * pp]) > 4 * W;
-        const bool f2 = a2 && qg_l1_reg(cp, qp[2 * pp + 1]) > 4 * W;
+        const bool f1 = a1 && qg_l1_reg(cp, qp[2 * pp]) > 4 * A.w;
+        const bool f2 = a2 && qg_l1_reg(cp, qp[2 * pp + 1]) > 4 * A.w;
         c_qgram += (uint32_t)f1 + (uint32_t)f2;
         a1 = a1 && !f1;
         a2 = a2 && !f2;
@@ -704,34 +759,23 @@ int ed_qg_scatter_launch(const EdQgArgs &A, hipStream_t st) {
     return NMZ_OK;
 }
 
-int ed_qg_filter_launch(const EdQgArgs &A, uint32_t band, bool count, hipStream_t st) {
+int ed_qg_filter_launch(const EdQgArgs &A, bool count, hipStream_t st) {
     if (A.n_tiles == 0) return NMZ_OK;
     NMZ_CHECK(A.n_tiles < (1ULL << 31), "too many traces for one launch");
     const dim3 g((unsigned)A.n_tiles), b(256);
-#define NMZ_QG(Wv)                                                                          \
-    case Wv:                                                                                \
-        if (count) hipLaunchKernelGGL((k_ed_qg_filter<Wv, true>), g, b, 0, st, A);           \
-        else hipLaunchKernelGGL((k_ed_qg_filter<Wv, false>), g, b, 0, st, A);                \
-        break;
-    switch (band) {
-        NMZ_QG(8)
-        NMZ_QG(16)
-        NMZ_QG(32)
-        default: return fail(NMZ_EINVAL, "internal: band has no bit-parallel kernel");
-    }
-#undef NMZ_QG
+    if (count) hipLaunchKernelGGL(k_ed_qg_filter<true>, g, b, 0, st, A);
+    else hipLaunchKernelGGL(k_ed_qg_filter<false>, g, b, 0, st, A);
     NMZ_HIP(hipGetLastError());
     return NMZ_OK;
 }
 
 // One work item: <= ED_BV_ITEM entries of query pair p (items dealt in XCD-remapped order, so a pair's items and
 // its neighbours' -- near-duplicates share candidates -- run on one XCD).
-template <int W>
+template <int W, bool CMP>
 __global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv_dp(EdBvArgs A, const uint32_t *__restrict__ ioff,
                                                                 const uint32_t *__restrict__ poff,
                                                                 const uint32_t *__restrict__ ent, uint32_t n_pairs,
                                                                 uint32_t n_items) {
-    using SH = BvShape<W>;
     extern __shared__ uint32_t peq[];
     uint32_t &pool_next = peq[A.lds_dw];
     const uint32_t nblk = gridDim.x, per_xcd = nblk / 8;
@@ -750,26 +794,17 @@ __global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv_dp(EdBvArgs A, con
     {
         uint4 *p4 = (uint4 *)peq;
         for (uint32_t i = threadIdx.x; i < A.lds_dw / 4; i += 256) p4[i] = make_uint4(0, 0, 0, 0);
-        if (threadIdx.x == 0) pool_next = 256;
+        if (threadIdx.x == 0) {
+            pool_next = 256;
+            peq[A.lds_dw + 3] = 0;  // compact tables: rows claimed
+        }
     }
     __syncthreads();
-    {
-        const uint16_t *a1 = A.bsym + A.soff[q1];
-        for (uint32_t i = threadIdx.x; i < n1; i += 256) {
-            const uint32_t pos = i + 1 + SH::OFF;
-            atomicOr(&peq[(uint32_t)a1[i] / 4 + (pos >> 5) * 2 + 0], 1u << (pos & 31));
-        }
-        if (has2) {
-            const uint16_t *a2 = A.bsym + A.soff[q2];
-            for (uint32_t i = threadIdx.x; i < n2; i += 256) {
-                const uint32_t pos = i + 1 + SH::OFF;
-                atomicOr(&peq[(uint32_t)a2[i] / 4 + (pos >> 5) * 2 + 1], 1u << (pos & 31));
-            }
-        }
-    }
+    bv_peq_build<W, CMP>(peq, A.rmap_dw, A.claim_dw, A.row_bytes, &peq[A.lds_dw + 3], A.bsym + A.soff[q1], n1,
+                         has2 ? A.bsym + A.soff[q2] : nullptr, n2);
     __syncthreads();
     uint32_t c_dp_pairs = 0, c_in_band = 0, c_blocks = 0, c_dp_cand = 0, c_live = 0;
-    bv_dp_run<W>(A, peq, pool_next, ns, q1, q2, n1, n2, has2,
+    bv_dp_run<W, CMP>(A, peq, pool_next, ns, q1, q2, n1, n2, has2,
                  [&](uint32_t i, uint32_t &jj, bool &a1, bool &a2) {
                      const uint32_t e = ent[e0 + i];
                      jj = e & 0x3fffffffu;
@@ -781,16 +816,23 @@ __global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv_dp(EdBvArgs A, con
 }
 
 int ed_bv_dp_launch(const EdBvArgs &A, const uint32_t *ioff, const uint32_t *poff, const uint32_t *ent,
-                    uint32_t n_pairs, uint32_t n_items, uint32_t band, hipStream_t st) {
+                    uint32_t n_pairs, uint32_t n_items, uint32_t bw, bool cmp, hipStream_t st) {
     if (n_items == 0) return NMZ_OK;
     const unsigned blocks = (n_items + 7) / 8 * 8;  // a multiple of 8 for the XCD remap
     const size_t lds = (size_t)A.lds_dw * 4 + 16;
-    switch (band) {
-        case 8: hipLaunchKernelGGL(k_ed_bv_dp<8>, dim3(blocks), dim3(256), lds, st, A, ioff, poff, ent, n_pairs, n_items); break;
-        case 16: hipLaunchKernelGGL(k_ed_bv_dp<16>, dim3(blocks), dim3(256), lds, st, A, ioff, poff, ent, n_pairs, n_items); break;
-        case 32: hipLaunchKernelGGL(k_ed_bv_dp<32>, dim3(blocks), dim3(256), lds, st, A, ioff, poff, ent, n_pairs, n_items); break;
+#define NMZ_DP(Wv, C) hipLaunchKernelGGL((k_ed_bv_dp<Wv, C>), dim3(blocks), dim3(256), lds, st, A, ioff, poff, ent, n_pairs, n_items)
+    switch (bw * 2 + (cmp ? 1 : 0)) {
+        case 16: NMZ_DP(8, false); break;
+        case 17: NMZ_DP(8, true); break;
+        case 32: NMZ_DP(16, false); break;
+        case 33: NMZ_DP(16, true); break;
+        case 64: NMZ_DP(32, false); break;
+        case 65: NMZ_DP(32, true); break;
+        case 128: NMZ_DP(64, false); break;
+        case 129: NMZ_DP(64, true); break;
         default: return fail(NMZ_EINVAL, "internal: band has no bit-parallel kernel");
     }
+#undef NMZ_DP
     NMZ_HIP(hipGetLastError());
     return NMZ_OK;
 }
@@ -803,7 +845,7 @@ int ed_bv_dp_launch(const EdBvArgs &A, const uint32_t *ioff, const uint32_t *pof
 // match no stored symbol). Each workgroup takes a pool of stored traces; lanes refill as in k_ed_bv.
 // Results go to the queries' k-NN lists only (keys dist << 32 | stored id).
 // ---------------------------------------------------------------------------
-template <int W>
+template <int W, bool CMP>
 __global__ __launch_bounds__(256) void k_ed_bv_query(EdBvQueryArgs A) {
     using SH = BvShape<W>;
     extern __shared__ uint32_t peq[];
@@ -817,19 +859,20 @@ __global__ __launch_bounds__(256) void k_ed_bv_query(EdBvQueryArgs A) {
     {
         uint4 *p4 = (uint4 *)peq;
         for (uint32_t i = threadIdx.x; i < A.lds_dw / 4; i += 256) p4[i] = make_uint4(0, 0, 0, 0);
-        if (threadIdx.x == 0) pool_next = 256;
+        if (threadIdx.x == 0) {
+            pool_next = 256;
+            peq[A.lds_dw + 3] = 0;  // compact tables: rows claimed
+        }
         for (uint32_t i = threadIdx.x; i < 2 * ED_QG_BUCKETS; i += 256) qhist[i] = 0;
     }
     __syncthreads();
     for (uint32_t q = 0; q < A.n_queries; ++q) {
         const uint16_t *a = A.qs + A.qoff[q];
-        for (uint32_t i = threadIdx.x; i < A.nq[q]; i += 256) {
-            if (i + 1 < A.nq[q]) atomicAdd(&qhist[q * ED_QG_BUCKETS + qg_bucket(a[i], a[i + 1])], 1u);
-            if (a[i] == 0xffffu) continue;
-            const uint32_t p = i + 1 + SH::OFF;
-            atomicOr(&peq[(uint32_t)a[i] / 4 + (p >> 5) * 2 + q], 1u << (p & 31));
-        }
+        for (uint32_t i = threadIdx.x; i + 1 < A.nq[q]; i += 256)
+            atomicAdd(&qhist[q * ED_QG_BUCKETS + qg_bucket(a[i], a[i + 1])], 1u);
     }
+    bv_peq_build<W, CMP>(peq, A.rmap_dw, A.claim_dw, A.row_bytes, &peq[A.lds_dw + 3], A.qs + A.qoff[0], A.nq[0],
+                         A.n_queries > 1 ? A.qs + A.qoff[1] : nullptr, A.n_queries > 1 ? A.nq[1] : 0);
     __syncthreads();
     if (threadIdx.x < 2 * ED_QG_DW) {
         uint32_t w = 0;
@@ -839,7 +882,9 @@ __global__ __launch_bounds__(256) void k_ed_bv_query(EdBvQueryArgs A) {
     }
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
-    uint32_t j = 0, m = 0, r1 = W + 1, r2 = W + 1, kb0 = 0;
+    const uint32_t w = A.w, w1 = A.w + 1;
+    const uint16_t *rmap = (const uint16_t *)(peq + A.rmap_dw);
+    uint32_t j = 0, m = 0, r1 = w1, r2 = w1, kb0 = 0;
     bool run1 = false, run2 = false, active = false;
     const uint16_t *stream = A.bsym;
     BvState<SH::KF> S1, S2;
@@ -848,7 +893,7 @@ __global__ __launch_bounds__(256) void k_ed_bv_query(EdBvQueryArgs A) {
     uint32_t kb = 0;
     bool need = true, first = true;
     auto publish = [&](bool fin) {  // in-band results only (k_knn_fill completes the lists, as in k_ed_bv)
-        const bool b1 = fin && r1 <= W, b2 = fin && has2 && r2 <= W;
+        const bool b1 = fin && r1 <= w, b2 = fin && has2 && r2 <= w;
         if (__any(b1)) bv_knn_insert_wave(A.knn, A.k, b1 ? (((uint64_t)r1 << 32) | j) : UINT64_MAX, lane);
         if (__any(b2)) bv_knn_insert_wave(A.knn + A.k, A.k, b2 ? (((uint64_t)r2 << 32) | j) : UINT64_MAX, lane);
     };
@@ -874,19 +919,19 @@ __global__ __launch_bounds__(256) void k_ed_bv_query(EdBvQueryArgs A) {
                     j = pool_lo + idx;
                     m = A.len[j];
                     stream = A.bsym + A.soff[j];
-                    r1 = W + 1;
-                    r2 = W + 1;
-                    const int32_t dd1 = (int32_t)m - (int32_t)n1, dd2 = (int32_t)m - (int32_t)n2;
-                    run1 = dd1 <= W && dd1 >= -W;
-                    run2 = has2 && dd2 <= W && dd2 >= -W;
+                    r1 = w1;
+                    r2 = w1;
+                    const int32_t dd1 = (int32_t)m - (int32_t)n1, dd2 = (int32_t)m - (int32_t)n2, ww = (int32_t)w;
+                    run1 = dd1 <= ww && dd1 >= -ww;
+                    run2 = has2 && dd2 <= ww && dd2 >= -ww;
                     if (run1 && (n1 == 0 || m == 0)) { r1 = n1 + m; run1 = false; }
                     if (run2 && (n2 == 0 || m == 0)) { r2 = n2 + m; run2 = false; }
                     if (A.prof && (run1 || run2)) {  // q-gram bound, as in k_ed_bv
                         uint32_t l1, l2;
                         qg_l1x2(A.prof + (uint64_t)j * (ED_QG_DW / 4), (const uint4 *)qprof,
                                 (const uint4 *)(qprof + ED_QG_DW), l1, l2);
-                        run1 = run1 && l1 <= 4 * W;
-                        run2 = run2 && l2 <= 4 * W;
+                        run1 = run1 && l1 <= 4 * w;
+                        run2 = run2 && l2 <= 4 * w;
                     }
                     if (run1 || run2) {
                         need = false;
@@ -908,14 +953,14 @@ __global__ __launch_bounds__(256) void k_ed_bv_query(EdBvQueryArgs A) {
         const uint32_t base = (lkb + 1) * 8;
         const bool here = active && (run1 || run2) && m > j0 && m <= j0 + 32;
         if (__any(here)) {
-            bv_block<W, true>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2);
+            bv_block<W, CMP, true>(S1, S2, peq, rmap, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
         } else {
-            bv_block<W, false>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2);
+            bv_block<W, CMP, false>(S1, S2, peq, rmap, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
         }
         S1.T += 32 - __builtin_popcount(S1.acc);
         S2.T += 32 - __builtin_popcount(S2.acc);
-        if (run1 && bv_lower_bound<W>(S1, S1.T) > W) run1 = false;
-        if (run2 && bv_lower_bound<W>(S2, S2.T) > W) run2 = false;
+        if (run1 && bv_lower_bound<W>(S1, S1.T) > w) run1 = false;
+        if (run2 && bv_lower_bound<W>(S2, S2.T) > w) run2 = false;
 #pragma unroll
         for (int r = 0; r < 16; ++r) cur[r] = nxt[r];
         ++kb;
@@ -928,30 +973,67 @@ __global__ __launch_bounds__(256) void k_ed_bv_query(EdBvQueryArgs A) {
     }
 }
 
-int ed_bv_query_launch(const EdBvQueryArgs &A, uint32_t band, uint32_t blocks, hipStream_t st) {
+int ed_bv_query_launch(const EdBvQueryArgs &A, uint32_t bw, bool cmp, uint32_t blocks, hipStream_t st) {
     const size_t lds = (size_t)A.lds_dw * 4 + 16 + (2 * ED_QG_DW + 2 * ED_QG_BUCKETS) * 4;
-    switch (band) {
-        case 8: hipLaunchKernelGGL(k_ed_bv_query<8>, dim3(blocks), dim3(256), lds, st, A); break;
-        case 16: hipLaunchKernelGGL(k_ed_bv_query<16>, dim3(blocks), dim3(256), lds, st, A); break;
-        case 32: hipLaunchKernelGGL(k_ed_bv_query<32>, dim3(blocks), dim3(256), lds, st, A); break;
+    if (lds > 65536) {
+        static_assert(ED_BV_LDS_MAX <= 160 * 1024, "LDS");
+        NMZ_CHECK(lds <= ED_BV_LDS_MAX, "the query has too many distinct symbols for the bit-parallel search");
+#define NMZ_ATTR(Wv, C)                                                                                        \
+    if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_ed_bv_query<Wv, C>),                              \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)ED_BV_LDS_MAX) != hipSuccess)     \
+        return fail(NMZ_EHIP, "hipFuncSetAttribute failed");
+        switch (bw * 2 + (cmp ? 1 : 0)) {
+            case 16: NMZ_ATTR(8, false) break;
+            case 17: NMZ_ATTR(8, true) break;
+            case 32: NMZ_ATTR(16, false) break;
+            case 33: NMZ_ATTR(16, true) break;
+            case 64: NMZ_ATTR(32, false) break;
+            case 65: NMZ_ATTR(32, true) break;
+            case 128: NMZ_ATTR(64, false) break;
+            case 129: NMZ_ATTR(64, true) break;
+            default: break;
+        }
+#undef NMZ_ATTR
+    }
+#define NMZ_Q(Wv, C) hipLaunchKernelGGL((k_ed_bv_query<Wv, C>), dim3(blocks), dim3(256), lds, st, A)
+    switch (bw * 2 + (cmp ? 1 : 0)) {
+        case 16: NMZ_Q(8, false); break;
+        case 17: NMZ_Q(8, true); break;
+        case 32: NMZ_Q(16, false); break;
+        case 33: NMZ_Q(16, true); break;
+        case 64: NMZ_Q(32, false); break;
+        case 65: NMZ_Q(32, true); break;
+        case 128: NMZ_Q(64, false); break;
+        case 129: NMZ_Q(64, true); break;
         default: return fail(NMZ_EINVAL, "internal: band has no bit-parallel kernel");
     }
+#undef NMZ_Q
     NMZ_HIP(hipGetLastError());
     return NMZ_OK;
 }
 
-bool ed_bv_supported(uint32_t band) { return band == 8 || band == 16 || band == 32; }
+// any band w <= 64 runs on the kernels of the smallest template band W >= w
+bool ed_bv_supported(uint32_t band) { return band <= 64; }
+uint32_t ed_bv_template(uint32_t band) { return band <= 8 ? 8 : band <= 16 ? 16 : band <= 32 ? 32 : 64; }
 
-int ed_bv_launch(const EdBvArgs &A, uint32_t band, uint64_t blocks, hipStream_t st) {
+int ed_bv_launch(const EdBvArgs &A, uint32_t bw, bool cmp, uint64_t blocks, hipStream_t st) {
     // + pool counters, query q-gram profiles, the pool's survivor list (u16, 14-bit pool index)
     if (A.pool > (1u << 14)) return fail(NMZ_EINVAL, "internal: bit-parallel pool above 16384 candidates");
     const size_t lds = (size_t)A.lds_dw * 4 + 16 + 2 * ED_QG_DW * 4 + ((size_t)A.pool * 2 + 15) / 16 * 16;
-    switch (band) {
-        case 8: hipLaunchKernelGGL(k_ed_bv<8>, dim3((unsigned)blocks), dim3(256), lds, st, A); break;
-        case 16: hipLaunchKernelGGL(k_ed_bv<16>, dim3((unsigned)blocks), dim3(256), lds, st, A); break;
-        case 32: hipLaunchKernelGGL(k_ed_bv<32>, dim3((unsigned)blocks), dim3(256), lds, st, A); break;
+    NMZ_CHECK(lds <= 65536, "internal: bit-parallel LDS above 64 KiB");
+#define NMZ_BV(Wv, C) hipLaunchKernelGGL((k_ed_bv<Wv, C>), dim3((unsigned)blocks), dim3(256), lds, st, A)
+    switch (bw * 2 + (cmp ? 1 : 0)) {
+        case 16: NMZ_BV(8, false); break;
+        case 17: NMZ_BV(8, true); break;
+        case 32: NMZ_BV(16, false); break;
+        case 33: NMZ_BV(16, true); break;
+        case 64: NMZ_BV(32, false); break;
+        case 65: NMZ_BV(32, true); break;
+        case 128: NMZ_BV(64, false); break;
+        case 129: NMZ_BV(64, true); break;
         default: return fail(NMZ_EINVAL, "internal: band has no bit-parallel kernel");
     }
+#undef NMZ_BV
     NMZ_HIP(hipGetLastError());
     return NMZ_OK;
 }

@@ -16,6 +16,8 @@
 //   * the one-bit band slide Xs = Xv >> 1, whose top bit comes from the next
 //     lane through a DPP wave_shl:1 move.
 // ~55 VALU instructions per column cover 2w+1 = 8193 DP cells.
+// Bands 64 < w <= 8192 run on the kernel of the smallest W = 1024 * 2^k >= w with w applied at run time
+// (length band, cut-off, clamp; exact as in ed_bv.hip: min(D_W, w + 1) = min(D_w, w + 1)).
 #include "nmz_common.h"
 #include "nmz_internal.h"
 
@@ -142,9 +144,10 @@ __global__ __launch_bounds__(256) void k_ed_wide(EdWideArgs A) {
     const uint64_t j = __builtin_amdgcn_readfirstlane((uint32_t)(i + 1 + (p - base(i))));
     const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)(A.off[i + 1] - A.off[i]));
     const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(A.off[j + 1] - A.off[j]));
-    uint32_t r = W + 1;
+    const uint32_t w = A.w;
+    uint32_t r = w + 1;
     const int64_t dd = (int64_t)m - (int64_t)n;
-    if (dd <= (int64_t)W && dd >= -(int64_t)W) {
+    if (dd <= (int64_t)w && dd >= -(int64_t)w) {
         if (n == 0 || m == 0) {
             r = n + m;
         } else {
@@ -204,7 +207,7 @@ __global__ __launch_bounds__(256) void k_ed_wide(EdWideArgs A) {
                 for (int k = 0; k < 32; ++k) cur[k] = nxt[k];
                 T += 32 - __builtin_popcount(__builtin_amdgcn_readfirstlane(S.acc));
                 if (j0 + 32 == m) {
-                    r = min((uint32_t)((int32_t)T + wide_prefix<KL>(S, n + W - m, lane)), W + 1);
+                    r = min((uint32_t)((int32_t)T + wide_prefix<KL>(S, n + W - m, lane)), w + 1);
                     done = true;
                     break;
                 }
@@ -212,7 +215,7 @@ __global__ __launch_bounds__(256) void k_ed_wide(EdWideArgs A) {
 #pragma unroll
                 for (int k = 0; k < KL; ++k) mc += __builtin_popcount(S.M[k]);
                 mc = wave_sum_u32(mc);
-                if ((int32_t)T - (int32_t)mc > (int32_t)W) {  // band minimum > w: result w+1
+                if ((int32_t)T - (int32_t)mc > (int32_t)w) {  // band minimum > w: result w+1
                     done = true;
                     break;
                 }
@@ -227,7 +230,7 @@ __global__ __launch_bounds__(256) void k_ed_wide(EdWideArgs A) {
                 }
                 const uint32_t acc0 = __builtin_amdgcn_readfirstlane(S.acc);
                 const uint32_t Tj = T + tail - __builtin_popcount(acc0 >> (32 - tail));
-                r = min((uint32_t)((int32_t)Tj + wide_prefix<KL>(S, n + W - m, lane)), W + 1);
+                r = min((uint32_t)((int32_t)Tj + wide_prefix<KL>(S, n + W - m, lane)), w + 1);
             }
         }
     }
@@ -254,7 +257,8 @@ __global__ void k_wide_peq_build(const uint16_t *__restrict__ sym, const uint64_
     }
 }
 
-bool ed_wide_supported(uint32_t band) { return band == 1024 || band == 2048 || band == 4096 || band == 8192; }
+bool ed_wide_supported(uint32_t band) { return band > 64 && band <= 8192; }
+uint32_t ed_wide_template(uint32_t band) { return band <= 1024 ? 1024 : band <= 2048 ? 2048 : band <= 4096 ? 4096 : 8192; }
 
 uint32_t ed_wide_ndw(uint32_t band, uint32_t max_len) {
     const uint32_t KL = band / 1024;

@@ -52,7 +52,7 @@ constexpr PowTable make_pow_table() {
 // loop passes it in a VGPR the compiler cannot see through, so that the subtract is a full-rate VGPR-VGPR add
 // instead of an add with a literal.
 constexpr uint32_t NEG_M31 = 0u - M31;
-__device__ __forceinline__ uint32_t modmul(uint32_t a, uint32_t b, uint32_t nm = NEG_M31) {
+__host__ __device__ __forceinline__ uint32_t modmul(uint32_t a, uint32_t b, uint32_t nm = NEG_M31) {
     const uint64_t p = (uint64_t)a * (2u * b);
     const uint32_t r = (uint32_t)(p >> 32) + ((uint32_t)p >> 1);
     uint32_t t;
@@ -63,7 +63,7 @@ __device__ __forceinline__ uint32_t modmul(uint32_t a, uint32_t b, uint32_t nm =
 // (a * b mod (2^31 - 1)) << 8 for a, b in [1, 2^31 - 1): only the low 24 bits of the residue survive the shift.
 // r = Q + R (as in modmul) is never M, because a * b is not 0 mod the prime M; so the residue is r when r < 2^31
 // and r - M = r + 1 - 2^31 otherwise, and its low 24 bits are those of r + (r >> 31). No compare, no select.
-__device__ __forceinline__ uint32_t modmul_shl8(uint32_t a, uint32_t b) {
+__host__ __device__ __forceinline__ uint32_t modmul_shl8(uint32_t a, uint32_t b) {
     const uint64_t p = (uint64_t)a * (2u * b);
     const uint32_t r = (uint32_t)(p >> 32) + ((uint32_t)p >> 1);
     return (r + (r >> 31)) << 8;
@@ -79,7 +79,7 @@ __host__ __device__ inline uint32_t seed_reduce(int64_t seed) {
 
 // seeded vec[i] for a compile-time index
 template <int I>
-__device__ __forceinline__ uint64_t vec_c(uint32_t s, uint32_t nm = NEG_M31) {
+__host__ __device__ __forceinline__ uint64_t vec_c(uint32_t s, uint32_t nm = NEG_M31) {
     constexpr uint32_t ca = pow_a(21 + 3 * I), cb = pow_a(22 + 3 * I), cc = pow_a(23 + 3 * I);
     constexpr uint64_t ck = NMZ_GO_RNG_COOKED[I];
     const uint32_t xb = modmul(s, cb, nm), xc = modmul(s, cc, nm);
@@ -90,17 +90,17 @@ __device__ __forceinline__ uint64_t vec_c(uint32_t s, uint32_t nm = NEG_M31) {
 
 // high word of the seeded vec[I] (only x_{21+3I} and x_{22+3I} enter it)
 template <int I>
-__device__ __forceinline__ uint32_t vec_hi(uint32_t s, uint32_t nm = NEG_M31) {
+__host__ __device__ __forceinline__ uint32_t vec_hi(uint32_t s, uint32_t nm = NEG_M31) {
     constexpr uint32_t ca = pow_a(21 + 3 * I), cb = pow_a(22 + 3 * I);
     constexpr uint64_t ck = NMZ_GO_RNG_COOKED[I];
     return modmul_shl8(s, ca) ^ (modmul(s, cb, nm) >> 12) ^ (uint32_t)(ck >> 32);
 }
 
 // outputs 0 and 1 after Seed (no state)
-__device__ __forceinline__ uint64_t out0(uint32_t s, uint32_t nm = NEG_M31) {
+__host__ __device__ __forceinline__ uint64_t out0(uint32_t s, uint32_t nm = NEG_M31) {
     return vec_c<333>(s, nm) + vec_c<606>(s, nm);
 }
-__device__ __forceinline__ uint64_t out1(uint32_t s, uint32_t nm = NEG_M31) {
+__host__ __device__ __forceinline__ uint64_t out1(uint32_t s, uint32_t nm = NEG_M31) {
     return vec_c<332>(s, nm) + vec_c<605>(s, nm);
 }
 

@@ -159,10 +159,26 @@ inline ModParams make_mod(uint64_t m) {
 // v mod m for any 64-bit v and m < 2^31, mu = floor(2^64 / m) (2^64 - 1 for m = 1): q = floor(v * mu / 2^64)
 // is floor(v / m) or one less, so r = v - q*m < 2m < 2^32 and only the low words are needed:
 // r = v_lo - q_lo * m (mod 2^32), with v*mu = vl*mul + (vh*mul + vl*muh) 2^32 + vh*muh 2^64.
-__device__ __forceinline__ uint32_t mod_barrett_small(uint64_t v, uint32_t m, uint64_t mu) {
+// high word of a 32 x 32-bit product (v_mul_hi_u32 on the device; the host decision path shares the code)
+__host__ __device__ __forceinline__ uint32_t umulhi32(uint32_t a, uint32_t b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __umulhi(a, b);
+#else
+    return (uint32_t)(((uint64_t)a * b) >> 32);
+#endif
+}
+__host__ __device__ __forceinline__ uint64_t umulhi64(uint64_t a, uint64_t b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __umul64hi(a, b);
+#else
+    return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+__host__ __device__ __forceinline__ uint32_t mod_barrett_small(uint64_t v, uint32_t m, uint64_t mu) {
     const uint32_t vl = (uint32_t)v, vh = (uint32_t)(v >> 32);
     const uint32_t mul = (uint32_t)mu, muh = (uint32_t)(mu >> 32);
-    const uint64_t a = (uint64_t)vh * mul + __umulhi(vl, mul);
+    const uint64_t a = (uint64_t)vh * mul + umulhi32(vl, mul);
     const uint64_t b = (uint64_t)vl * muh + (uint32_t)a;
     const uint32_t ql = vh * muh + (uint32_t)(a >> 32) + (uint32_t)(b >> 32);
     const uint32_t r = vl - ql * m;

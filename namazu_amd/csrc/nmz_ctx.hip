@@ -404,6 +404,19 @@ int nmz_fnv1a64_batch(nmz_ctx *ctx, const uint64_t *off, const uint8_t *bytes, u
     return NMZ_OK;
 }
 
+int nmz_fnv1a64_batch_host(const uint64_t *off, const uint8_t *bytes, uint64_t n, uint64_t *out) {
+    if (n == 0) return NMZ_OK;
+    NMZ_CHECK(off && out, "NULL argument");
+    for (uint64_t i = 0; i < n; ++i) {
+        NMZ_CHECK(off[i] <= off[i + 1], "offsets must not decrease");
+        NMZ_CHECK(off[i] == off[i + 1] || bytes, "bytes is NULL");
+        uint64_t h = FNV_OFFSET;
+        for (uint64_t b = off[i]; b < off[i + 1]; ++b) h = fnv_step(h, bytes[b]);
+        out[i] = h;
+    }
+    return NMZ_OK;
+}
+
 int nmz_random_params_resolve(int64_t min_ns, int64_t max_ns, double p, nmz_random_params *out) {
     NMZ_CHECK(out != nullptr, "out is NULL");
     // randompolicy.go:223-225: "bad faultActionProbability"

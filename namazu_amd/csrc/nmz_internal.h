@@ -24,7 +24,11 @@ struct Carve {
     static size_t bytes_for(size_t count, size_t elem) { return (count * elem + 255) & ~size_t(255); }
 };
 
-bool ed_bv_supported(uint32_t band);
+bool ed_bv_supported(uint32_t band);   // band <= 64
+uint32_t ed_bv_template(uint32_t band);  // the kernels' template band W >= band: 8, 16, 32 or 64
+// LDS of one bit-parallel workgroup: the kernels with a pool (k_ed_bv, k_ed_bv_dp) stay within 64 KiB (several
+// workgroups per CU); single queries (k_ed_bv_query, ~N / 256 workgroups) may take up to ED_BV_LDS_MAX
+constexpr size_t ED_BV_LDS_MAX = 160 * 1024;
 
 // bit-parallel banded edit distance (ed_bv.hip): 2 queries x a pool of ED_BV_POOL candidates per workgroup
 constexpr uint32_t ED_BV_POOL = 1024;  // base pool; the plan scales it up to 4x for large N (ed.hip)
@@ -39,6 +43,10 @@ struct EdBvArgs {
     const uint4 *prof;            // [N][ED_QG_DW / 4] q-gram profiles (ed_qgram_profiles), or nullptr: no filter
     uint64_t n_chunks;            // chunks of this shard
     uint32_t N, G, k, lds_dw, shard, n_shards, pool;
+    uint32_t w;                   // the requested band (<= the kernel's template W)
+    // compact tables (CMP kernels): LDS dword offsets of the id -> row map (u16) and of the claim bitmap, and the
+    // bytes per Peq row; lds_dw covers Peq rows + map + bitmap
+    uint32_t rmap_dw, claim_dw, row_bytes;
     uint32_t rq;                  // queries per block row (64 x ED_BV_ROW_WAVES64); rq / 2 workgroups share a chunk
 };
 // Block rows of the bit-parallel search: rq = 64 * ED_BV_RW queries; the rq / 2 workgroups of one chunk (one query
@@ -79,11 +87,12 @@ struct EdQgArgs {
                                  // scatter pass, or nullptr (the write pass recomputes the filter)
     uint64_t n_tiles;
     uint32_t N, k, QB, NCB, shard, n_shards;
+    uint32_t w;                  // band
 };
-int ed_qg_filter_launch(const EdQgArgs &A, uint32_t band, bool count, hipStream_t st);
+int ed_qg_filter_launch(const EdQgArgs &A, bool count, hipStream_t st);
 int ed_qg_scatter_launch(const EdQgArgs &A, hipStream_t st);
 int ed_bv_dp_launch(const EdBvArgs &A, const uint32_t *ioff, const uint32_t *poff, const uint32_t *ent,
-                    uint32_t n_pairs, uint32_t n_items, uint32_t band, hipStream_t st);
+                    uint32_t n_pairs, uint32_t n_items, uint32_t bw, bool cmp, hipStream_t st);
 // single-query search on a bit-parallel plan (ed_bv.hip k_ed_bv_query): 1-2 external queries vs every stored trace
 struct EdBvQueryArgs {
     const uint16_t *bsym;  // the plan's stored streams
@@ -95,11 +104,12 @@ struct EdBvQueryArgs {
     uint64_t *knn;         // [n_queries][k]
     const uint4 *prof;     // the stored traces' q-gram profiles, or nullptr: no filter
     uint32_t N, k, lds_dw, pool, n_queries;
+    uint32_t w, rmap_dw, claim_dw, row_bytes;  // band; compact tables as in EdBvArgs
 };
-int ed_bv_query_launch(const EdBvQueryArgs &A, uint32_t band, uint32_t blocks, hipStream_t st);
+int ed_bv_query_launch(const EdBvQueryArgs &A, uint32_t bw, bool cmp, uint32_t blocks, hipStream_t st);
 // unique.hip: sorted distinct symbols on the device (hipcub radix sort + unique); *n_uniq on the host
 int device_unique_u64(const uint64_t *d_sym, uint64_t total, uint64_t *d_uniq, uint64_t *n_uniq, hipStream_t st);
-int ed_bv_launch(const EdBvArgs &A, uint32_t band, uint64_t blocks, hipStream_t st);
+int ed_bv_launch(const EdBvArgs &A, uint32_t bw, bool cmp, uint64_t blocks, hipStream_t st);
 
 // wide-band bit-parallel edit distance (ed_wide.hip): one pair per wave
 struct EdWideArgs {
@@ -113,12 +123,13 @@ struct EdWideArgs {
     uint64_t n_pairs;      // N(N-1)/2
     uint64_t n_waves;      // waves of this shard (chunks of 32 pairs dealt round-robin)
     uint32_t N, k, n_sym, ndw, shard, n_shards;
+    uint32_t w;            // the requested band (<= the kernel's W)
 };
-bool ed_wide_supported(uint32_t band);
+bool ed_wide_supported(uint32_t band);   // 64 < band <= 8192
+uint32_t ed_wide_template(uint32_t band);  // W = 1024, 2048, 4096 or 8192 >= band
 uint32_t ed_wide_ndw(uint32_t band, uint32_t max_len);
 int ed_wide_build_peq(const uint16_t *d_sym, const uint64_t *d_off, uint32_t N, uint32_t n_sym, uint32_t ndw,
                       uint32_t band, uint32_t *d_peq, hipStream_t st);
 int ed_wide_launch(const EdWideArgs &A, uint32_t band, hipStream_t st);
-int ed_bv_launch(const EdBvArgs &A, uint32_t band, uint64_t blocks, hipStream_t st);
 
 }  // namespace nmz

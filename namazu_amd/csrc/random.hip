@@ -29,20 +29,30 @@ constexpr uint32_t INT31N_MAX = 0x7fffffffu - (0x80000000u % INTN_N);  // rand.g
 
 __constant__ uint64_t d_cooked[gorand::LEN] = NMZ_GO_RNG_COOKED_INIT;
 __device__ const gorand::PowTable d_powa = gorand::make_pow_table();
+// the same tables for the host decision path (nmz_random_decide_host): the decision code below is shared
+static constexpr gorand::PowTable h_powa = gorand::make_pow_table();
+static constexpr uint64_t h_cooked[gorand::LEN] = NMZ_GO_RNG_COOKED_INIT;
+#ifdef __HIP_DEVICE_COMPILE__
+#define NMZ_POWA(i) d_powa.v[i]
+#define NMZ_COOKED(i) d_cooked[i]
+#else
+#define NMZ_POWA(i) h_powa.v[i]
+#define NMZ_COOKED(i) h_cooked[i]
+#endif
 
 // seeded vec[p] for a runtime index (slow path)
-__device__ uint64_t vec_rt(uint32_t s, int p) {
-    const uint32_t xa = gorand::modmul(s, d_powa.v[21 + 3 * p]);
-    const uint32_t xb = gorand::modmul(s, d_powa.v[22 + 3 * p]);
-    const uint32_t xc = gorand::modmul(s, d_powa.v[23 + 3 * p]);
-    const uint64_t ck = d_cooked[p];
+__host__ __device__ uint64_t vec_rt(uint32_t s, int p) {
+    const uint32_t xa = gorand::modmul(s, NMZ_POWA(21 + 3 * p));
+    const uint32_t xb = gorand::modmul(s, NMZ_POWA(22 + 3 * p));
+    const uint32_t xc = gorand::modmul(s, NMZ_POWA(23 + 3 * p));
+    const uint64_t ck = NMZ_COOKED(p);
     const uint32_t lo = (xb << 20) ^ xc ^ (uint32_t)ck;
     const uint32_t hi = (xa << 8) ^ (xb >> 12) ^ (uint32_t)(ck >> 32);
     return ((uint64_t)hi << 32) | lo;
 }
 
 // y_t for 0 <= t < 607: y_t = y_{t-607} + y_{t-273}, y_s (s<0) = vec[(333-s) mod 607]
-__device__ uint64_t go_output(uint32_t s, int t) {
+__host__ __device__ uint64_t go_output(uint32_t s, int t) {
     uint64_t acc = 0;
     int u = t;
     while (u >= 0) {
@@ -65,8 +75,8 @@ struct RandomKParams {
 };
 
 // v mod n for v < 2^63, n not a power of two, mu = floor(2^64/n)
-__device__ __forceinline__ uint64_t mod_barrett(uint64_t v, uint64_t n, uint64_t mu) {
-    const uint64_t q = __umul64hi(v, mu);
+__host__ __device__ __forceinline__ uint64_t mod_barrett(uint64_t v, uint64_t n, uint64_t mu) {
+    const uint64_t q = umulhi64(v, mu);
     uint64_t r = v - q * n;
     return r >= n ? r - n : r;
 }
@@ -80,7 +90,7 @@ struct Decision {
 // One decision given the reduced Go seed s (1 <= s < 2^31-1) and uniform class bits.
 // cp = P.cls[cls & NMZ_EV_PRIORITIZED], selected by the caller (the sweep keeps both classes in SGPRs
 // instead of indexing the kernel-argument struct, which costs a scalar load and wait per event)
-__device__ __forceinline__ Decision decide(uint32_t s, uint32_t cls, const ClassParams &cp, int32_t fault_threshold,
+__host__ __device__ __forceinline__ Decision decide(uint32_t s, uint32_t cls, const ClassParams &cp, int32_t fault_threshold,
                                            uint32_t nm = gorand::NEG_M31) {
     Decision d{0, 0, 0};
     int t = 0;
@@ -209,7 +219,7 @@ __global__ __launch_bounds__(256) void k_random_table(const uint64_t *__restrict
                                             evclass[e]);
 }
 
-__device__ __forceinline__ uint64_t seed_prefix(uint64_t seed) {
+__host__ __device__ __forceinline__ uint64_t seed_prefix(uint64_t seed) {
     uint64_t h = FNV_OFFSET;
 #pragma unroll
     for (int i = 0; i < 8; ++i) h = fnv_step(h, (uint32_t)(seed >> (8 * i)) & 0xff);
@@ -671,6 +681,31 @@ int nmz_random_sweep(nmz_ctx *ctx, uint64_t seed0, uint64_t n_seeds, const uint6
                 topk[i].first_fault = NMZ_NONE;
             }
         }
+    }
+    return NMZ_OK;
+}
+
+// Online decisions on the calling host thread (Random.QueueEvent decides at enqueue, util/queue/impl.go:35-46,
+// 110-128): the same FNV, seed reduction and decide() closed forms the kernels run (shared __host__ __device__
+// code above), one event at a time, no device work.
+int nmz_random_decide_host(uint64_t seed, const uint64_t *evhash, const uint8_t *evclass, uint32_t n_events,
+                           const nmz_random_params *params, int64_t *delays, uint8_t *faults) {
+    RandomKParams kp;
+    NMZ_TRY(make_kparams(params, kp));
+    if (n_events == 0) return NMZ_OK;
+    NMZ_CHECK(evhash && evclass && delays && faults, "NULL argument");
+    const uint64_t h0 = seed_prefix(seed);
+    for (uint32_t e = 0; e < n_events; ++e) {
+        const uint32_t cls = evclass[e];
+        NMZ_CHECK((cls & ~(NMZ_EV_PRIORITIZED | NMZ_EV_FAULTABLE)) == 0,
+                  "evclass has unknown bits (ProcSetEvent decisions are out of scope)");
+        uint64_t h = h0;
+        for (int i = 0; i < 8; ++i) h = fnv_step(h, (uint32_t)(evhash[e] >> (8 * i)) & 0xff);
+        const Decision d = decide(gorand::seed_reduce((int64_t)h), cls, kp.cls[cls & NMZ_EV_PRIORITIZED],
+                                  kp.fault_threshold);
+        if (d.overflow) return fail(NMZ_ERANGE, "a decision needed more than 607 Go rng outputs");
+        delays[e] = d.delay;
+        faults[e] = (uint8_t)d.fault;
     }
     return NMZ_OK;
 }

@@ -1681,6 +1681,30 @@ int nmz_replayable_sweep(nmz_ctx *ctx, const uint32_t *seed_off, const uint8_t *
     return NMZ_OK;
 }
 
+// Online decisions on the calling host thread (Replayable.QueueEvent decides at enqueue, replayablepolicy.go:
+// 116-126): FNV-1a 64 over seed || hint, then % uint64(maxInterval) -- k_replayable_dump's direct form.
+int nmz_replayable_decide_host(const uint8_t *seed, uint32_t seed_len, const uint32_t *hint_off,
+                               const uint8_t *hint_bytes, uint32_t n_events, int64_t max_interval_ns,
+                               int64_t *delays) {
+    if (n_events == 0) return NMZ_OK;
+    NMZ_CHECK(hint_off && delays && (seed_len == 0 || seed), "NULL argument");
+    const uint64_t m = (uint64_t)max_interval_ns;  // uint64(r.MaxInterval), replayablepolicy.go:110
+    uint64_t h0 = FNV_OFFSET;
+    for (uint32_t i = 0; i < seed_len; ++i) h0 = fnv_step(h0, seed[i]);
+    for (uint32_t e = 0; e < n_events; ++e) {
+        NMZ_CHECK(hint_off[e] <= hint_off[e + 1], "hint offsets must not decrease");
+        NMZ_CHECK(hint_off[e] == hint_off[e + 1] || hint_bytes, "hint_bytes is NULL");
+        if (m == 0) {  // :101-104
+            delays[e] = 0;
+            continue;
+        }
+        uint64_t h = h0;
+        for (uint32_t b = hint_off[e]; b < hint_off[e + 1]; ++b) h = fnv_step(h, hint_bytes[b]);
+        delays[e] = (int64_t)(h % m);
+    }
+    return NMZ_OK;
+}
+
 // Online decisions for one seed (Replayable.QueueEvent -> determineInterval, replayablepolicy.go:100-126): a batch
 // of n pending events, one thread per event (k_replayable_dump: plain FNV over seed || hint, then % m). No plan:
 // a batch of a few events needs no correction tables, only the launch.

@@ -1,0 +1,152 @@
+// Time-bounded queue: the delivery half of the online decision path (host code only).
+//
+// The reference's queue (util/queue/impl.go:64-128, BasicTBQueue) releases every item after its duration:
+// a goroutine per ranged item (`<-time.After(duration); dequeueChan <- item`) and, for fixed durations, one
+// goroutine over an infinite channel so that equal durations keep their enqueue order (impl_test.go:50-63).
+// Here one timer thread owns a min-heap of (due time, enqueue sequence) and moves every item whose due time
+// has come to a FIFO that consumers block on (ActionChan). Due times are CLOCK_MONOTONIC nanoseconds
+// (std::chrono::steady_clock; Python's time.monotonic_ns), so a caller stamps the enqueue time, decides the
+// delay (nmz_*_decide_host) and enqueues at enqueue + delay; the item records when it was released, so the
+// delivered-delay error (release - due) is exact whatever the consumer does. Equal due times release in
+// enqueue order. The timer sleeps until shortly before the earliest due time and spins the rest, so releases
+// are not late by a futex wake-up.
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <queue>
+#include <thread>
+#include <vector>
+
+#include "nmz_common.h"
+
+namespace nmz {
+
+static inline int64_t mono_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+struct TbItem {
+    int64_t due;
+    uint64_t seq, id;
+    bool operator>(const TbItem &o) const { return due != o.due ? due > o.due : seq > o.seq; }
+};
+struct TbReady {
+    uint64_t id;
+    int64_t due, released;
+};
+
+constexpr int64_t TB_SPIN_NS = 150'000;  // sleep until this much before the due time, then spin
+
+}  // namespace nmz
+
+struct nmz_tbqueue {
+    std::mutex mu;
+    std::condition_variable timer_cv, ready_cv;
+    std::priority_queue<nmz::TbItem, std::vector<nmz::TbItem>, std::greater<nmz::TbItem>> heap;
+    std::deque<nmz::TbReady> ready;
+    uint64_t seq = 0, n_enq = 0, n_rel = 0, n_deq = 0;
+    bool stop = false;
+    std::thread timer;
+
+    void loop() {
+        std::unique_lock<std::mutex> lk(mu);
+        while (!stop) {
+            if (heap.empty()) {
+                timer_cv.wait(lk);
+                continue;
+            }
+            const int64_t due = heap.top().due;
+            int64_t now = nmz::mono_ns();
+            if (due - now > nmz::TB_SPIN_NS) {
+                timer_cv.wait_until(lk, std::chrono::steady_clock::time_point(
+                                            std::chrono::nanoseconds(due - nmz::TB_SPIN_NS)));
+                continue;  // an earlier item may have arrived
+            }
+            if (now < due) {
+                lk.unlock();
+                while (nmz::mono_ns() < due) std::this_thread::yield();
+                lk.lock();
+                now = nmz::mono_ns();
+            }
+            bool any = false;
+            while (!heap.empty() && heap.top().due <= now) {
+                const nmz::TbItem it = heap.top();
+                heap.pop();
+                ready.push_back(nmz::TbReady{it.id, it.due, now});
+                ++n_rel;
+                any = true;
+            }
+            if (any) ready_cv.notify_all();
+        }
+    }
+};
+
+using namespace nmz;
+
+extern "C" {
+
+int nmz_tbqueue_create(nmz_tbqueue **out) {
+    NMZ_CHECK(out != nullptr, "out is NULL");
+    auto *q = new nmz_tbqueue();
+    q->timer = std::thread([q] { q->loop(); });
+    *out = q;
+    return NMZ_OK;
+}
+
+int nmz_tbqueue_destroy(nmz_tbqueue *q) {
+    if (!q) return NMZ_OK;
+    {
+        std::lock_guard<std::mutex> lk(q->mu);
+        q->stop = true;
+    }
+    q->timer_cv.notify_all();
+    q->ready_cv.notify_all();
+    q->timer.join();
+    delete q;
+    return NMZ_OK;
+}
+
+int64_t nmz_monotonic_ns(void) { return mono_ns(); }
+
+int nmz_tbqueue_enqueue(nmz_tbqueue *q, uint64_t id, int64_t due_ns) {
+    NMZ_CHECK(q != nullptr, "queue is NULL");
+    {
+        std::lock_guard<std::mutex> lk(q->mu);
+        NMZ_CHECK(!q->stop, "queue is closed");
+        q->heap.push(TbItem{due_ns, q->seq++, id});
+        ++q->n_enq;
+    }
+    q->timer_cv.notify_one();
+    return NMZ_OK;
+}
+
+int nmz_tbqueue_dequeue(nmz_tbqueue *q, int64_t timeout_ns, uint64_t *id, int64_t *due_ns, int64_t *released_ns) {
+    NMZ_CHECK(q && id, "NULL argument");
+    std::unique_lock<std::mutex> lk(q->mu);
+    auto has = [q] { return !q->ready.empty() || q->stop; };
+    if (timeout_ns < 0) {
+        q->ready_cv.wait(lk, has);
+    } else if (!q->ready_cv.wait_for(lk, std::chrono::nanoseconds(timeout_ns), has)) {
+        return fail(NMZ_EAGAIN, "nothing released within the timeout");
+    }
+    if (q->ready.empty()) return fail(NMZ_EAGAIN, "queue is closed");
+    const TbReady r = q->ready.front();
+    q->ready.pop_front();
+    ++q->n_deq;
+    *id = r.id;
+    if (due_ns) *due_ns = r.due;
+    if (released_ns) *released_ns = r.released;
+    return NMZ_OK;
+}
+
+int nmz_tbqueue_stats(nmz_tbqueue *q, uint64_t *enqueued, uint64_t *released, uint64_t *dequeued) {
+    NMZ_CHECK(q != nullptr, "queue is NULL");
+    std::lock_guard<std::mutex> lk(q->mu);
+    if (enqueued) *enqueued = q->n_enq;
+    if (released) *released = q->n_rel;
+    if (dequeued) *dequeued = q->n_deq;
+    return NMZ_OK;
+}
+
+}  // extern "C"

@@ -12,14 +12,16 @@ Mirrors nmz/explorepolicy:
 Error behaviour follows the Go code: LoadConfig *returns* an error value
 (None on success) instead of raising; runtime failures raise (Go panics).
 
-Every delay / fault decision -- batch sweeps and the online QueueEvent path --
-is computed by libnmz_gpu.so on the GPU. There is no CPU decision path.
+Every delay / fault decision is computed by libnmz_gpu.so: batch sweeps on the
+GPU; the online QueueEvent path by the library's host decision functions, which
+run the kernels' own closed forms (shared code) on the calling thread, because
+the reference decides at enqueue and a GPU launch per event would cost more than
+the decision. NMZ_ONLINE=gpu decides queued events in GPU launches
+instead. Without the library nothing runs (namazu_amd._lib raises).
 
-QueueEvent never blocks (randompolicy_test.go:112-118 asserts it): it appends the
-event to a pending list and returns. A decision thread takes every event queued
-since its last launch and decides the whole batch in one call
-(nmz_random_decide / nmz_replayable_decide); a delivery thread puts each action
-on ActionChan at its enqueue time + its delay, as the reference's per-event
+QueueEvent never blocks on the consumer (randompolicy_test.go:112-118 asserts it):
+it decides the event and returns; a delivery thread puts each action on
+ActionChan at its enqueue time + its delay, as the reference's per-event
 goroutine + time.After does (replayablepolicy.go:121-125, util/queue/impl.go:110-128).
 """
 import collections
@@ -78,41 +80,136 @@ class SweepResult:
         self.topk = topk
 
 
+class ActionChannel:
+    """ExplorePolicy.ActionChan() over the library's time-bounded queue (nmz_tbqueue_*, the reference's
+    BasicTBQueue, util/queue/impl.go:64-128): put_at(due_ns, action) hands an action to the native timer
+    thread, which releases it at its due time (CLOCK_MONOTONIC ns); get() blocks (with the GIL released) until an
+    action is released, like a receive on the Go channel. Equal due times keep their enqueue order. Each get()
+    records the action's delivered-delay error (release time - due time, both taken natively)."""
+
+    def __init__(self, history=100_000):
+        self.L = _lib.load()
+        self.q = ctypes.c_void_p()
+        _lib.check(self.L.nmz_tbqueue_create(ctypes.byref(self.q)))
+        self._items = {}
+        self._ids = itertools.count()
+        self._lock = threading.Lock()
+        self.delivery_err_ns = collections.deque(maxlen=history)
+
+    def put_at(self, due_ns, action):
+        with self._lock:
+            i = next(self._ids)
+            self._items[i] = action
+        _lib.check(self.L.nmz_tbqueue_enqueue(self.q, i, int(due_ns)))
+
+    def put(self, action):
+        self.put_at(self.L.nmz_monotonic_ns(), action)
+
+    def get(self, block=True, timeout=None):
+        i, due, rel = ctypes.c_uint64(), ctypes.c_int64(), ctypes.c_int64()
+        t = -1 if (block and timeout is None) else int((timeout if block else 0) * 1e9)
+        rc = self.L.nmz_tbqueue_dequeue(self.q, t, ctypes.byref(i), ctypes.byref(due), ctypes.byref(rel))
+        if rc == _lib.NMZ_EAGAIN:
+            raise queue.Empty
+        _lib.check(rc)
+        self.delivery_err_ns.append(rel.value - due.value)
+        with self._lock:
+            return self._items.pop(i.value)
+
+    def get_nowait(self):
+        return self.get(block=False)
+
+    def stats(self):
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.check(self.L.nmz_tbqueue_stats(self.q, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return a.value, b.value, c.value  # enqueued, released, dequeued
+
+    def close(self):
+        if self.q:
+            self.L.nmz_tbqueue_destroy(self.q)
+            self.q = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class OnlineDecider:
-    """The QueueEvent engine: pending events -> batched GPU decisions -> timed delivery.
+    """The QueueEvent engine: each event's decision, then its delivery at enqueue time + delay.
 
-    decide_batch(events) -> [(delay_ns, action)] runs on the decision thread. latencies_ns holds the
-    enqueue-to-decided time of recent events (bench.py reports p50/p99); batch_sizes the sizes of recent
-    launches. A decision failure is kept and raised by the next submit(), where a Go policy would panic
-    (randompolicy.go:343, replayablepolicy.go:120)."""
+    The reference decides at enqueue, on the caller's goroutine (util/queue/impl.go:35-46,110-128;
+    replayablepolicy.go:116-126), and delivers after time.After(delay). Two ways to decide:
+      * "host" (the default): submit() decides the event on the calling thread through the library's host
+        decision path (nmz_random_decide_host / nmz_replayable_decide_host: the kernels' own closed forms,
+        shared code, no launch), so a decision never waits for a GPU launch or for other events;
+      * "gpu" (NMZ_ONLINE=gpu): a decision thread decides the queued events in GPU launches of at most
+        `max_batch` events (nmz_random_decide / nmz_replayable_decide).
+    Each action goes to ActionChan at its enqueue time + its delay: the library's time-bounded queue releases it
+    from a native timer thread (ActionChannel; without one, a Python delivery thread). latencies_ns holds the
+    enqueue-to-decided time of recent events, delivery_err_ns the delivered-delay error (actual delivery -
+    (enqueue + decided delay)); bench.py reports their percentiles. A GPU decision failure is kept and raised by
+    the next submit(), where a Go policy would panic (randompolicy.go:343, replayablepolicy.go:120)."""
 
-    def __init__(self, decide_batch, deliver, history=100_000):
+    def __init__(self, decide_batch, deliver, decide_one=None, history=100_000, max_batch=64, chan=None):
         self._decide_batch = decide_batch
+        self._decide_one = decide_one
         self._deliver = deliver
+        self._chan = chan  # an ActionChannel: the native queue times the deliveries (no Python delivery thread)
+        self.mode = os.environ.get("NMZ_ONLINE", "host") if decide_one is not None else "gpu"
+        self.max_batch = max_batch
         self._pending = []
         self._cv = threading.Condition()
         self._heap = []
         self._hcv = threading.Condition()
         self._seq = itertools.count()
         self.latencies_ns = collections.deque(maxlen=history)
+        self.delivery_err_ns = chan.delivery_err_ns if chan is not None else collections.deque(maxlen=history)
         self.batch_sizes = collections.deque(maxlen=history)
         self.error = None
         self._started = False
         self._n_in = 0
         self._n_decided = 0
+        self._n_delivered = 0
 
     def _start(self):
-        for fn in (self._decide_loop, self._deliver_loop):
+        loops = [] if self._chan is not None else [self._deliver_loop]
+        if self.mode != "host":
+            loops.append(self._decide_loop)
+        for fn in loops:
             threading.Thread(target=fn, daemon=True).start()
         self._started = True
+
+    def _now(self):
+        return _lib.load().nmz_monotonic_ns() if self._chan is not None else time.monotonic_ns()
+
+    def _schedule(self, due_ns, action):
+        if self._chan is not None:
+            self._chan.put_at(due_ns, action)
+            return
+        with self._hcv:
+            heapq.heappush(self._heap, (due_ns, next(self._seq), action))
+            self._hcv.notify()
 
     def submit(self, event):
         if self.error is not None:
             raise RuntimeError(f"explore policy decision failed: {self.error}") from self.error
+        if not self._started:
+            with self._cv:
+                if not self._started:
+                    self._start()
+        t0 = self._now()
+        if self.mode == "host":
+            delay, action = self._decide_one(event)  # raises like the reference's panic
+            self.latencies_ns.append(self._now() - t0)
+            self._schedule(t0 + max(int(delay), 0), action)
+            with self._cv:
+                self._n_in += 1
+                self._n_decided += 1
+            return
         with self._cv:
-            if not self._started:
-                self._start()
-            self._pending.append((time.monotonic_ns(), event))
+            self._pending.append((t0, event))
             self._n_in += 1
             self._cv.notify()
 
@@ -125,12 +222,26 @@ class OnlineDecider:
                     return False
         return self.error is None
 
+    def wait_delivered(self, timeout=10.0):
+        """Block until every submitted event's action has been released to ActionChan (tests and bench only)."""
+        end = time.monotonic() + timeout
+        while time.monotonic() < end:
+            with self._cv:
+                n_in = self._n_in
+                done = self._n_delivered if self._chan is None else None
+            if done is None:
+                done = self._chan.stats()[1]
+            if done >= n_in:
+                return True
+            time.sleep(0.001)
+        return False
+
     def _decide_loop(self):
         while True:
             with self._cv:
                 while not self._pending:
                     self._cv.wait()
-                batch, self._pending = self._pending, []
+                batch, self._pending = self._pending[:self.max_batch], self._pending[self.max_batch:]
             try:
                 out = self._decide_batch([e for _, e in batch])
             except Exception as e:  # noqa: BLE001 -- surfaced by the next submit()
@@ -138,30 +249,36 @@ class OnlineDecider:
                 with self._cv:
                     self._cv.notify_all()
                 return
-            now = time.monotonic_ns()
+            now = self._now()
             self.batch_sizes.append(len(batch))
-            with self._hcv:
-                for (t0, _), (delay, action) in zip(batch, out):
-                    self.latencies_ns.append(now - t0)
-                    heapq.heappush(self._heap, (t0 + max(int(delay), 0), next(self._seq), action))
-                self._hcv.notify()
+            for (t0, _), (delay, action) in zip(batch, out):
+                self.latencies_ns.append(now - t0)
+                self._schedule(t0 + max(int(delay), 0), action)
             with self._cv:
                 self._n_decided += len(batch)
                 self._cv.notify_all()
 
     def _deliver_loop(self):
+        """Python delivery for a caller-supplied deliver() (no ActionChannel): every action due, in due order."""
         while True:
             with self._hcv:
                 while True:
                     if self._heap:
-                        wait = (self._heap[0][0] - time.monotonic_ns()) / 1e9
-                        if wait <= 0:
-                            _, _, action = heapq.heappop(self._heap)
+                        wait_ns = self._heap[0][0] - time.monotonic_ns()
+                        if wait_ns <= 0:
                             break
-                        self._hcv.wait(wait)
+                        self._hcv.wait(wait_ns / 1e9)
                     else:
                         self._hcv.wait()
-            self._deliver(action)
+                now = time.monotonic_ns()
+                due_items = []
+                while self._heap and self._heap[0][0] <= now:
+                    due_items.append(heapq.heappop(self._heap))
+            for due, _, action in due_items:
+                self._deliver(action)
+                self.delivery_err_ns.append(time.monotonic_ns() - due)
+            with self._cv:
+                self._n_delivered += len(due_items)
 
 
 class ExplorePolicy:
@@ -171,8 +288,9 @@ class ExplorePolicy:
 
     def __init__(self, device=0):
         self._device = device
-        self._action_ch = queue.Queue()  # unbuffered Go channel -> thread-safe queue
-        self.online = OnlineDecider(self._decide_batch, self._action_ch.put)
+        self._action_ch = ActionChannel()  # the Go channel the reference's TBQueue feeds
+        self.online = OnlineDecider(self._decide_batch, self._action_ch.put, decide_one=self._decide_one,
+                                    chan=self._action_ch)
 
     def Name(self):
         return self.NAME
@@ -187,10 +305,14 @@ class ExplorePolicy:
         return self._action_ch
 
     def QueueEvent(self, event):
-        """Non-blocking: the decision and the delayed delivery happen on the policy's threads."""
+        """Non-blocking (never waits for the action's consumer): the event is decided at enqueue, as the reference
+        does, and its action is delivered at enqueue + delay by the policy's delivery thread."""
         self.online.submit(event)
 
     def _decide_batch(self, events):
+        raise NotImplementedError
+
+    def _decide_one(self, event):
         raise NotImplementedError
 
     def _ctx(self):
@@ -262,6 +384,16 @@ class Replayable(ExplorePolicy):
 
     def _decide_batch(self, events):
         return list(zip(self.decide_intervals(events).tolist(), [e.DefaultAction() for e in events]))
+
+    def _decide_one(self, event):
+        """determineInterval on this thread (nmz_replayable_decide_host): FNV-1a 64 over seed || hint % maxInterval."""
+        hint = event.ReplayHint().encode()
+        seed = self.Seed.encode() if isinstance(self.Seed, str) else bytes(self.Seed)
+        off = (ctypes.c_uint32 * 2)(0, len(hint))
+        out = ctypes.c_int64()
+        _lib.check(_lib.load().nmz_replayable_decide_host(seed or None, len(seed), off, hint or None, 1,
+                                                          int(self.MaxInterval), ctypes.byref(out)))
+        return out.value, event.DefaultAction()
 
 
 # ----------------------------------------------------------------- random
@@ -391,6 +523,30 @@ class Random(ExplorePolicy):
         d, f = self.decide_events(events)
         return [(int(dl), e.DefaultFaultAction() if fl else e.DefaultAction())
                 for dl, fl, e in zip(d.tolist(), f.tolist(), events)]
+
+    def event_class(self, ev):
+        if ev.Class() == "ProcSetEvent":
+            raise ValueError("ProcSetEvent decisions belong to procPolicy (out of scope)")
+        c = _lib.NMZ_EV_PRIORITIZED if ev.EntityID() in self.PrioritizedEntities else 0
+        return c | (_lib.NMZ_EV_FAULTABLE if ev.faultable() else 0)
+
+    def _decide_one(self, event):
+        """makeActionForEvent + the queue's delay draw on this thread (nmz_random_decide_host): the event's hash
+        (FNV-1a 64 of its canonical JSON, nmz_fnv1a64_batch_host), its class, and the kernels' closed forms."""
+        L = _lib.load()
+        js = event.canonical_json()
+        js = js.encode() if isinstance(js, str) else bytes(js)
+        off = (ctypes.c_uint64 * 2)(0, len(js))
+        h = ctypes.c_uint64()
+        _lib.check(L.nmz_fnv1a64_batch_host(off, js or None, 1, ctypes.byref(h)))
+        cls = ctypes.c_uint8(self.event_class(event))
+        key = (self.MinInterval, self.MaxInterval, self.FaultActionProbability)
+        if getattr(self, "_params_key", None) != key:
+            self._params, self._params_key = self.params(), key
+        d, f = ctypes.c_int64(), ctypes.c_uint8()
+        _lib.check(L.nmz_random_decide_host(int(self.Seed), ctypes.byref(h), ctypes.byref(cls), 1,
+                                            ctypes.byref(self._params), ctypes.byref(d), ctypes.byref(f)))
+        return d.value, (event.DefaultFaultAction() if f.value else event.DefaultAction())
 
 
 RegisterKnownExplorePolicies()

@@ -271,9 +271,10 @@ def ed_pairs(ts, pairs, band, ctx=None):
 class SimilarityIndex:
     """A stored TraceSet resident on the GPU for single-query similarity search.
 
-    Band 8, 16 or 32 (the bit-parallel plan): each query() is one nmz_ed_plan_query_knn launch over the
-    resident traces. Other bands, alphabets too large for LDS, or queries longer than every stored trace go
-    through nmz_ed_pairs (the generic GPU kernel) against the same TraceSet."""
+    Band <= 64 (the bit-parallel plan, direct or compact tables): each query() is one nmz_ed_plan_query_knn
+    launch over the resident traces. Other bands, stores or queries whose symbols do not fit the LDS tables, or
+    queries longer than every stored trace go through nmz_ed_pairs (the generic GPU kernel) against the same
+    TraceSet."""
 
     def __init__(self, ts, band, ctx=None):
         import ctypes
@@ -297,9 +298,12 @@ class SimilarityIndex:
         qs = [np.asarray(q, np.uint64) for q in queries]
         if self.bitparallel and k <= 64 and max(len(q) for q in qs) <= self.maxlen:
             qset = TraceSet(qs)
-            _lib.check(_lib.load().nmz_ed_plan_query_knn(self.plan, _lib.ptr(qset.off), _lib.ptr(qset.sym), n, k,
-                                                          _lib.ptr(ids), _lib.ptr(ds)))
-            return ids, ds
+            try:
+                _lib.check(_lib.load().nmz_ed_plan_query_knn(self.plan, _lib.ptr(qset.off), _lib.ptr(qset.sym), n,
+                                                              k, _lib.ptr(ids), _lib.ptr(ds)))
+                return ids, ds
+            except _lib.NmzInvalidArgument:
+                pass  # compact tables: the queries hold more distinct symbols than LDS rows -> generic kernel
         for r, q in enumerate(qs):  # generic kernel, pairs (query, every stored trace)
             both = TraceSet([q] + [self.ts.trace(i) for i in range(N)])
             pairs = np.stack([np.zeros(N, np.uint32), np.arange(1, N + 1, dtype=np.uint32)], 1)

@@ -80,13 +80,22 @@ def etcd_traces(n, length, seed=0xE7CD):
 
 
 def clustered_traces(n, length, seed=0x5EED, n_symbols=48, family=1024, edits_mean=6.0,
-                     p_transpose=0.02, p_subst=0.005):
+                     p_transpose=0.02, p_subst=0.005, alphabet_total=None):
     """configs[2] search workload: n traces in families of `family` near-duplicates (module docstring).
-    Trace i belongs to family i // family (contiguous ids). Returns a historystorage.TraceSet."""
+    Trace i belongs to family i // family (contiguous ids). Returns a historystorage.TraceSet.
+    alphabet_total: each family's events are its own `n_symbols` symbols drawn from a store-wide alphabet of
+    that many (different scenarios record different event maps, SURVEY A11: every distinct event map is a
+    symbol), so the store holds thousands of distinct symbols while a trace holds at most n_symbols."""
     from .historystorage import TraceSet
     rng = np.random.default_rng(seed)
     base = _markov_base(length, n_symbols, rng)
-    sym_hash = splitmix64(seed ^ 0xABCDEF, n_symbols)
+    n_fam0 = max(1, -(-n // family))
+    if alphabet_total:
+        fmap = np.stack([rng.choice(alphabet_total, n_symbols, replace=False) for _ in range(n_fam0)])
+        sym_hash = splitmix64(seed ^ 0xABCDEF, alphabet_total)
+    else:
+        fmap = None
+        sym_hash = splitmix64(seed ^ 0xABCDEF, n_symbols)
     n_fam = max(1, -(-n // family))
     parents = np.broadcast_to(base, (n_fam, length)).copy()
     _mutate(parents, rng, n_symbols, p_transpose, p_subst)
@@ -107,6 +116,8 @@ def clustered_traces(n, length, seed=0x5EED, n_symbols=48, family=1024, edits_me
             t[r, i + 1] = a
         r, i = rows[~swap], pos[~swap]
         t[r, i] = rng.integers(0, n_symbols, size=r.size)
+        if fmap is not None:  # local symbols -> the family's store-wide ids
+            t = fmap[(np.arange(c0, c0 + c) // family)[:, None], t]
         ids[c0:c0 + c] = t
     ts = TraceSet([])
     ts.off = np.arange(n + 1, dtype=np.uint64) * np.uint64(length)

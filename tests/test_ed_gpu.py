@@ -52,12 +52,40 @@ def test_knn_bv_pool_sizes(ctx, monkeypatch, pool):
     assert np.array_equal(ids, oi) and np.array_equal(ds, od)
 
 
-@pytest.mark.parametrize("w", [0, 1, 5, 31, 33, 100])
-def test_knn_generic_bands(ctx, w):
+@pytest.mark.parametrize("w", [0, 1, 5, 31, 33, 100, 9000])
+def test_knn_any_band_short_traces(ctx, w):
+    """Short and empty traces at bands the kernels' template W does not equal (bit-parallel W >= w for w <= 64,
+    wide for 64 < w <= 8192, generic beyond)."""
     ts = make_traces(60, 0, 60, 0.2)
     ids, ds = knn(ctx, ts, w, 5)
     oi, od = O.ed_allpairs_knn(ts.off, ts.sym, w, 5)
     assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+
+
+def _plan_kind(ctx, ts, w):
+    L = _lib.load()
+    plan = ctypes.c_void_p()
+    _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), len(ts), w, ctypes.byref(plan)))
+    kind = L.nmz_ed_plan_is_fast(plan)
+    L.nmz_ed_plan_destroy(plan)
+    return kind
+
+
+@pytest.mark.parametrize("w,n,lmin,lmax,mut,kind", [
+    (1, 200, 100, 110, 0.004, 2), (5, 200, 100, 120, 0.02, 2), (20, 200, 150, 250, 0.05, 2),
+    (33, 150, 200, 300, 0.08, 2), (50, 150, 300, 420, 0.1, 2), (64, 120, 300, 400, 0.12, 2),
+    (100, 12, 600, 650, 0.08, 3), (700, 10, 1900, 2100, 0.2, 3), (1500, 8, 3800, 4200, 0.2, 3)])
+def test_knn_band_routing(ctx, w, n, lmin, lmax, mut, kind):
+    """Every band reaches a fast kernel: w <= 64 the bit-parallel kernels of the smallest W in {8, 16, 32, 64}
+    >= w, 64 < w <= 8192 the wide kernel of the smallest W = 1024 * 2^k >= w, each with w applied at run time
+    (length band, q-gram bound, cut-off, clamp at w + 1). Mutation rates put distances on both sides of w."""
+    ts = make_traces(n, lmin, lmax, mut, alphabet=16, rng=np.random.default_rng(w * 31 + n))
+    assert _plan_kind(ctx, ts, w) == kind
+    k = min(6, n - 1)
+    ids, ds = knn(ctx, ts, w, k)
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, w, k, nthreads=16)
+    assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+    assert (od <= w).any() and (od == w + 1).any()  # both sides of the band were exercised
 
 
 def test_knn_large_alphabet_falls_back(ctx):
@@ -237,9 +265,9 @@ def test_knn_wide_etcd_shape(ctx):
 
 @pytest.mark.parametrize("w,alphabet,lmin,lmax,n,kind", [
     (32, 20, 150, 260, 400, 2),     # k_ed_bv
-    (16, 3000, 100, 140, 200, 1),   # k_ed_tile
+    (16, 3000, 300, 400, 200, 1),   # k_ed_tile (a query pair's symbols exceed the compact tables)
     (1024, 16, 1500, 1700, 12, 3),  # k_ed_wide
-    (5, 12, 10, 60, 90, 0),         # k_ed_generic
+    (9000, 12, 10, 60, 90, 0),      # k_ed_generic (beyond the wide kernels)
 ])
 def test_knn_shards_merge_to_full(ctx, w, alphabet, lmin, lmax, n, kind):
     """The multi-GPU path on one device: shard s of 3 into separate partial lists,
@@ -448,3 +476,82 @@ def test_knn_two_phase_entry_limit_fallback(ctx, monkeypatch, limit):
     L.nmz_ed_plan_destroy(plan)
     ref = (od.astype(np.uint64) << np.uint64(32)) | oi.astype(np.uint64)
     assert np.array_equal(sharded, ref)
+
+
+def _family_store(n, family, per_family, alphabet_total, seed, length=2048):
+    from namazu_amd.synth import clustered_traces
+    return clustered_traces(n, length, seed=seed, n_symbols=per_family, family=family,
+                            alphabet_total=alphabet_total, edits_mean=10.0)
+
+
+def test_knn_compact_tables_5000_symbol_store(ctx):
+    """A store whose alphabet (>= 5,000 distinct events, L = 2,048) is far beyond the direct LDS tables (117
+    symbols) stays on the bit-parallel kernels with compact tables (each workgroup's rows = its query pair's own
+    symbols): all-pairs k-NN vs the oracle, the 3-shard merge path, and single queries (nmz_ed_plan_query_knn)
+    vs brute force."""
+    import torch
+    ts = _family_store(520, 4, 40, 200_000, seed=9)
+    assert len(np.unique(ts.sym)) >= 5000
+    n, k, w = len(ts), 8, 32
+    assert _plan_kind(ctx, ts, w) == 2
+    ids, ds = knn(ctx, ts, w, k)
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, w, k, nthreads=16)
+    assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+    assert (od[:, 0] <= w).all()  # every trace has family members inside the band
+    L = _lib.load()
+    plan = ctypes.c_void_p()
+    _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), n, w, ctypes.byref(plan)))
+    S = 3
+    parts = torch.empty(S * n * k, dtype=torch.int64, device="cuda")
+    out = torch.empty(n * k, dtype=torch.int64, device="cuda")
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for sh in range(S):
+        _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, sh, S, ctypes.c_void_p(parts.data_ptr() + sh * n * k * 8),
+                                                   stream))
+    _lib.check(L.nmz_knn_merge_dev(ctx.handle, ctypes.c_void_p(parts.data_ptr()), S, n, k,
+                                   ctypes.c_void_p(out.data_ptr()), stream))
+    _lib.check(L.nmz_ed_knn_fill_dev(plan, k, ctypes.c_void_p(out.data_ptr()), stream))
+    torch.cuda.synchronize()
+    L.nmz_ed_plan_destroy(plan)
+    keys = out.cpu().numpy().view(np.uint64).reshape(n, k)
+    assert np.array_equal((keys >> np.uint64(32)).astype(np.uint32), od)
+    assert np.array_equal((keys & np.uint64(0xFFFFFFFF)).astype(np.uint32), oi)
+    idx = hs.SimilarityIndex(ts, w, ctx=ctx)
+    assert idx.bitparallel
+    rng = np.random.default_rng(4)
+    t = ts.trace(101).copy()
+    t[rng.random(len(t)) < 0.004] = np.uint64(77777)  # a symbol the store never saw
+    qs = [ts.trace(17), t, ts.trace(400)[:2000]]
+    qi, qd = idx.query(qs, 6)
+    idx.close()
+    for r, q in enumerate(qs):
+        both = hs.TraceSet([q] + [ts.trace(i) for i in range(n)])
+        pairs = np.stack([np.zeros(n, np.uint32), np.arange(1, n + 1, dtype=np.uint32)], 1)
+        d = O.ed_pairs(both.off, both.sym, pairs, w, nthreads=16)
+        order = np.lexsort((np.arange(n), d))[:6]
+        assert qd[r].tolist() == d[order].tolist() and qi[r].tolist() == order.tolist(), r
+
+
+@pytest.mark.parametrize("w", [8, 21, 32, 64])
+def test_knn_compact_tables_forced(ctx, monkeypatch, w):
+    """NMZ_ED_COMPACT forces the compact tables on a small-alphabet store: the same lists as the direct tables
+    and the oracle, through the two-phase search, the single-kernel search (NMZ_ED_TWO_PHASE=0) and both plan
+    builds (device: >= 2^20 symbols; NMZ_ED_HOST_REMAP: host)."""
+    ts = make_traces(560, 1850, 2000, 0.004, alphabet=30, rng=np.random.default_rng(w))
+    assert int(ts.off[-1]) >= 1 << 20
+    k = 5
+    ref_i, ref_d = knn(ctx, ts, w, k)
+    monkeypatch.setenv("NMZ_ED_COMPACT", "1")
+    for env in ({}, {"NMZ_ED_TWO_PHASE": "0"}, {"NMZ_ED_HOST_REMAP": "1"}):
+        for key, v in env.items():
+            monkeypatch.setenv(key, v)
+        assert _plan_kind(ctx, ts, w) == 2
+        ci, cd = knn(ctx, ts, w, k)
+        assert np.array_equal(ci, ref_i) and np.array_equal(cd, ref_d), env
+        for key in env:
+            monkeypatch.delenv(key)
+    for q in [0, 301, 559]:
+        pairs = np.array([[q, c] for c in range(len(ts)) if c != q], np.uint32)
+        d = O.ed_pairs(ts.off, ts.sym, pairs, w, nthreads=16)
+        order = np.lexsort((pairs[:, 1], d))[:k]
+        assert ref_d[q].tolist() == d[order].tolist() and ref_i[q].tolist() == pairs[order, 1].tolist()

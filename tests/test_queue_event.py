@@ -228,3 +228,160 @@ def test_online_decide_edge_cases(ctx):
     assert L.nmz_random_decide(ctx.handle, 1, _lib.ptr(eh), _lib.ptr(ok), 2, ctypes.byref(q), _lib.ptr(d),
                                _lib.ptr(f)) == _lib.NMZ_EINVAL
     assert L.nmz_random_decide(ctx.handle, 1, None, None, 0, ctypes.byref(p), None, None) == _lib.NMZ_OK
+
+
+# ------------------------------------------------------------------ host decision path (CPU: no device work)
+def _host_random(seed, eh, ec, params):
+    import ctypes
+    from namazu_amd import _lib
+    eh = np.ascontiguousarray(eh, np.uint64)
+    ec = np.ascontiguousarray(ec, np.uint8)
+    d = np.zeros(max(len(eh), 1), np.int64)
+    f = np.zeros(max(len(eh), 1), np.uint8)
+    _lib.check(_lib.load().nmz_random_decide_host(seed, _lib.ptr(eh), _lib.ptr(ec), len(eh), ctypes.byref(params),
+                                                  _lib.ptr(d), _lib.ptr(f)))
+    return d[:len(eh)], f[:len(eh)]
+
+
+@pytest.mark.parametrize("mn,mx,p", [(30_000_000, 100_000_000, 0.1), (0, 3_000_000_000, 0.5),
+                                     (5_000_000, 5_000_000, 0.999), (1, 2, 1.0), (0, 1 << 40, 0.0),
+                                     (-7, 9_000_000_000_000, 0.3)])
+def test_host_random_decisions_match_oracle(golden, mn, mx, p):
+    """nmz_random_decide_host (the online path: the kernels' closed forms on the host) vs the oracle's full
+    rand.Seed per decision, every class, the searched rejection vectors (re-draws after a ranged delay and for a
+    fixed-duration class), seeds 0 / 2^64 - 1 / the vectors' seed."""
+    from namazu_amd import _lib
+    from oracle import oracle as O
+    g = golden("random_rejections.json")
+    rng = np.random.default_rng(mx % 1000 + 3)
+    eh = np.concatenate([rng.integers(0, 2**64, 400, dtype=np.uint64), np.array(g["ranged"] + g["fixed"], np.uint64)])
+    ec = rng.integers(0, 4, len(eh)).astype(np.uint8)
+    ec[-8:] = 2
+    params = _lib.resolve_random_params(mn, mx, p)
+    pr = O.random_params(mn, mx, p)
+    for seed in (0, 2**64 - 1, g["seed"], 1234567):
+        d, f = _host_random(seed, eh, ec, params)
+        for i in range(len(eh)):
+            od, of, _ = O.random_decide(seed, int(eh[i]), int(ec[i]), pr)
+            assert (int(d[i]), bool(f[i])) == (od, of), (seed, i)
+
+
+def test_host_replayable_and_fnv_match_oracle():
+    """nmz_replayable_decide_host: FNV-1a 64(seed || hint) % uint64(maxInterval), every modulus class (0, small,
+    >= 2^30, uint64 of negative durations); nmz_fnv1a64_batch_host vs the published vectors."""
+    import ctypes
+    from namazu_amd import _lib
+    from namazu_amd.explorepolicy import to_csr
+    from namazu_amd.signal import fnv1a64
+    from oracle import oracle as O
+    L = _lib.load()
+    hints = ["", "a", "hint-entity-0-1", "-9223372036854775808"] + [str(x) for x in range(-50, 50, 7)]
+    ho, hb = to_csr(hints)
+    for seed in [b"", b"foobar", b"1048575"]:
+        sb = np.frombuffer(seed, np.uint8).copy() if seed else np.zeros(1, np.uint8)
+        for m in [0, 1, 100_000_000, (1 << 30) + 3, -5_000_000, -1, 2**63 - 1]:
+            out = np.zeros(len(hints), np.int64)
+            _lib.check(L.nmz_replayable_decide_host(_lib.ptr(sb), len(seed), _lib.ptr(ho), _lib.ptr(hb), len(hints), m,
+                                                    _lib.ptr(out)))
+            assert out.tolist() == [O.replayable_interval(seed.decode(), h, m) for h in hints]
+    strs = [b"", b"a", b"foobar", b"x" * 1000]
+    off, data = to_csr(strs)
+    off64 = off.astype(np.uint64)
+    out = np.zeros(len(strs), np.uint64)
+    _lib.check(L.nmz_fnv1a64_batch_host(_lib.ptr(off64), _lib.ptr(data), len(strs), _lib.ptr(out)))
+    assert out.tolist() == [fnv1a64(x) for x in strs]
+    assert int(out[2]) == 0x85944171F73967E8
+    bad = np.array([0, 4], np.uint8)
+    eh = np.array([1, 2], np.uint64)
+    d = np.zeros(2, np.int64)
+    f = np.zeros(2, np.uint8)
+    p = _lib.resolve_random_params(1, 5, 0.5)
+    assert L.nmz_random_decide_host(1, _lib.ptr(eh), _lib.ptr(bad), 2, ctypes.byref(p), _lib.ptr(d),
+                                    _lib.ptr(f)) == _lib.NMZ_EINVAL
+
+
+def test_queue_event_host_path_decides_at_enqueue():
+    """QueueEvent in the default host mode (no device needed): every event is decided inside QueueEvent (the
+    reference decides at enqueue, util/queue/impl.go:35-46), the actions equal the oracle's decisions and arrive
+    no earlier than enqueue + delay, in due-time order."""
+    from oracle import oracle as O
+    p = _random_policy()
+    assert p.online.mode == "host"
+    events = [packet_event(i, 4) for i in range(300)]
+    t0 = time.monotonic_ns()
+    for ev in events:
+        p.QueueEvent(ev)
+    assert p.online._n_decided == len(events)  # decided synchronously
+    got = [p.ActionChan().get(timeout=10) for _ in events]
+    pr = O.random_params(p.MinInterval, p.MaxInterval, p.FaultActionProbability)
+    want = {}
+    for ev in events:
+        d, f, _ = O.random_decide(p.Seed, ev.evhash(), int(p.event_class(ev)), pr)
+        want[ev.ID()] = (d, "PacketFaultAction" if f else "EventAcceptanceAction")
+    assert sorted(a.Event().ID() for a in got) == sorted(want)
+    assert all(a.Class() == want[a.Event().ID()][1] for a in got)
+    assert (time.monotonic_ns() - t0) >= max(d for d, _ in want.values()) - 1_000_000
+    assert p.online.wait_delivered(5) and min(p.online.delivery_err_ns) >= 0
+
+
+# ------------------------------------------------------------------ GPU: host path == GPU path; burst timing
+@pytest.mark.gpu
+def test_host_and_gpu_online_decisions_agree(ctx):
+    """nmz_random_decide_host == nmz_random_decide (GPU launch) == the sweep's dump, 3,000 events;
+    nmz_replayable_decide_host == nmz_replayable_decide."""
+    import ctypes
+    from namazu_amd import _lib
+    from namazu_amd.explorepolicy import to_csr
+    p = _random_policy()
+    rng = np.random.default_rng(41)
+    eh = rng.integers(0, 2**64, 3000, dtype=np.uint64)
+    ec = rng.integers(0, 4, 3000, dtype=np.uint8)
+    r = p.Sweep(p.Seed, 1, eh, ec, n_dump=1)
+    dh, fh = _host_random(p.Seed, eh, ec, p.params())
+    assert np.array_equal(dh, r.delays[0]) and np.array_equal(fh, r.faults[0])
+
+    class _E:
+        def __init__(self, h, c):
+            self.h, self.c = h, c
+    p.event_inputs = lambda evs: (np.array([e.h for e in evs], np.uint64), np.array([e.c for e in evs], np.uint8))
+    dg, fg = p.decide_events([_E(h, c) for h, c in zip(eh, ec)])
+    assert np.array_equal(dg, dh) and np.array_equal(fg, fh.astype(bool))
+    L = _lib.load()
+    ho, hb = to_csr([f"hint-entity-{i % 7}-{i}" for i in range(2000)])
+    sb = np.frombuffer(b"foobar", np.uint8).copy()
+    a, b = np.zeros(2000, np.int64), np.zeros(2000, np.int64)
+    _lib.check(L.nmz_replayable_decide(ctx.handle, _lib.ptr(sb), 6, _lib.ptr(ho), _lib.ptr(hb), 2000, 1_000_000_000,
+                                       _lib.ptr(a)))
+    _lib.check(L.nmz_replayable_decide_host(_lib.ptr(sb), 6, _lib.ptr(ho), _lib.ptr(hb), 2000, 1_000_000_000,
+                                            _lib.ptr(b)))
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.gpu
+def test_queue_event_burst_keeps_the_decided_timing(ctx):
+    """A 2,000-event burst (QueueEvent back to back, configs[0]'s 30-100 ms delays, 4 prioritized entities):
+    enqueue -> decided p99 < 5 ms and delivered-delay error (actual delivery - (enqueue + decided delay)) p99
+    < 1 ms, so the executed schedule is the decided one (util/queue/impl.go:110-128)."""
+    p = ep.Random()
+    assert p.LoadConfig(Config({"explorePolicy": "random", "explorePolicyParam": {
+        "minInterval": "30ms", "maxInterval": "100ms", "faultActionProbability": 0.1, "seed": 1,
+        "prioritizedEntities": [f"entity-{i}" for i in range(4)]}})) is None
+    for ev in [packet_event(i, 16) for i in range(20)]:  # warm-up (library load, threads)
+        p.QueueEvent(ev)
+    assert p.online.wait_delivered(5)
+    for _ in range(20):
+        p.ActionChan().get(timeout=5)
+    p.online.latencies_ns.clear()
+    p.online.delivery_err_ns.clear()
+    events = [packet_event(i, 16) for i in range(2000)]
+    for ev in events:
+        p.QueueEvent(ev)
+    assert p.online.wait_delivered(10)
+    for _ in events:  # the consumer (the orchestrator's actionRoutine); release times were stamped natively
+        p.ActionChan().get(timeout=5)
+    lat = np.array(p.online.latencies_ns) / 1e6
+    err = np.array(p.online.delivery_err_ns) / 1e6
+    assert len(lat) == 2000 and len(err) == 2000
+    assert np.percentile(lat, 99) < 5.0, np.percentile(lat, 99)
+    assert np.percentile(err, 99) < 1.0, np.percentile(err, 99)
+    assert err.min() >= 0

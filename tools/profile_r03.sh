@@ -7,7 +7,7 @@
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-prof}; shift || true
-LEGS=${*:-replayable random ed_clustered ed_survey ed_wide visualize}
+LEGS=${*:-replayable random ed_clustered ed_survey ed_alphabet ed_wide visualize}
 mkdir -p $R/gpurun_out/$TAG
 python3 $R/tools/kernel_isa.py $R/namazu_amd/libnmz_gpu.so $R/gpurun_out/$TAG/isa.json > /dev/null
 cd /tmp && export TMPDIR=/tmp

@@ -21,12 +21,16 @@ LEGS = {
     # two-phase search: the DP kernel per pair that ran the DP (the k_ed_bv counters of the bench workload:
     # 51,032,886 clustered, 306,187 survey), the filter passes (count + write, one key) per pair of the search
     # the filter phase is the count pass plus the scatter (write) pass: bench.py times both under one name
-    "ed_clustered": [("void nmz::k_ed_bv_dp<32>", "k_ed_bv_dp:clustered", "DP pair", 51_032_886),
-                     ("void nmz::k_ed_qg_filter<32", "k_ed_qg_filter:clustered", "pair", 100_000 * 99_999 // 2),
+    "ed_clustered": [("void nmz::k_ed_bv_dp<32, false>", "k_ed_bv_dp:clustered", "DP pair", 51_032_886),
+                     ("void nmz::k_ed_qg_filter<", "k_ed_qg_filter:clustered", "pair", 100_000 * 99_999 // 2),
                      ("nmz::k_ed_qg_scatter", "k_ed_qg_filter:clustered", "pair", 100_000 * 99_999 // 2)],
-    "ed_survey": [("void nmz::k_ed_bv_dp<32>", "k_ed_bv_dp:survey", "DP pair", 306_187),
-                  ("void nmz::k_ed_qg_filter<32", "k_ed_qg_filter:survey", "pair", 100_000 * 99_999 // 2),
+    "ed_survey": [("void nmz::k_ed_bv_dp<32, false>", "k_ed_bv_dp:survey", "DP pair", 306_187),
+                  ("void nmz::k_ed_qg_filter<", "k_ed_qg_filter:survey", "pair", 100_000 * 99_999 // 2),
                   ("nmz::k_ed_qg_scatter", "k_ed_qg_filter:survey", "pair", 100_000 * 99_999 // 2)],
+    # compact tables (a store-wide alphabet of thousands of events): the CMP instantiation
+    "ed_alphabet": [("void nmz::k_ed_bv_dp<32, true>", "k_ed_bv_dp:alphabet", "DP pair", 51_000_000),
+                    ("void nmz::k_ed_qg_filter<", "k_ed_qg_filter:alphabet", "pair", 100_000 * 99_999 // 2),
+                    ("nmz::k_ed_qg_scatter", "k_ed_qg_filter:alphabet", "pair", 100_000 * 99_999 // 2)],
     "ed_wide": [("void nmz::k_ed_wide<4>", "k_ed_wide", "pair", 256 * 255 // 2)],
     # one launch per mode per step (PO first, then exact): the profile's average mixes both modes, so the
     # per-mode figures come from the two kernel instantiations
