@@ -411,6 +411,60 @@ def bench_random_fault_sweep(args, torch, D, ctx, L, stream):
     return out
 
 
+def bench_replayable_cliffs(args, torch, D, ctx, L, stream):
+    """K1 outside configs[1]'s comfort zone (the reference accepts any Duration, replayablepolicy.go:66-72):
+    maxInterval 2 s and 3 s (residues >= 2^31: the 32-bit sums overflow and are corrected) at configs[1]'s shape,
+    and a 10,000-event trace whose order-query row image exceeds LDS (class segments split into passes). One
+    2^20-seed sweep + top-64 per step on one stream (no pipelining), decisions/s and the sweep's kernel time."""
+    from namazu_amd import _lib
+    S = args.seeds
+    csr = decimal_csr(0, S)
+    dev = torch.device("cuda", D.local_rank)
+    d_soff = torch.from_numpy(csr[0].view(np.int32)).to(dev)
+    d_sb = torch.from_numpy(csr[1]).to(dev)
+    d_stats = torch.empty(S * 32, dtype=torch.uint8, device=dev)
+    d_tk = torch.empty(64 * 24, dtype=torch.uint8, device=dev)
+    out = []
+    for E, m in ((4096, 2_000_000_000), (4096, 3_000_000_000), (10_000, MAX_INTERVAL_NS)):
+        hoff, hb = __import__("namazu_amd.explorepolicy", fromlist=["to_csr"]).to_csr(zk_hints(E))
+        plan = ctypes.c_void_p()
+        _lib.check(L.nmz_replayable_plan_create(ctx.handle, host_ptr(hoff), host_ptr(hb), E, m, S, ctypes.byref(plan)))
+
+        def step():
+            _lib.check(L.nmz_replayable_sweep_topk_dev(plan, ctypes.c_void_p(d_soff.data_ptr()),
+                                                       ctypes.c_void_p(d_sb.data_ptr()), S, 0, 64,
+                                                       ctypes.c_void_p(d_stats.data_ptr()),
+                                                       ctypes.c_void_p(d_tk.data_ptr()), stream))
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        tot, cnt = ctypes.c_double(), ctypes.c_uint64()
+        _lib.check(L.nmz_timing_enable(ctx.handle, 1))
+        L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
+        steps = 10
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        _lib.check(L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
+        _lib.check(L.nmz_timing_enable(ctx.handle, 0))
+        stats = np.frombuffer(d_stats.cpu().numpy().tobytes(), dtype=_lib.SCHED_STATS_DTYPE)
+        parity = None
+        if D.rank == 0 and args.cpu_baseline:
+            from oracle import oracle as O
+            n = 2048
+            st, _ = O.replayable_sweep(csr[0][: n + 1].copy(), csr[1], hoff, hb, m, nthreads=cpu_threads())
+            parity = bool(np.array_equal(st, stats[:n]))
+        L.nmz_replayable_plan_destroy(plan)
+        out.append(dict(events=E, max_interval_ns=m, value=S * E * steps / el, unit="decisions/s",
+                        ms_per_step=el / steps * 1e3, kernel_ms=tot.value / max(cnt.value, 1),
+                        parity_with_oracle_first_2048_seeds=parity))
+    return dict(metric="replayable seed sweep outside configs[1]: long intervals and long traces",
+                config={"workload": "K1 cliffs: maxInterval 2 s / 3 s at 2^20 x 4,096; 2^20 seeds x 10,000 events",
+                        "seeds": S}, lines=out)
+
+
 def bench_visualize(args, torch, D, ctx, L, stream):
     """`nmz tools visualize` over a 100k-run store (2,048 events, 16 entities; runs repeat earlier runs exactly or
     re-interleaved across entities): the unique-trace curve in the reference's default partial-order mode and
@@ -886,7 +940,8 @@ def main():
                     help="run the legs through one nmz_open_group over devices 0..N-1 in this process (C ABI "
                          "multi-GPU path) instead of one process per GPU")
     ap.add_argument("--group-shards", type=int, default=0, help="shards of the --group run (0: one per device)")
-    ap.add_argument("--legs", default="replayable,random,ed_clustered,ed_survey,ed_alphabet,ed_wide,visualize,config0",
+    ap.add_argument("--legs", default="replayable,random,ed_clustered,ed_survey,ed_alphabet,ed_wide,replayable_cliffs,"
+                                      "visualize,config0",
                     help="comma list of legs to run (profiling runs one leg at a time); the headline line "
                          "needs 'replayable'")
     args = ap.parse_args()
@@ -935,6 +990,8 @@ def main():
         for leg, spec in (("ed_clustered", ed3), ("ed_survey", ed3s), ("ed_alphabet", ed3a), ("ed_wide", ed5)):
             if leg in args.legs:
                 sec.append(bench_ed_secondary(args, torch, D, ctx, L, stream, spec))
+        if "replayable_cliffs" in args.legs and D.rank == 0:
+            sec.append(bench_replayable_cliffs(args, torch, D, ctx, L, stream))
         if "visualize" in args.legs and D.rank == 0:
             sec.append(bench_visualize(args, torch, D, ctx, L, stream))
         if "config0" in args.legs and D.rank == 0 and D.world == 1 and args.cpu_baseline:

@@ -132,27 +132,25 @@ enum ModKind : int { MOD_ZERO = 0, MOD_FAST = 1, MOD_GENERAL = 2 };
 struct ModParams {
     uint64_t m;
     uint32_t m32;
-    uint32_t k64;   // 2^64 mod m (FAST only)
-    uint32_t m_k64; // (m - k64) mod m, added when the 64-bit add carried
-    uint64_t mu;    // floor(2^64 / m) for mod_barrett_small (FAST only; 2^64 - 1 for m = 1)
+    uint32_t k64;   // 2^64 mod m (m < 2^32)
+    uint32_t m_k64; // (m - k64) mod m, added when the 64-bit add carried (m < 2^32)
+    uint64_t mu;    // floor(2^64 / m) for mod_barrett_small / mod_barrett64 (m < 2^32; 2^64 - 1 for m = 1)
     int kind;
+    bool m32ok;     // 0 < m < 2^32: residues fit 32 bits (the order-query statistics apply)
 };
 
 inline ModParams make_mod(uint64_t m) {
     ModParams p{};
     p.m = m;
-    if (m == 0) {
-        p.kind = MOD_ZERO;
-    } else if (m < (1ULL << 30)) {
-        p.kind = MOD_FAST;
+    p.m32ok = m != 0 && m < (1ULL << 32);
+    if (p.m32ok) {
         p.m32 = (uint32_t)m;
         uint64_t k = (uint64_t)(((unsigned __int128)1 << 64) % m);
         p.k64 = (uint32_t)k;
         p.m_k64 = (uint32_t)((m - k) % m);
         p.mu = m == 1 ? ~0ULL : (uint64_t)(((unsigned __int128)1 << 64) / m);
-    } else {
-        p.kind = MOD_GENERAL;
     }
+    p.kind = m == 0 ? MOD_ZERO : (m < (1ULL << 30) ? MOD_FAST : MOD_GENERAL);
     return p;
 }
 
@@ -184,6 +182,13 @@ __host__ __device__ __forceinline__ uint32_t mod_barrett_small(uint64_t v, uint3
     const uint32_t r = vl - ql * m;
     uint32_t t;
     return __builtin_sub_overflow(r, m, &t) ? r : t;
+}
+
+// v mod m for any 64-bit v and 0 < m < 2^32, mu = floor(2^64 / m): the quotient estimate is floor(v / m) or one
+// less, so one conditional subtract.
+__host__ __device__ __forceinline__ uint32_t mod_barrett64(uint64_t v, uint64_t m, uint64_t mu) {
+    const uint64_t r = v - umulhi64(v, mu) * m;
+    return (uint32_t)(r >= m ? r - m : r);
 }
 
 // Reduce s in [0, 3m) to [0, m) for m < 2^30 with two branch-free min steps.

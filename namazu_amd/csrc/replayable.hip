@@ -57,11 +57,18 @@ struct nmz_replayable_plan {
     nmz::DevBuf partial;                // per-chunk partial (sum, key) per seed
     nmz::DevBuf topk_lists;             // top-k selection scratch (nmz_replayable_sweep_topk_dev)
     nmz::DevBuf plan_mem;
-    // order-query statistics (k_replayable_sweep_oq): per-row blobs staged whole into LDS
+    // order-query statistics (k_replayable_sweep_oq): per-row blobs staged whole into LDS, one blob per pass
+    // (a row whose image exceeds LDS is split into passes over disjoint class segments; the per-seed statistics
+    // of the passes combine: sums add, maxima max)
     bool oq = false;
-    uint32_t oq_rb16 = 0;               // row image bytes / 16
-    uint4 *d_oq_blob = nullptr;         // [256][rb16] row images (level arrays {Cm, ~e} + samples of C)
-    uint64_t *d_oq_rowsum = nullptr;    // [256] sum of C mod m over the row
+    struct OqPass {
+        uint32_t c0, c1;                // OqClass range of the pass
+        uint64_t off16;                 // first uint4 of the pass's [256][rb16] images in d_oq_blob
+        uint32_t rb16;                  // row image bytes / 16
+    };
+    std::vector<OqPass> oq_passes;
+    uint4 *d_oq_blob = nullptr;         // per pass [256][rb16] row images (level arrays {Cm, ~e} + samples of C)
+    uint64_t *d_oq_rowsum = nullptr;    // [passes][256] sum of C mod m over the pass's part of the row
     nmz::OqClass *d_oq_classes = nullptr;
     nmz::DevBuf oq_mem;
 };
@@ -714,7 +721,7 @@ __global__ __launch_bounds__(256) void k_replayable_merge(const uint4 *__restric
 }
 
 // ---------------------------------------------------------------------------
-// Order-query statistics (MOD_FAST): the per-seed sum, max and first argmax of
+// Order-query statistics (0 < m < 2^32): the per-seed sum, max and first argmax of
 // every decision of a (row L, class) segment without deciding event by event.
 //
 // Inside a segment (C-sorted) every decision is t = (base + Cm) mod m with
@@ -752,7 +759,8 @@ struct OqClass {
     uint32_t start, count;  // table segment (C order)
     uint32_t lv[3];         // level-array bases in the row image (uint2 units)
     uint32_t samp, samp_p2; // sample base; sample slots (a power of two >= ceil(n / 8))
-    uint32_t pad[3];
+    uint32_t pass;          // the pass (row image) holding this segment
+    uint32_t pad[2];
 };
 
 // plan: one workgroup per (top block, row L): the top block's entries (C order) sorted by (Cm, ~e) with a
@@ -761,17 +769,20 @@ struct OqClass {
 // Also writes the 8-event samples of C and adds the block's C mod m to the row sum.
 __global__ __launch_bounds__(256) void k_replayable_oq_levels(const uint4 *__restrict__ table, uint32_t E,
                                                               const uint4 *__restrict__ tb_list,
-                                                              const OqClass *__restrict__ classes, uint32_t rb16,
+                                                              const OqClass *__restrict__ classes,
+                                                              const uint4 *__restrict__ passes,
                                                               uint4 *__restrict__ blob,
                                                               unsigned long long *__restrict__ rowsum) {
     __shared__ uint64_t key[OQ_S0];
     __shared__ unsigned long long part[4];
     const uint4 tb = tb_list[blockIdx.x];  // {class, block start in the segment, size, 0}
     const OqClass ci = classes[tb.x];
+    const uint4 ps = passes[ci.pass];      // {image offset lo, hi (uint4 units), rb16, 0}
     const uint32_t L = blockIdx.y, lo = tb.y, size = tb.z, n = ci.count;
     const bool levels = n > OQ_BRUTE;
     const uint4 *__restrict__ row = table + (uint64_t)L * E + ci.start + lo;
-    uint2 *img = reinterpret_cast<uint2 *>(blob + (uint64_t)L * rb16);
+    uint2 *img = reinterpret_cast<uint2 *>(blob + ((uint64_t)ps.y << 32 | ps.x) + (uint64_t)L * ps.z);
+    rowsum += 256 * ci.pass;
     uint64_t s = 0;
     for (uint32_t i = threadIdx.x; i < OQ_S0; i += 256) {
         if (i < size) {
@@ -828,12 +839,16 @@ __global__ __launch_bounds__(256) void k_replayable_oq_levels(const uint4 *__res
     }
 }
 
-// one decision from a table entry {C lo, C hi, Cm, ~e}: counts carry-free events (d) and wraps (W)
+// one decision from a table entry {C lo, C hi, Cm, ~e}: counts carry-free events (d) and wraps (W).
+// BIG: m >= 2^31, where base + Cm can overflow 32 bits (then the true sum exceeds m, and t = sum - m < m is exact
+// modulo 2^32)
+template <bool BIG>
 __device__ __forceinline__ void oq_decide(uint4 q, uint64_t nH, uint32_t Hm, uint32_t Hm2, uint32_t m, uint32_t &d,
                                           uint32_t &W, uint64_t &key) {
     const bool nc = (((uint64_t)q.y << 32) | q.x) <= nH;
-    const uint32_t s = (nc ? Hm : Hm2) + q.z;
-    const bool wrap = s >= m;
+    const uint32_t b = nc ? Hm : Hm2;
+    const uint32_t s = b + q.z;
+    const bool wrap = BIG ? (s < b || s >= m) : s >= m;
     const uint32_t t = wrap ? s - m : s;
     d += nc;
     W += wrap;
@@ -903,18 +918,22 @@ __device__ __forceinline__ void oq_accum(int side, uint32_t rs, uint32_t cnt, ui
 
 // One seed's statistics over one class segment (replayablepolicy.go:100-114 restated per segment, see above):
 // adds d Hm + (n - d) Hm2 to sum, the segment's wraps to W, and folds its maximum key {t, ~e} into key.
+// BIG: 2^31 <= m < 2^32 (block results need no change: t = b + Cm - wrap * m is exact modulo 2^32).
+template <bool BIG>
 __device__ __forceinline__ void oq_seed_class(const OqClass &ci, const uint2 *__restrict__ img,
                                               const uint4 *__restrict__ row, uint64_t h0, uint32_t m, uint64_t mu,
                                               uint32_t m_k64, uint64_t &sum, uint32_t &W, uint64_t &key) {
     const uint32_t n = ci.count, cs = ci.start;
     const uint64_t H = h0 * ci.pn;
     const uint64_t nH = ~H;
-    const uint32_t Hm = mod_barrett_small(H, m, mu);
+    // Hm = H mod m; Hm2 = (Hm + 2^64 mod m) mod m, where for m >= 2^31 the 32-bit add may overflow (then the true
+    // value exceeds m and one subtract, modulo 2^32, is exact)
+    const uint32_t Hm = BIG ? mod_barrett64(H, m, mu) : mod_barrett_small(H, m, mu);
     const uint32_t t2 = Hm + m_k64;
-    const uint32_t Hm2 = min(t2, t2 - m);
+    const uint32_t Hm2 = BIG ? ((t2 < Hm || t2 >= m) ? t2 - m : t2) : min(t2, t2 - m);
     uint32_t d = 0;
     if (n <= OQ_BRUTE) {
-        for (uint32_t i = 0; i < n; ++i) oq_decide(row[cs + i], nH, Hm, Hm2, m, d, W, key);
+        for (uint32_t i = 0; i < n; ++i) oq_decide<BIG>(row[cs + i], nH, Hm, Hm2, m, d, W, key);
     } else {
         const uint32_t XA = m - Hm, XB = m - Hm2;
         const uint32_t ns = (n + 7) >> 3, nt = (n + OQ_S0 - 1) / OQ_S0;
@@ -946,7 +965,7 @@ __device__ __forceinline__ void oq_seed_class(const OqClass &ci, const uint2 *__
             for (uint32_t i = 0; i < 8; ++i) {
                 uint32_t dd = 0, ww = 0;
                 uint64_t kk = 0;
-                oq_decide(q[i], nH, Hm, Hm2, m, dd, ww, kk);
+                oq_decide<BIG>(q[i], nH, Hm, Hm2, m, dd, ww, kk);
                 const bool in = i < nb;
                 d += in ? dd : 0u;
                 W += in ? ww : 0u;
@@ -1025,8 +1044,16 @@ __device__ __forceinline__ void oq_seed_class(const OqClass &ci, const uint2 *__
     sum += (uint64_t)d * Hm + (uint64_t)(n - d) * Hm2;
 }
 
+// ACC: a later pass over other class segments of the row -- combine with the statistics of the earlier passes
+template <bool ACC>
 __device__ __forceinline__ void oq_store(nmz_sched_stats *__restrict__ stats, uint32_t idx, uint64_t sum,
                                          uint64_t key) {
+    if constexpr (ACC) {
+        const nmz_sched_stats o = stats[idx];
+        sum += o.sum_delay_ns;
+        const uint64_t ko = ((uint64_t)o.max_delay_ns << 32) | (uint32_t)~o.argmax_event;
+        key = ko > key ? ko : key;
+    }
     nmz_sched_stats st;
     st.sum_delay_ns = sum;
     st.max_delay_ns = (int64_t)(key >> 32);
@@ -1053,6 +1080,7 @@ __device__ unsigned long long g_oq_trace[256][16][10];
 constexpr uint32_t OQ_TAIL = 64;
 constexpr uint32_t OQ_TAIL_LDS = OQ_TAIL * 16 + 16;  // {sum, key} per tail seed + the chunk counter
 
+template <bool BIG, bool ACC>
 __global__ __launch_bounds__(OQ_WG) void k_replayable_sweep_oq(
     const uint32_t *__restrict__ bucket_off, const uint64_t *__restrict__ sorted_h0,
     const uint32_t *__restrict__ sorted_idx, const uint4 *__restrict__ table, uint32_t E,
@@ -1114,9 +1142,9 @@ __global__ __launch_bounds__(OQ_WG) void k_replayable_sweep_oq(
         uint32_t W = 0;
         for (uint32_t c = 0; c < n_classes; ++c) {
             const OqClass ci = classes[c];
-            oq_seed_class(ci, img, row, h0, m, mu, m_k64, sum, W, key);
+            oq_seed_class<BIG>(ci, img, row, h0, m, mu, m_k64, sum, W, key);
         }
-        oq_store(stats, sorted_idx[j], sum + rsum - (uint64_t)W * m, key);
+        oq_store<ACC>(stats, sorted_idx[j], sum + rsum - (uint64_t)W * m, key);
 #ifdef OQ_TRACE
         if (lane == 0 && tr_n < 8) g_oq_trace[L][wave][tr_n] = wall_clock64();
         ++tr_n;
@@ -1132,7 +1160,7 @@ __global__ __launch_bounds__(OQ_WG) void k_replayable_sweep_oq(
             uint32_t W = 0;
             for (uint32_t c = part; c < n_classes; c += P) {
                 const OqClass ci = classes[c];
-                oq_seed_class(ci, img, row, h0, m, mu, m_k64, sum, W, key);
+                oq_seed_class<BIG>(ci, img, row, h0, m, mu, m_k64, sum, W, key);
             }
             if (jj < tail) {
                 atomicAdd(tacc + 2 * jj, (unsigned long long)(sum - (uint64_t)W * m));
@@ -1141,7 +1169,8 @@ __global__ __launch_bounds__(OQ_WG) void k_replayable_sweep_oq(
         }
         __syncthreads();
         if (threadIdx.x < tail)
-            oq_store(stats, sorted_idx[smain + threadIdx.x], tacc[2 * threadIdx.x] + rsum, tacc[2 * threadIdx.x + 1]);
+            oq_store<ACC>(stats, sorted_idx[smain + threadIdx.x], tacc[2 * threadIdx.x] + rsum,
+                          tacc[2 * threadIdx.x + 1]);
 #ifdef OQ_TRACE
         if (lane == 0) g_oq_trace[L][wave][8] = wall_clock64();
 #endif
@@ -1249,65 +1278,140 @@ static bool replay_oq_enabled() {
     return on;
 }
 
-// Build the order-query row images after the C sort (MOD_FAST, a row image that fits one workgroup's LDS).
+// image size (uint2 units, before the region offsets) of one class segment's order-query arrays
+struct OqLen {
+    uint64_t v[4] = {0, 0, 0, 0};  // level 0, 1, 2 and samples
+};
+static OqLen oq_seg_len(uint32_t n) {
+    OqLen l;
+    if (n > OQ_BRUTE) {
+        l.v[0] = oq_skew(oq_round(n, OQ_S0));
+        l.v[1] = l.v[2] = oq_skew(oq_round(n, OQ_S1));
+        uint32_t p2 = 1;
+        while (p2 < (n + 7) / 8) p2 <<= 1;
+        l.v[3] = oq_skew(p2);
+    }
+    return l;
+}
+static uint64_t oq_image_bytes(const uint64_t (&len)[4]) {
+    return ((len[0] + len[1] + len[2] + len[3]) * 8 + 15) & ~15ull;
+}
+
+// Build the order-query row images after the C sort (0 < m < 2^32). A row image that fits one workgroup's LDS
+// is one pass over the length classes (configs[1]: 110 KB at E = 4,096). A longer trace splits its classes into
+// C-sorted sub-segments of at most OQ_SUBSEG events -- each one is a segment in its own right: every decision of
+// it is (base + Cm) mod m with the same carry rule (C > ~H), just over fewer events -- and packs them into passes
+// whose images fit; the kernel runs once per pass and combines the passes' statistics per seed.
+constexpr uint32_t OQ_SUBSEG = 4096;
 static int oq_build(nmz_replayable_plan *p, const std::vector<ClassInfo> &cls, hipStream_t st) {
     const uint32_t E = p->n_events;
     p->oq = false;
-    if (p->mod.kind != MOD_FAST || E == 0) return NMZ_OK;
-    std::vector<OqClass> oc(cls.size());
-    std::vector<uint4> tbl;
-    uint64_t len[4] = {1, 0, 0, 0};  // level 0, 1, 2 and samples (uint2 units); slot 0 stays free, so the read
-                                     // below a block (unused when the count is 0) never leaves the image
-    for (size_t c = 0; c < cls.size(); ++c) {
-        const uint32_t n = cls[c].count;
-        OqClass &o = oc[c];
-        o = OqClass{};
-        o.pn = cls[c].pn;
-        o.start = cls[c].start;
-        o.count = n;
-        if (n > OQ_BRUTE) {
-            o.lv[0] = (uint32_t)len[0];
-            len[0] += oq_skew(oq_round(n, OQ_S0));
-            o.lv[1] = (uint32_t)len[1];
-            o.lv[2] = (uint32_t)len[2];
-            len[1] += oq_skew(oq_round(n, OQ_S1));
-            len[2] += oq_skew(oq_round(n, OQ_S1));
-            o.samp = (uint32_t)len[3];
-            uint32_t p2 = 1;
-            while (p2 < (n + 7) / 8) p2 <<= 1;
-            o.samp_p2 = p2;
-            len[3] += oq_skew(p2);
+    p->oq_passes.clear();
+    if (!p->mod.m32ok || E == 0) return NMZ_OK;
+    uint64_t budget = OQ_LDS_MAX - OQ_TAIL_LDS;
+    if (const char *e = getenv("NMZ_REPLAY_OQ_BUDGET"))  // tests: force several passes on short traces
+        budget = std::min<uint64_t>(budget, std::max<uint64_t>(4096, strtoull(e, nullptr, 10)));
+    // segments: the classes whole when the whole row fits one pass, else sub-segments of <= OQ_SUBSEG events
+    std::vector<ClassInfo> seg;
+    {
+        uint64_t len[4] = {1, 0, 0, 0};
+        for (const ClassInfo &c : cls) {
+            const OqLen l = oq_seg_len(c.count);
+            for (int r = 0; r < 4; ++r) len[r] += l.v[r];
         }
-        for (uint32_t lo = 0; lo < n; lo += OQ_S0) tbl.push_back(make_uint4((uint32_t)c, lo, std::min(OQ_S0, n - lo), 0));
+        const bool split = oq_image_bytes(len) > budget;
+        // sub-segments small enough that one always fits the budget
+        uint32_t sub = OQ_SUBSEG;
+        while (sub > OQ_S0) {
+            const OqLen l = oq_seg_len(sub);
+            const uint64_t one[4] = {1 + l.v[0], l.v[1], l.v[2], l.v[3]};
+            if (oq_image_bytes(one) <= budget) break;
+            sub /= 2;
+        }
+        for (const ClassInfo &c : cls) {
+            if (!split || c.count <= sub) {
+                seg.push_back(c);
+                continue;
+            }
+            for (uint32_t lo = 0; lo < c.count; lo += sub)
+                seg.push_back(ClassInfo{c.pn, c.start + lo, std::min(sub, c.count - lo)});
+        }
     }
-    const uint64_t total = len[0] + len[1] + len[2] + len[3];
-    const uint64_t rb = (total * 8 + 15) & ~15ull;
-    if (rb + OQ_TAIL_LDS > OQ_LDS_MAX) return NMZ_OK;
-    for (OqClass &o : oc) {  // regions: level 0 | level 1 | level 2 | samples
-        o.lv[1] += (uint32_t)len[0];
-        o.lv[2] += (uint32_t)(len[0] + len[1]);
-        o.samp += (uint32_t)(len[0] + len[1] + len[2]);
+    // passes: consecutive segments while the image fits (slot 0 of every image stays free, so the read below a
+    // block, unused when the count is 0, never leaves the image)
+    std::vector<OqClass> oc(seg.size());
+    std::vector<uint4> tbl;
+    uint64_t off16 = 0;
+    for (size_t c0 = 0; c0 < seg.size();) {
+        uint64_t len[4] = {1, 0, 0, 0};
+        size_t c1 = c0;
+        for (; c1 < seg.size(); ++c1) {
+            const OqLen l = oq_seg_len(seg[c1].count);
+            uint64_t t[4];
+            for (int r = 0; r < 4; ++r) t[r] = len[r] + l.v[r];
+            if (c1 > c0 && oq_image_bytes(t) > budget) break;
+            OqClass &o = oc[c1];
+            o = OqClass{};
+            o.pn = seg[c1].pn;
+            o.start = seg[c1].start;
+            o.count = seg[c1].count;
+            o.pass = (uint32_t)p->oq_passes.size();
+            if (o.count > OQ_BRUTE) {
+                o.lv[0] = (uint32_t)len[0];
+                o.lv[1] = (uint32_t)len[1];
+                o.lv[2] = (uint32_t)len[2];
+                o.samp = (uint32_t)len[3];
+                uint32_t p2 = 1;
+                while (p2 < (o.count + 7) / 8) p2 <<= 1;
+                o.samp_p2 = p2;
+            }
+            for (int r = 0; r < 4; ++r) len[r] = t[r];
+            for (uint32_t lo = 0; lo < o.count; lo += OQ_S0)
+                tbl.push_back(make_uint4((uint32_t)c1, lo, std::min(OQ_S0, o.count - lo), 0));
+        }
+        const uint64_t rb = oq_image_bytes(len);
+        if (rb > budget) return NMZ_OK;  // cannot happen with OQ_SUBSEG segments; keep the per-decision sweep
+        for (size_t c = c0; c < c1; ++c) {  // regions: level 0 | level 1 | level 2 | samples
+            oc[c].lv[1] += (uint32_t)len[0];
+            oc[c].lv[2] += (uint32_t)(len[0] + len[1]);
+            oc[c].samp += (uint32_t)(len[0] + len[1] + len[2]);
+        }
+        p->oq_passes.push_back(nmz_replayable_plan::OqPass{(uint32_t)c0, (uint32_t)c1, off16, (uint32_t)(rb / 16)});
+        off16 += 256 * (rb / 16);
+        c0 = c1;
     }
     // function attributes are per device, and contexts on several devices (or threads) build plans
-    // concurrently: set it on every build (cheap) instead of behind a process-wide flag
-    if (hipFuncSetAttribute(reinterpret_cast<const void *>(k_replayable_sweep_oq),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)OQ_LDS_MAX) != hipSuccess)
-        return NMZ_OK;  // keep the per-decision sweep
-    const size_t need = Carve::bytes_for(256 * rb / 16, 16) + Carve::bytes_for(256, 8) +
-                        Carve::bytes_for(oc.size(), sizeof(OqClass)) + Carve::bytes_for(tbl.size(), 16);
+    // concurrently: set them on every build (cheap) instead of behind a process-wide flag
+    for (const void *f : {reinterpret_cast<const void *>(k_replayable_sweep_oq<false, false>),
+                          reinterpret_cast<const void *>(k_replayable_sweep_oq<false, true>),
+                          reinterpret_cast<const void *>(k_replayable_sweep_oq<true, false>),
+                          reinterpret_cast<const void *>(k_replayable_sweep_oq<true, true>)})
+        if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)OQ_LDS_MAX) != hipSuccess) {
+            p->oq_passes.clear();
+            return NMZ_OK;  // keep the per-decision sweep
+        }
+    const size_t np = p->oq_passes.size();
+    std::vector<uint4> passes(np);
+    for (size_t i = 0; i < np; ++i)
+        passes[i] = make_uint4((uint32_t)p->oq_passes[i].off16, (uint32_t)(p->oq_passes[i].off16 >> 32),
+                               p->oq_passes[i].rb16, 0);
+    const size_t need = Carve::bytes_for(off16, 16) + Carve::bytes_for(256 * np, 8) +
+                        Carve::bytes_for(oc.size(), sizeof(OqClass)) + Carve::bytes_for(tbl.size(), 16) +
+                        Carve::bytes_for(np, 16);
     NMZ_TRY(p->oq_mem.ensure(need));
     Carve cv(p->oq_mem.ptr);
-    p->d_oq_blob = cv.take<uint4>(256 * rb / 16);
-    p->d_oq_rowsum = cv.take<uint64_t>(256);
+    p->d_oq_blob = cv.take<uint4>(off16);
+    p->d_oq_rowsum = cv.take<uint64_t>(256 * np);
     p->d_oq_classes = cv.take<OqClass>(oc.size());
     uint4 *d_tbl = cv.take<uint4>(tbl.size());
-    p->oq_rb16 = (uint32_t)(rb / 16);
-    NMZ_HIP(hipMemsetAsync(p->d_oq_blob, 0, 256 * rb, st));
-    NMZ_HIP(hipMemsetAsync(p->d_oq_rowsum, 0, 256 * 8, st));
+    uint4 *d_passes = cv.take<uint4>(np);
+    NMZ_HIP(hipMemsetAsync(p->d_oq_blob, 0, off16 * 16, st));
+    NMZ_HIP(hipMemsetAsync(p->d_oq_rowsum, 0, 256 * np * 8, st));
     NMZ_HIP(hipMemcpyAsync(p->d_oq_classes, oc.data(), oc.size() * sizeof(OqClass), hipMemcpyHostToDevice, st));
     NMZ_HIP(hipMemcpyAsync(d_tbl, tbl.data(), tbl.size() * 16, hipMemcpyHostToDevice, st));
+    NMZ_HIP(hipMemcpyAsync(d_passes, passes.data(), np * 16, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_replayable_oq_levels, dim3((unsigned)tbl.size(), 256), dim3(256), 0, st, p->d_table, E, d_tbl,
-                       p->d_oq_classes, p->oq_rb16, p->d_oq_blob,
+                       p->d_oq_classes, d_passes, p->d_oq_blob,
                        reinterpret_cast<unsigned long long *>(p->d_oq_rowsum));
     NMZ_HIP(hipGetLastError());
     NMZ_HIP(hipStreamSynchronize(st));  // the host vectors above are pageable
@@ -1368,13 +1472,21 @@ static int replayable_stats(nmz_replayable_plan *p, hipStream_t st, const uint32
     const int U = replay_u();
     const uint32_t per_unit = 64u * (uint32_t)U;
     const uint64_t max_units = S / per_unit + 256;
-    if (p->oq && replay_oq_enabled()) {
+    if (p->oq && (replay_oq_enabled() || p->mod.kind != MOD_FAST)) {
         NMZ_TRY(bucket_seeds_counted(st, sc.h0, S, OQ_WG, sc.b, sc.counter));
         KernelTimer kt(p->ctx, st, "replayable_sweep");
-        hipLaunchKernelGGL(k_replayable_sweep_oq, dim3(256), dim3(OQ_WG), p->oq_rb16 * 16u + OQ_TAIL_LDS, st, sc.b.offset,
-                           sc.b.sorted_h0, sc.b.sorted_idx, p->d_table, E, p->d_oq_blob, p->oq_rb16,
-                           reinterpret_cast<const unsigned long long *>(p->d_oq_rowsum), p->d_oq_classes,
-                           p->n_classes, p->mod.m32, p->mod.mu, p->mod.m_k64, d_stats, kt.span());
+        unsigned long long *span = kt.span();
+        const bool big = p->mod.m32 >= 0x80000000u;
+        for (size_t i = 0; i < p->oq_passes.size(); ++i) {
+            const nmz_replayable_plan::OqPass &ps = p->oq_passes[i];
+            auto kern = big ? (i ? k_replayable_sweep_oq<true, true> : k_replayable_sweep_oq<true, false>)
+                            : (i ? k_replayable_sweep_oq<false, true> : k_replayable_sweep_oq<false, false>);
+            hipLaunchKernelGGL(kern, dim3(256), dim3(OQ_WG), ps.rb16 * 16u + OQ_TAIL_LDS, st, sc.b.offset,
+                               sc.b.sorted_h0, sc.b.sorted_idx, p->d_table, E, p->d_oq_blob + ps.off16, ps.rb16,
+                               reinterpret_cast<const unsigned long long *>(p->d_oq_rowsum + 256 * i),
+                               p->d_oq_classes + ps.c0, ps.c1 - ps.c0, p->mod.m32, p->mod.mu, p->mod.m_k64, d_stats,
+                               span);
+        }
         NMZ_HIP(hipGetLastError());
         return NMZ_OK;
     }
@@ -1514,7 +1626,7 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
         DevBuf &tmp = ctx->buf[10];
         if (tmp.ensure((size_t)256 * E * sizeof(uint4)) != NMZ_OK) return cleanup(NMZ_ENOMEM);
         hipLaunchKernelGGL(k_replayable_table, dim3(E), dim3(256), 0, st, d_hoff, d_hbytes, d_perm, E, p->mod.m,
-                           p->mod.kind == MOD_FAST ? 1 : 0, tmp.as<uint4>());
+                           p->mod.m32ok ? 1 : 0, tmp.as<uint4>());
         uint32_t max_class = 0;
         for (const ClassInfo &c : cls) max_class = std::max(max_class, c.count);
         bool bad = false;
@@ -1523,7 +1635,7 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
                                p->d_classes, E, p->d_table);
             // no sync when the order-query images follow: oq_build synchronises after its kernels
             bad = hipGetLastError() != hipSuccess ||
-                  (p->mod.kind != MOD_FAST && hipStreamSynchronize(st) != hipSuccess);
+                  (!p->mod.m32ok && hipStreamSynchronize(st) != hipSuccess);
         } else if (max_class <= 16384) {  // O(n^2) rank sort on the device
             hipLaunchKernelGGL(k_replayable_table_sort, dim3(ceil_div(E, 256), 256), dim3(256), 0, st,
                                tmp.as<uint4>(), p->d_classes, p->n_classes, E, p->d_table);

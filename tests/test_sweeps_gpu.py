@@ -37,6 +37,7 @@ def test_replayable_golden_foobar(ctx, golden):
 
 
 @pytest.mark.parametrize("m", [100_000_000, 1_000_000_000, 10_000_000, 1, 2, 999, 2**30 - 1, 2**30, 2**30 + 5,
+                               2_000_000_000, 2**31 - 1, 2**31, 3_000_000_000, 2**32 - 1, 2**32,
                                2**62 + 11, 2**63 - 1, -5_000_000, -1, 0])
 def test_replayable_moduli(ctx, m):
     seeds = [str(i) for i in range(700)] + ["", "foobar", "x" * 50]
@@ -63,7 +64,7 @@ def test_replayable_many_length_classes_and_ties(ctx):
         assert np.array_equal(r.stats, st)
 
 
-@pytest.mark.parametrize("m", [1, 2, 3, 7, 1000, 100_000_000, 2**30 - 1])
+@pytest.mark.parametrize("m", [1, 2, 3, 7, 1000, 100_000_000, 2**30 - 1, 2**31 + 3, 2**32 - 1])
 def test_replayable_order_query_block_edges(ctx, m):
     """K1's order-query statistics (k_replayable_sweep_oq): length classes whose sizes sit on both sides of the
     8-, 64- and 512-event block edges and of the per-event threshold (24), shuffled so the original event order
@@ -110,6 +111,38 @@ def test_replayable_event_counts_around_stage_and_chunk_edges(ctx, E):
     r = p.Sweep(seeds, hints, n_dump=3, ctx=ctx)
     st, dl = rep_oracle(seeds, hints, 100_000_000, n_dump=3)
     assert np.array_equal(r.stats, st) and np.array_equal(r.delays, dl)
+
+
+@pytest.mark.parametrize("E,m", [(10_000, 100_000_000), (10_000, 2_000_000_000), (6_500, 2**32 - 1)])
+def test_replayable_long_trace_multi_pass(ctx, E, m):
+    """Traces whose order-query row image exceeds LDS (E > ~6k): length classes split into C-sorted sub-segments
+    packed into passes, one kernel run per pass, statistics combined per seed (sum adds, max keys max), incl.
+    maxInterval 2 s and 2^32 - 1 ns (m >= 2^31: 32-bit residue sums that overflow), vs the oracle."""
+    rng = np.random.default_rng(E + m % 1000)
+    hints = zk_hints(E, rng) + ["h" * (i % 7) for i in range(40)]
+    seeds = [str(i) for i in range(300)] + ["foobar"]
+    p = Replayable()
+    p.MaxInterval = m
+    r = p.Sweep(seeds, hints, n_dump=2, k=8, ctx=ctx)
+    st, dl = rep_oracle(seeds, hints, m, n_dump=2)
+    assert np.array_equal(r.stats, st) and np.array_equal(r.delays, dl)
+    assert np.array_equal(r.topk, O.topk_from_stats(st, 0, 8))
+
+
+@pytest.mark.parametrize("budget,m", [(16384, 100_000_000), (30_000, 7), (60_000, 2**31 + 9)])
+def test_replayable_forced_passes(ctx, monkeypatch, budget, m):
+    """NMZ_REPLAY_OQ_BUDGET shrinks the row-image budget so a 3,000-event trace runs as many passes over small
+    sub-segments (and the rows' partial chunks accumulate across passes); results equal the oracle's."""
+    monkeypatch.setenv("NMZ_REPLAY_OQ_BUDGET", str(budget))
+    rng = np.random.default_rng(budget)
+    hints = zk_hints(3000, rng) + ["x" * (i % 5) for i in range(30)]
+    seeds = [str(i) for i in range(1500)]
+    p = Replayable()
+    p.MaxInterval = m
+    r = p.Sweep(seeds, hints, k=5, ctx=ctx)
+    st, _ = rep_oracle(seeds, hints, m)
+    assert np.array_equal(r.stats, st)
+    assert np.array_equal(r.topk, O.topk_from_stats(st, 0, 5))
 
 
 def _seeds_in_one_row(row, n):
