@@ -855,10 +855,21 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
     return NMZ_OK;
 }
 
-// work items per query pair: ceil(entries / ED_BV_ITEM) (items[n_pairs] = 0 closes the scan)
-__global__ void k_bv_items(const uint32_t *__restrict__ cnt, uint32_t n, uint32_t *__restrict__ items) {
+// work items per query pair: ceil(entries / item) (items[n_pairs] = 0 closes the scan)
+__global__ void k_bv_items(const uint32_t *__restrict__ cnt, uint32_t n, uint32_t item, uint32_t *__restrict__ items) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i <= n) items[i] = i < n ? (cnt[i] + ED_BV_ITEM - 1) / ED_BV_ITEM : 0u;
+    if (i <= n) items[i] = i < n ? (cnt[i] + item - 1) / item : 0u;
+}
+
+// Entries per DP work item. One workgroup runs one item with its pair's Peq tables; the last items of a launch
+// leave CUs idle until they end, so their length is the launch's tail (~1 item per CU slot): a shard of the
+// 8-GPU search has 1/8 of the items, so the tail weighs 8x more there.
+uint32_t ed_bv_item() {
+    if (const char *e = getenv("NMZ_ED_ITEM")) {
+        const uint32_t v = (uint32_t)atoi(e);
+        if (v >= 64 && v <= ED_BV_ITEM && (v & (v - 1)) == 0) return v;
+    }
+    return ED_BV_ITEM;
 }
 
 // The two-phase bit-parallel search of one shard (nmz_internal.h EdQgArgs): filter count pass, scans (entry and
@@ -906,10 +917,13 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A) {
     const uint32_t N = p->n, n_pairs = (N + 1) / 2, QB = (N + 63) / 64, NCB = (N + 255) / 256;
     const uint32_t shard = A.shard, n_shards = A.n_shards;
     if (N >= (1u << 30)) return 1;  // entries carry j in 30 bits
-    // this shard's tiles (qb << 32 | cb), built and uploaded once per (shard, n_shards): a tile belongs to shard
-    // tile_mix(qb << 32 | cb) mod n_shards. The DP work is data-dependent and clustered (the clustered workload's
-    // families put it in the few tiles next to the diagonal, with a period of 16 query blocks); a hash breaks
-    // that periodicity, where a round-robin deal aligned with it (8 shards: max/mean shard time 1.27)
+    // this shard's tiles (qb << 32 | cb), built and uploaded once per (shard, n_shards): every tile of query block
+    // qb belongs to shard tile_mix(qb) mod n_shards. Whole query blocks, so a query pair's DP entries stay in one
+    // shard's work items: dealt by tile, a pair's near-duplicate candidates (a few 256-wide tiles) spread over
+    // several shards, every shard built the pair's Peq tables for a fraction of its entries, and the 8 shards
+    // summed to 1.15x the unsharded search. The DP work is data-dependent and clustered (the clustered workload's
+    // families put it next to the diagonal, with a period of 16 query blocks); a hash breaks that periodicity,
+    // where a round-robin deal aligned with it (8 shards: max/mean shard time 1.27)
     const uint64_t key = ((uint64_t)shard << 32) | n_shards;
     DevBuf &tl = p->tile_list[key];
     if (!p->tile_count.count(key)) {
@@ -917,7 +931,7 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A) {
         for (uint32_t qb = 0; qb < QB; ++qb)
             for (uint32_t cb = qb / 4; cb < NCB; ++cb) {
                 const uint64_t id = ((uint64_t)qb << 32) | cb;
-                if (n_shards == 1 || tile_mix(id) % n_shards == shard) tiles.push_back(id);
+                if (n_shards == 1 || tile_mix(qb) % n_shards == shard) tiles.push_back(id);
             }
         NMZ_TRY(tl.ensure(Carve::bytes_for(tiles.size() + 1, 8)));
         if (!tiles.empty()) NMZ_HIP(hipMemcpy(tl.ptr, tiles.data(), tiles.size() * 8, hipMemcpyHostToDevice));
@@ -961,7 +975,8 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A) {
         NMZ_TRY(ed_qg_filter_launch(Q, true, st));
     }
     NMZ_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_cnt, d_poff, (int)n_pairs + 1, st));
-    hipLaunchKernelGGL(k_bv_items, dim3(ceil_div(n_pairs + 1, 256)), dim3(256), 0, st, d_cnt, n_pairs, d_items);
+    const uint32_t item = ed_bv_item();
+    hipLaunchKernelGGL(k_bv_items, dim3(ceil_div(n_pairs + 1, 256)), dim3(256), 0, st, d_cnt, n_pairs, item, d_items);
     NMZ_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_items, d_ioff, (int)n_pairs + 1, st));
     // the entry total in 64 bits: the u32 scans above wrap beyond 2^32 entries (about N^2 / 4 for a store of
     // near-duplicates), so their totals are trusted only once this sum is within ED_TP_MAX_ENTRIES
@@ -983,7 +998,7 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A) {
         else NMZ_TRY(ed_qg_filter_launch(Q, false, st));
     }
     KernelTimer kt(p->ctx, st, "ed_bv_dp");
-    return ed_bv_dp_launch(A, d_ioff, d_poff, Q.ent, n_pairs, (uint32_t)n_items, p->bw, p->cmp, st);
+    return ed_bv_dp_launch(A, d_ioff, d_poff, Q.ent, n_pairs, (uint32_t)n_items, item, p->bw, p->cmp, st);
 }
 
 static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_knn, uint32_t shard = 0,

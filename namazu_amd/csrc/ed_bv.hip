@@ -769,13 +769,13 @@ int ed_qg_filter_launch(const EdQgArgs &A, bool count, hipStream_t st) {
     return NMZ_OK;
 }
 
-// One work item: <= ED_BV_ITEM entries of query pair p (items dealt in XCD-remapped order, so a pair's items and
+// One work item: <= `item` entries of query pair p (items dealt in XCD-remapped order, so a pair's items and
 // its neighbours' -- near-duplicates share candidates -- run on one XCD).
 template <int W, bool CMP>
 __global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv_dp(EdBvArgs A, const uint32_t *__restrict__ ioff,
                                                                 const uint32_t *__restrict__ poff,
                                                                 const uint32_t *__restrict__ ent, uint32_t n_pairs,
-                                                                uint32_t n_items) {
+                                                                uint32_t n_items, uint32_t item) {
     extern __shared__ uint32_t peq[];
     uint32_t &pool_next = peq[A.lds_dw];
     const uint32_t nblk = gridDim.x, per_xcd = nblk / 8;
@@ -787,7 +787,7 @@ __global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv_dp(EdBvArgs A, con
         if (ioff[mid] <= lb) lo = mid; else hi = mid;
     }
     const uint32_t p = lo, ci = lb - ioff[p];
-    const uint32_t e0 = poff[p] + ci * ED_BV_ITEM, e1 = min(poff[p + 1], e0 + ED_BV_ITEM), ns = e1 - e0;
+    const uint32_t e0 = poff[p] + ci * item, e1 = min(poff[p + 1], e0 + item), ns = e1 - e0;
     const uint32_t q1 = 2 * p, q2 = q1 + 1;
     const bool has2 = q2 < A.N;
     const uint32_t n1 = A.len[q1], n2 = has2 ? A.len[q2] : 0;
@@ -816,11 +816,12 @@ __global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv_dp(EdBvArgs A, con
 }
 
 int ed_bv_dp_launch(const EdBvArgs &A, const uint32_t *ioff, const uint32_t *poff, const uint32_t *ent,
-                    uint32_t n_pairs, uint32_t n_items, uint32_t bw, bool cmp, hipStream_t st) {
+                    uint32_t n_pairs, uint32_t n_items, uint32_t item, uint32_t bw, bool cmp, hipStream_t st) {
     if (n_items == 0) return NMZ_OK;
     const unsigned blocks = (n_items + 7) / 8 * 8;  // a multiple of 8 for the XCD remap
     const size_t lds = (size_t)A.lds_dw * 4 + 16;
-#define NMZ_DP(Wv, C) hipLaunchKernelGGL((k_ed_bv_dp<Wv, C>), dim3(blocks), dim3(256), lds, st, A, ioff, poff, ent, n_pairs, n_items)
+#define NMZ_DP(Wv, C) \
+    hipLaunchKernelGGL((k_ed_bv_dp<Wv, C>), dim3(blocks), dim3(256), lds, st, A, ioff, poff, ent, n_pairs, n_items, item)
     switch (bw * 2 + (cmp ? 1 : 0)) {
         case 16: NMZ_DP(8, false); break;
         case 17: NMZ_DP(8, true); break;

@@ -72,8 +72,10 @@ int ed_qgram_profiles(const uint16_t *bs, const uint64_t *soff, const uint32_t *
 //   1. k_ed_qg_filter over tiles of 64 queries x 256 candidates (a candidate's profile in registers against 64
 //      query profiles in LDS) decides every pair's length band and q-gram bound; a count pass sizes, and a write
 //      pass fills, per query pair (2p, 2p + 1) a list of entries j | run1 << 30 | run2 << 31 (pairs needing a DP);
-//   2. k_ed_bv_dp runs work items of <= ED_BV_ITEM entries of one query pair each (its Peq tables in LDS).
-constexpr uint32_t ED_BV_ITEM = 4096;
+//   2. k_ed_bv_dp runs work items of <= `item` entries of one query pair each (its Peq tables in LDS);
+//      ed_bv_item() picks the size (NMZ_ED_ITEM overrides, a power of two in [64, 4096]).
+constexpr uint32_t ED_BV_ITEM = 4096;  // the largest item
+uint32_t ed_bv_item();
 struct EdQgArgs {
     const uint4 *prof;           // [N][ED_QG_DW / 4] q-gram profiles
     const uint32_t *len;         // [N]
@@ -92,7 +94,7 @@ struct EdQgArgs {
 int ed_qg_filter_launch(const EdQgArgs &A, bool count, hipStream_t st);
 int ed_qg_scatter_launch(const EdQgArgs &A, hipStream_t st);
 int ed_bv_dp_launch(const EdBvArgs &A, const uint32_t *ioff, const uint32_t *poff, const uint32_t *ent,
-                    uint32_t n_pairs, uint32_t n_items, uint32_t bw, bool cmp, hipStream_t st);
+                    uint32_t n_pairs, uint32_t n_items, uint32_t item, uint32_t bw, bool cmp, hipStream_t st);
 // single-query search on a bit-parallel plan (ed_bv.hip k_ed_bv_query): 1-2 external queries vs every stored trace
 struct EdBvQueryArgs {
     const uint16_t *bsym;  // the plan's stored streams

@@ -8,8 +8,11 @@
 // (std::chrono::steady_clock; Python's time.monotonic_ns), so a caller stamps the enqueue time, decides the
 // delay (nmz_*_decide_host) and enqueues at enqueue + delay; the item records when it was released, so the
 // delivered-delay error (release - due) is exact whatever the consumer does. Equal due times release in
-// enqueue order. The timer sleeps until shortly before the earliest due time and spins the rest, so releases
-// are not late by a futex wake-up.
+// enqueue order. The timer sleeps until shortly before the earliest due time and busy-waits the rest (no
+// sched_yield: under CFS a yielding thread can lose the CPU for a whole time slice), with a 1 ns timer slack
+// (the default 50 us slack makes a timed wait wake late).
+#include <sys/prctl.h>
+
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -36,7 +39,7 @@ struct TbReady {
     int64_t due, released;
 };
 
-constexpr int64_t TB_SPIN_NS = 150'000;  // sleep until this much before the due time, then spin
+constexpr int64_t TB_SPIN_NS = 100'000;  // sleep until this much before the due time, then spin
 
 }  // namespace nmz
 
@@ -50,6 +53,7 @@ struct nmz_tbqueue {
     std::thread timer;
 
     void loop() {
+        (void)prctl(PR_SET_TIMERSLACK, 1UL, 0UL, 0UL, 0UL);
         std::unique_lock<std::mutex> lk(mu);
         while (!stop) {
             if (heap.empty()) {
@@ -65,7 +69,7 @@ struct nmz_tbqueue {
             }
             if (now < due) {
                 lk.unlock();
-                while (nmz::mono_ns() < due) std::this_thread::yield();
+                while (nmz::mono_ns() < due) __builtin_ia32_pause();
                 lk.lock();
                 now = nmz::mono_ns();
             }

