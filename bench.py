@@ -45,8 +45,23 @@ MAX_INTERVAL_NS = 100_000_000
 VALU_TABLE = os.path.join(HERE, "profiles", "valu_per_unit.json")
 
 
-# the K1 kernel the product runs: order-query statistics unless NMZ_REPLAY_OQ=0 selects the per-decision sweep
-K1_KERNEL = "k_replayable_sweep_fast" if os.environ.get("NMZ_REPLAY_OQ") == "0" else "k_replayable_sweep_oq"
+# the K1 kernel a replayable plan runs (nmz_replayable_plan_kernel): wavelet-tree statistics by default,
+# order-query statistics with NMZ_REPLAY_WT=0 (or when the trees do not fit), the per-decision sweep with
+# NMZ_REPLAY_OQ=0 on top
+K1_KERNELS = {2: "k_replayable_sweep_wt", 1: "k_replayable_sweep_oq", 0: "k_replayable_sweep_fast"}
+K1_ALGORITHM = {
+    "k_replayable_sweep_wt": "wavelet-tree statistics: per (seed, hint-length class) three bucket-indexed searches "
+                             "and two wavelet-tree descents over the rank permutation of the C-sorted segment "
+                             "(DESIGN.md section 4); units = seed x event decisions covered",
+    "k_replayable_sweep_oq": "order-query statistics: per (seed, hint-length class) binary searches over "
+                             "C-mod-m-sorted blocks (DESIGN.md section 4); units = seed x event decisions covered",
+}
+
+
+def k1_kernel(L, plan):
+    if os.environ.get("NMZ_REPLAY_OQ") == "0":
+        return "k_replayable_sweep_fast"
+    return K1_KERNELS[L.nmz_replayable_plan_kernel(plan)]
 
 
 def valu_entry(kernel):
@@ -198,6 +213,7 @@ def bench_replayable(args, torch, D, ctx, L, stream):
                                                 ctypes.byref(plan)))
         plans.append(plan)
     plan_ms = (time.time() - t0) * 1e3 / NP
+    k1 = k1_kernel(L, plans[0])
     dev = torch.device("cuda", D.local_rank)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(NP - 1)]
     d_soff = [torch.from_numpy(so.view(np.int32)).to(dev) for so, _ in csr]
@@ -304,7 +320,7 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     return dict(S=S, E=E, hints=(hoff, hb), seeds=csr[0], elapsed=el_max,
                 kern_ms=kern_ms_span if kern_ms_span is not None else kern_ms_timed, kern_ms_events=kern_ms_timed,
                 kern_ms_span=kern_ms_span, kern_ms_isolated=kern_ms, plan_ms=plan_ms, stats=stats, topk=merged, pipeline=NP,
-                e2e_s=e2e, e2e_plan_s=e2e_plan)
+                e2e_s=e2e, e2e_plan_s=e2e_plan, k1_kernel=k1)
 
 
 def cpu_baseline_replayable(r, args):
@@ -784,7 +800,7 @@ def headline_line(args, torch, D, ctx, L, stream):
         "config": {"workload": "configs[1] replayable seed sweep", "seeds_per_gpu": r["S"], "events": r["E"],
                    "max_interval_ns": MAX_INTERVAL_NS, "topk": 64, "pipeline_streams": r["pipeline"],
                    "parallelism": f"seed-range x{D.world}" + (" + RCCL all_gather top-k" if D.world > 1 else "")},
-        "roofline": roofline_valu(K1_KERNEL, dec_launch, r["kern_ms"]),
+        "roofline": roofline_valu(r["k1_kernel"], dec_launch, r["kern_ms"]),
         # a new trace's plan (tables + segment sorts + allocations), median over the end-to-end traces;
         # plan_ms_first_three includes the process's first launches (module load) when the bench starts
         "plan_ms": float(np.median(r["e2e_plan_s"])) * 1e3,
@@ -799,16 +815,14 @@ def headline_line(args, torch, D, ctx, L, stream):
     }
     if line["roofline"]:
         rf = line["roofline"]
-        if K1_KERNEL == "k_replayable_sweep_oq":
-            # the kernel derives each seed's statistics (sum, max, argmax) from order queries, not one decision
+        if r["k1_kernel"] in K1_ALGORITHM:
+            # the kernel derives each seed's statistics (sum, max, argmax) from searches, not one decision
             # at a time: a unit is a decision whose effect on the statistics is covered, bit-exact vs the oracle
             rf["unit_kind"] = "stats-equivalent decision"
-            # the order-query kernel does not decide event by event: its lane-instructions per decision are the
-            # per-seed searches spread over the 4,096 decisions they settle. The per-decision kernel's own
-            # ceiling (issue peak / its measured lane-instructions per decision) is the rate an ideal
-            # event-by-event sweep could reach on this chip.
-            rf["algorithm"] = ("order-query statistics: per (seed, hint-length class) binary searches over "
-                               "C-mod-m-sorted blocks (DESIGN.md section 4); units = seed x event decisions covered")
+            # its lane-instructions per decision are the per-seed searches spread over the 4,096 decisions they
+            # settle. The per-decision kernel's own ceiling (issue peak / its measured lane-instructions per
+            # decision) is the rate an ideal event-by-event sweep could reach on this chip.
+            rf["algorithm"] = K1_ALGORITHM[r["k1_kernel"]]
             pd = valu_entry("k_replayable_sweep_fast")
             if pd and isa_state(pd)[0]:
                 ceil = PEAK_VALU_TOPS * 1e12 / pd["ops_per_unit"]

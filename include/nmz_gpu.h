@@ -182,6 +182,11 @@ int nmz_replayable_plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uin
                                uint32_t n_events, int64_t max_interval_ns,
                                uint64_t max_seeds, nmz_replayable_plan **out);
 int nmz_replayable_plan_destroy(nmz_replayable_plan *plan);
+/* Which statistics kernel the plan's sweeps take (diagnostic): 2 = wavelet-tree statistics (k_replayable_sweep_wt,
+ * the default when 0 < max_interval < 2^32, every hint-length class has <= 4,096 events and the row image fits LDS),
+ * 1 = order-query statistics (k_replayable_sweep_oq), 0 = per-decision sweeps; -1 for a NULL plan. The environment
+ * variable NMZ_REPLAY_WT=0 at plan creation skips the wavelet trees (A/B runs). */
+int nmz_replayable_plan_kernel(const nmz_replayable_plan *plan);
 int nmz_replayable_sweep_dev(nmz_replayable_plan *plan, const uint32_t *d_seed_off,
                              const uint8_t *d_seed_bytes, uint64_t n_seeds,
                              nmz_sched_stats *d_stats, void *stream);
@@ -279,6 +284,11 @@ int nmz_ed_allpairs_knn_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys,
  * so the merged lists take (band + 1, id) for the smallest ids not listed (not the trace
  * itself), in increasing id, up to k. On other plans the fill leaves complete lists
  * unchanged. (nmz_ed_allpairs_knn[_dev] fill by themselves.) */
+/* Host-only (no device work): the shard that owns query block qb (queries 64 qb .. 64 qb + 63) of the two-phase
+ * bit-parallel search under nmz_ed_allpairs_knn_shard_dev with n_shards shards: every pair (i, j), i < j, belongs
+ * to the shard of block i / 64 (MurmurHash3's 64-bit finaliser of qb, mod n_shards). tests/test_dist_cpu.py deals
+ * pairs by it. */
+uint32_t nmz_ed_block_shard(uint32_t qb, uint32_t n_shards);
 int nmz_ed_allpairs_knn_shard_dev(nmz_ed_plan *plan, uint32_t k, uint32_t shard, uint32_t n_shards,
                                   uint64_t *d_knn_keys, void *stream);
 int nmz_knn_merge_dev(nmz_ctx *ctx, const uint64_t *d_parts, uint32_t n_parts, uint32_t n_traces,

@@ -69,6 +69,7 @@ SIGNATURES = {
     "nmz_replayable_sweep": (_int, [_P, _P, _P, _u64, _P, _P, _u32, _i64, _P, _P, _u64, _u32, _P]),
     "nmz_replayable_plan_create": (_int, [_P, _P, _P, _u32, _i64, _u64, ctypes.POINTER(_P)]),
     "nmz_replayable_plan_destroy": (_int, [_P]),
+    "nmz_replayable_plan_kernel": (_int, [_P]),
     "nmz_replayable_sweep_dev": (_int, [_P, _P, _P, _u64, _P, _P]),
     "nmz_replayable_sweep_topk_dev": (_int, [_P, _P, _P, _u64, _u64, _u32, _P, _P, _P]),
     "nmz_replayable_decide": (_int, [_P, _P, _u32, _P, _P, _u32, _i64, _P]),
@@ -82,6 +83,7 @@ SIGNATURES = {
     "nmz_ed_plan_create": (_int, [_P, _P, _P, _u32, _u32, ctypes.POINTER(_P)]),
     "nmz_ed_plan_destroy": (_int, [_P]),
     "nmz_ed_plan_is_fast": (_int, [_P]),
+    "nmz_ed_block_shard": (_u32, [_u32, _u32]),
     "nmz_ed_allpairs_knn_dev": (_int, [_P, _u32, _P, _P]),
     "nmz_ed_allpairs_knn_shard_dev": (_int, [_P, _u32, _u32, _u32, _P, _P]),
     "nmz_knn_merge_dev": (_int, [_P, _P, _u32, _u32, _u32, _P, _P]),

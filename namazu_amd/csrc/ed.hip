@@ -1285,6 +1285,10 @@ int nmz_ed_allpairs_knn_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys,
     return nmz_ed_allpairs_knn_shard_dev(plan, k, 0, 1, d_knn_keys, stream);
 }
 
+uint32_t nmz_ed_block_shard(uint32_t qb, uint32_t n_shards) {
+    return n_shards <= 1 ? 0u : (uint32_t)(tile_mix(qb) % n_shards);
+}
+
 int nmz_ed_allpairs_knn_shard_dev(nmz_ed_plan *plan, uint32_t k, uint32_t shard, uint32_t n_shards,
                                   uint64_t *d_knn_keys, void *stream) {
     NMZ_CHECK(plan != nullptr, "plan is NULL");

@@ -134,4 +134,25 @@ int ed_wide_build_peq(const uint16_t *d_sym, const uint64_t *d_off, uint32_t N, 
                       uint32_t band, uint32_t *d_peq, hipStream_t st);
 int ed_wide_launch(const EdWideArgs &A, uint32_t band, hipStream_t st);
 
+// replayable plan: one hint-length class (a segment of every table row)
+struct ClassInfo {
+    uint64_t pn;     // P^len
+    uint32_t start;  // first position in the length-sorted event order
+    uint32_t count;
+};
+// K1 wavelet-tree statistics (replayable_wt.hip): per-row images built once per plan, staged into LDS per sweep
+struct WtState {
+    bool on = false;
+    uint32_t rb16 = 0, n_classes = 0, msh = 0;
+    uint4 *d_blob = nullptr;                // [256][rb16] row images
+    unsigned long long *d_rowsum = nullptr;  // [256] sum of C mod m over the row
+    void *d_classes = nullptr;              // [n_classes] segment descriptors
+    DevBuf mem;
+};
+bool wt_enabled();
+int wt_build(WtState &w, const uint4 *d_table, uint32_t E, const ClassInfo *cls, uint32_t n_cls,
+             const ModParams &mod, hipStream_t st);
+int wt_sweep(const WtState &w, nmz_ctx *ctx, hipStream_t st, const Buckets &b, const uint4 *d_table, uint32_t E,
+             const ModParams &mod, nmz_sched_stats *d_stats);
+
 }  // namespace nmz

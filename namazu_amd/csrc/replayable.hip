@@ -32,12 +32,6 @@
 
 namespace nmz {
 
-struct ClassInfo {
-    uint64_t pn;     // P^len
-    uint32_t start;  // first position in the length-sorted event order
-    uint32_t count;
-};
-
 struct OqClass;
 
 }  // namespace nmz
@@ -71,6 +65,7 @@ struct nmz_replayable_plan {
     uint64_t *d_oq_rowsum = nullptr;    // [passes][256] sum of C mod m over the pass's part of the row
     nmz::OqClass *d_oq_classes = nullptr;
     nmz::DevBuf oq_mem;
+    nmz::WtState wt;                    // wavelet-tree statistics (k_replayable_sweep_wt, the default when it fits)
 };
 
 namespace nmz {
@@ -1472,6 +1467,10 @@ static int replayable_stats(nmz_replayable_plan *p, hipStream_t st, const uint32
     const int U = replay_u();
     const uint32_t per_unit = 64u * (uint32_t)U;
     const uint64_t max_units = S / per_unit + 256;
+    if (p->wt.on && (replay_oq_enabled() || p->mod.kind != MOD_FAST)) {
+        NMZ_TRY(bucket_seeds_counted(st, sc.h0, S, OQ_WG, sc.b, sc.counter));
+        return wt_sweep(p->wt, p->ctx, st, sc.b, p->d_table, E, p->mod, d_stats);
+    }
     if (p->oq && (replay_oq_enabled() || p->mod.kind != MOD_FAST)) {
         NMZ_TRY(bucket_seeds_counted(st, sc.h0, S, OQ_WG, sc.b, sc.counter));
         KernelTimer kt(p->ctx, st, "replayable_sweep");
@@ -1555,7 +1554,8 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
     *out = nullptr;
     auto *p = new nmz_replayable_plan();
     p->ctx = ctx;
-    for (DevBuf *b : {&p->seed_scratch, &p->partial, &p->topk_lists, &p->plan_mem, &p->oq_mem}) b->pool = &ctx->pool;
+    for (DevBuf *b : {&p->seed_scratch, &p->partial, &p->topk_lists, &p->plan_mem, &p->oq_mem, &p->wt.mem})
+        b->pool = &ctx->pool;
     p->n_events = E;
     p->max_interval = max_interval;
     p->mod = make_mod((uint64_t)max_interval);  // uint64(r.MaxInterval), replayablepolicy.go:110
@@ -1612,6 +1612,7 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
         p->partial.release();
         p->topk_lists.release();
         p->oq_mem.release();
+        p->wt.mem.release();
         delete p;
         return code;
     };
@@ -1660,10 +1661,14 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
         }
         if (bad)
             return cleanup(fail(NMZ_EHIP, "plan table kernel failed"));
-        const int orc = oq_build(p, cls, st);
+        // wavelet-tree images (the default sweep when they fit), else the order-query images
+        int orc = wt_build(p->wt, p->d_table, E, cls.data(), (uint32_t)cls.size(), p->mod, st);
+        if (orc != NMZ_OK) return cleanup(orc);
+        if (!p->wt.on) orc = oq_build(p, cls, st);
         if (orc != NMZ_OK) return cleanup(orc);
         // the plan is complete before it is returned: sweeps may run on any stream
-        if (!p->oq && hipStreamSynchronize(st) != hipSuccess) return cleanup(fail(NMZ_EHIP, "plan build failed"));
+        if (!p->oq && !p->wt.on && hipStreamSynchronize(st) != hipSuccess)
+            return cleanup(fail(NMZ_EHIP, "plan build failed"));
     }
     *out = p;
     return NMZ_OK;
@@ -1701,9 +1706,15 @@ int nmz_replayable_plan_destroy(nmz_replayable_plan *plan) {
         plan->partial.release();
         plan->topk_lists.release();
         plan->oq_mem.release();
+        plan->wt.mem.release();
     }
     delete plan;
     return NMZ_OK;
+}
+
+int nmz_replayable_plan_kernel(const nmz_replayable_plan *plan) {
+    if (!plan) return -1;
+    return plan->wt.on ? 2 : plan->oq ? 1 : 0;
 }
 
 int nmz_replayable_sweep_dev(nmz_replayable_plan *plan, const uint32_t *d_seed_off, const uint8_t *d_seed_bytes,
@@ -1757,6 +1768,7 @@ int nmz_replayable_sweep(nmz_ctx *ctx, const uint32_t *seed_off, const uint8_t *
             p->partial.release();
             p->topk_lists.release();
             p->oq_mem.release();
+        p->wt.mem.release();
             delete p;
         }
     } pg{plan};

@@ -26,6 +26,28 @@ def shard_range(total, world, rank):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+_M64 = (1 << 64) - 1
+
+
+def ed_block_shard(qb, world):
+    """Shard owning query block qb (queries 64 qb .. 64 qb + 63) of the two-phase all-pairs search
+    (nmz_ed_allpairs_knn_shard_dev; csrc/ed.hip tile_mix): MurmurHash3's 64-bit finaliser of qb mod world. Whole
+    query blocks, so a query pair's DP entries stay in one shard; the hash breaks the clustered workloads' period."""
+    if world <= 1:
+        return 0
+    x = qb
+    x ^= x >> 33
+    x = (x * 0xFF51AFD7ED558CCD) & _M64
+    x ^= x >> 33
+    x = (x * 0xC4CEB9FE1A85EC53) & _M64
+    return (x ^ (x >> 33)) % world
+
+
+def ed_pair_shard(i, j, world):
+    """Shard owning the pair (i, j): the block of the smaller index (the filter runs every j > q of query q)."""
+    return ed_block_shard(min(i, j) // 64, world)
+
+
 def merge_topk(entries, k):
     """Deterministic merge of top-k candidate arrays (TOPK_DTYPE)."""
     a = np.concatenate([np.frombuffer(np.ascontiguousarray(e).tobytes(), TOPK_DTYPE) for e in entries])

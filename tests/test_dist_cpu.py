@@ -1,8 +1,9 @@
 """CPU (gloo, world_size 2): the N>1 host logic -- seed-range sharding (dist.shard_range), all_gather of per-rank
 top-k and k-NN partial lists (dist.gather_topk, dist.all_gather_bytes), deterministic merges (dist.merge_topk,
-dist.merge_knn_keys) -- checked against the single-process oracle result. There is no device here, so each rank's
-share is computed by the oracle; the same path with every rank on the device (the product's shard functions and
-the device merge) runs in tests/test_dist_gpu.py."""
+dist.merge_knn_keys) -- checked against the single-process oracle result. The shares are dealt by the product's
+own rules (dist.shard_range for seeds; dist.ed_pair_shard, checked against the library's nmz_ed_block_shard, for
+trace pairs); there is no device here, so each rank's share of the work is computed by the oracle. The same path
+with every rank on the device (the product's shard functions and the device merge) runs in tests/test_dist_gpu.py."""
 import os
 import socket
 
@@ -12,6 +13,9 @@ import torch.multiprocessing as mp
 
 from namazu_amd import dist as nd
 from oracle import oracle as O
+
+
+ED_N = 300  # five query blocks of 64
 
 
 def _free_port():
@@ -39,13 +43,15 @@ def _worker(rank, world, port, q):
         local = O.topk_from_stats(st, 1000 + lo, K)
         merged = nd.gather_topk(dist, local, K)
         # k-NN partial lists: each rank computes a disjoint subset of pairs
-        N, k, w = 24, 5, 4
+        N, k, w = ED_N, 5, 4
         trs = [rng.integers(0, 3, rng.integers(3, 10)).astype(np.uint64) for _ in range(N)]
         off = np.zeros(N + 1, np.uint64)
         off[1:] = np.cumsum([len(t) for t in trs])
         sym = np.concatenate(trs)
-        pairs = np.array([[i, j] for i in range(N) for j in range(i + 1, N)], np.uint32)
-        mine = pairs[rank::world]
+        # the two-phase search's dealing: pair (i, j), i < j, belongs to the shard of query block i // 64
+        pairs = np.array([[i, j] for i in range(N) for j in range(i + 1, N) if nd.ed_pair_shard(i, j, world) == rank],
+                         np.uint32).reshape(-1, 2)
+        mine = pairs
         d = O.ed_pairs(off, sym, mine, w)
         keys = np.full((N, k), np.iinfo(np.uint64).max, np.uint64)
         # as a bit-parallel shard lists them: in-band results only; the merge is completed by fill_knn_keys
@@ -60,7 +66,7 @@ def _worker(rank, world, port, q):
         parts = nd.all_gather_bytes(dist, t)
         merged_knn = nd.fill_knn_keys(nd.merge_knn_keys([pp.numpy().view(np.uint64).reshape(N, k) for pp in parts], k),
                                       N, w + 1)
-        q.put((rank, merged.tobytes(), merged_knn.tobytes()))
+        q.put((rank, merged.tobytes(), merged_knn.tobytes(), len(mine)))
     finally:
         dist.destroy_process_group()
 
@@ -84,12 +90,13 @@ def test_gloo_sharded_topk_and_knn(world):
     ec = rng.integers(0, 4, size=E, dtype=np.uint8)
     st, _, _ = O.random_sweep(1000, S, eh, ec, O.random_params(30_000_000, 100_000_000, 0.3))
     exp = O.topk_from_stats(st, 1000, K)
-    N, k, w = 24, 5, 4
+    N, k, w = ED_N, 5, 4
     trs = [rng.integers(0, 3, rng.integers(3, 10)).astype(np.uint64) for _ in range(N)]
     off = np.zeros(N + 1, np.uint64)
     off[1:] = np.cumsum([len(t) for t in trs])
     oi, od = O.ed_allpairs_knn(off, np.concatenate(trs), w, k)
-    for rank, tk, kn in res:
+    assert sum(r[3] for r in res) == N * (N - 1) // 2 and min(r[3] for r in res) > 0  # a partition, both busy
+    for rank, tk, kn, _ in res:
         assert np.frombuffer(tk, O.TOPK_DTYPE).tolist() == exp.tolist()
         keys = np.frombuffer(kn, np.uint64).reshape(N, k)
         ids = (keys & np.uint64(0xFFFFFFFF)).astype(np.uint32)
@@ -118,3 +125,14 @@ def test_merge_topk_is_order_independent():
     m2 = nd.merge_topk([a[3:], a[:3]], 4)
     assert m1.tolist() == m2.tolist()
     assert m1["seed"].tolist() == [1, 9, 5, 7]
+
+
+def test_ed_pair_dealing_matches_library():
+    """dist.ed_block_shard restates the library's dealing rule (csrc/ed.hip tile_mix; host-only entry point)."""
+    from namazu_amd import _lib
+    L = _lib.load()
+    for world in [1, 2, 3, 8]:
+        for qb in list(range(300)) + [2**20 + 7, 2**31 - 1]:
+            assert L.nmz_ed_block_shard(qb, world) == nd.ed_block_shard(qb, world)
+    # every block has an owner in range, and 8 shards all get blocks
+    assert sorted({nd.ed_block_shard(qb, 8) for qb in range(1563)}) == list(range(8))

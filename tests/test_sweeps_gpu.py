@@ -26,6 +26,42 @@ def rep_oracle(seeds, hints, m, n_dump=0):
 
 
 # ---------------------------------------------------------------- K1
+@pytest.fixture(params=["wt", "oq"])
+def k1(request, monkeypatch):
+    """K1's two statistics kernels: wavelet trees (the default) and order queries (NMZ_REPLAY_WT=0 at plan
+    creation); plans that neither fits take the per-decision sweep either way."""
+    if request.param == "oq":
+        monkeypatch.setenv("NMZ_REPLAY_WT", "0")
+    else:
+        monkeypatch.delenv("NMZ_REPLAY_WT", raising=False)
+    return request.param
+
+
+def test_replayable_plan_kernel_choice(ctx, monkeypatch):
+    """configs[1]-shaped traces take the wavelet-tree kernel; NMZ_REPLAY_WT=0 the order-query kernel; classes
+    beyond 4,096 events the order-query kernel; maxInterval >= 2^32 the per-decision sweep."""
+    L = _lib.load()
+
+    def kind(hints, m):
+        ho, hb = to_csr(hints)
+        plan = ctypes.c_void_p()
+        _lib.check(L.nmz_replayable_plan_create(ctx.handle, _lib.ptr(ho), _lib.ptr(hb), len(hints), m, 1024,
+                                                ctypes.byref(plan)))
+        try:
+            return L.nmz_replayable_plan_kernel(plan)
+        finally:
+            L.nmz_replayable_plan_destroy(plan)
+
+    monkeypatch.delenv("NMZ_REPLAY_WT", raising=False)
+    hints = zk_hints(4096)
+    assert kind(hints, 100_000_000) == 2
+    assert kind(hints, 2**32 - 1) == 2
+    assert kind(hints, 2**32) == 0
+    assert kind(["x" * 5] * 4097, 100_000_000) == 1
+    monkeypatch.setenv("NMZ_REPLAY_WT", "0")
+    assert kind(hints, 100_000_000) == 1
+
+
 def test_replayable_golden_foobar(ctx, golden):
     for case in golden("replayable_foobar.json")["cases"]:
         p = Replayable()
@@ -39,7 +75,7 @@ def test_replayable_golden_foobar(ctx, golden):
 @pytest.mark.parametrize("m", [100_000_000, 1_000_000_000, 10_000_000, 1, 2, 999, 2**30 - 1, 2**30, 2**30 + 5,
                                2_000_000_000, 2**31 - 1, 2**31, 3_000_000_000, 2**32 - 1, 2**32,
                                2**62 + 11, 2**63 - 1, -5_000_000, -1, 0])
-def test_replayable_moduli(ctx, m):
+def test_replayable_moduli(ctx, k1, m):
     seeds = [str(i) for i in range(700)] + ["", "foobar", "x" * 50]
     hints = zk_hints(97) + ["", "a", "hint-entity-0-0", "z" * 33]
     p = Replayable()
@@ -51,7 +87,7 @@ def test_replayable_moduli(ctx, m):
     assert np.array_equal(r.topk, O.topk_from_stats(st, 0, 10))
 
 
-def test_replayable_many_length_classes_and_ties(ctx):
+def test_replayable_many_length_classes_and_ties(ctx, k1):
     """Hints of every length 0..40 (41 classes) and a tiny modulus (many ties):
     argmax must be the first original event index."""
     hints = ["h" * (i % 41) + str(i % 3) * (i % 2) for i in range(300)]
@@ -65,7 +101,7 @@ def test_replayable_many_length_classes_and_ties(ctx):
 
 
 @pytest.mark.parametrize("m", [1, 2, 3, 7, 1000, 100_000_000, 2**30 - 1, 2**31 + 3, 2**32 - 1])
-def test_replayable_order_query_block_edges(ctx, m):
+def test_replayable_order_query_block_edges(ctx, k1, m):
     """K1's order-query statistics (k_replayable_sweep_oq): length classes whose sizes sit on both sides of the
     8-, 64- and 512-event block edges and of the per-event threshold (24), shuffled so the original event order
     mixes the classes; tiny moduli make most maxima ties, which must resolve to the first original event."""
@@ -83,7 +119,7 @@ def test_replayable_order_query_block_edges(ctx, m):
     assert np.array_equal(r.stats, st) and np.array_equal(r.delays, dl)
 
 
-def test_replayable_repeated_hints_plan_sort_fallback(ctx):
+def test_replayable_repeated_hints_plan_sort_fallback(ctx, k1):
     """Many identical hints give identical C values in every table row, so one top-12-bit bucket of the plan's
     segment sort overflows and the segment takes the bitonic sort; ties in C must keep the event order."""
     rng = np.random.default_rng(7)
@@ -100,7 +136,7 @@ def test_replayable_repeated_hints_plan_sort_fallback(ctx):
 
 
 @pytest.mark.parametrize("E", [1, 3, 63, 64, 65, 127, 2047, 2048, 2049, 4097, 9000])
-def test_replayable_event_counts_around_stage_and_chunk_edges(ctx, E):
+def test_replayable_event_counts_around_stage_and_chunk_edges(ctx, k1, E):
     """K1 stages 64 events at a time (the next chunk's load is clamped to the last event) and works in
     2,048-event items: trace lengths on either side of both edges, vs the oracle."""
     rng = np.random.default_rng(E)
@@ -114,7 +150,7 @@ def test_replayable_event_counts_around_stage_and_chunk_edges(ctx, E):
 
 
 @pytest.mark.parametrize("E,m", [(10_000, 100_000_000), (10_000, 2_000_000_000), (6_500, 2**32 - 1)])
-def test_replayable_long_trace_multi_pass(ctx, E, m):
+def test_replayable_long_trace_multi_pass(ctx, k1, E, m):
     """Traces whose order-query row image exceeds LDS (E > ~6k): length classes split into C-sorted sub-segments
     packed into passes, one kernel run per pass, statistics combined per seed (sum adds, max keys max), incl.
     maxInterval 2 s and 2^32 - 1 ns (m >= 2^31: 32-bit residue sums that overflow), vs the oracle."""
@@ -134,6 +170,7 @@ def test_replayable_forced_passes(ctx, monkeypatch, budget, m):
     """NMZ_REPLAY_OQ_BUDGET shrinks the row-image budget so a 3,000-event trace runs as many passes over small
     sub-segments (and the rows' partial chunks accumulate across passes); results equal the oracle's."""
     monkeypatch.setenv("NMZ_REPLAY_OQ_BUDGET", str(budget))
+    monkeypatch.setenv("NMZ_REPLAY_WT", "0")  # the order-query kernel's passes
     rng = np.random.default_rng(budget)
     hints = zk_hints(3000, rng) + ["x" * (i % 5) for i in range(30)]
     seeds = [str(i) for i in range(1500)]
@@ -165,7 +202,7 @@ def _seeds_in_one_row(row, n):
 
 
 @pytest.mark.parametrize("n", [1, 37, 64, 960, 1024, 1064, 1088, 2100])
-def test_replayable_one_row_chunks_and_partial_chunk(ctx, n):
+def test_replayable_one_row_chunks_and_partial_chunk(ctx, k1, n):
     """K1 takes a row's seeds in 64-seed chunks from an LDS counter and shares the row's partial chunk (n mod 64
     seeds) between its waves by class segment: all seeds in one row, counts on both sides of whole chunks and of
     one chunk per wave (1,024), with 20 length classes (some per-event, some order-query) so a wave takes

@@ -1,0 +1,170 @@
+"""Host simulation of K1's wavelet-tree statistics (namazu_amd/csrc/replayable_wt.hip), step for step, against
+per-event decisions. A design check for the plan layout and the descents -- not the product, not the oracle.
+
+usage: python tools/wt_sim.py [trials]
+"""
+import random
+import sys
+
+
+def bitlen(x):
+    return x.bit_length()
+
+
+def build(cm, e, chi):
+    """cm, e, chi per position (C order). Returns the image as Python lists."""
+    n = len(cm)
+    keys = sorted(((cm[i] << 32) | ((0xFFFF - e[i]) << 16) | i) for i in range(n))
+    cm_r = [k >> 32 for k in keys] + [0xFFFFFFFF]
+    e_r = [0xFFFF - ((k >> 16) & 0xFFFF) for k in keys]
+    S = [0] * n
+    for j, k in enumerate(keys):
+        S[k & 0xFFFF] = j
+    K = bitlen(n)
+    nw = n // 32 + 1
+    lv = []
+    cur = S
+    for l in range(K):
+        k = K - l
+        h = 1 << (k - 1)
+        wb = [0] * nw
+        for j in range(n):
+            if cur[j] & h:
+                wb[j >> 5] |= 1 << (j & 31)
+        cum = [0] * nw
+        acc = 0
+        for w in range(nw):
+            cum[w] = acc
+            acc += bin(wb[w]).count("1")
+        lv.append([(wb[w], cum[w]) for w in range(nw)])
+        nxt = [None] * n
+        for j in range(n):
+            v = cur[j]
+            s0 = v & ~(2 * h - 1)
+            r1 = cum[j >> 5] + bin(wb[j >> 5] & ((1 << (j & 31)) - 1)).count("1") - (s0 >> 1)
+            nxt[(s0 + h + r1) if (v & h) else (j - r1)] = v
+        assert None not in nxt
+        cur = nxt
+    assert cur == list(range(n))
+    return dict(n=n, K=K, nw=nw, lv=lv, cm=cm_r, e=e_r, chi=list(chi) + [0xFFFFFFFF])
+
+
+def ones(lvl, s, p):
+    w = lvl[p >> 5]
+    return w[1] + bin(w[0] & ((1 << (p & 31)) - 1)).count("1") - (s >> 1)
+
+
+def query(img, d, RA, RB, Hm, Hm2, m):
+    """returns (W, keyA or None, keyB or None) following wt_seed_class after the searches."""
+    n, K, lv, cm, ev = img["n"], img["K"], img["lv"], img["cm"], img["e"]
+    NONE = None
+    oA = oB = d
+    cA = cB = 0
+    lA = sA = qA = lB = sB = qB = None
+    lA = lB = NONE
+    sA = qA = sB = qB = 0
+    for l in range(K):
+        h = 1 << (K - l - 1)
+        msk = ~(2 * h - 1)
+        lvl = lv[l]
+        s = RA & msk
+        o = ones(lvl, s, s + oA)
+        z = oA - o
+        if RA & h:
+            if z:
+                lA, sA, qA = l + 1, s, z
+            oA = o
+        else:
+            cA += o
+            oA = z
+        s = RB & msk
+        o = ones(lvl, s, s + oB)
+        z = oB - o
+        if RB & h:
+            if min(n - s, h) > z:
+                lB, sB, qB = l + 1, s, z
+            oB = o
+        else:
+            cB += o
+            oB = z
+    cA += oA
+    cB += oB
+    W = cA + (n - RB) - cB
+    hasA, hasB = d > 0, d < n
+    wrapA, wrapB = lA is NONE, lB is NONE
+    if wrapA:
+        lA, sA, qA = 0, 0, d
+    if wrapB:
+        lB, sB, qB = 0, 0, d
+    if not hasA:
+        lA = K
+    if not hasB:
+        lB = K
+    for l in range(min(lA, lB), K):
+        h = 1 << (K - l - 1)
+        lvl = lv[l]
+        if l >= lA:
+            o = ones(lvl, sA, sA + qA)
+            if o:
+                sA += h
+                qA = o
+        if l >= lB:
+            o = ones(lvl, sB, sB + qB)
+            size = min(n - sB, 2 * h)
+            if size > h + o:
+                sB += h
+                qB = o
+            else:
+                qB -= o
+    kA = kB = None
+    if hasA:
+        t = (Hm + cm[sA] - (m if wrapA else 0)) % (1 << 32)
+        kA = (t << 32) | (0xFFFFFFFF - ev[sA])
+    if hasB:
+        t = (Hm2 + cm[sB] - (m if wrapB else 0)) % (1 << 32)
+        kB = (t << 32) | (0xFFFFFFFF - ev[sB])
+    return W, kA, kB
+
+
+def brute(cm, e, d, Hm, Hm2, m):
+    W = 0
+    best = None
+    for i in range(len(cm)):
+        b = Hm if i < d else Hm2
+        s = b + cm[i]
+        wrap = s >= m
+        t = s - m if wrap else s
+        W += wrap
+        k = (t << 32) | (0xFFFFFFFF - e[i])
+        best = k if best is None or k > best else best
+    return W, best
+
+
+def main():
+    trials = int(sys.argv[1]) if len(sys.argv) > 1 else 300
+    rng = random.Random(7)
+    for t in range(trials):
+        n = rng.choice([9, 10, 31, 32, 33, 63, 64, 65, 100, 127, 128, 129, 200, 255, 256, 257, 511, 512, 700])
+        m = rng.choice([1, 2, 3, 7, 100, 1000, 10 ** 8, (1 << 30) - 1, (1 << 31) + 5, (1 << 32) - 1])
+        dup = rng.random() < 0.3
+        vals = [rng.randrange(m) for _ in range(max(1, n // 8 if dup else n))]
+        cm = [rng.choice(vals) for _ in range(n)]
+        e = rng.sample(range(4096), n)
+        img = build(cm, e, [0] * n)
+        for _ in range(30):
+            d = rng.choice([0, n, rng.randrange(n + 1)])
+            Hm = rng.randrange(m)
+            Hm2 = rng.randrange(m)
+            XA, XB = m - Hm, m - Hm2
+            RA = sum(1 for x in cm if x < XA)
+            RB = sum(1 for x in cm if x < XB)
+            W, kA, kB = query(img, d, RA, RB, Hm, Hm2, m)
+            bW, bk = brute(cm, e, d, Hm, Hm2, m)
+            k = max(x for x in (kA, kB) if x is not None)
+            assert W == bW, (n, m, d, W, bW)
+            assert k == bk, (n, m, d, hex(k), hex(bk))
+    print("ok", trials)
+
+
+if __name__ == "__main__":
+    main()
