@@ -94,7 +94,9 @@ def roofline_valu(kernel, units, kernel_ms):
     fingerprint differs (or the entry has none) the roofline is marked stale and carries no frac."""
     e = valu_entry(kernel)
     if e is None:
-        return None
+        return {"bound": "valu", "kernel": kernel, "kernel_ms": kernel_ms, "stale": True, "achieved": None,
+                "frac": None, "peak": PEAK_VALU_TOPS, "unit": "Tops/s", "traffic": None,
+                "why": "no profiles/valu_per_unit.json entry for this kernel yet"}
     fresh, isa = isa_state(e)
     achieved = e["ops_per_unit"] * units / (kernel_ms * 1e-3) / 1e12
     traffic = e.get("hbm_bytes_per_launch")

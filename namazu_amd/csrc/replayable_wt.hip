@@ -41,8 +41,10 @@ struct WtClass {
     uint32_t o_chi, o_e;      //   Cm by rank (+ sentinel); C's high word by position (+ sentinel); e by rank (u16)
     uint32_t o_im, o_ic;      //   bucket indexes (u16): first rank with Cm >= b << msh (257); first position
                               //   with C_hi >= b << 24 (256)
+    uint32_t o_pm;            //   per d in [0, n]: {largest rank at positions < d, largest rank at positions >= d}
+                              //   (u16 pairs: the maximum of a part none of whose Cm is below its bound)
     uint32_t K, nw;           // levels (2^K > n); words per level (n / 32 + 1)
-    uint32_t rM, rC;          // lifting-search rounds (largest bucket's bit length; set by the plan kernel)
+    uint32_t rS;              // lifting-search rounds (the largest bucket's bit length; set by the plan kernel)
 };
 static_assert(sizeof(WtClass) == 56, "WtClass layout");
 
@@ -151,10 +153,36 @@ __global__ __launch_bounds__(1024) void k_replayable_wt_build(const uint4 *__res
         atomicMax(bmax + 1, b - a);
     }
     __syncthreads();
-    if (tid == 0) {
-        atomicMax(&classes[c].rM, 32u - __clz(bmax[0]));
-        atomicMax(&classes[c].rC, 32u - __clz(bmax[1]));
+    if (tid == 0) atomicMax(&classes[c].rS, 32u - __clz(max(bmax[0], bmax[1])));
+    // prefix / suffix maxima of the ranks (wave 0 / wave 1, 64 positions or fewer per lane)
+    if (wave < 2) {
+        uint16_t *pm = reinterpret_cast<uint16_t *>(img + ci.o_pm);
+        const uint32_t cs = (n + 63) / 64, j0 = min(lane * cs, n), j1 = min(j0 + cs, n);
+        uint32_t mx = 0;
+        for (uint32_t j = j0; j < j1; ++j) mx = max(mx, (uint32_t)S0[j]);
+        uint32_t ex = 0;  // prefix: maximum of the lanes before; suffix: of the lanes after
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = wave == 0 ? __shfl_up(mx, o, 64) : __shfl_down(mx, o, 64);
+            const bool in = wave == 0 ? lane >= (uint32_t)o : lane + o < 64;
+            mx = in ? max(mx, v) : mx;
+            ex = in ? max(ex, v) : ex;
+        }
+        if (wave == 0) {
+            uint32_t run = ex;
+            for (uint32_t j = j0; j < j1; ++j) {
+                pm[2 * j] = (uint16_t)run;
+                run = max(run, (uint32_t)S0[j]);
+            }
+            if (j1 == n && j0 < j1) pm[2 * n] = (uint16_t)run;
+        } else {
+            uint32_t run = ex;
+            for (uint32_t j = j1; j > j0; --j) {
+                run = max(run, (uint32_t)S0[j - 1]);
+                pm[2 * (j - 1) + 1] = (uint16_t)run;
+            }
+        }
     }
+    __syncthreads();
     // wavelet levels
     const uint32_t K = ci.K, nw = ci.nw;
     uint2 *lv = reinterpret_cast<uint2 *>(img + ci.o_lv);
@@ -252,20 +280,17 @@ __device__ __forceinline__ void wt_seed_class(const WtClass &ci, const char *__r
     const uint16_t *__restrict__ ev = reinterpret_cast<const uint16_t *>(img + ci.o_e);
     const uint16_t *__restrict__ im = reinterpret_cast<const uint16_t *>(img + ci.o_im);
     const uint16_t *__restrict__ ic = reinterpret_cast<const uint16_t *>(img + ci.o_ic);
+    const uint32_t *__restrict__ pm = reinterpret_cast<const uint32_t *>(img + ci.o_pm);
     const uint32_t nh = (uint32_t)(nH >> 32);
     const uint32_t XA = m - Hm, XB = m - Hm2;  // t wraps <=> Cm >= X
-    // lifting searches from the bucket starts: every entry past the bucket is >= the bound, and the sentinel at n
-    // ends every probe past the array
+    // three lifting searches stepped together (every read of a round in flight at once) from the bucket starts:
+    // every entry past the bucket is >= the bound, and the sentinel at n ends every probe past the array
     uint32_t pd = ic[nh >> 24], RA = im[XA >> msh], RB = im[XB >> msh];
-    {
-        const uint32_t rC = ci.rC, rM = ci.rM;
-        for (uint32_t st = (1u << max(rC, rM)) >> 1; st; st >>= 1) {
-            if (st < (1u << rC)) pd += chi[min(pd + st - 1, n)] < nh ? st : 0u;
-            if (st < (1u << rM)) {
-                RA += cm[min(RA + st - 1, n)] < XA ? st : 0u;
-                RB += cm[min(RB + st - 1, n)] < XB ? st : 0u;
-            }
-        }
+    for (uint32_t st = (1u << ci.rS) >> 1; st; st >>= 1) {
+        const uint32_t a = chi[min(pd + st - 1, n)], b = cm[min(RA + st - 1, n)], c = cm[min(RB + st - 1, n)];
+        pd += a < nh ? st : 0u;
+        RA += b < XA ? st : 0u;
+        RB += c < XB ? st : 0u;
     }
     // d = #{C <= ~H}: #{C_hi < ~H_hi} plus the entries whose high word equals ~H_hi and low word is <= ~H_lo
     // (about n / 2^32 of the queries: the low words come from the table row)
@@ -274,8 +299,10 @@ __device__ __forceinline__ void wt_seed_class(const WtClass &ci, const char *__r
         const uint32_t nl = (uint32_t)nH;
         while (d < n && chi[d] == nh && row[ci.start + d].x <= nl) ++d;
     }
-    // descents along R_A's and R_B's paths with the prefix [0, d): counts of ranks >= R, and the deepest level
-    // where a part's elements below R branch off (the predecessor's subtree)
+    const uint32_t pmd = pm[d];  // the parts' largest ranks (used when a part has nothing below its bound)
+    // descents along R_A's and R_B's paths with the prefix [0, d), branch-free with both reads of a level in
+    // flight: counts of ranks >= R, and the deepest level where a part's elements below R branch off (the
+    // predecessor's subtree: node start s, prefix offset q)
     const uint2 *__restrict__ lv = reinterpret_cast<const uint2 *>(img + ci.o_lv);
     const uint32_t K = ci.K, nw = ci.nw;
     uint32_t oA = d, oB = d, cA = 0, cB = 0;
@@ -283,78 +310,52 @@ __device__ __forceinline__ void wt_seed_class(const WtClass &ci, const char *__r
     for (uint32_t l = 0; l < K; ++l) {
         const uint32_t h = 1u << (K - l - 1), msk = ~(2 * h - 1);
         const uint2 *__restrict__ lvl = lv + l * nw;
-        {
-            const uint32_t s = RA & msk;
-            const uint32_t ones = wt_ones(lvl, s, s + oA);
-            const uint32_t z = oA - ones;
-            if (RA & h) {
-                if (z) {
-                    lA = l + 1;
-                    sA = s;
-                    qA = z;
-                }
-                oA = ones;
-            } else {
-                cA += ones;
-                oA = z;
-            }
-        }
-        {
-            const uint32_t s = RB & msk;
-            const uint32_t ones = wt_ones(lvl, s, s + oB);
-            const uint32_t z = oB - ones;
-            if (RB & h) {
-                if (min(n - s, h) > z) {  // zeros of the node past the prefix: the suffix has elements below R_B
-                    lB = l + 1;
-                    sB = s;
-                    qB = z;
-                }
-                oB = ones;
-            } else {
-                cB += ones;
-                oB = z;
-            }
-        }
+        const uint32_t s1 = RA & msk, p1 = s1 + oA, s2 = RB & msk, p2 = s2 + oB;
+        const uint2 w1 = lvl[p1 >> 5], w2 = lvl[p2 >> 5];
+        const uint32_t o1 = w1.y + __popc(__builtin_amdgcn_ubfe(w1.x, 0u, p1)) - (s1 >> 1);
+        const uint32_t o2 = w2.y + __popc(__builtin_amdgcn_ubfe(w2.x, 0u, p2)) - (s2 >> 1);
+        const uint32_t z1 = oA - o1, z2 = oB - o2;
+        const bool b1 = RA & h, b2 = RB & h;
+        const bool u1 = b1 && z1 != 0;
+        const bool u2 = b2 && min(n - s2, h) > z2;  // zeros of the node past the prefix: suffix elements below R_B
+        lA = u1 ? l + 1 : lA;
+        sA = u1 ? s1 : sA;
+        qA = u1 ? z1 : qA;
+        lB = u2 ? l + 1 : lB;
+        sB = u2 ? s2 : sB;
+        qB = u2 ? z2 : qB;
+        cA += b1 ? 0u : o1;
+        cB += b2 ? 0u : o2;
+        oA = b1 ? o1 : z1;
+        oB = b2 ? o2 : z2;
     }
     cA += oA;  // the leaf R itself, if in the prefix
     cB += oB;
     W += cA + (n - RB) - cB;
-    // predecessor descents: the prefix part takes the largest rank among its first qA entries of node sA, the
-    // suffix part the largest among entries qB.. of node sB; a part with nothing below its bound wraps, and its
-    // maximum is its largest rank overall (descent from the root)
+    // predecessor descents: the prefix part takes the largest rank among the first qA entries of node sA, the
+    // suffix part the largest among entries qB.. of node sB. A part with nothing below its bound wraps, and its
+    // maximum is its largest rank overall (pm). Levels no lane of the wave needs are skipped.
     const bool hasA = d > 0, hasB = d < n, wrapA = lA == WT_NONE, wrapB = lB == WT_NONE;
-    if (wrapA) {
-        lA = 0;
-        sA = 0;
-        qA = d;
-    }
-    if (wrapB) {
-        lB = 0;
-        sB = 0;
-        qB = d;
-    }
-    if (!hasA) lA = K;
-    if (!hasB) lB = K;
-    for (uint32_t l = min(lA, lB); l < K; ++l) {
+    if (wrapA || !hasA) lA = K;
+    if (wrapB || !hasB) lB = K;
+    if (wrapA) sA = pmd & 0xffffu;
+    if (wrapB) sB = pmd >> 16;
+    const uint32_t l0 = min(lA, lB);
+    for (uint32_t l = 0; l < K; ++l) {
+        if (!__builtin_amdgcn_ballot_w64(l >= l0)) continue;
         const uint32_t h = 1u << (K - l - 1);
         const uint2 *__restrict__ lvl = lv + l * nw;
-        if (l >= lA) {
-            const uint32_t ones = wt_ones(lvl, sA, sA + qA);
-            if (ones) {
-                sA += h;
-                qA = ones;
-            }
-        }
-        if (l >= lB) {
-            const uint32_t ones = wt_ones(lvl, sB, sB + qB);
-            const uint32_t size = min(n - sB, 2 * h);
-            if (size > h + ones) {  // ones of the node past the prefix
-                sB += h;
-                qB = ones;
-            } else {
-                qB -= ones;
-            }
-        }
+        const uint32_t p1 = sA + qA, p2 = sB + qB;
+        const uint2 w1 = lvl[p1 >> 5], w2 = lvl[p2 >> 5];
+        const uint32_t o1 = w1.y + __popc(__builtin_amdgcn_ubfe(w1.x, 0u, p1)) - (sA >> 1);
+        const uint32_t o2 = w2.y + __popc(__builtin_amdgcn_ubfe(w2.x, 0u, p2)) - (sB >> 1);
+        const bool a1 = l >= lA, a2 = l >= lB;
+        const bool g1 = a1 && o1 != 0;
+        const bool g2 = a2 && min(n - sB, 2 * h) > h + o2;  // ones of the node past the prefix
+        sA += g1 ? h : 0u;
+        qA = g1 ? o1 : qA;
+        sB += g2 ? h : 0u;
+        qB = a2 ? (g2 ? o2 : qB - o2) : qB;
     }
     if (hasA) {
         const uint32_t t = Hm + cm[sA] - (wrapA ? m : 0u);
@@ -500,6 +501,8 @@ int wt_build(WtState &w, const uint4 *d_table, uint32_t E, const ClassInfo *cls,
         off += r16(257 * 2);
         o.o_ic = (uint32_t)off;
         off += r16(256 * 2);
+        o.o_pm = (uint32_t)off;
+        off += r16((uint64_t)(o.n + 1) * 4);
     }
     const uint64_t rb = std::max<uint64_t>(16, r16(off));
     if (rb + 16 > WT_LDS_MAX) return NMZ_OK;
