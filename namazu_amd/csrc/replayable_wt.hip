@@ -56,7 +56,7 @@ static_assert(sizeof(WtClass) == 56, "WtClass layout");
 // per 32 positions. Also adds the segment's sum of Cm to the row sum (every segment, short ones included).
 // ---------------------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void k_replayable_wt_build(const uint4 *__restrict__ table, uint32_t E,
-                                                              WtClass *__restrict__ classes, uint32_t msh,
+                                                              WtClass *__restrict__ classes, uint32_t msh, uint32_t mbits,
                                                               uint4 *__restrict__ blob, uint32_t rb16,
                                                               unsigned long long *__restrict__ rowsum) {
     extern __shared__ uint4 wt_build_lds[];
@@ -66,7 +66,8 @@ __global__ __launch_bounds__(1024) void k_replayable_wt_build(const uint4 *__res
     uint32_t *wb = reinterpret_cast<uint32_t *>(S0 + 2 * WT_NMAX);             // [WT_NMAX / 32 + 1]
     uint32_t *cum = wb + WT_NMAX / 32 + 4;                                     // [WT_NMAX / 32 + 1]
     unsigned long long *part = reinterpret_cast<unsigned long long *>(cum + WT_NMAX / 32 + 4);  // [16]
-    uint32_t *bmax = reinterpret_cast<uint32_t *>(part + 16);                  // [2]
+    uint32_t *bmax = reinterpret_cast<uint32_t *>(part + 16);                  // [4]
+    uint64_t *tmp = reinterpret_cast<uint64_t *>(bmax + 4);                    // [WT_NMAX] sorted keys
     const uint32_t c = blockIdx.x, L = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const WtClass ci = classes[c];
     const uint32_t n = ci.n;
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(1024) void k_replayable_wt_build(const uint4 *__res
     for (uint32_t i = tid; i < n; i += 1024) s += row[i].z;
     for (int o = 32; o; o >>= 1) s += __shfl_xor(s, o, 64);
     if (lane == 0) part[wave] = s;
-    if (tid < 2) bmax[tid] = 0;
+    if (tid < 4) bmax[tid] = 0;
     __syncthreads();
     if (tid == 0) {
         unsigned long long t = 0;
@@ -84,33 +85,93 @@ __global__ __launch_bounds__(1024) void k_replayable_wt_build(const uint4 *__res
         atomicAdd(rowsum + L, t);
     }
     if (n <= WT_BRUTE) return;
-    uint32_t np = 1;
-    while (np < n) np <<= 1;
-    for (uint32_t i = tid; i < np; i += 1024) {
-        if (i < n) {
-            const uint4 q = row[i];
-            chi[i] = q.y;
-            const uint32_t e = ~q.w;  // < 65536 (the host checks E)
-            key[i] = ((uint64_t)q.z << 32) | ((uint64_t)(0xffffu - e) << 16) | i;
-        } else {
-            key[i] = ~0ull;
-        }
+    uint32_t np = 1, lgp = 0;
+    while (np < n) {
+        np <<= 1;
+        ++lgp;
     }
-    for (uint32_t k = 2; k <= np; k <<= 1)
-        for (uint32_t j = k >> 1; j; j >>= 1) {
+    for (uint32_t i = tid; i < n; i += 1024) {
+        const uint4 q = row[i];
+        chi[i] = q.y;
+        const uint32_t e = ~q.w;  // < 65536 (the host checks E)
+        key[i] = ((uint64_t)q.z << 32) | ((uint64_t)(0xffffu - e) << 16) | i;
+    }
+    // sort the keys: counting sort on the top lg(np) bits of Cm (uniform in [0, m): ~1 key per bucket), then an
+    // insertion sort per bucket (a thread per bucket); a bucket of more than 32 keys (repeated hints: equal Cm)
+    // sends the whole segment to a bitonic sort
+    {
+        uint32_t *bc = reinterpret_cast<uint32_t *>(S0);  // [np] bucket counts, then bucket ends
+        const uint32_t sh = mbits > lgp ? mbits - lgp : 0u;
+        for (uint32_t b = tid; b < np; b += 1024) bc[b] = 0;
+        if (tid == 0) bmax[0] = 0;
+        __syncthreads();
+        for (uint32_t i = tid; i < n; i += 1024) atomicAdd(&bc[(uint32_t)(key[i] >> 32) >> sh], 1u);
+        __syncthreads();
+        {  // exclusive scan over np <= 4096 counts: 4 per thread, wave scans, then the 16 wave totals
+            const uint32_t b0 = 4 * tid;
+            uint32_t c4[4], t = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                c4[k] = b0 + k < np ? bc[b0 + k] : 0u;
+                t += c4[k];
+                if (c4[k] > 32) atomicMax(bmax, c4[k]);
+            }
+            uint32_t inc = t;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t v = __shfl_up(inc, o, 64);
+                if (lane >= (uint32_t)o) inc += v;
+            }
+            if (lane == 63) cum[wave] = inc;
             __syncthreads();
-            for (uint32_t i = tid; i < np; i += 1024) {
-                const uint32_t l = i ^ j;
-                if (l > i) {
-                    const uint64_t a = key[i], b = key[l];
-                    if ((a > b) == ((i & k) == 0)) {
-                        key[i] = b;
-                        key[l] = a;
-                    }
-                }
+            uint32_t base = inc - t;
+            for (uint32_t w = 0; w < wave; ++w) base += cum[w];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (b0 + k < np) bc[b0 + k] = base;  // bucket start (a cursor while scattering, then the end)
+                base += c4[k];
             }
         }
-    __syncthreads();
+        __syncthreads();
+        const bool bitonic = bmax[0] > 32;
+        if (!bitonic) {
+            for (uint32_t i = tid; i < n; i += 1024) {
+                const uint64_t kk = key[i];
+                tmp[atomicAdd(&bc[(uint32_t)(kk >> 32) >> sh], 1u)] = kk;
+            }
+            __syncthreads();
+            for (uint32_t b = tid; b < np; b += 1024) {  // bucket b: [end of b - 1, end of b)
+                const uint32_t lo = b ? bc[b - 1] : 0u, hi = bc[b];
+                for (uint32_t i = lo + 1; i < hi; ++i) {
+                    const uint64_t v = tmp[i];
+                    uint32_t j = i;
+                    while (j > lo && tmp[j - 1] > v) {
+                        tmp[j] = tmp[j - 1];
+                        --j;
+                    }
+                    tmp[j] = v;
+                }
+            }
+            __syncthreads();
+            key = tmp;
+        } else {
+            for (uint32_t i = n + tid; i < np; i += 1024) key[i] = ~0ull;
+            for (uint32_t k = 2; k <= np; k <<= 1)
+                for (uint32_t j = k >> 1; j; j >>= 1) {
+                    __syncthreads();
+                    for (uint32_t i = tid; i < np; i += 1024) {
+                        const uint32_t l = i ^ j;
+                        if (l > i) {
+                            const uint64_t a = key[i], b = key[l];
+                            if ((a > b) == ((i & k) == 0)) {
+                                key[i] = b;
+                                key[l] = a;
+                            }
+                        }
+                    }
+                }
+            __syncthreads();
+        }
+    }
     uint32_t *cm_img = reinterpret_cast<uint32_t *>(img + ci.o_cm);
     uint32_t *chi_img = reinterpret_cast<uint32_t *>(img + ci.o_chi);
     uint16_t *e_img = reinterpret_cast<uint16_t *>(img + ci.o_e);
@@ -137,7 +198,7 @@ __global__ __launch_bounds__(1024) void k_replayable_wt_build(const uint4 *__res
         };
         const uint32_t a = lb((uint64_t)tid << msh), b = tid < 256 ? lb((uint64_t)(tid + 1) << msh) : n;
         reinterpret_cast<uint16_t *>(img + ci.o_im)[tid] = (uint16_t)a;
-        atomicMax(bmax, b - a);
+        atomicMax(bmax + 2, b - a);
     } else if (tid >= 320 && tid < 320 + 256) {
         const uint32_t bk = tid - 320;
         auto lb = [&](uint64_t x) {  // first position with C_hi >= x
@@ -150,39 +211,55 @@ __global__ __launch_bounds__(1024) void k_replayable_wt_build(const uint4 *__res
         };
         const uint32_t a = lb((uint64_t)bk << 24), b = lb((uint64_t)(bk + 1) << 24);
         reinterpret_cast<uint16_t *>(img + ci.o_ic)[bk] = (uint16_t)a;
-        atomicMax(bmax + 1, b - a);
+        atomicMax(bmax + 3, b - a);
     }
     __syncthreads();
-    if (tid == 0) atomicMax(&classes[c].rS, 32u - __clz(max(bmax[0], bmax[1])));
-    // prefix / suffix maxima of the ranks (wave 0 / wave 1, 64 positions or fewer per lane)
-    if (wave < 2) {
-        uint16_t *pm = reinterpret_cast<uint16_t *>(img + ci.o_pm);
-        const uint32_t cs = (n + 63) / 64, j0 = min(lane * cs, n), j1 = min(j0 + cs, n);
-        uint32_t mx = 0;
-        for (uint32_t j = j0; j < j1; ++j) mx = max(mx, (uint32_t)S0[j]);
-        uint32_t ex = 0;  // prefix: maximum of the lanes before; suffix: of the lanes after
+    if (tid == 0) atomicMax(&classes[c].rS, 32u - __clz(max(bmax[2], bmax[3])));
+    // prefix / suffix maxima of the ranks: pm[d] = {max rank at positions < d, max rank at positions >= d};
+    // 4 positions per thread, wave scans (up for the prefix, down for the suffix), then the 16 wave totals
+    {
+        const uint32_t j0 = 4 * tid;
+        uint32_t v[4], pre[4], suf[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = j0 + k < n ? (uint32_t)S0[j0 + k] : 0u;
+        pre[0] = v[0];
+        suf[3] = v[3];
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+            pre[k] = max(pre[k - 1], v[k]);
+            suf[3 - k] = max(suf[4 - k], v[3 - k]);
+        }
+        uint32_t up = pre[3], dn = suf[0], exu = 0, exd = 0;
         for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t v = wave == 0 ? __shfl_up(mx, o, 64) : __shfl_down(mx, o, 64);
-            const bool in = wave == 0 ? lane >= (uint32_t)o : lane + o < 64;
-            mx = in ? max(mx, v) : mx;
-            ex = in ? max(ex, v) : ex;
-        }
-        if (wave == 0) {
-            uint32_t run = ex;
-            for (uint32_t j = j0; j < j1; ++j) {
-                pm[2 * j] = (uint16_t)run;
-                run = max(run, (uint32_t)S0[j]);
+            const uint32_t a = __shfl_up(up, o, 64), b = __shfl_down(dn, o, 64);
+            if (lane >= (uint32_t)o) {
+                up = max(up, a);
+                exu = max(exu, a);
             }
-            if (j1 == n && j0 < j1) pm[2 * n] = (uint16_t)run;
-        } else {
-            uint32_t run = ex;
-            for (uint32_t j = j1; j > j0; --j) {
-                run = max(run, (uint32_t)S0[j - 1]);
-                pm[2 * (j - 1) + 1] = (uint16_t)run;
+            if (lane + o < 64) {
+                dn = max(dn, b);
+                exd = max(exd, b);
             }
         }
+        if (lane == 63) wb[wave] = up;
+        if (lane == 0) wb[16 + wave] = dn;
+        __syncthreads();
+        for (uint32_t w = 0; w < 16; ++w) {
+            if (w < wave) exu = max(exu, wb[w]);
+            if (w > wave) exd = max(exd, wb[16 + w]);
+        }
+        uint32_t *pm = reinterpret_cast<uint32_t *>(img + ci.o_pm);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t j = j0 + k;
+            if (j <= n) {
+                const uint32_t lo = max(exu, k ? pre[k - 1] : 0u);  // positions < j
+                const uint32_t hi = j < n ? max(exd, suf[k]) : 0u;  // positions >= j
+                pm[j] = lo | hi << 16;
+            }
+        }
+        __syncthreads();  // wb is the level loop's next
     }
-    __syncthreads();
     // wavelet levels
     const uint32_t K = ci.K, nw = ci.nw;
     uint2 *lv = reinterpret_cast<uint2 *>(img + ci.o_lv);
@@ -470,7 +547,8 @@ static uint32_t wt_threads() {
     return t;
 }
 
-constexpr size_t WT_BUILD_LDS = WT_NMAX * 8 + WT_NMAX * 4 + 2 * WT_NMAX * 2 + 2 * (WT_NMAX / 32 + 4) * 4 + 16 * 8 + 16;
+constexpr size_t WT_BUILD_LDS =
+    WT_NMAX * 8 + WT_NMAX * 4 + 2 * WT_NMAX * 2 + 2 * (WT_NMAX / 32 + 4) * 4 + 16 * 8 + 16 + WT_NMAX * 8;
 
 int wt_build(WtState &w, const uint4 *d_table, uint32_t E, const ClassInfo *cls, uint32_t n_cls,
              const ModParams &mod, hipStream_t st) {
@@ -485,7 +563,7 @@ int wt_build(WtState &w, const uint4 *d_table, uint32_t E, const ClassInfo *cls,
         o.pn = cls[c].pn;
         o.start = cls[c].start;
         o.n = cls[c].count;
-        if (o.n > WT_NMAX) return NMZ_OK;  // keep the order-query sweep
+        if (o.n >= WT_NMAX) return NMZ_OK;  // keep the order-query sweep (pm and the sort take n < 4,096)
         if (o.n <= WT_BRUTE) continue;
         o.K = bitlen(o.n);  // 2^K > n >= every bound R
         o.nw = o.n / 32 + 1;
@@ -525,7 +603,7 @@ int wt_build(WtState &w, const uint4 *d_table, uint32_t E, const ClassInfo *cls,
     NMZ_HIP(hipMemsetAsync(w.d_rowsum, 0, 256 * 8, st));
     NMZ_HIP(hipMemcpyAsync(d_cls, oc.data(), n_cls * sizeof(WtClass), hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_replayable_wt_build, dim3(n_cls, 256), dim3(1024), WT_BUILD_LDS, st, d_table, E, d_cls,
-                       w.msh, w.d_blob, w.rb16, w.d_rowsum);
+                       w.msh, bitlen(mod.m32), w.d_blob, w.rb16, w.d_rowsum);
     NMZ_HIP(hipGetLastError());
     NMZ_HIP(hipStreamSynchronize(st));  // the host vector above is pageable
     w.on = true;
