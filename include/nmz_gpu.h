@@ -273,6 +273,11 @@ int nmz_ed_allpairs_knn(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
 typedef struct nmz_ed_plan nmz_ed_plan;
 int nmz_ed_plan_create(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, uint32_t n_traces,
                        uint32_t band, nmz_ed_plan **out);
+/* The same plan from event hashes already in device memory: off (host, n_traces + 1 offsets) and d_sym (device,
+ * off[n_traces] u64, read during the call). Multi-GPU callers upload 1/N of the symbols per device and all_gather
+ * them over RCCL instead of pushing the whole store through every device's PCIe link. */
+int nmz_ed_plan_create_dev(nmz_ctx *ctx, const uint64_t *off, const uint64_t *d_sym, uint32_t n_traces,
+                           uint32_t band, nmz_ed_plan **out);
 int nmz_ed_plan_destroy(nmz_ed_plan *plan);
 int nmz_ed_plan_is_fast(const nmz_ed_plan *plan);
 int nmz_ed_allpairs_knn_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys, void *stream);

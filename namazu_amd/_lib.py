@@ -82,6 +82,7 @@ SIGNATURES = {
     "nmz_ed_allpairs_knn": (_int, [_P, _P, _P, _u32, _u32, _u32, _P, _P]),
     "nmz_ed_plan_create": (_int, [_P, _P, _P, _u32, _u32, ctypes.POINTER(_P)]),
     "nmz_ed_plan_destroy": (_int, [_P]),
+    "nmz_ed_plan_create_dev": (_int, [_P, _P, _P, _u32, _u32, ctypes.POINTER(_P)]),
     "nmz_ed_plan_is_fast": (_int, [_P]),
     "nmz_ed_block_shard": (_u32, [_u32, _u32]),
     "nmz_ed_allpairs_knn_dev": (_int, [_P, _u32, _P, _P]),

@@ -505,21 +505,28 @@ static uint32_t ed_bv_row_queries() {
 // The bit-parallel plan built on the device: upload the symbols, sort/unique them (dense ids = ranks), write the
 // candidate streams with a binary search per symbol. Returns 1 (not applicable: the alphabet does not fit the
 // bit-parallel LDS tables) so the caller falls back to the host build and the other kernels.
+// d_sym_in: the symbols already on the device (nmz_ed_plan_create_dev), else uploaded from sym.
 static int ed_plan_build_bv_device(nmz_ed_plan *p, const uint64_t *off, const uint64_t *sym, uint32_t N,
-                                   uint32_t band, uint32_t maxlen) {
+                                   uint32_t band, uint32_t maxlen, const uint64_t *d_sym_in) {
     hipStream_t st = p->ctx->stream;
     const uint64_t total = off[N];
-    NMZ_CHECK(total == 0 || sym, "sym is NULL");
+    NMZ_CHECK(total == 0 || sym || d_sym_in, "sym is NULL");
     DevBuf tmp;
     struct Release {
         DevBuf &b;
         ~Release() { b.release(); }
     } release_tmp{tmp};
-    NMZ_TRY(tmp.ensure(Carve::bytes_for(total, 8) * 2 + Carve::bytes_for(N + 1, 8)));
+    NMZ_TRY(tmp.ensure(Carve::bytes_for(d_sym_in ? 0 : total, 8) + Carve::bytes_for(total, 8) +
+                       Carve::bytes_for(N + 1, 8)));
     Carve tv(tmp.ptr);
-    uint64_t *d_sym = tv.take<uint64_t>(total), *d_uniq = tv.take<uint64_t>(total);
+    const uint64_t *d_sym = d_sym_in;
+    if (!d_sym_in) {
+        uint64_t *d_up = tv.take<uint64_t>(total);
+        NMZ_HIP(hipMemcpyAsync(d_up, sym, total * 8, hipMemcpyHostToDevice, st));
+        d_sym = d_up;
+    }
+    uint64_t *d_uniq = tv.take<uint64_t>(total);
     uint64_t *d_off = tv.take<uint64_t>(N + 1);
-    NMZ_HIP(hipMemcpyAsync(d_sym, sym, total * 8, hipMemcpyHostToDevice, st));
     NMZ_HIP(hipMemcpyAsync(d_off, off, (N + 1) * 8, hipMemcpyHostToDevice, st));
     uint64_t n_uniq = 0;
     NMZ_TRY(device_unique_u64(d_sym, total, d_uniq, &n_uniq, st));
@@ -610,8 +617,9 @@ static int ed_plan_build_bv_device(nmz_ed_plan *p, const uint64_t *off, const ui
     return NMZ_OK;
 }
 
+// d_sym: the symbols on the device instead of sym (host); the host build paths take a copy of them
 static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, uint32_t N, uint32_t band,
-                         nmz_ed_plan **out) {
+                         nmz_ed_plan **out, const uint64_t *d_sym = nullptr) {
     NMZ_CHECK(ctx && out, "NULL argument");
     NMZ_CHECK(N == 0 || off, "off is NULL");
     *out = nullptr;
@@ -625,7 +633,7 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
     for (uint32_t i = 0; i < N; ++i) maxlen = std::max<uint32_t>(maxlen, (uint32_t)(off[i + 1] - off[i]));
     if (ed_bv_supported(band) && maxlen + ed_bv_template(band) < MAX_FAST_LEN && total >= ED_DEVICE_REMAP_MIN &&
         total < (1ULL << 31) && !getenv("NMZ_ED_HOST_REMAP")) {
-        const int rc = ed_plan_build_bv_device(p, off, sym, N, band, maxlen);
+        const int rc = ed_plan_build_bv_device(p, off, sym, N, band, maxlen, d_sym);
         if (rc == NMZ_OK) {
             *out = p;
             return NMZ_OK;
@@ -639,6 +647,14 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         p->n = N;
         p->band = band;
     }
+    std::vector<uint64_t> hsym;  // the host paths read the symbols on the host
+    if (d_sym && total) {
+        hsym.resize(total);
+        NMZ_HIP(hipMemcpyAsync(hsym.data(), d_sym, total * 8, hipMemcpyDeviceToHost, st));
+        NMZ_HIP(hipStreamSynchronize(st));
+        sym = hsym.data();
+    }
+    NMZ_CHECK(total == 0 || sym, "sym is NULL");
     // dense symbol ids (exact remap: a == b <=> id(a) == id(b))
     std::vector<uint16_t> ids;
     const bool want_wide = ed_wide_supported(band);
@@ -1279,6 +1295,16 @@ int nmz_ed_plan_query_knn(nmz_ed_plan *plan, const uint64_t *q_off, const uint64
     NMZ_HIP(hipMemcpyAsync(knn_dist, d_ds, nk * 4, hipMemcpyDeviceToHost, st));
     NMZ_HIP(hipStreamSynchronize(st));
     return NMZ_OK;
+}
+
+int nmz_ed_plan_create_dev(nmz_ctx *ctx, const uint64_t *off, const uint64_t *d_sym, uint32_t n_traces,
+                           uint32_t band, nmz_ed_plan **out) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    NMZ_CHECK(n_traces == 0 || off, "off is NULL");
+    NMZ_CHECK(n_traces == 0 || off[n_traces] == 0 || d_sym, "d_sym is NULL");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    return ed_plan_build(ctx, off, nullptr, n_traces, band, out, d_sym);
 }
 
 int nmz_ed_allpairs_knn_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys, void *stream) {

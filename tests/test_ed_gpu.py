@@ -176,6 +176,42 @@ def test_knn_device_plan_api(ctx):
     L.nmz_ed_plan_destroy(plan)
 
 
+@pytest.mark.parametrize("n,lmin,lmax,w,alphabet", [(300, 150, 200, 32, 12),     # host build (small store)
+                                                   (700, 1500, 1600, 16, 40),   # device build (>= 2^20 symbols)
+                                                   (40, 100, 300, 300, 12)])    # wide kernel (host build)
+def test_knn_plan_from_device_symbols(ctx, n, lmin, lmax, w, alphabet):
+    """nmz_ed_plan_create_dev (symbols already in HBM: the multi-GPU bench's all_gathered store) gives the same
+    k-NN lists as the host-array plan and the oracle, on the device build and on the host builds (which copy the
+    symbols back)."""
+    import torch
+    L = _lib.load()
+    rng = np.random.default_rng(n + w)
+    ts = make_traces(n, lmin, lmax, 0.03, alphabet=alphabet, rng=rng)
+    d_sym = torch.from_numpy(ts.sym.view(np.int64)).to("cuda")
+    torch.cuda.synchronize()
+    k = 6
+    out = []
+    for dev in (True, False):
+        plan = ctypes.c_void_p()
+        if dev:
+            _lib.check(L.nmz_ed_plan_create_dev(ctx.handle, _lib.ptr(ts.off), ctypes.c_void_p(d_sym.data_ptr()),
+                                                len(ts), w, ctypes.byref(plan)))
+        else:
+            _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), len(ts), w,
+                                            ctypes.byref(plan)))
+        d_keys = torch.empty(len(ts) * k, dtype=torch.int64, device="cuda")
+        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        _lib.check(L.nmz_ed_allpairs_knn_dev(plan, k, ctypes.c_void_p(d_keys.data_ptr()), stream))
+        torch.cuda.synchronize()
+        out.append(d_keys.cpu().numpy().view(np.uint64).reshape(-1, k))
+        L.nmz_ed_plan_destroy(plan)
+    assert np.array_equal(out[0], out[1])
+    if n <= 300:
+        oi, od = O.ed_allpairs_knn(ts.off, ts.sym, w, k)
+        assert np.array_equal((out[0] >> np.uint64(32)).astype(np.uint32), od)
+        assert np.array_equal((out[0] & np.uint64(0xFFFFFFFF)).astype(np.uint32), oi)
+
+
 def test_knn_config3_shape_sampled(ctx):
     """configs[2] trace shape (L = 2048, w = 32, k = 8, ZK-style mutations) at
     N = 2048: sampled brute-force parity for a few queries."""

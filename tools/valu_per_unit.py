@@ -15,7 +15,8 @@ import sys
 # leg -> [(kernel name prefix, key, unit, units per launch of the leg's default workload)]
 LEGS = {
     # the order-query kernel (default) and the per-decision sweep (NMZ_REPLAY_OQ=0 runs of the same leg)
-    "replayable": [("void nmz::k_replayable_sweep_oq<false, false>", "k_replayable_sweep_oq", "decision", 2**20 * 4096),
+    "replayable": [("void nmz::k_replayable_sweep_wt<false>", "k_replayable_sweep_wt", "decision", 2**20 * 4096),
+                   ("void nmz::k_replayable_sweep_oq<false, false>", "k_replayable_sweep_oq", "decision", 2**20 * 4096),
                    ("void nmz::k_replayable_sweep_fast", "k_replayable_sweep_fast", "decision", 2**20 * 4096)],
     "random": [("void nmz::k_random_sweep", "k_random_sweep", "decision", 10_000_000 * 10_000)],
     # two-phase search: the DP kernel per pair that ran the DP (the k_ed_bv counters of the bench workload:
@@ -28,7 +29,7 @@ LEGS = {
                   ("void nmz::k_ed_qg_filter<", "k_ed_qg_filter:survey", "pair", 100_000 * 99_999 // 2),
                   ("nmz::k_ed_qg_scatter", "k_ed_qg_filter:survey", "pair", 100_000 * 99_999 // 2)],
     # compact tables (a store-wide alphabet of thousands of events): the CMP instantiation
-    "ed_alphabet": [("void nmz::k_ed_bv_dp<32, true>", "k_ed_bv_dp:alphabet", "DP pair", 51_000_000),
+    "ed_alphabet": [("void nmz::k_ed_bv_dp<32, true>", "k_ed_bv_dp:alphabet", "DP pair", 51_031_728),
                     ("void nmz::k_ed_qg_filter<", "k_ed_qg_filter:alphabet", "pair", 100_000 * 99_999 // 2),
                     ("nmz::k_ed_qg_scatter", "k_ed_qg_filter:alphabet", "pair", 100_000 * 99_999 // 2)],
     "ed_wide": [("void nmz::k_ed_wide<4>", "k_ed_wide", "pair", 256 * 255 // 2)],
