@@ -895,13 +895,24 @@ uint32_t ed_bv_item() {
 constexpr uint64_t ED_TP_MAX_ENTRIES = 1ULL << 30;  // 4 GiB of entries
 constexpr uint64_t ED_TP_MAX_MASK_BYTES = 4ULL << 30;
 
-// MurmurHash3's 64-bit finaliser (host): the shard of a filter tile
+// MurmurHash3's 64-bit finaliser (host)
 static inline uint64_t tile_mix(uint64_t x) {
     x ^= x >> 33;
     x *= 0xff51afd7ed558ccdULL;
     x ^= x >> 33;
     x *= 0xc4ceb9fe1a85ec53ULL;
     return x ^ (x >> 33);
+}
+// The shard that owns query block qb (64 queries) of the two-phase search. Snake order (0, 1, .., S-1, S-1, .., 0,
+// repeated): a query block's work falls with qb inside the upper triangle (fewer candidates j > q) and inside
+// every family of near-duplicates, and each period of 2S blocks gives every shard one block from the front half and
+// its mirror from the back half, so linear trends cancel (NMZ_ED_DEAL=hash: the MurmurHash3 deal, for A/B runs).
+static uint32_t ed_block_shard(uint32_t qb, uint32_t n_shards) {
+    if (n_shards <= 1) return 0;
+    const char *e = getenv("NMZ_ED_DEAL");
+    if (e && std::string(e) == "hash") return (uint32_t)(tile_mix(qb) % n_shards);
+    const uint32_t r = qb % (2 * n_shards);
+    return r < n_shards ? r : 2 * n_shards - 1 - r;
 }
 // the entry-list limit (NMZ_ED_TP_MAX_ENTRIES lowers it, so tests can force the single-kernel fallback)
 static uint64_t ed_tp_max_entries() {
@@ -934,7 +945,7 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A) {
     const uint32_t shard = A.shard, n_shards = A.n_shards;
     if (N >= (1u << 30)) return 1;  // entries carry j in 30 bits
     // this shard's tiles (qb << 32 | cb), built and uploaded once per (shard, n_shards): every tile of query block
-    // qb belongs to shard tile_mix(qb) mod n_shards. Whole query blocks, so a query pair's DP entries stay in one
+    // qb belongs to shard ed_block_shard(qb). Whole query blocks, so a query pair's DP entries stay in one
     // shard's work items: dealt by tile, a pair's near-duplicate candidates (a few 256-wide tiles) spread over
     // several shards, every shard built the pair's Peq tables for a fraction of its entries, and the 8 shards
     // summed to 1.15x the unsharded search. The DP work is data-dependent and clustered (the clustered workload's
@@ -944,11 +955,10 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A) {
     DevBuf &tl = p->tile_list[key];
     if (!p->tile_count.count(key)) {
         std::vector<uint64_t> tiles;
-        for (uint32_t qb = 0; qb < QB; ++qb)
-            for (uint32_t cb = qb / 4; cb < NCB; ++cb) {
-                const uint64_t id = ((uint64_t)qb << 32) | cb;
-                if (n_shards == 1 || tile_mix(qb) % n_shards == shard) tiles.push_back(id);
-            }
+        for (uint32_t qb = 0; qb < QB; ++qb) {
+            if (ed_block_shard(qb, n_shards) != shard) continue;
+            for (uint32_t cb = qb / 4; cb < NCB; ++cb) tiles.push_back(((uint64_t)qb << 32) | cb);
+        }
         NMZ_TRY(tl.ensure(Carve::bytes_for(tiles.size() + 1, 8)));
         if (!tiles.empty()) NMZ_HIP(hipMemcpy(tl.ptr, tiles.data(), tiles.size() * 8, hipMemcpyHostToDevice));
         p->tile_count[key] = tiles.size();
@@ -1311,9 +1321,7 @@ int nmz_ed_allpairs_knn_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys,
     return nmz_ed_allpairs_knn_shard_dev(plan, k, 0, 1, d_knn_keys, stream);
 }
 
-uint32_t nmz_ed_block_shard(uint32_t qb, uint32_t n_shards) {
-    return n_shards <= 1 ? 0u : (uint32_t)(tile_mix(qb) % n_shards);
-}
+uint32_t nmz_ed_block_shard(uint32_t qb, uint32_t n_shards) { return ed_block_shard(qb, n_shards); }
 
 int nmz_ed_allpairs_knn_shard_dev(nmz_ed_plan *plan, uint32_t k, uint32_t shard, uint32_t n_shards,
                                   uint64_t *d_knn_keys, void *stream) {

@@ -12,6 +12,7 @@ completed with (band + 1, smallest unlisted ids) (nmz_ed_knn_fill_dev on the
 GPU, fill_knn_keys on the host).
 """
 import ctypes
+import os
 
 import numpy as np
 
@@ -31,16 +32,21 @@ _M64 = (1 << 64) - 1
 
 def ed_block_shard(qb, world):
     """Shard owning query block qb (queries 64 qb .. 64 qb + 63) of the two-phase all-pairs search
-    (nmz_ed_allpairs_knn_shard_dev; csrc/ed.hip tile_mix): MurmurHash3's 64-bit finaliser of qb mod world. Whole
-    query blocks, so a query pair's DP entries stay in one shard; the hash breaks the clustered workloads' period."""
+    (nmz_ed_allpairs_knn_shard_dev; csrc/ed.hip ed_block_shard): snake order 0, 1, .., world-1, world-1, .., 0,
+    repeated, so the falling work per block inside the upper triangle and inside each family of near-duplicates
+    cancels between a block and its mirror. Whole query blocks, so a query pair's DP entries stay in one shard.
+    NMZ_ED_DEAL=hash selects the MurmurHash3 deal (A/B runs)."""
     if world <= 1:
         return 0
-    x = qb
-    x ^= x >> 33
-    x = (x * 0xFF51AFD7ED558CCD) & _M64
-    x ^= x >> 33
-    x = (x * 0xC4CEB9FE1A85EC53) & _M64
-    return (x ^ (x >> 33)) % world
+    if os.environ.get("NMZ_ED_DEAL") == "hash":
+        x = qb
+        x ^= x >> 33
+        x = (x * 0xFF51AFD7ED558CCD) & _M64
+        x ^= x >> 33
+        x = (x * 0xC4CEB9FE1A85EC53) & _M64
+        return (x ^ (x >> 33)) % world
+    r = qb % (2 * world)
+    return r if r < world else 2 * world - 1 - r
 
 
 def ed_pair_shard(i, j, world):

@@ -47,12 +47,18 @@ def main():
     cnt = np.zeros(_lib.NMZ_ED_NCOUNTERS, np.uint64)
     for s in range(S):
         tot, c = ctypes.c_double(), ctypes.c_uint64()
+        ph = {n: (ctypes.c_double(), ctypes.c_uint64()) for n in (b"ed_qg_filter", b"ed_bv_dp")}
         L.nmz_timing_read(ctx.handle, b"ed_bv", ctypes.byref(tot), ctypes.byref(c), 1)
+        for n, (a, b) in ph.items():
+            L.nmz_timing_read(ctx.handle, n, ctypes.byref(a), ctypes.byref(b), 1)
         _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, s, S, ctypes.c_void_p(d.data_ptr()), stream))
         torch.cuda.synchronize()
         _lib.check(L.nmz_timing_read(ctx.handle, b"ed_bv", ctypes.byref(tot), ctypes.byref(c), 1))
+        for n, (a, b) in ph.items():
+            L.nmz_timing_read(ctx.handle, n, ctypes.byref(a), ctypes.byref(b), 1)
         _lib.check(L.nmz_ed_plan_counters(plan, _lib.ptr(cnt), stream))
-        rows.append({"shard": s, "kernel_ms": tot.value, "dp_pairs": int(cnt[0]), "blocks": int(cnt[2]),
+        rows.append({"shard": s, "kernel_ms": tot.value, "filter_ms": ph[b"ed_qg_filter"][0].value,
+                     "dp_ms": ph[b"ed_bv_dp"][0].value, "dp_pairs": int(cnt[0]), "blocks": int(cnt[2]),
                      "in_band": int(cnt[1])})
     L.nmz_ed_plan_destroy(plan)
     ms = np.array([r["kernel_ms"] for r in rows])
@@ -62,7 +68,8 @@ def main():
                       "blocks_max_over_mean": float(bl.max() / bl.mean()),
                       "sum_shard_ms": float(ms.sum()), "unsharded_ms": full_ms,
                       "max_shard_ms": float(ms.max()), "speedup_bound": float(full_ms / ms.max()),
-                      "item": int(os.environ.get("NMZ_ED_ITEM", "4096"))}, indent=1))
+                      "item": int(os.environ.get("NMZ_ED_ITEM", "4096")),
+                      "deal": os.environ.get("NMZ_ED_DEAL", "snake")}, indent=1))
 
 
 if __name__ == "__main__":
