@@ -72,6 +72,7 @@ struct nmz_ctx {
     // scratch slots reused across calls (host-pointer entry points)
     nmz::DevBuf buf[16];
     std::vector<nmz::DevBuf> pool;  // free plan buffers (DevBuf::pool), freed by nmz_close
+    bool wt_lds_attr = false;        // the wavelet-tree kernels' LDS attribute is set on this context's device
     NmzTiming timing;
 };
 

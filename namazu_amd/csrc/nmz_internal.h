@@ -150,9 +150,16 @@ struct WtState {
     DevBuf mem;
 };
 bool wt_enabled();
-int wt_build(WtState &w, const uint4 *d_table, uint32_t E, const ClassInfo *cls, uint32_t n_cls,
+int wt_build(WtState &w, nmz_ctx *ctx, const uint4 *d_table, uint32_t E, const ClassInfo *cls, uint32_t n_cls,
              const ModParams &mod, hipStream_t st);
+// topk_scratch (wt_topk_scratch_bytes(S), or nullptr): the sweep also leaves per-seed sums (in bucketed order) and
+// per-workgroup largest sums there for wt_topk
 int wt_sweep(const WtState &w, nmz_ctx *ctx, hipStream_t st, const Buckets &b, const uint4 *d_table, uint32_t E,
-             const ModParams &mod, nmz_sched_stats *d_stats);
+             const ModParams &mod, nmz_sched_stats *d_stats, uint64_t S, void *topk_scratch, uint32_t k);
+size_t wt_topk_scratch_bytes(uint64_t S);
+// the top-k (k <= 64) of a sweep that ran with topk_scratch; fresh scratch must be zeroed first (wt_topk_reset)
+int wt_topk(hipStream_t st, void *scratch, const uint32_t *sorted_idx, uint64_t S, uint64_t seed0, uint32_t k,
+            nmz_topk_entry *d_out);
+int wt_topk_reset(hipStream_t st, void *scratch);
 
 }  // namespace nmz

@@ -66,6 +66,8 @@ struct nmz_replayable_plan {
     nmz::OqClass *d_oq_classes = nullptr;
     nmz::DevBuf oq_mem;
     nmz::WtState wt;                    // wavelet-tree statistics (k_replayable_sweep_wt, the default when it fits)
+    nmz::DevBuf wt_topk;                // their top-k candidates (sums, workgroup maxima, candidates)
+    void *wt_topk_zeroed = nullptr;     // the wt_topk buffer whose counters were zeroed
 };
 
 namespace nmz {
@@ -1447,8 +1449,24 @@ static SeedScratch carve_seed_scratch(void *p, uint64_t S) {
 // enqueue the sweep for device-resident seeds
 // Stats for every seed.
 // Seeds: the CSR d_soff / d_sbytes, or (d_soff == nullptr) the decimal strings of dec_lo .. dec_lo + S - 1.
+// the wavelet-tree sweep runs this plan's sweeps
+static bool use_wt(const nmz_replayable_plan *p) {
+    return p->wt.on && (replay_oq_enabled() || p->mod.kind != MOD_FAST);
+}
+
+// top-k on the wavelet-tree path: candidates above the k-th largest workgroup maximum (NMZ_WT_TOPK=0: the general
+// selection, for A/B runs)
+static bool wt_topk_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("NMZ_WT_TOPK");
+        return !(e && std::string(e) == "0");
+    }();
+    return on;
+}
+
 static int replayable_stats(nmz_replayable_plan *p, hipStream_t st, const uint32_t *d_soff,
-                            const uint8_t *d_sbytes, uint64_t S, nmz_sched_stats *d_stats, uint64_t dec_lo = 0) {
+                            const uint8_t *d_sbytes, uint64_t S, nmz_sched_stats *d_stats, uint64_t dec_lo = 0,
+                            void *wt_topk_scratch = nullptr, uint32_t k = 0) {
     if (S == 0) return NMZ_OK;
     const uint32_t E = p->n_events;
     if (E == 0 || p->mod.kind == MOD_ZERO) {
@@ -1467,9 +1485,9 @@ static int replayable_stats(nmz_replayable_plan *p, hipStream_t st, const uint32
     const int U = replay_u();
     const uint32_t per_unit = 64u * (uint32_t)U;
     const uint64_t max_units = S / per_unit + 256;
-    if (p->wt.on && (replay_oq_enabled() || p->mod.kind != MOD_FAST)) {
+    if (use_wt(p)) {
         NMZ_TRY(bucket_seeds_counted(st, sc.h0, S, OQ_WG, sc.b, sc.counter));
-        return wt_sweep(p->wt, p->ctx, st, sc.b, p->d_table, E, p->mod, d_stats);
+        return wt_sweep(p->wt, p->ctx, st, sc.b, p->d_table, E, p->mod, d_stats, S, wt_topk_scratch, k);
     }
     if (p->oq && (replay_oq_enabled() || p->mod.kind != MOD_FAST)) {
         NMZ_TRY(bucket_seeds_counted(st, sc.h0, S, OQ_WG, sc.b, sc.counter));
@@ -1539,7 +1557,21 @@ static int replayable_run(nmz_replayable_plan *p, hipStream_t st, const uint32_t
                           nmz_topk_entry *d_topk = nullptr, uint64_t dec_lo = 0) {
     NMZ_CHECK(k <= 256, "top-k supports k <= 256");
     NMZ_CHECK(k == 0 || d_topk, "d_topk is NULL");
-    NMZ_TRY(replayable_stats(p, st, d_soff, d_sbytes, S, d_stats, dec_lo));
+    // the wavelet-tree sweep's own candidates (k <= 64; more than one general-selection list, so that the gated
+    // fallback has its merge levels): the general selection runs only when they overflow
+    const bool fused = k && k <= 64 && S > 0 && use_wt(p) && wt_topk_enabled();
+    if (fused) {
+        NMZ_TRY(p->wt_topk.ensure(wt_topk_scratch_bytes(S)));
+        if (p->wt_topk.ptr != p->wt_topk_zeroed) {  // fresh or pooled memory: the self-resetting counters start at 0
+            NMZ_TRY(wt_topk_reset(st, p->wt_topk.ptr));
+            p->wt_topk_zeroed = p->wt_topk.ptr;
+        }
+    }
+    NMZ_TRY(replayable_stats(p, st, d_soff, d_sbytes, S, d_stats, dec_lo, fused ? p->wt_topk.ptr : nullptr, k));
+    if (fused) {
+        const SeedScratch sc = carve_seed_scratch(p->seed_scratch.ptr, p->max_seeds);
+        return wt_topk(st, p->wt_topk.ptr, sc.b.sorted_idx, S, seed0, k, d_topk);
+    }
     if (k) {
         NMZ_TRY(p->topk_lists.ensure(topk_scratch_entries(S, k) * sizeof(nmz_topk_entry)));
         NMZ_TRY(topk_select(st, d_stats, S, seed0, k, p->topk_lists.as<nmz_topk_entry>(), d_topk));
@@ -1554,7 +1586,8 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
     *out = nullptr;
     auto *p = new nmz_replayable_plan();
     p->ctx = ctx;
-    for (DevBuf *b : {&p->seed_scratch, &p->partial, &p->topk_lists, &p->plan_mem, &p->oq_mem, &p->wt.mem})
+    for (DevBuf *b : {&p->seed_scratch, &p->partial, &p->topk_lists, &p->plan_mem, &p->oq_mem, &p->wt.mem,
+                      &p->wt_topk})
         b->pool = &ctx->pool;
     p->n_events = E;
     p->max_interval = max_interval;
@@ -1613,6 +1646,7 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
         p->topk_lists.release();
         p->oq_mem.release();
         p->wt.mem.release();
+        p->wt_topk.release();
         delete p;
         return code;
     };
@@ -1662,7 +1696,7 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
         if (bad)
             return cleanup(fail(NMZ_EHIP, "plan table kernel failed"));
         // wavelet-tree images (the default sweep when they fit), else the order-query images
-        int orc = wt_build(p->wt, p->d_table, E, cls.data(), (uint32_t)cls.size(), p->mod, st);
+        int orc = wt_build(p->wt, ctx, p->d_table, E, cls.data(), (uint32_t)cls.size(), p->mod, st);
         if (orc != NMZ_OK) return cleanup(orc);
         if (!p->wt.on) orc = oq_build(p, cls, st);
         if (orc != NMZ_OK) return cleanup(orc);
@@ -1707,6 +1741,7 @@ int nmz_replayable_plan_destroy(nmz_replayable_plan *plan) {
         plan->topk_lists.release();
         plan->oq_mem.release();
         plan->wt.mem.release();
+        plan->wt_topk.release();
     }
     delete plan;
     return NMZ_OK;
@@ -1769,6 +1804,7 @@ int nmz_replayable_sweep(nmz_ctx *ctx, const uint32_t *seed_off, const uint8_t *
             p->topk_lists.release();
             p->oq_mem.release();
         p->wt.mem.release();
+        p->wt_topk.release();
             delete p;
         }
     } pg{plan};

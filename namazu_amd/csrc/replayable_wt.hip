@@ -31,7 +31,7 @@ namespace nmz {
 
 constexpr uint32_t WT_BRUTE = 8;       // segments of at most this many events: per-event decisions
 constexpr uint32_t WT_NMAX = 4096;     // largest segment the plan kernel sorts in LDS
-constexpr uint32_t WT_LDS_MAX = 160 * 1024;
+constexpr uint32_t WT_LDS_MAX = 160 * 1024 - 256;  // dynamic LDS; the sweep kernel's few static bytes need the rest
 constexpr uint32_t WT_NONE = 0xffffffffu;
 
 struct WtClass {
@@ -326,6 +326,19 @@ __device__ __forceinline__ void wt_decide(uint4 q, uint64_t nH, uint32_t Hm, uin
     key = k > key ? k : key;
 }
 
+// Wave-uniform operands of the descents copied into VGPRs, so their VOP2 forms take no SGPR or inline-constant
+// operand (tools/ubench measures those forms at half the VGPR-only issue rate): 1-2 % on K1, consistently across
+// four A/B pairs (profiles/r03r_wt_vgprc_ab.json); -DWT_SGPR_CONST builds the compiler's forms
+#ifndef WT_SGPR_CONST
+__device__ __forceinline__ uint32_t wt_v(uint32_t x) {
+    uint32_t v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(x));
+    return v;
+}
+#else
+__device__ __forceinline__ uint32_t wt_v(uint32_t x) { return x; }
+#endif
+
 // ones among the first p entries of a level, minus those before the node that starts at s (s >> 1: every node
 // before it is whole and half ones)
 __device__ __forceinline__ uint32_t wt_ones(const uint2 *__restrict__ lvl, uint32_t s, uint32_t p) {
@@ -384,21 +397,23 @@ __device__ __forceinline__ void wt_seed_class(const WtClass &ci, const char *__r
     const uint32_t K = ci.K, nw = ci.nw;
     uint32_t oA = d, oB = d, cA = 0, cB = 0;
     uint32_t lA = WT_NONE, sA = 0, qA = 0, lB = WT_NONE, sB = 0, qB = 0;
+    const uint32_t nv = wt_v(n), one = wt_v(1u), five = wt_v(5u);
     for (uint32_t l = 0; l < K; ++l) {
-        const uint32_t h = 1u << (K - l - 1), msk = ~(2 * h - 1);
+        const uint32_t hs = 1u << (K - l - 1);
+        const uint32_t h = wt_v(hs), msk = wt_v(~(2 * hs - 1)), l1 = wt_v(l + 1);
         const uint2 *__restrict__ lvl = lv + l * nw;
         const uint32_t s1 = RA & msk, p1 = s1 + oA, s2 = RB & msk, p2 = s2 + oB;
-        const uint2 w1 = lvl[p1 >> 5], w2 = lvl[p2 >> 5];
-        const uint32_t o1 = w1.y + __popc(__builtin_amdgcn_ubfe(w1.x, 0u, p1)) - (s1 >> 1);
-        const uint32_t o2 = w2.y + __popc(__builtin_amdgcn_ubfe(w2.x, 0u, p2)) - (s2 >> 1);
+        const uint2 w1 = lvl[p1 >> five], w2 = lvl[p2 >> five];
+        const uint32_t o1 = w1.y + __popc(__builtin_amdgcn_ubfe(w1.x, 0u, p1)) - (s1 >> one);
+        const uint32_t o2 = w2.y + __popc(__builtin_amdgcn_ubfe(w2.x, 0u, p2)) - (s2 >> one);
         const uint32_t z1 = oA - o1, z2 = oB - o2;
         const bool b1 = RA & h, b2 = RB & h;
         const bool u1 = b1 && z1 != 0;
-        const bool u2 = b2 && min(n - s2, h) > z2;  // zeros of the node past the prefix: suffix elements below R_B
-        lA = u1 ? l + 1 : lA;
+        const bool u2 = b2 && min(nv - s2, h) > z2;  // zeros of the node past the prefix: suffix elements below R_B
+        lA = u1 ? l1 : lA;
         sA = u1 ? s1 : sA;
         qA = u1 ? z1 : qA;
-        lB = u2 ? l + 1 : lB;
+        lB = u2 ? l1 : lB;
         sB = u2 ? s2 : sB;
         qB = u2 ? z2 : qB;
         cA += b1 ? 0u : o1;
@@ -420,15 +435,16 @@ __device__ __forceinline__ void wt_seed_class(const WtClass &ci, const char *__r
     const uint32_t l0 = min(lA, lB);
     for (uint32_t l = 0; l < K; ++l) {
         if (!__builtin_amdgcn_ballot_w64(l >= l0)) continue;
-        const uint32_t h = 1u << (K - l - 1);
+        const uint32_t hs = 1u << (K - l - 1);
+        const uint32_t h = wt_v(hs), h2 = wt_v(2 * hs), lv1 = wt_v(l);
         const uint2 *__restrict__ lvl = lv + l * nw;
         const uint32_t p1 = sA + qA, p2 = sB + qB;
-        const uint2 w1 = lvl[p1 >> 5], w2 = lvl[p2 >> 5];
-        const uint32_t o1 = w1.y + __popc(__builtin_amdgcn_ubfe(w1.x, 0u, p1)) - (sA >> 1);
-        const uint32_t o2 = w2.y + __popc(__builtin_amdgcn_ubfe(w2.x, 0u, p2)) - (sB >> 1);
-        const bool a1 = l >= lA, a2 = l >= lB;
+        const uint2 w1 = lvl[p1 >> five], w2 = lvl[p2 >> five];
+        const uint32_t o1 = w1.y + __popc(__builtin_amdgcn_ubfe(w1.x, 0u, p1)) - (sA >> one);
+        const uint32_t o2 = w2.y + __popc(__builtin_amdgcn_ubfe(w2.x, 0u, p2)) - (sB >> one);
+        const bool a1 = lv1 >= lA, a2 = lv1 >= lB;
         const bool g1 = a1 && o1 != 0;
-        const bool g2 = a2 && min(n - sB, 2 * h) > h + o2;  // ones of the node past the prefix
+        const bool g2 = a2 && min(nv - sB, h2) > h + o2;  // ones of the node past the prefix
         sA += g1 ? h : 0u;
         qA = g1 ? o1 : qA;
         sB += g2 ? h : 0u;
@@ -447,6 +463,25 @@ __device__ __forceinline__ void wt_seed_class(const WtClass &ci, const char *__r
     sum += (uint64_t)d * Hm + (uint64_t)(n - d) * Hm2;
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// top-k on the wavelet-tree path (k <= 64; order: sum desc as int64, seed asc; n_fault = 0 for this policy).
+// Each workgroup's largest sum is the largest of a group of seeds, and the groups are disjoint, so the k-th largest
+// of the group maxima (or of a subset of them) is a value at least k seeds reach: no seed below it is in the top k.
+// One kernel (every block derives tau itself: cheaper than a launch) appends the seeds at or above tau (a few
+// hundred), and a one-block kernel ranks them exactly by counting; more than
+// WT_CAND candidates (heavy ties, e.g. maxInterval 1) take a slow exact selection there instead. The candidate
+// counter resets itself. (A "last block" handing tau or the ranking to the final workgroup of a kernel needs
+// device-scope fences, i.e. L2 writebacks on every XCD: +40 us on the sweep.)
+// ---------------------------------------------------------------------------------------------------------------
+constexpr uint32_t WT_CAND = 1024;
+constexpr uint32_t WT_MAX_GROUPS = 256 * 8;
+struct WtTopkState {
+    uint32_t n_cand, pad[3];
+    unsigned long long gmax[WT_MAX_GROUPS];
+    unsigned long long cand_key[WT_CAND];
+    unsigned long long cand_idx[WT_CAND];
+};
+
 // G workgroups per row L: each stages the row image into LDS and takes a contiguous share of the row's 64-seed
 // chunks, which its waves take one at a time from an LDS counter.
 template <bool BIG>
@@ -455,15 +490,19 @@ __global__ __launch_bounds__(1024) void k_replayable_sweep_wt(
     const uint32_t *__restrict__ sorted_idx, const uint4 *__restrict__ table, uint32_t E,
     const uint4 *__restrict__ blob, uint32_t rb16, const unsigned long long *__restrict__ rowsum,
     const WtClass *__restrict__ classes, uint32_t n_classes, uint32_t m, uint64_t mu, uint32_t m_k64, uint32_t msh,
-    uint32_t G, nmz_sched_stats *__restrict__ stats, unsigned long long *__restrict__ span) {
+    uint32_t G, nmz_sched_stats *__restrict__ stats, unsigned long long *__restrict__ span,
+    uint64_t *__restrict__ sums, WtTopkState *__restrict__ tk, uint32_t k) {
     extern __shared__ uint4 wt_lds[];
     const uint32_t L = blockIdx.x / G, g = blockIdx.x % G;
     const uint32_t s0 = bucket_off[L], s1 = bucket_off[L + 1];
     const uint32_t nch = (s1 - s0 + 63) / 64;
     const uint32_t c0 = g * nch / G, c1 = (g + 1) * nch / G;
-    if (c0 == c1) return;
-    if (span && threadIdx.x == 0) atomicMax(span, ~(unsigned long long)wall_clock64());
     uint32_t *ctr = reinterpret_cast<uint32_t *>(wt_lds + rb16);
+    if (c0 == c1) {  // no seeds (an empty group: the smallest key)
+        if (tk && threadIdx.x == 0) tk->gmax[blockIdx.x] = 0ull;
+        return;
+    }
+    if (span && threadIdx.x == 0) atomicMax(span, ~(unsigned long long)wall_clock64());
     {
         const uint4 *__restrict__ src = blob + (uint64_t)L * rb16;
         // every load of a pass in flight at once (indices clamped to the image, stores unconditional)
@@ -476,7 +515,10 @@ __global__ __launch_bounds__(1024) void k_replayable_sweep_wt(
 #pragma unroll
             for (uint32_t k = 0; k < B; ++k) wt_lds[min(i0 + k * nt + threadIdx.x, rb16 - 1)] = v[k];
         }
-        if (threadIdx.x == 0) *ctr = c0;
+        if (threadIdx.x == 0) {
+            *ctr = c0;
+            ctr[2] = ctr[3] = 0;  // the workgroup's largest sum key
+        }
     }
     __syncthreads();
     const char *img = reinterpret_cast<const char *>(wt_lds);
@@ -494,21 +536,217 @@ __global__ __launch_bounds__(1024) void k_replayable_sweep_wt(
         uint32_t W = 0;
         for (uint32_t c = 0; c < n_classes; ++c)
             wt_seed_class<BIG>(classes[c], img, row, h0, m, mu, m_k64, msh, sum, W, key);
+        const uint64_t total = sum + rsum - (uint64_t)W * m;
+        if (tk) {  // the chunk's largest sum, in the top-k's order (int64, as an order-preserving u64 key)
+            uint64_t km = j < s1 ? total ^ (1ull << 63) : 0ull;
+            for (int o = 32; o; o >>= 1) {
+                const uint64_t v = __shfl_xor(km, o, 64);
+                km = v > km ? v : km;
+            }
+            if (lane == 0) atomicMax(reinterpret_cast<unsigned long long *>(ctr + 2), (unsigned long long)km);
+        }
         if (j < s1) {
+            const uint32_t idx = sorted_idx[j];
+            if (sums) sums[j] = total;  // in sorted order: the wave's 64 writes coalesce (by seed index they scatter,
+                                        // one 64-B line per seed: +20 us on the step)
             nmz_sched_stats st;
-            st.sum_delay_ns = sum + rsum - (uint64_t)W * m;
+            st.sum_delay_ns = total;
             st.max_delay_ns = (int64_t)(key >> 32);
             st.argmax_event = ~(uint32_t)key;
             st.n_fault = 0;
             st.first_fault = NMZ_NONE;
             st.flags = 0;
-            stats[sorted_idx[j]] = st;
+            stats[idx] = st;
         }
     }
-    if (span) {
+    if (span || tk) {
         __syncthreads();
-        if (threadIdx.x == 0) atomicMax(span + 1, (unsigned long long)wall_clock64());
+        if (span && threadIdx.x == 0) atomicMax(span + 1, (unsigned long long)wall_clock64());
+        if (tk && threadIdx.x == 0) tk->gmax[blockIdx.x] = *reinterpret_cast<const unsigned long long *>(ctr + 2);
     }
+}
+
+__device__ __forceinline__ bool wt_better(unsigned long long ka, uint64_t sa, unsigned long long kb, uint64_t sb) {
+    return ka > kb || (ka == kb && sa < sb);
+}
+
+// every block: tau = the k-th largest key of the first min(n, 256) groups (a subset's k-th largest is at most the
+// whole set's, so tau stays a value at least k seeds reach; ~k / subset size of the groups' maxima lie above it, so
+// a few hundred candidates), by counting; then a grid-stride scan of the sweep's sums appending the seeds at or
+// above tau. (All n = 512 groups bitonic-sorted per block: 45 barriers, ~13 us of the scan's latency.)
+__global__ __launch_bounds__(256) void k_wt_topk_scan(const uint64_t *__restrict__ sums,
+                                                      const uint32_t *__restrict__ sorted_idx, uint64_t S, uint32_t n,
+                                                      uint32_t k, WtTopkState *__restrict__ tk) {
+    __shared__ unsigned long long g[256];
+    __shared__ unsigned long long tau_s;
+    const uint32_t m = min(n, 256u);
+    if (threadIdx.x < m) g[threadIdx.x] = tk->gmax[threadIdx.x];
+    if (threadIdx.x == 0) tau_s = 0;  // fewer groups than k: every seed is a candidate
+    __syncthreads();
+    if (m >= k && threadIdx.x < m) {
+        const unsigned long long x = g[threadIdx.x];
+        uint32_t gt = 0, eq = 0;
+        for (uint32_t j = 0; j < m; ++j) {
+            gt += g[j] > x;
+            eq += g[j] == x;
+        }
+        if (gt < k && k <= gt + eq) tau_s = x;  // every writer writes the same value
+    }
+    __syncthreads();
+    const unsigned long long t = tau_s;
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * 256; i0 < S; i0 += (uint64_t)gridDim.x * 256) {
+        const uint64_t i = i0 + threadIdx.x;
+        unsigned long long key = 0;
+        const bool in = i < S && (key = sums[i] ^ (1ull << 63)) >= t;
+        const uint64_t bal = __ballot(in);
+        if (!bal) continue;
+        const uint32_t first = __ffsll((unsigned long long)bal) - 1;
+        uint32_t base = 0;
+        if (lane == first) base = atomicAdd(&tk->n_cand, (uint32_t)__popcll(bal));
+        base = __shfl(base, first, 64);
+        if (in) {
+            const uint32_t pos = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+            if (pos < WT_CAND) {
+                tk->cand_key[pos] = key;
+                tk->cand_idx[pos] = sorted_idx[i];
+            }
+        }
+    }
+}
+
+// one block: rank the candidates by counting and write the top k (past WT_CAND candidates: select them one rank at
+// a time over every seed: exact, slow); resets the candidate counter
+constexpr uint32_t WT_SEL_THREADS = 512;
+__global__ __launch_bounds__(WT_SEL_THREADS) void k_wt_topk_select(const uint64_t *__restrict__ sums,
+                                                                   const uint32_t *__restrict__ sorted_idx, uint64_t S,
+                                                                   uint64_t seed0, uint32_t k, uint32_t n_groups,
+                                                                   WtTopkState *__restrict__ tk,
+                                                                   nmz_topk_entry *__restrict__ out) {
+    constexpr uint32_t NT = WT_SEL_THREADS, NW = NT / 64;
+    __shared__ unsigned long long ck[WT_CAND], cs[WT_CAND], g[WT_MAX_GROUPS];
+    __shared__ unsigned long long bk[NW], bs[NW], tau2;
+    __shared__ uint32_t c2;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t c = tk->n_cand;
+    auto sentinel = [] {
+        nmz_topk_entry e;
+        e.seed = UINT64_MAX;
+        e.sum_delay_ns = INT64_MIN;
+        e.n_fault = 0;
+        e.first_fault = NMZ_NONE;
+        return e;
+    };
+    if (c <= WT_CAND) {
+        // the exact k-th largest group key (the scan's subset bound is looser): keep the candidates at or above it
+        // (every seed at or above it is a candidate, since the subset bound is at most it), ~k of them
+        const uint32_t n = n_groups;
+        for (uint32_t i = threadIdx.x; i < n; i += NT) g[i] = tk->gmax[i];
+        if (threadIdx.x == 0) {
+            tau2 = 0;
+            c2 = 0;
+        }
+        __syncthreads();
+        if (n >= k)
+            for (uint32_t i = threadIdx.x; i < n; i += NT) {
+                const unsigned long long x = g[i];
+                uint32_t gt = 0, eq = 0;
+                for (uint32_t j = 0; j < n; ++j) {
+                    gt += g[j] > x;
+                    eq += g[j] == x;
+                }
+                if (gt < k && k <= gt + eq) tau2 = x;  // every writer writes the same value
+            }
+        __syncthreads();
+        const unsigned long long t2 = tau2;
+        for (uint32_t i = threadIdx.x; i < c; i += NT) {
+            const unsigned long long key = tk->cand_key[i];
+            if (key >= t2) {
+                const uint32_t pos = atomicAdd(&c2, 1u);
+                ck[pos] = key;
+                cs[pos] = seed0 + tk->cand_idx[i];  // seeds wrap as elsewhere
+            }
+        }
+        __syncthreads();
+        const uint32_t cc = c2;
+        for (uint32_t i = threadIdx.x; i < cc; i += NT) {
+            const unsigned long long a = ck[i], sa = cs[i];
+            uint32_t r = 0;
+            for (uint32_t j = 0; j < cc; ++j) r += wt_better(ck[j], cs[j], a, sa);
+            if (r < k) {
+                nmz_topk_entry e;
+                e.seed = sa;
+                e.sum_delay_ns = (int64_t)(a ^ (1ull << 63));
+                e.n_fault = 0;
+                e.first_fault = NMZ_NONE;
+                out[r] = e;
+            }
+        }
+        for (uint32_t r = cc + threadIdx.x; r < k; r += NT) out[r] = sentinel();  // fewer seeds than k
+    } else {
+        // exact selection one rank at a time: the best entry after the previous one in (key desc, seed asc)
+        unsigned long long pk = ~0ull, ps = 0;
+        bool first_rank = true;
+        for (uint32_t r = 0; r < k; ++r) {
+            unsigned long long mk = 0, ms = ~0ull;
+            bool any = false;
+            for (uint64_t i = threadIdx.x; i < S; i += NT) {
+                const unsigned long long key = sums[i] ^ (1ull << 63), sd = seed0 + sorted_idx[i];
+                const bool after = first_rank || wt_better(pk, ps, key, sd);
+                if (after && (!any || wt_better(key, sd, mk, ms))) {
+                    mk = key;
+                    ms = sd;
+                    any = true;
+                }
+            }
+            if (!any) mk = 0, ms = ~0ull;
+            for (int o = 32; o; o >>= 1) {
+                const unsigned long long ok = __shfl_xor(mk, o, 64), os = __shfl_xor(ms, o, 64);
+                const bool oany = __shfl_xor((int)any, o, 64);
+                if (oany && (!any || wt_better(ok, os, mk, ms))) {
+                    mk = ok;
+                    ms = os;
+                    any = true;
+                }
+            }
+            __syncthreads();
+            if (lane == 0) {
+                bk[threadIdx.x >> 6] = any ? mk : 0;
+                bs[threadIdx.x >> 6] = any ? ms : ~0ull;
+                if (!any) bs[threadIdx.x >> 6] = ~0ull, bk[threadIdx.x >> 6] = 0;
+            }
+            __syncthreads();
+            // the block's best (empty slots hold key 0, seed ~0: never better than a real entry of key 0 with a
+            // smaller seed; a real entry of key 0 and seed ~0 is found by the any flags below)
+            unsigned long long bestk = 0, bests = ~0ull;
+            bool found = false;
+            for (uint32_t w = 0; w < NW; ++w) {
+                const bool real = !(bk[w] == 0 && bs[w] == ~0ull);
+                if (real && (!found || wt_better(bk[w], bs[w], bestk, bests))) {
+                    bestk = bk[w];
+                    bests = bs[w];
+                    found = true;
+                }
+            }
+            if (!found) {
+                for (uint32_t q = r + threadIdx.x; q < k; q += NT) out[q] = sentinel();
+                break;
+            }
+            if (threadIdx.x == 0) {
+                nmz_topk_entry e;
+                e.seed = bests;
+                e.sum_delay_ns = (int64_t)(bestk ^ (1ull << 63));
+                e.n_fault = 0;
+                e.first_fault = NMZ_NONE;
+                out[r] = e;
+            }
+            pk = bestk;
+            ps = bests;
+            first_rank = false;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) tk->n_cand = 0;
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -550,20 +788,32 @@ static uint32_t wt_threads() {
 constexpr size_t WT_BUILD_LDS =
     WT_NMAX * 8 + WT_NMAX * 4 + 2 * WT_NMAX * 2 + 2 * (WT_NMAX / 32 + 4) * 4 + 16 * 8 + 16 + WT_NMAX * 8;
 
-int wt_build(WtState &w, const uint4 *d_table, uint32_t E, const ClassInfo *cls, uint32_t n_cls,
+int wt_build(WtState &w, nmz_ctx *ctx, const uint4 *d_table, uint32_t E, const ClassInfo *cls, uint32_t n_cls,
              const ModParams &mod, hipStream_t st) {
     w.on = false;
     if (!wt_enabled() || !mod.m32ok || E == 0 || E > 65536) return NMZ_OK;
     auto r16 = [](uint64_t b) { return (b + 15) & ~15ull; };
+    // segments: a class of 4,096 events or more (the plan kernel sorts < 4,096 keys in LDS) splits into near-equal
+    // C-sorted sub-segments, each one a segment in its own right (every decision of it is (base + Cm) mod m with
+    // the same carry rule C > ~H, just over fewer events)
+    std::vector<ClassInfo> seg;
+    for (uint32_t c = 0; c < n_cls; ++c) {
+        const uint32_t n = cls[c].count, parts = (n + WT_NMAX - 2) / (WT_NMAX - 1);
+        for (uint32_t k = 0, lo = 0; k < parts; ++k) {
+            const uint32_t len = n / parts + (k < n % parts ? 1u : 0u);
+            seg.push_back(ClassInfo{cls[c].pn, cls[c].start + lo, len});
+            lo += len;
+        }
+    }
+    n_cls = (uint32_t)seg.size();
     std::vector<WtClass> oc(n_cls);
     uint64_t off = 0;
     for (uint32_t c = 0; c < n_cls; ++c) {
         WtClass &o = oc[c];
         o = WtClass{};
-        o.pn = cls[c].pn;
-        o.start = cls[c].start;
-        o.n = cls[c].count;
-        if (o.n >= WT_NMAX) return NMZ_OK;  // keep the order-query sweep (pm and the sort take n < 4,096)
+        o.pn = seg[c].pn;
+        o.start = seg[c].start;
+        o.n = seg[c].count;
         if (o.n <= WT_BRUTE) continue;
         o.K = bitlen(o.n);  // 2^K > n >= every bound R
         o.nw = o.n / 32 + 1;
@@ -587,11 +837,17 @@ int wt_build(WtState &w, const uint4 *d_table, uint32_t E, const ClassInfo *cls,
     w.rb16 = (uint32_t)(rb / 16);
     w.n_classes = n_cls;
     w.msh = mod.m32 > 255 ? bitlen(mod.m32) - 8 : 0;
-    for (const void *f : {reinterpret_cast<const void *>(k_replayable_sweep_wt<false>),
-                          reinterpret_cast<const void *>(k_replayable_sweep_wt<true>),
-                          reinterpret_cast<const void *>(k_replayable_wt_build)})
-        if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WT_LDS_MAX) != hipSuccess)
-            return NMZ_OK;
+    // function attributes are per device: once per context (a context owns one device; its calls are serialised)
+    if (!ctx->wt_lds_attr) {
+        for (const void *f : {reinterpret_cast<const void *>(k_replayable_sweep_wt<false>),
+                              reinterpret_cast<const void *>(k_replayable_sweep_wt<true>),
+                              reinterpret_cast<const void *>(k_replayable_wt_build)})
+            if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WT_LDS_MAX) != hipSuccess) {
+                (void)hipGetLastError();  // not sticky for the launches that follow: keep the order-query sweep
+                return NMZ_OK;
+            }
+        ctx->wt_lds_attr = true;
+    }
     const size_t need = Carve::bytes_for(256 * (size_t)w.rb16, 16) + Carve::bytes_for(256, 8) +
                         Carve::bytes_for(n_cls, sizeof(WtClass));
     NMZ_TRY(w.mem.ensure(need));
@@ -610,15 +866,49 @@ int wt_build(WtState &w, const uint4 *d_table, uint32_t E, const ClassInfo *cls,
     return NMZ_OK;
 }
 
+size_t wt_topk_scratch_bytes(uint64_t S) {
+    return Carve::bytes_for(1, sizeof(WtTopkState)) + Carve::bytes_for(S, 8);
+}
+
+int wt_topk_reset(hipStream_t st, void *scratch) {
+    NMZ_HIP(hipMemsetAsync(scratch, 0, sizeof(WtTopkState), st));
+    return NMZ_OK;
+}
+
+// the selection after a sweep that ran with this scratch (its per-seed sums and per-workgroup largest sums)
+int wt_topk(hipStream_t st, void *scratch, const uint32_t *sorted_idx, uint64_t S, uint64_t seed0, uint32_t k,
+            nmz_topk_entry *d_out) {
+    NMZ_CHECK(k >= 1 && k <= 64, "internal: wt_topk takes 1 <= k <= 64");
+    Carve cv(scratch);
+    WtTopkState *tk = cv.take<WtTopkState>(1);
+    const uint64_t *sums = cv.take<uint64_t>(S);
+    const unsigned blocks = (unsigned)std::min<uint64_t>(ceil_div(S, 256), 256);
+    hipLaunchKernelGGL(k_wt_topk_scan, dim3(blocks), dim3(256), 0, st, sums, sorted_idx, S, 256 * wt_groups(), k, tk);
+    hipLaunchKernelGGL(k_wt_topk_select, dim3(1), dim3(WT_SEL_THREADS), 0, st, sums, sorted_idx, S, seed0, k,
+                       256 * wt_groups(), tk, d_out);
+    NMZ_HIP(hipGetLastError());
+    return NMZ_OK;
+}
+
+// topk_scratch (wt_topk_scratch_bytes(S)) or nullptr: the sweep also leaves per-seed sums and per-workgroup largest
+// sums there for wt_topk
 int wt_sweep(const WtState &w, nmz_ctx *ctx, hipStream_t st, const Buckets &b, const uint4 *d_table, uint32_t E,
-             const ModParams &mod, nmz_sched_stats *d_stats) {
+             const ModParams &mod, nmz_sched_stats *d_stats, uint64_t S, void *topk_scratch, uint32_t k) {
+    WtTopkState *tk = nullptr;
+    uint64_t *sums = nullptr;
+    if (topk_scratch) {
+        Carve cv(topk_scratch);
+        tk = cv.take<WtTopkState>(1);
+        sums = cv.take<uint64_t>(S);
+    }
     const uint32_t G = wt_groups(), nt = wt_threads();
     KernelTimer kt(ctx, st, "replayable_sweep");
     unsigned long long *span = kt.span();
     auto kern = mod.m32 >= 0x80000000u ? k_replayable_sweep_wt<true> : k_replayable_sweep_wt<false>;
-    hipLaunchKernelGGL(kern, dim3(256 * G), dim3(nt), w.rb16 * 16u + 16u, st, b.offset, b.sorted_h0, b.sorted_idx,
+    const size_t lds = w.rb16 * 16u + 16u;
+    hipLaunchKernelGGL(kern, dim3(256 * G), dim3(nt), lds, st, b.offset, b.sorted_h0, b.sorted_idx,
                        d_table, E, w.d_blob, w.rb16, w.d_rowsum, static_cast<const WtClass *>(w.d_classes),
-                       w.n_classes, mod.m32, mod.mu, mod.m_k64, w.msh, G, d_stats, span);
+                       w.n_classes, mod.m32, mod.mu, mod.m_k64, w.msh, G, d_stats, span, sums, tk, k);
     NMZ_HIP(hipGetLastError());
     return NMZ_OK;
 }

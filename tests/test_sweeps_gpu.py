@@ -38,8 +38,8 @@ def k1(request, monkeypatch):
 
 
 def test_replayable_plan_kernel_choice(ctx, monkeypatch):
-    """configs[1]-shaped traces take the wavelet-tree kernel; NMZ_REPLAY_WT=0 the order-query kernel; classes
-    beyond 4,096 events the order-query kernel; maxInterval >= 2^32 the per-decision sweep."""
+    """configs[1]-shaped traces take the wavelet-tree kernel (classes of 4,096 events or more as sub-segments);
+    NMZ_REPLAY_WT=0 or a row image beyond LDS the order-query kernel; maxInterval >= 2^32 the per-decision sweep."""
     L = _lib.load()
 
     def kind(hints, m):
@@ -57,7 +57,8 @@ def test_replayable_plan_kernel_choice(ctx, monkeypatch):
     assert kind(hints, 100_000_000) == 2
     assert kind(hints, 2**32 - 1) == 2
     assert kind(hints, 2**32) == 0
-    assert kind(["x" * 5] * 4097, 100_000_000) == 1
+    assert kind(["x" * 5] * 4097, 100_000_000) == 2  # one class of 4,097: two wavelet-tree sub-segments
+    assert kind(zk_hints(12_000), 100_000_000) == 1  # row image beyond LDS: order-query passes
     monkeypatch.setenv("NMZ_REPLAY_WT", "0")
     assert kind(hints, 100_000_000) == 1
 
@@ -147,6 +148,31 @@ def test_replayable_event_counts_around_stage_and_chunk_edges(ctx, k1, E):
     r = p.Sweep(seeds, hints, n_dump=3, ctx=ctx)
     st, dl = rep_oracle(seeds, hints, 100_000_000, n_dump=3)
     assert np.array_equal(r.stats, st) and np.array_equal(r.delays, dl)
+
+
+@pytest.mark.parametrize("m", [100_000_000, 7, 2**31 + 3])
+def test_replayable_one_long_class_sub_segments(ctx, monkeypatch, m):
+    """4,500 hints of one length (one class of 4,500 >= 4,096 events: two wavelet-tree sub-segments of the C-sorted
+    class, each with its own carry split and statistics) plus a few short hints, tiny modulus for ties, vs the
+    oracle; the plan must take the wavelet-tree kernel."""
+    monkeypatch.delenv("NMZ_REPLAY_WT", raising=False)
+    rng = np.random.default_rng(m % 1000)
+    hints = [str(x) for x in rng.integers(10**9, 10**10, size=4500)] + ["ab", "abc", "q"] * 3
+    hints = [hints[i] for i in rng.permutation(len(hints))]
+    seeds = [str(i) for i in range(400)] + ["foobar"]
+    L = _lib.load()
+    ho, hb = to_csr(hints)
+    plan = ctypes.c_void_p()
+    _lib.check(L.nmz_replayable_plan_create(ctx.handle, _lib.ptr(ho), _lib.ptr(hb), len(hints), m, 512,
+                                            ctypes.byref(plan)))
+    assert L.nmz_replayable_plan_kernel(plan) == 2
+    L.nmz_replayable_plan_destroy(plan)
+    p = Replayable()
+    p.MaxInterval = m
+    r = p.Sweep(seeds, hints, n_dump=2, k=8, ctx=ctx)
+    st, dl = rep_oracle(seeds, hints, m, n_dump=2)
+    assert np.array_equal(r.stats, st) and np.array_equal(r.delays, dl)
+    assert np.array_equal(r.topk, O.topk_from_stats(st, 0, 8))
 
 
 @pytest.mark.parametrize("E,m", [(10_000, 100_000_000), (10_000, 2_000_000_000), (6_500, 2**32 - 1)])
@@ -286,10 +312,16 @@ def test_replayable_device_plan_api(ctx):
     (3_000_000_000, 2500, 50, 32, 5),         # MOD_GENERAL: separate selection
     (0, 700, 20, 8, 0),                       # maxInterval 0: constant stats, all ties
     (1_000_000, 0, 20, 8, 0),                 # no seeds: sentinels
+    # wavelet-tree sweeps with their own top-k candidates (k <= 64, > 2,048 seeds):
+    (100_000_000, 9000, 120, 64, 2**64 - 4000),  # candidates above the k-th workgroup maximum; seeds wrap
+    (7, 6000, 100, 33, 3),                    # sums 0..600: heavy ties, candidates overflow -> gated selection
+    (1, 5000, 40, 16, 11),                    # maxInterval 1: every sum 0, every seed a candidate -> gated
+    (2**31 + 3, 4000, 60, 1, 0),              # k = 1, m >= 2^31
 ])
 def test_replayable_sweep_topk_dev_matches_separate_selection(ctx, m, S, E, k, seed0):
-    """nmz_replayable_sweep_topk_dev (merge + first top-k level fused) == sweep_dev + topk_select_dev
-    == oracle."""
+    """nmz_replayable_sweep_topk_dev (its own top-k path per kernel: on the wavelet-tree path the candidates above
+    the k-th workgroup maximum, ranked by counting, or the gated general selection when they overflow) == the
+    oracle's top-k of the oracle's stats."""
     import torch
     L = _lib.load()
     hints = zk_hints(E)
