@@ -577,15 +577,24 @@ __device__ __forceinline__ bool wt_better(unsigned long long ka, uint64_t sa, un
 __global__ __launch_bounds__(256) void k_wt_topk_scan(const uint64_t *__restrict__ sums,
                                                       const uint32_t *__restrict__ sorted_idx, uint64_t S, uint32_t n,
                                                       uint32_t k, WtTopkState *__restrict__ tk) {
+    constexpr uint32_t PF = 16;  // sums per thread loaded before they are needed (their latency overlaps tau)
     __shared__ unsigned long long g[256];
     __shared__ unsigned long long tau_s;
     const uint32_t m = min(n, 256u);
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    uint64_t v[PF];
+#pragma unroll
+    for (uint32_t r = 0; r < PF; ++r) {
+        const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x + r * stride;
+        v[r] = i < S ? sums[i] : 0ull;
+    }
     if (threadIdx.x < m) g[threadIdx.x] = tk->gmax[threadIdx.x];
     if (threadIdx.x == 0) tau_s = 0;  // fewer groups than k: every seed is a candidate
     __syncthreads();
     if (m >= k && threadIdx.x < m) {
         const unsigned long long x = g[threadIdx.x];
         uint32_t gt = 0, eq = 0;
+#pragma unroll 8
         for (uint32_t j = 0; j < m; ++j) {
             gt += g[j] > x;
             eq += g[j] == x;
@@ -595,21 +604,25 @@ __global__ __launch_bounds__(256) void k_wt_topk_scan(const uint64_t *__restrict
     __syncthreads();
     const unsigned long long t = tau_s;
     const uint32_t lane = threadIdx.x & 63;
-    for (uint64_t i0 = (uint64_t)blockIdx.x * 256; i0 < S; i0 += (uint64_t)gridDim.x * 256) {
-        const uint64_t i = i0 + threadIdx.x;
-        unsigned long long key = 0;
-        const bool in = i < S && (key = sums[i] ^ (1ull << 63)) >= t;
-        const uint64_t bal = __ballot(in);
-        if (!bal) continue;
-        const uint32_t first = __ffsll((unsigned long long)bal) - 1;
-        uint32_t base = 0;
-        if (lane == first) base = atomicAdd(&tk->n_cand, (uint32_t)__popcll(bal));
-        base = __shfl(base, first, 64);
-        if (in) {
-            const uint32_t pos = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
-            if (pos < WT_CAND) {
-                tk->cand_key[pos] = key;
-                tk->cand_idx[pos] = sorted_idx[i];
+    for (uint64_t i0 = (uint64_t)blockIdx.x * 256; i0 < S; i0 += PF * stride) {
+#pragma unroll
+        for (uint32_t r = 0; r < PF; ++r) {
+            const uint64_t i = i0 + threadIdx.x + r * stride;
+            if (i0 != (uint64_t)blockIdx.x * 256) v[r] = i < S ? sums[i] : 0ull;  // past the first PF rounds
+            const unsigned long long key = v[r] ^ (1ull << 63);
+            const bool in = i < S && key >= t;
+            const uint64_t bal = __ballot(in);
+            if (!bal) continue;
+            const uint32_t first = __ffsll((unsigned long long)bal) - 1;
+            uint32_t base = 0;
+            if (lane == first) base = atomicAdd(&tk->n_cand, (uint32_t)__popcll(bal));
+            base = __shfl(base, first, 64);
+            if (in) {
+                const uint32_t pos = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+                if (pos < WT_CAND) {
+                    tk->cand_key[pos] = key;
+                    tk->cand_idx[pos] = sorted_idx[i];
+                }
             }
         }
     }
@@ -651,6 +664,7 @@ __global__ __launch_bounds__(WT_SEL_THREADS) void k_wt_topk_select(const uint64_
             for (uint32_t i = threadIdx.x; i < n; i += NT) {
                 const unsigned long long x = g[i];
                 uint32_t gt = 0, eq = 0;
+#pragma unroll 8
                 for (uint32_t j = 0; j < n; ++j) {
                     gt += g[j] > x;
                     eq += g[j] == x;
@@ -767,12 +781,15 @@ bool wt_enabled() {
     return !(e && std::string(e) == "0");
 }
 
-// workgroups per row and threads per workgroup (A/B knobs NMZ_WT_G = 1|2|4, NMZ_WT_THREADS = 256..1024)
+// workgroups per row and threads per workgroup (A/B knobs NMZ_WT_G = 1|2|4|8, NMZ_WT_THREADS = 64..1024)
 static uint32_t wt_groups() {
     static const uint32_t g = [] {
+        // one workgroup per row leaves half of each CU's wave slots and LDS to the step's other kernels (the seed
+        // prefix, bucketing and top-k of the neighbouring pipelined steps): configs[1] step 0.116 -> 0.113 ms with
+        // the fused top-k (profiles/r03y_wt_groups_ab.json); alone, 2 per row are 2 % faster
         const char *e = getenv("NMZ_WT_G");
-        const int v = e ? atoi(e) : 2;
-        return (uint32_t)((v == 1 || v == 2 || v == 4 || v == 8) ? v : 2);
+        const int v = e ? atoi(e) : 1;
+        return (uint32_t)((v == 1 || v == 2 || v == 4 || v == 8) ? v : 1);
     }();
     return g;
 }
