@@ -55,33 +55,37 @@ static_assert(sizeof(WtClass) == 56, "WtClass layout");
 // prefix pi starts at pi << (K-l), since the ranks are a permutation of [0, n)), one {32 bits, ones before} pair
 // per 32 positions. Also adds the segment's sum of Cm to the row sum (every segment, short ones included).
 // ---------------------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_replayable_wt_build(const uint4 *__restrict__ table, uint32_t E,
-                                                              WtClass *__restrict__ classes, uint32_t msh, uint32_t mbits,
-                                                              uint4 *__restrict__ blob, uint32_t rb16,
-                                                              unsigned long long *__restrict__ rowsum) {
+constexpr uint32_t WT_BT = 512, WT_BW = WT_BT / 64;  // plan kernel: threads and waves per workgroup
+__global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__restrict__ table, uint32_t E,
+                                                               WtClass *__restrict__ classes, uint32_t msh,
+                                                               uint32_t mbits, uint4 *__restrict__ blob, uint32_t rb16,
+                                                               unsigned long long *__restrict__ rowsum) {
+    // LDS (~73 KB, two workgroups per CU): the keys, then (after the sort) the rank arrays in their place; the
+    // sorted keys; bucket counts (np / 2 buckets); level words and counts; small scratch
     extern __shared__ uint4 wt_build_lds[];
     uint64_t *key = reinterpret_cast<uint64_t *>(wt_build_lds);                 // [WT_NMAX]
-    uint32_t *chi = reinterpret_cast<uint32_t *>(key + WT_NMAX);               // [WT_NMAX]
-    uint16_t *S0 = reinterpret_cast<uint16_t *>(chi + WT_NMAX);                // [2][WT_NMAX]
-    uint32_t *wb = reinterpret_cast<uint32_t *>(S0 + 2 * WT_NMAX);             // [WT_NMAX / 32 + 1]
-    uint32_t *cum = wb + WT_NMAX / 32 + 4;                                     // [WT_NMAX / 32 + 1]
-    unsigned long long *part = reinterpret_cast<unsigned long long *>(cum + WT_NMAX / 32 + 4);  // [16]
-    uint32_t *bmax = reinterpret_cast<uint32_t *>(part + 16);                  // [4]
-    uint64_t *tmp = reinterpret_cast<uint64_t *>(bmax + 4);                    // [WT_NMAX] sorted keys
+    uint16_t *S0 = reinterpret_cast<uint16_t *>(key);                           // [2][WT_NMAX], after the sort
+    uint64_t *srt = key + WT_NMAX;                                              // [WT_NMAX] sorted keys
+    uint32_t *bc = reinterpret_cast<uint32_t *>(srt + WT_NMAX);                 // [WT_NMAX / 2]
+    uint32_t *wb = bc + WT_NMAX / 2;                                            // [WT_NMAX / 32 + 4]
+    uint32_t *cum = wb + WT_NMAX / 32 + 4;                                      // [WT_NMAX / 32 + 4]
+    uint32_t *idx = cum + WT_NMAX / 32 + 4;                                     // [2][260] bucket indexes
+    unsigned long long *part = reinterpret_cast<unsigned long long *>(idx + 520);  // [WT_BW]
+    uint32_t *bmax = reinterpret_cast<uint32_t *>(part + WT_BW);               // [4]
     const uint32_t c = blockIdx.x, L = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const WtClass ci = classes[c];
     const uint32_t n = ci.n;
     const uint4 *__restrict__ row = table + (uint64_t)L * E + ci.start;
     char *img = reinterpret_cast<char *>(blob + (uint64_t)L * rb16);
     uint64_t s = 0;
-    for (uint32_t i = tid; i < n; i += 1024) s += row[i].z;
+    for (uint32_t i = tid; i < n; i += WT_BT) s += row[i].z;
     for (int o = 32; o; o >>= 1) s += __shfl_xor(s, o, 64);
     if (lane == 0) part[wave] = s;
     if (tid < 4) bmax[tid] = 0;
     __syncthreads();
     if (tid == 0) {
         unsigned long long t = 0;
-        for (int w = 0; w < 16; ++w) t += part[w];
+        for (uint32_t w = 0; w < WT_BW; ++w) t += part[w];
         atomicAdd(rowsum + L, t);
     }
     if (n <= WT_BRUTE) return;
@@ -90,29 +94,29 @@ __global__ __launch_bounds__(1024) void k_replayable_wt_build(const uint4 *__res
         np <<= 1;
         ++lgp;
     }
-    for (uint32_t i = tid; i < n; i += 1024) {
+    uint32_t *chi_img = reinterpret_cast<uint32_t *>(img + ci.o_chi);
+    for (uint32_t i = tid; i < n; i += WT_BT) {
         const uint4 q = row[i];
-        chi[i] = q.y;
+        chi_img[i] = q.y;
         const uint32_t e = ~q.w;  // < 65536 (the host checks E)
         key[i] = ((uint64_t)q.z << 32) | ((uint64_t)(0xffffu - e) << 16) | i;
     }
-    // sort the keys: counting sort on the top lg(np) bits of Cm (uniform in [0, m): ~1 key per bucket), then an
+    // sort the keys: counting sort on the top lg(np) - 1 bits of Cm (uniform in [0, m): ~2 keys per bucket), then an
     // insertion sort per bucket (a thread per bucket); a bucket of more than 32 keys (repeated hints: equal Cm)
     // sends the whole segment to a bitonic sort
     {
-        uint32_t *bc = reinterpret_cast<uint32_t *>(S0);  // [np] bucket counts, then bucket ends
-        const uint32_t sh = mbits > lgp ? mbits - lgp : 0u;
-        for (uint32_t b = tid; b < np; b += 1024) bc[b] = 0;
-        if (tid == 0) bmax[0] = 0;
+        const uint32_t nb = np >= 2 ? np / 2 : 1, lgb = lgp ? lgp - 1 : 0;
+        const uint32_t sh = mbits > lgb ? mbits - lgb : 0u;
+        for (uint32_t b = tid; b < nb; b += WT_BT) bc[b] = 0;
         __syncthreads();
-        for (uint32_t i = tid; i < n; i += 1024) atomicAdd(&bc[(uint32_t)(key[i] >> 32) >> sh], 1u);
+        for (uint32_t i = tid; i < n; i += WT_BT) atomicAdd(&bc[(uint32_t)(key[i] >> 32) >> sh], 1u);
         __syncthreads();
-        {  // exclusive scan over np <= 4096 counts: 4 per thread, wave scans, then the 16 wave totals
+        {  // exclusive scan over nb <= 2,048 counts: 4 per thread, wave scans, then the wave totals
             const uint32_t b0 = 4 * tid;
             uint32_t c4[4], t = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                c4[k] = b0 + k < np ? bc[b0 + k] : 0u;
+                c4[k] = b0 + k < nb ? bc[b0 + k] : 0u;
                 t += c4[k];
                 if (c4[k] > 32) atomicMax(bmax, c4[k]);
             }
@@ -127,38 +131,35 @@ __global__ __launch_bounds__(1024) void k_replayable_wt_build(const uint4 *__res
             for (uint32_t w = 0; w < wave; ++w) base += cum[w];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                if (b0 + k < np) bc[b0 + k] = base;  // bucket start (a cursor while scattering, then the end)
+                if (b0 + k < nb) bc[b0 + k] = base;  // bucket start (a cursor while scattering, then the end)
                 base += c4[k];
             }
         }
         __syncthreads();
-        const bool bitonic = bmax[0] > 32;
-        if (!bitonic) {
-            for (uint32_t i = tid; i < n; i += 1024) {
+        if (bmax[0] <= 32) {
+            for (uint32_t i = tid; i < n; i += WT_BT) {
                 const uint64_t kk = key[i];
-                tmp[atomicAdd(&bc[(uint32_t)(kk >> 32) >> sh], 1u)] = kk;
+                srt[atomicAdd(&bc[(uint32_t)(kk >> 32) >> sh], 1u)] = kk;
             }
             __syncthreads();
-            for (uint32_t b = tid; b < np; b += 1024) {  // bucket b: [end of b - 1, end of b)
+            for (uint32_t b = tid; b < nb; b += WT_BT) {  // bucket b: [end of b - 1, end of b)
                 const uint32_t lo = b ? bc[b - 1] : 0u, hi = bc[b];
                 for (uint32_t i = lo + 1; i < hi; ++i) {
-                    const uint64_t v = tmp[i];
+                    const uint64_t v = srt[i];
                     uint32_t j = i;
-                    while (j > lo && tmp[j - 1] > v) {
-                        tmp[j] = tmp[j - 1];
+                    while (j > lo && srt[j - 1] > v) {
+                        srt[j] = srt[j - 1];
                         --j;
                     }
-                    tmp[j] = v;
+                    srt[j] = v;
                 }
             }
-            __syncthreads();
-            key = tmp;
         } else {
-            for (uint32_t i = n + tid; i < np; i += 1024) key[i] = ~0ull;
+            for (uint32_t i = n + tid; i < np; i += WT_BT) key[i] = ~0ull;
             for (uint32_t k = 2; k <= np; k <<= 1)
                 for (uint32_t j = k >> 1; j; j >>= 1) {
                     __syncthreads();
-                    for (uint32_t i = tid; i < np; i += 1024) {
+                    for (uint32_t i = tid; i < np; i += WT_BT) {
                         const uint32_t l = i ^ j;
                         if (l > i) {
                             const uint64_t a = key[i], b = key[l];
@@ -170,66 +171,60 @@ __global__ __launch_bounds__(1024) void k_replayable_wt_build(const uint4 *__res
                     }
                 }
             __syncthreads();
+            for (uint32_t i = tid; i < n; i += WT_BT) srt[i] = key[i];
         }
+        __syncthreads();  // the keys' region becomes the rank arrays
     }
     uint32_t *cm_img = reinterpret_cast<uint32_t *>(img + ci.o_cm);
-    uint32_t *chi_img = reinterpret_cast<uint32_t *>(img + ci.o_chi);
     uint16_t *e_img = reinterpret_cast<uint16_t *>(img + ci.o_e);
-    for (uint32_t j = tid; j < n; j += 1024) {
-        const uint64_t kk = key[j];
+    for (uint32_t j = tid; j < n; j += WT_BT) {
+        const uint64_t kk = srt[j];
         cm_img[j] = (uint32_t)(kk >> 32);
         e_img[j] = (uint16_t)(0xffffu - ((kk >> 16) & 0xffffu));
         S0[kk & 0xffffu] = (uint16_t)j;
-        chi_img[j] = chi[j];
     }
     if (tid == 0) {
         cm_img[n] = ~0u;  // sentinels: never below a search bound
         chi_img[n] = ~0u;
     }
-    // bucket indexes and their largest bucket (the kernel's lifting searches take bitlen(largest) rounds)
+    // bucket indexes (first rank with Cm >= b << msh, b <= 256; first position with C_hi >= b << 24, b < 256): every
+    // position writes the buckets between its predecessor's and its own (the sorted order's boundaries)
+    uint32_t *im = idx, *ic = idx + 260;
+    for (uint32_t i = tid; i <= n; i += WT_BT) {
+        const int bm = i < n ? (int)((uint32_t)(srt[i] >> 32) >> msh) : 257;
+        const int pm_ = i ? (int)((uint32_t)(srt[i - 1] >> 32) >> msh) : -1;
+        for (int b = pm_ + 1; b <= min(bm, 256); ++b) im[b] = i;
+        const int bc2 = i < n ? (int)(row[i].y >> 24) : 256;
+        const int pc = i ? (int)(row[i - 1].y >> 24) : -1;
+        for (int b = pc + 1; b <= min(bc2, 255); ++b) ic[b] = i;
+    }
+    __syncthreads();
     if (tid < 257) {
-        auto lb = [&](uint64_t x) {  // first rank with Cm >= x
-            uint32_t lo = 0, hi = n;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if ((key[mid] >> 32) < x) lo = mid + 1; else hi = mid;
-            }
-            return lo;
-        };
-        const uint32_t a = lb((uint64_t)tid << msh), b = tid < 256 ? lb((uint64_t)(tid + 1) << msh) : n;
-        reinterpret_cast<uint16_t *>(img + ci.o_im)[tid] = (uint16_t)a;
-        atomicMax(bmax + 2, b - a);
-    } else if (tid >= 320 && tid < 320 + 256) {
-        const uint32_t bk = tid - 320;
-        auto lb = [&](uint64_t x) {  // first position with C_hi >= x
-            uint32_t lo = 0, hi = n;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (chi[mid] < x) lo = mid + 1; else hi = mid;
-            }
-            return lo;
-        };
-        const uint32_t a = lb((uint64_t)bk << 24), b = lb((uint64_t)(bk + 1) << 24);
-        reinterpret_cast<uint16_t *>(img + ci.o_ic)[bk] = (uint16_t)a;
-        atomicMax(bmax + 3, b - a);
+        reinterpret_cast<uint16_t *>(img + ci.o_im)[tid] = (uint16_t)im[tid];
+        atomicMax(bmax + 2, (tid < 256 ? im[tid + 1] : n) - im[tid]);
+    }
+    if (tid < 256) {
+        reinterpret_cast<uint16_t *>(img + ci.o_ic)[tid] = (uint16_t)ic[tid];
+        atomicMax(bmax + 3, (tid < 255 ? ic[tid + 1] : n) - ic[tid]);
     }
     __syncthreads();
     if (tid == 0) atomicMax(&classes[c].rS, 32u - __clz(max(bmax[2], bmax[3])));
     // prefix / suffix maxima of the ranks: pm[d] = {max rank at positions < d, max rank at positions >= d};
-    // 4 positions per thread, wave scans (up for the prefix, down for the suffix), then the 16 wave totals
+    // PP positions per thread, wave scans (up for the prefix, down for the suffix), then the wave totals
     {
-        const uint32_t j0 = 4 * tid;
-        uint32_t v[4], pre[4], suf[4];
+        constexpr uint32_t PP = WT_NMAX / WT_BT;
+        const uint32_t j0 = PP * tid;
+        uint32_t v[PP], pre[PP], suf[PP];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = j0 + k < n ? (uint32_t)S0[j0 + k] : 0u;
+        for (uint32_t k = 0; k < PP; ++k) v[k] = j0 + k < n ? (uint32_t)S0[j0 + k] : 0u;
         pre[0] = v[0];
-        suf[3] = v[3];
+        suf[PP - 1] = v[PP - 1];
 #pragma unroll
-        for (int k = 1; k < 4; ++k) {
+        for (uint32_t k = 1; k < PP; ++k) {
             pre[k] = max(pre[k - 1], v[k]);
-            suf[3 - k] = max(suf[4 - k], v[3 - k]);
+            suf[PP - 1 - k] = max(suf[PP - k], v[PP - 1 - k]);
         }
-        uint32_t up = pre[3], dn = suf[0], exu = 0, exd = 0;
+        uint32_t up = pre[PP - 1], dn = suf[0], exu = 0, exd = 0;
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t a = __shfl_up(up, o, 64), b = __shfl_down(dn, o, 64);
             if (lane >= (uint32_t)o) {
@@ -244,18 +239,18 @@ __global__ __launch_bounds__(1024) void k_replayable_wt_build(const uint4 *__res
         if (lane == 63) wb[wave] = up;
         if (lane == 0) wb[16 + wave] = dn;
         __syncthreads();
-        for (uint32_t w = 0; w < 16; ++w) {
+        for (uint32_t w = 0; w < WT_BW; ++w) {
             if (w < wave) exu = max(exu, wb[w]);
             if (w > wave) exd = max(exd, wb[16 + w]);
         }
-        uint32_t *pm = reinterpret_cast<uint32_t *>(img + ci.o_pm);
+        uint32_t *pmi = reinterpret_cast<uint32_t *>(img + ci.o_pm);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (uint32_t k = 0; k < PP; ++k) {
             const uint32_t j = j0 + k;
             if (j <= n) {
                 const uint32_t lo = max(exu, k ? pre[k - 1] : 0u);  // positions < j
                 const uint32_t hi = j < n ? max(exd, suf[k]) : 0u;  // positions >= j
-                pm[j] = lo | hi << 16;
+                pmi[j] = lo | hi << 16;
             }
         }
         __syncthreads();  // wb is the level loop's next
@@ -266,7 +261,7 @@ __global__ __launch_bounds__(1024) void k_replayable_wt_build(const uint4 *__res
     uint16_t *cur = S0, *nxt = S0 + WT_NMAX;
     for (uint32_t l = 0; l < K; ++l) {
         const uint32_t k = K - l, h = 1u << (k - 1);
-        for (uint32_t j0 = wave * 64; j0 < nw * 32; j0 += 1024) {
+        for (uint32_t j0 = wave * 64; j0 < nw * 32; j0 += WT_BT) {
             const uint32_t j = j0 + lane;
             const bool bit = j < n && (cur[j] & h);
             const uint64_t bal = __ballot(bit);
@@ -292,8 +287,8 @@ __global__ __launch_bounds__(1024) void k_replayable_wt_build(const uint4 *__res
             if (w0 + 2 < nw) cum[w0 + 2] = ex + c0 + c1;
         }
         __syncthreads();
-        for (uint32_t w = tid; w < nw; w += 1024) lv[l * nw + w] = make_uint2(wb[w], cum[w]);
-        for (uint32_t j = tid; j < n; j += 1024) {
+        for (uint32_t w = tid; w < nw; w += WT_BT) lv[l * nw + w] = make_uint2(wb[w], cum[w]);
+        for (uint32_t j = tid; j < n; j += WT_BT) {
             const uint32_t v = cur[j];
             const uint32_t s0 = v & ~(2 * h - 1);  // the node's first position
             const uint32_t r1 = cum[j >> 5] + __popc(wb[j >> 5] & ((1u << (j & 31)) - 1u)) - (s0 >> 1);
@@ -802,8 +797,8 @@ static uint32_t wt_threads() {
     return t;
 }
 
-constexpr size_t WT_BUILD_LDS =
-    WT_NMAX * 8 + WT_NMAX * 4 + 2 * WT_NMAX * 2 + 2 * (WT_NMAX / 32 + 4) * 4 + 16 * 8 + 16 + WT_NMAX * 8;
+constexpr size_t WT_BUILD_LDS = WT_NMAX * 8 * 2 + WT_NMAX / 2 * 4 + 2 * (WT_NMAX / 32 + 4) * 4 + 520 * 4 +
+                                WT_BW * 8 + 16;
 
 int wt_build(WtState &w, nmz_ctx *ctx, const uint4 *d_table, uint32_t E, const ClassInfo *cls, uint32_t n_cls,
              const ModParams &mod, hipStream_t st) {
@@ -875,7 +870,7 @@ int wt_build(WtState &w, nmz_ctx *ctx, const uint4 *d_table, uint32_t E, const C
     w.d_classes = d_cls;
     NMZ_HIP(hipMemsetAsync(w.d_rowsum, 0, 256 * 8, st));
     NMZ_HIP(hipMemcpyAsync(d_cls, oc.data(), n_cls * sizeof(WtClass), hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_replayable_wt_build, dim3(n_cls, 256), dim3(1024), WT_BUILD_LDS, st, d_table, E, d_cls,
+    hipLaunchKernelGGL(k_replayable_wt_build, dim3(n_cls, 256), dim3(WT_BT), WT_BUILD_LDS, st, d_table, E, d_cls,
                        w.msh, bitlen(mod.m32), w.d_blob, w.rb16, w.d_rowsum);
     NMZ_HIP(hipGetLastError());
     NMZ_HIP(hipStreamSynchronize(st));  // the host vector above is pageable
