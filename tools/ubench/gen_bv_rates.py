@@ -16,6 +16,26 @@ FORMS = [
     ("lshrrev_vs", "v_lshrrev_b32 {d}, %[sg], {d}"),
     ("add_vs", "v_add_u32 {d}, %[sg], {d}"),
     ("lshl_add_u64", "v_lshl_add_u64 {w}, {w}, 0, %[wa]"),
+    # forms of the issue-ceiling mixes (tools/issue_ceiling.py)
+    ("lshrrev_vv", "v_lshrrev_b32 {d}, %[a], {d}"),
+    ("lshrrev_vi", "v_lshrrev_b32 {d}, 3, {d}"),
+    ("xor_vi", "v_xor_b32 {d}, 1, {d}"),
+    ("xor_vv", "v_xor_b32 {d}, %[a], {d}"),
+    ("add3", "v_add3_u32 {d}, {d}, %[a], %[b]"),
+    ("lshl_add_u32", "v_lshl_add_u32 {d}, {d}, 2, %[a]"),
+    ("bfe_vvv", "v_bfe_u32 {d}, {d}, %[a], %[b]"),
+    ("bcnt_vi", "v_bcnt_u32_b32 {d}, {d}, 0"),
+    ("cndmask_vcc", "v_cndmask_b32 {d}, {d}, %[a], vcc"),
+    ("cndmask_e64_s", "v_cndmask_b32_e64 {d}, {d}, %[a], %[sm]"),
+    ("min_u32", "v_min_u32 {d}, {d}, %[a]"),
+    ("mul_hi_u32", "v_mul_hi_u32 {d}, {d}, %[a]"),
+    ("mul_u24", "v_mul_u32_u24 {d}, {d}, %[a]"),
+    ("mad_u64_u32", "v_mad_u64_u32 {w}, vcc, %[a], %[b], {w}"),
+    ("cmp_lt_e32", "v_cmp_lt_u32 vcc, {d}, %[a]"),
+    ("mov_dpp", "v_mov_b32_dpp {d}, {d} row_shr:1"),
+    ("subrev_co", "v_subrev_co_u32 {d}, vcc, {d}, %[a]"),
+    ("mov_vv", "v_mov_b32 {d}, %[a]"),
+    ("bitop3_vvi", "v_bitop3_b32 {d}, {d}, %[a], 5 bitop3:0xf1"),
 ]
 ITERS = 4096
 out = ['#include <hip/hip_runtime.h>', '#include <cstdio>', '#include <cstdint>', f'#define ITERS {ITERS}']
@@ -30,11 +50,12 @@ for n, (name, form) in enumerate(FORMS):
   uint64_t w0=v0, w1=v1, w2=v2, w3=v3, w4=v4, w5=v5, w6=v6, w7=v7, wa=(uint64_t)seed<<20;
   uint32_t a=seed*0x9e37u, b=seed^0x5555u;
   uint32_t sg = __builtin_amdgcn_readfirstlane(seed&31u);
+  uint64_t sm = __builtin_amdgcn_read_exec();
   uint64_t t0 = clock64();
   for (int it = 0; it < ITERS; ++it) {{
     asm volatile("{asm}" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6), "+v"(v7),
                  [w0] "+v"(w0), [w1] "+v"(w1), [w2] "+v"(w2), [w3] "+v"(w3), [w4] "+v"(w4), [w5] "+v"(w5), [w6] "+v"(w6), [w7] "+v"(w7)
-                 : [a] "v"(a), [b] "v"(b), [sg] "s"(sg), [wa] "v"(wa) : "vcc");
+                 : [a] "v"(a), [b] "v"(b), [sg] "s"(sg), [sm] "s"(sm), [wa] "v"(wa) : "vcc");
   }}
   uint64_t t1 = clock64();
   out[blockIdx.x*256+threadIdx.x] = v0^v1^v2^v3^v4^v5^v6^v7^(uint32_t)(w0^w1^w2^w3^w4^w5^w6^w7);
