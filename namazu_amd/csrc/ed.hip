@@ -516,7 +516,7 @@ static int ed_plan_build_bv_device(nmz_ed_plan *p, const uint64_t *off, const ui
         DevBuf &b;
         ~Release() { b.release(); }
     } release_tmp{tmp};
-    NMZ_TRY(tmp.ensure(Carve::bytes_for(d_sym_in ? 0 : total, 8) + Carve::bytes_for(total, 8) +
+    NMZ_TRY(tmp.ensure(Carve::bytes_for(d_sym_in ? 0 : total, 8) + Carve::bytes_for(MAX_FAST_SYMBOLS + 1, 8) +
                        Carve::bytes_for(N + 1, 8)));
     Carve tv(tmp.ptr);
     const uint64_t *d_sym = d_sym_in;
@@ -525,11 +525,11 @@ static int ed_plan_build_bv_device(nmz_ed_plan *p, const uint64_t *off, const ui
         NMZ_HIP(hipMemcpyAsync(d_up, sym, total * 8, hipMemcpyHostToDevice, st));
         d_sym = d_up;
     }
-    uint64_t *d_uniq = tv.take<uint64_t>(total);
+    uint64_t *d_uniq = tv.take<uint64_t>(MAX_FAST_SYMBOLS + 1);
     uint64_t *d_off = tv.take<uint64_t>(N + 1);
     NMZ_HIP(hipMemcpyAsync(d_off, off, (N + 1) * 8, hipMemcpyHostToDevice, st));
     uint64_t n_uniq = 0;
-    NMZ_TRY(device_unique_u64(d_sym, total, d_uniq, &n_uniq, st));
+    NMZ_TRY(device_unique_u64(d_sym, total, d_uniq, MAX_FAST_SYMBOLS, &n_uniq, st));
     const uint32_t bw = ed_bv_template(band);
     const uint32_t KF = (2 * bw + 31) / 32;
     const uint32_t ndw = ((maxlen + 31) / 32 + KF + 2) | 1;

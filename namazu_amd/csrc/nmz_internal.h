@@ -110,7 +110,8 @@ struct EdBvQueryArgs {
 };
 int ed_bv_query_launch(const EdBvQueryArgs &A, uint32_t bw, bool cmp, uint32_t blocks, hipStream_t st);
 // unique.hip: sorted distinct symbols on the device (hipcub radix sort + unique); *n_uniq on the host
-int device_unique_u64(const uint64_t *d_sym, uint64_t total, uint64_t *d_uniq, uint64_t *n_uniq, hipStream_t st);
+int device_unique_u64(const uint64_t *d_sym, uint64_t total, uint64_t *d_uniq, uint64_t cap, uint64_t *n_uniq,
+                      hipStream_t st);
 int ed_bv_launch(const EdBvArgs &A, uint32_t bw, bool cmp, uint64_t blocks, hipStream_t st);
 
 // wide-band bit-parallel edit distance (ed_wide.hip): one pair per wave

@@ -258,35 +258,140 @@ static int classes_launch(nmz_ctx *ctx, const uint64_t *d_sig, uint32_t N, uint3
     return NMZ_OK;
 }
 
-// Sorted distinct values of d_sym[0..total) into d_uniq (capacity total), their count into *n_uniq (host).
-// Scratch: 2 x total x 8 B + hipcub's temporary storage, allocated here and released before returning.
-int device_unique_u64(const uint64_t *d_sym, uint64_t total, uint64_t *d_uniq, uint64_t *n_uniq, hipStream_t st) {
+// Sorted distinct values of d_sym[0..total) (the bit-parallel ED plan's alphabet, ed.hip). A store holds
+// ~10^8 event hashes over at most a few thousand distinct events, so the distinct set comes from hashing, not
+// from sorting the store: each workgroup dedups its grid-stride share in an LDS open-addressing table (a plain
+// read finds a present key, a 64-bit LDS compare-and-swap claims a free slot) and then inserts its distinct keys
+// into one global table; a compaction writes the set out and a radix sort of those few keys orders it. The global
+// table has far more slots than any set the plan accepts (cap < 2^16 distinct, 2^20 slots) and a probe sequence
+// is bounded by the table size, so every insert ends even when the store has millions of distinct values: the
+// count then passes cap and the caller takes its other path.
+constexpr uint32_t DS_LDS_SLOTS = 4096, DS_LDS_MAX = 2048;  // per workgroup (32 KB); fill bound before going global
+constexpr uint32_t DS_G_SLOTS = 1u << 20;                  // global table (8 MB)
+constexpr uint64_t DS_EMPTY = ~0ull;                       // a free slot; the value itself is flagged separately
+
+__device__ __forceinline__ uint32_t ds_hash(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    return (uint32_t)x;
+}
+
+// flags[0] = global distinct count, flags[1] = DS_EMPTY seen
+__device__ __forceinline__ void ds_global_insert(unsigned long long *tab, uint32_t *flags, uint32_t cap, uint64_t x) {
+    uint32_t h = ds_hash(x) & (DS_G_SLOTS - 1);
+    for (uint32_t probe = 0; probe < DS_G_SLOTS; ++probe, h = (h + 1) & (DS_G_SLOTS - 1)) {
+        const uint64_t cur = __hip_atomic_load(&tab[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == x) return;
+        if (cur != DS_EMPTY) continue;
+        if (__hip_atomic_load(&flags[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > cap) return;  // too many: stop
+        const uint64_t old = atomicCAS(&tab[h], (unsigned long long)DS_EMPTY, (unsigned long long)x);
+        if (old == DS_EMPTY) {
+            atomicAdd(&flags[0], 1u);
+            return;
+        }
+        if (old == x) return;
+    }
+    atomicMax(&flags[0], cap + 1);  // table exhausted (only with far more than cap distinct values)
+}
+
+__global__ __launch_bounds__(256) void k_distinct_insert(const uint64_t *__restrict__ sym, uint64_t total,
+                                                         unsigned long long *__restrict__ tab, uint32_t *flags,
+                                                         uint32_t cap) {
+    __shared__ unsigned long long lt[DS_LDS_SLOTS];
+    __shared__ uint32_t lcount;
+    for (uint32_t i = threadIdx.x; i < DS_LDS_SLOTS; i += 256) lt[i] = DS_EMPTY;
+    if (threadIdx.x == 0) lcount = 0;
+    __syncthreads();
+    bool saw_empty = false;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += stride) {
+        const uint64_t x = sym[t];
+        if (x == DS_EMPTY) {
+            saw_empty = true;
+            continue;
+        }
+        uint32_t h = ds_hash(x) & (DS_LDS_SLOTS - 1);
+        bool done = false;
+        for (uint32_t probe = 0; probe < DS_LDS_SLOTS && !done; ++probe, h = (h + 1) & (DS_LDS_SLOTS - 1)) {
+            const uint64_t cur = lt[h];
+            if (cur == x) {
+                done = true;
+            } else if (cur == DS_EMPTY) {
+                if (atomicAdd(&lcount, 0u) >= DS_LDS_MAX) break;  // this workgroup's table is full enough: global
+                const uint64_t old = atomicCAS(&lt[h], (unsigned long long)DS_EMPTY, (unsigned long long)x);
+                if (old == DS_EMPTY) {
+                    atomicAdd(&lcount, 1u);
+                    done = true;
+                } else if (old == x) {
+                    done = true;
+                }
+            }
+        }
+        if (!done) ds_global_insert(tab, flags, cap, x);
+    }
+    if (saw_empty) flags[1] = 1u;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < DS_LDS_SLOTS; i += 256)
+        if (lt[i] != DS_EMPTY) ds_global_insert(tab, flags, cap, lt[i]);
+}
+
+__global__ __launch_bounds__(256) void k_distinct_compact(const unsigned long long *__restrict__ tab, uint32_t *flags,
+                                                          uint32_t cap, uint64_t *__restrict__ out) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= DS_G_SLOTS) return;
+    const uint64_t x = tab[i];
+    if (x == DS_EMPTY) return;
+    const uint32_t at = atomicAdd(&flags[2], 1u);
+    if (at < cap) out[at] = x;
+}
+
+// d_uniq: capacity cap + 1; *n_uniq > cap when there are more than cap distinct values (d_uniq is then not filled)
+int device_unique_u64(const uint64_t *d_sym, uint64_t total, uint64_t *d_uniq, uint64_t cap, uint64_t *n_uniq,
+                      hipStream_t st) {
     *n_uniq = 0;
     if (total == 0) return NMZ_OK;
-    NMZ_CHECK(total < (1ULL << 31), "more than 2^31-1 symbols for the device remap");
-    size_t sort_bytes = 0, uniq_bytes = 0;
+    NMZ_CHECK(cap > 0 && cap < DS_G_SLOTS / 8, "internal: distinct-set capacity out of range");
+    const uint32_t c32 = (uint32_t)cap;
+    size_t sort_bytes = 0;
     NMZ_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_bytes, (const uint64_t *)nullptr, (uint64_t *)nullptr,
-                                              (int)total, 0, 64, st));
-    NMZ_HIP(hipcub::DeviceSelect::Unique(nullptr, uniq_bytes, (const uint64_t *)nullptr, (uint64_t *)nullptr,
-                                         (uint64_t *)nullptr, (int)total, st));
+                                              (int)cap + 1, 0, 64, st));
     DevBuf scr;
-    NMZ_TRY(scr.ensure(Carve::bytes_for(total, 8) + Carve::bytes_for(1, 8) +
-                       Carve::bytes_for(std::max(sort_bytes, uniq_bytes) + 1, 1)));
+    NMZ_TRY(scr.ensure(Carve::bytes_for(DS_G_SLOTS, 8) + Carve::bytes_for(4, 4) + Carve::bytes_for(cap + 1, 8) +
+                       Carve::bytes_for(sort_bytes + 1, 1)));
     Carve cv(scr.ptr);
-    uint64_t *sorted = cv.take<uint64_t>(total);
-    uint64_t *d_n = cv.take<uint64_t>(1);
-    void *tmp = cv.take<char>(std::max(sort_bytes, uniq_bytes) + 1);
-    size_t b = sort_bytes;
+    unsigned long long *tab = cv.take<unsigned long long>(DS_G_SLOTS);
+    uint32_t *flags = cv.take<uint32_t>(4);
+    uint64_t *raw = cv.take<uint64_t>(cap + 1);
+    void *tmp = cv.take<char>(sort_bytes + 1);
     int rc = NMZ_OK;
-    if (hipcub::DeviceRadixSort::SortKeys(tmp, b, d_sym, sorted, (int)total, 0, 64, st) != hipSuccess) rc = NMZ_EHIP;
-    b = uniq_bytes;
-    if (rc == NMZ_OK && hipcub::DeviceSelect::Unique(tmp, b, sorted, d_uniq, d_n, (int)total, st) != hipSuccess)
-        rc = NMZ_EHIP;
-    if (rc == NMZ_OK && (hipMemcpyAsync(n_uniq, d_n, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                         hipStreamSynchronize(st) != hipSuccess))
-        rc = NMZ_EHIP;
+    uint32_t hf[4] = {0, 0, 0, 0};
+    auto ok = [&](hipError_t e) {
+        if (e != hipSuccess) rc = NMZ_EHIP;
+        return rc == NMZ_OK;
+    };
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(2048, (total + 255) / 256);
+    if (ok(hipMemsetAsync(tab, 0xff, (size_t)DS_G_SLOTS * 8, st)) && ok(hipMemsetAsync(flags, 0, 16, st))) {
+        hipLaunchKernelGGL(k_distinct_insert, dim3(blocks), dim3(256), 0, st, d_sym, total, tab, flags, c32);
+        hipLaunchKernelGGL(k_distinct_compact, dim3(DS_G_SLOTS / 256), dim3(256), 0, st, tab, flags, c32, raw);
+        if (ok(hipGetLastError()) && ok(hipMemcpyAsync(hf, flags, 16, hipMemcpyDeviceToHost, st)))
+            ok(hipStreamSynchronize(st));
+    }
+    if (rc == NMZ_OK) {
+        const uint64_t n = (uint64_t)hf[2] + hf[1];
+        if (hf[0] > c32 || n > cap) {
+            *n_uniq = cap + 1;
+        } else {
+            size_t b = sort_bytes;
+            if (hf[2] > 0) ok(hipcub::DeviceRadixSort::SortKeys(tmp, b, raw, d_uniq, (int)hf[2], 0, 64, st));
+            const uint64_t top = DS_EMPTY;  // the largest value: last in sorted order
+            if (rc == NMZ_OK && hf[1]) ok(hipMemcpyAsync(d_uniq + hf[2], &top, 8, hipMemcpyHostToDevice, st));
+            if (rc == NMZ_OK) ok(hipStreamSynchronize(st));  // before the scratch goes back
+            *n_uniq = n;
+        }
+    }
     scr.release();
-    return rc == NMZ_OK ? NMZ_OK : fail(NMZ_EHIP, "device symbol sort/unique failed");
+    return rc == NMZ_OK ? NMZ_OK : fail(NMZ_EHIP, "device distinct-symbol set failed");
 }
 
 }  // namespace nmz

@@ -407,6 +407,49 @@ def test_device_and_host_plan_builds_agree(ctx, monkeypatch):
         assert ds_d[q].tolist() == d[order].tolist() and ids_d[q].tolist() == pairs[order, 1].tolist()
 
 
+def test_device_plan_symbols_zero_and_all_ones(ctx, monkeypatch):
+    """The device plan's distinct-symbol set (an LDS + global hash set, csrc/unique.hip) keeps 0 and 2^64 - 1 (its
+    free-slot value) as symbols like any other: same k-NN lists as the host build and the oracle."""
+    rng = np.random.default_rng(78)
+    base = make_traces(600, 1700, 2000, 0.01, alphabet=40, rng=rng)
+    m = {np.uint64(3): np.uint64(0), np.uint64(0x9E3779B97F4A7C15 + 3): np.uint64(2**64 - 1)}
+    trs = []
+    for i in range(len(base)):
+        t = base.trace(i).copy()
+        for a, b in m.items():
+            t[t == a] = b
+        trs.append(t)
+    ts = hs.TraceSet(trs)
+    assert int(ts.off[-1]) >= 1 << 20 and (ts.sym == 0).any() and (ts.sym == np.uint64(2**64 - 1)).any()
+    ids_d, ds_d = knn(ctx, ts, 32, 5)
+    monkeypatch.setenv("NMZ_ED_HOST_REMAP", "1")
+    ids_h, ds_h = knn(ctx, ts, 32, 5)
+    assert np.array_equal(ids_d, ids_h) and np.array_equal(ds_d, ds_h)
+    for q in [0, 411]:
+        pairs = np.array([[q, c] for c in range(len(ts)) if c != q], np.uint32)
+        d = O.ed_pairs(ts.off, ts.sym, pairs, 32, nthreads=16)
+        order = np.lexsort((pairs[:, 1], d))[:5]
+        assert ds_d[q].tolist() == d[order].tolist() and ids_d[q].tolist() == pairs[order, 1].tolist()
+
+
+def test_device_plan_too_many_symbols_falls_back(ctx):
+    """A store of >= 2^20 symbols with ~10^6 distinct values: the device distinct set passes its cap (65,533), the
+    plan falls back to the host build and the exact generic kernel. All symbols distinct except one copied trace,
+    so every distance is beyond the band except the copy's (0)."""
+    rng = np.random.default_rng(79)
+    trs = [rng.integers(0, 2**64, size=7200, dtype=np.uint64) for _ in range(150)]
+    trs[111] = trs[17].copy()
+    ts = hs.TraceSet(trs)
+    assert int(ts.off[-1]) >= 1 << 20
+    ids, ds = knn(ctx, ts, 32, 3)
+    assert ds[111][0] == 0 and ids[111][0] == 17 and ds[17][0] == 0 and ids[17][0] == 111
+    others = np.ones(len(ts), bool)
+    others[[17, 111]] = False
+    assert (ds[others] == 33).all() and (ds[[17, 111], 1:] == 33).all()
+    # neighbours beyond the band are listed by index (the reference's stable order)
+    assert ids[0].tolist() == [1, 2, 3] and ids[17][1:].tolist() == [0, 1]
+
+
 def _edited_family(n, length, alphabet, max_edits, rng):
     """Traces = one base with 0..max_edits random edits each (adjacent transpositions, substitutions,
     insertions, deletions), so pair distances spread across the band edge and the q-gram bound's edge."""
