@@ -911,8 +911,16 @@ static uint32_t ed_block_shard(uint32_t qb, uint32_t n_shards) {
     if (n_shards <= 1) return 0;
     const char *e = getenv("NMZ_ED_DEAL");
     if (e && std::string(e) == "hash") return (uint32_t)(tile_mix(qb) % n_shards);
-    const uint32_t r = qb % (2 * n_shards);
-    return r < n_shards ? r : 2 * n_shards - 1 - r;
+    // snake: in each period of 2S blocks, block r and its mirror 2S-1-r form pair min(r, 2S-1-r); the pair goes to
+    // shard (pair + period) mod S (rotated snake), so over the periods every shard takes every pair position. A
+    // plain snake (shard = pair, NMZ_ED_DEAL=snake) gives shard s the same two positions in every period: when the
+    // work's own period matches (families of 16 blocks at 8 shards), shard 0 always holds each family's first and
+    // last block -- equal work, but the last block's short candidate lists run the DP less efficiently (1.15x)
+    const char *u = getenv("NMZ_ED_DEAL_UNIT");  // blocks per dealt unit (A/B)
+    const uint32_t unit = u && atoi(u) > 0 ? (uint32_t)atoi(u) : 1u, q = qb / unit;
+    const uint32_t r = q % (2 * n_shards), pr = r < n_shards ? r : 2 * n_shards - 1 - r;
+    if (e && std::string(e) == "snake") return pr;
+    return (pr + q / (2 * n_shards)) % n_shards;
 }
 // the entry-list limit (NMZ_ED_TP_MAX_ENTRIES lowers it, so tests can force the single-kernel fallback)
 static uint64_t ed_tp_max_entries() {

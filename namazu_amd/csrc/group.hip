@@ -11,7 +11,7 @@
 // Work is split into n_shards shards (>= the number of ranks: "virtual" shards, so one GPU runs the sharding
 // and merge logic of any shard count); shard s runs on rank s mod n_ranks. The sweeps shard by contiguous
 // seed range (dist.py shard_range: sizes differ by <= 1), the all-pairs search by the plan's own query-block
-// deal (nmz_ed_allpairs_knn_shard_dev: snake order, nmz_ed_block_shard). Each rank merges its shards' results on its device, one RCCL all_gather
+// deal (nmz_ed_allpairs_knn_shard_dev: rotated snake order, nmz_ed_block_shard). Each rank merges its shards' results on its device, one RCCL all_gather
 // over xGMI exchanges the ranks' lists (k x 24 B top-k, or N x k x 8 B k-NN keys), and a deterministic merge
 // -- (n_fault desc, sum_delay desc, seed asc) / (dist asc, id asc) -- gives every rank the same result.
 #include <rccl/rccl.h>

@@ -32,10 +32,11 @@ _M64 = (1 << 64) - 1
 
 def ed_block_shard(qb, world):
     """Shard owning query block qb (queries 64 qb .. 64 qb + 63) of the two-phase all-pairs search
-    (nmz_ed_allpairs_knn_shard_dev; csrc/ed.hip ed_block_shard): snake order 0, 1, .., world-1, world-1, .., 0,
-    repeated, so the falling work per block inside the upper triangle and inside each family of near-duplicates
-    cancels between a block and its mirror. Whole query blocks, so a query pair's DP entries stay in one shard.
-    NMZ_ED_DEAL=hash selects the MurmurHash3 deal (A/B runs)."""
+    (nmz_ed_allpairs_knn_shard_dev; csrc/ed.hip ed_block_shard): in each period of 2 world blocks, block r and
+    its mirror 2 world - 1 - r form a pair (the falling work per block inside the upper triangle and inside each
+    family of near-duplicates cancels between them), and pair p of period g goes to shard (p + g) mod world, so
+    every shard takes every position. Whole query blocks, so a query pair's DP entries stay in one shard.
+    NMZ_ED_DEAL=snake selects the unrotated snake, NMZ_ED_DEAL=hash the MurmurHash3 deal (A/B runs)."""
     if world <= 1:
         return 0
     if os.environ.get("NMZ_ED_DEAL") == "hash":
@@ -45,8 +46,13 @@ def ed_block_shard(qb, world):
         x ^= x >> 33
         x = (x * 0xC4CEB9FE1A85EC53) & _M64
         return (x ^ (x >> 33)) % world
-    r = qb % (2 * world)
-    return r if r < world else 2 * world - 1 - r
+    unit = int(os.environ.get("NMZ_ED_DEAL_UNIT", "1") or 1)
+    q = qb // (unit if unit > 0 else 1)
+    r = q % (2 * world)
+    pr = r if r < world else 2 * world - 1 - r
+    if os.environ.get("NMZ_ED_DEAL") == "snake":
+        return pr
+    return (pr + q // (2 * world)) % world  # rotated snake: the pair position moves one shard per period
 
 
 def ed_pair_shard(i, j, world):

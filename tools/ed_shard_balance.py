@@ -4,7 +4,9 @@
 Runs each of n_shards shards of the configs[2] search (nmz_ed_allpairs_knn_shard_dev: every n_shards-th
 work chunk) one after the other on one device and records, per shard, the kernel time (HIP events) and
 k_ed_bv's executed-block counter. The job finishes when the slowest rank does, so max / mean of these is
-the dealing's loss at n_shards GPUs. usage: ed_shard_balance.py [generator] [n_shards] > out.json
+the dealing's loss at n_shards GPUs. ED_BAL_ORDER=reverse runs the shards last to first (separates a trend over
+the run, e.g. the clock, from one over the shard index); ED_BAL_REPS=r times each shard r times back to back and
+keeps the last. usage: ed_shard_balance.py [generator] [n_shards] > out.json
 """
 import ctypes
 import json
@@ -45,7 +47,12 @@ def main():
     full_ms = tot.value
     rows = []
     cnt = np.zeros(_lib.NMZ_ED_NCOUNTERS, np.uint64)
-    for s in range(S):
+    order = list(range(S))[::-1] if os.environ.get("ED_BAL_ORDER") == "reverse" else list(range(S))
+    reps = max(1, int(os.environ.get("ED_BAL_REPS", "1")))
+    for s in order:
+        for _ in range(reps - 1):
+            _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, s, S, ctypes.c_void_p(d.data_ptr()), stream))
+        torch.cuda.synchronize()
         tot, c = ctypes.c_double(), ctypes.c_uint64()
         ph = {n: (ctypes.c_double(), ctypes.c_uint64()) for n in (b"ed_qg_filter", b"ed_bv_dp")}
         L.nmz_timing_read(ctx.handle, b"ed_bv", ctypes.byref(tot), ctypes.byref(c), 1)
@@ -61,6 +68,7 @@ def main():
                      "dp_ms": ph[b"ed_bv_dp"][0].value, "dp_pairs": int(cnt[0]), "blocks": int(cnt[2]),
                      "in_band": int(cnt[1])})
     L.nmz_ed_plan_destroy(plan)
+    rows.sort(key=lambda r: r["shard"])
     ms = np.array([r["kernel_ms"] for r in rows])
     bl = np.array([r["blocks"] for r in rows], np.float64)
     print(json.dumps({"generator": gen, "traces": N, "events": Lx, "band": w, "shards": S, "per_shard": rows,
@@ -69,7 +77,8 @@ def main():
                       "sum_shard_ms": float(ms.sum()), "unsharded_ms": full_ms,
                       "max_shard_ms": float(ms.max()), "speedup_bound": float(full_ms / ms.max()),
                       "item": int(os.environ.get("NMZ_ED_ITEM", "4096")),
-                      "deal": os.environ.get("NMZ_ED_DEAL", "snake")}, indent=1))
+                      "deal": os.environ.get("NMZ_ED_DEAL", "snake"),
+                      "order": "reverse" if order[0] else "forward", "reps": reps}, indent=1))
 
 
 if __name__ == "__main__":
