@@ -88,6 +88,21 @@ def isa_state(e):
     return fresh, detail
 
 
+def issue_ceiling(kernel, isa, lane_instr, kernel_ms):
+    """This launch's VALU issue time at the measured issue cost of the kernel's instruction forms
+    (tools/issue_ceiling.py -> profiles/issue_ceiling.json: mean cycles per wave-instruction of the hot loop)
+    over the measured kernel time, at the clock the chip held in the kernel's profile; None when the entry is
+    missing or priced other machine code."""
+    try:
+        e = json.load(open(os.path.join(HERE, "profiles", "issue_ceiling.json")))["kernels"][kernel]
+    except (OSError, KeyError, ValueError):
+        return None
+    if not e.get("isa") or any(isa.get(k, [None, None])[1] != h for k, h in e["isa"].items()):
+        return None
+    cyc = lane_instr / 64.0 * e["hot_loop"]["mean_cost"] / 1024.0
+    return cyc / (e["clock_ghz"] * 1e9) / (kernel_ms * 1e-3)
+
+
 def roofline_valu(kernel, units, kernel_ms):
     """VALU issue roofline of `kernel`: measured lane-instructions per unit x units / kernel time. The entry's
     lane-instructions per unit hold only for the machine code that was profiled: when the shipped kernel's
@@ -107,7 +122,9 @@ def roofline_valu(kernel, units, kernel_ms):
                 "frac": None, "peak": PEAK_VALU_TOPS, "unit": "Tops/s", "traffic": None,
                 "frac_if_profile_held": achieved / PEAK_VALU_TOPS, "ops_source": e["source"], "isa": isa,
                 "why": "the profiled kernel's machine code differs from the shipped library's (tools/kernel_isa.py)"}
+    ceil = issue_ceiling(kernel, isa, e["ops_per_unit"] * units, kernel_ms)
     return {"bound": "valu", "achieved": achieved, "peak": PEAK_VALU_TOPS, "unit": "Tops/s", "stale": False,
+            "frac_of_issue_ceiling": ceil,
             "frac": achieved / PEAK_VALU_TOPS, "traffic": traffic, "isa": isa, "traffic_unit": "bytes/launch (2 x FETCH_SIZE + WRITE_SIZE)",
             "kernel": kernel, "kernel_ms": kernel_ms, "ops_per_unit": e["ops_per_unit"], "units_per_launch": units,
             "ops_source": e["source"],

@@ -21,6 +21,8 @@ select form is priced at full rate, which is what it costs when its VCC producer
 ceiling is a lower bound on the duration, so `at_ceiling` can only be overstated by such optimistic prices.
 
 usage: issue_ceiling.py [--lib libnmz_gpu.so] [--out profiles/issue_ceiling.json]
+(bench.py reads profiles/issue_ceiling.json: `frac_of_issue_ceiling` in a leg's roofline, when the kernel's
+fingerprint there matches the shipped library)
 """
 import argparse
 import json
@@ -169,6 +171,7 @@ def main():
         wave_instr = e["ops_per_unit"] * e["units_per_launch"] / 64.0
         ghz, ns = e["clock_ghz"], e["avg_ns"]
         r = {"kernel": e["kernel"], "profile": e["source"], "fingerprint_matches_library": fresh,
+             "isa": e.get("isa", {}),
              "valu_wave_instr_per_launch": wave_instr, "avg_ns": ns, "clock_ghz": ghz,
              "hot_loop": {"bytes": [s, t], **lm}, "whole_kernel": wm}
         for tag, m in (("hot_loop", lm), ("whole_kernel", wm)):
