@@ -617,6 +617,90 @@ static int ed_plan_build_bv_device(nmz_ed_plan *p, const uint64_t *off, const ui
     return NMZ_OK;
 }
 
+// wide-band plan streams from device symbols: dense id (rank among the sorted distinct symbols) per position, in
+// CSR order (qsym), and the id's Peq row byte offset per position of each trace's padded row stream (rowb)
+__global__ __launch_bounds__(256) void k_ed_wide_remap(const uint64_t *__restrict__ off, const uint64_t *__restrict__ sym,
+                                                       const uint64_t *__restrict__ uniq, uint32_t n_uniq,
+                                                       const uint64_t *__restrict__ roff, uint32_t row_bytes,
+                                                       uint16_t *__restrict__ qsym, uint32_t *__restrict__ rowb) {
+    const uint32_t i = blockIdx.x;
+    const uint64_t b = off[i], n = off[i + 1] - b, ro = roff[i];
+    for (uint64_t t = threadIdx.x; t < n; t += 256) {
+        const uint64_t x = sym[b + t];
+        uint32_t lo = 0, hi = n_uniq;  // first index with uniq[idx] >= x (x is present)
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (uniq[mid] < x) lo = mid + 1; else hi = mid;
+        }
+        qsym[b + t] = (uint16_t)lo;
+        rowb[ro + t] = lo * row_bytes;
+    }
+}
+
+// The wide-band plan built on the device (the host build remaps every symbol through a hash map: ~100 ms for
+// configs[4]'s 1.7e7 symbols): distinct symbols from the device hash set, then one remap kernel. Returns 1 (not
+// applicable: alphabet or Peq tables too large) so the caller takes the host build.
+static int ed_plan_build_wide_device(nmz_ed_plan *p, const uint64_t *off, const uint64_t *sym, uint32_t N,
+                                     uint32_t band, uint32_t maxlen, const uint64_t *d_sym_in) {
+    hipStream_t st = p->ctx->stream;
+    const uint64_t total = off[N];
+    NMZ_CHECK(total == 0 || sym || d_sym_in, "sym is NULL");
+    DevBuf tmp;
+    struct Release {
+        DevBuf &b;
+        ~Release() { b.release(); }
+    } release_tmp{tmp};
+    NMZ_TRY(tmp.ensure(Carve::bytes_for(d_sym_in ? 0 : total, 8) + Carve::bytes_for(MAX_FAST_SYMBOLS + 1, 8) +
+                       Carve::bytes_for(N + 1, 8) * 2));
+    Carve tv(tmp.ptr);
+    const uint64_t *d_sym = d_sym_in;
+    if (!d_sym_in) {
+        uint64_t *d_up = tv.take<uint64_t>(total);
+        NMZ_HIP(hipMemcpyAsync(d_up, sym, total * 8, hipMemcpyHostToDevice, st));
+        d_sym = d_up;
+    }
+    uint64_t *d_uniq = tv.take<uint64_t>(MAX_FAST_SYMBOLS + 1);
+    uint64_t *d_off = tv.take<uint64_t>(N + 1), *d_roff = tv.take<uint64_t>(N + 1);
+    uint64_t n_uniq = 0;
+    NMZ_TRY(device_unique_u64(d_sym, total, d_uniq, MAX_FAST_SYMBOLS, &n_uniq, st));
+    if (n_uniq >= MAX_FAST_SYMBOLS) return 1;
+    const uint32_t n_sym = std::max((uint32_t)n_uniq, 1u);
+    p->ww = ed_wide_template(band);
+    const uint32_t ndw = ed_wide_ndw(p->ww, maxlen);
+    const uint64_t peq_bytes = (uint64_t)N * n_sym * ndw * 4;
+    if (peq_bytes > (16ULL << 30) || (uint64_t)n_sym * ndw * 4 >= (1ULL << 31)) return 1;
+    p->wide = true;
+    p->fast = true;
+    p->ndw = ndw;
+    p->n_sym = n_sym;
+    std::vector<uint64_t> roff(N + 1, 0);
+    for (uint32_t i = 0; i < N; ++i) roff[i + 1] = roff[i] + ((off[i + 1] - off[i] + 31) / 32 + 2) * 32;
+    const uint64_t nrow = roff[N] + 1;
+    NMZ_TRY(p->mem.ensure(Carve::bytes_for(total + 64, 2) + Carve::bytes_for(N + 1, 8) +
+                          Carve::bytes_for((uint64_t)N * n_sym * ndw, 4) + Carve::bytes_for(nrow, 4) +
+                          Carve::bytes_for(N + 1, 8)));
+    Carve cv(p->mem.ptr);
+    p->d_qsym = cv.take<uint16_t>(total + 64);
+    p->d_qoff = cv.take<uint64_t>(N + 1);
+    p->d_peq = cv.take<uint32_t>((uint64_t)N * n_sym * ndw);
+    p->d_rowb = cv.take<uint32_t>(nrow);
+    p->d_rowb_off = cv.take<uint64_t>(N + 1);
+    NMZ_HIP(hipMemcpyAsync(d_off, off, (N + 1) * 8, hipMemcpyHostToDevice, st));
+    NMZ_HIP(hipMemcpyAsync(d_roff, roff.data(), (N + 1) * 8, hipMemcpyHostToDevice, st));
+    NMZ_HIP(hipMemcpyAsync(p->d_qoff, off, (N + 1) * 8, hipMemcpyHostToDevice, st));
+    NMZ_HIP(hipMemcpyAsync(p->d_rowb_off, roff.data(), (N + 1) * 8, hipMemcpyHostToDevice, st));
+    NMZ_HIP(hipMemsetAsync(p->d_qsym, 0, (total + 64) * 2, st));
+    NMZ_HIP(hipMemsetAsync(p->d_rowb, 0, nrow * 4, st));
+    if (N) {
+        hipLaunchKernelGGL(k_ed_wide_remap, dim3(N), dim3(256), 0, st, d_off, d_sym, d_uniq, (uint32_t)n_uniq, d_roff,
+                           ndw * 4, p->d_qsym, p->d_rowb);
+        NMZ_HIP(hipGetLastError());
+    }
+    NMZ_TRY(ed_wide_build_peq(p->d_qsym, p->d_qoff, N, n_sym, ndw, p->ww, p->d_peq, st));
+    NMZ_HIP(hipStreamSynchronize(st));  // the host vectors above are pageable; the scratch goes back
+    return NMZ_OK;
+}
+
 // d_sym: the symbols on the device instead of sym (host); the host build paths take a copy of them
 static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, uint32_t N, uint32_t band,
                          nmz_ed_plan **out, const uint64_t *d_sym = nullptr) {
@@ -643,6 +727,20 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         delete p;
         if (!not_applicable) return rc;
         p = new nmz_ed_plan();  // alphabet too large for the bit-parallel tables: host build below
+        p->ctx = ctx;
+        p->n = N;
+        p->band = band;
+    }
+    if (ed_wide_supported(band) && total >= ED_DEVICE_REMAP_MIN && !getenv("NMZ_ED_HOST_REMAP")) {
+        const int rc = ed_plan_build_wide_device(p, off, sym, N, band, maxlen, d_sym);
+        if (rc == NMZ_OK) {
+            *out = p;
+            return NMZ_OK;
+        }
+        p->mem.release();
+        delete p;
+        if (rc != 1) return rc;
+        p = new nmz_ed_plan();  // alphabet or tables too large: the host build below
         p->ctx = ctx;
         p->n = N;
         p->band = band;

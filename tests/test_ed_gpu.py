@@ -432,6 +432,24 @@ def test_device_plan_symbols_zero_and_all_ones(ctx, monkeypatch):
         assert ds_d[q].tolist() == d[order].tolist() and ids_d[q].tolist() == pairs[order, 1].tolist()
 
 
+def test_wide_device_and_host_plan_builds_agree(ctx, monkeypatch):
+    """Wide-band stores of >= 2^20 symbols build k_ed_wide's plan on the device (hash-set alphabet + remap kernel,
+    ids by sorted rank instead of first appearance); NMZ_ED_HOST_REMAP forces the host build. Same k-NN lists,
+    and the oracle's for sampled queries."""
+    rng = np.random.default_rng(80)
+    ts = make_traces(300, 3600, 3900, 0.02, alphabet=40, rng=rng)
+    assert int(ts.off[-1]) >= 1 << 20
+    ids_d, ds_d = knn(ctx, ts, 1500, 4)
+    monkeypatch.setenv("NMZ_ED_HOST_REMAP", "1")
+    ids_h, ds_h = knn(ctx, ts, 1500, 4)
+    assert np.array_equal(ids_d, ids_h) and np.array_equal(ds_d, ds_h)
+    for q in [0, 157]:
+        pairs = np.array([[q, c] for c in range(len(ts)) if c != q], np.uint32)
+        d = O.ed_pairs(ts.off, ts.sym, pairs, 1500, nthreads=16)
+        order = np.lexsort((pairs[:, 1], d))[:4]
+        assert ds_d[q].tolist() == d[order].tolist() and ids_d[q].tolist() == pairs[order, 1].tolist()
+
+
 def test_device_plan_too_many_symbols_falls_back(ctx):
     """A store of >= 2^20 symbols with ~10^6 distinct values: the device distinct set passes its cap (65,533), the
     plan falls back to the host build and the exact generic kernel. All symbols distinct except one copied trace,
