@@ -1611,13 +1611,14 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
         for (size_t l = 1; l < pos.size(); ++l) pos[l] += pos[l - 1];
         for (uint32_t e = 0; e < E; ++e) perm[pos[hint_off[e + 1] - hint_off[e]]++] = e;
     }
-    std::vector<ClassInfo> cls;
-    for (uint32_t i = 0; i < E; ++i) {
+    std::vector<ClassInfo> cls;  // runs of equal length in the length-sorted order (P^len once per class)
+    for (uint32_t i = 0, prev = 0; i < E; ++i) {
         const uint32_t e = perm[i];
         const uint32_t len = hint_off[e + 1] - hint_off[e];
-        if (cls.empty() || fnv_pow(len) != cls.back().pn ||
-            len != hint_off[perm[cls.back().start] + 1] - hint_off[perm[cls.back().start]])
+        if (cls.empty() || len != prev) {
             cls.push_back(ClassInfo{fnv_pow(len), i, 0});
+            prev = len;
+        }
         cls.back().count++;
     }
     p->n_classes = (uint32_t)cls.size();
