@@ -976,8 +976,8 @@ def bench_group(args, torch):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--seeds", type=int, default=1 << 20)
     ap.add_argument("--events", type=int, default=4096)
     ap.add_argument("--cpu-seeds", type=int, default=1 << 18)
