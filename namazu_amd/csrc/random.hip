@@ -28,10 +28,10 @@ constexpr uint32_t INTN_N = 999;
 constexpr uint32_t INT31N_MAX = 0x7fffffffu - (0x80000000u % INTN_N);  // rand.go Int31n
 
 __constant__ uint64_t d_cooked[gorand::LEN] = NMZ_GO_RNG_COOKED_INIT;
-__device__ const gorand::PowTable d_powa = gorand::make_pow_table();
+[[maybe_unused]] __device__ const gorand::PowTable d_powa = gorand::make_pow_table();
 // the same tables for the host decision path (nmz_random_decide_host): the decision code below is shared
-static constexpr gorand::PowTable h_powa = gorand::make_pow_table();
-static constexpr uint64_t h_cooked[gorand::LEN] = NMZ_GO_RNG_COOKED_INIT;
+[[maybe_unused]] static constexpr gorand::PowTable h_powa = gorand::make_pow_table();
+[[maybe_unused]] static constexpr uint64_t h_cooked[gorand::LEN] = NMZ_GO_RNG_COOKED_INIT;
 #ifdef __HIP_DEVICE_COMPILE__
 #define NMZ_POWA(i) d_powa.v[i]
 #define NMZ_COOKED(i) d_cooked[i]
