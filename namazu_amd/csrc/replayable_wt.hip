@@ -43,10 +43,16 @@ struct WtClass {
                               //   with C_hi >= b << 24 (256)
     uint32_t o_pm;            //   per d in [0, n]: {largest rank at positions < d, largest rank at positions >= d}
                               //   (u16 pairs: the maximum of a part none of whose Cm is below its bound)
-    uint32_t K, nw;           // levels (2^K > n); words per level (n / 32 + 1)
+    uint32_t K, nw;           // rank bits (2^K > n); words per level (n / 32 + 1)
     uint32_t rS;              // lifting-search rounds (the largest bucket's bit length; set by the plan kernel)
+    uint32_t o_mk;            //   block masks [n / 32 + 1][33]: the ranks (bit r & 31) among the first o entries
+                              //   of each 32-rank block's node, o = 0..32
+    uint32_t pad;
 };
-static_assert(sizeof(WtClass) == 56, "WtClass layout");
+static_assert(sizeof(WtClass) == 64, "WtClass layout");
+
+// the tree stores the levels above the 32-rank blocks; the blocks' masks stand for the last five
+__host__ __device__ constexpr uint32_t wt_levels(uint32_t K) { return K > 5 ? K - 5 : 0; }
 
 // ---------------------------------------------------------------------------------------------------------------
 // plan: one workgroup per (segment, row L). Sorts the segment's keys (Cm << 32 | (0xffff - e) << 16 | position)
@@ -255,11 +261,11 @@ __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__re
         }
         __syncthreads();  // wb is the level loop's next
     }
-    // wavelet levels
-    const uint32_t K = ci.K, nw = ci.nw;
+    // wavelet levels above the 32-rank blocks
+    const uint32_t K = ci.K, nw = ci.nw, lb = wt_levels(K);
     uint2 *lv = reinterpret_cast<uint2 *>(img + ci.o_lv);
     uint16_t *cur = S0, *nxt = S0 + WT_NMAX;
-    for (uint32_t l = 0; l < K; ++l) {
+    for (uint32_t l = 0; l < lb; ++l) {
         const uint32_t k = K - l, h = 1u << (k - 1);
         for (uint32_t j0 = wave * 64; j0 < nw * 32; j0 += WT_BT) {
             const uint32_t j = j0 + lane;
@@ -298,6 +304,22 @@ __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__re
         uint16_t *t = cur;
         cur = nxt;
         nxt = t;
+    }
+    // level lb: the node of block b holds the ranks [32 b, 32 b + 32) in position order (all n ranks when K <= 5);
+    // mk[b][o] = OR of bit (rank & 31) over its first o entries: a prefix OR per block, 32 lanes per block
+    uint32_t *mk = reinterpret_cast<uint32_t *>(img + ci.o_mk);
+    const uint32_t nbk = n / 32 + 1;
+    for (uint32_t b0 = 2 * wave; b0 < nbk; b0 += 2 * WT_BW) {
+        const uint32_t b = b0 + (lane >> 5), j = 32 * b + (lane & 31);
+        uint32_t v = (b < nbk && j < n) ? 1u << (cur[j] & 31) : 0u;
+        for (int o = 1; o < 32; o <<= 1) {
+            const uint32_t u = __shfl_up(v, o, 64);
+            if ((lane & 31) >= (uint32_t)o) v |= u;
+        }
+        if (b < nbk) {
+            mk[b * 33 + (lane & 31) + 1] = v;
+            if ((lane & 31) == 0) mk[b * 33] = 0;
+        }
     }
 }
 
@@ -385,15 +407,16 @@ __device__ __forceinline__ void wt_seed_class(const WtClass &ci, const char *__r
         while (d < n && chi[d] == nh && row[ci.start + d].x <= nl) ++d;
     }
     const uint32_t pmd = pm[d];  // the parts' largest ranks (used when a part has nothing below its bound)
-    // descents along R_A's and R_B's paths with the prefix [0, d), branch-free with both reads of a level in
-    // flight: counts of ranks >= R, and the deepest level where a part's elements below R branch off (the
-    // predecessor's subtree: node start s, prefix offset q)
+    // descents along R_A's and R_B's paths with the prefix [0, d) down to R's 32-rank block, branch-free with both
+    // reads of a level in flight: counts of ranks >= R, and the deepest level where a part's elements below R branch
+    // off (the predecessor's subtree: node start s, prefix offset q)
     const uint2 *__restrict__ lv = reinterpret_cast<const uint2 *>(img + ci.o_lv);
-    const uint32_t K = ci.K, nw = ci.nw;
+    const uint32_t *__restrict__ mk = reinterpret_cast<const uint32_t *>(img + ci.o_mk);
+    const uint32_t K = ci.K, nw = ci.nw, lb = wt_levels(K);
     uint32_t oA = d, oB = d, cA = 0, cB = 0;
     uint32_t lA = WT_NONE, sA = 0, qA = 0, lB = WT_NONE, sB = 0, qB = 0;
     const uint32_t nv = wt_v(n), one = wt_v(1u), five = wt_v(5u);
-    for (uint32_t l = 0; l < K; ++l) {
+    for (uint32_t l = 0; l < lb; ++l) {
         const uint32_t hs = 1u << (K - l - 1);
         const uint32_t h = wt_v(hs), msk = wt_v(~(2 * hs - 1)), l1 = wt_v(l + 1);
         const uint2 *__restrict__ lvl = lv + l * nw;
@@ -416,43 +439,57 @@ __device__ __forceinline__ void wt_seed_class(const WtClass &ci, const char *__r
         oA = b1 ? o1 : z1;
         oB = b2 ? o2 : z2;
     }
-    cA += oA;  // the leaf R itself, if in the prefix
-    cB += oB;
+    // R's 32-rank block: its node's first o entries are the prefix part's elements in it (mk: their ranks' bits), so
+    // the ranks >= R among them finish the counts, and those below R hold the part's predecessor when any are there
+    const uint32_t bA = RA & ~31u, bB = RB & ~31u, rA = RA & 31u, rB = RB & 31u;
+    const uint32_t mA = mk[bA + (bA >> 5) + oA], mB = mk[bB + (bB >> 5) + oB];
+    cA += __popc(mA >> rA);
+    cB += __popc(mB >> rB);
     W += cA + (n - RB) - cB;
-    // predecessor descents: the prefix part takes the largest rank among the first qA entries of node sA, the
-    // suffix part the largest among entries qB.. of node sB. A part with nothing below its bound wraps, and its
-    // maximum is its largest rank overall (pm). Levels no lane of the wave needs are skipped.
-    const bool hasA = d > 0, hasB = d < n, wrapA = lA == WT_NONE, wrapB = lB == WT_NONE;
-    if (wrapA || !hasA) lA = K;
-    if (wrapB || !hasB) lB = K;
-    if (wrapA) sA = pmd & 0xffffu;
-    if (wrapB) sB = pmd >> 16;
+    const uint32_t belA = __builtin_amdgcn_ubfe(mA, 0u, rA), belB = __builtin_amdgcn_ubfe(~mB, 0u, rB);
+    // predecessors: in R's block when a part has an element below R there; else from the deepest branch-off level
+    // down to a block (second descent: the prefix part takes the largest rank among the first qA entries of node
+    // sA, the suffix part the largest among entries qB.. of node sB); a part with nothing below its bound wraps, and
+    // its maximum is its largest rank overall (pm). Levels no lane of the wave needs are skipped.
+    const bool hasA = d > 0, hasB = d < n, hitA = belA != 0, hitB = belB != 0;
+    const bool wrapA = !hitA && lA == WT_NONE, wrapB = !hitB && lB == WT_NONE;
+    const bool dA = hasA && !hitA && !wrapA, dB = hasB && !hitB && !wrapB;
+    if (!dA) lA = lb;
+    if (!dB) lB = lb;
     const uint32_t l0 = min(lA, lB);
-    for (uint32_t l = 0; l < K; ++l) {
-        if (!__builtin_amdgcn_ballot_w64(l >= l0)) continue;
-        const uint32_t hs = 1u << (K - l - 1);
-        const uint32_t h = wt_v(hs), h2 = wt_v(2 * hs), lv1 = wt_v(l);
-        const uint2 *__restrict__ lvl = lv + l * nw;
-        const uint32_t p1 = sA + qA, p2 = sB + qB;
-        const uint2 w1 = lvl[p1 >> five], w2 = lvl[p2 >> five];
-        const uint32_t o1 = w1.y + __popc(__builtin_amdgcn_ubfe(w1.x, 0u, p1)) - (sA >> one);
-        const uint32_t o2 = w2.y + __popc(__builtin_amdgcn_ubfe(w2.x, 0u, p2)) - (sB >> one);
-        const bool a1 = lv1 >= lA, a2 = lv1 >= lB;
-        const bool g1 = a1 && o1 != 0;
-        const bool g2 = a2 && min(nv - sB, h2) > h + o2;  // ones of the node past the prefix
-        sA += g1 ? h : 0u;
-        qA = g1 ? o1 : qA;
-        sB += g2 ? h : 0u;
-        qB = a2 ? (g2 ? o2 : qB - o2) : qB;
+    if (__builtin_amdgcn_ballot_w64(l0 < lb)) {
+        for (uint32_t l = 0; l < lb; ++l) {
+            if (!__builtin_amdgcn_ballot_w64(l >= l0)) continue;
+            const uint32_t hs = 1u << (K - l - 1);
+            const uint32_t h = wt_v(hs), h2 = wt_v(2 * hs), lv1 = wt_v(l);
+            const uint2 *__restrict__ lvl = lv + l * nw;
+            const uint32_t p1 = sA + qA, p2 = sB + qB;
+            const uint2 w1 = lvl[p1 >> five], w2 = lvl[p2 >> five];
+            const uint32_t o1 = w1.y + __popc(__builtin_amdgcn_ubfe(w1.x, 0u, p1)) - (sA >> one);
+            const uint32_t o2 = w2.y + __popc(__builtin_amdgcn_ubfe(w2.x, 0u, p2)) - (sB >> one);
+            const bool a1 = lv1 >= lA, a2 = lv1 >= lB;
+            const bool g1 = a1 && o1 != 0;
+            const bool g2 = a2 && min(nv - sB, h2) > h + o2;  // ones of the node past the prefix
+            sA += g1 ? h : 0u;
+            qA = g1 ? o1 : qA;
+            sB += g2 ? h : 0u;
+            qB = a2 ? (g2 ? o2 : qB - o2) : qB;
+        }
     }
+    // the descended lanes end in a block: the prefix part's elements are its first qA entries, the suffix part's the
+    // entries from qB on (of the block's min(n - sB, 32))
+    const uint32_t vA = mk[sA + (sA >> 5) + qA];
+    const uint32_t vB = ~mk[sB + (sB >> 5) + qB] & (0xffffffffu >> (32u - min(nv - sB, 32u)));
+    const uint32_t pA = hitA ? bA + 31u - __clz(belA) : wrapA ? (pmd & 0xffffu) : sA + 31u - __clz(vA);
+    const uint32_t pB = hitB ? bB + 31u - __clz(belB) : wrapB ? (pmd >> 16) : sB + 31u - __clz(vB);
     if (hasA) {
-        const uint32_t t = Hm + cm[sA] - (wrapA ? m : 0u);
-        const uint64_t k = ((uint64_t)t << 32) | (0xffffffffu - ev[sA]);
+        const uint32_t t = Hm + cm[pA] - (wrapA ? m : 0u);
+        const uint64_t k = ((uint64_t)t << 32) | (0xffffffffu - ev[pA]);
         key = k > key ? k : key;
     }
     if (hasB) {
-        const uint32_t t = Hm2 + cm[sB] - (wrapB ? m : 0u);
-        const uint64_t k = ((uint64_t)t << 32) | (0xffffffffu - ev[sB]);
+        const uint32_t t = Hm2 + cm[pB] - (wrapB ? m : 0u);
+        const uint64_t k = ((uint64_t)t << 32) | (0xffffffffu - ev[pB]);
         key = k > key ? k : key;
     }
     sum += (uint64_t)d * Hm + (uint64_t)(n - d) * Hm2;
@@ -830,7 +867,7 @@ int wt_build(WtState &w, nmz_ctx *ctx, const uint4 *d_table, uint32_t E, const C
         o.K = bitlen(o.n);  // 2^K > n >= every bound R
         o.nw = o.n / 32 + 1;
         o.o_lv = (uint32_t)off;
-        off += r16((uint64_t)o.K * o.nw * 8);
+        off += r16((uint64_t)wt_levels(o.K) * o.nw * 8);
         o.o_cm = (uint32_t)off;
         off += r16((uint64_t)(o.n + 1) * 4);
         o.o_chi = (uint32_t)off;
@@ -843,6 +880,8 @@ int wt_build(WtState &w, nmz_ctx *ctx, const uint4 *d_table, uint32_t E, const C
         off += r16(256 * 2);
         o.o_pm = (uint32_t)off;
         off += r16((uint64_t)(o.n + 1) * 4);
+        o.o_mk = (uint32_t)off;
+        off += r16((uint64_t)(o.n / 32 + 1) * 33 * 4);
     }
     const uint64_t rb = std::max<uint64_t>(16, r16(off));
     if (rb + 16 > WT_LDS_MAX) return NMZ_OK;

@@ -1,14 +1,10 @@
-#!/bin/bash
-# K1 A/B: sweep parity tests (default variant), then bench per (key, U, EC) variant.
-# usage: tools/k1_ab.sh "<key> <U> <EC>" ...   (key = f64 | u64)
-cd /tmp && export TMPDIR=/tmp
-R=${GRAFT_REPO_ROOT:-/root/repo}
-OUT=$R/gpurun_out/k1ab
-mkdir -p $OUT
-timeout -k 10 300 python3 -u -m pytest $R/tests/test_sweeps_gpu.py -x -q --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
-tail -2 $OUT/tests.log
-B="python3 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-secondary"
-for cfg in "$@"; do set -- $cfg
-  NMZ_REPLAY_KEY=$1 NMZ_REPLAY_U=$2 NMZ_REPLAY_EC=$3 timeout -k 10 120 $B > $OUT/bench_$1_$2_$3.json || exit 1
-  python3 -c "
-import json; d=json.load(open('$OUT/bench_$1_$2_$3.json')); print('key=$1 U=$2 EC=$3', round(d['ms_per_step'],4), round(d['roofline']['kernel_ms'],4), '%.4g'%d['value'])"; done
+# usage: bash tools/k1_ab.sh <tag> <variant> [rounds]: configs[1] bench leg, product library (new) vs
+# namazu_amd/libnmz_gpu_<variant>.so (old), alternating; prints ms/step and K1 alone
+tag=$1; v=$2; n=${3:-2}
+mkdir -p gpurun_out
+for i in $(seq 1 $n); do
+  timeout -k 10 120 python bench.py --legs replayable --no-cpu-baseline --e2e-traces 1 > gpurun_out/${tag}_new$i.json 2>/dev/null || exit $?
+  NMZ_LIB_PATH=$PWD/namazu_amd/libnmz_gpu_$v.so timeout -k 10 120 python bench.py --legs replayable --no-cpu-baseline --e2e-traces 1 > gpurun_out/${tag}_old$i.json 2>/dev/null || exit $?
+done
+for f in gpurun_out/${tag}_new*.json gpurun_out/${tag}_old*.json; do python3 -c "
+import json,sys;d=json.loads(open('$f').read().strip().splitlines()[-1]);print('$f', round(d['ms_per_step'],4), round(d['roofline']['kernel_ms_isolated'],4), d['roofline'].get('kernel_ms'))"; done

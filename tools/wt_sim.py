@@ -21,10 +21,11 @@ def build(cm, e, chi):
     for j, k in enumerate(keys):
         S[k & 0xFFFF] = j
     K = bitlen(n)
+    lb = K - 5 if K > 5 else 0  # levels above the 32-rank blocks
     nw = n // 32 + 1
     lv = []
     cur = S
-    for l in range(K):
+    for l in range(lb):
         k = K - l
         h = 1 << (k - 1)
         wb = [0] * nw
@@ -45,8 +46,23 @@ def build(cm, e, chi):
             nxt[(s0 + h + r1) if (v & h) else (j - r1)] = v
         assert None not in nxt
         cur = nxt
-    assert cur == list(range(n))
-    return dict(n=n, K=K, nw=nw, lv=lv, cm=cm_r, e=e_r, chi=list(chi) + [0xFFFFFFFF])
+    # level lb: the node of a 32-rank block b holds ranks [32b, 32b + 32) in position order; mk[b][o] = the set of
+    # those ranks (bit r & 31) among the node's first o entries
+    nb = n // 32 + 1
+    mk = []
+    for b in range(nb):
+        row = [0]
+        acc = 0
+        for j in range(32):
+            p = 32 * b + j
+            if p < n:
+                assert cur[p] >> 5 == b
+                acc |= 1 << (cur[p] & 31)
+            row.append(acc)
+        mk.append(row)
+    pm_lo = [max(S[:dd]) if dd else 0 for dd in range(n + 1)]
+    pm_hi = [max(S[dd:]) if dd < n else 0 for dd in range(n + 1)]
+    return dict(pm_lo=pm_lo, pm_hi=pm_hi, n=n, K=K, lb=lb, nw=nw, lv=lv, mk=mk, cm=cm_r, e=e_r, chi=list(chi) + [0xFFFFFFFF])
 
 
 def ones(lvl, s, p):
@@ -56,14 +72,14 @@ def ones(lvl, s, p):
 
 def query(img, d, RA, RB, Hm, Hm2, m):
     """returns (W, keyA or None, keyB or None) following wt_seed_class after the searches."""
-    n, K, lv, cm, ev = img["n"], img["K"], img["lv"], img["cm"], img["e"]
+    n, lb, lv, mk, cm, ev = img["n"], img["lb"], img["lv"], img["mk"], img["cm"], img["e"]
+    K = img["K"]
     NONE = None
     oA = oB = d
     cA = cB = 0
-    lA = sA = qA = lB = sB = qB = None
     lA = lB = NONE
     sA = qA = sB = qB = 0
-    for l in range(K):
+    for l in range(lb):
         h = 1 << (K - l - 1)
         msk = ~(2 * h - 1)
         lvl = lv[l]
@@ -87,20 +103,25 @@ def query(img, d, RA, RB, Hm, Hm2, m):
         else:
             cB += o
             oB = z
-    cA += oA
-    cB += oB
+    # the 32-rank block of R: its first o entries are the node's prefix elements
+    F = 0xFFFFFFFF
+    mA = mk[RA >> 5][oA]
+    mB = mk[RB >> 5][oB]
+    rA, rB = RA & 31, RB & 31
+    cA += bin(mA >> rA).count("1")
+    cB += bin(mB >> rB).count("1")
     W = cA + (n - RB) - cB
+    belA = mA & ((1 << rA) - 1)
+    belB = (~mB & F) & ((1 << rB) - 1)
     hasA, hasB = d > 0, d < n
-    wrapA, wrapB = lA is NONE, lB is NONE
-    if wrapA:
-        lA, sA, qA = 0, 0, d
-    if wrapB:
-        lB, sB, qB = 0, 0, d
-    if not hasA:
-        lA = K
-    if not hasB:
-        lB = K
-    for l in range(min(lA, lB), K):
+    hitA, hitB = belA != 0, belB != 0
+    wrapA = not hitA and lA is NONE
+    wrapB = not hitB and lB is NONE
+    dA = hasA and not hitA and not wrapA  # descend from the tracked level
+    dB = hasB and not hitB and not wrapB
+    lA = lA if dA else lb
+    lB = lB if dB else lb
+    for l in range(min(lA, lB), lb):
         h = 1 << (K - l - 1)
         lvl = lv[l]
         if l >= lA:
@@ -116,13 +137,32 @@ def query(img, d, RA, RB, Hm, Hm2, m):
                 qB = o
             else:
                 qB -= o
+    def top(x):
+        return x.bit_length() - 1
+    if hitA:
+        pA = (RA & ~31) + top(belA)
+    elif wrapA:
+        pA = img["pm_lo"][d]
+    else:
+        v = mk[sA >> 5][qA]
+        assert v
+        pA = sA + top(v)
+    if hitB:
+        pB = (RB & ~31) + top(belB)
+    elif wrapB:
+        pB = img["pm_hi"][d]
+    else:
+        size = min(n - sB, 32)
+        v = (~mk[sB >> 5][qB] & F) & (F >> (32 - size))
+        assert v
+        pB = sB + top(v)
     kA = kB = None
     if hasA:
-        t = (Hm + cm[sA] - (m if wrapA else 0)) % (1 << 32)
-        kA = (t << 32) | (0xFFFFFFFF - ev[sA])
+        t = (Hm + cm[pA] - (m if wrapA else 0)) % (1 << 32)
+        kA = (t << 32) | (0xFFFFFFFF - ev[pA])
     if hasB:
-        t = (Hm2 + cm[sB] - (m if wrapB else 0)) % (1 << 32)
-        kB = (t << 32) | (0xFFFFFFFF - ev[sB])
+        t = (Hm2 + cm[pB] - (m if wrapB else 0)) % (1 << 32)
+        kB = (t << 32) | (0xFFFFFFFF - ev[pB])
     return W, kA, kB
 
 
@@ -144,7 +184,7 @@ def main():
     trials = int(sys.argv[1]) if len(sys.argv) > 1 else 300
     rng = random.Random(7)
     for t in range(trials):
-        n = rng.choice([9, 10, 31, 32, 33, 63, 64, 65, 100, 127, 128, 129, 200, 255, 256, 257, 511, 512, 700])
+        n = rng.choice([9, 10, 15, 16, 31, 32, 33, 63, 64, 65, 96, 100, 127, 128, 129, 200, 255, 256, 257, 511, 512, 700, 1024, 2079])
         m = rng.choice([1, 2, 3, 7, 100, 1000, 10 ** 8, (1 << 30) - 1, (1 << 31) + 5, (1 << 32) - 1])
         dup = rng.random() < 0.3
         vals = [rng.randrange(m) for _ in range(max(1, n // 8 if dup else n))]
