@@ -954,6 +954,7 @@ def bench_group(args, torch):
         t0 = time.perf_counter()
         ep = G.EdGroupPlan(g, ts, 32)
         eplan_ms = (time.perf_counter() - t0) * 1e3
+        eplan_parts = ep.timing()  # per local device: 1/N share upload, RCCL all_gather, device plan build
         ep.knn(8)
         t0 = time.perf_counter()
         for _ in range(args.ed_steps):
@@ -963,7 +964,10 @@ def bench_group(args, torch):
         pairs = N * (N - 1) // 2
         sec.append(dict(metric="trace-pair edit distances/s (banded, all-pairs k-NN)", value=pairs * args.ed_steps / el,
                         unit="pairs/s", n_gpus=n_dev, steps=args.ed_steps, ms_per_step=el / args.ed_steps * 1e3,
-                        scaling="strong", plan_ms=eplan_ms,
+                        scaling="strong", plan_ms=eplan_ms, plan_upload_ms=eplan_parts["upload_ms"],
+                        plan_gather_ms=eplan_parts["gather_ms"], plan_build_ms=eplan_parts["build_ms"],
+                        plan_note="the store reaches each device as a 1/N share + one RCCL all_gather, then the plan "
+                                  "is built from device memory (nmz_ed_group_plan_create); times per local device",
                         config={"workload": "configs[2] clustered all-pairs search through a device group (C ABI)",
                                 "traces": N, "events": 2048, "band": 32, "k": 8, "shards": n_shards},
                         what="per step: nmz_ed_group_allpairs_knn -- shards, per-rank merge, RCCL all_gather, merge, "

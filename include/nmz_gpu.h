@@ -140,6 +140,11 @@ int nmz_fnv1a64_batch_host(const uint64_t *off, const uint8_t *bytes, uint64_t n
  * delivered-delay error of the online path. */
 typedef struct nmz_tbqueue nmz_tbqueue;
 int nmz_tbqueue_create(nmz_tbqueue **out);
+/* close: no further enqueues; every consumer blocked in dequeue (and every later dequeue) returns NMZ_EAGAIN.
+ * destroy: closes, joins the timer thread, waits until no call is inside dequeue, then frees the queue. A caller
+ * must not start a call on the queue once destroy has begun (close first, let the consumers return, then
+ * destroy: namazu_amd/explorepolicy.py ActionChannel.close). */
+int nmz_tbqueue_close(nmz_tbqueue *q);
 int nmz_tbqueue_destroy(nmz_tbqueue *q);
 int64_t nmz_monotonic_ns(void);
 int nmz_tbqueue_enqueue(nmz_tbqueue *q, uint64_t id, int64_t due_ns);
@@ -183,7 +188,8 @@ int nmz_replayable_plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uin
                                uint64_t max_seeds, nmz_replayable_plan **out);
 int nmz_replayable_plan_destroy(nmz_replayable_plan *plan);
 /* Which statistics kernel the plan's sweeps take (diagnostic): 2 = wavelet-tree statistics (k_replayable_sweep_wt,
- * the default when 0 < max_interval < 2^32, every hint-length class has <= 4,096 events and the row image fits LDS),
+ * the default when 0 < max_interval < 2^32, the trace has <= 65,536 events -- a hint-length class of 4,096 or more
+ * splits into sub-segments -- and the row image fits LDS),
  * 1 = order-query statistics (k_replayable_sweep_oq), 0 = per-decision sweeps; -1 for a NULL plan. The environment
  * variable NMZ_REPLAY_WT=0 at plan creation skips the wavelet trees (A/B runs). */
 int nmz_replayable_plan_kernel(const nmz_replayable_plan *plan);
@@ -291,7 +297,10 @@ int nmz_ed_allpairs_knn_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys,
  * unchanged. (nmz_ed_allpairs_knn[_dev] fill by themselves.) */
 /* Host-only (no device work): the shard that owns query block qb (queries 64 qb .. 64 qb + 63) of the two-phase
  * bit-parallel search under nmz_ed_allpairs_knn_shard_dev with n_shards shards: every pair (i, j), i < j, belongs
- * to the shard of block i / 64 (MurmurHash3's 64-bit finaliser of qb, mod n_shards). tests/test_dist_cpu.py deals
+ * to the shard of block i / 64, in rotated snake order (in each period of 2 n_shards blocks, block r and its mirror
+ * 2 n_shards - 1 - r form pair p = min(r, 2 n_shards - 1 - r), which goes to shard (p + period) mod n_shards). A
+ * fixed rule, the same in every process (no environment knob). A shard whose entry lists exceed the two-phase limit
+ * runs its own query blocks in batches, so every shard of a search deals by this rule. tests/test_dist_cpu.py deals
  * pairs by it. */
 uint32_t nmz_ed_block_shard(uint32_t qb, uint32_t n_shards);
 int nmz_ed_allpairs_knn_shard_dev(nmz_ed_plan *plan, uint32_t k, uint32_t shard, uint32_t n_shards,
@@ -352,10 +361,12 @@ int nmz_unique_traces_dev(nmz_ctx *ctx, const uint64_t *d_off, const uint64_t *d
  * devices, created once. Work is cut into n_shards shards (0 = one per rank; more than the ranks = "virtual"
  * shards, so a single GPU runs the sharding and merge logic of any shard count); shard s runs on rank
  * s mod n_ranks. Sweeps shard by contiguous seed range (sizes differ by <= 1), the all-pairs search by the
- * plan's tile hash (nmz_ed_allpairs_knn_shard_dev). Each rank merges its shards on its device, one RCCL
+ * plan's query-block deal (rotated snake order, nmz_ed_block_shard). Each rank merges its shards on its device,
+ * one RCCL
  * all_gather over xGMI exchanges the ranks' lists, and a deterministic merge -- (n_fault desc, sum_delay desc,
  * seed asc) for top-k, (dist asc, id asc) for k-NN -- makes the result identical to one unsharded call.
- * Group calls are synchronous and serialised per group; host buffers are borrowed for the call only. */
+ * Group calls are synchronous and serialised per group; host buffers are borrowed for the call only. A group call
+ * never changes the calling thread's current HIP device (nor does any single-context call). */
 typedef struct nmz_group nmz_group;
 #define NMZ_GROUP_ID_BYTES 128
 /* bit d of dev_mask = device d */
@@ -365,6 +376,8 @@ int nmz_open_group(uint32_t dev_mask, uint32_t n_shards, nmz_group **out);
  * the merged results. stats outputs hold the seeds of this rank's shards only. */
 int nmz_group_unique_id(uint8_t *id /* [NMZ_GROUP_ID_BYTES] */);
 int nmz_open_group_rank(const uint8_t *id, int n_ranks, int rank, int device, uint32_t n_shards, nmz_group **out);
+/* Waits for a group call already in progress, then frees the group; NMZ_EINVAL while group plans made on it are
+ * still alive (destroy them first). No call on the group may start once close has begun. */
 int nmz_close_group(nmz_group *g);
 int nmz_group_info(const nmz_group *g, int *n_ranks, int *n_local_devices, uint32_t *n_shards);
 
@@ -399,10 +412,15 @@ int nmz_random_sweep_topk_group(nmz_group *g, uint64_t seed0, uint64_t n_seeds, 
                                 const uint8_t *evclass, uint32_t n_events, const nmz_random_params *params,
                                 uint32_t k, nmz_sched_stats *stats, nmz_topk_entry *topk);
 
-/* all-pairs banded edit-distance k-NN over a group (as nmz_ed_allpairs_knn): every device holds the store. */
+/* all-pairs banded edit-distance k-NN over a group (as nmz_ed_allpairs_knn): every device holds the store. The
+ * store reaches the devices as 1/n_ranks shares: rank r uploads symbols [r S, r S + S) (S = ceil(total / n_ranks))
+ * through its own PCIe link, one RCCL all_gather over xGMI assembles the store on every device, and each device
+ * builds its plan from device memory (nmz_ed_plan_create_dev). nmz_ed_group_plan_timing reports, per local device,
+ * the share upload, the all_gather and the device plan build (ms, arrays of nmz_group_info's n_local_devices). */
 typedef struct nmz_ed_group_plan nmz_ed_group_plan;
 int nmz_ed_group_plan_create(nmz_group *g, const uint64_t *off, const uint64_t *sym, uint32_t n_traces,
                              uint32_t band, nmz_ed_group_plan **out);
+int nmz_ed_group_plan_timing(const nmz_ed_group_plan *gp, double *upload_ms, double *gather_ms, double *build_ms);
 int nmz_ed_group_plan_destroy(nmz_ed_group_plan *gp);
 int nmz_ed_group_allpairs_knn(nmz_ed_group_plan *gp, uint32_t k, uint32_t *knn_id, uint32_t *knn_dist);
 int nmz_ed_allpairs_knn_group(nmz_group *g, const uint64_t *off, const uint64_t *sym, uint32_t n_traces,

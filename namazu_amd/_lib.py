@@ -11,7 +11,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 # NMZ_LIB_PATH: an alternative in-tree build of the same library (tuning variants)
-LIB_PATH = os.environ.get("NMZ_LIB_PATH") or os.path.join(HERE, "libnmz_gpu.so")
+DEFAULT_LIB_PATH = os.path.join(HERE, "libnmz_gpu.so")
+LIB_PATH = os.environ.get("NMZ_LIB_PATH") or DEFAULT_LIB_PATH
 
 NMZ_OK = 0
 NMZ_EINVAL = -1
@@ -100,6 +101,7 @@ SIGNATURES = {
     "nmz_replayable_decide_host": (_int, [_P, _u32, _P, _P, _u32, _i64, _P]),
     "nmz_fnv1a64_batch_host": (_int, [_P, _P, _u64, _P]),
     "nmz_tbqueue_create": (_int, [ctypes.POINTER(_P)]),
+    "nmz_tbqueue_close": (_int, [_P]),
     "nmz_tbqueue_destroy": (_int, [_P]),
     "nmz_monotonic_ns": (_i64, []),
     "nmz_tbqueue_enqueue": (_int, [_P, _u64, _i64]),
@@ -122,6 +124,7 @@ SIGNATURES = {
     "nmz_random_sweep_topk_group": (_int, [_P, _u64, _u64, _P, _P, _u32, _P, _u32, _P, _P]),
     "nmz_ed_group_plan_create": (_int, [_P, _P, _P, _u32, _u32, ctypes.POINTER(_P)]),
     "nmz_ed_group_plan_destroy": (_int, [_P]),
+    "nmz_ed_group_plan_timing": (_int, [_P, _P, _P, _P]),
     "nmz_ed_group_allpairs_knn": (_int, [_P, _u32, _P, _P]),
     "nmz_ed_allpairs_knn_group": (_int, [_P, _P, _P, _u32, _u32, _u32, _P, _P]),
     "nmz_timing_enable": (_int, [_P, _int]),
@@ -153,7 +156,10 @@ def load():
             L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
         except OSError as e:
             raise NmzLibraryError(f"failed to load {LIB_PATH}: {e}") from e
+        variant = LIB_PATH != DEFAULT_LIB_PATH  # an A/B build (NMZ_LIB_PATH) may predate newer entry points
         for name, (res, args) in SIGNATURES.items():
+            if variant and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -400,6 +400,9 @@ struct nmz_ed_plan {
     std::map<uint64_t, nmz::DevBuf> tile_list;      // per (shard, n_shards): the shard's tiles (qb << 32 | cb)
     std::map<uint64_t, uint64_t> tile_count;
     nmz::DevBuf tp_mem, tp_ent, tp_mask;
+    // fixed at creation (NMZ_ED_QGRAM / NMZ_ED_TWO_PHASE, A/B knobs read once per plan), so every shard and every
+    // call of one plan takes the same search and deals pairs by the same rule
+    bool qgram = true, two_phase = true;
     uint16_t *d_qsym = nullptr, *d_csym = nullptr;
     uint64_t *d_qoff = nullptr, *d_coff = nullptr;
     uint32_t *d_gmax = nullptr, *d_len = nullptr;
@@ -708,6 +711,8 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
     NMZ_CHECK(N == 0 || off, "off is NULL");
     *out = nullptr;
     auto *p = new nmz_ed_plan();
+    p->qgram = ed_qgram_enabled();
+    p->two_phase = ed_two_phase_enabled();
     p->ctx = ctx;
     p->n = N;
     p->band = band;
@@ -727,6 +732,8 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         delete p;
         if (!not_applicable) return rc;
         p = new nmz_ed_plan();  // alphabet too large for the bit-parallel tables: host build below
+        p->qgram = ed_qgram_enabled();
+        p->two_phase = ed_two_phase_enabled();
         p->ctx = ctx;
         p->n = N;
         p->band = band;
@@ -741,6 +748,8 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         delete p;
         if (rc != 1) return rc;
         p = new nmz_ed_plan();  // alphabet or tables too large: the host build below
+        p->qgram = ed_qgram_enabled();
+        p->two_phase = ed_two_phase_enabled();
         p->ctx = ctx;
         p->n = N;
         p->band = band;
@@ -993,32 +1002,18 @@ uint32_t ed_bv_item() {
 constexpr uint64_t ED_TP_MAX_ENTRIES = 1ULL << 30;  // 4 GiB of entries
 constexpr uint64_t ED_TP_MAX_MASK_BYTES = 4ULL << 30;
 
-// MurmurHash3's 64-bit finaliser (host)
-static inline uint64_t tile_mix(uint64_t x) {
-    x ^= x >> 33;
-    x *= 0xff51afd7ed558ccdULL;
-    x ^= x >> 33;
-    x *= 0xc4ceb9fe1a85ec53ULL;
-    return x ^ (x >> 33);
-}
-// The shard that owns query block qb (64 queries) of the two-phase search. Snake order (0, 1, .., S-1, S-1, .., 0,
-// repeated): a query block's work falls with qb inside the upper triangle (fewer candidates j > q) and inside
-// every family of near-duplicates, and each period of 2S blocks gives every shard one block from the front half and
-// its mirror from the back half, so linear trends cancel (NMZ_ED_DEAL=hash: the MurmurHash3 deal, for A/B runs).
+// The shard that owns query block qb (64 queries) of the two-phase search: rotated snake order. A query block's
+// work falls with qb inside the upper triangle (fewer candidates j > q) and inside every family of near-duplicates;
+// in each period of 2S blocks, block r and its mirror 2S-1-r form pair min(r, 2S-1-r), so linear trends cancel, and
+// the pair goes to shard (pair + period) mod S, so over the periods every shard takes every pair position. (A plain
+// snake gives shard s the same two positions in every period: when the work's own period matches -- families of 16
+// blocks at 8 shards -- shard 0 always held each family's first and last block, whose short candidate lists run the
+// DP less efficiently (1.15x); the MurmurHash3 deal of round 2 left max/mean 1.15. DESIGN.md section 6.) A fixed
+// rule, not a knob: one process per GPU computes its own shards' tiles, so the rule must be the same everywhere.
 static uint32_t ed_block_shard(uint32_t qb, uint32_t n_shards) {
     if (n_shards <= 1) return 0;
-    const char *e = getenv("NMZ_ED_DEAL");
-    if (e && std::string(e) == "hash") return (uint32_t)(tile_mix(qb) % n_shards);
-    // snake: in each period of 2S blocks, block r and its mirror 2S-1-r form pair min(r, 2S-1-r); the pair goes to
-    // shard (pair + period) mod S (rotated snake), so over the periods every shard takes every pair position. A
-    // plain snake (shard = pair, NMZ_ED_DEAL=snake) gives shard s the same two positions in every period: when the
-    // work's own period matches (families of 16 blocks at 8 shards), shard 0 always holds each family's first and
-    // last block -- equal work, but the last block's short candidate lists run the DP less efficiently (1.15x)
-    const char *u = getenv("NMZ_ED_DEAL_UNIT");  // blocks per dealt unit (A/B)
-    const uint32_t unit = u && atoi(u) > 0 ? (uint32_t)atoi(u) : 1u, q = qb / unit;
-    const uint32_t r = q % (2 * n_shards), pr = r < n_shards ? r : 2 * n_shards - 1 - r;
-    if (e && std::string(e) == "snake") return pr;
-    return (pr + q / (2 * n_shards)) % n_shards;
+    const uint32_t r = qb % (2 * n_shards), pr = r < n_shards ? r : 2 * n_shards - 1 - r;
+    return (pr + qb / (2 * n_shards)) % n_shards;
 }
 // the entry-list limit (NMZ_ED_TP_MAX_ENTRIES lowers it, so tests can force the single-kernel fallback)
 static uint64_t ed_tp_max_entries() {
@@ -1046,25 +1041,41 @@ __global__ __launch_bounds__(1024) void k_sum_u32_u64(const uint32_t *__restrict
     }
 }
 
-static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A) {
+// The shard's tiles in query-block order; the count pass sizes the entry lists. Entry lists beyond
+// ed_tp_max_entries() are split: the shard's query blocks run in batches (whole blocks, at least one per batch) whose
+// entries fit, each batch a count pass, scans, the write pass and the DP. Every shard of a search therefore covers
+// exactly its own query blocks, whatever its entry total (a single-kernel fallback per shard deals pairs by a
+// different rule, and shards that chose differently would drop or double pairs). Returns 1 only when the plan
+// cannot take the two-phase search at all (N >= 2^30: entries carry j in 30 bits), the same on every shard.
+static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t *d_knn) {
     const uint32_t N = p->n, n_pairs = (N + 1) / 2, QB = (N + 63) / 64, NCB = (N + 255) / 256;
     const uint32_t shard = A.shard, n_shards = A.n_shards;
-    if (N >= (1u << 30)) return 1;  // entries carry j in 30 bits
-    // this shard's tiles (qb << 32 | cb), built and uploaded once per (shard, n_shards): every tile of query block
-    // qb belongs to shard ed_block_shard(qb). Whole query blocks, so a query pair's DP entries stay in one
-    // shard's work items: dealt by tile, a pair's near-duplicate candidates (a few 256-wide tiles) spread over
+    if (N >= (1u << 30)) return 1;
+    // this shard's tiles (qb << 32 | cb), built and uploaded once per (shard, n_shards): every tile of
+    // query block qb belongs to shard ed_block_shard(qb). Whole query blocks, so a query pair's DP entries stay in
+    // one shard's work items: dealt by tile, a pair's near-duplicate candidates (a few 256-wide tiles) spread over
     // several shards, every shard built the pair's Peq tables for a fraction of its entries, and the 8 shards
     // summed to 1.15x the unsharded search. The DP work is data-dependent and clustered (the clustered workload's
     // families put it next to the diagonal, with a period of 16 query blocks); a hash breaks that periodicity,
     // where a round-robin deal aligned with it (8 shards: max/mean shard time 1.27)
     const uint64_t key = ((uint64_t)shard << 32) | n_shards;
     DevBuf &tl = p->tile_list[key];
-    if (!p->tile_count.count(key)) {
-        std::vector<uint64_t> tiles;
+    std::vector<uint32_t> qb_tiles;  // the shard's query blocks and their first tiles (for batches)
+    auto shard_tiles = [&](std::vector<uint64_t> *tiles) {
+        uint64_t t = 0;
+        qb_tiles.clear();
         for (uint32_t qb = 0; qb < QB; ++qb) {
             if (ed_block_shard(qb, n_shards) != shard) continue;
-            for (uint32_t cb = qb / 4; cb < NCB; ++cb) tiles.push_back(((uint64_t)qb << 32) | cb);
+            qb_tiles.push_back(qb);
+            qb_tiles.push_back((uint32_t)t);
+            for (uint32_t cb = qb / 4; cb < NCB; ++cb, ++t)
+                if (tiles) tiles->push_back(((uint64_t)qb << 32) | cb);
         }
+        return t;
+    };
+    if (!p->tile_count.count(key)) {
+        std::vector<uint64_t> tiles;
+        shard_tiles(&tiles);
         NMZ_TRY(tl.ensure(Carve::bytes_for(tiles.size() + 1, 8)));
         if (!tiles.empty()) NMZ_HIP(hipMemcpy(tl.ptr, tiles.data(), tiles.size() * 8, hipMemcpyHostToDevice));
         p->tile_count[key] = tiles.size();
@@ -1080,19 +1091,19 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A) {
     uint32_t *d_items = cv.take<uint32_t>(n_pairs + 1), *d_ioff = cv.take<uint32_t>(n_pairs + 1);
     uint32_t *d_cur = cv.take<uint32_t>(n_pairs + 1);
     void *d_scan = cv.take<char>(scan_bytes);
+    const uint64_t n_tiles_all = p->tile_count[key];
     EdQgArgs Q;
     Q.prof = A.prof;
     Q.len = A.len;
     Q.knn = A.knn;
     Q.counters = A.counters;
-    Q.tiles = tl.as<uint64_t>();
     Q.cnt = d_cnt;
     Q.cur = d_cur;
     Q.ent = nullptr;
-    Q.n_tiles = p->tile_count[key];
     // the count pass's survivor ballots (2 KiB per tile) let the write pass scatter without recomputing the filter
     Q.masks = nullptr;
-    if (Q.n_tiles * 2048 <= ED_TP_MAX_MASK_BYTES && p->tp_mask.ensure(Carve::bytes_for(Q.n_tiles * 2048, 1)) == NMZ_OK)
+    if (n_tiles_all * 2048 <= ED_TP_MAX_MASK_BYTES &&
+        p->tp_mask.ensure(Carve::bytes_for(n_tiles_all * 2048, 1)) == NMZ_OK)
         Q.masks = p->tp_mask.as<uint64_t>();
     Q.N = N;
     Q.k = A.k;
@@ -1101,36 +1112,72 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A) {
     Q.shard = shard;
     Q.n_shards = n_shards;
     Q.w = p->band;
-    NMZ_HIP(hipMemsetAsync(d_cnt, 0, (n_pairs + 1) * 4, st));
-    {
-        KernelTimer kt(p->ctx, st, "ed_qg_filter");
-        NMZ_TRY(ed_qg_filter_launch(Q, true, st));
-    }
-    NMZ_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_cnt, d_poff, (int)n_pairs + 1, st));
     const uint32_t item = ed_bv_item();
-    hipLaunchKernelGGL(k_bv_items, dim3(ceil_div(n_pairs + 1, 256)), dim3(256), 0, st, d_cnt, n_pairs, item, d_items);
-    NMZ_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_items, d_ioff, (int)n_pairs + 1, st));
-    // the entry total in 64 bits: the u32 scans above wrap beyond 2^32 entries (about N^2 / 4 for a store of
-    // near-duplicates), so their totals are trusted only once this sum is within ED_TP_MAX_ENTRIES
-    hipLaunchKernelGGL(k_sum_u32_u64, dim3(1), dim3(1024), 0, st, d_cnt, n_pairs, d_tot64);
-    NMZ_HIP(hipGetLastError());
+    // count pass + scans over tiles [t0, t1): entry and item totals
+    auto count = [&](uint64_t t0, uint64_t t1, uint64_t &tot64, uint32_t &tot_items) -> int {
+        Q.tiles = tl.as<uint64_t>() + t0;
+        Q.n_tiles = t1 - t0;
+        NMZ_HIP(hipMemsetAsync(d_cnt, 0, (n_pairs + 1) * 4, st));
+        {
+            KernelTimer kt(p->ctx, st, "ed_qg_filter");
+            NMZ_TRY(ed_qg_filter_launch(Q, true, st));
+        }
+        NMZ_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_cnt, d_poff, (int)n_pairs + 1, st));
+        hipLaunchKernelGGL(k_bv_items, dim3(ceil_div(n_pairs + 1, 256)), dim3(256), 0, st, d_cnt, n_pairs, item,
+                           d_items);
+        NMZ_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_items, d_ioff, (int)n_pairs + 1, st));
+        // the entry total in 64 bits: the u32 scans above wrap beyond 2^32 entries (about N^2 / 4 for a store of
+        // near-duplicates), so their totals are trusted only once this sum is within the limit
+        hipLaunchKernelGGL(k_sum_u32_u64, dim3(1), dim3(1024), 0, st, d_cnt, n_pairs, d_tot64);
+        NMZ_HIP(hipGetLastError());
+        NMZ_HIP(hipMemcpyAsync(&tot64, d_tot64, 8, hipMemcpyDeviceToHost, st));
+        NMZ_HIP(hipMemcpyAsync(&tot_items, d_ioff + n_pairs, 4, hipMemcpyDeviceToHost, st));
+        NMZ_HIP(hipStreamSynchronize(st));
+        return NMZ_OK;
+    };
+    // write pass + DP of the tiles the last count pass covered
+    auto write_dp = [&](uint64_t n_ent, uint32_t n_items) -> int {
+        NMZ_TRY(p->tp_ent.ensure(Carve::bytes_for(n_ent + 1, 4)));
+        Q.ent = p->tp_ent.as<uint32_t>();
+        NMZ_HIP(hipMemcpyAsync(d_cur, d_poff, (uint64_t)n_pairs * 4, hipMemcpyDeviceToDevice, st));
+        {
+            KernelTimer kt(p->ctx, st, "ed_qg_filter");
+            if (Q.masks) NMZ_TRY(ed_qg_scatter_launch(Q, st));
+            else NMZ_TRY(ed_qg_filter_launch(Q, false, st));
+        }
+        KernelTimer kt(p->ctx, st, "ed_bv_dp");
+        return ed_bv_dp_launch(A, d_ioff, d_poff, Q.ent, n_pairs, n_items, item, p->bw, p->cmp, st);
+    };
     uint64_t tot64 = 0;
     uint32_t tot_items = 0;
-    NMZ_HIP(hipMemcpyAsync(&tot64, d_tot64, 8, hipMemcpyDeviceToHost, st));
-    NMZ_HIP(hipMemcpyAsync(&tot_items, d_ioff + n_pairs, 4, hipMemcpyDeviceToHost, st));
-    NMZ_HIP(hipStreamSynchronize(st));
-    if (tot64 > ed_tp_max_entries()) return 1;
-    const uint64_t n_ent = tot64, n_items = tot_items;
-    NMZ_TRY(p->tp_ent.ensure(Carve::bytes_for(n_ent + 1, 4)));
-    Q.ent = p->tp_ent.as<uint32_t>();
-    NMZ_HIP(hipMemcpyAsync(d_cur, d_poff, (uint64_t)n_pairs * 4, hipMemcpyDeviceToDevice, st));
-    {
-        KernelTimer kt(p->ctx, st, "ed_qg_filter");
-        if (Q.masks) NMZ_TRY(ed_qg_scatter_launch(Q, st));
-        else NMZ_TRY(ed_qg_filter_launch(Q, false, st));
+    NMZ_TRY(count(0, n_tiles_all, tot64, tot_items));
+    const uint64_t limit = ed_tp_max_entries();
+    if (tot64 <= limit) return write_dp(tot64, tot_items);
+    // batches of whole query blocks: per-block totals from this count pass, then the lists and counters start over
+    // (the count pass lists pairs with an empty trace, and adds to the counters)
+    std::vector<uint32_t> cnt(n_pairs);
+    NMZ_HIP(hipMemcpy(cnt.data(), d_cnt, (size_t)n_pairs * 4, hipMemcpyDeviceToHost));
+    shard_tiles(nullptr);
+    const size_t nq = qb_tiles.size() / 2;
+    hipLaunchKernelGGL(k_knn_init, dim3(ceil_div((uint64_t)N * A.k, 256)), dim3(256), 0, st, d_knn, (uint64_t)N * A.k);
+    NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_CNT_WORDS * 8, st));
+    for (size_t b0 = 0; b0 < nq;) {
+        uint64_t acc = 0;
+        size_t b1 = b0;
+        while (b1 < nq) {
+            const uint32_t qb = qb_tiles[2 * b1];
+            uint64_t c = 0;
+            for (uint32_t pp = 32 * qb; pp < std::min(32 * qb + 32, n_pairs); ++pp) c += cnt[pp];
+            if (b1 > b0 && acc + c > limit) break;
+            acc += c;
+            ++b1;
+        }
+        const uint64_t t0 = qb_tiles[2 * b0 + 1], t1 = b1 < nq ? qb_tiles[2 * b1 + 1] : n_tiles_all;
+        NMZ_TRY(count(t0, t1, tot64, tot_items));
+        NMZ_TRY(write_dp(tot64, tot_items));
+        b0 = b1;
     }
-    KernelTimer kt(p->ctx, st, "ed_bv_dp");
-    return ed_bv_dp_launch(A, d_ioff, d_poff, Q.ent, n_pairs, (uint32_t)n_items, item, p->bw, p->cmp, st);
+    return NMZ_OK;
 }
 
 static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_knn, uint32_t shard = 0,
@@ -1168,7 +1215,7 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
         A.chunk_start = p->d_chunk_start;
         A.knn = d_knn;
         A.counters = p->d_counters;
-        A.prof = ed_qgram_enabled() ? (const uint4 *)p->d_prof : nullptr;
+        A.prof = p->qgram ? (const uint4 *)p->d_prof : nullptr;
         A.N = N;
         A.G = p->G;
         A.k = k;
@@ -1182,17 +1229,12 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
         A.n_shards = n_shards;
         NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_CNT_WORDS * 8, st));
         int rc = 1;
-        if (A.prof && ed_two_phase_enabled()) {  // filter tiles + DP work items (the search's "ed_bv" time)
+        if (A.prof && p->two_phase) {  // filter tiles + DP work items (the search's "ed_bv" time)
             KernelTimer kt(p->ctx, st, "ed_bv");
-            rc = ed_bv_two_phase(p, st, A);
+            rc = ed_bv_two_phase(p, st, A, d_knn);
             if (rc < 0) return rc;
         }
-        if (rc == 1) {  // the single-kernel search (no q-gram filter, or entry lists beyond ED_TP_MAX_ENTRIES)
-            // the two-phase count pass may already have listed pairs with an empty trace: start from empty
-            // lists, or the single kernel would list them a second time
-            if (A.prof && ed_two_phase_enabled())
-                hipLaunchKernelGGL(k_knn_init, dim3(ceil_div((uint64_t)N * k, 256)), dim3(256), 0, st, d_knn,
-                                   (uint64_t)N * k);
+        if (rc == 1) {  // the single-kernel search (no q-gram filter, or N >= 2^30): a plan-wide choice
             // this shard's chunks per row: cr = ((shard - b) mod n_shards) + n_shards * t
             std::vector<uint64_t> &ss = p->shard_start[((uint64_t)shard << 32) | n_shards];
             if (ss.empty()) {
@@ -1384,7 +1426,7 @@ int nmz_ed_plan_query_knn(nmz_ed_plan *plan, const uint64_t *q_off, const uint64
             A.nq[i] = (uint32_t)(q_off[qq + 1] - q_off[qq]);
         }
         A.knn = d_knn + (uint64_t)q * k;
-        A.prof = ed_qgram_enabled() ? (const uint4 *)plan->d_prof : nullptr;
+        A.prof = plan->qgram ? (const uint4 *)plan->d_prof : nullptr;
         A.N = N;
         A.k = k;
         A.lds_dw = plan->lds_dw;

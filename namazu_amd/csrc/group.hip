@@ -16,6 +16,7 @@
 // -- (n_fault desc, sum_delay desc, seed asc) / (dist asc, id asc) -- gives every rank the same result.
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -95,7 +96,8 @@ struct nmz_group {
     int n_ranks = 1;
     uint32_t n_shards = 1;
     bool multi_process = false;
-    std::mutex mu;  // group calls are serialised (their contexts and scratch are the group's own)
+    std::mutex mu;        // group calls are serialised (their contexts and scratch are the group's own)
+    uint32_t n_plans = 0;  // live group plans (nmz_close_group refuses to free a group they still use)
 };
 
 namespace nmz {
@@ -246,6 +248,7 @@ struct nmz_ed_group_plan {
     nmz_group *g;
     std::vector<nmz_ed_plan *> p;
     uint32_t n;
+    std::vector<double> upload_ms, gather_ms, build_ms;  // per local member (nmz_ed_group_plan_timing)
 };
 
 namespace nmz {
@@ -322,6 +325,7 @@ static int group_merge_knn(GroupMember &mb, uint64_t *parts, uint32_t n_parts, u
 extern "C" {
 
 int nmz_open_group(uint32_t dev_mask, uint32_t n_shards, nmz_group **out) {
+    DeviceRestore dr;  // the caller keeps its own current device
     NMZ_CHECK(out != nullptr, "out is NULL");
     *out = nullptr;
     int n = 0;
@@ -368,6 +372,7 @@ int nmz_group_unique_id(uint8_t *id) {
 }
 
 int nmz_open_group_rank(const uint8_t *id, int n_ranks, int rank, int device, uint32_t n_shards, nmz_group **out) {
+    DeviceRestore dr;  // the caller keeps its own current device
     NMZ_CHECK(out && id, "NULL argument");
     *out = nullptr;
     NMZ_CHECK(n_ranks >= 1 && rank >= 0 && rank < n_ranks, "bad rank");
@@ -398,9 +403,12 @@ int nmz_open_group_rank(const uint8_t *id, int n_ranks, int rank, int device, ui
 }
 
 int nmz_close_group(nmz_group *g) {
+    DeviceRestore dr;  // the caller keeps its own current device
     if (!g) return NMZ_OK;
-    {
+    {  // a call already inside the group finishes first (it holds the mutex); no call may start once close has
+       // begun (the caller's contract, include/nmz_gpu.h)
         std::lock_guard<std::mutex> lk(g->mu);
+        NMZ_CHECK(g->n_plans == 0, "the group still has live plans: destroy them before closing the group");
     }
     group_free(g);
     return NMZ_OK;
@@ -418,6 +426,7 @@ int nmz_group_info(const nmz_group *g, int *n_ranks, int *n_local_devices, uint3
 int nmz_replayable_group_plan_create(nmz_group *g, const uint32_t *hint_off, const uint8_t *hint_bytes,
                                      uint32_t n_events, int64_t max_interval_ns, uint64_t max_seeds_per_shard,
                                      nmz_replayable_group_plan **out) {
+    DeviceRestore dr;
     NMZ_CHECK(g && out, "NULL argument");
     *out = nullptr;
     std::lock_guard<std::mutex> lk(g->mu);
@@ -435,20 +444,24 @@ int nmz_replayable_group_plan_create(nmz_group *g, const uint32_t *hint_off, con
         delete gp;
         return fail(rc, msg);
     }
+    ++g->n_plans;
     *out = gp;
     return NMZ_OK;
 }
 
 int nmz_replayable_group_plan_destroy(nmz_replayable_group_plan *gp) {
+    DeviceRestore dr;
     if (!gp) return NMZ_OK;
     std::lock_guard<std::mutex> lk(gp->g->mu);
     (void)run_all(gp->g, [&](size_t i) { return nmz_replayable_plan_destroy(gp->p[i]); });
+    --gp->g->n_plans;
     delete gp;
     return NMZ_OK;
 }
 
 int nmz_replayable_group_sweep(nmz_replayable_group_plan *gp, const uint32_t *seed_off, const uint8_t *seed_bytes,
                                uint64_t n_seeds, uint32_t k, nmz_sched_stats *stats, nmz_topk_entry *topk) {
+    DeviceRestore dr;
     NMZ_CHECK(gp != nullptr, "plan is NULL");
     NMZ_CHECK(n_seeds == 0 || seed_off, "seed_off is NULL");
     nmz_group *g = gp->g;
@@ -498,6 +511,7 @@ int nmz_replayable_group_sweep(nmz_replayable_group_plan *gp, const uint32_t *se
 
 int nmz_replayable_group_sweep_decimal(nmz_replayable_group_plan *gp, uint64_t seed_lo, uint64_t n_seeds, uint32_t k,
                                        nmz_sched_stats *stats, nmz_topk_entry *topk) {
+    DeviceRestore dr;
     NMZ_CHECK(gp != nullptr, "plan is NULL");
     nmz_group *g = gp->g;
     std::lock_guard<std::mutex> lk(g->mu);
@@ -527,6 +541,7 @@ int nmz_replayable_sweep_topk_group(nmz_group *g, const uint32_t *seed_off, cons
 int nmz_random_group_plan_create(nmz_group *g, const uint64_t *evhash, const uint8_t *evclass, uint32_t n_events,
                                  const nmz_random_params *params, uint64_t max_seeds_per_shard,
                                  nmz_random_group_plan **out) {
+    DeviceRestore dr;
     NMZ_CHECK(g && out, "NULL argument");
     *out = nullptr;
     std::lock_guard<std::mutex> lk(g->mu);
@@ -544,20 +559,24 @@ int nmz_random_group_plan_create(nmz_group *g, const uint64_t *evhash, const uin
         delete gp;
         return fail(rc, msg);
     }
+    ++g->n_plans;
     *out = gp;
     return NMZ_OK;
 }
 
 int nmz_random_group_plan_destroy(nmz_random_group_plan *gp) {
+    DeviceRestore dr;
     if (!gp) return NMZ_OK;
     std::lock_guard<std::mutex> lk(gp->g->mu);
     (void)run_all(gp->g, [&](size_t i) { return nmz_random_plan_destroy(gp->p[i]); });
+    --gp->g->n_plans;
     delete gp;
     return NMZ_OK;
 }
 
 int nmz_random_group_sweep(nmz_random_group_plan *gp, uint64_t seed0, uint64_t n_seeds, uint32_t k,
                            nmz_sched_stats *stats, nmz_topk_entry *topk) {
+    DeviceRestore dr;
     NMZ_CHECK(gp != nullptr, "plan is NULL");
     nmz_group *g = gp->g;
     std::lock_guard<std::mutex> lk(g->mu);
@@ -587,34 +606,97 @@ int nmz_random_sweep_topk_group(nmz_group *g, uint64_t seed0, uint64_t n_seeds, 
 // ---- all-pairs banded edit distance k-NN ---------------------------------------------------------------------
 int nmz_ed_group_plan_create(nmz_group *g, const uint64_t *off, const uint64_t *sym, uint32_t n_traces,
                              uint32_t band, nmz_ed_group_plan **out) {
+    DeviceRestore dr;
     NMZ_CHECK(g && out, "NULL argument");
     *out = nullptr;
     std::lock_guard<std::mutex> lk(g->mu);
+    NMZ_CHECK(n_traces == 0 || (off && sym), "NULL argument");
     auto *gp = new nmz_ed_group_plan();
     gp->g = g;
     gp->n = n_traces;
     gp->p.assign(g->m.size(), nullptr);
-    // every device builds the same plan from the same host traces, concurrently on the workers
-    const int rc = run_all(g, [&](size_t i) { return nmz_ed_plan_create(g->m[i].ctx, off, sym, n_traces, band, &gp->p[i]); });
+    gp->upload_ms.assign(g->m.size(), 0.0);
+    gp->gather_ms.assign(g->m.size(), 0.0);
+    gp->build_ms.assign(g->m.size(), 0.0);
+    // The store reaches every device as a 1/R share through the device's own PCIe link (rank r uploads symbols
+    // [r S, r S + S), S = ceil(total / R), zero-padded) into its slot of a full-store buffer, one RCCL all_gather
+    // over xGMI fills the other slots in place, and each device builds the plan from device memory
+    // (nmz_ed_plan_create_dev; the plan reads the buffer during the call only). Before, every device pushed the
+    // whole store through its own link (configs[2]: 1.6 GB per device, 42 ms of a 59 ms plan). DESIGN.md section 6.
+    const uint64_t total = n_traces ? off[n_traces] : 0;
+    const uint64_t R = (uint64_t)g->n_ranks, share = std::max<uint64_t>((total + R - 1) / R, 1);
+    std::vector<DevBuf> full(g->m.size());
+    std::vector<void *> send(g->m.size()), recv(g->m.size());
+    using clk = std::chrono::steady_clock;
+    auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
+    int rc = run_all(g, [&](size_t i) {
+        const auto t0 = clk::now();
+        GroupMember &mb = g->m[i];
+        hipStream_t st = mb.ctx->stream;
+        NMZ_TRY(full[i].ensure(Carve::bytes_for(share * R, 8)));
+        uint64_t *d = full[i].as<uint64_t>();
+        const uint64_t lo = std::min<uint64_t>((uint64_t)mb.rank * share, total);
+        const uint64_t hi = std::min<uint64_t>(lo + share, total);
+        if (hi > lo) NMZ_HIP(hipMemcpyAsync(d + (uint64_t)mb.rank * share, sym + lo, (hi - lo) * 8, hipMemcpyHostToDevice, st));
+        if (hi - lo < share)
+            NMZ_HIP(hipMemsetAsync(d + (uint64_t)mb.rank * share + (hi - lo), 0, (share - (hi - lo)) * 8, st));
+        NMZ_HIP(hipStreamSynchronize(st));  // pageable source
+        send[i] = d + (uint64_t)mb.rank * share;
+        recv[i] = d;
+        gp->upload_ms[i] = ms_since(t0);
+        return NMZ_OK;
+    });
+    if (rc == NMZ_OK) {
+        const auto t0 = clk::now();
+        rc = group_allgather(g, send, recv, share * 8);
+        if (rc == NMZ_OK)
+            rc = run_all(g, [&](size_t i) {
+                NMZ_HIP(hipStreamSynchronize(g->m[i].ctx->stream));
+                gp->gather_ms[i] = ms_since(t0);
+                const auto t1 = clk::now();
+                NMZ_TRY(nmz_ed_plan_create_dev(g->m[i].ctx, off, full[i].as<uint64_t>(), n_traces, band, &gp->p[i]));
+                gp->build_ms[i] = ms_since(t1);
+                return NMZ_OK;
+            });
+    }
+    (void)run_all(g, [&](size_t i) {  // the plans hold what they need
+        (void)hipStreamSynchronize(g->m[i].ctx->stream);
+        full[i].release();
+        return NMZ_OK;
+    });
     if (rc != NMZ_OK) {
         const std::string msg = nmz_last_error();
         for (auto *p : gp->p) (void)nmz_ed_plan_destroy(p);
         delete gp;
         return fail(rc, msg);
     }
+    ++g->n_plans;
     *out = gp;
     return NMZ_OK;
 }
 
+int nmz_ed_group_plan_timing(const nmz_ed_group_plan *gp, double *upload_ms, double *gather_ms, double *build_ms) {
+    NMZ_CHECK(gp != nullptr, "plan is NULL");
+    for (size_t i = 0; i < gp->p.size(); ++i) {
+        if (upload_ms) upload_ms[i] = gp->upload_ms[i];
+        if (gather_ms) gather_ms[i] = gp->gather_ms[i];
+        if (build_ms) build_ms[i] = gp->build_ms[i];
+    }
+    return NMZ_OK;
+}
+
 int nmz_ed_group_plan_destroy(nmz_ed_group_plan *gp) {
+    DeviceRestore dr;
     if (!gp) return NMZ_OK;
     std::lock_guard<std::mutex> lk(gp->g->mu);
     (void)run_all(gp->g, [&](size_t i) { return nmz_ed_plan_destroy(gp->p[i]); });
+    --gp->g->n_plans;
     delete gp;
     return NMZ_OK;
 }
 
 int nmz_ed_group_allpairs_knn(nmz_ed_group_plan *gp, uint32_t k, uint32_t *knn_id, uint32_t *knn_dist) {
+    DeviceRestore dr;
     NMZ_CHECK(gp != nullptr, "plan is NULL");
     NMZ_CHECK(k >= 1 && k <= 64, "k must be in [1, 64]");
     nmz_group *g = gp->g;

@@ -90,9 +90,24 @@ struct KernelTimer {
     unsigned long long *span();
 };
 
-// RAII: bind the calling OS thread to the context's device (cgo threads migrate).
+// RAII: the caller's current HIP device is restored on return, so a call never changes the device of the thread
+// that made it (torch or other HIP work on that thread keeps its own).
+struct DeviceRestore {
+    int prev = -1;
+    DeviceRestore() {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    }
+    ~DeviceRestore() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// RAII: bind the calling OS thread to the context's device for the call (cgo threads migrate), then restore the
+// caller's device.
 struct CtxGuard {
     std::lock_guard<std::mutex> lk;
+    DeviceRestore restore;
     int rc = NMZ_OK;
     explicit CtxGuard(nmz_ctx *c) : lk(c->mu) {
         if (hipSetDevice(c->device) != hipSuccess) rc = fail(NMZ_EHIP, "hipSetDevice failed");

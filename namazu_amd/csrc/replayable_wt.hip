@@ -33,6 +33,7 @@ constexpr uint32_t WT_BRUTE = 8;       // segments of at most this many events: 
 constexpr uint32_t WT_NMAX = 4096;     // largest segment the plan kernel sorts in LDS
 constexpr uint32_t WT_LDS_MAX = 160 * 1024 - 256;  // dynamic LDS; the sweep kernel's few static bytes need the rest
 constexpr uint32_t WT_NONE = 0xffffffffu;
+constexpr uint32_t WT_PAD = 32;        // sentinels past Cm and C_hi: lifting searches of <= 5 rounds need no clamp
 
 struct WtClass {
     uint64_t pn;              // P^len
@@ -189,9 +190,9 @@ __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__re
         e_img[j] = (uint16_t)(0xffffu - ((kk >> 16) & 0xffffu));
         S0[kk & 0xffffu] = (uint16_t)j;
     }
-    if (tid == 0) {
-        cm_img[n] = ~0u;  // sentinels: never below a search bound
-        chi_img[n] = ~0u;
+    if (tid < WT_PAD) {
+        cm_img[n + tid] = ~0u;  // sentinels: never below a search bound
+        chi_img[n + tid] = ~0u;
     }
     // bucket indexes (first rank with Cm >= b << msh, b <= 256; first position with C_hi >= b << 24, b < 256): every
     // position writes the buckets between its predecessor's and its own (the sorted order's boundaries)
@@ -365,8 +366,13 @@ __device__ __forceinline__ uint32_t wt_ones(const uint2 *__restrict__ lvl, uint3
 
 // One seed's statistics over one segment: adds d Hm + (n - d) Hm2 to sum, the segment's wraps to W, and folds its
 // maximum key {t, ~e} into key.
+// wave-uniform constants the sweep keeps in VGPRs (operands of VOP2 forms)
+struct WtVConst {
+    uint32_t st4[5];  // lifting-search steps in bytes: 4 << r
+};
+
 template <bool BIG>
-__device__ __forceinline__ void wt_seed_class(const WtClass &ci, const char *__restrict__ img,
+__device__ __forceinline__ void wt_seed_class(const WtVConst &vc, const WtClass &ci, const char *__restrict__ img,
                                               const uint4 *__restrict__ row, uint64_t h0, uint32_t m, uint64_t mu,
                                               uint32_t m_k64, uint32_t msh, uint64_t &sum, uint32_t &W,
                                               uint64_t &key) {
@@ -392,13 +398,37 @@ __device__ __forceinline__ void wt_seed_class(const WtClass &ci, const char *__r
     const uint32_t XA = m - Hm, XB = m - Hm2;  // t wraps <=> Cm >= X
     // three lifting searches stepped together (every read of a round in flight at once) from the bucket starts:
     // every entry past the bucket is >= the bound, and the sentinel at n ends every probe past the array
-    uint32_t pd = ic[nh >> 24], RA = im[XA >> msh], RB = im[XB >> msh];
-    for (uint32_t st = (1u << ci.rS) >> 1; st; st >>= 1) {
-        const uint32_t a = chi[min(pd + st - 1, n)], b = cm[min(RA + st - 1, n)], c = cm[min(RB + st - 1, n)];
-        pd += a < nh ? st : 0u;
-        RA += b < XA ? st : 0u;
-        RB += c < XB ? st : 0u;
+    // (pointer form: a round's three probes are LDS reads with immediate offsets; WT_PAD sentinels end the probes of
+    // up to five rounds past the array, longer searches -- repeated hints -- clamp at the sentinel at n)
+    const uint32_t *pa = chi + ic[nh >> 24], *pb = cm + im[XA >> msh], *pc = cm + im[XB >> msh];
+    const uint32_t rS = ci.rS;
+#ifdef WT_ABL_LIFT
+    if (0)
+#endif
+    if (rS <= 5) {
+#pragma unroll
+        for (int r = 4; r >= 0; --r) {
+            if (rS > (uint32_t)r) {
+                constexpr uint32_t one = 1;
+                const uint32_t st = one << r, st4 = vc.st4[r];  // the step in bytes, in a VGPR (a VOP2 select)
+                const uint32_t a = pa[st - 1], b = pb[st - 1], c = pc[st - 1];
+                pa = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(pa) + (a < nh ? st4 : 0u));
+                pb = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(pb) + (b < XA ? st4 : 0u));
+                pc = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(pc) + (c < XB ? st4 : 0u));
+            }
+        }
+    } else {
+        const uint32_t *ea = chi + n, *eb = cm + n;
+        for (uint32_t st = (1u << rS) >> 1; st; st >>= 1) {
+            const uint32_t a = *min(pa + st - 1, ea), b = *min(pb + st - 1, eb), c = *min(pc + st - 1, eb);
+            pa += a < nh ? st : 0u;
+            pb += b < XA ? st : 0u;
+            pc += c < XB ? st : 0u;
+        }
     }
+    // (LDS addresses: the low words of the generic pointers)
+    auto lo = [](const uint32_t *q) { return (uint32_t)reinterpret_cast<uintptr_t>(q); };
+    const uint32_t pd = (lo(pa) - lo(chi)) >> 2, RA = (lo(pb) - lo(cm)) >> 2, RB = (lo(pc) - lo(cm)) >> 2;
     // d = #{C <= ~H}: #{C_hi < ~H_hi} plus the entries whose high word equals ~H_hi and low word is <= ~H_lo
     // (about n / 2^32 of the queries: the low words come from the table row)
     d = pd;
@@ -412,32 +442,58 @@ __device__ __forceinline__ void wt_seed_class(const WtClass &ci, const char *__r
     // off (the predecessor's subtree: node start s, prefix offset q)
     const uint2 *__restrict__ lv = reinterpret_cast<const uint2 *>(img + ci.o_lv);
     const uint32_t *__restrict__ mk = reinterpret_cast<const uint32_t *>(img + ci.o_mk);
+#ifdef WT_ABL_COUNT
+    const uint32_t K = ci.K, nw = ci.nw, lb = 0;
+#else
     const uint32_t K = ci.K, nw = ci.nw, lb = wt_levels(K);
+#endif
     uint32_t oA = d, oB = d, cA = 0, cB = 0;
     uint32_t lA = WT_NONE, sA = 0, qA = 0, lB = WT_NONE, sB = 0, qB = 0;
     const uint32_t nv = wt_v(n), one = wt_v(1u), five = wt_v(5u);
-    for (uint32_t l = 0; l < lb; ++l) {
-        const uint32_t hs = 1u << (K - l - 1);
-        const uint32_t h = wt_v(hs), msk = wt_v(~(2 * hs - 1)), l1 = wt_v(l + 1);
-        const uint2 *__restrict__ lvl = lv + l * nw;
-        const uint32_t s1 = RA & msk, p1 = s1 + oA, s2 = RB & msk, p2 = s2 + oB;
-        const uint2 w1 = lvl[p1 >> five], w2 = lvl[p2 >> five];
-        const uint32_t o1 = w1.y + __popc(__builtin_amdgcn_ubfe(w1.x, 0u, p1)) - (s1 >> one);
-        const uint32_t o2 = w2.y + __popc(__builtin_amdgcn_ubfe(w2.x, 0u, p2)) - (s2 >> one);
-        const uint32_t z1 = oA - o1, z2 = oB - o2;
-        const bool b1 = RA & h, b2 = RB & h;
-        const bool u1 = b1 && z1 != 0;
-        const bool u2 = b2 && min(nv - s2, h) > z2;  // zeros of the node past the prefix: suffix elements below R_B
-        lA = u1 ? l1 : lA;
-        sA = u1 ? s1 : sA;
-        qA = u1 ? z1 : qA;
-        lB = u2 ? l1 : lB;
-        sB = u2 ? s2 : sB;
-        qB = u2 ? z2 : qB;
-        cA += b1 ? 0u : o1;
-        cB += b2 ? 0u : o2;
-        oA = b1 ? o1 : z1;
-        oB = b2 ? o2 : z2;
+    if (lb) {
+        // level 0 (the root: both chains at offset d, one read); then the level constants live in VGPRs, halved per
+        // level (no SGPR operands, no per-level scalar shifts)
+        const uint32_t hs = 1u << (K - 1);
+        {
+            const uint2 w = lv[d >> 5];
+            const uint32_t o = w.y + __popc(__builtin_amdgcn_ubfe(w.x, 0u, d)), z = d - o;
+            const bool b1 = RA >= hs, b2 = RB >= hs;
+            const bool u1 = b1 && z != 0, u2 = b2 && hs > z;  // the root's left child is whole (n >= hs)
+            lA = u1 ? 1u : lA;
+            qA = u1 ? z : qA;
+            lB = u2 ? 1u : lB;
+            qB = u2 ? z : qB;
+            cA = b1 ? 0u : o;
+            cB = b2 ? 0u : o;
+            oA = b1 ? o : z;
+            oB = b2 ? o : z;
+        }
+        uint32_t h = wt_v(hs >> 1), msk = wt_v(~(hs - 1)), l1 = wt_v(2u);
+        const uint2 *__restrict__ lvl = lv + nw;
+        for (uint32_t l = 1; l < lb; ++l) {
+            const uint32_t s1 = RA & msk, p1 = s1 + oA, s2 = RB & msk, p2 = s2 + oB;
+            const uint2 w1 = lvl[p1 >> five], w2 = lvl[p2 >> five];
+            const uint32_t o1 = w1.y + __popc(__builtin_amdgcn_ubfe(w1.x, 0u, p1)) - (s1 >> one);
+            const uint32_t o2 = w2.y + __popc(__builtin_amdgcn_ubfe(w2.x, 0u, p2)) - (s2 >> one);
+            const uint32_t z1 = oA - o1, z2 = oB - o2;
+            const bool b1 = RA & h, b2 = RB & h;
+            const bool u1 = b1 && z1 != 0;
+            const bool u2 = b2 && min(nv - s2, h) > z2;  // zeros of the node past the prefix: suffix elements below R_B
+            lA = u1 ? l1 : lA;
+            sA = u1 ? s1 : sA;
+            qA = u1 ? z1 : qA;
+            lB = u2 ? l1 : lB;
+            sB = u2 ? s2 : sB;
+            qB = u2 ? z2 : qB;
+            cA += b1 ? 0u : o1;
+            cB += b2 ? 0u : o2;
+            oA = b1 ? o1 : z1;
+            oB = b2 ? o2 : z2;
+            h >>= 1;
+            msk = (uint32_t)((int32_t)msk >> 1);
+            l1 += 1;
+            lvl += nw;
+        }
     }
     // R's 32-rank block: its node's first o entries are the prefix part's elements in it (mk: their ranks' bits), so
     // the ranks >= R among them finish the counts, and those below R hold the part's predecessor when any are there
@@ -457,6 +513,9 @@ __device__ __forceinline__ void wt_seed_class(const WtClass &ci, const char *__r
     if (!dA) lA = lb;
     if (!dB) lB = lb;
     const uint32_t l0 = min(lA, lB);
+#ifdef WT_ABL_PRED
+    if (0)
+#endif
     if (__builtin_amdgcn_ballot_w64(l0 < lb)) {
         for (uint32_t l = 0; l < lb; ++l) {
             if (!__builtin_amdgcn_ballot_w64(l >= l0)) continue;
@@ -557,17 +616,36 @@ __global__ __launch_bounds__(1024) void k_replayable_sweep_wt(
     const uint4 *__restrict__ row = table + (uint64_t)L * E;
     const uint64_t rsum = rowsum[L];
     const uint32_t lane = threadIdx.x & 63;
-    for (;;) {
-        uint32_t ch = 0;
-        if (lane == 0) ch = atomicAdd(ctr, 1u);
-        ch = __builtin_amdgcn_readfirstlane(ch);
-        if (ch >= c1) break;
+    WtVConst vc;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) vc.st4[r] = wt_v(4u << r);
+    // chunks from the LDS counter; the next chunk's seeds and indices are loaded while this one runs
+    uint32_t ch = 0;
+    if (lane == 0) ch = atomicAdd(ctr, 1u);
+    ch = __builtin_amdgcn_readfirstlane(ch);
+    uint64_t h0n = 0;
+    uint32_t idxn = 0;
+    if (ch < c1) {
+        const uint32_t jn = min(s0 + ch * 64 + lane, s1 - 1);
+        h0n = sorted_h0[jn];
+        idxn = sorted_idx[jn];
+    }
+    while (ch < c1) {
         const uint32_t j = s0 + ch * 64 + lane;
-        const uint64_t h0 = sorted_h0[min(j, s1 - 1)];
+        const uint64_t h0 = h0n;
+        const uint32_t idx = idxn;
+        uint32_t chn = 0;
+        if (lane == 0) chn = atomicAdd(ctr, 1u);
+        chn = __builtin_amdgcn_readfirstlane(chn);
+        {
+            const uint32_t jn = min(s0 + chn * 64 + lane, s1 - 1);  // past the share: a valid seed, unused
+            h0n = sorted_h0[jn];
+            idxn = sorted_idx[jn];
+        }
         uint64_t sum = 0, key = 0;
         uint32_t W = 0;
         for (uint32_t c = 0; c < n_classes; ++c)
-            wt_seed_class<BIG>(classes[c], img, row, h0, m, mu, m_k64, msh, sum, W, key);
+            wt_seed_class<BIG>(vc, classes[c], img, row, h0, m, mu, m_k64, msh, sum, W, key);
         const uint64_t total = sum + rsum - (uint64_t)W * m;
         if (tk) {  // the chunk's largest sum, in the top-k's order (int64, as an order-preserving u64 key)
             uint64_t km = j < s1 ? total ^ (1ull << 63) : 0ull;
@@ -578,7 +656,6 @@ __global__ __launch_bounds__(1024) void k_replayable_sweep_wt(
             if (lane == 0) atomicMax(reinterpret_cast<unsigned long long *>(ctr + 2), (unsigned long long)km);
         }
         if (j < s1) {
-            const uint32_t idx = sorted_idx[j];
             if (sums) sums[j] = total;  // in sorted order: the wave's 64 writes coalesce (by seed index they scatter,
                                         // one 64-B line per seed: +20 us on the step)
             nmz_sched_stats st;
@@ -590,6 +667,7 @@ __global__ __launch_bounds__(1024) void k_replayable_sweep_wt(
             st.flags = 0;
             stats[idx] = st;
         }
+        ch = chn;
     }
     if (span || tk) {
         __syncthreads();
@@ -869,9 +947,9 @@ int wt_build(WtState &w, nmz_ctx *ctx, const uint4 *d_table, uint32_t E, const C
         o.o_lv = (uint32_t)off;
         off += r16((uint64_t)wt_levels(o.K) * o.nw * 8);
         o.o_cm = (uint32_t)off;
-        off += r16((uint64_t)(o.n + 1) * 4);
+        off += r16((uint64_t)(o.n + WT_PAD) * 4);
         o.o_chi = (uint32_t)off;
-        off += r16((uint64_t)(o.n + 1) * 4);
+        off += r16((uint64_t)(o.n + WT_PAD) * 4);
         o.o_e = (uint32_t)off;
         off += r16((uint64_t)o.n * 2);
         o.o_im = (uint32_t)off;

@@ -50,6 +50,8 @@ struct nmz_tbqueue {
     std::deque<nmz::TbReady> ready;
     uint64_t seq = 0, n_enq = 0, n_rel = 0, n_deq = 0;
     bool stop = false;
+    uint32_t users = 0;              // calls inside dequeue (destroy waits for them to leave before deleting)
+    std::condition_variable idle_cv;
     std::thread timer;
 
     void loop() {
@@ -98,15 +100,25 @@ int nmz_tbqueue_create(nmz_tbqueue **out) {
     return NMZ_OK;
 }
 
-int nmz_tbqueue_destroy(nmz_tbqueue *q) {
-    if (!q) return NMZ_OK;
+int nmz_tbqueue_close(nmz_tbqueue *q) {
+    NMZ_CHECK(q != nullptr, "queue is NULL");
     {
         std::lock_guard<std::mutex> lk(q->mu);
         q->stop = true;
     }
     q->timer_cv.notify_all();
-    q->ready_cv.notify_all();
+    q->ready_cv.notify_all();  // blocked consumers return NMZ_EAGAIN ("queue is closed")
+    return NMZ_OK;
+}
+
+int nmz_tbqueue_destroy(nmz_tbqueue *q) {
+    if (!q) return NMZ_OK;
+    nmz_tbqueue_close(q);
     q->timer.join();
+    {  // consumers woken by the close leave dequeue before the queue (its mutex and condition variables) goes
+        std::unique_lock<std::mutex> lk(q->mu);
+        q->idle_cv.wait(lk, [q] { return q->users == 0; });
+    }
     delete q;
     return NMZ_OK;
 }
@@ -128,6 +140,13 @@ int nmz_tbqueue_enqueue(nmz_tbqueue *q, uint64_t id, int64_t due_ns) {
 int nmz_tbqueue_dequeue(nmz_tbqueue *q, int64_t timeout_ns, uint64_t *id, int64_t *due_ns, int64_t *released_ns) {
     NMZ_CHECK(q && id, "NULL argument");
     std::unique_lock<std::mutex> lk(q->mu);
+    ++q->users;
+    struct Leave {  // every return path: the last consumer out of a closed queue lets destroy proceed
+        nmz_tbqueue *q;
+        ~Leave() {
+            if (--q->users == 0 && q->stop) q->idle_cv.notify_all();
+        }
+    } leave{q};
     auto has = [q] { return !q->ready.empty() || q->stop; };
     if (timeout_ns < 0) {
         q->ready_cv.wait(lk, has);

@@ -12,7 +12,6 @@ completed with (band + 1, smallest unlisted ids) (nmz_ed_knn_fill_dev on the
 GPU, fill_knn_keys on the host).
 """
 import ctypes
-import os
 
 import numpy as np
 
@@ -27,32 +26,18 @@ def shard_range(total, world, rank):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-_M64 = (1 << 64) - 1
-
-
 def ed_block_shard(qb, world):
     """Shard owning query block qb (queries 64 qb .. 64 qb + 63) of the two-phase all-pairs search
     (nmz_ed_allpairs_knn_shard_dev; csrc/ed.hip ed_block_shard): in each period of 2 world blocks, block r and
     its mirror 2 world - 1 - r form a pair (the falling work per block inside the upper triangle and inside each
     family of near-duplicates cancels between them), and pair p of period g goes to shard (p + g) mod world, so
-    every shard takes every position. Whole query blocks, so a query pair's DP entries stay in one shard.
-    NMZ_ED_DEAL=snake selects the unrotated snake, NMZ_ED_DEAL=hash the MurmurHash3 deal (A/B runs)."""
+    every shard takes every position. Whole query blocks, so a query pair's DP entries stay in one shard. A fixed
+    rule (no environment knob): every process of a job must deal the same way."""
     if world <= 1:
         return 0
-    if os.environ.get("NMZ_ED_DEAL") == "hash":
-        x = qb
-        x ^= x >> 33
-        x = (x * 0xFF51AFD7ED558CCD) & _M64
-        x ^= x >> 33
-        x = (x * 0xC4CEB9FE1A85EC53) & _M64
-        return (x ^ (x >> 33)) % world
-    unit = int(os.environ.get("NMZ_ED_DEAL_UNIT", "1") or 1)
-    q = qb // (unit if unit > 0 else 1)
-    r = q % (2 * world)
+    r = qb % (2 * world)
     pr = r if r < world else 2 * world - 1 - r
-    if os.environ.get("NMZ_ED_DEAL") == "snake":
-        return pr
-    return (pr + q // (2 * world)) % world  # rotated snake: the pair position moves one shard per period
+    return (pr + qb // (2 * world)) % world
 
 
 def ed_pair_shard(i, j, world):

@@ -94,21 +94,50 @@ class ActionChannel:
         self._items = {}
         self._ids = itertools.count()
         self._lock = threading.Lock()
+        self._idle = threading.Condition(self._lock)
+        self._calls = 0  # native calls in flight: close() frees the queue only after they have returned
+        self._closed = False
         self.delivery_err_ns = collections.deque(maxlen=history)
 
-    def put_at(self, due_ns, action):
+    def _enter(self):
         with self._lock:
-            i = next(self._ids)
-            self._items[i] = action
-        _lib.check(self.L.nmz_tbqueue_enqueue(self.q, i, int(due_ns)))
+            if self._closed:
+                raise ValueError("ActionChannel is closed")
+            self._calls += 1
+            return self.q
+
+    def _leave(self):
+        with self._lock:
+            self._calls -= 1
+            if self._calls == 0:
+                self._idle.notify_all()
+
+    def put_at(self, due_ns, action):
+        q = self._enter()
+        try:
+            with self._lock:
+                i = next(self._ids)
+                self._items[i] = action
+            _lib.check(self.L.nmz_tbqueue_enqueue(q, i, int(due_ns)))
+        finally:
+            self._leave()
 
     def put(self, action):
         self.put_at(self.L.nmz_monotonic_ns(), action)
 
     def get(self, block=True, timeout=None):
+        """Blocks until an action is released; queue.Empty on timeout, and once the channel is closed (a consumer
+        blocked in get() when close() runs returns with queue.Empty)."""
         i, due, rel = ctypes.c_uint64(), ctypes.c_int64(), ctypes.c_int64()
         t = -1 if (block and timeout is None) else int((timeout if block else 0) * 1e9)
-        rc = self.L.nmz_tbqueue_dequeue(self.q, t, ctypes.byref(i), ctypes.byref(due), ctypes.byref(rel))
+        try:
+            q = self._enter()
+        except ValueError:
+            raise queue.Empty
+        try:
+            rc = self.L.nmz_tbqueue_dequeue(q, t, ctypes.byref(i), ctypes.byref(due), ctypes.byref(rel))
+        finally:
+            self._leave()
         if rc == _lib.NMZ_EAGAIN:
             raise queue.Empty
         _lib.check(rc)
@@ -121,13 +150,27 @@ class ActionChannel:
 
     def stats(self):
         a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
-        _lib.check(self.L.nmz_tbqueue_stats(self.q, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        q = self._enter()
+        try:
+            _lib.check(self.L.nmz_tbqueue_stats(q, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        finally:
+            self._leave()
         return a.value, b.value, c.value  # enqueued, released, dequeued
 
     def close(self):
-        if self.q:
-            self.L.nmz_tbqueue_destroy(self.q)
+        """Closes the channel: blocked get() calls return (queue.Empty), then the native queue is freed once no
+        call is inside it (nmz_tbqueue_close, then nmz_tbqueue_destroy)."""
+        with self._lock:
+            if self._closed or not self.q:
+                return
+            self._closed = True
+            q = self.q
+        self.L.nmz_tbqueue_close(q)
+        with self._lock:
+            while self._calls:
+                self._idle.wait()
             self.q = None
+        self.L.nmz_tbqueue_destroy(q)
 
     def __del__(self):
         try:

@@ -47,8 +47,9 @@ class Group:
         return b.tobytes()
 
     def close(self):
+        """nmz_close_group: fails (NmzError, NMZ_EINVAL) while plans made on the group are alive."""
         if self.handle:
-            self.L.nmz_close_group(self.handle)
+            _lib.check(self.L.nmz_close_group(self.handle))
             self.handle = None
 
     def __enter__(self):
@@ -163,7 +164,22 @@ class EdGroupPlan:
         _lib.check(self.L.nmz_ed_group_allpairs_knn(self.h, k, _lib.ptr(ids), _lib.ptr(ds)))
         return ids.reshape(self.n, k), ds.reshape(self.n, k)
 
+    def timing(self):
+        """Per local device: (share upload, RCCL all_gather, device plan build) in ms (nmz_ed_group_plan_timing)."""
+        up, ga, bu = (np.zeros(self.g.n_local, np.float64) for _ in range(3))
+        _lib.check(self.L.nmz_ed_group_plan_timing(self.h, _lib.ptr(up), _lib.ptr(ga), _lib.ptr(bu)))
+        return dict(upload_ms=up.tolist(), gather_ms=ga.tolist(), build_ms=bu.tolist())
+
     def close(self):
         if self.h:
             self.L.nmz_ed_group_plan_destroy(self.h)
             self.h = None
+
+
+for _cls in (ReplayableGroupPlan, RandomGroupPlan, EdGroupPlan):
+    def _del(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+    _cls.__del__ = _del

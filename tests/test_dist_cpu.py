@@ -129,25 +129,34 @@ def test_merge_topk_is_order_independent():
 
 @pytest.mark.parametrize("deal", [None, "snake", "hash"])
 def test_ed_pair_dealing_matches_library(monkeypatch, deal):
-    """dist.ed_block_shard restates the library's dealing rule (csrc/ed.hip ed_block_shard; host-only entry point),
-    for the default rotated snake and both A/B deals."""
+    """dist.ed_block_shard restates the library's dealing rule (csrc/ed.hip ed_block_shard; host-only entry point).
+    The rule is fixed: the round-3 A/B knobs (NMZ_ED_DEAL, NMZ_ED_DEAL_UNIT) set in a process's environment change
+    nothing, so ranks with different environments still deal the same blocks (a rank that dealt differently would
+    drop or double pairs of the merged k-NN)."""
     from namazu_amd import _lib
     if deal:
         monkeypatch.setenv("NMZ_ED_DEAL", deal)
+        monkeypatch.setenv("NMZ_ED_DEAL_UNIT", "4")
     L = _lib.load()
+
+    def rotated_snake(qb, S):
+        r = qb % (2 * S)
+        return ((r if r < S else 2 * S - 1 - r) + qb // (2 * S)) % S
+
     for world in [1, 2, 3, 8]:
         for qb in list(range(300)) + [2**20 + 7, 2**31 - 1]:
-            assert L.nmz_ed_block_shard(qb, world) == nd.ed_block_shard(qb, world)
+            want = rotated_snake(qb, world) if world > 1 else 0
+            assert L.nmz_ed_block_shard(qb, world) == nd.ed_block_shard(qb, world) == want
     # every block has an owner in range, and 8 shards all get blocks
     assert sorted({nd.ed_block_shard(qb, 8) for qb in range(1563)}) == list(range(8))
-    if deal != "hash":  # a block and its mirror share a shard; every 2S blocks give each shard exactly two
-        for S in [2, 3, 8]:
-            for g in range(5):
-                own = [nd.ed_block_shard(2 * S * g + r, S) for r in range(2 * S)]
-                assert sorted(own) == sorted(list(range(S)) * 2)
-                assert all(own[r] == own[2 * S - 1 - r] for r in range(S))
-    if deal is None:  # rotated: over S periods a shard takes every pair position once
-        S = 8
-        for sh in range(S):
-            pos = {min(qb % 16, 15 - qb % 16) for qb in range(16 * S) if nd.ed_block_shard(qb, S) == sh}
-            assert pos == set(range(S))
+    # a block and its mirror share a shard; every 2S blocks give each shard exactly two
+    for S in [2, 3, 8]:
+        for g in range(5):
+            own = [nd.ed_block_shard(2 * S * g + r, S) for r in range(2 * S)]
+            assert sorted(own) == sorted(list(range(S)) * 2)
+            assert all(own[r] == own[2 * S - 1 - r] for r in range(S))
+    # rotated: over S periods a shard takes every pair position once
+    S = 8
+    for sh in range(S):
+        pos = {min(qb % 16, 15 - qb % 16) for qb in range(16 * S) if nd.ed_block_shard(qb, S) == sh}
+        assert pos == set(range(S))

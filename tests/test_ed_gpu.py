@@ -535,16 +535,19 @@ def test_knn_qgram_filter_exact(ctx, monkeypatch, w, alphabet, max_edits):
     assert c_on[0] + c_on[5] == c_off[0]  # every pair the bound settles would have run the DP
 
 
-@pytest.mark.parametrize("limit", [0, 1, 500])
-def test_knn_two_phase_entry_limit_fallback(ctx, monkeypatch, limit):
-    """Entry lists beyond the two-phase limit (2^30 entries; NMZ_ED_TP_MAX_ENTRIES lowers it) take the
-    single-kernel search after the count pass has run. The count pass lists pairs with an empty trace before the
-    total is known, so the fallback must start from empty lists: near-duplicates with empty traces in the store
-    (n + m <= w pairs), vs the oracle, through the one-shard and the 3-shard (merge + fill) paths."""
+@pytest.mark.parametrize("limit", [0, 1, 500, "mid"])
+def test_knn_two_phase_entry_limit_batches(ctx, monkeypatch, limit):
+    """Entry lists beyond the two-phase limit (2^30 entries; NMZ_ED_TP_MAX_ENTRIES lowers it) run in batches of
+    whole query blocks after the count pass (csrc/ed.hip ed_bv_two_phase). The count pass lists pairs with an empty
+    trace before the total is known, so the batches must start from empty lists: near-duplicates with empty traces
+    in the store (n + m <= w pairs), vs the oracle, through the one-shard and the 3-shard (merge + fill) paths.
+    "mid" puts the limit between the shards' own entry totals, so some shards of one search split into batches and
+    others do not: each must still cover exactly its own query blocks (no pair dropped or doubled)."""
     import torch
-    monkeypatch.setenv("NMZ_ED_TP_MAX_ENTRIES", str(limit))
+    if limit != "mid":
+        monkeypatch.setenv("NMZ_ED_TP_MAX_ENTRIES", str(limit))
     L = _lib.load()
-    rng = np.random.default_rng(77 + limit)
+    rng = np.random.default_rng(77 + (limit if limit != "mid" else 3))
     ts0 = _edited_family(500, 120, 16, 30, rng)
     trs = [ts0.trace(i) for i in range(len(ts0))]
     for i in (3, 40, 41, 333):
@@ -562,6 +565,15 @@ def test_knn_two_phase_entry_limit_fallback(ctx, monkeypatch, limit):
     S = 3
     parts = torch.empty(S * n * k, dtype=torch.int64, device="cuda")
     out = torch.empty(n * k, dtype=torch.int64, device="cuda")
+    if limit == "mid":  # the shards' DP pairs (= their entries) under the default limit, then a limit between them
+        per = []
+        for s in range(S):
+            _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, s, S, ctypes.c_void_p(parts.data_ptr()), stream))
+            cnt = np.zeros(6, np.uint64)
+            _lib.check(L.nmz_ed_plan_counters(plan, _lib.ptr(cnt), stream))
+            per.append(int(cnt[0]))
+        assert min(per) < max(per), per
+        monkeypatch.setenv("NMZ_ED_TP_MAX_ENTRIES", str((min(per) + max(per)) // 2))
     for s in range(S):
         _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, s, S, ctypes.c_void_p(parts.data_ptr() + s * n * k * 8),
                                                    stream))

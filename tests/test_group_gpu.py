@@ -154,10 +154,11 @@ def _family(n, length, alphabet, edits, seed):
     return hs.TraceSet(out)
 
 
-@pytest.mark.parametrize("band,n_shards", [(32, 1), (32, 8), (32, 11), (16, 3), (5, 8)])
+@pytest.mark.parametrize("band,n_shards", [(32, 1), (32, 8), (32, 11), (16, 3), (5, 8), (100, 3)])
 def test_group_ed_allpairs_knn_equals_oracle(groups, band, n_shards):
-    """All-pairs k-NN over a group: shards by the plan's tile hash, per-rank merge of the shards' partial lists
-    (chained 8 at a time beyond 8 shards), RCCL all_gather, merge and band + 1 fill; vs the oracle."""
+    """All-pairs k-NN over a group: the store as 1/n_ranks shares + RCCL all_gather + device plan builds, shards by
+    the plan's query-block deal, per-rank merge of the shards' partial lists (chained 8 at a time beyond 8
+    shards), RCCL all_gather, merge and band + 1 fill; vs the oracle (band 100: the wide kernel)."""
     g = groups(n_shards)
     ts = _family(300, 200, 12, 40, band * 100 + n_shards)
     k = 8
@@ -166,8 +167,27 @@ def test_group_ed_allpairs_knn_equals_oracle(groups, band, n_shards):
     assert np.array_equal(ids, oi) and np.array_equal(ds, od)
     p = G.EdGroupPlan(g, ts, band)
     i2, d2 = p.knn(k)
+    t = p.timing()
     p.close()
     assert np.array_equal(i2, oi) and np.array_equal(d2, od)
+    assert all(len(v) == g.n_local and all(x >= 0 for x in v) for v in t.values())
+    assert t["build_ms"][0] > 0
+
+
+def test_group_close_refuses_live_plans_and_keeps_caller_device():
+    """nmz_close_group refuses while a group plan is alive (closing under a live plan freed what the plan
+    still used), and group calls leave the calling thread's current device as it was."""
+    import torch
+    g = G.Group((0,), n_shards=2)
+    ts = _family(40, 50, 6, 5, 1)
+    p = G.EdGroupPlan(g, ts, 8)
+    with pytest.raises(_lib.NmzError):
+        g.close()
+    p.knn(4)
+    assert torch.cuda.current_device() == 0
+    p.close()
+    g.close()
+    g.close()  # idempotent
 
 
 def test_group_rank_form_single_rank(groups):
