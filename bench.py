@@ -731,32 +731,36 @@ def bench_ed_secondary(args, torch, D, ctx, L, stream, spec):
     counters = np.zeros(_lib.NMZ_ED_NCOUNTERS, np.uint64)
     _lib.check(L.nmz_ed_plan_counters(plan, _lib.ptr(counters), stream))
     single = None
-    if kind == "k_ed_bv" and D.rank == 0:
-        # single queries against the resident store (SearchSimilar): 8 stored traces as queries, one call
+    if kind in ("k_ed_bv", "k_ed_wide") and D.rank == 0:
+        # single queries against the resident store (SearchSimilar): stored traces as queries, one call
+        # (k_ed_bv_query for band <= 64, k_ed_wide_query above)
         from namazu_amd.historystorage import TraceSet
-        qset = TraceSet([ts.trace(i) for i in range(8)])
+        NQ = 8 if kind == "k_ed_bv" else 4
+        qset = TraceSet([ts.trace(i) for i in range(NQ)])
         kq = k + 1  # a stored trace queried finds itself too
-        qi = np.zeros(8 * kq, np.uint32)
-        qd = np.zeros(8 * kq, np.uint32)
+        qi = np.zeros(NQ * kq, np.uint32)
+        qd = np.zeros(NQ * kq, np.uint32)
         reps = []
         for _ in range(3):
             t0 = time.perf_counter()
-            _lib.check(L.nmz_ed_plan_query_knn(plan, _lib.ptr(qset.off), _lib.ptr(qset.sym), 8, kq, _lib.ptr(qi),
+            _lib.check(L.nmz_ed_plan_query_knn(plan, _lib.ptr(qset.off), _lib.ptr(qset.sym), NQ, kq, _lib.ptr(qi),
                                                _lib.ptr(qd)))
             reps.append(time.perf_counter() - t0)
         # the all-pairs k-NN lists of the same traces (self excluded) must agree with the single-query answers
         agree = None
         if D.world == 1:
-            keys8 = d_out.cpu().numpy().view(np.uint64).reshape(N, k)[:8]
+            keys8 = d_out.cpu().numpy().view(np.uint64).reshape(N, k)[:NQ]
             agree = True
-            for i in range(8):
-                keep = qi.reshape(8, kq)[i] != i
-                ids_i, ds_i = qi.reshape(8, kq)[i][keep][:k], qd.reshape(8, kq)[i][keep][:k]
+            for i in range(NQ):
+                keep = qi.reshape(NQ, kq)[i] != i
+                ids_i, ds_i = qi.reshape(NQ, kq)[i][keep][:k], qd.reshape(NQ, kq)[i][keep][:k]
                 agree &= bool(np.array_equal((keys8[i] >> np.uint64(32)).astype(np.uint32), ds_i) and
                               np.array_equal((keys8[i] & np.uint64(0xFFFFFFFF)).astype(np.uint32), ids_i))
-        single = dict(queries=8, ms_per_query=min(reps) * 1e3 / 8, pairs_per_s=8 * (N - 1) / min(reps),
-                      agrees_with_allpairs=agree,
-                      what="nmz_ed_plan_query_knn: 8 query traces vs the resident store, host arrays in and out")
+        single = dict(queries=NQ, ms_per_query=min(reps) * 1e3 / NQ, pairs_per_s=NQ * N / min(reps),
+                      agrees_with_allpairs=agree, kernel=kind + "_query",
+                      what=f"nmz_ed_plan_query_knn: {NQ} stored traces as queries vs the resident store, host arrays "
+                           "in and out; agrees_with_allpairs compares each answer (self excluded) with the "
+                           "all-pairs k-NN list")
     L.nmz_ed_plan_destroy(plan)
     pairs = N * (N - 1) // 2
     cells_per_pair = ED_LEN * (2 * ED_BAND + 1) - ED_BAND * (ED_BAND + 1)

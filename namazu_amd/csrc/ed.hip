@@ -254,46 +254,82 @@ __global__ __launch_bounds__(256) void k_ed_tile(EdArgs A) {
 // ---------------------------------------------------------------------------
 // generic: one thread per pair, u64 symbols, band row in global scratch
 // ---------------------------------------------------------------------------
+// ED_W(a, b) with the band row D[t] = cell (i, i + t - W) in global scratch (column t at scratch[t * stride]):
+// one thread per pair, any band, any symbol type
+template <typename T>
+__device__ uint32_t generic_band_dist(const T *__restrict__ a, int64_t n, const T *__restrict__ b, int64_t m, uint32_t W,
+                                      uint32_t *__restrict__ scratch, uint64_t stride) {
+    const uint32_t NB = 2 * W + 1;
+    const uint32_t INF = 0x3fffffffu;
+    const int64_t dd = m - n;
+    if (dd > (int64_t)W || dd < -(int64_t)W) return W + 1;
+    // row 0: D(0, j) = j
+    for (uint32_t t = 0; t < NB; ++t) scratch[t * stride] = (t >= W) ? (t - W) : INF;
+    for (int64_t i = 1; i <= n; ++i) {
+        uint32_t left = INF;
+        for (uint32_t t = 0; t < NB; ++t) {
+            const int64_t jj = i + (int64_t)t - (int64_t)W;
+            uint32_t v;
+            if (jj < 0 || jj > m) {
+                v = INF;
+            } else if (jj == 0) {
+                v = (uint32_t)i;
+            } else {
+                const uint32_t diag = scratch[t * stride];
+                const uint32_t up = (t + 1 < NB) ? scratch[(t + 1) * stride] : INF;
+                v = diag + (a[i - 1] != b[jj - 1] ? 1u : 0u);
+                v = min(v, min(up, left) + 1);
+                v = min(v, INF);
+            }
+            scratch[t * stride] = v;
+            left = v;
+        }
+    }
+    return min(scratch[(uint32_t)(dd + W) * stride], W + 1);
+}
+
 __global__ __launch_bounds__(256) void k_ed_generic(const uint64_t *__restrict__ off, const uint64_t *__restrict__ sym,
                                                     const uint32_t *__restrict__ pairs, uint64_t n_pairs, uint32_t W,
                                                     uint32_t *__restrict__ scratch, uint32_t *__restrict__ dist) {
     const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t NB = 2 * W + 1;
-    const uint32_t INF = 0x3fffffffu;
     for (uint64_t p = tid; p < n_pairs; p += nthr) {
         const uint32_t ia = pairs[2 * p], ib = pairs[2 * p + 1];
-        const uint64_t *a = sym + off[ia], *b = sym + off[ib];
-        const int64_t n = (int64_t)(off[ia + 1] - off[ia]), m = (int64_t)(off[ib + 1] - off[ib]);
-        const int64_t dd = m - n;
-        if (dd > (int64_t)W || dd < -(int64_t)W) {
-            dist[p] = W + 1;
-            continue;
-        }
-        // D[t] = cell (i, i + t - W); row 0: D(0, j) = j
-        for (uint32_t t = 0; t < NB; ++t) scratch[t * nthr + tid] = (t >= W) ? (t - W) : INF;
-        for (int64_t i = 1; i <= n; ++i) {
-            uint32_t left = INF;
-            for (uint32_t t = 0; t < NB; ++t) {
-                const int64_t jj = i + (int64_t)t - (int64_t)W;
-                uint32_t v;
-                if (jj < 0 || jj > m) {
-                    v = INF;
-                } else if (jj == 0) {
-                    v = (uint32_t)i;
-                } else {
-                    const uint32_t diag = scratch[t * nthr + tid];
-                    const uint32_t up = (t + 1 < NB) ? scratch[(t + 1) * nthr + tid] : INF;
-                    v = diag + (a[i - 1] != b[jj - 1] ? 1u : 0u);
-                    v = min(v, min(up, left) + 1);
-                    v = min(v, INF);
-                }
-                scratch[t * nthr + tid] = v;
-                left = v;
-            }
-        }
-        const uint32_t v = scratch[(uint32_t)(dd + W) * nthr + tid];
-        dist[p] = min(v, W + 1);
+        dist[p] = generic_band_dist(sym + off[ia], (int64_t)(off[ia + 1] - off[ia]), sym + off[ib],
+                                    (int64_t)(off[ib + 1] - off[ib]), W, scratch + tid, nthr);
+    }
+}
+
+__device__ __forceinline__ void knn_insert_key(uint64_t *list, uint32_t k, uint64_t key) {
+    if (key >= __hip_atomic_load(&list[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    for (uint32_t s = 0; s < k; ++s) {
+        const uint64_t old = atomicMin((unsigned long long *)&list[s], (unsigned long long)key);
+        if (old == UINT64_MAX) return;
+        key = old > key ? old : key;
+    }
+}
+
+// Single queries against a resident store without a bit-parallel query kernel (k_ed_tile's dense ids, the generic
+// plan's u64 symbols, or a bit-parallel plan's encoded streams when a query pair's symbols overflow the compact
+// tables): thread per (query, stored trace) pair; stored trace j at sym[soff[j]], length slen[j] (or the CSR
+// difference when slen is NULL); in-band results into the query's list
+__global__ __launch_bounds__(256) void k_ed_query_generic(const uint64_t *__restrict__ soff,
+                                                          const uint32_t *__restrict__ slen, const void *__restrict__ sym,
+                                                          bool wide_sym, const uint64_t *__restrict__ qstart,
+                                                          const uint32_t *__restrict__ qlen, const void *__restrict__ qsym,
+                                                          uint32_t n_q, uint32_t N, uint32_t W, uint32_t k,
+                                                          uint32_t *__restrict__ scratch, uint64_t *__restrict__ knn) {
+    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint64_t p = tid; p < (uint64_t)n_q * N; p += nthr) {
+        const uint32_t q = (uint32_t)(p / N), j = (uint32_t)(p % N);
+        const int64_t n = qlen[q], m = slen ? (int64_t)slen[j] : (int64_t)(soff[j + 1] - soff[j]);
+        const uint32_t r = wide_sym
+            ? generic_band_dist((const uint64_t *)qsym + qstart[q], n, (const uint64_t *)sym + soff[j], m, W,
+                                scratch + tid, nthr)
+            : generic_band_dist((const uint16_t *)qsym + qstart[q], n, (const uint16_t *)sym + soff[j], m, W,
+                                scratch + tid, nthr);
+        if (r <= W) knn_insert_key(knn + (uint64_t)q * k, k, ((uint64_t)r << 32) | j);
     }
 }
 
@@ -375,6 +411,7 @@ struct nmz_ed_plan {
     uint64_t *d_soff = nullptr;    // bv: per-trace stream offsets
     uint32_t pool = 0;
     bool wide = false;             // wide-band bit-parallel kernel (k_ed_wide) usable
+    bool tile = false;             // k_ed_tile (dense ids in d_qsym / d_qoff)
     uint32_t n_sym = 0;
     uint32_t *d_peq = nullptr;     // wide: [N][n_sym][ndw] match bitmaps
     uint32_t *d_rowb = nullptr;    // wide: per-position Peq row byte offsets (EdWideArgs::rowb)
@@ -700,7 +737,13 @@ static int ed_plan_build_wide_device(nmz_ed_plan *p, const uint64_t *off, const 
         NMZ_HIP(hipGetLastError());
     }
     NMZ_TRY(ed_wide_build_peq(p->d_qsym, p->d_qoff, N, n_sym, ndw, p->ww, p->d_peq, st));
+    // the dictionary for single queries (nmz_ed_plan_query_knn): symbol -> rank
+    std::vector<uint64_t> uniq(n_uniq);
+    if (n_uniq) NMZ_HIP(hipMemcpyAsync(uniq.data(), d_uniq, n_uniq * 8, hipMemcpyDeviceToHost, st));
     NMZ_HIP(hipStreamSynchronize(st));  // the host vectors above are pageable; the scratch goes back
+    p->dict.reserve(n_uniq * 2);
+    for (uint64_t i = 0; i < n_uniq; ++i) p->dict.emplace(uniq[i], (uint32_t)i);
+    p->maxlen = maxlen;
     return NMZ_OK;
 }
 
@@ -844,6 +887,7 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         }
     }
     p->fast = fast;
+    p->maxlen = maxlen;
     if (fast && p->wide) {
         // per-position Peq row byte offsets, each trace padded to whole 32-column blocks + 2 spare blocks
         std::vector<uint64_t> roff(N + 1, 0);
@@ -872,6 +916,7 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         rc = ed_wide_build_peq(p->d_qsym, p->d_qoff, N, p->n_sym, p->ndw, p->ww, p->d_peq, st);
         if (rc != NMZ_OK) return cleanup(rc);
         if (hipStreamSynchronize(st)) return cleanup(fail(NMZ_EHIP, "ED plan build failed"));
+        p->dict = std::move(dict);
     } else if (fast && p->bv) {
         const uint32_t rq = ed_bv_row_queries();
         const uint32_t G = (N + rq - 1) / rq;
@@ -959,6 +1004,8 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
             hipMemcpyAsync(p->d_len, len.data(), (N + 1) * 4, hipMemcpyHostToDevice, st) ||
             hipStreamSynchronize(st))
             return cleanup(fail(NMZ_EHIP, "ED plan upload failed"));
+        p->dict = std::move(dict);
+        p->tile = true;
     } else {
         p->fast = false;
         p->bv = false;
@@ -1364,21 +1411,39 @@ int nmz_ed_plan_counters(nmz_ed_plan *plan, uint64_t *out, void *stream) {
     return NMZ_OK;
 }
 
-int nmz_ed_plan_query_knn(nmz_ed_plan *plan, const uint64_t *q_off, const uint64_t *q_sym, uint32_t n_queries,
-                          uint32_t k, uint32_t *knn_id, uint32_t *knn_dist) {
-    NMZ_CHECK(plan != nullptr, "plan is NULL");
-    NMZ_CHECK(k >= 1 && k <= 64, "k must be in [1, 64]");
-    NMZ_CHECK(plan->bv, "single-query search needs a bit-parallel plan (band <= 64, alphabet or query pairs within LDS)");
-    NMZ_CHECK(n_queries == 0 || (q_off && knn_id && knn_dist), "NULL argument");
-    CtxGuard g(plan->ctx);
-    NMZ_TRY(g.rc);
-    if (n_queries == 0) return NMZ_OK;
-    const uint64_t total = q_off[n_queries];
-    NMZ_CHECK(total == 0 || q_sym, "q_sym is NULL");
-    for (uint32_t q = 0; q < n_queries; ++q) {
-        NMZ_CHECK(q_off[q] <= q_off[q + 1], "query offsets must not decrease");
-        NMZ_CHECK(q_off[q + 1] - q_off[q] <= plan->maxlen, "query longer than the longest stored trace");
-    }
+}  // extern "C"
+
+namespace nmz {
+
+// k_ed_query_generic over the resident store (soff/slen/sym as the kernel takes them) for n_q queries whose
+// symbols (already in the store's encoding) are at d_qs + qstart[q], lengths qlen[q] (host arrays)
+static int ed_query_generic_launch(nmz_ed_plan *plan, const uint64_t *soff, const uint32_t *slen, const void *sym,
+                                   bool wide_sym, const void *d_qs, const std::vector<uint64_t> &qstart,
+                                   const std::vector<uint32_t> &qlen, uint64_t *d_knn, uint32_t k) {
+    hipStream_t st = plan->ctx->stream;
+    const uint32_t N = plan->n, W = plan->band, n_q = (uint32_t)qlen.size();
+    const unsigned threads =
+        (unsigned)std::max<uint64_t>(256, std::min<uint64_t>(256 * 1024, (1ULL << 28) / (2ULL * W + 1)) / 256 * 256);
+    DevBuf &scr = plan->ctx->buf[15];
+    NMZ_TRY(scr.ensure(Carve::bytes_for(n_q + 1, 8) + Carve::bytes_for(n_q + 1, 4) +
+                       Carve::bytes_for((uint64_t)(2 * W + 1) * threads, 4)));
+    Carve cv(scr.ptr);
+    uint64_t *d_qstart = cv.take<uint64_t>(n_q + 1);
+    uint32_t *d_qlen = cv.take<uint32_t>(n_q + 1);
+    uint32_t *d_row = cv.take<uint32_t>((uint64_t)(2 * W + 1) * threads);
+    NMZ_HIP(hipMemcpyAsync(d_qstart, qstart.data(), n_q * 8, hipMemcpyHostToDevice, st));
+    NMZ_HIP(hipMemcpyAsync(d_qlen, qlen.data(), n_q * 4, hipMemcpyHostToDevice, st));
+    KernelTimer kt(plan->ctx, st, "ed_query_generic");
+    hipLaunchKernelGGL(k_ed_query_generic, dim3(threads / 256), dim3(256), 0, st, soff, slen, sym, wide_sym, d_qstart,
+                       d_qlen, d_qs, n_q, N, W, k, d_row, d_knn);
+    NMZ_HIP(hipGetLastError());
+    NMZ_HIP(hipStreamSynchronize(st));  // pageable sources
+    return NMZ_OK;
+}
+
+// nmz_ed_plan_query_knn on a bit-parallel plan: k_ed_bv_query, two queries per launch
+static int ed_query_bv(nmz_ed_plan *plan, const uint64_t *q_off, const uint64_t *q_sym, uint32_t n_queries,
+                       uint32_t k, uint64_t *d_knn) {
     hipStream_t st = plan->ctx->stream;
     const uint32_t N = plan->n;
     // query streams in the plan's Peq-row offsets (unknown symbols: 0xffff), each padded by one 32-block
@@ -1402,18 +1467,21 @@ int nmz_ed_plan_query_knn(nmz_ed_plan *plan, const uint64_t *q_off, const uint64
                     ++qd[q];
                 }
     }
-    const uint64_t nk = (uint64_t)n_queries * k;
-    DevBuf &scr = plan->ctx->buf[11];
-    NMZ_TRY(scr.ensure(Carve::bytes_for(qs.size(), 2) + Carve::bytes_for(nk, 8) + 2 * Carve::bytes_for(nk, 4)));
-    Carve cv(scr.ptr);
-    uint16_t *d_qs = cv.take<uint16_t>(qs.size());
-    uint64_t *d_knn = cv.take<uint64_t>(nk);
-    uint32_t *d_id = cv.take<uint32_t>(nk), *d_ds = cv.take<uint32_t>(nk);
+    DevBuf &scr = plan->ctx->buf[13];
+    NMZ_TRY(scr.ensure(Carve::bytes_for(qs.size(), 2)));
+    uint16_t *d_qs = scr.as<uint16_t>();
     NMZ_HIP(hipMemcpyAsync(d_qs, qs.data(), qs.size() * 2, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_knn_init, dim3(ceil_div(nk, 256)), dim3(256), 0, st, d_knn, nk);
+    std::vector<uint32_t> spill;  // queries for the generic kernel
     // a pool of 256 stored traces per workgroup: one pass of lanes, ~N/256 workgroups
     const uint32_t pool = N >= 256u * 1024u ? 1024u : 256u;
     for (uint32_t q = 0; q < n_queries && N; q += 2) {
+        const uint32_t nq2 = std::min(2u, n_queries - q);
+        bool longq = false;  // a query longer than the Peq tables (the longest stored trace): generic kernel
+        for (uint32_t i = 0; i < nq2; ++i) longq |= q_off[q + i + 1] - q_off[q + i] > plan->maxlen;
+        if (longq) {
+            for (uint32_t i = 0; i < nq2; ++i) spill.push_back(q + i);
+            continue;
+        }
         EdBvQueryArgs A;
         A.bsym = plan->d_bsym;
         A.soff = plan->d_soff;
@@ -1437,14 +1505,175 @@ int nmz_ed_plan_query_knn(nmz_ed_plan *plan, const uint64_t *q_off, const uint64
         A.row_bytes = plan->row_bytes;
         if (plan->cmp) {
             const uint32_t R = qd[q] + (A.n_queries > 1 ? qd[q + 1] : 0);
-            NMZ_CHECK(bv_compact_layout(plan->n_sym, R, plan->ndw, 16 + (2 * ED_QG_DW + 2 * ED_QG_BUCKETS) * 4,
-                                        ED_BV_LDS_MAX, A.lds_dw, A.rmap_dw, A.claim_dw),
-                      "the queries have too many distinct symbols for the bit-parallel search");
+            if (!bv_compact_layout(plan->n_sym, R, plan->ndw, 16 + (2 * ED_QG_DW + 2 * ED_QG_BUCKETS) * 4,
+                                   ED_BV_LDS_MAX, A.lds_dw, A.rmap_dw, A.claim_dw)) {
+                // the pair's symbols overflow the compact tables: these queries take the generic kernel over the
+                // same encoded streams (below)
+                for (uint32_t i = 0; i < A.n_queries; ++i) spill.push_back(q + i);
+                continue;
+            }
         }
         KernelTimer kt(plan->ctx, st, "ed_bv_query");
         NMZ_TRY(ed_bv_query_launch(A, plan->bw, plan->cmp, ceil_div(N, pool), st));
     }
-    // k_ed_bv_query lists in-band results only: every other stored trace is at band + 1
+    // stored trace j: stream at d_bsym + soff[j], d_len[j] symbols, in the same encoding as qs (an unseen query
+    // symbol, 0xffff, equals no stored entry: row byte offsets are even, compact ids < 0xfffe)
+    for (const uint32_t q : spill) {
+        std::vector<uint64_t> qstart{qoff[q]};
+        std::vector<uint32_t> qlen{(uint32_t)(q_off[q + 1] - q_off[q])};
+        NMZ_TRY(ed_query_generic_launch(plan, plan->d_soff, plan->d_len, plan->d_bsym, false, d_qs, qstart, qlen,
+                                        d_knn + (uint64_t)q * k, k));
+    }
+    NMZ_HIP(hipStreamSynchronize(st));  // the host vectors are pageable
+    return NMZ_OK;
+}
+
+// nmz_ed_plan_query_knn on a wide plan: each query's match table over the store's alphabet (one more row for symbols
+// the store has never seen), then k_ed_wide_query over (query, stored trace) waves; tables in batches of <= 2 GiB
+static int ed_query_wide(nmz_ed_plan *plan, const uint64_t *q_off, const uint64_t *q_sym, uint32_t n_queries,
+                         uint32_t k, uint64_t *d_knn) {
+    hipStream_t st = plan->ctx->stream;
+    const uint32_t N = plan->n, ns1 = plan->n_sym + 1, ndw = plan->ndw;
+    const uint64_t tbl = (uint64_t)ns1 * ndw;  // dwords per query table
+    const uint32_t batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_queries, (2ULL << 30) / (tbl * 4)));
+    uint64_t maxq = 0;
+    for (uint32_t q = 0; q < n_queries; ++q)
+        maxq = std::max<uint64_t>(maxq, std::min<uint64_t>(q_off[q + 1] - q_off[q], plan->maxlen));
+    DevBuf &scr = plan->ctx->buf[13];
+    NMZ_TRY(scr.ensure(Carve::bytes_for(batch * tbl, 4) + Carve::bytes_for(batch * maxq + 64, 2) +
+                       Carve::bytes_for(batch + 1, 8) + Carve::bytes_for(batch, 4)));
+    Carve cv(scr.ptr);
+    uint32_t *d_tbl = cv.take<uint32_t>(batch * tbl);
+    uint16_t *d_ids = cv.take<uint16_t>(batch * maxq + 64);
+    uint64_t *d_qoff = cv.take<uint64_t>(batch + 1);
+    uint32_t *d_qlen = cv.take<uint32_t>(batch);
+    auto ids_of = [&](uint64_t b0, uint64_t n, std::vector<uint16_t> &ids, uint16_t unseen) {
+        ids.resize(n);
+        for (uint64_t t = 0; t < n; ++t) {
+            auto it = plan->dict.find(q_sym[b0 + t]);
+            ids[t] = (uint16_t)(it != plan->dict.end() ? it->second : unseen);
+        }
+    };
+    // queries [q0, q0 + nb), each within the tables
+    auto run = [&](uint32_t q0, uint32_t nb) -> int {
+        const uint64_t b0 = q_off[q0], nsym = q_off[q0 + nb] - b0;
+        std::vector<uint16_t> ids;
+        std::vector<uint64_t> qo(nb + 1);
+        std::vector<uint32_t> ql(nb);
+        ids_of(b0, nsym, ids, (uint16_t)plan->n_sym);  // unseen: the spare row
+        for (uint32_t q = 0; q <= nb; ++q) qo[q] = q_off[q0 + q] - b0;
+        for (uint32_t q = 0; q < nb; ++q) ql[q] = (uint32_t)(qo[q + 1] - qo[q]);
+        if (nsym) NMZ_HIP(hipMemcpyAsync(d_ids, ids.data(), nsym * 2, hipMemcpyHostToDevice, st));
+        NMZ_HIP(hipMemcpyAsync(d_qoff, qo.data(), (nb + 1) * 8, hipMemcpyHostToDevice, st));
+        NMZ_HIP(hipMemcpyAsync(d_qlen, ql.data(), nb * 4, hipMemcpyHostToDevice, st));
+        NMZ_TRY(ed_wide_build_peq(d_ids, d_qoff, nb, ns1, ndw, plan->ww, d_tbl, st));
+        EdWideArgs A;
+        A.sym = plan->d_qsym;
+        A.off = plan->d_qoff;
+        A.rowb = plan->d_rowb;
+        A.rowb_off = plan->d_rowb_off;
+        A.peq = nullptr;
+        A.knn = d_knn + (uint64_t)q0 * k;
+        A.n_pairs = (uint64_t)nb * N;
+        A.n_waves = A.n_pairs;
+        A.N = N;
+        A.k = k;
+        A.n_sym = ns1;
+        A.ndw = ndw;
+        A.shard = 0;
+        A.n_shards = 1;
+        A.w = plan->band;
+        KernelTimer kt(plan->ctx, st, "ed_wide_query");
+        NMZ_TRY(ed_wide_query_launch(A, plan->ww, d_tbl, tbl, d_qlen, nb, st));
+        NMZ_HIP(hipStreamSynchronize(st));  // the host vectors are pageable and the tables are reused
+        return NMZ_OK;
+    };
+    uint32_t q0 = 0;
+    for (uint32_t q = 0; q <= n_queries; ++q) {
+        const bool end = q == n_queries, longq = !end && q_off[q + 1] - q_off[q] > plan->maxlen;
+        if ((end || longq || q - q0 == batch) && q > q0) NMZ_TRY(run(q0, q - q0));
+        if (longq) {  // longer than the tables: the generic kernel over the plan's dense ids (unseen: 0xffff)
+            std::vector<uint16_t> ids;
+            const uint64_t n = q_off[q + 1] - q_off[q];
+            ids_of(q_off[q], n, ids, 0xffff);
+            DevBuf one;
+            struct R {
+                DevBuf &b;
+                ~R() { b.release(); }
+            } rel{one};
+            NMZ_TRY(one.ensure(Carve::bytes_for(n + 1, 2)));
+            NMZ_HIP(hipMemcpyAsync(one.ptr, ids.data(), n * 2, hipMemcpyHostToDevice, st));
+            NMZ_TRY(ed_query_generic_launch(plan, plan->d_qoff, nullptr, plan->d_qsym, false, one.ptr,
+                                            std::vector<uint64_t>{0}, std::vector<uint32_t>{(uint32_t)n},
+                                            d_knn + (uint64_t)q * k, k));
+        }
+        if (end || longq || q - q0 == batch) q0 = longq ? q + 1 : q;
+    }
+    return NMZ_OK;
+}
+
+// nmz_ed_plan_query_knn on the other plans (k_ed_tile's dense ids, or the generic plan's u64 symbols)
+static int ed_query_generic(nmz_ed_plan *plan, const uint64_t *q_off, const uint64_t *q_sym, uint32_t n_queries,
+                            uint32_t k, uint64_t *d_knn) {
+    hipStream_t st = plan->ctx->stream;
+    const bool dense = plan->tile;  // dense u16 ids (unseen query symbols: 0xffff, never a stored id)
+    static_assert(MAX_FAST_SYMBOLS <= 0xffff, "0xffff must not be a dense id");
+    const uint64_t total = q_off[n_queries];
+    DevBuf &scr = plan->ctx->buf[13];
+    NMZ_TRY(scr.ensure(Carve::bytes_for(total + 1, dense ? 2 : 8)));
+    void *d_qs = scr.ptr;
+    std::vector<uint16_t> ids;
+    if (dense) {
+        ids.resize(total);
+        for (uint64_t t = 0; t < total; ++t) {
+            auto it = plan->dict.find(q_sym[t]);
+            ids[t] = it != plan->dict.end() ? (uint16_t)it->second : (uint16_t)0xffff;
+        }
+        if (total) NMZ_HIP(hipMemcpyAsync(d_qs, ids.data(), total * 2, hipMemcpyHostToDevice, st));
+    } else if (total) {
+        NMZ_HIP(hipMemcpyAsync(d_qs, q_sym, total * 8, hipMemcpyHostToDevice, st));
+    }
+    std::vector<uint64_t> qstart(n_queries);
+    std::vector<uint32_t> qlen(n_queries);
+    for (uint32_t q = 0; q < n_queries; ++q) {
+        qstart[q] = q_off[q];
+        qlen[q] = (uint32_t)(q_off[q + 1] - q_off[q]);
+    }
+    return ed_query_generic_launch(plan, dense ? plan->d_qoff : plan->d_off64,
+                                   nullptr, dense ? (const void *)plan->d_qsym : (const void *)plan->d_sym64, !dense,
+                                   d_qs, qstart, qlen, d_knn, k);
+}
+
+}  // namespace nmz
+
+extern "C" {
+
+int nmz_ed_plan_query_knn(nmz_ed_plan *plan, const uint64_t *q_off, const uint64_t *q_sym, uint32_t n_queries,
+                          uint32_t k, uint32_t *knn_id, uint32_t *knn_dist) {
+    NMZ_CHECK(plan != nullptr, "plan is NULL");
+    NMZ_CHECK(k >= 1 && k <= 64, "k must be in [1, 64]");
+    NMZ_CHECK(n_queries == 0 || (q_off && knn_id && knn_dist), "NULL argument");
+    CtxGuard g(plan->ctx);
+    NMZ_TRY(g.rc);
+    if (n_queries == 0) return NMZ_OK;
+    const uint64_t total = q_off[n_queries];
+    NMZ_CHECK(total == 0 || q_sym, "q_sym is NULL");
+    for (uint32_t q = 0; q < n_queries; ++q) NMZ_CHECK(q_off[q] <= q_off[q + 1], "query offsets must not decrease");
+    hipStream_t st = plan->ctx->stream;
+    const uint32_t N = plan->n;
+    const uint64_t nk = (uint64_t)n_queries * k;
+    DevBuf &scr = plan->ctx->buf[11];
+    NMZ_TRY(scr.ensure(Carve::bytes_for(nk, 8) + 2 * Carve::bytes_for(nk, 4)));
+    Carve cv(scr.ptr);
+    uint64_t *d_knn = cv.take<uint64_t>(nk);
+    uint32_t *d_id = cv.take<uint32_t>(nk), *d_ds = cv.take<uint32_t>(nk);
+    hipLaunchKernelGGL(k_knn_init, dim3(ceil_div(nk, 256)), dim3(256), 0, st, d_knn, nk);
+    if (N) {
+        if (plan->bv) NMZ_TRY(ed_query_bv(plan, q_off, q_sym, n_queries, k, d_knn));
+        else if (plan->wide) NMZ_TRY(ed_query_wide(plan, q_off, q_sym, n_queries, k, d_knn));
+        else NMZ_TRY(ed_query_generic(plan, q_off, q_sym, n_queries, k, d_knn));
+    }
+    // the query kernels list in-band results only: every other stored trace is at band + 1
     hipLaunchKernelGGL(k_knn_fill, dim3(ceil_div(n_queries, 256)), dim3(256), 0, st, d_knn, n_queries, k, N,
                        plan->band + 1, 0);
     hipLaunchKernelGGL(k_knn_final, dim3(ceil_div(nk, 256)), dim3(256), 0, st, d_knn, nk, d_id, d_ds);

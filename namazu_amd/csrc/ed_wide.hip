@@ -124,9 +124,91 @@ __device__ __forceinline__ void wide_load(uint32_t (&d)[KL + 1], const uint32_t 
     }
 }
 
+// ED_w of one pair: the query side's match table `prow` ([n_sym][ndw], the query's length n) against stored trace
+// j (length m) as the text, one wave; wave-uniform arguments. min(D_band, w + 1).
+template <int KL>
+__device__ __forceinline__ uint32_t wide_pair(const EdWideArgs &A, const uint32_t *prow, uint32_t n, uint64_t j,
+                                              uint32_t m, uint32_t lane) {
+    constexpr uint32_t W = 1024 * KL;
+    const uint32_t w = A.w;
+    uint32_t r = w + 1;
+    const int64_t dd = (int64_t)m - (int64_t)n;
+    if (dd > (int64_t)w || dd < -(int64_t)w) return r;
+    if (n == 0 || m == 0) return n + m;
+    // The query's match table through a buffer descriptor: per column the load's scalar offset
+    // is (row byte offset of the candidate's symbol) + (band dword) * 4, the lane's part a
+    // constant VGPR -- one s_add per column instead of a 64-bit address computation.
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)prow, (short)0, (int)(A.n_sym * A.ndw * 4), 0x00020000);
+    const uint32_t voff = KL * lane * 4;
+    // candidate's per-position row offsets: wave-uniform, read through the scalar cache
+    typedef const uint32_t __attribute__((address_space(4))) *cptr;
+    const uint64_t rb = __builtin_amdgcn_readfirstlane((uint32_t)A.rowb_off[j]) |
+                        ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(A.rowb_off[j] >> 32)) << 32);
+    const cptr rowb = (cptr)(const void *)(A.rowb + rb);
+    WideState<KL> S;
+#pragma unroll
+    for (int k = 0; k < KL; ++k) {
+        S.M[k] = (32 * (KL * lane + k) < W) ? 0xffffffffu : 0u;
+        S.P[k] = ~S.M[k];
+    }
+    S.acc = 0;
+    uint32_t T = W;
+    // Eq dwords of column jj (1-based): row b_{jj}, dword (jj+31)>>5 + KL*lane, shift (jj-1)&31
+    auto load_col = [&](uint32_t (&d)[KL + 1], uint32_t row_bytes, uint32_t jj) {
+        const uint32_t so = row_bytes + ((jj + 31) >> 5) * 4;
+        if constexpr (KL == 4) {
+            const u32x4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, so, 0);
+            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+            d[4] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + 16, so, 0);
+        } else {
+#pragma unroll
+            for (int k = 0; k <= KL; ++k) d[k] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + 4 * k, so, 0);
+        }
+    };
+    constexpr int D = 8;
+    uint32_t cur[32], nxt[32];  // row offsets of this block's and the next block's columns
+#pragma unroll
+    for (int k = 0; k < 32; ++k) cur[k] = rowb[k];
+    uint32_t ring[D][KL + 1];
+#pragma unroll
+    for (int u = 0; u < D; ++u) load_col(ring[u], cur[u], 1 + u);
+    uint32_t j0 = 0;
+    for (; j0 + 32 <= m; j0 += 32) {
+#pragma unroll
+        for (int k = 0; k < 32; ++k) nxt[k] = rowb[j0 + 32 + k];  // streams carry 2 spare blocks
+#pragma unroll
+        for (int t = 0; t < 32; ++t) {
+            uint32_t dcur[KL + 1];
+#pragma unroll
+            for (int k = 0; k <= KL; ++k) dcur[k] = ring[t % D][k];
+            load_col(ring[t % D], t + D < 32 ? cur[t + D] : nxt[t + D - 32], j0 + t + 1 + D);
+            wide_column<KL>(S, dcur, t, lane);
+        }
+#pragma unroll
+        for (int k = 0; k < 32; ++k) cur[k] = nxt[k];
+        T += 32 - __builtin_popcount(__builtin_amdgcn_readfirstlane(S.acc));
+        if (j0 + 32 == m) return min((uint32_t)((int32_t)T + wide_prefix<KL>(S, n + W - m, lane)), w + 1);
+        uint32_t mc = 0;
+#pragma unroll
+        for (int k = 0; k < KL; ++k) mc += __builtin_popcount(S.M[k]);
+        mc = wave_sum_u32(mc);
+        if ((int32_t)T - (int32_t)mc > (int32_t)w) return r;  // band minimum > w: result w+1
+    }
+    // tail: fewer than 32 columns left, column m ends inside this block
+    const uint32_t tail = m - j0;
+    for (uint32_t t = 0; t < tail; ++t) {
+        uint32_t dcur[KL + 1];
+        load_col(dcur, rowb[j0 + t], j0 + t + 1);
+        wide_column<KL>(S, dcur, t, lane);
+    }
+    const uint32_t acc0 = __builtin_amdgcn_readfirstlane(S.acc);
+    const uint32_t Tj = T + tail - __builtin_popcount(acc0 >> (32 - tail));
+    return min((uint32_t)((int32_t)Tj + wide_prefix<KL>(S, n + W - m, lane)), w + 1);
+}
+
 template <int KL>
 __global__ __launch_bounds__(256) void k_ed_wide(EdWideArgs A) {
-    constexpr uint32_t W = 1024 * KL;
     const uint32_t nblk = gridDim.x, per_xcd = nblk / 8;
     const uint32_t lb = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
     const uint32_t lwave = __builtin_amdgcn_readfirstlane(lb * 4 + (threadIdx.x >> 6));  // wave-uniform
@@ -144,100 +226,32 @@ __global__ __launch_bounds__(256) void k_ed_wide(EdWideArgs A) {
     const uint64_t j = __builtin_amdgcn_readfirstlane((uint32_t)(i + 1 + (p - base(i))));
     const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)(A.off[i + 1] - A.off[i]));
     const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(A.off[j + 1] - A.off[j]));
-    const uint32_t w = A.w;
-    uint32_t r = w + 1;
-    const int64_t dd = (int64_t)m - (int64_t)n;
-    if (dd <= (int64_t)w && dd >= -(int64_t)w) {
-        if (n == 0 || m == 0) {
-            r = n + m;
-        } else {
-            const uint32_t *prow = A.peq + (uint64_t)i * A.n_sym * A.ndw;
-            // The query's match table through a buffer descriptor: per column the load's scalar offset
-            // is (row byte offset of the candidate's symbol) + (band dword) * 4, the lane's part a
-            // constant VGPR -- one s_add per column instead of a 64-bit address computation.
-            const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-                (void *)prow, (short)0, (int)(A.n_sym * A.ndw * 4), 0x00020000);
-            const uint32_t voff = KL * lane * 4;
-            // candidate's per-position row offsets: wave-uniform, read through the scalar cache
-            typedef const uint32_t __attribute__((address_space(4))) *cptr;
-            const uint64_t rb = __builtin_amdgcn_readfirstlane((uint32_t)A.rowb_off[j]) |
-                                ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(A.rowb_off[j] >> 32)) << 32);
-            const cptr rowb = (cptr)(const void *)(A.rowb + rb);
-            WideState<KL> S;
-#pragma unroll
-            for (int k = 0; k < KL; ++k) {
-                S.M[k] = (32 * (KL * lane + k) < W) ? 0xffffffffu : 0u;
-                S.P[k] = ~S.M[k];
-            }
-            S.acc = 0;
-            uint32_t T = W;
-            // Eq dwords of column jj (1-based): row b_{jj}, dword (jj+31)>>5 + KL*lane, shift (jj-1)&31
-            auto load_col = [&](uint32_t (&d)[KL + 1], uint32_t row_bytes, uint32_t jj) {
-                const uint32_t so = row_bytes + ((jj + 31) >> 5) * 4;
-                if constexpr (KL == 4) {
-                    const u32x4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, so, 0);
-                    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-                    d[4] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + 16, so, 0);
-                } else {
-#pragma unroll
-                    for (int k = 0; k <= KL; ++k) d[k] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + 4 * k, so, 0);
-                }
-            };
-            constexpr int D = 8;
-            uint32_t cur[32], nxt[32];  // row offsets of this block's and the next block's columns
-#pragma unroll
-            for (int k = 0; k < 32; ++k) cur[k] = rowb[k];
-            uint32_t ring[D][KL + 1];
-#pragma unroll
-            for (int u = 0; u < D; ++u) load_col(ring[u], cur[u], 1 + u);
-            bool done = false;
-            uint32_t j0 = 0;
-            for (; j0 + 32 <= m; j0 += 32) {
-#pragma unroll
-                for (int k = 0; k < 32; ++k) nxt[k] = rowb[j0 + 32 + k];  // streams carry 2 spare blocks
-#pragma unroll
-                for (int t = 0; t < 32; ++t) {
-                    uint32_t dcur[KL + 1];
-#pragma unroll
-                    for (int k = 0; k <= KL; ++k) dcur[k] = ring[t % D][k];
-                    load_col(ring[t % D], t + D < 32 ? cur[t + D] : nxt[t + D - 32], j0 + t + 1 + D);
-                    wide_column<KL>(S, dcur, t, lane);
-                }
-#pragma unroll
-                for (int k = 0; k < 32; ++k) cur[k] = nxt[k];
-                T += 32 - __builtin_popcount(__builtin_amdgcn_readfirstlane(S.acc));
-                if (j0 + 32 == m) {
-                    r = min((uint32_t)((int32_t)T + wide_prefix<KL>(S, n + W - m, lane)), w + 1);
-                    done = true;
-                    break;
-                }
-                uint32_t mc = 0;
-#pragma unroll
-                for (int k = 0; k < KL; ++k) mc += __builtin_popcount(S.M[k]);
-                mc = wave_sum_u32(mc);
-                if ((int32_t)T - (int32_t)mc > (int32_t)w) {  // band minimum > w: result w+1
-                    done = true;
-                    break;
-                }
-            }
-            if (!done) {
-                // tail: fewer than 32 columns left, column m ends inside this block
-                const uint32_t tail = m - j0;
-                for (uint32_t t = 0; t < tail; ++t) {
-                    uint32_t dcur[KL + 1];
-                    load_col(dcur, rowb[j0 + t], j0 + t + 1);
-                    wide_column<KL>(S, dcur, t, lane);
-                }
-                const uint32_t acc0 = __builtin_amdgcn_readfirstlane(S.acc);
-                const uint32_t Tj = T + tail - __builtin_popcount(acc0 >> (32 - tail));
-                r = min((uint32_t)((int32_t)Tj + wide_prefix<KL>(S, n + W - m, lane)), w + 1);
-            }
-        }
-    }
+    const uint32_t r = wide_pair<KL>(A, A.peq + (uint64_t)i * A.n_sym * A.ndw, n, j, m, lane);
     if (lane == 0) {
         wide_knn_insert(A.knn + i * A.k, A.k, ((uint64_t)r << 32) | j);
         wide_knn_insert(A.knn + j * A.k, A.k, ((uint64_t)r << 32) | i);
     }
+}
+
+// Single queries against the resident store (nmz_ed_plan_query_knn on a wide plan): wave (query q, stored trace j),
+// the query's match table built for this call (qpeq: [n_q][qstride] dwords, rows over the store's alphabet; query
+// symbols the store has never seen set bits in a row no stored trace names), results straight into the query's
+// k-NN list. A query's waves are consecutive in the XCD-remapped order, so its table stays in one XCD's L2.
+template <int KL>
+__global__ __launch_bounds__(256) void k_ed_wide_query(EdWideArgs A, const uint32_t *__restrict__ qpeq,
+                                                       uint64_t qstride, const uint32_t *__restrict__ qlen,
+                                                       uint32_t n_q) {
+    const uint32_t nblk = gridDim.x, per_xcd = nblk / 8;
+    const uint32_t lb = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
+    const uint64_t lwave = __builtin_amdgcn_readfirstlane(lb * 4 + (threadIdx.x >> 6));
+    const uint32_t lane = threadIdx.x & 63;
+    if (lwave >= (uint64_t)n_q * A.N) return;
+    const uint32_t q = __builtin_amdgcn_readfirstlane((uint32_t)(lwave / A.N));
+    const uint64_t j = __builtin_amdgcn_readfirstlane((uint32_t)(lwave % A.N));
+    const uint32_t n = __builtin_amdgcn_readfirstlane(qlen[q]);
+    const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(A.off[j + 1] - A.off[j]));
+    const uint32_t r = wide_pair<KL>(A, qpeq + (uint64_t)q * qstride, n, j, m, lane);
+    if (lane == 0 && r <= A.w) wide_knn_insert(A.knn + (uint64_t)q * A.k, A.k, ((uint64_t)r << 32) | j);
 }
 
 // match bitmaps: peq[i][c][dword], bit (pos + 1 + OFF) of row sym[pos] for every position of trace i
@@ -270,6 +284,24 @@ int ed_wide_build_peq(const uint16_t *d_sym, const uint64_t *d_off, uint32_t N, 
     NMZ_HIP(hipMemsetAsync(d_peq, 0, (size_t)N * n_sym * ndw * 4, st));
     hipLaunchKernelGGL(k_wide_peq_build, dim3(2048), dim3(256), 0, st, d_sym, d_off, N, n_sym, ndw, band + 31,
                        d_peq);
+    NMZ_HIP(hipGetLastError());
+    return NMZ_OK;
+}
+
+int ed_wide_query_launch(const EdWideArgs &A, uint32_t band, const uint32_t *qpeq, uint64_t qstride,
+                         const uint32_t *qlen, uint32_t n_q, hipStream_t st) {
+    uint64_t blocks = ((uint64_t)n_q * A.N + 3) / 4;
+    blocks = (blocks + 7) / 8 * 8;
+    if (blocks == 0) return NMZ_OK;
+    NMZ_CHECK(blocks < (1ULL << 30), "too many pairs for one launch");
+    const dim3 g((unsigned)blocks), b(256);
+    switch (band) {
+        case 1024: hipLaunchKernelGGL(k_ed_wide_query<1>, g, b, 0, st, A, qpeq, qstride, qlen, n_q); break;
+        case 2048: hipLaunchKernelGGL(k_ed_wide_query<2>, g, b, 0, st, A, qpeq, qstride, qlen, n_q); break;
+        case 4096: hipLaunchKernelGGL(k_ed_wide_query<4>, g, b, 0, st, A, qpeq, qstride, qlen, n_q); break;
+        case 8192: hipLaunchKernelGGL(k_ed_wide_query<8>, g, b, 0, st, A, qpeq, qstride, qlen, n_q); break;
+        default: return fail(NMZ_EINVAL, "internal: band has no wide kernel");
+    }
     NMZ_HIP(hipGetLastError());
     return NMZ_OK;
 }

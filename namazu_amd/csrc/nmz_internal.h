@@ -134,6 +134,10 @@ uint32_t ed_wide_ndw(uint32_t band, uint32_t max_len);
 int ed_wide_build_peq(const uint16_t *d_sym, const uint64_t *d_off, uint32_t N, uint32_t n_sym, uint32_t ndw,
                       uint32_t band, uint32_t *d_peq, hipStream_t st);
 int ed_wide_launch(const EdWideArgs &A, uint32_t band, hipStream_t st);
+// single queries: wave (q, j) over n_q query tables qpeq + q * qstride (rows over the store's alphabet) x the N
+// stored traces of A; in-band results into A.knn + q * k
+int ed_wide_query_launch(const EdWideArgs &A, uint32_t band, const uint32_t *qpeq, uint64_t qstride,
+                         const uint32_t *qlen, uint32_t n_q, hipStream_t st);
 
 // replayable plan: one hint-length class (a segment of every table row)
 struct ClassInfo {

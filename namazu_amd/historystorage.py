@@ -269,12 +269,12 @@ def ed_pairs(ts, pairs, band, ctx=None):
 
 
 class SimilarityIndex:
-    """A stored TraceSet resident on the GPU for single-query similarity search.
+    """A stored TraceSet resident on the GPU for single-query similarity search (SearchSimilar).
 
-    Band <= 64 (the bit-parallel plan, direct or compact tables): each query() is one nmz_ed_plan_query_knn
-    launch over the resident traces. Other bands, stores or queries whose symbols do not fit the LDS tables, or
-    queries longer than every stored trace go through nmz_ed_pairs (the generic GPU kernel) against the same
-    TraceSet."""
+    Every band and plan kind answers through one nmz_ed_plan_query_knn call over the resident store: the
+    bit-parallel query kernel (band <= 64), the wide-band query kernel (64 < band <= 8,192: each query's match
+    table built once per call, one wave per (query, stored trace)), or the resident generic kernel (other plans,
+    queries whose symbols overflow the compact tables, and queries longer than every stored trace)."""
 
     def __init__(self, ts, band, ctx=None):
         import ctypes
@@ -285,32 +285,21 @@ class SimilarityIndex:
         L = _lib.load()
         _lib.check(L.nmz_ed_plan_create(self.ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), len(ts), self.band,
                                         ctypes.byref(self.plan)))
-        self.bitparallel = L.nmz_ed_plan_is_fast(self.plan) == 2
-        self.maxlen = int(np.diff(ts.off.astype(np.int64)).max()) if len(ts) else 0
+        self.kind = {3: "wide", 2: "bitparallel", 1: "tile", 0: "generic"}[L.nmz_ed_plan_is_fast(self.plan)]
+        self.bitparallel = self.kind == "bitparallel"
 
     def query(self, queries, k):
-        """queries: event-symbol arrays -> (ids [n, k], dists [n, k]), NMZ_NONE padded."""
+        """queries: event-symbol arrays -> (ids [n, k], dists [n, k]) by (ED_band asc, id asc), NMZ_NONE padded."""
         n, N = len(queries), len(self.ts)
         ids = np.full((n, k), _lib.NMZ_NONE, np.uint32)
         ds = np.full((n, k), _lib.NMZ_NONE, np.uint32)
         if n == 0 or N == 0 or k == 0:
             return ids, ds
-        qs = [np.asarray(q, np.uint64) for q in queries]
-        if self.bitparallel and k <= 64 and max(len(q) for q in qs) <= self.maxlen:
-            qset = TraceSet(qs)
-            try:
-                _lib.check(_lib.load().nmz_ed_plan_query_knn(self.plan, _lib.ptr(qset.off), _lib.ptr(qset.sym), n,
-                                                              k, _lib.ptr(ids), _lib.ptr(ds)))
-                return ids, ds
-            except _lib.NmzInvalidArgument:
-                pass  # compact tables: the queries hold more distinct symbols than LDS rows -> generic kernel
-        for r, q in enumerate(qs):  # generic kernel, pairs (query, every stored trace)
-            both = TraceSet([q] + [self.ts.trace(i) for i in range(N)])
-            pairs = np.stack([np.zeros(N, np.uint32), np.arange(1, N + 1, dtype=np.uint32)], 1)
-            d = ed_pairs(both, pairs, self.band, ctx=self.ctx)
-            order = np.lexsort((np.arange(N), d))[:k]
-            ids[r, :len(order)] = order
-            ds[r, :len(order)] = d[order]
+        if k > 64:
+            raise ValueError("nmz_ed_plan_query_knn answers k <= 64")
+        qset = TraceSet([np.asarray(q, np.uint64) for q in queries])
+        _lib.check(_lib.load().nmz_ed_plan_query_knn(self.plan, _lib.ptr(qset.off), _lib.ptr(qset.sym), n, k,
+                                                      _lib.ptr(ids), _lib.ptr(ds)))
         return ids, ds
 
     def close(self):

@@ -370,6 +370,71 @@ def test_similarity_index_queries_vs_oracle(ctx, w, n, lmin, lmax, mut, alphabet
     idx.close()
 
 
+def _query_vs_oracle(ts, qs, w, ids, ds, k):
+    n = len(ts)
+    for r, q in enumerate(qs):
+        both = hs.TraceSet([q] + [ts.trace(i) for i in range(n)])
+        pairs = np.stack([np.zeros(n, np.uint32), np.arange(1, n + 1, dtype=np.uint32)], 1)
+        d = O.ed_pairs(both.off, both.sym, pairs, w, nthreads=16)
+        order = np.lexsort((np.arange(n), d))[:k]
+        assert ds[r, :len(order)].tolist() == d[order].tolist(), r
+        assert ids[r, :len(order)].tolist() == order.tolist(), r
+
+
+@pytest.mark.parametrize("w", [100, 1024, 4096])
+def test_similarity_index_wide_band_queries_vs_oracle(ctx, w):
+    """Single queries for bands above 64 against a resident 65,536-event store (16 traces x 4,096 events): the
+    wide plan's query kernel (k_ed_wide_query: each query's match table once per call, a wave per (query, stored
+    trace)) vs the oracle's brute force. Queries: a stored trace (distance 0 to itself), a shortened one, a
+    mutated one with symbols the store never saw, an empty one, and one longer than every stored trace (within
+    the band of some of them: the resident generic kernel)."""
+    rng = np.random.default_rng(w)
+    ts = make_traces(16, 4096, 4096, 0.06, alphabet=30, rng=rng)
+    assert int(ts.off[-1]) == 65_536
+    idx = hs.SimilarityIndex(ts, w, ctx=ctx)
+    assert idx.kind == "wide"
+    t = ts.trace(7).copy()
+    t[rng.random(len(t)) < 0.05] = np.uint64(12345)  # unseen symbol
+    longer = np.concatenate([ts.trace(5), ts.trace(6)[:w // 2 + 10]])
+    qs = [ts.trace(3), ts.trace(9)[:4096 - w // 2], t, np.zeros(0, np.uint64), longer]
+    k = 8
+    ids, ds = idx.query(qs, k)
+    idx.close()
+    _query_vs_oracle(ts, qs, w, ids, ds, k)
+    assert ds[0, 0] == 0
+
+
+def test_similarity_index_generic_plan_queries_vs_oracle(ctx):
+    """A band beyond the wide kernels (9,000 > 8,192) makes a generic plan: its queries run on the resident u64
+    symbols (k_ed_query_generic), vs the oracle."""
+    rng = np.random.default_rng(5)
+    ts = make_traces(40, 150, 260, 0.2, alphabet=9, rng=rng)
+    idx = hs.SimilarityIndex(ts, 9000, ctx=ctx)
+    assert idx.kind == "generic"
+    qs = [ts.trace(2), ts.trace(30)[:100], np.zeros(0, np.uint64),
+          np.concatenate([ts.trace(1), ts.trace(1)]), np.full(40, 999, np.uint64)]
+    ids, ds = idx.query(qs, 6)
+    idx.close()
+    _query_vs_oracle(ts, qs, 9000, ids, ds, 6)
+
+
+def test_similarity_index_long_queries_on_bitparallel_plan(ctx):
+    """Queries longer than every stored trace on a bit-parallel plan (band 32): within the band of the longest
+    stored traces they have real distances <= 32, so they run on the resident generic kernel over the plan's
+    encoded streams instead of being refused."""
+    rng = np.random.default_rng(8)
+    ts = make_traces(120, 180, 200, 0.02, alphabet=14, rng=rng)
+    idx = hs.SimilarityIndex(ts, 32, ctx=ctx)
+    assert idx.bitparallel
+    L = max(len(ts.trace(i)) for i in range(len(ts)))
+    longest = [i for i in range(len(ts)) if len(ts.trace(i)) == L][0]
+    qs = [np.concatenate([ts.trace(longest), ts.trace(0)[:10]]), ts.trace(4), np.full(L + 40, 7, np.uint64)]
+    ids, ds = idx.query(qs, 5)
+    idx.close()
+    _query_vs_oracle(ts, qs, 32, ids, ds, 5)
+    assert ds[0, 0] <= 32
+
+
 def test_search_similar_on_storage_uses_resident_index(ctx, tmp_path):
     from namazu_amd.signal import Event
     from tests.test_host import _make_storage
@@ -499,17 +564,23 @@ def test_knn_qgram_filter_exact(ctx, monkeypatch, w, alphabet, max_edits):
     rng = np.random.default_rng(w * 1000 + alphabet)
     ts = _edited_family(400, 300, alphabet, max_edits, rng)
     n, k = len(ts), 8
-    plan = ctypes.c_void_p()
-    _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), n, w, ctypes.byref(plan)))
-    assert L.nmz_ed_plan_is_fast(plan) == 2
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
-    def run(qgram):
+    def make_plan(qgram):  # the filter switch is plan state, fixed at creation (NMZ_ED_QGRAM read then)
         monkeypatch.setenv("NMZ_ED_QGRAM", "1" if qgram else "0")
+        plan = ctypes.c_void_p()
+        _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), n, w, ctypes.byref(plan)))
+        assert L.nmz_ed_plan_is_fast(plan) == 2
+        return plan
+
+    def run(qgram):
+        plan = make_plan(qgram)
+        monkeypatch.setenv("NMZ_ED_QGRAM", "0" if qgram else "1")  # a later change does not reach the plan
         d = torch.empty(n * k, dtype=torch.int64, device="cuda")
         _lib.check(L.nmz_ed_allpairs_knn_dev(plan, k, ctypes.c_void_p(d.data_ptr()), stream))
         cnt = np.zeros(_lib.NMZ_ED_NCOUNTERS, np.uint64)
         _lib.check(L.nmz_ed_plan_counters(plan, _lib.ptr(cnt), stream))
+        L.nmz_ed_plan_destroy(plan)
         return d.cpu().numpy().view(np.uint64).reshape(n, k), cnt
 
     on, c_on = run(True)
@@ -517,7 +588,7 @@ def test_knn_qgram_filter_exact(ctx, monkeypatch, w, alphabet, max_edits):
     S = 3
     parts = torch.empty(S * n * k, dtype=torch.int64, device="cuda")
     out = torch.empty(n * k, dtype=torch.int64, device="cuda")
-    monkeypatch.setenv("NMZ_ED_QGRAM", "1")
+    plan = make_plan(True)
     for s in range(S):
         _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, s, S, ctypes.c_void_p(parts.data_ptr() + s * n * k * 8),
                                                    stream))
