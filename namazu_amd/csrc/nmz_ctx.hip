@@ -178,17 +178,23 @@ uint32_t scatter_per_thread() {
 }
 
 
+// The block's seeds are first counting-sorted by bucket in LDS (block-local ranks from LDS atomics, a scan of the
+// 256 counts), then written out in that order: consecutive threads write consecutive slots of one bucket's range,
+// so a wave's stores are runs of ~SCATTER_PER_THREAD entries instead of 64 scattered 8-B writes.
 template <uint32_t SCATTER_PER_THREAD>
 __global__ __launch_bounds__(256) void k_bucket_scatter(const uint64_t *__restrict__ h0, uint64_t n,
                                                         const uint32_t *__restrict__ offset,
                                                         uint32_t *__restrict__ cursor,
                                                         uint64_t *__restrict__ sorted_h0,
                                                         uint32_t *__restrict__ sorted_idx) {
-    __shared__ uint32_t cnt[256], base[256];
-    const uint32_t t = threadIdx.x;
+    constexpr uint32_t NB = 256 * SCATTER_PER_THREAD;
+    __shared__ uint32_t cnt[256], base[256], loff[256];
+    __shared__ uint16_t si[NB];  // the block's seeds in bucket order (offsets in the block; h0 re-read from L2)
+    __shared__ uint32_t wsum[4];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
     cnt[t] = 0;
     __syncthreads();
-    const uint64_t b0 = (uint64_t)blockIdx.x * 256 * SCATTER_PER_THREAD;
+    const uint64_t b0 = (uint64_t)blockIdx.x * NB;
     uint64_t hv[SCATTER_PER_THREAD];
     uint32_t rk[SCATTER_PER_THREAD];
 #pragma unroll
@@ -198,15 +204,39 @@ __global__ __launch_bounds__(256) void k_bucket_scatter(const uint64_t *__restri
         rk[r] = i < n ? atomicAdd(&cnt[hv[r] & 0xff], 1u) : 0u;
     }
     __syncthreads();
-    if (cnt[t]) base[t] = offset[t] + atomicAdd(&cursor[t * BUCKET_STRIDE], cnt[t]);
+    const uint32_t c = cnt[t];
+    if (c) base[t] = offset[t] + atomicAdd(&cursor[t * BUCKET_STRIDE], c);
+    // exclusive scan of the 256 counts: the buckets' local offsets
+    uint32_t a = c;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t v = __shfl_up(a, d, 64);
+        if (lane >= d) a += v;
+    }
+    if (lane == 63) wsum[w] = a;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (uint32_t i = 0; i < w; ++i) pre += wsum[i];
+    loff[t] = pre + a - c;
     __syncthreads();
 #pragma unroll
     for (uint32_t r = 0; r < SCATTER_PER_THREAD; ++r) {
         const uint64_t i = b0 + (uint64_t)r * 256 + t;
         if (i < n) {
-            const uint32_t pos = base[hv[r] & 0xff] + rk[r];
-            sorted_h0[pos] = hv[r];
-            sorted_idx[pos] = (uint32_t)i;
+            si[loff[hv[r] & 0xff] + rk[r]] = (uint16_t)(r * 256 + t);
+        }
+    }
+    __syncthreads();
+    const uint32_t m = (uint32_t)min<uint64_t>(NB, n - b0);
+#pragma unroll
+    for (uint32_t r = 0; r < SCATTER_PER_THREAD; ++r) {
+        const uint32_t j = r * 256 + t;
+        if (j < m) {
+            const uint32_t o = si[j];
+            const uint64_t h = h0[b0 + o];  // read by this block above: an L2 hit
+            const uint32_t bk = (uint32_t)h & 0xff;
+            const uint32_t pos = base[bk] + (j - loff[bk]);
+            sorted_h0[pos] = h;
+            sorted_idx[pos] = (uint32_t)(b0 + o);
         }
     }
 }

@@ -342,18 +342,38 @@ __device__ __forceinline__ uint64_t fnv_decimal_u64(uint64_t h, uint64_t v) {
 }
 
 // seed prefix of the seeds "seed_lo" .. "seed_lo + n - 1" (decimal strings generated here: no seed CSR), with
-// the same fused bucket histogram as k_seed_prefix
+// the same fused bucket histogram as k_seed_prefix. decimal(v) = decimal(v / 100) || two digits of v % 100 for
+// v >= 100, and a block's 256 ppt consecutive seeds share at most 256 ppt / 100 + 2 prefixes v / 100: one lane per
+// prefix hashes it (fnv_decimal_u64, ~300 VALU) into LDS once, then each seed takes its prefix's state and two FNV
+// steps (~25 VALU per seed instead of ~300). Seeds below 100, and a block whose range wraps past 2^64, hash
+// every seed in full.
+constexpr uint32_t DEC_MAX_PREFIX = 64;  // 256 ppt / 100 + 2 <= 64 for ppt <= 16
 __global__ __launch_bounds__(256) void k_seed_prefix_decimal(uint64_t seed_lo, uint64_t n, uint64_t *__restrict__ h0,
                                                              uint32_t *__restrict__ count, uint32_t ppt) {
     __shared__ uint32_t hist[256];
+    __shared__ uint64_t ph[DEC_MAX_PREFIX];
     hist[threadIdx.x] = 0;
-    __syncthreads();
     const uint64_t b0 = (uint64_t)blockIdx.x * 256 * ppt;
+    const uint64_t nb = min<uint64_t>(256 * (uint64_t)ppt, n - b0);  // seeds of this block (>= 1)
+    const uint64_t v0 = seed_lo + b0;
+    const uint64_t P0 = v0 / 100;
+    const uint32_t r0 = (uint32_t)(v0 - P0 * 100);
+    const uint32_t np = (r0 + (uint32_t)nb - 1) / 100 + 1;  // prefixes P0 .. P0 + np - 1
+    // the shared-prefix form: every seed >= 100, no wrap past 2^64, the prefixes fit the table
+    const bool fast = v0 >= 100 && v0 + (nb - 1) >= v0 && np <= DEC_MAX_PREFIX;
+    if (fast && threadIdx.x < np) ph[threadIdx.x] = fnv_decimal_u64(FNV_OFFSET, P0 + threadIdx.x);
+    __syncthreads();
     for (uint32_t r = 0; r < ppt; ++r) {
-        const uint64_t s = b0 + (uint64_t)r * 256 + threadIdx.x;
-        if (s < n) {
-            const uint64_t h = fnv_decimal_u64(FNV_OFFSET, seed_lo + s);
-            h0[s] = h;
+        const uint32_t i = r * 256 + threadIdx.x;
+        if (i < nb) {
+            uint64_t h;
+            if (fast) {
+                const uint32_t x = r0 + i, q = x / 100, lo = x - q * 100, d1 = lo / 10;
+                h = fnv_step(fnv_step(ph[q], '0' + d1), '0' + (lo - d1 * 10));
+            } else {
+                h = fnv_decimal_u64(FNV_OFFSET, v0 + i);
+            }
+            h0[b0 + i] = h;
             atomicAdd(&hist[h & 0xff], 1u);
         }
     }
