@@ -284,29 +284,64 @@ __global__ __launch_bounds__(1024) void k_replayable_table_segsort(const uint4 *
 // ---------------------------------------------------------------------------
 // seed prefix: h0 = FNV(seed bytes)
 // ---------------------------------------------------------------------------
+// A block's ppt * 256 seeds are contiguous in the CSR: their offsets and (when they fit SEED_LDS_BYTES) their bytes
+// are staged in LDS with coalesced loads, and each thread hashes its seeds from LDS. (Per-thread global loads of a
+// seed's offsets and bytes made every seed a chain of dependent global loads: ~21 us per 2^20 seeds.)
+#ifndef NMZ_SEED_LDS_BYTES
+#define NMZ_SEED_LDS_BYTES 16384
+#endif
+constexpr uint32_t SEED_LDS_BYTES = NMZ_SEED_LDS_BYTES;
+constexpr uint32_t SEED_LDS_MAX_SEEDS = NMZ_SEED_LDS_BYTES >= 16384 ? 256 * 16 : 256 * 8;
 __global__ __launch_bounds__(256) void k_seed_prefix(const uint32_t *__restrict__ soff,
                                                      const uint8_t *__restrict__ sbytes, uint64_t n,
                                                      uint64_t *__restrict__ h0, uint32_t *__restrict__ count,
                                                      uint32_t ppt) {
     // fused bucket histogram (low byte of h0): LDS counts, one global atomic per (block, bucket)
     __shared__ uint32_t hist[256];
+    __shared__ uint32_t so[SEED_LDS_BYTES ? SEED_LDS_MAX_SEEDS + 1 : 1];
+    __shared__ uint32_t sb[SEED_LDS_BYTES ? SEED_LDS_BYTES / 4 : 1];
     hist[threadIdx.x] = 0;
-    __syncthreads();
     const uint64_t b0 = (uint64_t)blockIdx.x * 256 * ppt;
+    const uint32_t nb = (uint32_t)min<uint64_t>(256 * (uint64_t)ppt, n - b0);
+    const bool staged_off = NMZ_SEED_LDS_BYTES > 0 && nb <= SEED_LDS_MAX_SEEDS;
+    if (staged_off)
+        for (uint32_t i = threadIdx.x; i <= nb; i += 256) so[i] = soff[b0 + i];
+    __syncthreads();
+    const uint32_t B0 = staged_off ? so[0] : 0u, B1 = staged_off ? so[nb] : 0u;
+    // LDS byte off0 + p holds seed byte B0 + p, off0 = the address's offset in its dword, so the whole dwords
+    // between the first and last partial dword copy as aligned dwords (no byte outside [B0, B1) is read)
+    const uint32_t off0 = (uint32_t)(reinterpret_cast<uintptr_t>(sbytes + B0) & 3u), total = B1 - B0;
+    const bool staged = staged_off && off0 + total <= SEED_LDS_BYTES;
+    const uint32_t A0 = B0 - off0;  // seed byte positions map to LDS byte (position - A0)
+    if (staged) {
+        uint8_t *lbw = reinterpret_cast<uint8_t *>(sb);
+        const uint32_t head = min((4u - off0) & 3u, total), nint = (total - head) / 4, tail0 = head + 4 * nint;
+        if (threadIdx.x < head) lbw[off0 + threadIdx.x] = sbytes[B0 + threadIdx.x];
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(sbytes + B0 + head);
+        for (uint32_t i = threadIdx.x; i < nint; i += 256) sb[(off0 + head) / 4 + i] = src[i];
+        if (threadIdx.x < total - tail0) lbw[off0 + tail0 + threadIdx.x] = sbytes[B0 + tail0 + threadIdx.x];
+    }
+    __syncthreads();
+    const uint8_t *lb = reinterpret_cast<const uint8_t *>(sb);
     for (uint32_t r = 0; r < ppt; ++r) {
-        const uint64_t s = b0 + (uint64_t)r * 256 + threadIdx.x;
-        if (s < n) {
+        const uint32_t i = r * 256 + threadIdx.x;
+        if (i < nb) {
             uint64_t h = FNV_OFFSET;
-            uint32_t i = soff[s];
-            const uint32_t end = soff[s + 1];
-            // bytes up to a 4-byte boundary, then whole dwords, then the tail
-            for (; i < end && (reinterpret_cast<uintptr_t>(sbytes + i) & 3); ++i) h = fnv_step(h, sbytes[i]);
-            for (; i + 4 <= end; i += 4) {
-                const uint32_t w = *reinterpret_cast<const uint32_t *>(sbytes + i);
-                h = fnv_step(fnv_step(fnv_step(fnv_step(h, w & 0xff), (w >> 8) & 0xff), (w >> 16) & 0xff), w >> 24);
+            if (staged) {
+                const uint32_t e = so[i + 1] - A0;
+                for (uint32_t t = so[i] - A0; t < e; ++t) h = fnv_step(h, lb[t]);
+            } else {
+                uint32_t t = soff[b0 + i];
+                const uint32_t end = soff[b0 + i + 1];
+                // bytes up to a 4-byte boundary, then whole dwords, then the tail
+                for (; t < end && (reinterpret_cast<uintptr_t>(sbytes + t) & 3); ++t) h = fnv_step(h, sbytes[t]);
+                for (; t + 4 <= end; t += 4) {
+                    const uint32_t w = *reinterpret_cast<const uint32_t *>(sbytes + t);
+                    h = fnv_step(fnv_step(fnv_step(fnv_step(h, w & 0xff), (w >> 8) & 0xff), (w >> 16) & 0xff), w >> 24);
+                }
+                for (; t < end; ++t) h = fnv_step(h, sbytes[t]);
             }
-            for (; i < end; ++i) h = fnv_step(h, sbytes[i]);
-            h0[s] = h;
+            h0[b0 + i] = h;
             atomicAdd(&hist[h & 0xff], 1u);
         }
     }

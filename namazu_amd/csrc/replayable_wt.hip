@@ -371,21 +371,32 @@ struct WtVConst {
     uint32_t st4[5];  // lifting-search steps in bytes: 4 << r
 };
 
-template <bool BIG>
+// NS seeds per lane (arrays indexed by u, unrolled): the wave-uniform control -- segment parameters, lifting
+// rounds, level constants, loop trips, ballots -- is paid once for NS seeds, and the NS seeds' read chains are
+// independent, so a wave keeps 2 NS dependent LDS chains in flight per descent level instead of 2.
+template <bool BIG, int NS>
 __device__ __forceinline__ void wt_seed_class(const WtVConst &vc, const WtClass &ci, const char *__restrict__ img,
-                                              const uint4 *__restrict__ row, uint64_t h0, uint32_t m, uint64_t mu,
-                                              uint32_t m_k64, uint32_t msh, uint64_t &sum, uint32_t &W,
-                                              uint64_t &key) {
+                                              const uint4 *__restrict__ row, const uint64_t (&h0)[NS], uint32_t m,
+                                              uint64_t mu, uint32_t m_k64, uint32_t msh, uint64_t (&sum)[NS],
+                                              uint32_t (&W)[NS], uint64_t (&key)[NS]) {
     const uint32_t n = ci.n;
-    const uint64_t H = h0 * ci.pn;
-    const uint64_t nH = ~H;
-    const uint32_t Hm = BIG ? mod_barrett64(H, m, mu) : mod_barrett_small(H, m, mu);
-    const uint32_t t2 = Hm + m_k64;
-    const uint32_t Hm2 = BIG ? ((t2 < Hm || t2 >= m) ? t2 - m : t2) : min(t2, t2 - m);
-    uint32_t d = 0;
+    uint64_t nH[NS];
+    uint32_t Hm[NS], Hm2[NS];
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+        const uint64_t H = h0[u] * ci.pn;
+        nH[u] = ~H;
+        Hm[u] = BIG ? mod_barrett64(H, m, mu) : mod_barrett_small(H, m, mu);
+        const uint32_t t2 = Hm[u] + m_k64;
+        Hm2[u] = BIG ? ((t2 < Hm[u] || t2 >= m) ? t2 - m : t2) : min(t2, t2 - m);
+    }
     if (n <= WT_BRUTE) {
-        for (uint32_t i = 0; i < n; ++i) wt_decide<BIG>(row[ci.start + i], nH, Hm, Hm2, m, d, W, key);
-        sum += (uint64_t)d * Hm + (uint64_t)(n - d) * Hm2;
+#pragma unroll
+        for (int u = 0; u < NS; ++u) {
+            uint32_t d = 0;
+            for (uint32_t i = 0; i < n; ++i) wt_decide<BIG>(row[ci.start + i], nH[u], Hm[u], Hm2[u], m, d, W[u], key[u]);
+            sum[u] += (uint64_t)d * Hm[u] + (uint64_t)(n - d) * Hm2[u];
+        }
         return;
     }
     const uint32_t *__restrict__ cm = reinterpret_cast<const uint32_t *>(img + ci.o_cm);
@@ -394,13 +405,21 @@ __device__ __forceinline__ void wt_seed_class(const WtVConst &vc, const WtClass 
     const uint16_t *__restrict__ im = reinterpret_cast<const uint16_t *>(img + ci.o_im);
     const uint16_t *__restrict__ ic = reinterpret_cast<const uint16_t *>(img + ci.o_ic);
     const uint32_t *__restrict__ pm = reinterpret_cast<const uint32_t *>(img + ci.o_pm);
-    const uint32_t nh = (uint32_t)(nH >> 32);
-    const uint32_t XA = m - Hm, XB = m - Hm2;  // t wraps <=> Cm >= X
-    // three lifting searches stepped together (every read of a round in flight at once) from the bucket starts:
-    // every entry past the bucket is >= the bound, and the sentinel at n ends every probe past the array
-    // (pointer form: a round's three probes are LDS reads with immediate offsets; WT_PAD sentinels end the probes of
-    // up to five rounds past the array, longer searches -- repeated hints -- clamp at the sentinel at n)
-    const uint32_t *pa = chi + ic[nh >> 24], *pb = cm + im[XA >> msh], *pc = cm + im[XB >> msh];
+    uint32_t nh[NS], XA[NS], XB[NS];
+    const uint32_t *pa[NS], *pb[NS], *pc[NS];
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+        nh[u] = (uint32_t)(nH[u] >> 32);
+        XA[u] = m - Hm[u];  // t wraps <=> Cm >= X
+        XB[u] = m - Hm2[u];
+        // three lifting searches stepped together (every read of a round in flight at once) from the bucket starts:
+        // every entry past the bucket is >= the bound, and the sentinel at n ends every probe past the array
+        // (pointer form: a round's probes are LDS reads with immediate offsets; WT_PAD sentinels end the probes of up
+        // to five rounds past the array, longer searches -- repeated hints -- clamp at the sentinel at n)
+        pa[u] = chi + ic[nh[u] >> 24];
+        pb[u] = cm + im[XA[u] >> msh];
+        pc[u] = cm + im[XB[u] >> msh];
+    }
     const uint32_t rS = ci.rS;
 #ifdef WT_ABL_LIFT
     if (0)
@@ -411,34 +430,45 @@ __device__ __forceinline__ void wt_seed_class(const WtVConst &vc, const WtClass 
             if (rS > (uint32_t)r) {
                 constexpr uint32_t one = 1;
                 const uint32_t st = one << r, st4 = vc.st4[r];  // the step in bytes, in a VGPR (a VOP2 select)
-                const uint32_t a = pa[st - 1], b = pb[st - 1], c = pc[st - 1];
-                pa = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(pa) + (a < nh ? st4 : 0u));
-                pb = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(pb) + (b < XA ? st4 : 0u));
-                pc = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(pc) + (c < XB ? st4 : 0u));
+#pragma unroll
+                for (int u = 0; u < NS; ++u) {
+                    const uint32_t a = pa[u][st - 1], b = pb[u][st - 1], c = pc[u][st - 1];
+                    pa[u] = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(pa[u]) + (a < nh[u] ? st4 : 0u));
+                    pb[u] = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(pb[u]) + (b < XA[u] ? st4 : 0u));
+                    pc[u] = reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(pc[u]) + (c < XB[u] ? st4 : 0u));
+                }
             }
         }
     } else {
         const uint32_t *ea = chi + n, *eb = cm + n;
         for (uint32_t st = (1u << rS) >> 1; st; st >>= 1) {
-            const uint32_t a = *min(pa + st - 1, ea), b = *min(pb + st - 1, eb), c = *min(pc + st - 1, eb);
-            pa += a < nh ? st : 0u;
-            pb += b < XA ? st : 0u;
-            pc += c < XB ? st : 0u;
+#pragma unroll
+            for (int u = 0; u < NS; ++u) {
+                const uint32_t a = *min(pa[u] + st - 1, ea), b = *min(pb[u] + st - 1, eb), c = *min(pc[u] + st - 1, eb);
+                pa[u] += a < nh[u] ? st : 0u;
+                pb[u] += b < XA[u] ? st : 0u;
+                pc[u] += c < XB[u] ? st : 0u;
+            }
         }
     }
     // (LDS addresses: the low words of the generic pointers)
     auto lo = [](const uint32_t *q) { return (uint32_t)reinterpret_cast<uintptr_t>(q); };
-    const uint32_t pd = (lo(pa) - lo(chi)) >> 2, RA = (lo(pb) - lo(cm)) >> 2, RB = (lo(pc) - lo(cm)) >> 2;
-    // d = #{C <= ~H}: #{C_hi < ~H_hi} plus the entries whose high word equals ~H_hi and low word is <= ~H_lo
-    // (about n / 2^32 of the queries: the low words come from the table row)
-    d = pd;
-    if (chi[d] == nh) {
-        const uint32_t nl = (uint32_t)nH;
-        while (d < n && chi[d] == nh && row[ci.start + d].x <= nl) ++d;
+    uint32_t d[NS], RA[NS], RB[NS], pmd[NS];
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+        RA[u] = (lo(pb[u]) - lo(cm)) >> 2;
+        RB[u] = (lo(pc[u]) - lo(cm)) >> 2;
+        // d = #{C <= ~H}: #{C_hi < ~H_hi} plus the entries whose high word equals ~H_hi and low word is <= ~H_lo
+        // (about n / 2^32 of the queries: the low words come from the table row)
+        d[u] = (lo(pa[u]) - lo(chi)) >> 2;
+        if (chi[d[u]] == nh[u]) {
+            const uint32_t nl = (uint32_t)nH[u];
+            while (d[u] < n && chi[d[u]] == nh[u] && row[ci.start + d[u]].x <= nl) ++d[u];
+        }
+        pmd[u] = pm[d[u]];  // the parts' largest ranks (used when a part has nothing below its bound)
     }
-    const uint32_t pmd = pm[d];  // the parts' largest ranks (used when a part has nothing below its bound)
-    // descents along R_A's and R_B's paths with the prefix [0, d) down to R's 32-rank block, branch-free with both
-    // reads of a level in flight: counts of ranks >= R, and the deepest level where a part's elements below R branch
+    // descents along R_A's and R_B's paths with the prefix [0, d) down to R's 32-rank block, branch-free with every
+    // read of a level in flight: counts of ranks >= R, and the deepest level where a part's elements below R branch
     // off (the predecessor's subtree: node start s, prefix offset q)
     const uint2 *__restrict__ lv = reinterpret_cast<const uint2 *>(img + ci.o_lv);
     const uint32_t *__restrict__ mk = reinterpret_cast<const uint32_t *>(img + ci.o_mk);
@@ -447,48 +477,56 @@ __device__ __forceinline__ void wt_seed_class(const WtVConst &vc, const WtClass 
 #else
     const uint32_t K = ci.K, nw = ci.nw, lb = wt_levels(K);
 #endif
-    uint32_t oA = d, oB = d, cA = 0, cB = 0;
-    uint32_t lA = WT_NONE, sA = 0, qA = 0, lB = WT_NONE, sB = 0, qB = 0;
+    uint32_t oA[NS], oB[NS], cA[NS], cB[NS], lA[NS], sA[NS], qA[NS], lB[NS], sB[NS], qB[NS];
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+        oA[u] = oB[u] = d[u];
+        cA[u] = cB[u] = 0;
+        lA[u] = lB[u] = WT_NONE;
+        sA[u] = qA[u] = sB[u] = qB[u] = 0;
+    }
     const uint32_t nv = wt_v(n), one = wt_v(1u), five = wt_v(5u);
     if (lb) {
         // level 0 (the root: both chains at offset d, one read); then the level constants live in VGPRs, halved per
         // level (no SGPR operands, no per-level scalar shifts)
         const uint32_t hs = 1u << (K - 1);
-        {
-            const uint2 w = lv[d >> 5];
-            const uint32_t o = w.y + __popc(__builtin_amdgcn_ubfe(w.x, 0u, d)), z = d - o;
-            const bool b1 = RA >= hs, b2 = RB >= hs;
+#pragma unroll
+        for (int u = 0; u < NS; ++u) {
+            const uint2 w = lv[d[u] >> 5];
+            const uint32_t o = w.y + __popc(__builtin_amdgcn_ubfe(w.x, 0u, d[u])), z = d[u] - o;
+            const bool b1 = RA[u] >= hs, b2 = RB[u] >= hs;
             const bool u1 = b1 && z != 0, u2 = b2 && hs > z;  // the root's left child is whole (n >= hs)
-            lA = u1 ? 1u : lA;
-            qA = u1 ? z : qA;
-            lB = u2 ? 1u : lB;
-            qB = u2 ? z : qB;
-            cA = b1 ? 0u : o;
-            cB = b2 ? 0u : o;
-            oA = b1 ? o : z;
-            oB = b2 ? o : z;
+            lA[u] = u1 ? 1u : lA[u];
+            qA[u] = u1 ? z : qA[u];
+            lB[u] = u2 ? 1u : lB[u];
+            qB[u] = u2 ? z : qB[u];
+            cA[u] = b1 ? 0u : o;
+            cB[u] = b2 ? 0u : o;
+            oA[u] = b1 ? o : z;
+            oB[u] = b2 ? o : z;
         }
         uint32_t h = wt_v(hs >> 1), msk = wt_v(~(hs - 1)), l1 = wt_v(2u);
         const uint2 *__restrict__ lvl = lv + nw;
         for (uint32_t l = 1; l < lb; ++l) {
-            const uint32_t s1 = RA & msk, p1 = s1 + oA, s2 = RB & msk, p2 = s2 + oB;
-            const uint2 w1 = lvl[p1 >> five], w2 = lvl[p2 >> five];
-            const uint32_t o1 = w1.y + __popc(__builtin_amdgcn_ubfe(w1.x, 0u, p1)) - (s1 >> one);
-            const uint32_t o2 = w2.y + __popc(__builtin_amdgcn_ubfe(w2.x, 0u, p2)) - (s2 >> one);
-            const uint32_t z1 = oA - o1, z2 = oB - o2;
-            const bool b1 = RA & h, b2 = RB & h;
-            const bool u1 = b1 && z1 != 0;
-            const bool u2 = b2 && min(nv - s2, h) > z2;  // zeros of the node past the prefix: suffix elements below R_B
-            lA = u1 ? l1 : lA;
-            sA = u1 ? s1 : sA;
-            qA = u1 ? z1 : qA;
-            lB = u2 ? l1 : lB;
-            sB = u2 ? s2 : sB;
-            qB = u2 ? z2 : qB;
-            cA += b1 ? 0u : o1;
-            cB += b2 ? 0u : o2;
-            oA = b1 ? o1 : z1;
-            oB = b2 ? o2 : z2;
+#pragma unroll
+            for (int u = 0; u < NS; ++u) {
+                const uint32_t s1 = RA[u] & msk, p1 = s1 + oA[u], s2 = RB[u] & msk, p2 = s2 + oB[u];
+                const uint2 w1 = lvl[p1 >> five], w2 = lvl[p2 >> five];
+                const uint32_t o1 = w1.y + __popc(__builtin_amdgcn_ubfe(w1.x, 0u, p1)) - (s1 >> one);
+                const uint32_t o2 = w2.y + __popc(__builtin_amdgcn_ubfe(w2.x, 0u, p2)) - (s2 >> one);
+                const uint32_t z1 = oA[u] - o1, z2 = oB[u] - o2;
+                const bool b1 = RA[u] & h, b2 = RB[u] & h;
+                const bool u1 = b1 && z1 != 0;
+                const bool u2 = b2 && min(nv - s2, h) > z2;  // zeros of the node past the prefix: suffix elements < R_B
+                lA[u] = u1 ? l1 : lA[u];  // (the node start there is R & msk of that level: rebuilt from lA below)
+                qA[u] = u1 ? z1 : qA[u];
+                lB[u] = u2 ? l1 : lB[u];
+                qB[u] = u2 ? z2 : qB[u];
+                cA[u] += b1 ? 0u : o1;
+                cB[u] += b2 ? 0u : o2;
+                oA[u] = b1 ? o1 : z1;
+                oB[u] = b2 ? o2 : z2;
+            }
             h >>= 1;
             msk = (uint32_t)((int32_t)msk >> 1);
             l1 += 1;
@@ -497,22 +535,34 @@ __device__ __forceinline__ void wt_seed_class(const WtVConst &vc, const WtClass 
     }
     // R's 32-rank block: its node's first o entries are the prefix part's elements in it (mk: their ranks' bits), so
     // the ranks >= R among them finish the counts, and those below R hold the part's predecessor when any are there
-    const uint32_t bA = RA & ~31u, bB = RB & ~31u, rA = RA & 31u, rB = RB & 31u;
-    const uint32_t mA = mk[bA + (bA >> 5) + oA], mB = mk[bB + (bB >> 5) + oB];
-    cA += __popc(mA >> rA);
-    cB += __popc(mB >> rB);
-    W += cA + (n - RB) - cB;
-    const uint32_t belA = __builtin_amdgcn_ubfe(mA, 0u, rA), belB = __builtin_amdgcn_ubfe(~mB, 0u, rB);
-    // predecessors: in R's block when a part has an element below R there; else from the deepest branch-off level
-    // down to a block (second descent: the prefix part takes the largest rank among the first qA entries of node
-    // sA, the suffix part the largest among entries qB.. of node sB); a part with nothing below its bound wraps, and
-    // its maximum is its largest rank overall (pm). Levels no lane of the wave needs are skipped.
-    const bool hasA = d > 0, hasB = d < n, hitA = belA != 0, hitB = belB != 0;
-    const bool wrapA = !hitA && lA == WT_NONE, wrapB = !hitB && lB == WT_NONE;
-    const bool dA = hasA && !hitA && !wrapA, dB = hasB && !hitB && !wrapB;
-    if (!dA) lA = lb;
-    if (!dB) lB = lb;
-    const uint32_t l0 = min(lA, lB);
+    uint32_t belA[NS], belB[NS];
+    bool hitA[NS], hitB[NS], wrapA[NS], wrapB[NS];
+    uint32_t l0 = WT_NONE;
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+        const uint32_t bA = RA[u] & ~31u, bB = RB[u] & ~31u, rA = RA[u] & 31u, rB = RB[u] & 31u;
+        const uint32_t mA = mk[bA + (bA >> 5) + oA[u]], mB = mk[bB + (bB >> 5) + oB[u]];
+        cA[u] += __popc(mA >> rA);
+        cB[u] += __popc(mB >> rB);
+        W[u] += cA[u] + (n - RB[u]) - cB[u];
+        belA[u] = __builtin_amdgcn_ubfe(mA, 0u, rA);
+        belB[u] = __builtin_amdgcn_ubfe(~mB, 0u, rB);
+        // predecessors: in R's block when a part has an element below R there; else from the deepest branch-off
+        // level down to a block (second descent: the prefix part takes the largest rank among the first qA entries of
+        // node sA, the suffix part the largest among entries qB.. of node sB); a part with nothing below its bound
+        // wraps, and its maximum is its largest rank overall (pm). Levels no lane of the wave needs are skipped.
+        hitA[u] = belA[u] != 0;
+        hitB[u] = belB[u] != 0;
+        wrapA[u] = !hitA[u] && lA[u] == WT_NONE;
+        wrapB[u] = !hitB[u] && lB[u] == WT_NONE;
+        const bool dA = d[u] > 0 && !hitA[u] && !wrapA[u], dB = d[u] < n && !hitB[u] && !wrapB[u];
+        if (!dA) lA[u] = lb;
+        if (!dB) lB[u] = lb;
+        // the branch-off node: the left child recorded at level lA - 1 starts at R & ~(2^(K - lA + 1) - 1)
+        sA[u] = RA[u] & ~((2u << (K - lA[u])) - 1u);
+        sB[u] = RB[u] & ~((2u << (K - lB[u])) - 1u);
+        l0 = min(l0, min(lA[u], lB[u]));
+    }
 #ifdef WT_ABL_PRED
     if (0)
 #endif
@@ -522,36 +572,43 @@ __device__ __forceinline__ void wt_seed_class(const WtVConst &vc, const WtClass 
             const uint32_t hs = 1u << (K - l - 1);
             const uint32_t h = wt_v(hs), h2 = wt_v(2 * hs), lv1 = wt_v(l);
             const uint2 *__restrict__ lvl = lv + l * nw;
-            const uint32_t p1 = sA + qA, p2 = sB + qB;
-            const uint2 w1 = lvl[p1 >> five], w2 = lvl[p2 >> five];
-            const uint32_t o1 = w1.y + __popc(__builtin_amdgcn_ubfe(w1.x, 0u, p1)) - (sA >> one);
-            const uint32_t o2 = w2.y + __popc(__builtin_amdgcn_ubfe(w2.x, 0u, p2)) - (sB >> one);
-            const bool a1 = lv1 >= lA, a2 = lv1 >= lB;
-            const bool g1 = a1 && o1 != 0;
-            const bool g2 = a2 && min(nv - sB, h2) > h + o2;  // ones of the node past the prefix
-            sA += g1 ? h : 0u;
-            qA = g1 ? o1 : qA;
-            sB += g2 ? h : 0u;
-            qB = a2 ? (g2 ? o2 : qB - o2) : qB;
+#pragma unroll
+            for (int u = 0; u < NS; ++u) {
+                const uint32_t p1 = sA[u] + qA[u], p2 = sB[u] + qB[u];
+                const uint2 w1 = lvl[p1 >> five], w2 = lvl[p2 >> five];
+                const uint32_t o1 = w1.y + __popc(__builtin_amdgcn_ubfe(w1.x, 0u, p1)) - (sA[u] >> one);
+                const uint32_t o2 = w2.y + __popc(__builtin_amdgcn_ubfe(w2.x, 0u, p2)) - (sB[u] >> one);
+                const bool a1 = lv1 >= lA[u], a2 = lv1 >= lB[u];
+                const bool g1 = a1 && o1 != 0;
+                const bool g2 = a2 && min(nv - sB[u], h2) > h + o2;  // ones of the node past the prefix
+                sA[u] += g1 ? h : 0u;
+                qA[u] = g1 ? o1 : qA[u];
+                sB[u] += g2 ? h : 0u;
+                qB[u] = a2 ? (g2 ? o2 : qB[u] - o2) : qB[u];
+            }
         }
     }
     // the descended lanes end in a block: the prefix part's elements are its first qA entries, the suffix part's the
     // entries from qB on (of the block's min(n - sB, 32))
-    const uint32_t vA = mk[sA + (sA >> 5) + qA];
-    const uint32_t vB = ~mk[sB + (sB >> 5) + qB] & (0xffffffffu >> (32u - min(nv - sB, 32u)));
-    const uint32_t pA = hitA ? bA + 31u - __clz(belA) : wrapA ? (pmd & 0xffffu) : sA + 31u - __clz(vA);
-    const uint32_t pB = hitB ? bB + 31u - __clz(belB) : wrapB ? (pmd >> 16) : sB + 31u - __clz(vB);
-    if (hasA) {
-        const uint32_t t = Hm + cm[pA] - (wrapA ? m : 0u);
-        const uint64_t k = ((uint64_t)t << 32) | (0xffffffffu - ev[pA]);
-        key = k > key ? k : key;
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+        const uint32_t vA = mk[sA[u] + (sA[u] >> 5) + qA[u]];
+        const uint32_t vB = ~mk[sB[u] + (sB[u] >> 5) + qB[u]] & (0xffffffffu >> (32u - min(nv - sB[u], 32u)));
+        const uint32_t bA = RA[u] & ~31u, bB = RB[u] & ~31u;
+        const uint32_t pA = hitA[u] ? bA + 31u - __clz(belA[u]) : wrapA[u] ? (pmd[u] & 0xffffu) : sA[u] + 31u - __clz(vA);
+        const uint32_t pB = hitB[u] ? bB + 31u - __clz(belB[u]) : wrapB[u] ? (pmd[u] >> 16) : sB[u] + 31u - __clz(vB);
+        if (d[u] > 0) {
+            const uint32_t t = Hm[u] + cm[pA] - (wrapA[u] ? m : 0u);
+            const uint64_t k = ((uint64_t)t << 32) | (0xffffffffu - ev[pA]);
+            key[u] = k > key[u] ? k : key[u];
+        }
+        if (d[u] < n) {
+            const uint32_t t = Hm2[u] + cm[pB] - (wrapB[u] ? m : 0u);
+            const uint64_t k = ((uint64_t)t << 32) | (0xffffffffu - ev[pB]);
+            key[u] = k > key[u] ? k : key[u];
+        }
+        sum[u] += (uint64_t)d[u] * Hm[u] + (uint64_t)(n - d[u]) * Hm2[u];
     }
-    if (hasB) {
-        const uint32_t t = Hm2 + cm[pB] - (wrapB ? m : 0u);
-        const uint64_t k = ((uint64_t)t << 32) | (0xffffffffu - ev[pB]);
-        key = k > key ? k : key;
-    }
-    sum += (uint64_t)d * Hm + (uint64_t)(n - d) * Hm2;
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -573,9 +630,9 @@ struct WtTopkState {
     unsigned long long cand_idx[WT_CAND];
 };
 
-// G workgroups per row L: each stages the row image into LDS and takes a contiguous share of the row's 64-seed
-// chunks, which its waves take one at a time from an LDS counter.
-template <bool BIG>
+// G workgroups per row L: each stages the row image into LDS and takes a contiguous share of the row's chunks of
+// 64 NS seeds (NS per lane), which its waves take one at a time from an LDS counter.
+template <bool BIG, int NS>
 __global__ __launch_bounds__(1024) void k_replayable_sweep_wt(
     const uint32_t *__restrict__ bucket_off, const uint64_t *__restrict__ sorted_h0,
     const uint32_t *__restrict__ sorted_idx, const uint4 *__restrict__ table, uint32_t E,
@@ -583,10 +640,11 @@ __global__ __launch_bounds__(1024) void k_replayable_sweep_wt(
     const WtClass *__restrict__ classes, uint32_t n_classes, uint32_t m, uint64_t mu, uint32_t m_k64, uint32_t msh,
     uint32_t G, nmz_sched_stats *__restrict__ stats, unsigned long long *__restrict__ span,
     uint64_t *__restrict__ sums, WtTopkState *__restrict__ tk, uint32_t k) {
+    constexpr uint32_t CS = 64 * NS;  // seeds per chunk
     extern __shared__ uint4 wt_lds[];
     const uint32_t L = blockIdx.x / G, g = blockIdx.x % G;
     const uint32_t s0 = bucket_off[L], s1 = bucket_off[L + 1];
-    const uint32_t nch = (s1 - s0 + 63) / 64;
+    const uint32_t nch = (s1 - s0 + CS - 1) / CS;
     const uint32_t c0 = g * nch / G, c1 = (g + 1) * nch / G;
     uint32_t *ctr = reinterpret_cast<uint32_t *>(wt_lds + rb16);
     if (c0 == c1) {  // no seeds (an empty group: the smallest key)
@@ -623,49 +681,64 @@ __global__ __launch_bounds__(1024) void k_replayable_sweep_wt(
     uint32_t ch = 0;
     if (lane == 0) ch = atomicAdd(ctr, 1u);
     ch = __builtin_amdgcn_readfirstlane(ch);
-    uint64_t h0n = 0;
-    uint32_t idxn = 0;
-    if (ch < c1) {
-        const uint32_t jn = min(s0 + ch * 64 + lane, s1 - 1);
-        h0n = sorted_h0[jn];
-        idxn = sorted_idx[jn];
+    uint64_t h0n[NS];
+    uint32_t idxn[NS];
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+        const uint32_t jn = min(s0 + ch * CS + u * 64 + lane, s1 - 1);  // past the share: a valid seed, unused
+        h0n[u] = sorted_h0[jn];
+        idxn[u] = sorted_idx[jn];
     }
     while (ch < c1) {
-        const uint32_t j = s0 + ch * 64 + lane;
-        const uint64_t h0 = h0n;
-        const uint32_t idx = idxn;
+        const uint32_t j0 = s0 + ch * CS + lane;
+        uint64_t h0[NS];
+        uint32_t idx[NS];
+#pragma unroll
+        for (int u = 0; u < NS; ++u) {
+            h0[u] = h0n[u];
+            idx[u] = idxn[u];
+        }
         uint32_t chn = 0;
         if (lane == 0) chn = atomicAdd(ctr, 1u);
         chn = __builtin_amdgcn_readfirstlane(chn);
-        {
-            const uint32_t jn = min(s0 + chn * 64 + lane, s1 - 1);  // past the share: a valid seed, unused
-            h0n = sorted_h0[jn];
-            idxn = sorted_idx[jn];
+#pragma unroll
+        for (int u = 0; u < NS; ++u) {
+            const uint32_t jn = min(s0 + chn * CS + u * 64 + lane, s1 - 1);
+            h0n[u] = sorted_h0[jn];
+            idxn[u] = sorted_idx[jn];
         }
-        uint64_t sum = 0, key = 0;
-        uint32_t W = 0;
+        uint64_t sum[NS], key[NS];
+        uint32_t W[NS];
+#pragma unroll
+        for (int u = 0; u < NS; ++u) sum[u] = key[u] = W[u] = 0;
         for (uint32_t c = 0; c < n_classes; ++c)
-            wt_seed_class<BIG>(vc, classes[c], img, row, h0, m, mu, m_k64, msh, sum, W, key);
-        const uint64_t total = sum + rsum - (uint64_t)W * m;
-        if (tk) {  // the chunk's largest sum, in the top-k's order (int64, as an order-preserving u64 key)
-            uint64_t km = j < s1 ? total ^ (1ull << 63) : 0ull;
+            wt_seed_class<BIG, NS>(vc, classes[c], img, row, h0, m, mu, m_k64, msh, sum, W, key);
+        uint64_t km = 0;  // the chunk's largest sum, in the top-k's order (int64, as an order-preserving u64 key)
+#pragma unroll
+        for (int u = 0; u < NS; ++u) {
+            const uint32_t j = j0 + u * 64;
+            const uint64_t total = sum[u] + rsum - (uint64_t)W[u] * m;
+            if (j < s1) {
+                const uint64_t kk = total ^ (1ull << 63);
+                km = kk > km ? kk : km;
+                if (sums) sums[j] = total;  // in sorted order: the wave's 64 writes coalesce (by seed index they
+                                            // scatter, one 64-B line per seed: +20 us on the step)
+                nmz_sched_stats st;
+                st.sum_delay_ns = total;
+                st.max_delay_ns = (int64_t)(key[u] >> 32);
+                st.argmax_event = ~(uint32_t)key[u];
+                st.n_fault = 0;
+                st.first_fault = NMZ_NONE;
+                st.flags = 0;
+                stats[idx[u]] = st;
+            }
+        }
+        if (tk) {
             for (int o = 32; o; o >>= 1) {
                 const uint64_t v = __shfl_xor(km, o, 64);
                 km = v > km ? v : km;
             }
             if (lane == 0) atomicMax(reinterpret_cast<unsigned long long *>(ctr + 2), (unsigned long long)km);
-        }
-        if (j < s1) {
-            if (sums) sums[j] = total;  // in sorted order: the wave's 64 writes coalesce (by seed index they scatter,
-                                        // one 64-B line per seed: +20 us on the step)
-            nmz_sched_stats st;
-            st.sum_delay_ns = total;
-            st.max_delay_ns = (int64_t)(key >> 32);
-            st.argmax_event = ~(uint32_t)key;
-            st.n_fault = 0;
-            st.first_fault = NMZ_NONE;
-            st.flags = 0;
-            stats[idx] = st;
         }
         ch = chn;
     }
@@ -968,8 +1041,8 @@ int wt_build(WtState &w, nmz_ctx *ctx, const uint4 *d_table, uint32_t E, const C
     w.msh = mod.m32 > 255 ? bitlen(mod.m32) - 8 : 0;
     // function attributes are per device: once per context (a context owns one device; its calls are serialised)
     if (!ctx->wt_lds_attr) {
-        for (const void *f : {reinterpret_cast<const void *>(k_replayable_sweep_wt<false>),
-                              reinterpret_cast<const void *>(k_replayable_sweep_wt<true>),
+        for (const void *f : {reinterpret_cast<const void *>(k_replayable_sweep_wt<false, 1>),
+                              reinterpret_cast<const void *>(k_replayable_sweep_wt<true, 1>),
                               reinterpret_cast<const void *>(k_replayable_wt_build)})
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WT_LDS_MAX) != hipSuccess) {
                 (void)hipGetLastError();  // not sticky for the launches that follow: keep the order-query sweep
@@ -1033,7 +1106,10 @@ int wt_sweep(const WtState &w, nmz_ctx *ctx, hipStream_t st, const Buckets &b, c
     const uint32_t G = wt_groups(), nt = wt_threads();
     KernelTimer kt(ctx, st, "replayable_sweep");
     unsigned long long *span = kt.span();
-    auto kern = mod.m32 >= 0x80000000u ? k_replayable_sweep_wt<true> : k_replayable_sweep_wt<false>;
+    const bool big = mod.m32 >= 0x80000000u;
+    // one seed per lane: two (NS = 2, 106 VGPRs) measured slower, K1 span 0.074 vs 0.059 ms
+    // (profiles/r04/k1_ns2_rejected/)
+    auto kern = big ? k_replayable_sweep_wt<true, 1> : k_replayable_sweep_wt<false, 1>;
     const size_t lds = w.rb16 * 16u + 16u;
     hipLaunchKernelGGL(kern, dim3(256 * G), dim3(nt), lds, st, b.offset, b.sorted_h0, b.sorted_idx,
                        d_table, E, w.d_blob, w.rb16, w.d_rowsum, static_cast<const WtClass *>(w.d_classes),

@@ -272,6 +272,26 @@ def test_replayable_bucket_boundaries(ctx):
         assert np.array_equal(r.stats, st), n
 
 
+def test_replayable_seed_prefix_staging(ctx):
+    """k_seed_prefix stages a block's 2,048 seed offsets and bytes in LDS when the bytes fit 32 KB (whole dwords
+    between partial head and tail dwords at any alignment) and hashes from global memory otherwise: short seeds
+    (staged), long seeds (not staged), blocks of each kind side by side, empty and multi-byte UTF-8 seeds."""
+    rng = np.random.default_rng(17)
+    alphabet = list("0123456789abcdefXYZ-_") + ["\u00e9", "\u4e2d", "\U0001f600"]
+
+    def rand_seeds(n, lmax):
+        return ["".join(rng.choice(alphabet, size=int(rng.integers(0, lmax + 1)))) for _ in range(n)]
+
+    hints = zk_hints(70)
+    for seeds in (rand_seeds(6000, 12), rand_seeds(3000, 60), rand_seeds(2048, 6) + rand_seeds(2048, 40) +
+                  rand_seeds(777, 3)):
+        p = Replayable()
+        p.MaxInterval = 100_000_000
+        r = p.Sweep(seeds, hints, ctx=ctx)
+        st, _ = rep_oracle(seeds, hints, 100_000_000)
+        assert np.array_equal(r.stats, st)
+
+
 def test_replayable_device_plan_api(ctx):
     """nmz_replayable_plan_create + nmz_replayable_sweep_dev on resident buffers."""
     import torch

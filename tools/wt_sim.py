@@ -121,6 +121,13 @@ def query(img, d, RA, RB, Hm, Hm2, m):
     dB = hasB and not hitB and not wrapB
     lA = lA if dA else lb
     lB = lB if dB else lb
+    # the kernel does not track the node start: it rebuilds it from the level (R & ~(2^(K - l + 1) - 1))
+    if dA:
+        assert sA == RA & ~((2 << (K - lA)) - 1)
+        sA = RA & ~((2 << (K - lA)) - 1)
+    if dB:
+        assert sB == RB & ~((2 << (K - lB)) - 1)
+        sB = RB & ~((2 << (K - lB)) - 1)
     for l in range(min(lA, lB), lb):
         h = 1 << (K - l - 1)
         lvl = lv[l]
