@@ -106,9 +106,12 @@ struct EdArgs {
 };
 
 template <int W>
-__global__ __launch_bounds__(256) void k_ed_tile(EdArgs A) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_ed_tile(EdArgs A) {
+    // at least two waves per SIMD: at W = 32 the compiler's own allocation was 256 VGPRs + 26 AGPRs (one wave); bound
+    // to 256 it spills ~23 VGPRs (the row-block size R = 2, 4, 8 changes nothing)
+    constexpr int R = ED_R;
     constexpr int NB = 2 * W + 1;       // band cells
-    constexpr int NW = 2 * W + ED_R;    // window symbols
+    constexpr int NW = 2 * W + R;       // window symbols
     // XCD-aware: hardware block b runs on XCD b%8; give each XCD a contiguous
     // range of logical blocks so waves sharing a candidate group share an L2.
     const uint32_t nblk = gridDim.x, per_xcd = nblk / 8;
@@ -169,13 +172,13 @@ __global__ __launch_bounds__(256) void k_ed_tile(EdArgs A) {
             // next extraction row for the halves that are still alive
             const uint32_t stop = min(nrows, min(n1 > i0 ? n1 : nrows, n2 > i0 ? n2 : nrows));
             const uint32_t stop_u = __builtin_amdgcn_readfirstlane(stop);
-            if (i0 + ED_R <= stop_u) {
+            if (i0 + R <= stop_u) {
                 // prefetch the symbols entering the window after this block
-                uint32_t nxt[ED_R];
+                uint32_t nxt[R];
 #pragma unroll
-                for (int r = 0; r < ED_R; ++r) nxt[r] = load_sym((int64_t)i0 - W + NW + r);
+                for (int r = 0; r < R; ++r) nxt[r] = load_sym((int64_t)i0 - W + NW + r);
 #pragma unroll
-                for (int r = 0; r < ED_R; ++r) {
+                for (int r = 0; r < R; ++r) {
                     const uint32_t i = i0 + r;  // computing row i+1, symbols a[i]
                     const uint32_t s1 = i < n1 ? a1[i] : QUERY_PAD, s2 = i < n2 ? a2[i] : QUERY_PAD;
                     const uint32_t ap = __builtin_amdgcn_readfirstlane(s1 | (s2 << 16));
@@ -191,10 +194,10 @@ __global__ __launch_bounds__(256) void k_ed_tile(EdArgs A) {
                     }
                 }
 #pragma unroll
-                for (int t = 0; t < NW - ED_R; ++t) win[t] = win[t + ED_R];
+                for (int t = 0; t < NW - R; ++t) win[t] = win[t + R];
 #pragma unroll
-                for (int r = 0; r < ED_R; ++r) win[NW - ED_R + r] = nxt[r];
-                i0 += ED_R;
+                for (int r = 0; r < R; ++r) win[NW - R + r] = nxt[r];
+                i0 += R;
             } else {
                 // single row (lands exactly on an extraction row)
                 const uint32_t i = i0;

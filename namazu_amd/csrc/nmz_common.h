@@ -50,6 +50,16 @@ struct DevBuf {
     T *as() const { return static_cast<T *>(ptr); }
 };
 
+// Grow-only pinned host staging owned by a context: a plan's inputs are packed here and reach the device in one
+// asynchronous copy (a pageable hipMemcpyAsync stages through a driver buffer and returns only when that is done).
+// A user waits for the copy to complete before packing the next inputs (plan builds end with a stream sync).
+struct HostPin {
+    void *ptr = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes);
+    void release();
+};
+
 }  // namespace nmz
 
 // Optional HIP-event timing of the dominant kernels (bench.py reads it).
@@ -72,6 +82,7 @@ struct nmz_ctx {
     // scratch slots reused across calls (host-pointer entry points)
     nmz::DevBuf buf[16];
     std::vector<nmz::DevBuf> pool;  // free plan buffers (DevBuf::pool), freed by nmz_close
+    nmz::HostPin pin[2];             // pinned staging of plan inputs ([0] replayable plan, [1] its wavelet classes)
     bool wt_lds_attr = false;        // the wavelet-tree kernels' LDS attribute is set on this context's device
     NmzTiming timing;
 };

@@ -20,6 +20,24 @@ int fail(int code, const std::string &msg) {
     return code;
 }
 
+int HostPin::ensure(size_t bytes) {
+    if (bytes <= cap) return NMZ_OK;
+    release();
+    const size_t want = std::max<size_t>(bytes * 3 / 2, 4096);
+    if (hipHostMalloc(&ptr, want, hipHostMallocDefault) != hipSuccess) {
+        ptr = nullptr;
+        return fail(NMZ_ENOMEM, "hipHostMalloc of " + std::to_string(want) + " bytes failed");
+    }
+    cap = want;
+    return NMZ_OK;
+}
+
+void HostPin::release() {
+    if (ptr) (void)hipHostFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+}
+
 int DevBuf::ensure(size_t bytes) {
     if (bytes <= cap) return NMZ_OK;
     // a pooled buffer that grows goes back to the pool, where the next plan of this context may take it and
@@ -302,6 +320,7 @@ int nmz_close(nmz_ctx *ctx) {
     {
         CtxGuard g(ctx);
         for (auto &b : ctx->buf) b.release();
+        for (auto &b : ctx->pin) b.release();
         for (auto &b : ctx->pool) (void)hipFree(b.ptr);
         ctx->pool.clear();
         for (auto &kv : ctx->timing.events)

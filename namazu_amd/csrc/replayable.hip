@@ -22,6 +22,7 @@
 //     registers; the argmax tie-break uses the key (t << 32 | ~e) so the
 //     sorted event order still yields the first original index.
 #include <algorithm>
+#include <cstring>
 #include <cstdlib>
 #include <numeric>
 #include <string>
@@ -68,6 +69,13 @@ struct nmz_replayable_plan {
     nmz::WtState wt;                    // wavelet-tree statistics (k_replayable_sweep_wt, the default when it fits)
     nmz::DevBuf wt_topk;                // their top-k candidates (sums, workgroup maxima, candidates)
     void *wt_topk_zeroed = nullptr;     // the wt_topk buffer whose counters were zeroed
+    // the streams the plan's sweeps were enqueued on, each with an event recorded after its latest sweep:
+    // destroy waits for exactly that work (and the context's stream), not for the whole device
+    struct Use {
+        hipStream_t st;
+        hipEvent_t ev;
+    };
+    std::vector<Use> uses;
 };
 
 namespace nmz {
@@ -1607,9 +1615,41 @@ static int replayable_stats(nmz_replayable_plan *p, hipStream_t st, const uint32
 // Optional top-k (k > 0): by (sum_delay desc, seed asc) over the seeds' stats (n_fault = 0), seed =
 // seed0 + seed index. (A merge kernel with the first selection level fused in measured 66 us against
 // 21 + 29 us for k_replayable_merge + k_topk_chunk at 2^20 seeds, so the levels stay separate.)
+static int replayable_run_on(nmz_replayable_plan *p, hipStream_t st, const uint32_t *d_soff, const uint8_t *d_sbytes,
+                             uint64_t S, nmz_sched_stats *d_stats, uint64_t seed0, uint32_t k, nmz_topk_entry *d_topk,
+                             uint64_t dec_lo);
+
 static int replayable_run(nmz_replayable_plan *p, hipStream_t st, const uint32_t *d_soff, const uint8_t *d_sbytes,
                           uint64_t S, nmz_sched_stats *d_stats, uint64_t seed0 = 0, uint32_t k = 0,
                           nmz_topk_entry *d_topk = nullptr, uint64_t dec_lo = 0) {
+    const int rc = replayable_run_on(p, st, d_soff, d_sbytes, S, d_stats, seed0, k, d_topk, dec_lo);
+    if (st != p->ctx->stream) {  // destroy synchronises the context's stream itself
+        nmz_replayable_plan::Use *u = nullptr;
+        for (auto &x : p->uses)
+            if (x.st == st) u = &x;
+        if (!u) {
+            hipEvent_t ev;
+            NMZ_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            p->uses.push_back({st, ev});
+            u = &p->uses.back();
+        }
+        NMZ_HIP(hipEventRecord(u->ev, st));
+    }
+    return rc;
+}
+
+static void plan_wait_uses(nmz_replayable_plan *p) {
+    for (auto &u : p->uses) {
+        (void)hipEventSynchronize(u.ev);
+        (void)hipEventDestroy(u.ev);
+    }
+    p->uses.clear();
+    (void)hipStreamSynchronize(p->ctx->stream);
+}
+
+static int replayable_run_on(nmz_replayable_plan *p, hipStream_t st, const uint32_t *d_soff, const uint8_t *d_sbytes,
+                             uint64_t S, nmz_sched_stats *d_stats, uint64_t seed0, uint32_t k, nmz_topk_entry *d_topk,
+                             uint64_t dec_lo) {
     NMZ_CHECK(k <= 256, "top-k supports k <= 256");
     NMZ_CHECK(k == 0 || d_topk, "d_topk is NULL");
     // the wavelet-tree sweep's own candidates (k <= 64; more than one general-selection list, so that the gated
@@ -1698,12 +1738,15 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
         delete p;
         return rc;
     }
+    // the small inputs first (one contiguous region, packed in the context's pinned staging at the same offsets:
+    // one asynchronous upload), then the table
     Carve cv(p->plan_mem.ptr);
     p->d_classes = cv.take<ClassInfo>(cls.size() + 1);
-    p->d_table = cv.take<uint4>((size_t)256 * E + 1);
     uint32_t *d_perm = cv.take<uint32_t>(E + 1);
     uint32_t *d_hoff = p->d_hoff = cv.take<uint32_t>(E + 1);
     uint8_t *d_hbytes = p->d_hbytes = cv.take<uint8_t>(nbytes + 1);
+    const size_t in_bytes = (size_t)(reinterpret_cast<char *>(cv.take<uint4>(0)) - reinterpret_cast<char *>(p->plan_mem.ptr));
+    p->d_table = cv.take<uint4>((size_t)256 * E + 1);
     auto cleanup = [&](int code) {
         (void)hipStreamSynchronize(st);  // pooled buffers: no work may still use them
         p->plan_mem.release();
@@ -1717,10 +1760,17 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
         return code;
     };
     if (E) {
-        if (hipMemcpyAsync(p->d_classes, cls.data(), cls.size() * sizeof(ClassInfo), hipMemcpyHostToDevice, st) ||
-            hipMemcpyAsync(d_perm, perm.data(), E * 4, hipMemcpyHostToDevice, st) ||
-            hipMemcpyAsync(d_hoff, hint_off, (E + 1) * 4, hipMemcpyHostToDevice, st) ||
-            (nbytes && hipMemcpyAsync(d_hbytes, hint_bytes, nbytes, hipMemcpyHostToDevice, st)))
+        HostPin &pin = ctx->pin[0];
+        if (pin.ensure(in_bytes) != NMZ_OK) return cleanup(NMZ_ENOMEM);
+        {
+            char *h = static_cast<char *>(pin.ptr);
+            auto at = [&](const void *d) { return h + (static_cast<const char *>(d) - static_cast<char *>(p->plan_mem.ptr)); };
+            std::memcpy(at(p->d_classes), cls.data(), cls.size() * sizeof(ClassInfo));
+            std::memcpy(at(d_perm), perm.data(), (size_t)E * 4);
+            std::memcpy(at(d_hoff), hint_off, (size_t)(E + 1) * 4);
+            if (nbytes) std::memcpy(at(d_hbytes), hint_bytes, nbytes);
+        }
+        if (hipMemcpyAsync(p->plan_mem.ptr, pin.ptr, in_bytes, hipMemcpyHostToDevice, st))
             return cleanup(fail(NMZ_EHIP, "plan upload failed"));
         // unsorted table into scratch (the context's, grow-only: no free, so no device sync), then the
         // per-(L, class) C sort into place
@@ -1799,8 +1849,8 @@ int nmz_replayable_plan_destroy(nmz_replayable_plan *plan) {
     {
         CtxGuard g(plan->ctx);
         // the buffers go back to the context's pool, where the next plan may write them at once: wait for the
-        // work still reading them (hipFree, which this replaces, synchronised the device as well)
-        (void)hipDeviceSynchronize();
+        // work still reading them -- the sweeps on every stream the plan was used on, and the context's stream
+        plan_wait_uses(plan);
         plan->plan_mem.release();
         plan->seed_scratch.release();
         plan->partial.release();
@@ -1863,14 +1913,14 @@ int nmz_replayable_sweep(nmz_ctx *ctx, const uint32_t *seed_off, const uint8_t *
     struct PlanGuard {
         nmz_replayable_plan *p;
         ~PlanGuard() {
-            (void)hipStreamSynchronize(p->ctx->stream);  // pooled buffers: no work may still use them
+            plan_wait_uses(p);  // pooled buffers: no work may still use them
             p->plan_mem.release();
             p->seed_scratch.release();
             p->partial.release();
             p->topk_lists.release();
             p->oq_mem.release();
-        p->wt.mem.release();
-        p->wt_topk.release();
+            p->wt.mem.release();
+            p->wt_topk.release();
             delete p;
         }
     } pg{plan};

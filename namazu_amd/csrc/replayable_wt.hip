@@ -20,6 +20,7 @@
 // predecessor reads -- ~50 LDS reads instead of ~150 for the sorted-block searches of k_replayable_sweep_oq,
 // and a row image of ~13 B per event instead of ~27, so two rows fit one CU's LDS.
 #include <algorithm>
+#include <cstring>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -33,7 +34,21 @@ constexpr uint32_t WT_BRUTE = 8;       // segments of at most this many events: 
 constexpr uint32_t WT_NMAX = 4096;     // largest segment the plan kernel sorts in LDS
 constexpr uint32_t WT_LDS_MAX = 160 * 1024 - 256;  // dynamic LDS; the sweep kernel's few static bytes need the rest
 constexpr uint32_t WT_NONE = 0xffffffffu;
-constexpr uint32_t WT_PAD = 32;        // sentinels past Cm and C_hi: lifting searches of <= 5 rounds need no clamp
+constexpr uint32_t WT_PAD = 32;
+#ifdef WT_BUILD_TRACE
+// timing-only builds: wall_clock64() at the plan kernel's phase boundaries, per workgroup (tools/wt_build_trace.py)
+constexpr uint32_t WT_TRACE_PHASES = 10, WT_TRACE_WGS = 8192;
+__device__ unsigned long long g_wt_build_trace[WT_TRACE_WGS * WT_TRACE_PHASES];
+#define WT_STAMP(k)                                                                                              \
+    do {                                                                                                         \
+        if (threadIdx.x == 0 && blockIdx.y * gridDim.x + blockIdx.x < WT_TRACE_WGS)                              \
+            g_wt_build_trace[(blockIdx.y * gridDim.x + blockIdx.x) * WT_TRACE_PHASES + (k)] = wall_clock64();    \
+    } while (0)
+#else
+#define WT_STAMP(k) \
+    do {            \
+    } while (0)
+#endif        // sentinels past Cm and C_hi: lifting searches of <= 5 rounds need no clamp
 
 struct WtClass {
     uint64_t pn;              // P^len
@@ -80,12 +95,22 @@ __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__re
     unsigned long long *part = reinterpret_cast<unsigned long long *>(idx + 520);  // [WT_BW]
     uint32_t *bmax = reinterpret_cast<uint32_t *>(part + WT_BW);               // [4]
     const uint32_t c = blockIdx.x, L = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    WT_STAMP(0);
     const WtClass ci = classes[c];
     const uint32_t n = ci.n;
     const uint4 *__restrict__ row = table + (uint64_t)L * E + ci.start;
     char *img = reinterpret_cast<char *>(blob + (uint64_t)L * rb16);
+    // the segment's entries, read once (every load in flight): the row sum, C's high words and the sort keys
+    constexpr uint32_t PPT = WT_NMAX / WT_BT;
+    uint4 q[PPT];
+#pragma unroll
+    for (uint32_t k = 0; k < PPT; ++k) {
+        const uint32_t i = tid + k * WT_BT;
+        q[k] = i < n ? row[i] : make_uint4(0, 0, 0, 0);
+    }
     uint64_t s = 0;
-    for (uint32_t i = tid; i < n; i += WT_BT) s += row[i].z;
+#pragma unroll
+    for (uint32_t k = 0; k < PPT; ++k) s += q[k].z;
     for (int o = 32; o; o >>= 1) s += __shfl_xor(s, o, 64);
     if (lane == 0) part[wave] = s;
     if (tid < 4) bmax[tid] = 0;
@@ -95,6 +120,7 @@ __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__re
         for (uint32_t w = 0; w < WT_BW; ++w) t += part[w];
         atomicAdd(rowsum + L, t);
     }
+    WT_STAMP(1);
     if (n <= WT_BRUTE) return;
     uint32_t np = 1, lgp = 0;
     while (np < n) {
@@ -102,12 +128,15 @@ __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__re
         ++lgp;
     }
     uint32_t *chi_img = reinterpret_cast<uint32_t *>(img + ci.o_chi);
-    for (uint32_t i = tid; i < n; i += WT_BT) {
-        const uint4 q = row[i];
-        chi_img[i] = q.y;
-        const uint32_t e = ~q.w;  // < 65536 (the host checks E)
-        key[i] = ((uint64_t)q.z << 32) | ((uint64_t)(0xffffu - e) << 16) | i;
+#pragma unroll
+    for (uint32_t k = 0; k < PPT; ++k) {
+        const uint32_t i = tid + k * WT_BT;
+        if (i >= n) break;
+        chi_img[i] = q[k].y;
+        const uint32_t e = ~q[k].w;  // < 65536 (the host checks E)
+        key[i] = ((uint64_t)q[k].z << 32) | ((uint64_t)(0xffffu - e) << 16) | i;
     }
+    WT_STAMP(2);
     // sort the keys: counting sort on the top lg(np) - 1 bits of Cm (uniform in [0, m): ~2 keys per bucket), then an
     // insertion sort per bucket (a thread per bucket); a bucket of more than 32 keys (repeated hints: equal Cm)
     // sends the whole segment to a bitonic sort
@@ -181,6 +210,13 @@ __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__re
             for (uint32_t i = tid; i < n; i += WT_BT) srt[i] = key[i];
         }
         __syncthreads();  // the keys' region becomes the rank arrays
+        WT_STAMP(3);
+    }
+    uint32_t *chiL = reinterpret_cast<uint32_t *>(key) + WT_NMAX;  // C_hi by position (the bucket index below)
+#pragma unroll
+    for (uint32_t k = 0; k < PPT; ++k) {
+        const uint32_t i = tid + k * WT_BT;
+        if (i < n) chiL[i] = q[k].y;
     }
     uint32_t *cm_img = reinterpret_cast<uint32_t *>(img + ci.o_cm);
     uint16_t *e_img = reinterpret_cast<uint16_t *>(img + ci.o_e);
@@ -194,6 +230,8 @@ __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__re
         cm_img[n + tid] = ~0u;  // sentinels: never below a search bound
         chi_img[n + tid] = ~0u;
     }
+    __syncthreads();  // chiL complete
+    WT_STAMP(4);
     // bucket indexes (first rank with Cm >= b << msh, b <= 256; first position with C_hi >= b << 24, b < 256): every
     // position writes the buckets between its predecessor's and its own (the sorted order's boundaries)
     uint32_t *im = idx, *ic = idx + 260;
@@ -201,8 +239,8 @@ __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__re
         const int bm = i < n ? (int)((uint32_t)(srt[i] >> 32) >> msh) : 257;
         const int pm_ = i ? (int)((uint32_t)(srt[i - 1] >> 32) >> msh) : -1;
         for (int b = pm_ + 1; b <= min(bm, 256); ++b) im[b] = i;
-        const int bc2 = i < n ? (int)(row[i].y >> 24) : 256;
-        const int pc = i ? (int)(row[i - 1].y >> 24) : -1;
+        const int bc2 = i < n ? (int)(chiL[i] >> 24) : 256;
+        const int pc = i ? (int)(chiL[i - 1] >> 24) : -1;
         for (int b = pc + 1; b <= min(bc2, 255); ++b) ic[b] = i;
     }
     __syncthreads();
@@ -216,6 +254,7 @@ __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__re
     }
     __syncthreads();
     if (tid == 0) atomicMax(&classes[c].rS, 32u - __clz(max(bmax[2], bmax[3])));
+    WT_STAMP(5);
     // prefix / suffix maxima of the ranks: pm[d] = {max rank at positions < d, max rank at positions >= d};
     // PP positions per thread, wave scans (up for the prefix, down for the suffix), then the wave totals
     {
@@ -262,50 +301,60 @@ __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__re
         }
         __syncthreads();  // wb is the level loop's next
     }
-    // wavelet levels above the 32-rank blocks
+    WT_STAMP(6);
+    // wavelet levels above the 32-rank blocks. Per level, wave w ballots a contiguous range of 64-position groups
+    // (bit K-1-l of the rank at each position, in this level's order), the 8 wave totals give each wave its ones
+    // before its range, and every position's destination in the next level's order follows from the ones before it
+    // in its node: one barrier for the totals, one for the next order (no serial scan of the words).
     const uint32_t K = ci.K, nw = ci.nw, lb = wt_levels(K);
     uint2 *lv = reinterpret_cast<uint2 *>(img + ci.o_lv);
     uint16_t *cur = S0, *nxt = S0 + WT_NMAX;
+    constexpr uint32_t MAXG = (WT_NMAX / 64 + 1 + WT_BW - 1) / WT_BW;  // groups per wave, at most
+    const uint32_t ng = (nw * 32 + 63) / 64, gpw = (ng + WT_BW - 1) / WT_BW, g0 = wave * gpw;
+    uint32_t *wtot = cum;  // [WT_BW]
     for (uint32_t l = 0; l < lb; ++l) {
-        const uint32_t k = K - l, h = 1u << (k - 1);
-        for (uint32_t j0 = wave * 64; j0 < nw * 32; j0 += WT_BT) {
-            const uint32_t j = j0 + lane;
-            const bool bit = j < n && (cur[j] & h);
-            const uint64_t bal = __ballot(bit);
-            if (lane == 0) {
-                wb[j0 >> 5] = (uint32_t)bal;
-                if ((j0 >> 5) + 1 < nw) wb[(j0 >> 5) + 1] = (uint32_t)(bal >> 32);
+        const uint32_t h = 1u << (K - l - 1);
+        uint64_t bal[MAXG];
+        uint32_t vv[MAXG], tot = 0;
+#pragma unroll
+        for (uint32_t gi = 0; gi < MAXG; ++gi) {
+            const uint32_t g = g0 + gi, j = g * 64 + lane;
+            bal[gi] = 0;
+            vv[gi] = 0;
+            if (gi < gpw && g < ng) {
+                vv[gi] = j < n ? cur[j] : 0u;
+                bal[gi] = __ballot(j < n && (vv[gi] & h));
+                tot += (uint32_t)__popcll(bal[gi]);
             }
         }
+        if (lane == 0) wtot[wave] = tot;
         __syncthreads();
-        if (wave == 0) {  // exclusive scan of the words' popcounts (nw <= 129 words, 3 per lane)
-            const uint32_t w0 = 3 * lane;
-            const uint32_t c0 = w0 < nw ? __popc(wb[w0]) : 0u, c1 = w0 + 1 < nw ? __popc(wb[w0 + 1]) : 0u,
-                           c2 = w0 + 2 < nw ? __popc(wb[w0 + 2]) : 0u;
-            const uint32_t t = c0 + c1 + c2;
-            uint32_t inc = t;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t v = __shfl_up(inc, o, 64);
-                if (lane >= (uint32_t)o) inc += v;
+        uint32_t pre = 0;
+        for (uint32_t w = 0; w < wave; ++w) pre += wtot[w];
+        const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+        for (uint32_t gi = 0; gi < MAXG; ++gi) {
+            const uint32_t g = g0 + gi, j = g * 64 + lane;
+            if (gi < gpw && g < ng) {
+                const uint64_t bg = bal[gi];
+                if (lane == 0) lv[l * nw + 2 * g] = make_uint2((uint32_t)bg, pre);
+                if (lane == 1 && 2 * g + 1 < nw)
+                    lv[l * nw + 2 * g + 1] = make_uint2((uint32_t)(bg >> 32), pre + (uint32_t)__popc((uint32_t)bg));
+                if (j < n) {
+                    const uint32_t v = vv[gi];
+                    const uint32_t s0 = v & ~(2 * h - 1);  // the node's first position
+                    const uint32_t r1 = pre + (uint32_t)__popcll(bg & below) - (s0 >> 1);
+                    nxt[(v & h) ? s0 + h + r1 : j - r1] = (uint16_t)v;
+                }
+                pre += (uint32_t)__popcll(bg);
             }
-            const uint32_t ex = inc - t;
-            if (w0 < nw) cum[w0] = ex;
-            if (w0 + 1 < nw) cum[w0 + 1] = ex + c0;
-            if (w0 + 2 < nw) cum[w0 + 2] = ex + c0 + c1;
-        }
-        __syncthreads();
-        for (uint32_t w = tid; w < nw; w += WT_BT) lv[l * nw + w] = make_uint2(wb[w], cum[w]);
-        for (uint32_t j = tid; j < n; j += WT_BT) {
-            const uint32_t v = cur[j];
-            const uint32_t s0 = v & ~(2 * h - 1);  // the node's first position
-            const uint32_t r1 = cum[j >> 5] + __popc(wb[j >> 5] & ((1u << (j & 31)) - 1u)) - (s0 >> 1);
-            nxt[(v & h) ? s0 + h + r1 : j - r1] = (uint16_t)v;
         }
         __syncthreads();
         uint16_t *t = cur;
         cur = nxt;
         nxt = t;
     }
+    WT_STAMP(7);
     // level lb: the node of block b holds the ranks [32 b, 32 b + 32) in position order (all n ranks when K <= 5);
     // mk[b][o] = OR of bit (rank & 31) over its first o entries: a prefix OR per block, 32 lanes per block
     uint32_t *mk = reinterpret_cast<uint32_t *>(img + ci.o_mk);
@@ -322,6 +371,10 @@ __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__re
             if ((lane & 31) == 0) mk[b * 33] = 0;
         }
     }
+#ifdef WT_BUILD_TRACE
+    __syncthreads();
+#endif
+    WT_STAMP(8);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -1059,11 +1112,13 @@ int wt_build(WtState &w, nmz_ctx *ctx, const uint4 *d_table, uint32_t E, const C
     WtClass *d_cls = cv.take<WtClass>(n_cls);
     w.d_classes = d_cls;
     NMZ_HIP(hipMemsetAsync(w.d_rowsum, 0, 256 * 8, st));
-    NMZ_HIP(hipMemcpyAsync(d_cls, oc.data(), n_cls * sizeof(WtClass), hipMemcpyHostToDevice, st));
+    NMZ_TRY(ctx->pin[1].ensure(n_cls * sizeof(WtClass)));
+    std::memcpy(ctx->pin[1].ptr, oc.data(), n_cls * sizeof(WtClass));
+    NMZ_HIP(hipMemcpyAsync(d_cls, ctx->pin[1].ptr, n_cls * sizeof(WtClass), hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_replayable_wt_build, dim3(n_cls, 256), dim3(WT_BT), WT_BUILD_LDS, st, d_table, E, d_cls,
                        w.msh, bitlen(mod.m32), w.d_blob, w.rb16, w.d_rowsum);
     NMZ_HIP(hipGetLastError());
-    NMZ_HIP(hipStreamSynchronize(st));  // the host vector above is pageable
+    NMZ_HIP(hipStreamSynchronize(st));  // the plan is complete when it is returned (and the pinned staging free)
     w.on = true;
     return NMZ_OK;
 }
@@ -1119,3 +1174,10 @@ int wt_sweep(const WtState &w, nmz_ctx *ctx, hipStream_t st, const Buckets &b, c
 }
 
 }  // namespace nmz
+
+#ifdef WT_BUILD_TRACE
+extern "C" int nmz_debug_wt_build_trace(unsigned long long *out, uint32_t n) {
+    const uint32_t m = std::min<uint32_t>(n, nmz::WT_TRACE_WGS * nmz::WT_TRACE_PHASES);
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(nmz::g_wt_build_trace), m * 8) == hipSuccess ? 0 : -1;
+}
+#endif
