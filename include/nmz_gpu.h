@@ -186,6 +186,16 @@ typedef struct nmz_replayable_plan nmz_replayable_plan;
 int nmz_replayable_plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hint_bytes,
                                uint32_t n_events, int64_t max_interval_ns,
                                uint64_t max_seeds, nmz_replayable_plan **out);
+/* The same, returning as soon as the build is enqueued on the context's stream (the host arrays may be
+ * reused at once: they are staged in pinned memory). A sweep through the plan on any stream waits for the
+ * build on the device; destroy waits for it and for the plan's sweeps. For a stream of traces: create trace
+ * i + 1's plan (on a second context, so its build overlaps) while trace i sweeps. Plans the wavelet-tree plan
+ * kernel does not build in one launch (a class of 4,096 events or more, order-query or per-decision plans)
+ * are built synchronously as by nmz_replayable_plan_create. */
+int nmz_replayable_plan_create_async(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hint_bytes,
+                                     uint32_t n_events, int64_t max_interval_ns, uint64_t max_seeds,
+                                     nmz_replayable_plan **out);
+/* Waits for the plan's build and for the sweeps enqueued through it (not for the device or other streams). */
 int nmz_replayable_plan_destroy(nmz_replayable_plan *plan);
 /* Which statistics kernel the plan's sweeps take (diagnostic): 2 = wavelet-tree statistics (k_replayable_sweep_wt,
  * the default when 0 < max_interval < 2^32, the trace has <= 65,536 events -- a hint-length class of 4,096 or more
@@ -311,10 +321,11 @@ int nmz_ed_knn_fill_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys, voi
 /* Single queries against a resident store (HistoryStorage similarity search; the reference's own
  * search re-decodes every stored trace per query, naive.go:235-252 "FIXME: quite ineffective"):
  * the plan's stored traces stay on the device; each of n_queries query traces (CSR q_off/q_sym,
- * u64 event hashes, no longer than the longest stored trace) gets its k nearest stored traces by
- * (ED_band asc, id asc), ED_band as in nmz_ed_pairs. knn_id/knn_dist are [n_queries * k], NMZ_NONE
- * where fewer than k traces exist. Needs a bit-parallel plan (nmz_ed_plan_is_fast == 2: band 8, 16
- * or 32); NMZ_EINVAL otherwise. Synchronous. */
+ * u64 event hashes, any length) gets its k nearest stored traces by (ED_band asc, id asc), ED_band
+ * as in nmz_ed_pairs. knn_id/knn_dist are [n_queries * k], NMZ_NONE where fewer than k traces
+ * exist. Any plan and band: bit-parallel plans (band <= 64) run k_ed_bv's query form, wide plans
+ * (64 < band <= 8,192) k_ed_wide_query, the others (and queries longer than the plan's kernel
+ * takes) a generic per-pair kernel over the resident store. 1 <= k <= 64. Synchronous. */
 int nmz_ed_plan_query_knn(nmz_ed_plan *plan, const uint64_t *q_off, const uint64_t *q_sym, uint32_t n_queries,
                           uint32_t k, uint32_t *knn_id, uint32_t *knn_dist);
 /* Work counters of the plan's latest search (synchronises `stream`, NULL = the context's stream).

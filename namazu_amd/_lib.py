@@ -69,6 +69,7 @@ SIGNATURES = {
     "nmz_fnv1a64_batch": (_int, [_P, _P, _P, _u64, _P]),
     "nmz_replayable_sweep": (_int, [_P, _P, _P, _u64, _P, _P, _u32, _i64, _P, _P, _u64, _u32, _P]),
     "nmz_replayable_plan_create": (_int, [_P, _P, _P, _u32, _i64, _u64, ctypes.POINTER(_P)]),
+    "nmz_replayable_plan_create_async": (_int, [_P, _P, _P, _u32, _i64, _u64, ctypes.POINTER(_P)]),
     "nmz_replayable_plan_destroy": (_int, [_P]),
     "nmz_replayable_plan_kernel": (_int, [_P]),
     "nmz_replayable_sweep_dev": (_int, [_P, _P, _P, _u64, _P, _P]),

@@ -52,11 +52,14 @@ struct DevBuf {
 
 // Grow-only pinned host staging owned by a context: a plan's inputs are packed here and reach the device in one
 // asynchronous copy (a pageable hipMemcpyAsync stages through a driver buffer and returns only when that is done).
-// A user waits for the copy to complete before packing the next inputs (plan builds end with a stream sync).
+// The copy reading it is marked with an event (mark); ensure() waits for it before the buffer is packed again,
+// so a build that returns before its upload finished (nmz_replayable_plan_create_async) is safe.
 struct HostPin {
     void *ptr = nullptr;
     size_t cap = 0;
-    int ensure(size_t bytes);
+    hipEvent_t busy = nullptr;  // recorded after the last copy out of the buffer
+    int ensure(size_t bytes);   // waits for that copy, then grows (a power of two of at least 1 MiB)
+    int mark(hipStream_t st);
     void release();
 };
 

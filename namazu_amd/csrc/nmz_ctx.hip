@@ -21,9 +21,15 @@ int fail(int code, const std::string &msg) {
 }
 
 int HostPin::ensure(size_t bytes) {
+    if (busy && hipEventSynchronize(busy) != hipSuccess) return fail(NMZ_EHIP, "pinned staging wait failed");
     if (bytes <= cap) return NMZ_OK;
-    release();
-    const size_t want = std::max<size_t>(bytes * 3 / 2, 4096);
+    if (ptr) (void)hipHostFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+    // a power of two of at least 1 MiB: a stream of plans of slightly different sizes settles on one buffer
+    // (hipHostFree of an outgrown one synchronises the device)
+    size_t want = size_t(1) << 20;
+    while (want < bytes) want <<= 1;
     if (hipHostMalloc(&ptr, want, hipHostMallocDefault) != hipSuccess) {
         ptr = nullptr;
         return fail(NMZ_ENOMEM, "hipHostMalloc of " + std::to_string(want) + " bytes failed");
@@ -32,7 +38,20 @@ int HostPin::ensure(size_t bytes) {
     return NMZ_OK;
 }
 
+int HostPin::mark(hipStream_t st) {
+    if (!busy && hipEventCreateWithFlags(&busy, hipEventDisableTiming) != hipSuccess) {
+        busy = nullptr;
+        return fail(NMZ_EHIP, "hipEventCreate failed");
+    }
+    return hipEventRecord(busy, st) == hipSuccess ? NMZ_OK : fail(NMZ_EHIP, "hipEventRecord failed");
+}
+
 void HostPin::release() {
+    if (busy) {
+        (void)hipEventSynchronize(busy);
+        (void)hipEventDestroy(busy);
+    }
+    busy = nullptr;
     if (ptr) (void)hipHostFree(ptr);
     ptr = nullptr;
     cap = 0;
@@ -46,10 +65,17 @@ int DevBuf::ensure(size_t bytes) {
     if (ptr && pool && hipDeviceSynchronize() != hipSuccess) return fail(NMZ_EHIP, "hipDeviceSynchronize failed");
     release();
     size_t want = bytes < 256 ? 256 : bytes;
-    if (pool) {  // best fit among the pooled buffers (at most 4x the request, so small plans leave large ones)
+    if (pool && want >= (size_t(1) << 16)) {  // pooled: 1/8-power-of-two steps, so similar sizes reuse a buffer
+        size_t g = size_t(1) << 13;
+        while ((g << 4) <= want) g <<= 1;
+        want = (want + g - 1) & ~(g - 1);
+    }
+    if (pool) {  // best fit among the pooled buffers, at most 1.25x the request: a plan's buffers of other roles
+                 // (and small plans' large ones) stay for the requests they fit (a fresh hipMalloc of tens of MB
+                 // stalls the host for ~40 ms)
         size_t best = pool->size();
         for (size_t i = 0; i < pool->size(); ++i)
-            if ((*pool)[i].cap >= want && (*pool)[i].cap <= 4 * want &&
+            if ((*pool)[i].cap >= want && (*pool)[i].cap <= want + want / 4 &&
                 (best == pool->size() || (*pool)[i].cap < (*pool)[best].cap))
                 best = i;
         if (best < pool->size()) {

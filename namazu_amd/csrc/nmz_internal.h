@@ -152,9 +152,45 @@ struct WtState {
     uint4 *d_blob = nullptr;                // [256][rb16] row images
     unsigned long long *d_rowsum = nullptr;  // [256] sum of C mod m over the row
     void *d_classes = nullptr;              // [n_classes] segment descriptors
-    DevBuf mem;
+    DevBuf mem;                             // the row images
+    DevBuf aux;                             // separate path: row sums and segment descriptors
 };
 bool wt_enabled();
+struct WtClass {
+    uint64_t pn;              // P^len
+    uint32_t start, n;        // table segment (C order)
+    uint32_t o_lv, o_cm;      // byte offsets in the row image: wavelet levels [K][nw] {bits, ones before};
+    uint32_t o_chi, o_e;      //   Cm by rank (+ sentinel); C's high word by position (+ sentinel); e by rank (u16)
+    uint32_t o_im, o_ic;      //   bucket indexes (u16): first rank with Cm >= b << msh (257); first position
+                              //   with C_hi >= b << 24 (256)
+    uint32_t o_pm;            //   per d in [0, n]: {largest rank at positions < d, largest rank at positions >= d}
+                              //   (u16 pairs: the maximum of a part none of whose Cm is below its bound)
+    uint32_t K, nw;           // rank bits (2^K > n); words per level (n / 32 + 1)
+    uint32_t rS;              // lifting-search rounds (the largest bucket's bit length; set by the plan kernel)
+    uint32_t o_mk;            //   block masks [n / 32 + 1][33]: the ranks (bit r & 31) among the first o entries
+                              //   of each 32-rank block's node, o = 0..32
+    uint32_t order;           // plan kernel: the segment whose rows the order-th group of 256 workgroups builds
+};
+static_assert(sizeof(WtClass) == 64, "WtClass layout");
+
+// The wavelet-tree images: wt_layout (host only) decides whether they apply and lays out the segments (fused: every
+// class must be one segment), wt_launch runs the plan kernel with the classes and zeroed row sums already on the
+// device -- with hints (fused) the kernel computes the correction table itself (FNV of each hint per row L, C-sorted
+// per class) into hints->table and zeroes the two given ranges; wt_build = the separate path (table built first).
+struct WtPlanHints {
+    const uint32_t *hoff;
+    const uint8_t *hbytes;
+    const uint32_t *perm;
+    uint4 *table;
+    uint32_t *zero0;
+    uint32_t n_zero0;
+    uint32_t *zero1;
+    uint32_t n_zero1;
+};
+bool wt_layout(WtState &w, nmz_ctx *ctx, uint32_t E, const ClassInfo *cls, uint32_t n_cls, const ModParams &mod,
+               bool fused, std::vector<WtClass> &oc);
+int wt_launch(WtState &w, const uint4 *d_table, uint32_t E, const ModParams &mod, hipStream_t st,
+              const WtPlanHints *hints, WtClass *d_cls, unsigned long long *d_rowsum, bool sync);
 int wt_build(WtState &w, nmz_ctx *ctx, const uint4 *d_table, uint32_t E, const ClassInfo *cls, uint32_t n_cls,
              const ModParams &mod, hipStream_t st);
 // topk_scratch (wt_topk_scratch_bytes(S), or nullptr): the sweep also leaves per-seed sums (in bucketed order) and
@@ -162,9 +198,8 @@ int wt_build(WtState &w, nmz_ctx *ctx, const uint4 *d_table, uint32_t E, const C
 int wt_sweep(const WtState &w, nmz_ctx *ctx, hipStream_t st, const Buckets &b, const uint4 *d_table, uint32_t E,
              const ModParams &mod, nmz_sched_stats *d_stats, uint64_t S, void *topk_scratch, uint32_t k);
 size_t wt_topk_scratch_bytes(uint64_t S);
-// the top-k (k <= 64) of a sweep that ran with topk_scratch; fresh scratch must be zeroed first (wt_topk_reset)
+// the top-k (k <= 64) of a sweep that ran with topk_scratch (the sweep zeroes its candidate counter)
 int wt_topk(hipStream_t st, void *scratch, const uint32_t *sorted_idx, uint64_t S, uint64_t seed0, uint32_t k,
             nmz_topk_entry *d_out);
-int wt_topk_reset(hipStream_t st, void *scratch);
 
 }  // namespace nmz

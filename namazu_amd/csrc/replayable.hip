@@ -68,9 +68,11 @@ struct nmz_replayable_plan {
     nmz::DevBuf oq_mem;
     nmz::WtState wt;                    // wavelet-tree statistics (k_replayable_sweep_wt, the default when it fits)
     nmz::DevBuf wt_topk;                // their top-k candidates (sums, workgroup maxima, candidates)
-    void *wt_topk_zeroed = nullptr;     // the wt_topk buffer whose counters were zeroed
+    // recorded on the context's stream after the plan's build: a sweep on another stream waits for it on the
+    // device (nmz_replayable_plan_create_async returns before the build has run)
+    hipEvent_t built = nullptr;
     // the streams the plan's sweeps were enqueued on, each with an event recorded after its latest sweep:
-    // destroy waits for exactly that work (and the context's stream), not for the whole device
+    // destroy waits for exactly that work and the build, not for the whole device or the context's stream
     struct Use {
         hipStream_t st;
         hipEvent_t ev;
@@ -1622,29 +1624,35 @@ static int replayable_run_on(nmz_replayable_plan *p, hipStream_t st, const uint3
 static int replayable_run(nmz_replayable_plan *p, hipStream_t st, const uint32_t *d_soff, const uint8_t *d_sbytes,
                           uint64_t S, nmz_sched_stats *d_stats, uint64_t seed0 = 0, uint32_t k = 0,
                           nmz_topk_entry *d_topk = nullptr, uint64_t dec_lo = 0) {
-    const int rc = replayable_run_on(p, st, d_soff, d_sbytes, S, d_stats, seed0, k, d_topk, dec_lo);
-    if (st != p->ctx->stream) {  // destroy synchronises the context's stream itself
-        nmz_replayable_plan::Use *u = nullptr;
-        for (auto &x : p->uses)
-            if (x.st == st) u = &x;
-        if (!u) {
-            hipEvent_t ev;
-            NMZ_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-            p->uses.push_back({st, ev});
-            u = &p->uses.back();
-        }
-        NMZ_HIP(hipEventRecord(u->ev, st));
+    nmz_replayable_plan::Use *u = nullptr;
+    for (auto &x : p->uses)
+        if (x.st == st) u = &x;
+    if (!u) {  // the plan's first sweep on this stream: the stream waits for the build (a no-op once it is done)
+        hipEvent_t ev;
+        NMZ_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        p->uses.push_back({st, ev});
+        u = &p->uses.back();
+        if (p->built && st != p->ctx->stream) NMZ_HIP(hipStreamWaitEvent(st, p->built, 0));
     }
+    const int rc = replayable_run_on(p, st, d_soff, d_sbytes, S, d_stats, seed0, k, d_topk, dec_lo);
+    NMZ_HIP(hipEventRecord(u->ev, st));
     return rc;
 }
 
+// the plan's build and every sweep enqueued with it are done: its pooled buffers may go back to the context
 static void plan_wait_uses(nmz_replayable_plan *p) {
     for (auto &u : p->uses) {
         (void)hipEventSynchronize(u.ev);
         (void)hipEventDestroy(u.ev);
     }
     p->uses.clear();
-    (void)hipStreamSynchronize(p->ctx->stream);
+    if (p->built) {
+        (void)hipEventSynchronize(p->built);
+        (void)hipEventDestroy(p->built);
+        p->built = nullptr;
+    } else {
+        (void)hipStreamSynchronize(p->ctx->stream);
+    }
 }
 
 static int replayable_run_on(nmz_replayable_plan *p, hipStream_t st, const uint32_t *d_soff, const uint8_t *d_sbytes,
@@ -1656,11 +1664,7 @@ static int replayable_run_on(nmz_replayable_plan *p, hipStream_t st, const uint3
     // fallback has its merge levels): the general selection runs only when they overflow
     const bool fused = k && k <= 64 && S > 0 && use_wt(p) && wt_topk_enabled();
     if (fused) {
-        NMZ_TRY(p->wt_topk.ensure(wt_topk_scratch_bytes(S)));
-        if (p->wt_topk.ptr != p->wt_topk_zeroed) {  // fresh or pooled memory: the self-resetting counters start at 0
-            NMZ_TRY(wt_topk_reset(st, p->wt_topk.ptr));
-            p->wt_topk_zeroed = p->wt_topk.ptr;
-        }
+        NMZ_TRY(p->wt_topk.ensure(wt_topk_scratch_bytes(S)));  // the sweep zeroes its candidate counter
     }
     NMZ_TRY(replayable_stats(p, st, d_soff, d_sbytes, S, d_stats, dec_lo, fused ? p->wt_topk.ptr : nullptr, k));
     if (fused) {
@@ -1675,14 +1679,14 @@ static int replayable_run_on(nmz_replayable_plan *p, hipStream_t st, const uint3
 }
 
 static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hint_bytes, uint32_t E,
-                       int64_t max_interval, uint64_t max_seeds, nmz_replayable_plan **out) {
+                       int64_t max_interval, uint64_t max_seeds, nmz_replayable_plan **out, bool async = false) {
     NMZ_CHECK(ctx && out, "NULL argument");
     NMZ_CHECK(E == 0 || hint_off, "hint_off is NULL");
     *out = nullptr;
     auto *p = new nmz_replayable_plan();
     p->ctx = ctx;
     for (DevBuf *b : {&p->seed_scratch, &p->partial, &p->topk_lists, &p->plan_mem, &p->oq_mem, &p->wt.mem,
-                      &p->wt_topk})
+                      &p->wt.aux, &p->wt_topk})
         b->pool = &ctx->pool;
     p->n_events = E;
     p->max_interval = max_interval;
@@ -1719,15 +1723,25 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
     p->n_classes = (uint32_t)cls.size();
     const uint64_t nbytes = E ? hint_off[E] : 0;
 
+    // the wavelet-tree plan kernel computes and C-sorts the table itself when every class fits one of its segments:
+    // its segment descriptors and zeroed row sums go up with the plan's inputs, and it zeroes the seed scratch's
+    // counters itself -- one upload and one launch. (NMZ_WT_FUSED=0 takes the separate kernels always: parity tests
+    // and A/B runs.)
+    std::vector<WtClass> woc;
+    const bool fused = E && !(getenv("NMZ_WT_FUSED") && atoi(getenv("NMZ_WT_FUSED")) == 0) &&
+                       wt_layout(p->wt, ctx, E, cls.data(), (uint32_t)cls.size(), p->mod, true, woc);
     size_t need = Carve::bytes_for(cls.size() + 1, sizeof(ClassInfo)) + Carve::bytes_for((size_t)256 * E + 1, 16) +
                   Carve::bytes_for(E + 1, 4) * 2 + Carve::bytes_for(nbytes + 1, 1);
+    if (fused) need += Carve::bytes_for(woc.size(), sizeof(WtClass)) + Carve::bytes_for(256, 8);
     int rc = p->plan_mem.ensure(need);
-    if (rc == NMZ_OK && E && p->mod.kind != MOD_ZERO) {
+    SeedScratch sc0{};
+    const bool seeds = E && p->mod.kind != MOD_ZERO;
+    if (rc == NMZ_OK && seeds) {
         rc = p->seed_scratch.ensure(seed_scratch_bytes(max_seeds));
         if (rc == NMZ_OK) {  // bucket counters and the work-item counter start at zero (k_bucket_scan re-zeroes)
-            SeedScratch sc0 = carve_seed_scratch(p->seed_scratch.ptr, max_seeds);
-            if (hipMemsetAsync(sc0.b.count, 0, 256 * BUCKET_STRIDE * sizeof(uint32_t), st) != hipSuccess ||
-                hipMemsetAsync(sc0.counter, 0, 4 * sizeof(uint32_t), st) != hipSuccess)
+            sc0 = carve_seed_scratch(p->seed_scratch.ptr, max_seeds);
+            if (!fused && (hipMemsetAsync(sc0.b.count, 0, 256 * BUCKET_STRIDE * sizeof(uint32_t), st) != hipSuccess ||
+                           hipMemsetAsync(sc0.counter, 0, 4 * sizeof(uint32_t), st) != hipSuccess))
                 rc = fail(NMZ_EHIP, "hipMemsetAsync of the seed scratch failed");
         }
     }
@@ -1745,6 +1759,8 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
     uint32_t *d_perm = cv.take<uint32_t>(E + 1);
     uint32_t *d_hoff = p->d_hoff = cv.take<uint32_t>(E + 1);
     uint8_t *d_hbytes = p->d_hbytes = cv.take<uint8_t>(nbytes + 1);
+    WtClass *d_wcls = fused ? cv.take<WtClass>(woc.size()) : nullptr;
+    unsigned long long *d_rowsum = fused ? cv.take<unsigned long long>(256) : nullptr;
     const size_t in_bytes = (size_t)(reinterpret_cast<char *>(cv.take<uint4>(0)) - reinterpret_cast<char *>(p->plan_mem.ptr));
     p->d_table = cv.take<uint4>((size_t)256 * E + 1);
     auto cleanup = [&](int code) {
@@ -1755,6 +1771,7 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
         p->topk_lists.release();
         p->oq_mem.release();
         p->wt.mem.release();
+        p->wt.aux.release();
         p->wt_topk.release();
         delete p;
         return code;
@@ -1769,57 +1786,76 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
             std::memcpy(at(d_perm), perm.data(), (size_t)E * 4);
             std::memcpy(at(d_hoff), hint_off, (size_t)(E + 1) * 4);
             if (nbytes) std::memcpy(at(d_hbytes), hint_bytes, nbytes);
-        }
-        if (hipMemcpyAsync(p->plan_mem.ptr, pin.ptr, in_bytes, hipMemcpyHostToDevice, st))
-            return cleanup(fail(NMZ_EHIP, "plan upload failed"));
-        // unsorted table into scratch (the context's, grow-only: no free, so no device sync), then the
-        // per-(L, class) C sort into place
-        DevBuf &tmp = ctx->buf[10];
-        if (tmp.ensure((size_t)256 * E * sizeof(uint4)) != NMZ_OK) return cleanup(NMZ_ENOMEM);
-        hipLaunchKernelGGL(k_replayable_table, dim3(E), dim3(256), 0, st, d_hoff, d_hbytes, d_perm, E, p->mod.m,
-                           p->mod.m32ok ? 1 : 0, tmp.as<uint4>());
-        uint32_t max_class = 0;
-        for (const ClassInfo &c : cls) max_class = std::max(max_class, c.count);
-        bool bad = false;
-        if (max_class <= SEG_SORT_MAX && !getenv("NMZ_REPLAY_RANKSORT")) {  // LDS bitonic sort per segment
-            hipLaunchKernelGGL(k_replayable_table_segsort, dim3(p->n_classes, 256), dim3(1024), 0, st, tmp.as<uint4>(),
-                               p->d_classes, E, p->d_table);
-            // no sync when the order-query images follow: oq_build synchronises after its kernels
-            bad = hipGetLastError() != hipSuccess ||
-                  (!p->mod.m32ok && hipStreamSynchronize(st) != hipSuccess);
-        } else if (max_class <= 16384) {  // O(n^2) rank sort on the device
-            hipLaunchKernelGGL(k_replayable_table_sort, dim3(ceil_div(E, 256), 256), dim3(256), 0, st,
-                               tmp.as<uint4>(), p->d_classes, p->n_classes, E, p->d_table);
-            bad = hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess;
-        } else {  // very large classes: sort the segments on the host
-            std::vector<uint4> h((size_t)256 * E);
-            bad = hipGetLastError() != hipSuccess ||
-                  hipMemcpyAsync(h.data(), tmp.ptr, h.size() * sizeof(uint4), hipMemcpyDeviceToHost, st) !=
-                      hipSuccess ||
-                  hipStreamSynchronize(st) != hipSuccess;
-            if (!bad) {
-                auto key = [](const uint4 &q) { return ((uint64_t)q.y << 32) | q.x; };
-                for (uint32_t L = 0; L < 256; ++L)
-                    for (const ClassInfo &c : cls)
-                        std::stable_sort(h.begin() + (size_t)L * E + c.start,
-                                         h.begin() + (size_t)L * E + c.start + c.count,
-                                         [&](const uint4 &a, const uint4 &b) { return key(a) < key(b); });
-                bad = hipMemcpyAsync(p->d_table, h.data(), h.size() * sizeof(uint4), hipMemcpyHostToDevice, st) !=
-                          hipSuccess ||
-                      hipStreamSynchronize(st) != hipSuccess;
+            if (fused) {
+                std::memcpy(at(d_wcls), woc.data(), woc.size() * sizeof(WtClass));
+                std::memset(at(d_rowsum), 0, 256 * 8);
             }
         }
-        if (bad)
-            return cleanup(fail(NMZ_EHIP, "plan table kernel failed"));
-        // wavelet-tree images (the default sweep when they fit), else the order-query images
-        int orc = wt_build(p->wt, ctx, p->d_table, E, cls.data(), (uint32_t)cls.size(), p->mod, st);
-        if (orc != NMZ_OK) return cleanup(orc);
-        if (!p->wt.on) orc = oq_build(p, cls, st);
-        if (orc != NMZ_OK) return cleanup(orc);
-        // the plan is complete before it is returned: sweeps may run on any stream
+        if (hipMemcpyAsync(p->plan_mem.ptr, pin.ptr, in_bytes, hipMemcpyHostToDevice, st) || pin.mark(st))
+            return cleanup(fail(NMZ_EHIP, "plan upload failed"));
+        if (fused) {
+            const WtPlanHints hz{d_hoff, d_hbytes, d_perm, p->d_table,
+                                 seeds ? sc0.b.count : nullptr, seeds ? 256 * BUCKET_STRIDE : 0u,
+                                 seeds ? sc0.counter : nullptr, seeds ? 4u : 0u};
+            const int wrc = wt_launch(p->wt, p->d_table, E, p->mod, st, &hz, d_wcls, d_rowsum, !async);
+            if (wrc != NMZ_OK) return cleanup(wrc);
+        }
+        if (!p->wt.on) {
+            // unsorted table into scratch (the context's, grow-only: no free, so no device sync), then the
+            // per-(L, class) C sort into place
+            DevBuf &tmp = ctx->buf[10];
+            if (tmp.ensure((size_t)256 * E * sizeof(uint4)) != NMZ_OK) return cleanup(NMZ_ENOMEM);
+            hipLaunchKernelGGL(k_replayable_table, dim3(E), dim3(256), 0, st, d_hoff, d_hbytes, d_perm, E, p->mod.m,
+                               p->mod.m32ok ? 1 : 0, tmp.as<uint4>());
+            uint32_t max_class = 0;
+            for (const ClassInfo &c : cls) max_class = std::max(max_class, c.count);
+            bool bad = false;
+            if (max_class <= SEG_SORT_MAX && !getenv("NMZ_REPLAY_RANKSORT")) {  // LDS bitonic sort per segment
+                hipLaunchKernelGGL(k_replayable_table_segsort, dim3(p->n_classes, 256), dim3(1024), 0, st,
+                                   tmp.as<uint4>(), p->d_classes, E, p->d_table);
+                // no sync when the order-query images follow: oq_build synchronises after its kernels
+                bad = hipGetLastError() != hipSuccess ||
+                      (!p->mod.m32ok && hipStreamSynchronize(st) != hipSuccess);
+            } else if (max_class <= 16384) {  // O(n^2) rank sort on the device
+                hipLaunchKernelGGL(k_replayable_table_sort, dim3(ceil_div(E, 256), 256), dim3(256), 0, st,
+                                   tmp.as<uint4>(), p->d_classes, p->n_classes, E, p->d_table);
+                bad = hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess;
+            } else {  // very large classes: sort the segments on the host
+                std::vector<uint4> h((size_t)256 * E);
+                bad = hipGetLastError() != hipSuccess ||
+                      hipMemcpyAsync(h.data(), tmp.ptr, h.size() * sizeof(uint4), hipMemcpyDeviceToHost, st) !=
+                          hipSuccess ||
+                      hipStreamSynchronize(st) != hipSuccess;
+                if (!bad) {
+                    auto key = [](const uint4 &q) { return ((uint64_t)q.y << 32) | q.x; };
+                    for (uint32_t L = 0; L < 256; ++L)
+                        for (const ClassInfo &c : cls)
+                            std::stable_sort(h.begin() + (size_t)L * E + c.start,
+                                             h.begin() + (size_t)L * E + c.start + c.count,
+                                             [&](const uint4 &a, const uint4 &b) { return key(a) < key(b); });
+                    bad = hipMemcpyAsync(p->d_table, h.data(), h.size() * sizeof(uint4), hipMemcpyHostToDevice, st) !=
+                              hipSuccess ||
+                          hipStreamSynchronize(st) != hipSuccess;
+                }
+            }
+            if (bad)
+                return cleanup(fail(NMZ_EHIP, "plan table kernel failed"));
+            // wavelet-tree images (the default sweep when they fit), else the order-query images
+            int orc = wt_build(p->wt, ctx, p->d_table, E, cls.data(), (uint32_t)cls.size(), p->mod, st);
+            if (orc != NMZ_OK) return cleanup(orc);
+            if (!p->wt.on) orc = oq_build(p, cls, st);
+            if (orc != NMZ_OK) return cleanup(orc);
+        }
+        // the plan is complete before it is returned (sweeps may run on any stream), or, from the asynchronous
+        // entry point with the wavelet-tree plan kernel, enqueued: sweeps on other streams wait for `built`
         if (!p->oq && !p->wt.on && hipStreamSynchronize(st) != hipSuccess)
             return cleanup(fail(NMZ_EHIP, "plan build failed"));
     }
+    if (hipEventCreateWithFlags(&p->built, hipEventDisableTiming) != hipSuccess) {
+        p->built = nullptr;
+        return cleanup(fail(NMZ_EHIP, "hipEventCreate failed"));
+    }
+    if (hipEventRecord(p->built, st) != hipSuccess) return cleanup(fail(NMZ_EHIP, "hipEventRecord failed"));
     *out = p;
     return NMZ_OK;
 }
@@ -1844,6 +1880,15 @@ int nmz_replayable_plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uin
     return plan_create(ctx, hint_off, hint_bytes, n_events, max_interval_ns, max_seeds, out);
 }
 
+int nmz_replayable_plan_create_async(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hint_bytes,
+                                     uint32_t n_events, int64_t max_interval_ns, uint64_t max_seeds,
+                                     nmz_replayable_plan **out) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    return plan_create(ctx, hint_off, hint_bytes, n_events, max_interval_ns, max_seeds, out, true);
+}
+
 int nmz_replayable_plan_destroy(nmz_replayable_plan *plan) {
     if (!plan) return NMZ_OK;
     {
@@ -1857,6 +1902,7 @@ int nmz_replayable_plan_destroy(nmz_replayable_plan *plan) {
         plan->topk_lists.release();
         plan->oq_mem.release();
         plan->wt.mem.release();
+        plan->wt.aux.release();
         plan->wt_topk.release();
     }
     delete plan;
@@ -1920,6 +1966,7 @@ int nmz_replayable_sweep(nmz_ctx *ctx, const uint32_t *seed_off, const uint8_t *
             p->topk_lists.release();
             p->oq_mem.release();
             p->wt.mem.release();
+            p->wt.aux.release();
             p->wt_topk.release();
             delete p;
         }

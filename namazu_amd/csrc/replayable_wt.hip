@@ -21,6 +21,7 @@
 // and a row image of ~13 B per event instead of ~27, so two rows fit one CU's LDS.
 #include <algorithm>
 #include <cstring>
+#include <numeric>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -42,7 +43,7 @@ __device__ unsigned long long g_wt_build_trace[WT_TRACE_WGS * WT_TRACE_PHASES];
 #define WT_STAMP(k)                                                                                              \
     do {                                                                                                         \
         if (threadIdx.x == 0 && blockIdx.y * gridDim.x + blockIdx.x < WT_TRACE_WGS)                              \
-            g_wt_build_trace[(blockIdx.y * gridDim.x + blockIdx.x) * WT_TRACE_PHASES + (k)] = wall_clock64();    \
+            g_wt_build_trace[(L * gridDim.x + c) * WT_TRACE_PHASES + (k)] = wall_clock64();                      \
     } while (0)
 #else
 #define WT_STAMP(k) \
@@ -50,22 +51,7 @@ __device__ unsigned long long g_wt_build_trace[WT_TRACE_WGS * WT_TRACE_PHASES];
     } while (0)
 #endif        // sentinels past Cm and C_hi: lifting searches of <= 5 rounds need no clamp
 
-struct WtClass {
-    uint64_t pn;              // P^len
-    uint32_t start, n;        // table segment (C order)
-    uint32_t o_lv, o_cm;      // byte offsets in the row image: wavelet levels [K][nw] {bits, ones before};
-    uint32_t o_chi, o_e;      //   Cm by rank (+ sentinel); C's high word by position (+ sentinel); e by rank (u16)
-    uint32_t o_im, o_ic;      //   bucket indexes (u16): first rank with Cm >= b << msh (257); first position
-                              //   with C_hi >= b << 24 (256)
-    uint32_t o_pm;            //   per d in [0, n]: {largest rank at positions < d, largest rank at positions >= d}
-                              //   (u16 pairs: the maximum of a part none of whose Cm is below its bound)
-    uint32_t K, nw;           // rank bits (2^K > n); words per level (n / 32 + 1)
-    uint32_t rS;              // lifting-search rounds (the largest bucket's bit length; set by the plan kernel)
-    uint32_t o_mk;            //   block masks [n / 32 + 1][33]: the ranks (bit r & 31) among the first o entries
-                              //   of each 32-rank block's node, o = 0..32
-    uint32_t pad;
-};
-static_assert(sizeof(WtClass) == 64, "WtClass layout");
+// WtClass (the segment descriptor) is in nmz_internal.h: the plan's host code packs it with the plan's inputs
 
 // the tree stores the levels above the 32-rank blocks; the blocks' masks stand for the last five
 __host__ __device__ constexpr uint32_t wt_levels(uint32_t K) { return K > 5 ? K - 5 : 0; }
@@ -78,10 +64,54 @@ __host__ __device__ constexpr uint32_t wt_levels(uint32_t K) { return K > 5 ? K 
 // per 32 positions. Also adds the segment's sum of Cm to the row sum (every segment, short ones included).
 // ---------------------------------------------------------------------------------------------------------------
 constexpr uint32_t WT_BT = 512, WT_BW = WT_BT / 64;  // plan kernel: threads and waves per workgroup
+
+// exclusive scan in place over nb <= 2,048 bucket counts (4 per thread, wave scans, then the wave totals in cum);
+// *big gets the largest count above 32 (a bucket the per-bucket insertion sort should not take)
+__device__ __forceinline__ void wt_bucket_scan(uint32_t *bc, uint32_t nb, uint32_t *cum, uint32_t *big, uint32_t tid) {
+    const uint32_t lane = tid & 63, wave = tid >> 6, b0 = 4 * tid;
+    uint32_t c4[4], t = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        c4[k] = b0 + k < nb ? bc[b0 + k] : 0u;
+        t += c4[k];
+        if (c4[k] > 32) atomicMax(big, c4[k]);
+    }
+    uint32_t inc = t;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += v;
+    }
+    if (lane == 63) cum[wave] = inc;
+    __syncthreads();
+    uint32_t base = inc - t;
+    for (uint32_t w = 0; w < wave; ++w) base += cum[w];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (b0 + k < nb) bc[b0 + k] = base;  // bucket start (a cursor while scattering, then the end)
+        base += c4[k];
+    }
+    __syncthreads();
+}
+
+// the plan's hints on the device, for the fused plan kernel (it computes and C-sorts its own table segments)
+struct WtHints {
+    const uint32_t *hoff;   // [E + 1] hint byte offsets (original event order)
+    const uint8_t *hbytes;
+    const uint32_t *perm;   // [E] length-sorted position -> event
+    uint64_t m;             // the modulus (< 2^32 on this path) and floor(2^64 / m)
+    uint64_t mu;
+    uint4 *table;           // [256][E] out: {C lo, C hi, C mod m, ~e}, C-sorted per segment
+    uint32_t *zero0;        // ranges the first workgroup zeroes (the plan's seed-scratch counters)
+    uint32_t n_zero0;
+    uint32_t *zero1;
+    uint32_t n_zero1;
+};
+
+template <bool FUSED>
 __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__restrict__ table, uint32_t E,
                                                                WtClass *__restrict__ classes, uint32_t msh,
                                                                uint32_t mbits, uint4 *__restrict__ blob, uint32_t rb16,
-                                                               unsigned long long *__restrict__ rowsum) {
+                                                               unsigned long long *__restrict__ rowsum, WtHints hz) {
     // LDS (~73 KB, two workgroups per CU): the keys, then (after the sort) the rank arrays in their place; the
     // sorted keys; bucket counts (np / 2 buckets); level words and counts; small scratch
     extern __shared__ uint4 wt_build_lds[];
@@ -94,26 +124,165 @@ __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__re
     uint32_t *idx = cum + WT_NMAX / 32 + 4;                                     // [2][260] bucket indexes
     unsigned long long *part = reinterpret_cast<unsigned long long *>(idx + 520);  // [WT_BW]
     uint32_t *bmax = reinterpret_cast<uint32_t *>(part + WT_BW);               // [4]
-    const uint32_t c = blockIdx.x, L = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // workgroups start in dispatch order (x fastest): the largest segments' rows first, so the small segments'
+    // short workgroups fill in behind them instead of holding slots the large ones wait for
+    const uint32_t lin = blockIdx.y * gridDim.x + blockIdx.x, L = lin & 255u;
+    const uint32_t c = classes[lin >> 8].order, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     WT_STAMP(0);
     const WtClass ci = classes[c];
     const uint32_t n = ci.n;
-    const uint4 *__restrict__ row = table + (uint64_t)L * E + ci.start;
+    uint32_t np = 1, lgp = 0;
+    while (np < n) {
+        np <<= 1;
+        ++lgp;
+    }
+    const uint32_t nb = np >= 2 ? np / 2 : 1, lgb = lgp ? lgp - 1 : 0;  // sort buckets (~2 keys each) and their bits
+    if (tid < 4) bmax[tid] = 0;
     char *img = reinterpret_cast<char *>(blob + (uint64_t)L * rb16);
-    // the segment's entries, read once (every load in flight): the row sum, C's high words and the sort keys
+    // the segment's entries, one load each (every load in flight): the row sum, C's high words and the sort keys
     constexpr uint32_t PPT = WT_NMAX / WT_BT;
     uint4 q[PPT];
+    if constexpr (FUSED) {
+        if (lin == 0) {
+            for (uint32_t i = tid; i < hz.n_zero0; i += WT_BT) hz.zero0[i] = 0;
+            for (uint32_t i = tid; i < hz.n_zero1; i += WT_BT) hz.zero1[i] = 0;
+        }
+        // C = FNV-1a(seed bytes L, hint) - L * P^len (the table's correction, k_replayable_table) for the segment's
+        // events, a thread per event and all of a thread's events in step (one hint length per segment), then
+        // the stable C order through LDS: a counting sort on C's top bits and an insertion sort per bucket, or a
+        // bitonic sort of (C, position) when a bucket holds more than 32 (repeated hints)
+        uint16_t *posL = reinterpret_cast<uint16_t *>(key);  // [WT_NMAX] the sorted order's positions
+        uint16_t *eL = posL + WT_NMAX;                       // [WT_NMAX] event by position (E <= 65,536)
+        uint64_t h[PPT];
+        uint32_t b0[PPT];
+        uint32_t len = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < PPT; ++k) {
-        const uint32_t i = tid + k * WT_BT;
-        q[k] = i < n ? row[i] : make_uint4(0, 0, 0, 0);
+        for (uint32_t k = 0; k < PPT; ++k) {
+            const uint32_t i = tid + k * WT_BT;
+            h[k] = L;
+            b0[k] = 0;
+            if (i < n) {
+                const uint32_t e = hz.perm[ci.start + i];
+                eL[i] = (uint16_t)e;
+                b0[k] = hz.hoff[e];
+                len = hz.hoff[e + 1] - b0[k];
+            }
+        }
+        len = __builtin_amdgcn_readfirstlane(len);  // lane 0 holds an event of the segment (n >= 1)
+        // 16 hint bytes per round: the 5 aligned words covering them, all rounds' loads in flight together, then
+        // v_alignbit to the hint's own byte order
+        const uint32_t *__restrict__ hw = reinterpret_cast<const uint32_t *>(hz.hbytes);
+        for (uint32_t c0 = 0; c0 < len; c0 += 16) {
+            uint32_t w[PPT][5];
+#pragma unroll
+            for (uint32_t k = 0; k < PPT; ++k) {
+                const uint32_t a = (b0[k] + c0) >> 2, wl = (b0[k] + len - 1) >> 2;
+#pragma unroll
+                for (uint32_t j = 0; j < 5; ++j) w[k][j] = tid + k * WT_BT < n ? hw[min(a + j, wl)] : 0u;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < PPT; ++k) {
+                const uint32_t sh = 8 * (b0[k] & 3);
+                uint32_t u[4];
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) u[j] = __builtin_amdgcn_alignbit(w[k][j + 1], w[k][j], sh);
+#pragma unroll
+                for (uint32_t b = 0; b < 16; ++b)
+                    if (c0 + b < len) h[k] = fnv_step(h[k], (u[b >> 2] >> (8 * (b & 3))) & 0xffu);
+            }
+        }
+        const uint32_t shc = 64 - lgb;
+        auto cb = [&](uint64_t C) { return lgb ? (uint32_t)(C >> shc) : 0u; };
+        for (uint32_t b = tid; b < nb; b += WT_BT) bc[b] = 0;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < PPT; ++k) {
+            h[k] -= (uint64_t)L * ci.pn;  // C
+            if (tid + k * WT_BT < n) atomicAdd(&bc[cb(h[k])], 1u);
+        }
+        __syncthreads();
+        wt_bucket_scan(bc, nb, cum, bmax + 1, tid);
+        if (bmax[1] == 0) {
+#pragma unroll
+            for (uint32_t k = 0; k < PPT; ++k) {
+                const uint32_t i = tid + k * WT_BT;
+                if (i < n) {
+                    const uint32_t slot = atomicAdd(&bc[cb(h[k])], 1u);
+                    srt[slot] = h[k];
+                    posL[slot] = (uint16_t)i;
+                }
+            }
+            __syncthreads();
+            for (uint32_t b = tid; b < nb; b += WT_BT) {  // bucket b: [end of b - 1, end of b)
+                const uint32_t lo = b ? bc[b - 1] : 0u, hi = bc[b];
+                for (uint32_t i = lo + 1; i < hi; ++i) {
+                    const uint64_t v = srt[i];
+                    const uint16_t pv = posL[i];
+                    uint32_t j = i;
+                    while (j > lo && (srt[j - 1] > v || (srt[j - 1] == v && posL[j - 1] > pv))) {
+                        srt[j] = srt[j - 1];
+                        posL[j] = posL[j - 1];
+                        --j;
+                    }
+                    srt[j] = v;
+                    posL[j] = pv;
+                }
+            }
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < PPT; ++k) {
+                const uint32_t i = tid + k * WT_BT;
+                if (i < np) {
+                    srt[i] = i < n ? h[k] : ~0ull;
+                    posL[i] = (uint16_t)i;
+                }
+            }
+            for (uint32_t k = 2; k <= np; k <<= 1)
+                for (uint32_t j = k >> 1; j; j >>= 1) {
+                    __syncthreads();
+                    for (uint32_t i = tid; i < np; i += WT_BT) {
+                        const uint32_t l = i ^ j;
+                        if (l > i) {
+                            const uint64_t a = srt[i], b = srt[l];
+                            const uint16_t pa = posL[i], pb = posL[l];
+                            if ((a > b || (a == b && pa > pb)) == ((i & k) == 0)) {
+                                srt[i] = b;
+                                srt[l] = a;
+                                posL[i] = pb;
+                                posL[l] = pa;
+                            }
+                        }
+                    }
+                }
+        }
+        __syncthreads();
+        // the C-sorted entries (thread tid holds positions tid + k * WT_BT), written out as the table's row segment
+        uint4 *__restrict__ out = hz.table + (uint64_t)L * E + ci.start;
+#pragma unroll
+        for (uint32_t k = 0; k < PPT; ++k) {
+            const uint32_t j = tid + k * WT_BT;
+            q[k] = make_uint4(0, 0, 0, 0);
+            if (j < n) {
+                const uint64_t C = srt[j];
+                const uint32_t e = eL[posL[j]];
+                q[k] = make_uint4((uint32_t)C, (uint32_t)(C >> 32), mod_barrett64(C, hz.m, hz.mu), ~e);
+                out[j] = q[k];
+            }
+        }
+        __syncthreads();  // posL (the key region) and srt are free again
+    } else {
+        const uint4 *__restrict__ row = table + (uint64_t)L * E + ci.start;
+#pragma unroll
+        for (uint32_t k = 0; k < PPT; ++k) {
+            const uint32_t i = tid + k * WT_BT;
+            q[k] = i < n ? row[i] : make_uint4(0, 0, 0, 0);
+        }
     }
     uint64_t s = 0;
 #pragma unroll
     for (uint32_t k = 0; k < PPT; ++k) s += q[k].z;
     for (int o = 32; o; o >>= 1) s += __shfl_xor(s, o, 64);
     if (lane == 0) part[wave] = s;
-    if (tid < 4) bmax[tid] = 0;
     __syncthreads();
     if (tid == 0) {
         unsigned long long t = 0;
@@ -122,11 +291,6 @@ __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__re
     }
     WT_STAMP(1);
     if (n <= WT_BRUTE) return;
-    uint32_t np = 1, lgp = 0;
-    while (np < n) {
-        np <<= 1;
-        ++lgp;
-    }
     uint32_t *chi_img = reinterpret_cast<uint32_t *>(img + ci.o_chi);
 #pragma unroll
     for (uint32_t k = 0; k < PPT; ++k) {
@@ -141,37 +305,12 @@ __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__re
     // insertion sort per bucket (a thread per bucket); a bucket of more than 32 keys (repeated hints: equal Cm)
     // sends the whole segment to a bitonic sort
     {
-        const uint32_t nb = np >= 2 ? np / 2 : 1, lgb = lgp ? lgp - 1 : 0;
         const uint32_t sh = mbits > lgb ? mbits - lgb : 0u;
         for (uint32_t b = tid; b < nb; b += WT_BT) bc[b] = 0;
         __syncthreads();
         for (uint32_t i = tid; i < n; i += WT_BT) atomicAdd(&bc[(uint32_t)(key[i] >> 32) >> sh], 1u);
         __syncthreads();
-        {  // exclusive scan over nb <= 2,048 counts: 4 per thread, wave scans, then the wave totals
-            const uint32_t b0 = 4 * tid;
-            uint32_t c4[4], t = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                c4[k] = b0 + k < nb ? bc[b0 + k] : 0u;
-                t += c4[k];
-                if (c4[k] > 32) atomicMax(bmax, c4[k]);
-            }
-            uint32_t inc = t;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t v = __shfl_up(inc, o, 64);
-                if (lane >= (uint32_t)o) inc += v;
-            }
-            if (lane == 63) cum[wave] = inc;
-            __syncthreads();
-            uint32_t base = inc - t;
-            for (uint32_t w = 0; w < wave; ++w) base += cum[w];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (b0 + k < nb) bc[b0 + k] = base;  // bucket start (a cursor while scattering, then the end)
-                base += c4[k];
-            }
-        }
-        __syncthreads();
+        wt_bucket_scan(bc, nb, cum, bmax, tid);
         if (bmax[0] <= 32) {
             for (uint32_t i = tid; i < n; i += WT_BT) {
                 const uint64_t kk = key[i];
@@ -253,7 +392,9 @@ __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__re
         atomicMax(bmax + 3, (tid < 255 ? ic[tid + 1] : n) - ic[tid]);
     }
     __syncthreads();
+#ifndef WT_ABL_RS_ATOMIC
     if (tid == 0) atomicMax(&classes[c].rS, 32u - __clz(max(bmax[2], bmax[3])));
+#endif
     WT_STAMP(5);
     // prefix / suffix maxima of the ranks: pm[d] = {max rank at positions < d, max rank at positions >= d};
     // PP positions per thread, wave scans (up for the prefix, down for the suffix), then the wave totals
@@ -668,13 +809,13 @@ __device__ __forceinline__ void wt_seed_class(const WtVConst &vc, const WtClass 
 // top-k on the wavelet-tree path (k <= 64; order: sum desc as int64, seed asc; n_fault = 0 for this policy).
 // Each workgroup's largest sum is the largest of a group of seeds, and the groups are disjoint, so the k-th largest
 // of the group maxima (or of a subset of them) is a value at least k seeds reach: no seed below it is in the top k.
-// One kernel (every block derives tau itself: cheaper than a launch) appends the seeds at or above tau (a few
-// hundred), and a one-block kernel ranks them exactly by counting; more than
-// WT_CAND candidates (heavy ties, e.g. maxInterval 1) take a slow exact selection there instead. The candidate
+// One kernel (every block derives tau itself: cheaper than a launch) appends the seeds at or above tau (hundreds to
+// a few thousand), and a one-block kernel sorts them (bitonic, LDS); more than WT_CAND candidates (heavy ties, e.g.
+// maxInterval 1) take a slow exact selection there instead. The candidate
 // counter resets itself. (A "last block" handing tau or the ranking to the final workgroup of a kernel needs
 // device-scope fences, i.e. L2 writebacks on every XCD: +40 us on the sweep.)
 // ---------------------------------------------------------------------------------------------------------------
-constexpr uint32_t WT_CAND = 1024;
+constexpr uint32_t WT_CAND = 4096;
 constexpr uint32_t WT_MAX_GROUPS = 256 * 8;
 struct WtTopkState {
     uint32_t n_cand, pad[3];
@@ -700,6 +841,7 @@ __global__ __launch_bounds__(1024) void k_replayable_sweep_wt(
     const uint32_t nch = (s1 - s0 + CS - 1) / CS;
     const uint32_t c0 = g * nch / G, c1 = (g + 1) * nch / G;
     uint32_t *ctr = reinterpret_cast<uint32_t *>(wt_lds + rb16);
+    if (tk && blockIdx.x == 0 && threadIdx.x == 0) tk->n_cand = 0;  // the top-k scan after this sweep appends
     if (c0 == c1) {  // no seeds (an empty group: the smallest key)
         if (tk && threadIdx.x == 0) tk->gmax[blockIdx.x] = 0ull;
         return;
@@ -806,17 +948,19 @@ __device__ __forceinline__ bool wt_better(unsigned long long ka, uint64_t sa, un
     return ka > kb || (ka == kb && sa < sb);
 }
 
-// every block: tau = the k-th largest key of the first min(n, 256) groups (a subset's k-th largest is at most the
-// whole set's, so tau stays a value at least k seeds reach; ~k / subset size of the groups' maxima lie above it, so
-// a few hundred candidates), by counting; then a grid-stride scan of the sweep's sums appending the seeds at or
-// above tau. (All n = 512 groups bitonic-sorted per block: 45 barriers, ~13 us of the scan's latency.)
+// every block: tau = the k-th largest key of min(n, 512) groups sampled evenly over all rows (a subset's k-th largest
+// is at most the whole set's, so tau stays a value at least k seeds reach; ~k n / 512 of the groups' maxima lie
+// above it), by counting; then a grid-stride scan of the sweep's sums appending the seeds at or above tau (hundreds
+// to a few thousand: a row whose sums peak high holds many seeds near its peak). (The first 256 groups alone -- a few rows -- let one configs[1] trace in 17 overflow the
+// candidate list into the slow exact selection: 50 ms.)
 __global__ __launch_bounds__(256) void k_wt_topk_scan(const uint64_t *__restrict__ sums,
                                                       const uint32_t *__restrict__ sorted_idx, uint64_t S, uint32_t n,
                                                       uint32_t k, WtTopkState *__restrict__ tk) {
     constexpr uint32_t PF = 16;  // sums per thread loaded before they are needed (their latency overlaps tau)
-    __shared__ unsigned long long g[256];
+    constexpr uint32_t NS = 512;  // sampled groups
+    __shared__ unsigned long long g[NS];
     __shared__ unsigned long long tau_s;
-    const uint32_t m = min(n, 256u);
+    const uint32_t m = min(n, NS);
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     uint64_t v[PF];
 #pragma unroll
@@ -824,18 +968,20 @@ __global__ __launch_bounds__(256) void k_wt_topk_scan(const uint64_t *__restrict
         const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x + r * stride;
         v[r] = i < S ? sums[i] : 0ull;
     }
-    if (threadIdx.x < m) g[threadIdx.x] = tk->gmax[threadIdx.x];
+    for (uint32_t i = threadIdx.x; i < m; i += 256) g[i] = tk->gmax[(uint64_t)i * n / m];
     if (threadIdx.x == 0) tau_s = 0;  // fewer groups than k: every seed is a candidate
     __syncthreads();
-    if (m >= k && threadIdx.x < m) {
-        const unsigned long long x = g[threadIdx.x];
-        uint32_t gt = 0, eq = 0;
+    if (m >= k) {
+        for (uint32_t i = threadIdx.x; i < m; i += 256) {
+            const unsigned long long x = g[i];
+            uint32_t gt = 0, eq = 0;
 #pragma unroll 8
-        for (uint32_t j = 0; j < m; ++j) {
-            gt += g[j] > x;
-            eq += g[j] == x;
+            for (uint32_t j = 0; j < m; ++j) {
+                gt += g[j] > x;
+                eq += g[j] == x;
+            }
+            if (gt < k && k <= gt + eq) tau_s = x;  // every writer writes the same value
         }
-        if (gt < k && k <= gt + eq) tau_s = x;  // every writer writes the same value
     }
     __syncthreads();
     const unsigned long long t = tau_s;
@@ -864,18 +1010,18 @@ __global__ __launch_bounds__(256) void k_wt_topk_scan(const uint64_t *__restrict
     }
 }
 
-// one block: rank the candidates by counting and write the top k (past WT_CAND candidates: select them one rank at
-// a time over every seed: exact, slow); resets the candidate counter
+// one block: sort the candidates and write the top k (past WT_CAND candidates -- heavy ties, e.g. maxInterval 1 --
+// select them one rank at a time over every seed: exact, slow); resets the candidate counter
 constexpr uint32_t WT_SEL_THREADS = 512;
 __global__ __launch_bounds__(WT_SEL_THREADS) void k_wt_topk_select(const uint64_t *__restrict__ sums,
                                                                    const uint32_t *__restrict__ sorted_idx, uint64_t S,
-                                                                   uint64_t seed0, uint32_t k, uint32_t n_groups,
+                                                                   uint64_t seed0, uint32_t k,
                                                                    WtTopkState *__restrict__ tk,
                                                                    nmz_topk_entry *__restrict__ out) {
     constexpr uint32_t NT = WT_SEL_THREADS, NW = NT / 64;
-    __shared__ unsigned long long ck[WT_CAND], cs[WT_CAND], g[WT_MAX_GROUPS];
-    __shared__ unsigned long long bk[NW], bs[NW], tau2;
-    __shared__ uint32_t c2;
+    __shared__ unsigned long long ck[WT_CAND];
+    __shared__ uint32_t ci[WT_CAND];
+    __shared__ unsigned long long bk[NW], bs[NW];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t c = tk->n_cand;
     auto sentinel = [] {
@@ -887,52 +1033,47 @@ __global__ __launch_bounds__(WT_SEL_THREADS) void k_wt_topk_select(const uint64_
         return e;
     };
     if (c <= WT_CAND) {
-        // the exact k-th largest group key (the scan's subset bound is looser): keep the candidates at or above it
-        // (every seed at or above it is a candidate, since the subset bound is at most it), ~k of them
-        const uint32_t n = n_groups;
-        for (uint32_t i = threadIdx.x; i < n; i += NT) g[i] = tk->gmax[i];
-        if (threadIdx.x == 0) {
-            tau2 = 0;
-            c2 = 0;
+        // every seed at or above the scan's tau is a candidate (hundreds to a few thousand: a row whose sums peak
+        // high holds many near its peak): a bitonic sort of (key desc, seed asc) in LDS, padded with key 0 (a real
+        // key has its top bit set: sums are non-negative)
+        uint32_t p2 = 1;
+        while (p2 < c) p2 <<= 1;
+        for (uint32_t i = threadIdx.x; i < p2; i += NT) {
+            ck[i] = i < c ? tk->cand_key[i] : 0ull;
+            ci[i] = i < c ? (uint32_t)tk->cand_idx[i] : ~0u;
         }
-        __syncthreads();
-        if (n >= k)
-            for (uint32_t i = threadIdx.x; i < n; i += NT) {
-                const unsigned long long x = g[i];
-                uint32_t gt = 0, eq = 0;
-#pragma unroll 8
-                for (uint32_t j = 0; j < n; ++j) {
-                    gt += g[j] > x;
-                    eq += g[j] == x;
+        for (uint32_t kk = 2; kk <= p2; kk <<= 1)
+            for (uint32_t j = kk >> 1; j; j >>= 1) {
+                __syncthreads();
+                for (uint32_t i = threadIdx.x; i < p2; i += NT) {
+                    const uint32_t l = i ^ j;
+                    if (l > i) {
+                        const unsigned long long a = ck[i], b = ck[l];
+                        const uint32_t ia = ci[i], ib = ci[l];
+                        // l better than i (key desc, seed asc; padding last)
+                        const bool lb = b > a || (b == a && b != 0 && seed0 + ib < seed0 + ia);
+                        if (lb == ((i & kk) == 0)) {
+                            ck[i] = b;
+                            ck[l] = a;
+                            ci[i] = ib;
+                            ci[l] = ia;
+                        }
+                    }
                 }
-                if (gt < k && k <= gt + eq) tau2 = x;  // every writer writes the same value
             }
         __syncthreads();
-        const unsigned long long t2 = tau2;
-        for (uint32_t i = threadIdx.x; i < c; i += NT) {
-            const unsigned long long key = tk->cand_key[i];
-            if (key >= t2) {
-                const uint32_t pos = atomicAdd(&c2, 1u);
-                ck[pos] = key;
-                cs[pos] = seed0 + tk->cand_idx[i];  // seeds wrap as elsewhere
-            }
-        }
-        __syncthreads();
-        const uint32_t cc = c2;
-        for (uint32_t i = threadIdx.x; i < cc; i += NT) {
-            const unsigned long long a = ck[i], sa = cs[i];
-            uint32_t r = 0;
-            for (uint32_t j = 0; j < cc; ++j) r += wt_better(ck[j], cs[j], a, sa);
-            if (r < k) {
+        for (uint32_t r = threadIdx.x; r < k; r += NT) {
+            if (r < c) {
                 nmz_topk_entry e;
-                e.seed = sa;
-                e.sum_delay_ns = (int64_t)(a ^ (1ull << 63));
+                e.seed = seed0 + ci[r];  // seeds wrap as elsewhere
+                e.sum_delay_ns = (int64_t)(ck[r] ^ (1ull << 63));
                 e.n_fault = 0;
                 e.first_fault = NMZ_NONE;
                 out[r] = e;
+            } else {
+                out[r] = sentinel();  // fewer seeds than k
             }
         }
-        for (uint32_t r = cc + threadIdx.x; r < k; r += NT) out[r] = sentinel();  // fewer seeds than k
     } else {
         // exact selection one rank at a time: the best entry after the previous one in (key desc, seed asc)
         unsigned long long pk = ~0ull, ps = 0;
@@ -1041,10 +1182,14 @@ static uint32_t wt_threads() {
 constexpr size_t WT_BUILD_LDS = WT_NMAX * 8 * 2 + WT_NMAX / 2 * 4 + 2 * (WT_NMAX / 32 + 4) * 4 + 520 * 4 +
                                 WT_BW * 8 + 16;
 
-int wt_build(WtState &w, nmz_ctx *ctx, const uint4 *d_table, uint32_t E, const ClassInfo *cls, uint32_t n_cls,
-             const ModParams &mod, hipStream_t st) {
+bool wt_layout(WtState &w, nmz_ctx *ctx, uint32_t E, const ClassInfo *cls, uint32_t n_cls, const ModParams &mod,
+               bool fused, std::vector<WtClass> &oc) {
     w.on = false;
-    if (!wt_enabled() || !mod.m32ok || E == 0 || E > 65536) return NMZ_OK;
+    if (!wt_enabled() || !mod.m32ok || E == 0 || E > 65536) return false;
+    if (fused) {  // every class is one segment the plan kernel sorts itself
+        for (uint32_t c = 0; c < n_cls; ++c)
+            if (cls[c].count > WT_NMAX - 1) return false;
+    }
     auto r16 = [](uint64_t b) { return (b + 15) & ~15ull; };
     // segments: a class of 4,096 events or more (the plan kernel sorts < 4,096 keys in LDS) splits into near-equal
     // C-sorted sub-segments, each one a segment in its own right (every decision of it is (base + Cm) mod m with
@@ -1059,11 +1204,10 @@ int wt_build(WtState &w, nmz_ctx *ctx, const uint4 *d_table, uint32_t E, const C
         }
     }
     n_cls = (uint32_t)seg.size();
-    std::vector<WtClass> oc(n_cls);
+    oc.assign(n_cls, WtClass{});
     uint64_t off = 0;
     for (uint32_t c = 0; c < n_cls; ++c) {
         WtClass &o = oc[c];
-        o = WtClass{};
         o.pn = seg[c].pn;
         o.start = seg[c].start;
         o.n = seg[c].count;
@@ -1087,49 +1231,73 @@ int wt_build(WtState &w, nmz_ctx *ctx, const uint4 *d_table, uint32_t E, const C
         o.o_mk = (uint32_t)off;
         off += r16((uint64_t)(o.n / 32 + 1) * 33 * 4);
     }
+    {  // the plan kernel's dispatch order: segments by size, largest first
+        std::vector<uint32_t> ord(n_cls);
+        std::iota(ord.begin(), ord.end(), 0u);
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return oc[a].n > oc[b].n; });
+        for (uint32_t r = 0; r < n_cls; ++r) oc[r].order = ord[r];
+    }
     const uint64_t rb = std::max<uint64_t>(16, r16(off));
-    if (rb + 16 > WT_LDS_MAX) return NMZ_OK;
-    w.rb16 = (uint32_t)(rb / 16);
-    w.n_classes = n_cls;
-    w.msh = mod.m32 > 255 ? bitlen(mod.m32) - 8 : 0;
+    if (rb + 16 > WT_LDS_MAX) return false;
     // function attributes are per device: once per context (a context owns one device; its calls are serialised)
     if (!ctx->wt_lds_attr) {
         for (const void *f : {reinterpret_cast<const void *>(k_replayable_sweep_wt<false, 1>),
                               reinterpret_cast<const void *>(k_replayable_sweep_wt<true, 1>),
-                              reinterpret_cast<const void *>(k_replayable_wt_build)})
+                              reinterpret_cast<const void *>(k_replayable_wt_build<false>),
+                              reinterpret_cast<const void *>(k_replayable_wt_build<true>)})
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WT_LDS_MAX) != hipSuccess) {
                 (void)hipGetLastError();  // not sticky for the launches that follow: keep the order-query sweep
-                return NMZ_OK;
+                return false;
             }
         ctx->wt_lds_attr = true;
     }
-    const size_t need = Carve::bytes_for(256 * (size_t)w.rb16, 16) + Carve::bytes_for(256, 8) +
-                        Carve::bytes_for(n_cls, sizeof(WtClass));
-    NMZ_TRY(w.mem.ensure(need));
-    Carve cv(w.mem.ptr);
-    w.d_blob = cv.take<uint4>(256 * (size_t)w.rb16);
-    w.d_rowsum = cv.take<unsigned long long>(256);
-    WtClass *d_cls = cv.take<WtClass>(n_cls);
+    w.rb16 = (uint32_t)(rb / 16);
+    w.n_classes = n_cls;
+    w.msh = mod.m32 > 255 ? bitlen(mod.m32) - 8 : 0;
+    return true;
+}
+
+int wt_launch(WtState &w, const uint4 *d_table, uint32_t E, const ModParams &mod, hipStream_t st,
+              const WtPlanHints *hints, WtClass *d_cls, unsigned long long *d_rowsum, bool sync) {
+    NMZ_TRY(w.mem.ensure(Carve::bytes_for(256 * (size_t)w.rb16, 16)));
+    w.d_blob = w.mem.as<uint4>();
+    w.d_rowsum = d_rowsum;
     w.d_classes = d_cls;
-    NMZ_HIP(hipMemsetAsync(w.d_rowsum, 0, 256 * 8, st));
-    NMZ_TRY(ctx->pin[1].ensure(n_cls * sizeof(WtClass)));
-    std::memcpy(ctx->pin[1].ptr, oc.data(), n_cls * sizeof(WtClass));
-    NMZ_HIP(hipMemcpyAsync(d_cls, ctx->pin[1].ptr, n_cls * sizeof(WtClass), hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_replayable_wt_build, dim3(n_cls, 256), dim3(WT_BT), WT_BUILD_LDS, st, d_table, E, d_cls,
-                       w.msh, bitlen(mod.m32), w.d_blob, w.rb16, w.d_rowsum);
+    WtHints hz{};
+    if (hints)
+        hz = WtHints{hints->hoff, hints->hbytes, hints->perm, mod.m, mod.mu, hints->table, hints->zero0, hints->n_zero0,
+                     hints->zero1, hints->n_zero1};
+    if (hints)
+        hipLaunchKernelGGL(k_replayable_wt_build<true>, dim3(w.n_classes, 256), dim3(WT_BT), WT_BUILD_LDS, st, nullptr,
+                           E, d_cls, w.msh, bitlen(mod.m32), w.d_blob, w.rb16, d_rowsum, hz);
+    else
+        hipLaunchKernelGGL(k_replayable_wt_build<false>, dim3(w.n_classes, 256), dim3(WT_BT), WT_BUILD_LDS, st,
+                           d_table, E, d_cls, w.msh, bitlen(mod.m32), w.d_blob, w.rb16, d_rowsum, hz);
     NMZ_HIP(hipGetLastError());
-    NMZ_HIP(hipStreamSynchronize(st));  // the plan is complete when it is returned (and the pinned staging free)
+    if (sync) NMZ_HIP(hipStreamSynchronize(st));  // the plan is complete when it is returned
     w.on = true;
     return NMZ_OK;
 }
 
-size_t wt_topk_scratch_bytes(uint64_t S) {
-    return Carve::bytes_for(1, sizeof(WtTopkState)) + Carve::bytes_for(S, 8);
+int wt_build(WtState &w, nmz_ctx *ctx, const uint4 *d_table, uint32_t E, const ClassInfo *cls, uint32_t n_cls,
+             const ModParams &mod, hipStream_t st) {
+    std::vector<WtClass> oc;
+    if (!wt_layout(w, ctx, E, cls, n_cls, mod, false, oc)) return NMZ_OK;
+    // classes and row sums in their own buffer (the fused path uploads them with the plan's inputs)
+    NMZ_TRY(w.aux.ensure(Carve::bytes_for(256, 8) + Carve::bytes_for(oc.size(), sizeof(WtClass))));
+    Carve cv(w.aux.ptr);
+    unsigned long long *d_rowsum = cv.take<unsigned long long>(256);
+    WtClass *d_cls = cv.take<WtClass>(oc.size());
+    NMZ_HIP(hipMemsetAsync(d_rowsum, 0, 256 * 8, st));
+    NMZ_TRY(ctx->pin[1].ensure(oc.size() * sizeof(WtClass)));
+    std::memcpy(ctx->pin[1].ptr, oc.data(), oc.size() * sizeof(WtClass));
+    NMZ_HIP(hipMemcpyAsync(d_cls, ctx->pin[1].ptr, oc.size() * sizeof(WtClass), hipMemcpyHostToDevice, st));
+    NMZ_TRY(ctx->pin[1].mark(st));
+    return wt_launch(w, d_table, E, mod, st, nullptr, d_cls, d_rowsum, true);
 }
 
-int wt_topk_reset(hipStream_t st, void *scratch) {
-    NMZ_HIP(hipMemsetAsync(scratch, 0, sizeof(WtTopkState), st));
-    return NMZ_OK;
+size_t wt_topk_scratch_bytes(uint64_t S) {
+    return Carve::bytes_for(1, sizeof(WtTopkState)) + Carve::bytes_for(S, 8);
 }
 
 // the selection after a sweep that ran with this scratch (its per-seed sums and per-workgroup largest sums)
@@ -1141,8 +1309,8 @@ int wt_topk(hipStream_t st, void *scratch, const uint32_t *sorted_idx, uint64_t 
     const uint64_t *sums = cv.take<uint64_t>(S);
     const unsigned blocks = (unsigned)std::min<uint64_t>(ceil_div(S, 256), 256);
     hipLaunchKernelGGL(k_wt_topk_scan, dim3(blocks), dim3(256), 0, st, sums, sorted_idx, S, 256 * wt_groups(), k, tk);
-    hipLaunchKernelGGL(k_wt_topk_select, dim3(1), dim3(WT_SEL_THREADS), 0, st, sums, sorted_idx, S, seed0, k,
-                       256 * wt_groups(), tk, d_out);
+    hipLaunchKernelGGL(k_wt_topk_select, dim3(1), dim3(WT_SEL_THREADS), 0, st, sums, sorted_idx, S, seed0, k, tk,
+                       d_out);
     NMZ_HIP(hipGetLastError());
     return NMZ_OK;
 }

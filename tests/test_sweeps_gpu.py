@@ -26,14 +26,19 @@ def rep_oracle(seeds, hints, m, n_dump=0):
 
 
 # ---------------------------------------------------------------- K1
-@pytest.fixture(params=["wt", "oq"])
+@pytest.fixture(params=["wt", "wt_sep", "oq"])
 def k1(request, monkeypatch):
     """K1's two statistics kernels: wavelet trees (the default) and order queries (NMZ_REPLAY_WT=0 at plan
-    creation); plans that neither fits take the per-decision sweep either way."""
+    creation); plans that neither fits take the per-decision sweep either way. "wt" builds the wavelet-tree plan
+    with the fused plan kernel (it computes and C-sorts the correction table itself), "wt_sep" with the separate
+    table, sort and plan kernels (NMZ_WT_FUSED=0, the path for classes of 4,096 events or more)."""
+    monkeypatch.delenv("NMZ_WT_FUSED", raising=False)
     if request.param == "oq":
         monkeypatch.setenv("NMZ_REPLAY_WT", "0")
     else:
         monkeypatch.delenv("NMZ_REPLAY_WT", raising=False)
+        if request.param == "wt_sep":
+            monkeypatch.setenv("NMZ_WT_FUSED", "0")
     return request.param
 
 
@@ -323,6 +328,80 @@ def test_replayable_device_plan_api(ctx):
                                     len(seeds) + 1, ctypes.c_void_p(d_st.data_ptr()), stream)
     assert rc == _lib.NMZ_EINVAL
     L.nmz_replayable_plan_destroy(plan)
+
+
+@pytest.mark.parametrize("E,m,k", [(4096, 100_000_000, 64), (512, 2**31 + 3, 17), (1000, 1000, 64)])
+def test_replayable_topk_large_sweep(ctx, E, m, k):
+    """The wavelet-tree sweep's own top-k at 2^18 decimal seeds (thousands of workgroups: tau from sampled group
+    maxima, candidates ranked by counting) == the top-k of the same sweep's stats."""
+    import torch
+    L = _lib.load()
+    S = 1 << 18
+    ho, hb = to_csr(zk_hints(E, np.random.default_rng(E)))
+    plan = ctypes.c_void_p()
+    _lib.check(L.nmz_replayable_plan_create(ctx.handle, _lib.ptr(ho), _lib.ptr(hb), E, m, S, ctypes.byref(plan)))
+    d_st = torch.zeros(S * 32, dtype=torch.uint8, device="cuda")
+    d_tk = torch.zeros(k * 24, dtype=torch.uint8, device="cuda")
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(L.nmz_replayable_sweep_decimal_topk_dev(plan, 10**12, S, k, ctypes.c_void_p(d_st.data_ptr()),
+                                                       ctypes.c_void_p(d_tk.data_ptr()), stream))
+    torch.cuda.synchronize()
+    L.nmz_replayable_plan_destroy(plan)
+    st = np.frombuffer(d_st.cpu().numpy().tobytes(), dtype=_lib.SCHED_STATS_DTYPE)
+    tk = np.frombuffer(d_tk.cpu().numpy().tobytes(), dtype=_lib.TOPK_DTYPE)
+    assert tk.tolist() == O.topk_from_stats(st, 10**12, k).tolist()
+
+
+def test_replayable_plan_create_async(ctx):
+    """nmz_replayable_plan_create_async: builds enqueued on two contexts' streams, sweeps enqueued at once on
+    another stream (which must wait for each build on the device), plans of several shapes (the one-launch
+    wavelet-tree build, a class of 4,096 events: the separate kernels, maxInterval >= 2^32: per-decision), the
+    staging reused by the next build before the previous one ran, and a plan destroyed with its build in flight."""
+    import torch
+    L = _lib.load()
+    ctx2 = _lib.Context(0)
+    try:
+        S = 2500
+        seeds = [str(i * 31) for i in range(S)]
+        so, sb = to_csr(seeds)
+        d_so = torch.from_numpy(so.view(np.int32)).cuda()
+        d_sb = torch.from_numpy(sb).cuda()
+        cases = [(zk_hints(600), 100_000_000), (zk_hints(97) + ["", "a"], 7), (["x" * 5] * 4097, 100_000_000),
+                 (zk_hints(300), 2**32 + 5), (zk_hints(2000), 2**31 + 3), (zk_hints(64), 1_000_000)]
+        st = torch.cuda.Stream()
+        plans, outs = [], []
+        for i, (hints, m) in enumerate(cases):
+            ho, hb = to_csr(hints)
+            p = ctypes.c_void_p()
+            _lib.check(L.nmz_replayable_plan_create_async((ctx, ctx2)[i % 2].handle, _lib.ptr(ho), _lib.ptr(hb),
+                                                          len(hints), m, S, ctypes.byref(p)))
+            del ho, hb  # the host arrays may go at once
+            d_st = torch.zeros(S * 32, dtype=torch.uint8, device="cuda")
+            d_tk = torch.zeros(16 * 24, dtype=torch.uint8, device="cuda")
+            with torch.cuda.stream(st):
+                _lib.check(L.nmz_replayable_sweep_topk_dev(p, ctypes.c_void_p(d_so.data_ptr()),
+                                                           ctypes.c_void_p(d_sb.data_ptr()), S, 0, 16,
+                                                           ctypes.c_void_p(d_st.data_ptr()),
+                                                           ctypes.c_void_p(d_tk.data_ptr()),
+                                                           ctypes.c_void_p(st.cuda_stream)))
+            plans.append(p)
+            outs.append((d_st, d_tk))
+        for p in plans:
+            L.nmz_replayable_plan_destroy(p)  # waits for its build and its sweep
+        for (hints, m), (d_st, d_tk) in zip(cases, outs):
+            got = np.frombuffer(d_st.cpu().numpy().tobytes(), dtype=_lib.SCHED_STATS_DTYPE)
+            ref, _ = rep_oracle(seeds, hints, m)
+            assert np.array_equal(got, ref), m
+            tk = np.frombuffer(d_tk.cpu().numpy().tobytes(), dtype=_lib.TOPK_DTYPE)
+            assert tk.tolist() == O.topk_from_stats(ref, 0, 16).tolist()
+        # destroyed while its build may still run
+        ho, hb = to_csr(zk_hints(3000))
+        p = ctypes.c_void_p()
+        _lib.check(L.nmz_replayable_plan_create_async(ctx.handle, _lib.ptr(ho), _lib.ptr(hb), 3000, 100_000_000, S,
+                                                      ctypes.byref(p)))
+        L.nmz_replayable_plan_destroy(p)
+    finally:
+        ctx2.close()
 
 
 @pytest.mark.parametrize("m,S,E,k,seed0", [

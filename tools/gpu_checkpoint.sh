@@ -7,4 +7,4 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -2 gpurun_out/${tag}_smoke.log
 timeout -k 10 900 python bench.py > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.log || { rc=$?; tail -20 gpurun_out/${tag}_bench.log; exit $rc; }
 python3 -c "
-import json;d=json.loads(open('gpurun_out/${tag}_bench.json').read().strip().splitlines()[-1]);print(d['value'], d['ms_per_step'], d['end_to_end'], d.get('end_to_end_stream'))"
+import json;d=json.loads(open('gpurun_out/${tag}_bench.json').read().strip().splitlines()[-1]);e=d['end_to_end'];print(d['value'], d['ms_per_step'], e['value'], e.get('ms_per_trace'), e.get('one_at_a_time', {}).get('value'), d['plan_ms'])"
