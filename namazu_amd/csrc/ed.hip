@@ -439,7 +439,7 @@ struct nmz_ed_plan {
     // bv, two-phase search: per-(shard, n_shards) tile starts (host, kept), scratch and the entry lists
     std::map<uint64_t, nmz::DevBuf> tile_list;      // per (shard, n_shards): the shard's tiles (qb << 32 | cb)
     std::map<uint64_t, uint64_t> tile_count;
-    nmz::DevBuf tp_mem, tp_ent, tp_mask;
+    nmz::DevBuf tp_mem, tp_ent, tp_rec;
     // fixed at creation (NMZ_ED_QGRAM / NMZ_ED_TWO_PHASE, A/B knobs read once per plan), so every shard and every
     // call of one plan takes the same search and deals pairs by the same rule
     bool qgram = true, two_phase = true;
@@ -1050,7 +1050,7 @@ uint32_t ed_bv_item() {
 // DP over the work items. Returns 1 when the entry lists would exceed ED_TP_MAX_ENTRIES (caller falls back to
 // the single-kernel search).
 constexpr uint64_t ED_TP_MAX_ENTRIES = 1ULL << 30;  // 4 GiB of entries
-constexpr uint64_t ED_TP_MAX_MASK_BYTES = 4ULL << 30;
+constexpr uint64_t ED_TP_MAX_REC_BYTES = 1ULL << 30;
 
 // The shard that owns query block qb (64 queries) of the two-phase search: rotated snake order. A query block's
 // work falls with qb inside the upper triangle (fewer candidates j > q) and inside every family of near-duplicates;
@@ -1060,6 +1060,8 @@ constexpr uint64_t ED_TP_MAX_MASK_BYTES = 4ULL << 30;
 // blocks at 8 shards -- shard 0 always held each family's first and last block, whose short candidate lists run the
 // DP less efficiently (1.15x); the MurmurHash3 deal of round 2 left max/mean 1.15. DESIGN.md section 6.) A fixed
 // rule, not a knob: one process per GPU computes its own shards' tiles, so the rule must be the same everywhere.
+// (Dealing runs of 4 or 16 consecutive blocks instead, to keep a family's candidates in one shard's L2, measured
+// worse: 8-shard sum / unsharded 1.17 / 1.16 clustered vs 1.14; profiles/r04/ed_deal_chunk_ab.)
 static uint32_t ed_block_shard(uint32_t qb, uint32_t n_shards) {
     if (n_shards <= 1) return 0;
     const uint32_t r = qb % (2 * n_shards), pr = r < n_shards ? r : 2 * n_shards - 1 - r;
@@ -1110,16 +1112,26 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     // where a round-robin deal aligned with it (8 shards: max/mean shard time 1.27)
     const uint64_t key = ((uint64_t)shard << 32) | n_shards;
     DevBuf &tl = p->tile_list[key];
-    std::vector<uint32_t> qb_tiles;  // the shard's query blocks and their first tiles (for batches)
+    // Tiles in 2-D superblocks of ED_SQ query blocks x ED_SC candidate blocks (2,048 queries x 4,096 candidates: 768
+    // KiB of profiles) and the filter kernels hand each XCD a contiguous range of the list, so an XCD's L2 holds a
+    // superblock's profiles while its tiles run (query-block order fetched every candidate profile once per query
+    // block: 7.1 GB per launch). Batches are whole groups of ED_SQ of the shard's query blocks.
+    constexpr uint32_t ED_SQ = 32, ED_SC = 16;
+    std::vector<uint32_t> qbs, grp;  // the shard's query blocks; per group: first index into qbs, first tile
     auto shard_tiles = [&](std::vector<uint64_t> *tiles) {
         uint64_t t = 0;
-        qb_tiles.clear();
-        for (uint32_t qb = 0; qb < QB; ++qb) {
-            if (ed_block_shard(qb, n_shards) != shard) continue;
-            qb_tiles.push_back(qb);
-            qb_tiles.push_back((uint32_t)t);
-            for (uint32_t cb = qb / 4; cb < NCB; ++cb, ++t)
-                if (tiles) tiles->push_back(((uint64_t)qb << 32) | cb);
+        qbs.clear();
+        grp.clear();
+        for (uint32_t qb = 0; qb < QB; ++qb)
+            if (ed_block_shard(qb, n_shards) == shard) qbs.push_back(qb);
+        for (size_t g0 = 0; g0 < qbs.size(); g0 += ED_SQ) {
+            const size_t g1 = std::min(qbs.size(), g0 + ED_SQ);
+            grp.push_back((uint32_t)g0);
+            grp.push_back((uint32_t)t);
+            for (uint32_t cb0 = qbs[g0] / 4; cb0 < NCB; cb0 += ED_SC)
+                for (size_t i = g0; i < g1; ++i)
+                    for (uint32_t cb = std::max(cb0, qbs[i] / 4); cb < std::min(NCB, cb0 + ED_SC); ++cb, ++t)
+                        if (tiles) tiles->push_back(((uint64_t)qbs[i] << 32) | cb);
         }
         return t;
     };
@@ -1150,11 +1162,18 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     Q.cnt = d_cnt;
     Q.cur = d_cur;
     Q.ent = nullptr;
-    // the count pass's survivor ballots (2 KiB per tile) let the write pass scatter without recomputing the filter
-    Q.masks = nullptr;
-    if (n_tiles_all * 2048 <= ED_TP_MAX_MASK_BYTES &&
-        p->tp_mask.ensure(Carve::bytes_for(n_tiles_all * 2048, 1)) == NMZ_OK)
-        Q.masks = p->tp_mask.as<uint64_t>();
+    // the count pass's survivor records (32 B per (wave, query pair) with survivors) let the write pass scatter
+    // without recomputing the filter; room for 16 per tile (a record list that overflows: the write pass recomputes)
+    const uint64_t rec_cap = std::min<uint64_t>(n_tiles_all * 16, ED_TP_MAX_REC_BYTES / 32);
+    Q.recs = nullptr;
+    Q.rec_cap = 0;
+    // (NMZ_ED_QG_RECOMPUTE=1 skips the records: the recompute path, for tests)
+    const char *rc_env = getenv("NMZ_ED_QG_RECOMPUTE");
+    if (!(rc_env && atoi(rc_env) == 1) && p->tp_rec.ensure(Carve::bytes_for(rec_cap * 32 + 16, 1)) == NMZ_OK) {
+        Q.recs = p->tp_rec.as<uint4>() + 1;
+        Q.rec_cap = (uint32_t)rec_cap;
+    }
+    Q.n_rec = Q.recs ? p->tp_rec.as<uint32_t>() : nullptr;  // the counter in the buffer's first 16 bytes
     Q.N = N;
     Q.k = A.k;
     Q.QB = QB;
@@ -1164,10 +1183,12 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     Q.w = p->band;
     const uint32_t item = ed_bv_item();
     // count pass + scans over tiles [t0, t1): entry and item totals
+    uint32_t n_rec = 0;
     auto count = [&](uint64_t t0, uint64_t t1, uint64_t &tot64, uint32_t &tot_items) -> int {
         Q.tiles = tl.as<uint64_t>() + t0;
         Q.n_tiles = t1 - t0;
         NMZ_HIP(hipMemsetAsync(d_cnt, 0, (n_pairs + 1) * 4, st));
+        if (Q.recs) NMZ_HIP(hipMemsetAsync(Q.n_rec, 0, 4, st));
         {
             KernelTimer kt(p->ctx, st, "ed_qg_filter");
             NMZ_TRY(ed_qg_filter_launch(Q, true, st));
@@ -1182,6 +1203,7 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
         NMZ_HIP(hipGetLastError());
         NMZ_HIP(hipMemcpyAsync(&tot64, d_tot64, 8, hipMemcpyDeviceToHost, st));
         NMZ_HIP(hipMemcpyAsync(&tot_items, d_ioff + n_pairs, 4, hipMemcpyDeviceToHost, st));
+        if (Q.recs) NMZ_HIP(hipMemcpyAsync(&n_rec, Q.n_rec, 4, hipMemcpyDeviceToHost, st));
         NMZ_HIP(hipStreamSynchronize(st));
         return NMZ_OK;
     };
@@ -1192,7 +1214,7 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
         NMZ_HIP(hipMemcpyAsync(d_cur, d_poff, (uint64_t)n_pairs * 4, hipMemcpyDeviceToDevice, st));
         {
             KernelTimer kt(p->ctx, st, "ed_qg_filter");
-            if (Q.masks) NMZ_TRY(ed_qg_scatter_launch(Q, st));
+            if (Q.recs && n_rec <= Q.rec_cap) NMZ_TRY(ed_qg_scatter_launch(Q, n_rec, st));
             else NMZ_TRY(ed_qg_filter_launch(Q, false, st));
         }
         KernelTimer kt(p->ctx, st, "ed_bv_dp");
@@ -1208,21 +1230,22 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     std::vector<uint32_t> cnt(n_pairs);
     NMZ_HIP(hipMemcpy(cnt.data(), d_cnt, (size_t)n_pairs * 4, hipMemcpyDeviceToHost));
     shard_tiles(nullptr);
-    const size_t nq = qb_tiles.size() / 2;
+    const size_t ng = grp.size() / 2;
     hipLaunchKernelGGL(k_knn_init, dim3(ceil_div((uint64_t)N * A.k, 256)), dim3(256), 0, st, d_knn, (uint64_t)N * A.k);
     NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_CNT_WORDS * 8, st));
-    for (size_t b0 = 0; b0 < nq;) {
+    for (size_t b0 = 0; b0 < ng;) {
         uint64_t acc = 0;
         size_t b1 = b0;
-        while (b1 < nq) {
-            const uint32_t qb = qb_tiles[2 * b1];
+        while (b1 < ng) {
+            const size_t i1 = b1 + 1 < ng ? grp[2 * (b1 + 1)] : qbs.size();
             uint64_t c = 0;
-            for (uint32_t pp = 32 * qb; pp < std::min(32 * qb + 32, n_pairs); ++pp) c += cnt[pp];
+            for (size_t i = grp[2 * b1]; i < i1; ++i)
+                for (uint32_t pp = 32 * qbs[i]; pp < std::min(32 * qbs[i] + 32, n_pairs); ++pp) c += cnt[pp];
             if (b1 > b0 && acc + c > limit) break;
             acc += c;
             ++b1;
         }
-        const uint64_t t0 = qb_tiles[2 * b0 + 1], t1 = b1 < nq ? qb_tiles[2 * b1 + 1] : n_tiles_all;
+        const uint64_t t0 = grp[2 * b0 + 1], t1 = b1 < ng ? grp[2 * b1 + 1] : n_tiles_all;
         NMZ_TRY(count(t0, t1, tot64, tot_items));
         NMZ_TRY(write_dp(tot64, tot_items));
         b0 = b1;
@@ -1387,7 +1410,7 @@ int nmz_ed_plan_destroy(nmz_ed_plan *plan) {
         plan->mem.release();
         plan->tp_mem.release();
         plan->tp_ent.release();
-        plan->tp_mask.release();
+        plan->tp_rec.release();
         for (auto &kv : plan->tile_list) kv.second.release();
     }
     delete plan;
@@ -1776,7 +1799,7 @@ int nmz_ed_allpairs_knn(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, 
             p->mem.release();
             p->tp_mem.release();
             p->tp_ent.release();
-            p->tp_mask.release();
+            p->tp_rec.release();
             for (auto &kv : p->tile_list) kv.second.release();
             delete p;
         }

@@ -637,11 +637,18 @@ __device__ __forceinline__ uint32_t qg_l1_reg(const uint4 (&c)[ED_QG_DW / 4], co
 
 // One tile: queries [64 qb, 64 qb + 64) x candidates [256 cb, 256 cb + 256), pairs j > q only (the shard's tile
 // list: csrc/ed.hip ed_bv_two_phase).
+// the tile of hardware block b: XCD b % 8 takes a contiguous eighth of the list (its superblocks' profiles stay in
+// that XCD's L2); the grid is a multiple of 8
+__device__ __forceinline__ uint64_t qg_tile_of_block() {
+    const uint64_t per = gridDim.x / 8;
+    return (uint64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+}
+
 template <bool COUNT>
 __global__ __launch_bounds__(256) void k_ed_qg_filter(EdQgArgs A) {
     __shared__ uint4 qp[64][ED_QG_DW / 4];
     __shared__ uint32_t qlen[64];
-    const uint64_t t = blockIdx.x;
+    const uint64_t t = qg_tile_of_block();
     if (t >= A.n_tiles) return;
     const uint64_t tq = A.tiles[t];
     const uint32_t qb = (uint32_t)(tq >> 32), cb = (uint32_t)tq;
@@ -698,11 +705,14 @@ __global__ __launch_bounds__(256) void k_ed_qg_filter(EdQgArgs A) {
         a2 = a2 && !f2;
         const bool sv = a1 || a2;
         const uint64_t mask = __ballot(sv);
-        if (COUNT && A.masks) {  // the survivors for the scatter pass: two ballots per (wave, pair)
+        if (COUNT && A.recs && mask) {  // the survivors for the scatter pass: one record per (wave, pair)
             const uint64_t m1 = __ballot(a1), m2 = __ballot(a2);
             if (lane == 0) {
-                ulonglong2 *mk = (ulonglong2 *)A.masks + ((uint64_t)t * 4 + wave) * 32 + pp;
-                *mk = make_ulonglong2(m1, m2);
+                const uint32_t r = atomicAdd(A.n_rec, 1u);
+                if (r < A.rec_cap) {
+                    A.recs[2 * (uint64_t)r] = make_uint4(q1 >> 1, 256 * cb + 64 * wave, (uint32_t)m1, (uint32_t)(m1 >> 32));
+                    A.recs[2 * (uint64_t)r + 1] = make_uint4((uint32_t)m2, (uint32_t)(m2 >> 32), 0u, 0u);
+                }
             }
         }
         if (mask) {
@@ -727,34 +737,29 @@ __global__ __launch_bounds__(256) void k_ed_qg_filter(EdQgArgs A) {
     if (COUNT) bv_flush_counters(A.counters, 0, c_in_band, 0, 0, 0, c_qgram);
 }
 
-// The write pass from the count pass's ballots (EdQgArgs::masks): per (wave, pair) with survivors, one cursor
-// atomic and the entries -- no profile loads, no L1s.
-__global__ __launch_bounds__(256) void k_ed_qg_scatter(EdQgArgs A) {
-    const uint64_t t = blockIdx.x;
-    if (t >= A.n_tiles) return;
-    const uint64_t tq = A.tiles[t];
-    const uint32_t qb = (uint32_t)(tq >> 32), cb = (uint32_t)tq;
-    const uint32_t j = 256 * cb + threadIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t np = min(32u, (A.N - 64 * qb + 1) / 2);
-    const ulonglong2 *mk = (const ulonglong2 *)A.masks + ((uint64_t)t * 4 + wave) * 32;
-    for (uint32_t pp = 0; pp < np; ++pp) {
-        const ulonglong2 mm = mk[pp];
-        const uint64_t mask = mm.x | mm.y;
-        if (!mask) continue;
-        const uint32_t p = (64 * qb + 2 * pp) >> 1;
+// The write pass from the count pass's records (EdQgArgs::recs): a wave per record -- one cursor atomic and the
+// entries; no profile loads, no L1s, and nothing read for the (wave, pair)s without survivors (most of them: the
+// dense per-tile ballots this replaces were 2 KiB per tile, 0.6 GB read per launch on configs[2]).
+__global__ __launch_bounds__(256) void k_ed_qg_scatter(EdQgArgs A, uint32_t n_rec) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nw = gridDim.x * 4;
+    for (uint32_t r = blockIdx.x * 4 + (threadIdx.x >> 6); r < n_rec; r += nw) {
+        const uint4 h = A.recs[2 * (uint64_t)r], g = A.recs[2 * (uint64_t)r + 1];
+        const uint64_t m1 = ((uint64_t)h.w << 32) | h.z, m2 = ((uint64_t)g.y << 32) | g.x, mask = m1 | m2;
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&A.cur[p], (uint32_t)__popcll(mask));
+        if (lane == 0) base = atomicAdd(&A.cur[h.x], (uint32_t)__popcll(mask));
         base = __shfl(base, 0, 64);
         const uint64_t bit = 1ull << lane;
         if (mask & bit)
             A.ent[base + __popcll(mask & (bit - 1))] =
-                j | ((uint32_t)((mm.x & bit) != 0) << 30) | ((uint32_t)((mm.y & bit) != 0) << 31);
+                (h.y + lane) | ((uint32_t)((m1 & bit) != 0) << 30) | ((uint32_t)((m2 & bit) != 0) << 31);
     }
 }
 
-int ed_qg_scatter_launch(const EdQgArgs &A, hipStream_t st) {
-    if (A.n_tiles == 0) return NMZ_OK;
-    hipLaunchKernelGGL(k_ed_qg_scatter, dim3((unsigned)A.n_tiles), dim3(256), 0, st, A);
+int ed_qg_scatter_launch(const EdQgArgs &A, uint32_t n_rec, hipStream_t st) {
+    if (n_rec == 0) return NMZ_OK;
+    const uint32_t blocks = (n_rec + 3) / 4 < 8192 ? (n_rec + 3) / 4 : 8192;
+    hipLaunchKernelGGL(k_ed_qg_scatter, dim3(blocks), dim3(256), 0, st, A, n_rec);
     NMZ_HIP(hipGetLastError());
     return NMZ_OK;
 }
@@ -762,7 +767,7 @@ int ed_qg_scatter_launch(const EdQgArgs &A, hipStream_t st) {
 int ed_qg_filter_launch(const EdQgArgs &A, bool count, hipStream_t st) {
     if (A.n_tiles == 0) return NMZ_OK;
     NMZ_CHECK(A.n_tiles < (1ULL << 31), "too many traces for one launch");
-    const dim3 g((unsigned)A.n_tiles), b(256);
+    const dim3 g((unsigned)((A.n_tiles + 7) / 8 * 8)), b(256);
     if (count) hipLaunchKernelGGL(k_ed_qg_filter<true>, g, b, 0, st, A);
     else hipLaunchKernelGGL(k_ed_qg_filter<false>, g, b, 0, st, A);
     NMZ_HIP(hipGetLastError());

@@ -85,14 +85,17 @@ struct EdQgArgs {
     uint32_t *cnt;               // count pass: [n_pairs] entries per query pair
     uint32_t *cur;               // write pass: [n_pairs] cursors, starting at the pairs' entry offsets
     uint32_t *ent;               // write pass: the entries
-    uint64_t *masks;             // count pass: [n_tiles][4 waves][32 pairs] 2 ballots (run1, run2) for the
-                                 // scatter pass, or nullptr (the write pass recomputes the filter)
+    uint4 *recs;                 // count pass: one record per (wave, query pair) with survivors -- {pair, first
+                                 // candidate, run1 ballot} and {run2 ballot} (2 uint4) -- for the scatter pass, or
+                                 // nullptr (the write pass recomputes the filter)
+    uint32_t *n_rec;             // records appended (may exceed rec_cap: then the write pass recomputes)
+    uint32_t rec_cap;
     uint64_t n_tiles;
     uint32_t N, k, QB, NCB, shard, n_shards;
     uint32_t w;                  // band
 };
 int ed_qg_filter_launch(const EdQgArgs &A, bool count, hipStream_t st);
-int ed_qg_scatter_launch(const EdQgArgs &A, hipStream_t st);
+int ed_qg_scatter_launch(const EdQgArgs &A, uint32_t n_rec, hipStream_t st);
 int ed_bv_dp_launch(const EdBvArgs &A, const uint32_t *ioff, const uint32_t *poff, const uint32_t *ent,
                     uint32_t n_pairs, uint32_t n_items, uint32_t item, uint32_t bw, bool cmp, hipStream_t st);
 // single-query search on a bit-parallel plan (ed_bv.hip k_ed_bv_query): 1-2 external queries vs every stored trace

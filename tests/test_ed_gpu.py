@@ -554,12 +554,16 @@ def _edited_family(n, length, alphabet, max_edits, rng):
     return hs.TraceSet(out)
 
 
+@pytest.mark.parametrize("recompute", [False, True])
 @pytest.mark.parametrize("w,alphabet,max_edits", [(32, 48, 90), (16, 6, 40), (8, 200, 25)])
-def test_knn_qgram_filter_exact(ctx, monkeypatch, w, alphabet, max_edits):
+def test_knn_qgram_filter_exact(ctx, monkeypatch, w, alphabet, max_edits, recompute):
     """The q-gram lower bound (bigram profiles > 4w apart => ED_w = w + 1 without a DP) and the in-band-only
     publishing + k_knn_fill: the all-pairs k-NN equals the oracle's and the run with the filter off, the counters
-    show pairs settled by the bound and pairs that ran the DP, and the shard path (merge + fill) agrees too."""
+    show pairs settled by the bound and pairs that ran the DP, and the shard path (merge + fill) agrees too. The
+    write pass runs from the count pass's survivor records, or (recompute) re-runs the filter."""
     import torch
+    if recompute:
+        monkeypatch.setenv("NMZ_ED_QG_RECOMPUTE", "1")
     L = _lib.load()
     rng = np.random.default_rng(w * 1000 + alphabet)
     ts = _edited_family(400, 300, alphabet, max_edits, rng)

@@ -47,10 +47,15 @@ KERNELS = {
     "k_ed_bv_dp:clustered": "_ZN3nmz10k_ed_bv_dpILi32ELb0E",
     "k_ed_bv_dp:alphabet": "_ZN3nmz10k_ed_bv_dpILi32ELb1E",
     "k_ed_wide": "_ZN3nmz9k_ed_wideILi4E",
+    # the q-gram filter's key holds its count and scatter passes (one timer in bench.py); the count pass's hot loop
+    # (v_sad_u8, measured at 4.10 cycles: profiles/r04/r04ub_issue_rates.log) prices both
+    "k_ed_qg_filter:survey": "_ZN3nmz14k_ed_qg_filterILb1E",
+    "k_ed_qg_filter:clustered": "_ZN3nmz14k_ed_qg_filterILb1E",
 }
 
 # cycles per wave64 instruction per SIMD at 8 waves/SIMD, tools/ubench/bv_rates.hip (profiles/r03ub_issue_rates.log)
-FORM_COST = {"v_bitop3_b32": 2.8, "v_alignbit_b32": 4.4, "v_lshl_add_u64": 4.35, "v_mad_u64_u32": 4.2}
+FORM_COST = {"v_bitop3_b32": 2.8, "v_alignbit_b32": 4.4, "v_lshl_add_u64": 4.35, "v_mad_u64_u32": 4.2,
+             "v_sad_u8": 4.10}
 HALF_OPS = ("v_min_u32", "v_max_u32", "v_min_i32", "v_max_i32", "v_readfirstlane", "v_cmp", "v_cmpx", "v_mul",
             "v_mad", "v_bcnt", "v_mbcnt", "v_bfe", "v_bfi", "v_add3", "v_lshl_add", "v_lshl_or", "v_and_or", "v_or3",
             "v_xor3", "v_xad", "v_perm", "v_readlane", "v_writelane", "v_lshlrev_b64", "v_lshrrev_b64")

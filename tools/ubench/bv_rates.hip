@@ -498,6 +498,70 @@ __global__ __launch_bounds__(256) void k30(uint32_t* out, uint64_t* clk, uint32_
   out[blockIdx.x*256+threadIdx.x] = v0^v1^v2^v3^v4^v5^v6^v7^(uint32_t)(w0^w1^w2^w3^w4^w5^w6^w7);
   if (threadIdx.x == 0 && blockIdx.x == 0) clk[30] = t1 - t0;
 }
+__global__ __launch_bounds__(256) void k31(uint32_t* out, uint64_t* clk, uint32_t seed) {
+  uint32_t v0=threadIdx.x+seed, v1=v0*3, v2=v0*5, v3=v0*7, v4=v0*9, v5=v0*11, v6=v0*13, v7=v0*15;
+  uint64_t w0=v0, w1=v1, w2=v2, w3=v3, w4=v4, w5=v5, w6=v6, w7=v7, wa=(uint64_t)seed<<20;
+  uint32_t a=seed*0x9e37u, b=seed^0x5555u;
+  uint32_t sg = __builtin_amdgcn_readfirstlane(seed&31u);
+  uint64_t sm = __builtin_amdgcn_read_exec();
+  uint64_t t0 = clock64();
+  for (int it = 0; it < ITERS; ++it) {
+    asm volatile("v_sad_u8 %0, %[a], %[b], %0\n\tv_sad_u8 %1, %[a], %[b], %1\n\tv_sad_u8 %2, %[a], %[b], %2\n\tv_sad_u8 %3, %[a], %[b], %3\n\tv_sad_u8 %4, %[a], %[b], %4\n\tv_sad_u8 %5, %[a], %[b], %5\n\tv_sad_u8 %6, %[a], %[b], %6\n\tv_sad_u8 %7, %[a], %[b], %7\n\tv_sad_u8 %0, %[a], %[b], %0\n\tv_sad_u8 %1, %[a], %[b], %1\n\tv_sad_u8 %2, %[a], %[b], %2\n\tv_sad_u8 %3, %[a], %[b], %3\n\tv_sad_u8 %4, %[a], %[b], %4\n\tv_sad_u8 %5, %[a], %[b], %5\n\tv_sad_u8 %6, %[a], %[b], %6\n\tv_sad_u8 %7, %[a], %[b], %7\n\tv_sad_u8 %0, %[a], %[b], %0\n\tv_sad_u8 %1, %[a], %[b], %1\n\tv_sad_u8 %2, %[a], %[b], %2\n\tv_sad_u8 %3, %[a], %[b], %3\n\tv_sad_u8 %4, %[a], %[b], %4\n\tv_sad_u8 %5, %[a], %[b], %5\n\tv_sad_u8 %6, %[a], %[b], %6\n\tv_sad_u8 %7, %[a], %[b], %7\n\tv_sad_u8 %0, %[a], %[b], %0\n\tv_sad_u8 %1, %[a], %[b], %1\n\tv_sad_u8 %2, %[a], %[b], %2\n\tv_sad_u8 %3, %[a], %[b], %3\n\tv_sad_u8 %4, %[a], %[b], %4\n\tv_sad_u8 %5, %[a], %[b], %5\n\tv_sad_u8 %6, %[a], %[b], %6\n\tv_sad_u8 %7, %[a], %[b], %7" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6), "+v"(v7),
+                 [w0] "+v"(w0), [w1] "+v"(w1), [w2] "+v"(w2), [w3] "+v"(w3), [w4] "+v"(w4), [w5] "+v"(w5), [w6] "+v"(w6), [w7] "+v"(w7)
+                 : [a] "v"(a), [b] "v"(b), [sg] "s"(sg), [sm] "s"(sm), [wa] "v"(wa) : "vcc");
+  }
+  uint64_t t1 = clock64();
+  out[blockIdx.x*256+threadIdx.x] = v0^v1^v2^v3^v4^v5^v6^v7^(uint32_t)(w0^w1^w2^w3^w4^w5^w6^w7);
+  if (threadIdx.x == 0 && blockIdx.x == 0) clk[31] = t1 - t0;
+}
+__global__ __launch_bounds__(256) void k32(uint32_t* out, uint64_t* clk, uint32_t seed) {
+  uint32_t v0=threadIdx.x+seed, v1=v0*3, v2=v0*5, v3=v0*7, v4=v0*9, v5=v0*11, v6=v0*13, v7=v0*15;
+  uint64_t w0=v0, w1=v1, w2=v2, w3=v3, w4=v4, w5=v5, w6=v6, w7=v7, wa=(uint64_t)seed<<20;
+  uint32_t a=seed*0x9e37u, b=seed^0x5555u;
+  uint32_t sg = __builtin_amdgcn_readfirstlane(seed&31u);
+  uint64_t sm = __builtin_amdgcn_read_exec();
+  uint64_t t0 = clock64();
+  for (int it = 0; it < ITERS; ++it) {
+    asm volatile("v_sad_u8 %0, %[a], %[sg], %0\n\tv_sad_u8 %1, %[a], %[sg], %1\n\tv_sad_u8 %2, %[a], %[sg], %2\n\tv_sad_u8 %3, %[a], %[sg], %3\n\tv_sad_u8 %4, %[a], %[sg], %4\n\tv_sad_u8 %5, %[a], %[sg], %5\n\tv_sad_u8 %6, %[a], %[sg], %6\n\tv_sad_u8 %7, %[a], %[sg], %7\n\tv_sad_u8 %0, %[a], %[sg], %0\n\tv_sad_u8 %1, %[a], %[sg], %1\n\tv_sad_u8 %2, %[a], %[sg], %2\n\tv_sad_u8 %3, %[a], %[sg], %3\n\tv_sad_u8 %4, %[a], %[sg], %4\n\tv_sad_u8 %5, %[a], %[sg], %5\n\tv_sad_u8 %6, %[a], %[sg], %6\n\tv_sad_u8 %7, %[a], %[sg], %7\n\tv_sad_u8 %0, %[a], %[sg], %0\n\tv_sad_u8 %1, %[a], %[sg], %1\n\tv_sad_u8 %2, %[a], %[sg], %2\n\tv_sad_u8 %3, %[a], %[sg], %3\n\tv_sad_u8 %4, %[a], %[sg], %4\n\tv_sad_u8 %5, %[a], %[sg], %5\n\tv_sad_u8 %6, %[a], %[sg], %6\n\tv_sad_u8 %7, %[a], %[sg], %7\n\tv_sad_u8 %0, %[a], %[sg], %0\n\tv_sad_u8 %1, %[a], %[sg], %1\n\tv_sad_u8 %2, %[a], %[sg], %2\n\tv_sad_u8 %3, %[a], %[sg], %3\n\tv_sad_u8 %4, %[a], %[sg], %4\n\tv_sad_u8 %5, %[a], %[sg], %5\n\tv_sad_u8 %6, %[a], %[sg], %6\n\tv_sad_u8 %7, %[a], %[sg], %7" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6), "+v"(v7),
+                 [w0] "+v"(w0), [w1] "+v"(w1), [w2] "+v"(w2), [w3] "+v"(w3), [w4] "+v"(w4), [w5] "+v"(w5), [w6] "+v"(w6), [w7] "+v"(w7)
+                 : [a] "v"(a), [b] "v"(b), [sg] "s"(sg), [sm] "s"(sm), [wa] "v"(wa) : "vcc");
+  }
+  uint64_t t1 = clock64();
+  out[blockIdx.x*256+threadIdx.x] = v0^v1^v2^v3^v4^v5^v6^v7^(uint32_t)(w0^w1^w2^w3^w4^w5^w6^w7);
+  if (threadIdx.x == 0 && blockIdx.x == 0) clk[32] = t1 - t0;
+}
+__global__ __launch_bounds__(256) void k33(uint32_t* out, uint64_t* clk, uint32_t seed) {
+  uint32_t v0=threadIdx.x+seed, v1=v0*3, v2=v0*5, v3=v0*7, v4=v0*9, v5=v0*11, v6=v0*13, v7=v0*15;
+  uint64_t w0=v0, w1=v1, w2=v2, w3=v3, w4=v4, w5=v5, w6=v6, w7=v7, wa=(uint64_t)seed<<20;
+  uint32_t a=seed*0x9e37u, b=seed^0x5555u;
+  uint32_t sg = __builtin_amdgcn_readfirstlane(seed&31u);
+  uint64_t sm = __builtin_amdgcn_read_exec();
+  uint64_t t0 = clock64();
+  for (int it = 0; it < ITERS; ++it) {
+    asm volatile("v_mbcnt_lo_u32_b32 %0, %[a], %0\n\tv_mbcnt_lo_u32_b32 %1, %[a], %1\n\tv_mbcnt_lo_u32_b32 %2, %[a], %2\n\tv_mbcnt_lo_u32_b32 %3, %[a], %3\n\tv_mbcnt_lo_u32_b32 %4, %[a], %4\n\tv_mbcnt_lo_u32_b32 %5, %[a], %5\n\tv_mbcnt_lo_u32_b32 %6, %[a], %6\n\tv_mbcnt_lo_u32_b32 %7, %[a], %7\n\tv_mbcnt_lo_u32_b32 %0, %[a], %0\n\tv_mbcnt_lo_u32_b32 %1, %[a], %1\n\tv_mbcnt_lo_u32_b32 %2, %[a], %2\n\tv_mbcnt_lo_u32_b32 %3, %[a], %3\n\tv_mbcnt_lo_u32_b32 %4, %[a], %4\n\tv_mbcnt_lo_u32_b32 %5, %[a], %5\n\tv_mbcnt_lo_u32_b32 %6, %[a], %6\n\tv_mbcnt_lo_u32_b32 %7, %[a], %7\n\tv_mbcnt_lo_u32_b32 %0, %[a], %0\n\tv_mbcnt_lo_u32_b32 %1, %[a], %1\n\tv_mbcnt_lo_u32_b32 %2, %[a], %2\n\tv_mbcnt_lo_u32_b32 %3, %[a], %3\n\tv_mbcnt_lo_u32_b32 %4, %[a], %4\n\tv_mbcnt_lo_u32_b32 %5, %[a], %5\n\tv_mbcnt_lo_u32_b32 %6, %[a], %6\n\tv_mbcnt_lo_u32_b32 %7, %[a], %7\n\tv_mbcnt_lo_u32_b32 %0, %[a], %0\n\tv_mbcnt_lo_u32_b32 %1, %[a], %1\n\tv_mbcnt_lo_u32_b32 %2, %[a], %2\n\tv_mbcnt_lo_u32_b32 %3, %[a], %3\n\tv_mbcnt_lo_u32_b32 %4, %[a], %4\n\tv_mbcnt_lo_u32_b32 %5, %[a], %5\n\tv_mbcnt_lo_u32_b32 %6, %[a], %6\n\tv_mbcnt_lo_u32_b32 %7, %[a], %7" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6), "+v"(v7),
+                 [w0] "+v"(w0), [w1] "+v"(w1), [w2] "+v"(w2), [w3] "+v"(w3), [w4] "+v"(w4), [w5] "+v"(w5), [w6] "+v"(w6), [w7] "+v"(w7)
+                 : [a] "v"(a), [b] "v"(b), [sg] "s"(sg), [sm] "s"(sm), [wa] "v"(wa) : "vcc");
+  }
+  uint64_t t1 = clock64();
+  out[blockIdx.x*256+threadIdx.x] = v0^v1^v2^v3^v4^v5^v6^v7^(uint32_t)(w0^w1^w2^w3^w4^w5^w6^w7);
+  if (threadIdx.x == 0 && blockIdx.x == 0) clk[33] = t1 - t0;
+}
+__global__ __launch_bounds__(256) void k34(uint32_t* out, uint64_t* clk, uint32_t seed) {
+  uint32_t v0=threadIdx.x+seed, v1=v0*3, v2=v0*5, v3=v0*7, v4=v0*9, v5=v0*11, v6=v0*13, v7=v0*15;
+  uint64_t w0=v0, w1=v1, w2=v2, w3=v3, w4=v4, w5=v5, w6=v6, w7=v7, wa=(uint64_t)seed<<20;
+  uint32_t a=seed*0x9e37u, b=seed^0x5555u;
+  uint32_t sg = __builtin_amdgcn_readfirstlane(seed&31u);
+  uint64_t sm = __builtin_amdgcn_read_exec();
+  uint64_t t0 = clock64();
+  for (int it = 0; it < ITERS; ++it) {
+    asm volatile("v_mbcnt_hi_u32_b32 %0, %[a], %0\n\tv_mbcnt_hi_u32_b32 %1, %[a], %1\n\tv_mbcnt_hi_u32_b32 %2, %[a], %2\n\tv_mbcnt_hi_u32_b32 %3, %[a], %3\n\tv_mbcnt_hi_u32_b32 %4, %[a], %4\n\tv_mbcnt_hi_u32_b32 %5, %[a], %5\n\tv_mbcnt_hi_u32_b32 %6, %[a], %6\n\tv_mbcnt_hi_u32_b32 %7, %[a], %7\n\tv_mbcnt_hi_u32_b32 %0, %[a], %0\n\tv_mbcnt_hi_u32_b32 %1, %[a], %1\n\tv_mbcnt_hi_u32_b32 %2, %[a], %2\n\tv_mbcnt_hi_u32_b32 %3, %[a], %3\n\tv_mbcnt_hi_u32_b32 %4, %[a], %4\n\tv_mbcnt_hi_u32_b32 %5, %[a], %5\n\tv_mbcnt_hi_u32_b32 %6, %[a], %6\n\tv_mbcnt_hi_u32_b32 %7, %[a], %7\n\tv_mbcnt_hi_u32_b32 %0, %[a], %0\n\tv_mbcnt_hi_u32_b32 %1, %[a], %1\n\tv_mbcnt_hi_u32_b32 %2, %[a], %2\n\tv_mbcnt_hi_u32_b32 %3, %[a], %3\n\tv_mbcnt_hi_u32_b32 %4, %[a], %4\n\tv_mbcnt_hi_u32_b32 %5, %[a], %5\n\tv_mbcnt_hi_u32_b32 %6, %[a], %6\n\tv_mbcnt_hi_u32_b32 %7, %[a], %7\n\tv_mbcnt_hi_u32_b32 %0, %[a], %0\n\tv_mbcnt_hi_u32_b32 %1, %[a], %1\n\tv_mbcnt_hi_u32_b32 %2, %[a], %2\n\tv_mbcnt_hi_u32_b32 %3, %[a], %3\n\tv_mbcnt_hi_u32_b32 %4, %[a], %4\n\tv_mbcnt_hi_u32_b32 %5, %[a], %5\n\tv_mbcnt_hi_u32_b32 %6, %[a], %6\n\tv_mbcnt_hi_u32_b32 %7, %[a], %7" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6), "+v"(v7),
+                 [w0] "+v"(w0), [w1] "+v"(w1), [w2] "+v"(w2), [w3] "+v"(w3), [w4] "+v"(w4), [w5] "+v"(w5), [w6] "+v"(w6), [w7] "+v"(w7)
+                 : [a] "v"(a), [b] "v"(b), [sg] "s"(sg), [sm] "s"(sm), [wa] "v"(wa) : "vcc");
+  }
+  uint64_t t1 = clock64();
+  out[blockIdx.x*256+threadIdx.x] = v0^v1^v2^v3^v4^v5^v6^v7^(uint32_t)(w0^w1^w2^w3^w4^w5^w6^w7);
+  if (threadIdx.x == 0 && blockIdx.x == 0) clk[34] = t1 - t0;
+}
 int main() {
   const int blocks = 256 * 8;  // 8 waves per SIMD
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1); float ms[64];
@@ -533,8 +597,12 @@ int main() {
   hipLaunchKernelGGL(k28, dim3(blocks), dim3(256), 0, 0, out, clk, 7u); hipEventRecord(e0); hipLaunchKernelGGL(k28, dim3(blocks), dim3(256), 0, 0, out, clk, 7u); hipEventRecord(e1); hipEventSynchronize(e1); hipEventElapsedTime(&ms[28], e0, e1);
   hipLaunchKernelGGL(k29, dim3(blocks), dim3(256), 0, 0, out, clk, 7u); hipEventRecord(e0); hipLaunchKernelGGL(k29, dim3(blocks), dim3(256), 0, 0, out, clk, 7u); hipEventRecord(e1); hipEventSynchronize(e1); hipEventElapsedTime(&ms[29], e0, e1);
   hipLaunchKernelGGL(k30, dim3(blocks), dim3(256), 0, 0, out, clk, 7u); hipEventRecord(e0); hipLaunchKernelGGL(k30, dim3(blocks), dim3(256), 0, 0, out, clk, 7u); hipEventRecord(e1); hipEventSynchronize(e1); hipEventElapsedTime(&ms[30], e0, e1);
-  const char* names[] = {"bitop3_vvv", "alignbit_vvv", "alignbit_vvs", "alignbit_vvi", "add_co", "addc_co", "bcnt", "and_or", "or_vv", "lshrrev_vs", "add_vs", "lshl_add_u64", "lshrrev_vv", "lshrrev_vi", "xor_vi", "xor_vv", "add3", "lshl_add_u32", "bfe_vvv", "bcnt_vi", "cndmask_vcc", "cndmask_e64_s", "min_u32", "mul_hi_u32", "mul_u24", "mad_u64_u32", "cmp_lt_e32", "mov_dpp", "subrev_co", "mov_vv", "bitop3_vvi"};
-  for (int n = 0; n < 31; ++n)
+  hipLaunchKernelGGL(k31, dim3(blocks), dim3(256), 0, 0, out, clk, 7u); hipEventRecord(e0); hipLaunchKernelGGL(k31, dim3(blocks), dim3(256), 0, 0, out, clk, 7u); hipEventRecord(e1); hipEventSynchronize(e1); hipEventElapsedTime(&ms[31], e0, e1);
+  hipLaunchKernelGGL(k32, dim3(blocks), dim3(256), 0, 0, out, clk, 7u); hipEventRecord(e0); hipLaunchKernelGGL(k32, dim3(blocks), dim3(256), 0, 0, out, clk, 7u); hipEventRecord(e1); hipEventSynchronize(e1); hipEventElapsedTime(&ms[32], e0, e1);
+  hipLaunchKernelGGL(k33, dim3(blocks), dim3(256), 0, 0, out, clk, 7u); hipEventRecord(e0); hipLaunchKernelGGL(k33, dim3(blocks), dim3(256), 0, 0, out, clk, 7u); hipEventRecord(e1); hipEventSynchronize(e1); hipEventElapsedTime(&ms[33], e0, e1);
+  hipLaunchKernelGGL(k34, dim3(blocks), dim3(256), 0, 0, out, clk, 7u); hipEventRecord(e0); hipLaunchKernelGGL(k34, dim3(blocks), dim3(256), 0, 0, out, clk, 7u); hipEventRecord(e1); hipEventSynchronize(e1); hipEventElapsedTime(&ms[34], e0, e1);
+  const char* names[] = {"bitop3_vvv", "alignbit_vvv", "alignbit_vvs", "alignbit_vvi", "add_co", "addc_co", "bcnt", "and_or", "or_vv", "lshrrev_vs", "add_vs", "lshl_add_u64", "lshrrev_vv", "lshrrev_vi", "xor_vi", "xor_vv", "add3", "lshl_add_u32", "bfe_vvv", "bcnt_vi", "cndmask_vcc", "cndmask_e64_s", "min_u32", "mul_hi_u32", "mul_u24", "mad_u64_u32", "cmp_lt_e32", "mov_dpp", "subrev_co", "mov_vv", "bitop3_vvi", "sad_u8_vvv", "sad_u8_vsv", "mbcnt_lo", "mbcnt_hi"};
+  for (int n = 0; n < 35; ++n)
     printf("%-14s %.3f ms  %.2f cyc@2.4GHz per wave-instr per SIMD  (clock64 %.2f)\n", names[n], ms[n], ms[n] * 1e-3 * 2.4e9 / (4096 * 32.0 * 8.0), (double)clk[n] / (4096 * 32.0));
   return 0;
 }

@@ -36,6 +36,12 @@ FORMS = [
     ("subrev_co", "v_subrev_co_u32 {d}, vcc, {d}, %[a]"),
     ("mov_vv", "v_mov_b32 {d}, %[a]"),
     ("bitop3_vvi", "v_bitop3_b32 {d}, {d}, %[a], 5 bitop3:0xf1"),
+    # the q-gram filter and its scatter (k_ed_qg_filter / k_ed_qg_scatter): SAD accumulation chains, the
+    # SGPR-operand form, and the lane-prefix count of the entry scatter
+    ("sad_u8_vvv", "v_sad_u8 {d}, %[a], %[b], {d}"),
+    ("sad_u8_vsv", "v_sad_u8 {d}, %[a], %[sg], {d}"),
+    ("mbcnt_lo", "v_mbcnt_lo_u32_b32 {d}, %[a], {d}"),
+    ("mbcnt_hi", "v_mbcnt_hi_u32_b32 {d}, %[a], {d}"),
 ]
 ITERS = 4096
 out = ['#include <hip/hip_runtime.h>', '#include <cstdio>', '#include <cstdint>', f'#define ITERS {ITERS}']

@@ -15,7 +15,7 @@ import sys
 # leg -> [(kernel name prefix, key, unit, units per launch of the leg's default workload)]
 LEGS = {
     # the order-query kernel (default) and the per-decision sweep (NMZ_REPLAY_OQ=0 runs of the same leg)
-    "replayable": [("void nmz::k_replayable_sweep_wt<false>", "k_replayable_sweep_wt", "decision", 2**20 * 4096),
+    "replayable": [("void nmz::k_replayable_sweep_wt<false", "k_replayable_sweep_wt", "decision", 2**20 * 4096),
                    ("void nmz::k_replayable_sweep_oq<false, false>", "k_replayable_sweep_oq", "decision", 2**20 * 4096),
                    ("void nmz::k_replayable_sweep_fast", "k_replayable_sweep_fast", "decision", 2**20 * 4096)],
     "random": [("void nmz::k_random_sweep", "k_random_sweep", "decision", 10_000_000 * 10_000)],
