@@ -78,6 +78,10 @@ def main():
                         o = out[key]
                         o["ops_per_unit"] += e["SQ_INSTS_VALU"] * 64 / n
                         o["avg_ns"] += e["avg_ns"]
+                        if o.get("grbm") is not None and e.get("GRBM_GUI_ACTIVE") is not None:
+                            # the clock over all of the key's kernels, weighted by their time
+                            o["grbm"] += e["GRBM_GUI_ACTIVE"]
+                            o["clock_ghz"] = o["grbm"] / 8 / o["avg_ns"]
                         o["kernel"] += " + " + name
                         o["isa"][name] = kernel_isa.lookup(fps, name)
                         if o.get("hbm_bytes_per_launch") is not None and e.get("hbm_bytes_fetch_x2") is not None:
@@ -88,7 +92,7 @@ def main():
                                 "kernel": name, "avg_ns": e["avg_ns"],
                                 "source": f"SQ_INSTS_VALU per launch, profiles/{tag}_{leg}_summary.json",
                                 "hbm_bytes_per_launch": e.get("hbm_bytes_fetch_x2"),
-                                "clock_ghz": e.get("clock_ghz"),
+                                "clock_ghz": e.get("clock_ghz"), "grbm": e.get("GRBM_GUI_ACTIVE"),
                                 # fingerprints of the profiled kernels (tools/kernel_isa.py): bench.py marks the
                                 # entry stale when the shipped library's kernels differ
                                 "isa": {name: kernel_isa.lookup(fps, name)}}
