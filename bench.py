@@ -363,13 +363,14 @@ def bench_replayable(args, torch, D, ctx, L, stream):
         # consecutive traces sweep on two streams: trace i's top-k selection overlaps trace i + 1's sweep
         sws = [torch.cuda.current_stream(dev), torch.cuda.Stream(dev)]
 
+        seedset = [None]  # one prepared seed set (prefix hashes bucketed once) for every trace of the stream
+
         def sweep(i, p):
             with torch.cuda.stream(sws[i % 2]):
-                _lib.check(L.nmz_replayable_sweep_topk_dev(p, ctypes.c_void_p(d_soff[0].data_ptr()),
-                                                           ctypes.c_void_p(d_sb[0].data_ptr()), S, seed_lo[0], K_TOP,
-                                                           ctypes.c_void_p(sts[i % 2].data_ptr()),
-                                                           ctypes.c_void_p(tks[i % 2].data_ptr()),
-                                                           ctypes.c_void_p(sws[i % 2].cuda_stream)))
+                _lib.check(L.nmz_replayable_sweep_seeds_topk_dev(p, seedset[0], seed_lo[0], K_TOP,
+                                                                 ctypes.c_void_p(sts[i % 2].data_ptr()),
+                                                                 ctypes.c_void_p(tks[i % 2].data_ptr()),
+                                                                 ctypes.c_void_p(sws[i % 2].cuda_stream)))
                 tkh[i % 2].copy_(tks[i % 2], non_blocking=True)  # on the same stream, after the sweep
                 evs[i % 2].record()
 
@@ -378,10 +379,15 @@ def bench_replayable(args, torch, D, ctx, L, stream):
             heads.append(int(np.frombuffer(tkh[i % 2].numpy().tobytes(), dtype=_lib.TOPK_DTYPE)["seed"][0]))
             L.nmz_replayable_plan_destroy(p)
 
-        AHEAD = 2  # plan builds enqueued this many traces ahead (a producer thread measured slower: 0.23 ms/trace)
+        # plan builds enqueued this many traces ahead (a producer thread measured slower: 0.23 ms/trace)
+        AHEAD = int(os.environ.get("NMZ_BENCH_AHEAD", "2"))
 
         def run(n):
             heads, iter_s = [], []
+            ss = ctypes.c_void_p()
+            _lib.check(L.nmz_replayable_seeds_create(ctx.handle, ctypes.c_void_p(d_soff[0].data_ptr()),
+                                                     ctypes.c_void_p(d_sb[0].data_ptr()), S, 0, ctypes.byref(ss)))
+            seedset[0] = ss
             plans = {j: make(j) for j in range(min(AHEAD, n))}
             for i in range(n):
                 ti = time.perf_counter()
@@ -392,6 +398,7 @@ def bench_replayable(args, torch, D, ctx, L, stream):
                     finish(i - 1, plans.pop(i - 1), heads)
                 iter_s.append(time.perf_counter() - ti)
             finish(n - 1, plans.pop(n - 1), heads)
+            L.nmz_replayable_seeds_destroy(ss)
             return heads, iter_s
 
         run(min(T, 6))  # each context's pooled buffers and pinned staging for its live plans
@@ -938,9 +945,10 @@ def headline_line(args, torch, D, ctx, L, stream):
             "top1_head": p["top1"], "agrees_with_one_at_a_time": p["agrees"],
             "iter_ms_median": p["iter_ms_median"], "iter_ms_max": p["iter_ms_max"],
             "what": "every trace gets its own plan (nmz_replayable_plan_create_async from host hints, inside the "
-                    "timing), one 2^20-seed sweep with top-64 and the top-64 on the host; one host thread enqueues "
-                    "trace i+2's plan build (two contexts) while trace i sweeps (two streams); whole elapsed time / "
-                    "traces. plan_ms: one plan built alone (one_at_a_time)",
+                    "timing), one 2^20-seed sweep with top-64 and the top-64 on the host; the seeds' prefix hashes "
+                    "are prepared once for the stream (nmz_replayable_seeds_create, inside the timing); one host "
+                    "thread enqueues trace i+2's plan build (two contexts) while trace i sweeps (two streams); whole "
+                    "elapsed time / traces. plan_ms: one plan built alone (one_at_a_time)",
             "one_at_a_time": one}
     else:
         line["end_to_end"] = dict(one, mode="one_at_a_time")

@@ -195,6 +195,19 @@ int nmz_replayable_plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uin
 int nmz_replayable_plan_create_async(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hint_bytes,
                                      uint32_t n_events, int64_t max_interval_ns, uint64_t max_seeds,
                                      nmz_replayable_plan **out);
+/* A prepared seed set for sweeping one set of seeds over many traces' plans: the seeds' prefix hashes (FNV of the
+ * seed bytes), bucketed by table row once, instead of per sweep. d_seed_off / d_seed_bytes: device CSR of the seed
+ * strings, or d_seed_off == NULL: the decimal strings of dec_lo .. dec_lo + n_seeds - 1. Synchronous; the set may be
+ * swept through any plan on the same device and stream (results identical to nmz_replayable_sweep_topk_dev and
+ * nmz_replayable_sweep_decimal_topk_dev over the same seeds). Destroy waits for the device. */
+typedef struct nmz_replayable_seeds nmz_replayable_seeds;
+int nmz_replayable_seeds_create(nmz_ctx *ctx, const uint32_t *d_seed_off, const uint8_t *d_seed_bytes,
+                                uint64_t n_seeds, uint64_t dec_lo, nmz_replayable_seeds **out);
+int nmz_replayable_seeds_destroy(nmz_replayable_seeds *seeds);
+/* nmz_replayable_sweep_topk_dev over a prepared seed set: stats for every seed of the set, and (k > 0) the top-k
+ * with seed = seed0 + the seed's index. */
+int nmz_replayable_sweep_seeds_topk_dev(nmz_replayable_plan *plan, const nmz_replayable_seeds *seeds, uint64_t seed0,
+                                        uint32_t k, nmz_sched_stats *d_stats, nmz_topk_entry *d_topk, void *stream);
 /* Waits for the plan's build and for the sweeps enqueued through it (not for the device or other streams). */
 int nmz_replayable_plan_destroy(nmz_replayable_plan *plan);
 /* Which statistics kernel the plan's sweeps take (diagnostic): 2 = wavelet-tree statistics (k_replayable_sweep_wt,

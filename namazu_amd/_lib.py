@@ -70,6 +70,9 @@ SIGNATURES = {
     "nmz_replayable_sweep": (_int, [_P, _P, _P, _u64, _P, _P, _u32, _i64, _P, _P, _u64, _u32, _P]),
     "nmz_replayable_plan_create": (_int, [_P, _P, _P, _u32, _i64, _u64, ctypes.POINTER(_P)]),
     "nmz_replayable_plan_create_async": (_int, [_P, _P, _P, _u32, _i64, _u64, ctypes.POINTER(_P)]),
+    "nmz_replayable_seeds_create": (_int, [_P, _P, _P, _u64, _u64, ctypes.POINTER(_P)]),
+    "nmz_replayable_seeds_destroy": (_int, [_P]),
+    "nmz_replayable_sweep_seeds_topk_dev": (_int, [_P, _P, _u64, _u32, _P, _P, _P]),
     "nmz_replayable_plan_destroy": (_int, [_P]),
     "nmz_replayable_plan_kernel": (_int, [_P]),
     "nmz_replayable_sweep_dev": (_int, [_P, _P, _P, _u64, _P, _P]),

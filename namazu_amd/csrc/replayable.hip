@@ -1529,9 +1529,24 @@ static bool wt_topk_enabled() {
     return on;
 }
 
+}  // namespace nmz
+
+// A prepared seed set (nmz_replayable_seeds_create): the seeds' prefix hashes, bucketed by row at the statistics
+// kernels' granularity, and the row histogram (the per-decision sweeps bucket the hashes again at theirs)
+struct nmz_replayable_seeds {
+    nmz_ctx *ctx = nullptr;
+    uint64_t S = 0;
+    nmz::DevBuf mem;
+    nmz::SeedScratch sc{};
+    uint32_t *hist = nullptr;  // [256 * BUCKET_STRIDE] the prefix kernel's row counts
+};
+
+namespace nmz {
+
 static int replayable_stats(nmz_replayable_plan *p, hipStream_t st, const uint32_t *d_soff,
                             const uint8_t *d_sbytes, uint64_t S, nmz_sched_stats *d_stats, uint64_t dec_lo = 0,
-                            void *wt_topk_scratch = nullptr, uint32_t k = 0) {
+                            void *wt_topk_scratch = nullptr, uint32_t k = 0,
+                            const nmz_replayable_seeds *pre = nullptr) {
     if (S == 0) return NMZ_OK;
     const uint32_t E = p->n_events;
     if (E == 0 || p->mod.kind == MOD_ZERO) {
@@ -1539,23 +1554,35 @@ static int replayable_stats(nmz_replayable_plan *p, hipStream_t st, const uint32
         NMZ_HIP(hipGetLastError());
         return NMZ_OK;
     }
-    NMZ_CHECK(S <= p->max_seeds, "more seeds than the plan was created for");
-    SeedScratch sc = carve_seed_scratch(p->seed_scratch.ptr, p->max_seeds);
-    if (d_soff)
-        hipLaunchKernelGGL(k_seed_prefix, dim3(ceil_div(S, 256 * prefix_per_thread())), dim3(256), 0, st, d_soff,
-                           d_sbytes, S, sc.h0, sc.b.count, prefix_per_thread());
-    else
-        hipLaunchKernelGGL(k_seed_prefix_decimal, dim3(ceil_div(S, 256 * prefix_per_thread())), dim3(256), 0, st,
-                           dec_lo, S, sc.h0, sc.b.count, prefix_per_thread());
+    const bool stats_kernel = use_wt(p) || (p->oq && (replay_oq_enabled() || p->mod.kind != MOD_FAST));
+    SeedScratch sc;
+    if (pre && stats_kernel) {
+        sc = pre->sc;  // bucketed already
+    } else {
+        NMZ_CHECK(S <= p->max_seeds, "more seeds than the plan was created for");
+        sc = carve_seed_scratch(p->seed_scratch.ptr, p->max_seeds);
+        if (pre) {  // a per-decision sweep of prepared seeds: their hashes and row counts, bucketed here
+            NMZ_HIP(hipMemcpyAsync(sc.b.count, pre->hist, 256 * BUCKET_STRIDE * sizeof(uint32_t),
+                                   hipMemcpyDeviceToDevice, st));
+            sc.h0 = pre->sc.h0;
+        } else if (d_soff) {
+            hipLaunchKernelGGL(k_seed_prefix, dim3(ceil_div(S, 256 * prefix_per_thread())), dim3(256), 0, st, d_soff,
+                               d_sbytes, S, sc.h0, sc.b.count, prefix_per_thread());
+        } else {
+            hipLaunchKernelGGL(k_seed_prefix_decimal, dim3(ceil_div(S, 256 * prefix_per_thread())), dim3(256), 0, st,
+                               dec_lo, S, sc.h0, sc.b.count, prefix_per_thread());
+        }
+    }
+    const bool bucketed = pre && stats_kernel;
     const int U = replay_u();
     const uint32_t per_unit = 64u * (uint32_t)U;
     const uint64_t max_units = S / per_unit + 256;
     if (use_wt(p)) {
-        NMZ_TRY(bucket_seeds_counted(st, sc.h0, S, OQ_WG, sc.b, sc.counter));
+        if (!bucketed) NMZ_TRY(bucket_seeds_counted(st, sc.h0, S, OQ_WG, sc.b, sc.counter));
         return wt_sweep(p->wt, p->ctx, st, sc.b, p->d_table, E, p->mod, d_stats, S, wt_topk_scratch, k);
     }
     if (p->oq && (replay_oq_enabled() || p->mod.kind != MOD_FAST)) {
-        NMZ_TRY(bucket_seeds_counted(st, sc.h0, S, OQ_WG, sc.b, sc.counter));
+        if (!bucketed) NMZ_TRY(bucket_seeds_counted(st, sc.h0, S, OQ_WG, sc.b, sc.counter));
         KernelTimer kt(p->ctx, st, "replayable_sweep");
         unsigned long long *span = kt.span();
         const bool big = p->mod.m32 >= 0x80000000u;
@@ -1619,11 +1646,12 @@ static int replayable_stats(nmz_replayable_plan *p, hipStream_t st, const uint32
 // 21 + 29 us for k_replayable_merge + k_topk_chunk at 2^20 seeds, so the levels stay separate.)
 static int replayable_run_on(nmz_replayable_plan *p, hipStream_t st, const uint32_t *d_soff, const uint8_t *d_sbytes,
                              uint64_t S, nmz_sched_stats *d_stats, uint64_t seed0, uint32_t k, nmz_topk_entry *d_topk,
-                             uint64_t dec_lo);
+                             uint64_t dec_lo, const nmz_replayable_seeds *pre);
 
 static int replayable_run(nmz_replayable_plan *p, hipStream_t st, const uint32_t *d_soff, const uint8_t *d_sbytes,
                           uint64_t S, nmz_sched_stats *d_stats, uint64_t seed0 = 0, uint32_t k = 0,
-                          nmz_topk_entry *d_topk = nullptr, uint64_t dec_lo = 0) {
+                          nmz_topk_entry *d_topk = nullptr, uint64_t dec_lo = 0,
+                          const nmz_replayable_seeds *pre = nullptr) {
     nmz_replayable_plan::Use *u = nullptr;
     for (auto &x : p->uses)
         if (x.st == st) u = &x;
@@ -1634,7 +1662,7 @@ static int replayable_run(nmz_replayable_plan *p, hipStream_t st, const uint32_t
         u = &p->uses.back();
         if (p->built && st != p->ctx->stream) NMZ_HIP(hipStreamWaitEvent(st, p->built, 0));
     }
-    const int rc = replayable_run_on(p, st, d_soff, d_sbytes, S, d_stats, seed0, k, d_topk, dec_lo);
+    const int rc = replayable_run_on(p, st, d_soff, d_sbytes, S, d_stats, seed0, k, d_topk, dec_lo, pre);
     NMZ_HIP(hipEventRecord(u->ev, st));
     return rc;
 }
@@ -1657,7 +1685,7 @@ static void plan_wait_uses(nmz_replayable_plan *p) {
 
 static int replayable_run_on(nmz_replayable_plan *p, hipStream_t st, const uint32_t *d_soff, const uint8_t *d_sbytes,
                              uint64_t S, nmz_sched_stats *d_stats, uint64_t seed0, uint32_t k, nmz_topk_entry *d_topk,
-                             uint64_t dec_lo) {
+                             uint64_t dec_lo, const nmz_replayable_seeds *pre) {
     NMZ_CHECK(k <= 256, "top-k supports k <= 256");
     NMZ_CHECK(k == 0 || d_topk, "d_topk is NULL");
     // the wavelet-tree sweep's own candidates (k <= 64; more than one general-selection list, so that the gated
@@ -1666,10 +1694,11 @@ static int replayable_run_on(nmz_replayable_plan *p, hipStream_t st, const uint3
     if (fused) {
         NMZ_TRY(p->wt_topk.ensure(wt_topk_scratch_bytes(S)));  // the sweep zeroes its candidate counter
     }
-    NMZ_TRY(replayable_stats(p, st, d_soff, d_sbytes, S, d_stats, dec_lo, fused ? p->wt_topk.ptr : nullptr, k));
-    if (fused) {
-        const SeedScratch sc = carve_seed_scratch(p->seed_scratch.ptr, p->max_seeds);
-        return wt_topk(st, p->wt_topk.ptr, sc.b.sorted_idx, S, seed0, k, d_topk);
+    NMZ_TRY(replayable_stats(p, st, d_soff, d_sbytes, S, d_stats, dec_lo, fused ? p->wt_topk.ptr : nullptr, k, pre));
+    if (fused) {  // the seeds' order of the sweep that ran (the prepared set's, or this plan's own bucketing)
+        const uint32_t *sidx = pre ? pre->sc.b.sorted_idx
+                                   : carve_seed_scratch(p->seed_scratch.ptr, p->max_seeds).b.sorted_idx;
+        return wt_topk(st, p->wt_topk.ptr, sidx, S, seed0, k, d_topk);
     }
     if (k) {
         NMZ_TRY(p->topk_lists.ensure(topk_scratch_entries(S, k) * sizeof(nmz_topk_entry)));
@@ -1931,6 +1960,72 @@ int nmz_replayable_sweep_topk_dev(nmz_replayable_plan *plan, const uint32_t *d_s
     NMZ_TRY(g.rc);
     hipStream_t st = stream ? (hipStream_t)stream : plan->ctx->stream;
     return replayable_run(plan, st, d_seed_off, d_seed_bytes, n_seeds, d_stats, seed0, k, d_topk);
+}
+
+int nmz_replayable_seeds_create(nmz_ctx *ctx, const uint32_t *d_seed_off, const uint8_t *d_seed_bytes, uint64_t n_seeds,
+                                uint64_t dec_lo, nmz_replayable_seeds **out) {
+    NMZ_CHECK(ctx != nullptr && out != nullptr, "NULL argument");
+    NMZ_CHECK(n_seeds >= 1 && n_seeds < (1ULL << 32), "1 <= n_seeds < 2^32");
+    NMZ_CHECK(!d_seed_off || d_seed_bytes, "d_seed_bytes is NULL");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    *out = nullptr;
+    auto *s = new nmz_replayable_seeds();
+    s->ctx = ctx;
+    s->S = n_seeds;
+    s->mem.pool = &ctx->pool;  // a stream of seed sets of one size reuses one buffer (no hipMalloc per set)
+    hipStream_t st = ctx->stream;
+    const int rc = s->mem.ensure(seed_scratch_bytes(n_seeds) + Carve::bytes_for(256 * BUCKET_STRIDE, 4));
+    if (rc != NMZ_OK) {
+        delete s;
+        return rc;
+    }
+    s->sc = carve_seed_scratch(s->mem.ptr, n_seeds);
+    s->hist = reinterpret_cast<uint32_t *>(static_cast<char *>(s->mem.ptr) + seed_scratch_bytes(n_seeds));
+    auto fail_hip = [&]() {
+        (void)hipStreamSynchronize(st);
+        s->mem.release();
+        delete s;
+        return fail(NMZ_EHIP, "seed set build failed");
+    };
+    if (hipMemsetAsync(s->sc.b.count, 0, 256 * BUCKET_STRIDE * sizeof(uint32_t), st) != hipSuccess ||
+        hipMemsetAsync(s->sc.counter, 0, 4 * sizeof(uint32_t), st) != hipSuccess)
+        return fail_hip();
+    if (d_seed_off)
+        hipLaunchKernelGGL(k_seed_prefix, dim3(ceil_div(n_seeds, 256 * prefix_per_thread())), dim3(256), 0, st,
+                           d_seed_off, d_seed_bytes, n_seeds, s->sc.h0, s->sc.b.count, prefix_per_thread());
+    else
+        hipLaunchKernelGGL(k_seed_prefix_decimal, dim3(ceil_div(n_seeds, 256 * prefix_per_thread())), dim3(256), 0,
+                           st, dec_lo, n_seeds, s->sc.h0, s->sc.b.count, prefix_per_thread());
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(s->hist, s->sc.b.count, 256 * BUCKET_STRIDE * sizeof(uint32_t), hipMemcpyDeviceToDevice, st) !=
+            hipSuccess ||
+        bucket_seeds_counted(st, s->sc.h0, n_seeds, OQ_WG, s->sc.b, s->sc.counter) != NMZ_OK ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return fail_hip();
+    *out = s;
+    return NMZ_OK;
+}
+
+int nmz_replayable_seeds_destroy(nmz_replayable_seeds *seeds) {
+    if (!seeds) return NMZ_OK;
+    {
+        CtxGuard g(seeds->ctx);
+        (void)hipDeviceSynchronize();  // sweeps on any stream may still read the set (its buffer goes to the pool)
+        seeds->mem.release();
+    }
+    delete seeds;
+    return NMZ_OK;
+}
+
+int nmz_replayable_sweep_seeds_topk_dev(nmz_replayable_plan *plan, const nmz_replayable_seeds *seeds, uint64_t seed0,
+                                        uint32_t k, nmz_sched_stats *d_stats, nmz_topk_entry *d_topk, void *stream) {
+    NMZ_CHECK(plan != nullptr && seeds != nullptr, "NULL argument");
+    NMZ_CHECK(seeds->ctx->device == plan->ctx->device, "the seed set and the plan are on different devices");
+    CtxGuard g(plan->ctx);
+    NMZ_TRY(g.rc);
+    hipStream_t st = stream ? (hipStream_t)stream : plan->ctx->stream;
+    return replayable_run(plan, st, nullptr, nullptr, seeds->S, d_stats, seed0, k, d_topk, 0, seeds);
 }
 
 int nmz_replayable_sweep_decimal_topk_dev(nmz_replayable_plan *plan, uint64_t seed_lo, uint64_t n_seeds, uint32_t k,

@@ -352,6 +352,75 @@ def test_replayable_topk_large_sweep(ctx, E, m, k):
     assert tk.tolist() == O.topk_from_stats(st, 10**12, k).tolist()
 
 
+@pytest.mark.parametrize("kind", ["csr", "decimal"])
+def test_replayable_seed_set(ctx, monkeypatch, kind):
+    """nmz_replayable_sweep_seeds_topk_dev over one prepared seed set (prefix hashes bucketed once) == the plain
+    sweep of the same seeds, on every statistics path: wavelet trees (fused and separate plan builds), order
+    queries, and the per-decision sweeps (maxInterval >= 2^32: the prepared hashes bucketed per sweep), stats and
+    top-k, with several plans sweeping the one set; more seeds than a plan was created for take the set's buckets."""
+    import torch
+    L = _lib.load()
+    S, k = 3000, 16
+    seeds = [str(i * 7) for i in range(S)] if kind == "csr" else None
+    d_so = d_sb = None
+    if kind == "csr":
+        so, sb = to_csr(seeds)
+        d_so = torch.from_numpy(so.view(np.int32)).cuda()
+        d_sb = torch.from_numpy(sb).cuda()
+    dec_lo = 10**9
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    ss = ctypes.c_void_p()
+    _lib.check(L.nmz_replayable_seeds_create(ctx.handle, ctypes.c_void_p(d_so.data_ptr() if d_so is not None else 0),
+                                             ctypes.c_void_p(d_sb.data_ptr() if d_sb is not None else 0), S, dec_lo,
+                                             ctypes.byref(ss)))
+    try:
+        cases = [("wt", 100_000_000, S), ("wt_sep", 100_000_000, S), ("oq", 7, S), ("fast", 2**32 + 5, S),
+                 ("wt", 2**31 + 3, 1000)]
+        for path, m, max_seeds in cases:
+            monkeypatch.delenv("NMZ_REPLAY_WT", raising=False)
+            monkeypatch.delenv("NMZ_WT_FUSED", raising=False)
+            if path == "oq":
+                monkeypatch.setenv("NMZ_REPLAY_WT", "0")
+            if path == "wt_sep":
+                monkeypatch.setenv("NMZ_WT_FUSED", "0")
+            hints = zk_hints(257)
+            ho, hb = to_csr(hints)
+            plan = ctypes.c_void_p()
+            _lib.check(L.nmz_replayable_plan_create(ctx.handle, _lib.ptr(ho), _lib.ptr(hb), len(hints), m, max_seeds,
+                                                    ctypes.byref(plan)))
+            outs = []
+            for use_set in ((True, False) if max_seeds >= S else (True,)):
+                d_st = torch.zeros(S * 32, dtype=torch.uint8, device="cuda")
+                d_tk = torch.zeros(k * 24, dtype=torch.uint8, device="cuda")
+                if use_set:
+                    _lib.check(L.nmz_replayable_sweep_seeds_topk_dev(plan, ss, 5, k, ctypes.c_void_p(d_st.data_ptr()),
+                                                                     ctypes.c_void_p(d_tk.data_ptr()), stream))
+                elif kind == "csr":
+                    _lib.check(L.nmz_replayable_sweep_topk_dev(plan, ctypes.c_void_p(d_so.data_ptr()),
+                                                               ctypes.c_void_p(d_sb.data_ptr()), S, 5, k,
+                                                               ctypes.c_void_p(d_st.data_ptr()),
+                                                               ctypes.c_void_p(d_tk.data_ptr()), stream))
+                else:
+                    _lib.check(L.nmz_replayable_sweep_decimal_topk_dev(plan, dec_lo, S, k,
+                                                                       ctypes.c_void_p(d_st.data_ptr()),
+                                                                       ctypes.c_void_p(d_tk.data_ptr()), stream))
+                torch.cuda.synchronize()
+                outs.append((d_st.cpu().numpy().copy(), d_tk.cpu().numpy().copy()))
+            L.nmz_replayable_plan_destroy(plan)
+            if len(outs) == 2:
+                assert np.array_equal(outs[0][0], outs[1][0]), (path, m)
+                if kind == "csr":  # the decimal sweep numbers its top-k seeds from dec_lo, the set's from seed0
+                    assert np.array_equal(outs[0][1], outs[1][1]), (path, m)
+            st = np.frombuffer(outs[0][0].tobytes(), dtype=_lib.SCHED_STATS_DTYPE)
+            tk = np.frombuffer(outs[0][1].tobytes(), dtype=_lib.TOPK_DTYPE)
+            assert tk.tolist() == O.topk_from_stats(st, 5, k).tolist()
+            if kind == "csr" and path in ("wt", "oq", "fast"):
+                ref, _ = rep_oracle(seeds, hints, m)
+                assert np.array_equal(st, ref)
+    finally:
+        L.nmz_replayable_seeds_destroy(ss)
+
+
 def test_replayable_plan_create_async(ctx):
     """nmz_replayable_plan_create_async: builds enqueued on two contexts' streams, sweeps enqueued at once on
     another stream (which must wait for each build on the device), plans of several shapes (the one-launch
