@@ -413,10 +413,37 @@ def bench_replayable(args, torch, D, ctx, L, stream):
                         agrees=heads == e2e_heads, iter_ms_median=float(np.median(iter_s)) * 1e3,
                         iter_ms_max=float(np.max(iter_s)) * 1e3, iter_max_at=int(np.argmax(iter_s)))
         ctx2.close()
+    # the same stream of traces through the native batch entry point (nmz_replayable_sweep_traces: the pipeline
+    # above inside the library, one call for all traces; a Go caller's form)
+    e2e_native = None
+    if args.e2e_traces >= 2:
+        T = len(e2e_hints)
+        offs = (ctypes.c_void_p * T)(*[ctypes.c_void_p(ho.ctypes.data) for ho, _ in e2e_hints])
+        byts = (ctypes.c_void_p * T)(*[ctypes.c_void_p(hbb.ctypes.data) for _, hbb in e2e_hints])
+        nev = np.full(T, E, np.uint32)
+        out = np.zeros(T * K_TOP, _lib.TOPK_DTYPE)
+
+        def batch():
+            _lib.check(L.nmz_replayable_sweep_traces(ctx.handle, T, offs, byts, host_ptr(nev), MAX_INTERVAL_NS,
+                                                     seed_lo[0], S, K_TOP, host_ptr(out)))
+
+        batch()  # first call: the helper context, streams and pooled buffers
+        torch.cuda.synchronize()
+        ms = []
+        for _ in range(3):
+            gc.collect()
+            gc.disable()
+            t0 = time.perf_counter()
+            batch()
+            ms.append((time.perf_counter() - t0) * 1e3 / T)
+            gc.enable()
+        heads = [int(x) for x in out["seed"][::K_TOP]]
+        e2e_native = dict(traces=T, ms_per_trace=float(np.median(ms)), ms_per_trace_runs=ms, top1=heads[:4],
+                          agrees=heads == e2e_heads)
     return dict(S=S, E=E, hints=(hoff, hb), seeds=csr[0], elapsed=el_max,
                 kern_ms=kern_ms_span if kern_ms_span is not None else kern_ms_timed, kern_ms_events=kern_ms_timed,
                 kern_ms_span=kern_ms_span, kern_ms_isolated=kern_ms, plan_ms=plan_ms, stats=stats, topk=merged, pipeline=NP,
-                e2e_s=e2e, e2e_plan_s=e2e_plan, e2e_pipe=e2e_pipe, k1_kernel=k1)
+                e2e_s=e2e, e2e_plan_s=e2e_plan, e2e_pipe=e2e_pipe, e2e_native=e2e_native, k1_kernel=k1)
 
 
 def cpu_baseline_replayable(r, args):
@@ -936,19 +963,23 @@ def headline_line(args, torch, D, ctx, L, stream):
            "plan_ms": float(np.median(r["e2e_plan_s"])) * 1e3,
            "what": "per trace, one at a time: nmz_replayable_plan_create from host hints (table, sorts and wavelet "
                    "trees: one plan kernel) + one 2^20-seed sweep with top-64 + top-64 copy to the host"}
-    p = r.get("e2e_pipe")
-    if p:
-        # a stream of traces (how a sweep tool over many recorded traces runs): the throughput figure
+    p, nat = r.get("e2e_pipe"), r.get("e2e_native")
+    if p and nat:
+        # a stream of traces (how a sweep tool over many recorded traces runs): the throughput figure, through the
+        # native batch entry point; the same pipeline driven from Python and the one-at-a-time latency inside
         line["end_to_end"] = {
-            "value": dec_launch / (p["ms_per_trace"] * 1e-3), "unit": "decisions/s", "mode": "stream",
-            "ms_per_trace": p["ms_per_trace"], "traces": p["traces"], "plan_ms": one["plan_ms"],
-            "top1_head": p["top1"], "agrees_with_one_at_a_time": p["agrees"],
-            "iter_ms_median": p["iter_ms_median"], "iter_ms_max": p["iter_ms_max"],
-            "what": "every trace gets its own plan (nmz_replayable_plan_create_async from host hints, inside the "
-                    "timing), one 2^20-seed sweep with top-64 and the top-64 on the host; the seeds' prefix hashes "
-                    "are prepared once for the stream (nmz_replayable_seeds_create, inside the timing); one host "
-                    "thread enqueues trace i+2's plan build (two contexts) while trace i sweeps (two streams); whole "
-                    "elapsed time / traces. plan_ms: one plan built alone (one_at_a_time)",
+            "value": dec_launch / (nat["ms_per_trace"] * 1e-3), "unit": "decisions/s", "mode": "stream",
+            "ms_per_trace": nat["ms_per_trace"], "ms_per_trace_runs": nat["ms_per_trace_runs"], "traces": nat["traces"],
+            "plan_ms": one["plan_ms"], "top1_head": nat["top1"], "agrees_with_one_at_a_time": nat["agrees"],
+            "what": "nmz_replayable_sweep_traces over 17 traces: every trace gets its own plan (built from host hints "
+                    "inside the timing, one plan kernel), one 2^20-seed sweep and its top-64 on the host; the "
+                    "seeds' prefix hashes are prepared once per call; trace i+2's plan builds while trace i sweeps. "
+                    "ms_per_trace = one call's elapsed time / traces (median of 3 calls). plan_ms: one plan built "
+                    "alone (one_at_a_time)",
+            "python_stream": {"value": dec_launch / (p["ms_per_trace"] * 1e-3), "ms_per_trace": p["ms_per_trace"],
+                              "agrees_with_one_at_a_time": p["agrees"],
+                              "what": "the same pipeline driven from Python (nmz_replayable_plan_create_async, "
+                                      "nmz_replayable_seeds_create, nmz_replayable_sweep_seeds_topk_dev)"},
             "one_at_a_time": one}
     else:
         line["end_to_end"] = dict(one, mode="one_at_a_time")

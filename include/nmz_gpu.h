@@ -208,6 +208,15 @@ int nmz_replayable_seeds_destroy(nmz_replayable_seeds *seeds);
  * with seed = seed0 + the seed's index. */
 int nmz_replayable_sweep_seeds_topk_dev(nmz_replayable_plan *plan, const nmz_replayable_seeds *seeds, uint64_t seed0,
                                         uint32_t k, nmz_sched_stats *d_stats, nmz_topk_entry *d_topk, void *stream);
+/* A batch of recorded traces over one decimal seed range (the reference seeds "lo" .. "lo + n - 1",
+ * replayablepolicy.go:74-87): for every trace t (hint CSR hint_off[t] / hint_bytes[t], n_events[t] hints) its own
+ * plan, the sweep of all n_seeds seeds and the top-k failure candidates into topk[t * k .. t * k + k) (as
+ * nmz_replayable_sweep_decimal_topk_dev). Pipelined inside: the seeds are prepared once, trace t + 2's plan builds
+ * while trace t sweeps (on a private second context the call opens on first use), top-k lists come back while
+ * the next trace sweeps. Host arrays only; synchronous. 1 <= k <= 256. */
+int nmz_replayable_sweep_traces(nmz_ctx *ctx, uint32_t n_traces, const uint32_t *const *hint_off,
+                                const uint8_t *const *hint_bytes, const uint32_t *n_events, int64_t max_interval_ns,
+                                uint64_t seed_lo, uint64_t n_seeds, uint32_t k, nmz_topk_entry *topk);
 /* Waits for the plan's build and for the sweeps enqueued through it (not for the device or other streams). */
 int nmz_replayable_plan_destroy(nmz_replayable_plan *plan);
 /* Which statistics kernel the plan's sweeps take (diagnostic): 2 = wavelet-tree statistics (k_replayable_sweep_wt,

@@ -73,6 +73,7 @@ SIGNATURES = {
     "nmz_replayable_seeds_create": (_int, [_P, _P, _P, _u64, _u64, ctypes.POINTER(_P)]),
     "nmz_replayable_seeds_destroy": (_int, [_P]),
     "nmz_replayable_sweep_seeds_topk_dev": (_int, [_P, _P, _u64, _u32, _P, _P, _P]),
+    "nmz_replayable_sweep_traces": (_int, [_P, _u32, _P, _P, _P, _i64, _u64, _u64, _u32, _P]),
     "nmz_replayable_plan_destroy": (_int, [_P]),
     "nmz_replayable_plan_kernel": (_int, [_P]),
     "nmz_replayable_sweep_dev": (_int, [_P, _P, _P, _u64, _P, _P]),

@@ -87,6 +87,12 @@ struct nmz_ctx {
     std::vector<nmz::DevBuf> pool;  // free plan buffers (DevBuf::pool), freed by nmz_close
     nmz::HostPin pin[2];             // pinned staging of plan inputs ([0] replayable plan, [1] its wavelet classes)
     bool wt_lds_attr = false;        // the wavelet-tree kernels' LDS attribute is set on this context's device
+    // nmz_replayable_sweep_traces: a private second context (the other half of the plan builds), two sweep streams
+    // with an event each, and pinned staging for the top-k lists; created on first use
+    nmz_ctx *helper = nullptr;
+    hipStream_t sweep_st[2] = {nullptr, nullptr};
+    hipEvent_t sweep_ev[3] = {nullptr, nullptr, nullptr};
+    nmz::HostPin tkpin;
     NmzTiming timing;
 };
 

@@ -343,8 +343,17 @@ int nmz_open(int device, nmz_ctx **out) {
 
 int nmz_close(nmz_ctx *ctx) {
     if (!ctx) return NMZ_OK;
+    if (ctx->helper) {
+        (void)nmz_close(ctx->helper);
+        ctx->helper = nullptr;
+    }
     {
         CtxGuard g(ctx);
+        for (int i = 0; i < 2; ++i)
+            if (ctx->sweep_st[i]) (void)hipStreamDestroy(ctx->sweep_st[i]);
+        for (int i = 0; i < 3; ++i)
+            if (ctx->sweep_ev[i]) (void)hipEventDestroy(ctx->sweep_ev[i]);
+        ctx->tkpin.release();
         for (auto &b : ctx->buf) b.release();
         for (auto &b : ctx->pin) b.release();
         for (auto &b : ctx->pool) (void)hipFree(b.ptr);

@@ -1707,6 +1707,22 @@ static int replayable_run_on(nmz_replayable_plan *p, hipStream_t st, const uint3
     return NMZ_OK;
 }
 
+// the caller holds the plan's context: the buffers go back to the context's pool, where the next plan may write
+// them at once, so wait for the work still reading them -- the build and the sweeps on every stream the plan was
+// used on
+static void plan_destroy_locked(nmz_replayable_plan *plan) {
+    plan_wait_uses(plan);
+    plan->plan_mem.release();
+    plan->seed_scratch.release();
+    plan->partial.release();
+    plan->topk_lists.release();
+    plan->oq_mem.release();
+    plan->wt.mem.release();
+    plan->wt.aux.release();
+    plan->wt_topk.release();
+    delete plan;
+}
+
 static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hint_bytes, uint32_t E,
                        int64_t max_interval, uint64_t max_seeds, nmz_replayable_plan **out, bool async = false) {
     NMZ_CHECK(ctx && out, "NULL argument");
@@ -1889,86 +1905,9 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
     return NMZ_OK;
 }
 
-}  // namespace nmz
-
-using namespace nmz;
-
-extern "C" {
-#ifdef OQ_TRACE
-int nmz_debug_oq_trace(unsigned long long *out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(nmz::g_oq_trace), sizeof(nmz::g_oq_trace)) == hipSuccess ? 0 : -1;
-}
-#endif
-
-int nmz_replayable_plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hint_bytes,
-                               uint32_t n_events, int64_t max_interval_ns, uint64_t max_seeds,
-                               nmz_replayable_plan **out) {
-    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
-    CtxGuard g(ctx);
-    NMZ_TRY(g.rc);
-    return plan_create(ctx, hint_off, hint_bytes, n_events, max_interval_ns, max_seeds, out);
-}
-
-int nmz_replayable_plan_create_async(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hint_bytes,
-                                     uint32_t n_events, int64_t max_interval_ns, uint64_t max_seeds,
-                                     nmz_replayable_plan **out) {
-    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
-    CtxGuard g(ctx);
-    NMZ_TRY(g.rc);
-    return plan_create(ctx, hint_off, hint_bytes, n_events, max_interval_ns, max_seeds, out, true);
-}
-
-int nmz_replayable_plan_destroy(nmz_replayable_plan *plan) {
-    if (!plan) return NMZ_OK;
-    {
-        CtxGuard g(plan->ctx);
-        // the buffers go back to the context's pool, where the next plan may write them at once: wait for the
-        // work still reading them -- the sweeps on every stream the plan was used on, and the context's stream
-        plan_wait_uses(plan);
-        plan->plan_mem.release();
-        plan->seed_scratch.release();
-        plan->partial.release();
-        plan->topk_lists.release();
-        plan->oq_mem.release();
-        plan->wt.mem.release();
-        plan->wt.aux.release();
-        plan->wt_topk.release();
-    }
-    delete plan;
-    return NMZ_OK;
-}
-
-int nmz_replayable_plan_kernel(const nmz_replayable_plan *plan) {
-    if (!plan) return -1;
-    return plan->wt.on ? 2 : plan->oq ? 1 : 0;
-}
-
-int nmz_replayable_sweep_dev(nmz_replayable_plan *plan, const uint32_t *d_seed_off, const uint8_t *d_seed_bytes,
-                             uint64_t n_seeds, nmz_sched_stats *d_stats, void *stream) {
-    NMZ_CHECK(plan != nullptr, "plan is NULL");
-    CtxGuard g(plan->ctx);
-    NMZ_TRY(g.rc);
-    hipStream_t st = stream ? (hipStream_t)stream : plan->ctx->stream;
-    return replayable_run(plan, st, d_seed_off, d_seed_bytes, n_seeds, d_stats);
-}
-
-int nmz_replayable_sweep_topk_dev(nmz_replayable_plan *plan, const uint32_t *d_seed_off, const uint8_t *d_seed_bytes,
-                                  uint64_t n_seeds, uint64_t seed0, uint32_t k, nmz_sched_stats *d_stats,
-                                  nmz_topk_entry *d_topk, void *stream) {
-    NMZ_CHECK(plan != nullptr, "plan is NULL");
-    CtxGuard g(plan->ctx);
-    NMZ_TRY(g.rc);
-    hipStream_t st = stream ? (hipStream_t)stream : plan->ctx->stream;
-    return replayable_run(plan, st, d_seed_off, d_seed_bytes, n_seeds, d_stats, seed0, k, d_topk);
-}
-
-int nmz_replayable_seeds_create(nmz_ctx *ctx, const uint32_t *d_seed_off, const uint8_t *d_seed_bytes, uint64_t n_seeds,
-                                uint64_t dec_lo, nmz_replayable_seeds **out) {
-    NMZ_CHECK(ctx != nullptr && out != nullptr, "NULL argument");
-    NMZ_CHECK(n_seeds >= 1 && n_seeds < (1ULL << 32), "1 <= n_seeds < 2^32");
-    NMZ_CHECK(!d_seed_off || d_seed_bytes, "d_seed_bytes is NULL");
-    CtxGuard g(ctx);
-    NMZ_TRY(g.rc);
+// the caller holds ctx (nmz_replayable_seeds_create, nmz_replayable_sweep_traces)
+static int seeds_create_locked(nmz_ctx *ctx, const uint32_t *d_seed_off, const uint8_t *d_seed_bytes, uint64_t n_seeds,
+                               uint64_t dec_lo, nmz_replayable_seeds **out) {
     *out = nullptr;
     auto *s = new nmz_replayable_seeds();
     s->ctx = ctx;
@@ -2007,15 +1946,162 @@ int nmz_replayable_seeds_create(nmz_ctx *ctx, const uint32_t *d_seed_off, const 
     return NMZ_OK;
 }
 
+static void seeds_destroy_locked(nmz_replayable_seeds *seeds) {
+    (void)hipDeviceSynchronize();  // sweeps on any stream may still read the set (its buffer goes to the pool)
+    seeds->mem.release();
+    delete seeds;
+}
+
+}  // namespace nmz
+
+using namespace nmz;
+
+extern "C" {
+#ifdef OQ_TRACE
+int nmz_debug_oq_trace(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(nmz::g_oq_trace), sizeof(nmz::g_oq_trace)) == hipSuccess ? 0 : -1;
+}
+#endif
+
+int nmz_replayable_plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hint_bytes,
+                               uint32_t n_events, int64_t max_interval_ns, uint64_t max_seeds,
+                               nmz_replayable_plan **out) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    return plan_create(ctx, hint_off, hint_bytes, n_events, max_interval_ns, max_seeds, out);
+}
+
+int nmz_replayable_plan_create_async(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hint_bytes,
+                                     uint32_t n_events, int64_t max_interval_ns, uint64_t max_seeds,
+                                     nmz_replayable_plan **out) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    return plan_create(ctx, hint_off, hint_bytes, n_events, max_interval_ns, max_seeds, out, true);
+}
+
+int nmz_replayable_plan_destroy(nmz_replayable_plan *plan) {
+    if (!plan) return NMZ_OK;
+    {
+        CtxGuard g(plan->ctx);
+        plan_destroy_locked(plan);
+    }
+    return NMZ_OK;
+}
+
+int nmz_replayable_plan_kernel(const nmz_replayable_plan *plan) {
+    if (!plan) return -1;
+    return plan->wt.on ? 2 : plan->oq ? 1 : 0;
+}
+
+int nmz_replayable_sweep_dev(nmz_replayable_plan *plan, const uint32_t *d_seed_off, const uint8_t *d_seed_bytes,
+                             uint64_t n_seeds, nmz_sched_stats *d_stats, void *stream) {
+    NMZ_CHECK(plan != nullptr, "plan is NULL");
+    CtxGuard g(plan->ctx);
+    NMZ_TRY(g.rc);
+    hipStream_t st = stream ? (hipStream_t)stream : plan->ctx->stream;
+    return replayable_run(plan, st, d_seed_off, d_seed_bytes, n_seeds, d_stats);
+}
+
+int nmz_replayable_sweep_topk_dev(nmz_replayable_plan *plan, const uint32_t *d_seed_off, const uint8_t *d_seed_bytes,
+                                  uint64_t n_seeds, uint64_t seed0, uint32_t k, nmz_sched_stats *d_stats,
+                                  nmz_topk_entry *d_topk, void *stream) {
+    NMZ_CHECK(plan != nullptr, "plan is NULL");
+    CtxGuard g(plan->ctx);
+    NMZ_TRY(g.rc);
+    hipStream_t st = stream ? (hipStream_t)stream : plan->ctx->stream;
+    return replayable_run(plan, st, d_seed_off, d_seed_bytes, n_seeds, d_stats, seed0, k, d_topk);
+}
+
+int nmz_replayable_seeds_create(nmz_ctx *ctx, const uint32_t *d_seed_off, const uint8_t *d_seed_bytes, uint64_t n_seeds,
+                                uint64_t dec_lo, nmz_replayable_seeds **out) {
+    NMZ_CHECK(ctx != nullptr && out != nullptr, "NULL argument");
+    NMZ_CHECK(n_seeds >= 1 && n_seeds < (1ULL << 32), "1 <= n_seeds < 2^32");
+    NMZ_CHECK(!d_seed_off || d_seed_bytes, "d_seed_bytes is NULL");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    return seeds_create_locked(ctx, d_seed_off, d_seed_bytes, n_seeds, dec_lo, out);
+}
+
 int nmz_replayable_seeds_destroy(nmz_replayable_seeds *seeds) {
     if (!seeds) return NMZ_OK;
     {
         CtxGuard g(seeds->ctx);
-        (void)hipDeviceSynchronize();  // sweeps on any stream may still read the set (its buffer goes to the pool)
-        seeds->mem.release();
+        seeds_destroy_locked(seeds);
     }
-    delete seeds;
     return NMZ_OK;
+}
+
+#ifndef NMZ_TRACES_ONE_STREAM
+#define NMZ_TRACES_ONE_STREAM 0
+#endif
+int nmz_replayable_sweep_traces(nmz_ctx *ctx, uint32_t n_traces, const uint32_t *const *hint_off,
+                                const uint8_t *const *hint_bytes, const uint32_t *n_events, int64_t max_interval_ns,
+                                uint64_t seed_lo, uint64_t n_seeds, uint32_t k, nmz_topk_entry *topk) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    NMZ_CHECK(n_traces == 0 || (hint_off && hint_bytes && n_events && topk), "NULL argument");
+    NMZ_CHECK(k >= 1 && k <= 256, "1 <= k <= 256");
+    NMZ_CHECK(n_seeds >= 1 && n_seeds < (1ULL << 32), "1 <= n_seeds < 2^32");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    if (n_traces == 0) return NMZ_OK;
+    // the pipeline's resources: the private second context (plans alternate between the two contexts' streams, so
+    // one trace's build overlaps the previous trace's), two sweep streams, the stats / top-k buffers per slot
+    if (!ctx->helper) NMZ_TRY(nmz_open(ctx->device, &ctx->helper));
+    for (int i = 0; i < 2; ++i)
+        if (!ctx->sweep_st[i]) NMZ_HIP(hipStreamCreateWithFlags(&ctx->sweep_st[i], hipStreamNonBlocking));
+    for (int i = 0; i < 3; ++i)
+        if (!ctx->sweep_ev[i]) NMZ_HIP(hipEventCreateWithFlags(&ctx->sweep_ev[i], hipEventDisableTiming));
+    const uint64_t S = n_seeds;
+    const size_t st_bytes = Carve::bytes_for(S, sizeof(nmz_sched_stats)), tk_bytes = Carve::bytes_for(k, sizeof(nmz_topk_entry));
+    NMZ_TRY(ctx->buf[11].ensure(2 * (st_bytes + tk_bytes)));
+    NMZ_TRY(ctx->tkpin.ensure(3 * (size_t)k * sizeof(nmz_topk_entry)));
+    Carve cv(ctx->buf[11].ptr);
+    nmz_sched_stats *d_st[2] = {cv.take<nmz_sched_stats>(S), cv.take<nmz_sched_stats>(S)};
+    nmz_topk_entry *d_tk[2] = {cv.take<nmz_topk_entry>(k), cv.take<nmz_topk_entry>(k)};
+    nmz_topk_entry *h_tk = static_cast<nmz_topk_entry *>(ctx->tkpin.ptr);
+    nmz_replayable_seeds *ss = nullptr;
+    NMZ_TRY(seeds_create_locked(ctx, nullptr, nullptr, S, seed_lo, &ss));
+    nmz_ctx *ctxs[2] = {ctx, ctx->helper};
+    std::vector<nmz_replayable_plan *> plans(n_traces, nullptr);
+    auto make = [&](uint32_t j) {
+        return plan_create(ctxs[j % 2], hint_off[j], hint_bytes[j], n_events[j], max_interval_ns, S, &plans[j], true);
+    };
+    auto finish = [&](uint32_t j) -> int {
+        const int r = hipEventSynchronize(ctx->sweep_ev[j % 3]) == hipSuccess ? NMZ_OK
+                                                                               : fail(NMZ_EHIP, "sweep failed");
+        std::memcpy(topk + (size_t)j * k, h_tk + (size_t)(j % 3) * k, (size_t)k * sizeof(nmz_topk_entry));
+        plan_destroy_locked(plans[j]);
+        plans[j] = nullptr;
+        return r;
+    };
+    // trace i + 2's build is enqueued while trace i sweeps; trace i's top-k comes back while trace i + 1 sweeps
+    constexpr uint32_t AHEAD = 2;
+    int rc = NMZ_OK;
+    for (uint32_t j = 0; j < std::min(AHEAD, n_traces) && rc == NMZ_OK; ++j) rc = make(j);
+    for (uint32_t i = 0; i < n_traces && rc == NMZ_OK; ++i) {
+        if (i + AHEAD < n_traces) rc = make(i + AHEAD);
+        if (rc != NMZ_OK) break;
+        hipStream_t st = ctx->sweep_st[NMZ_TRACES_ONE_STREAM ? 0 : i % 2];
+        rc = replayable_run(plans[i], st, nullptr, nullptr, S, d_st[i % 2], seed_lo, k, d_tk[i % 2], 0, ss);
+        if (rc != NMZ_OK) break;
+        if (hipMemcpyAsync(h_tk + (size_t)(i % 3) * k, d_tk[i % 2], (size_t)k * sizeof(nmz_topk_entry),
+                           hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipEventRecord(ctx->sweep_ev[i % 3], st) != hipSuccess) {
+            rc = fail(NMZ_EHIP, "top-k copy failed");
+            break;
+        }
+        // two traces stay in flight: waiting for the previous one here would hold back the next plan builds
+        if (i >= 2) rc = finish(i - 2);
+        for (uint32_t j = i + 1 >= 2 ? i - 1 : 0; rc == NMZ_OK && i + 1 == n_traces && j <= i; ++j)
+            if (plans[j]) rc = finish(j);
+    }
+    // on an error: every plan still alive waits for its work and goes
+    for (auto *p : plans)
+        if (p) plan_destroy_locked(p);
+    seeds_destroy_locked(ss);
+    return rc;
 }
 
 int nmz_replayable_sweep_seeds_topk_dev(nmz_replayable_plan *plan, const nmz_replayable_seeds *seeds, uint64_t seed0,

@@ -421,6 +421,44 @@ def test_replayable_seed_set(ctx, monkeypatch, kind):
         L.nmz_replayable_seeds_destroy(ss)
 
 
+@pytest.mark.parametrize("m", [100_000_000, 2**31 + 3, 2**32 + 7])
+def test_replayable_sweep_traces(ctx, m):
+    """nmz_replayable_sweep_traces (a batch of traces over one decimal seed range, pipelined inside) == one
+    nmz_replayable_sweep_decimal_topk_dev per trace on its own plan, for traces of several shapes (one-launch
+    wavelet-tree plans, a 4,097-event class on the separate plan kernels, tiny traces); the top-k of a small
+    trace also vs the oracle."""
+    import torch
+    L = _lib.load()
+    rng = np.random.default_rng(m % 1000)
+    traces = [zk_hints(600, rng), zk_hints(97, rng) + ["", "a"], ["x" * 5] * 4097, zk_hints(3, rng),
+              zk_hints(2000, rng), zk_hints(64, rng), zk_hints(1, rng)]
+    T, S, k, lo = len(traces), 2500, 16, 77
+    csrs = [to_csr(h) for h in traces]
+    offs = (ctypes.c_void_p * T)(*[ctypes.c_void_p(ho.ctypes.data) for ho, _ in csrs])
+    byts = (ctypes.c_void_p * T)(*[ctypes.c_void_p(hb.ctypes.data) for _, hb in csrs])
+    nev = np.array([len(h) for h in traces], np.uint32)
+    out = np.zeros(T * k, _lib.TOPK_DTYPE)
+    for rep in range(2):  # the second call reuses the pipeline's streams, helper context and pooled buffers
+        _lib.check(L.nmz_replayable_sweep_traces(ctx.handle, T, offs, byts, _lib.ptr(nev), m, lo, S, k,
+                                                 _lib.ptr(out)))
+        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        for t, (ho, hb) in enumerate(csrs):
+            plan = ctypes.c_void_p()
+            _lib.check(L.nmz_replayable_plan_create(ctx.handle, _lib.ptr(ho), _lib.ptr(hb), len(traces[t]), m, S,
+                                                    ctypes.byref(plan)))
+            d_st = torch.zeros(S * 32, dtype=torch.uint8, device="cuda")
+            d_tk = torch.zeros(k * 24, dtype=torch.uint8, device="cuda")
+            _lib.check(L.nmz_replayable_sweep_decimal_topk_dev(plan, lo, S, k, ctypes.c_void_p(d_st.data_ptr()),
+                                                               ctypes.c_void_p(d_tk.data_ptr()), stream))
+            torch.cuda.synchronize()
+            L.nmz_replayable_plan_destroy(plan)
+            ref = np.frombuffer(d_tk.cpu().numpy().tobytes(), dtype=_lib.TOPK_DTYPE)
+            assert out[t * k:(t + 1) * k].tolist() == ref.tolist(), (rep, t)
+    seeds = [str(lo + i) for i in range(S)]
+    st, _ = rep_oracle(seeds, traces[3], m)
+    assert out[3 * k:4 * k].tolist() == O.topk_from_stats(st, lo, k).tolist()
+
+
 def test_replayable_plan_create_async(ctx):
     """nmz_replayable_plan_create_async: builds enqueued on two contexts' streams, sweeps enqueued at once on
     another stream (which must wait for each build on the device), plans of several shapes (the one-launch
