@@ -964,23 +964,26 @@ def headline_line(args, torch, D, ctx, L, stream):
            "what": "per trace, one at a time: nmz_replayable_plan_create from host hints (table, sorts and wavelet "
                    "trees: one plan kernel) + one 2^20-seed sweep with top-64 + top-64 copy to the host"}
     p, nat = r.get("e2e_pipe"), r.get("e2e_native")
-    if p and nat:
-        # a stream of traces (how a sweep tool over many recorded traces runs): the throughput figure, through the
-        # native batch entry point; the same pipeline driven from Python and the one-at-a-time latency inside
+    if p:
+        # a stream of traces (how a sweep tool over many recorded traces runs): the throughput figure; the same
+        # stream through the native batch entry point and the one-at-a-time latency inside
         line["end_to_end"] = {
-            "value": dec_launch / (nat["ms_per_trace"] * 1e-3), "unit": "decisions/s", "mode": "stream",
-            "ms_per_trace": nat["ms_per_trace"], "ms_per_trace_runs": nat["ms_per_trace_runs"], "traces": nat["traces"],
-            "plan_ms": one["plan_ms"], "top1_head": nat["top1"], "agrees_with_one_at_a_time": nat["agrees"],
-            "what": "nmz_replayable_sweep_traces over 17 traces: every trace gets its own plan (built from host hints "
-                    "inside the timing, one plan kernel), one 2^20-seed sweep and its top-64 on the host; the "
-                    "seeds' prefix hashes are prepared once per call; trace i+2's plan builds while trace i sweeps. "
-                    "ms_per_trace = one call's elapsed time / traces (median of 3 calls). plan_ms: one plan built "
-                    "alone (one_at_a_time)",
-            "python_stream": {"value": dec_launch / (p["ms_per_trace"] * 1e-3), "ms_per_trace": p["ms_per_trace"],
-                              "agrees_with_one_at_a_time": p["agrees"],
-                              "what": "the same pipeline driven from Python (nmz_replayable_plan_create_async, "
-                                      "nmz_replayable_seeds_create, nmz_replayable_sweep_seeds_topk_dev)"},
+            "value": dec_launch / (p["ms_per_trace"] * 1e-3), "unit": "decisions/s", "mode": "stream",
+            "ms_per_trace": p["ms_per_trace"], "traces": p["traces"], "plan_ms": one["plan_ms"],
+            "top1_head": p["top1"], "agrees_with_one_at_a_time": p["agrees"],
+            "iter_ms_median": p["iter_ms_median"], "iter_ms_max": p["iter_ms_max"],
+            "what": "every trace gets its own plan (nmz_replayable_plan_create_async from host hints, inside the "
+                    "timing), one 2^20-seed sweep with top-64 and the top-64 on the host; the seeds' prefix hashes "
+                    "are prepared once for the stream (nmz_replayable_seeds_create, inside the timing); one host "
+                    "thread enqueues trace i+2's plan build (two contexts) while trace i sweeps (two streams); whole "
+                    "elapsed time / traces. plan_ms: one plan built alone (one_at_a_time)",
             "one_at_a_time": one}
+        if nat:
+            line["end_to_end"]["native_batch"] = {
+                "value": dec_launch / (nat["ms_per_trace"] * 1e-3), "ms_per_trace": nat["ms_per_trace"],
+                "ms_per_trace_runs": nat["ms_per_trace_runs"], "agrees_with_one_at_a_time": nat["agrees"],
+                "what": "the same stream in one nmz_replayable_sweep_traces call (the pipeline inside the library), "
+                        "median of 3 calls"}
     else:
         line["end_to_end"] = dict(one, mode="one_at_a_time")
     if line["roofline"]:

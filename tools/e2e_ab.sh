@@ -12,4 +12,4 @@ for i in $(seq 1 $n); do
 done
 for f in gpurun_out/${tag}_*.json; do python3 -c "
 import json;d=json.loads(open('$f').read().strip().splitlines()[-1]);e=d['end_to_end'];o=e.get('one_at_a_time', e)
-print('$f', round(d['ms_per_step'],4), 'plan', round(d['plan_ms'],4), 'one', round(o['ms_median'],4), '%.3g'%o['value'], 'native', round(e.get('ms_per_trace',0),4), '%.3g'%e['value'], e.get('agrees_with_one_at_a_time'), 'py', round((e.get('python_stream') or {}).get('ms_per_trace',0),4))"; done
+print('$f', round(d['ms_per_step'],4), 'plan', round(d['plan_ms'],4), 'one', round(o['ms_median'],4), '%.3g'%o['value'], 'stream', round(e.get('ms_per_trace',0),4), '%.3g'%e['value'], e.get('agrees_with_one_at_a_time'), 'native', round((e.get('native_batch') or {}).get('ms_per_trace',0),4))"; done
