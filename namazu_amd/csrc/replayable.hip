@@ -2080,10 +2080,20 @@ int nmz_replayable_sweep_traces(nmz_ctx *ctx, uint32_t n_traces, const uint32_t 
     constexpr uint32_t AHEAD = 2;
     int rc = NMZ_OK;
     for (uint32_t j = 0; j < std::min(AHEAD, n_traces) && rc == NMZ_OK; ++j) rc = make(j);
+    // trace i sweeps on the stream its plan was built on, and trace i + 2's build is enqueued behind that sweep
+    // (two streams in all, each serial: build, sweep, build, ...): 0.179 ms per trace against 0.188 with the
+    // builds and sweeps on four streams (NMZ_TRACES_MODE=0, profiles/r04/e2e_native_ab/). NMZ_TRACES_MODE=2: the
+    // same, with trace i's top-k read after trace i + 1's sweep is enqueued instead of trace i + 2's
+    static const int mode = [] {
+        const char *e = std::getenv("NMZ_TRACES_MODE");
+        return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 1;
+    }();
+    const bool same_stream = mode != 0;
+    const uint32_t lag = mode == 2 ? 1 : 2;
     for (uint32_t i = 0; i < n_traces && rc == NMZ_OK; ++i) {
-        if (i + AHEAD < n_traces) rc = make(i + AHEAD);
+        if (!same_stream && i + AHEAD < n_traces) rc = make(i + AHEAD);
         if (rc != NMZ_OK) break;
-        hipStream_t st = ctx->sweep_st[NMZ_TRACES_ONE_STREAM ? 0 : i % 2];
+        hipStream_t st = same_stream ? ctxs[i % 2]->stream : ctx->sweep_st[NMZ_TRACES_ONE_STREAM ? 0 : i % 2];
         rc = replayable_run(plans[i], st, nullptr, nullptr, S, d_st[i % 2], seed_lo, k, d_tk[i % 2], 0, ss);
         if (rc != NMZ_OK) break;
         if (hipMemcpyAsync(h_tk + (size_t)(i % 3) * k, d_tk[i % 2], (size_t)k * sizeof(nmz_topk_entry),
@@ -2092,9 +2102,11 @@ int nmz_replayable_sweep_traces(nmz_ctx *ctx, uint32_t n_traces, const uint32_t 
             rc = fail(NMZ_EHIP, "top-k copy failed");
             break;
         }
+        if (same_stream && i + AHEAD < n_traces) rc = make(i + AHEAD);
+        if (rc != NMZ_OK) break;
         // two traces stay in flight: waiting for the previous one here would hold back the next plan builds
-        if (i >= 2) rc = finish(i - 2);
-        for (uint32_t j = i + 1 >= 2 ? i - 1 : 0; rc == NMZ_OK && i + 1 == n_traces && j <= i; ++j)
+        if (i >= lag) rc = finish(i - lag);
+        for (uint32_t j = i + 1 >= lag ? i + 1 - lag : 0; rc == NMZ_OK && i + 1 == n_traces && j <= i; ++j)
             if (plans[j]) rc = finish(j);
     }
     // on an error: every plan still alive waits for its work and goes
