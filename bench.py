@@ -1120,7 +1120,7 @@ def main():
     ap.add_argument("--random-total", type=int, default=10_000_000)
     ap.add_argument("--random-steps", type=int, default=3)
     ap.add_argument("--cpu-random-seeds", type=int, default=256)
-    ap.add_argument("--e2e-traces", type=int, default=17)
+    ap.add_argument("--e2e-traces", type=int, default=64)
     ap.add_argument("--ed-traces", type=int, default=100_000)
     ap.add_argument("--ed-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")

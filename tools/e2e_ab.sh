@@ -1,4 +1,4 @@
-# usage: bash tools/e2e_ab.sh <tag> <rounds> <variant>...: configs[1] leg with 17 end-to-end traces, the product
+# usage: bash tools/e2e_ab.sh <tag> <rounds> <variant>...: configs[1] leg with the default stream of end-to-end traces (64), the product
 # library vs each namazu_amd/libnmz_gpu_<variant>.so (or, for a variant VAR=value, the product library with that
 # environment setting); prints step, plan and end-to-end (one at a time, streamed)
 tag=$1; n=$2; shift 2
@@ -7,7 +7,7 @@ for i in $(seq 1 $n); do
   for v in product "$@"; do
     if [ $v = product ]; then L=""; elif [[ $v == *=* ]]; then L="$v"; else L="NMZ_LIB_PATH=$PWD/namazu_amd/libnmz_gpu_$v.so"; fi
     name=${v//=/_}
-    env $L timeout -k 10 180 python bench.py --legs replayable --no-cpu-baseline --e2e-traces 17 --steps 50 > gpurun_out/${tag}_${name}_$i.json 2>/dev/null || exit $?
+    env $L timeout -k 10 180 python bench.py --legs replayable --no-cpu-baseline --steps 50 > gpurun_out/${tag}_${name}_$i.json 2>/dev/null || exit $?
   done
 done
 for f in gpurun_out/${tag}_*.json; do python3 -c "
