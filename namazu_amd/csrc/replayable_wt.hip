@@ -1012,7 +1012,10 @@ __global__ __launch_bounds__(256) void k_wt_topk_scan(const uint64_t *__restrict
 
 // one block: sort the candidates and write the top k (past WT_CAND candidates -- heavy ties, e.g. maxInterval 1 --
 // select them one rank at a time over every seed: exact, slow); resets the candidate counter
-constexpr uint32_t WT_SEL_THREADS = 512;
+#ifndef NMZ_WT_SEL_THREADS
+#define NMZ_WT_SEL_THREADS 512
+#endif
+constexpr uint32_t WT_SEL_THREADS = NMZ_WT_SEL_THREADS;
 __global__ __launch_bounds__(WT_SEL_THREADS) void k_wt_topk_select(const uint64_t *__restrict__ sums,
                                                                    const uint32_t *__restrict__ sorted_idx, uint64_t S,
                                                                    uint64_t seed0, uint32_t k,
