@@ -136,6 +136,79 @@ def roofline_valu(kernel, units, kernel_ms):
                               if e.get("clock_ghz") else None)}
 
 
+# The driver parses the LAST stdout line and keeps only the tail of stdout: the final line is a compact headline
+# (configs[1]: value, roofline, cpu_baseline, a short per-leg summary) capped at HEADLINE_MAX_BYTES; every
+# secondary leg goes out as its own earlier line ({"secondary_leg": ...}) and the full record to a file.
+HEADLINE_MAX_BYTES = 4096
+HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+                 "vs_baseline", "dtype", "data", "config")
+ROOFLINE_KEYS = ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic", "kernel_ms", "kernel_ms_source",
+                 "ops_per_unit", "units_per_launch", "unit_kind", "frac_of_issue_ceiling", "frac_at_clock",
+                 "clock_ghz", "kernel_ms_span", "kernel_ms_serial_span", "kernel_ms_events", "stale", "ops_source")
+CPU_KEYS = ("value", "unit", "cores", "kind", "sample", "parity_with_gpu", "seconds")
+
+
+def _round(v):
+    if isinstance(v, float):
+        return float(f"{v:.5g}")
+    if isinstance(v, dict):
+        return {k: _round(x) for k, x in v.items()}
+    if isinstance(v, list):
+        return [_round(x) for x in v]
+    return v
+
+
+def leg_summary(leg):
+    """One secondary leg as {leg, value, unit, ms_per_step, kernel, frac} for the headline's secondary_summary."""
+    cfg = leg.get("config") or {}
+    rf = leg.get("roofline") or {}
+    out = {"leg": leg.get("leg") or cfg.get("workload", leg.get("metric", "?"))[:40], "value": leg.get("value"),
+           "unit": leg.get("unit")}
+    for k in ("ms_per_step", "kernel_ms"):
+        if leg.get(k) is not None:
+            out[k] = leg[k]
+    if rf:
+        out["kernel"] = rf.get("kernel")
+        out["frac"] = rf.get("frac")
+    if "lines" in leg:  # the K1 cliffs leg: one figure per line
+        out["value"] = [x.get("value") for x in leg["lines"]]
+    if "gpu_batch" in leg:  # configs[0]
+        out["value"], out["ms"] = leg["gpu_batch"]["value"], leg["gpu_batch"]["ms"]
+    return _round(out)
+
+
+def headline_record(line):
+    """The compact final stdout line: the headline fields, a trimmed roofline and cpu_baseline, the end-to-end
+    figures and a per-leg summary of the secondary legs, below HEADLINE_MAX_BYTES (optional parts are dropped,
+    last first, if it would not fit)."""
+    rec = {k: line[k] for k in HEADLINE_KEYS if k in line}
+    if line.get("roofline"):
+        rec["roofline"] = {k: line["roofline"][k] for k in ROOFLINE_KEYS if k in line["roofline"]}
+    if line.get("cpu_baseline"):
+        rec["cpu_baseline"] = {k: line["cpu_baseline"][k] for k in CPU_KEYS if k in line["cpu_baseline"]}
+    e2e = line.get("end_to_end")
+    if e2e:
+        rec["end_to_end"] = {k: e2e[k] for k in ("value", "mode", "ms_per_trace", "traces", "plan_ms",
+                                                 "agrees_with_one_at_a_time") if k in e2e}
+        nb = e2e.get("native_batch")
+        if nb:
+            rec["end_to_end"]["native_batch"] = {k: nb[k] for k in ("value", "ms_per_trace",
+                                                                    "agrees_with_one_at_a_time") if k in nb}
+    optional = []
+    if line.get("secondary"):
+        rec["secondary_summary"] = [leg_summary(s) for s in line["secondary"]]
+        optional.append("secondary_summary")
+    if line.get("full_record"):
+        rec["full_record"] = line["full_record"]
+    rec = _round(rec)
+    optional += ["end_to_end", "data"]
+    text = json.dumps(rec, separators=(",", ":"))
+    while len(text) >= HEADLINE_MAX_BYTES and optional:
+        rec.pop(optional.pop(0), None)
+        text = json.dumps(rec, separators=(",", ":"))
+    return text
+
+
 def cpu_threads():
     """Host threads for the CPU baselines: the cores this process may run on (on the GPU box the CPU share
     set by OMP_NUM_THREADS, since nproc there counts the whole machine)."""
@@ -280,17 +353,25 @@ def bench_replayable(args, torch, D, ctx, L, stream):
         step()
     drain()
     torch.cuda.synchronize()
-    # the roofline's kernel time: K1 launches one at a time (HIP events on the launch stream), untimed
-    _lib.check(L.nmz_timing_enable(ctx.handle, 1))
+    # the roofline's kernel time: K1 launched back to back on ONE stream (no other stream's kernels beside it, the
+    # way rocprofv3 --kernel-trace times a dispatch), HIP events around each K1 launch plus its in-kernel span;
+    # enough launches that the engine clock has ramped (a handful after an idle sync run slow)
     tot, cnt = ctypes.c_double(), ctypes.c_uint64()
-    L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
-    for _ in range(5):
+    for _ in range(20):
         step(0)
-        drain()
+    drain()
+    _lib.check(L.nmz_timing_enable(ctx.handle, 1))
+    L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
+    L.nmz_timing_read_span(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
+    for _ in range(50):
+        step(0)
+    drain()
     torch.cuda.synchronize()
     _lib.check(L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
-    _lib.check(L.nmz_timing_enable(ctx.handle, 0))
     kern_ms = tot.value / max(cnt.value, 1)
+    _lib.check(L.nmz_timing_read_span(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
+    kern_ms_serial_span = tot.value / cnt.value if cnt.value else None
+    _lib.check(L.nmz_timing_enable(ctx.handle, 0))
     # the timed region: exactly args.steps pipelined steps; K1's launches are bracketed by HIP events on their
     # own streams (nmz_timing_*), so the roofline's kernel time comes from these same launches
     it[0] = 0
@@ -441,8 +522,8 @@ def bench_replayable(args, torch, D, ctx, L, stream):
         e2e_native = dict(traces=T, ms_per_trace=float(np.median(ms)), ms_per_trace_runs=ms, top1=heads[:4],
                           agrees=heads == e2e_heads)
     return dict(S=S, E=E, hints=(hoff, hb), seeds=csr[0], elapsed=el_max,
-                kern_ms=kern_ms_span if kern_ms_span is not None else kern_ms_timed, kern_ms_events=kern_ms_timed,
-                kern_ms_span=kern_ms_span, kern_ms_isolated=kern_ms, plan_ms=plan_ms, stats=stats, topk=merged, pipeline=NP,
+                kern_ms=kern_ms, kern_ms_events=kern_ms_timed, kern_ms_serial_span=kern_ms_serial_span,
+                kern_ms_span=kern_ms_span, plan_ms=plan_ms, stats=stats, topk=merged, pipeline=NP,
                 e2e_s=e2e, e2e_plan_s=e2e_plan, e2e_pipe=e2e_pipe, e2e_native=e2e_native, k1_kernel=k1)
 
 
@@ -1001,14 +1082,13 @@ def headline_line(args, torch, D, ctx, L, stream):
                 ceil = PEAK_VALU_TOPS * 1e12 / pd["ops_per_unit"]
                 rf["per_decision_ceiling"] = ceil
                 rf["vs_per_decision_ceiling"] = line["value"] / ceil
-        if r["kern_ms_span"] is not None:
-            rf["kernel_ms_source"] = ("in-kernel execution spans of the timed region's K1 launches (wall_clock64 at "
-                                      "the first workgroup start and the last wave end, nmz_timing_read_span): the "
-                                      "union of the spans / launches, so overlapping launches share their time")
-        else:
-            rf["kernel_ms_source"] = "HIP events around every K1 launch of the timed region (on its stream)"
-        rf["kernel_ms_events"] = r["kern_ms_events"]  # includes the wait for CUs held by another stream's K1
-        rf["kernel_ms_isolated"] = r["kern_ms_isolated"]
+        rf["kernel_ms_source"] = ("HIP events around K1, 50 launches back to back on one stream (as rocprofv3 "
+                                  "times a dispatch)")
+        # the timed region's own K1 launches: HIP events (include waits for CUs held by the other streams' kernels)
+        # and the union of their in-kernel spans; the serial launches' in-kernel span
+        rf["kernel_ms_events"] = r["kern_ms_events"]
+        rf["kernel_ms_span"] = r["kern_ms_span"]
+        rf["kernel_ms_serial_span"] = r["kern_ms_serial_span"]
         # the same lane-ops over the whole pipelined step (every kernel of the step on the clock)
         if not rf.get("stale"):
             rf["frac_of_step"] = (rf["ops_per_unit"] * dec_launch / (line["ms_per_step"] * 1e-3) / 1e12 /
@@ -1109,6 +1189,19 @@ def bench_group(args, torch):
     return line
 
 
+def write_final(out_fd, line, path):
+    """The full record (every leg, every field) to `path`, then the compact headline as the last stdout line."""
+    if path:
+        try:
+            os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+            with open(path, "w") as f:
+                json.dump(line, f, indent=1)
+            line = dict(line, full_record=os.path.relpath(os.path.abspath(path), HERE))
+        except OSError as e:
+            print(f"bench: could not write {path}: {e}", file=sys.stderr)
+    os.write(out_fd, (headline_record(line) + "\n").encode())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1125,6 +1218,9 @@ def main():
     ap.add_argument("--ed-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     ap.add_argument("--no-secondary", dest="secondary", action="store_false")
+    ap.add_argument("--full-record", default=os.path.join("gpurun_out", "bench_full.json"),
+                    help="file for the full JSON record (every leg); '' to skip. stdout's last line is the compact "
+                         "headline")
     ap.add_argument("--vis-traces", type=int, default=100_000)
     ap.add_argument("--vis-cpu-traces", type=int, default=1000)
     ap.add_argument("--group", action="store_true",
@@ -1137,7 +1233,8 @@ def main():
                          "needs 'replayable'")
     args = ap.parse_args()
     args.legs = set(args.legs.split(","))
-    # The JSON line is the only output on stdout: whatever the libraries write to fd 1 during the run
+    # The JSON lines are the only output on stdout (one per secondary leg, then the compact headline last):
+    # whatever the libraries write to fd 1 during the run
     # (gloo's connection messages, HIP/RCCL diagnostics) goes to stderr instead.
     sys.stdout.flush()
     out_fd = os.dup(1)
@@ -1146,7 +1243,7 @@ def main():
     import torch
     if args.group:
         line = bench_group(args, torch)
-        os.write(out_fd, (json.dumps(line) + "\n").encode())
+        write_final(out_fd, line, args.full_record)
         return
     D = Dist()
     torch.cuda.set_device(D.local_rank)
@@ -1181,20 +1278,26 @@ def main():
         ed5 = dict(workload="configs[4] long-trace stress, wide band", traces=256, events=65536, band=4096, k=8,
                    generator="etcd_traces", steps=args.ed_steps, valu_key="k_ed_wide")
         sec = []
+
+        def add(name, leg):  # each leg on its own stdout line as it finishes (never the last line)
+            leg = dict(leg, leg=name)
+            sec.append(leg)
+            if D.rank == 0:
+                os.write(out_fd, (json.dumps({"secondary_leg": leg}) + "\n").encode())
         if "random" in args.legs:
-            sec.append(bench_random_fault_sweep(args, torch, D, ctx, L, stream))
+            add("random", bench_random_fault_sweep(args, torch, D, ctx, L, stream))
         for leg, spec in (("ed_clustered", ed3), ("ed_survey", ed3s), ("ed_alphabet", ed3a), ("ed_wide", ed5)):
             if leg in args.legs:
-                sec.append(bench_ed_secondary(args, torch, D, ctx, L, stream, spec))
+                add(leg, bench_ed_secondary(args, torch, D, ctx, L, stream, spec))
         if "replayable_cliffs" in args.legs and D.rank == 0:
-            sec.append(bench_replayable_cliffs(args, torch, D, ctx, L, stream))
+            add("replayable_cliffs", bench_replayable_cliffs(args, torch, D, ctx, L, stream))
         if "visualize" in args.legs and D.rank == 0:
-            sec.append(bench_visualize(args, torch, D, ctx, L, stream))
+            add("visualize", bench_visualize(args, torch, D, ctx, L, stream))
         if "config0" in args.legs and D.rank == 0 and D.world == 1 and args.cpu_baseline:
-            sec.append(bench_config0(args, torch, D, ctx, L))
+            add("config0", bench_config0(args, torch, D, ctx, L))
         line["secondary"] = sec
     if D.rank == 0:
-        os.write(out_fd, (json.dumps(line) + "\n").encode())
+        write_final(out_fd, line, args.full_record)
     ctx.close()
     if D.pg:
         D.pg.destroy_process_group()
