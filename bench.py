@@ -876,6 +876,9 @@ def bench_ed_secondary(args, torch, D, ctx, L, stream, spec):
     del full, mine
     plan_ms = (time.time() - t0) * 1e3
     kind = {3: "k_ed_wide", 2: "k_ed_bv", 1: "k_ed_tile", 0: "k_ed_generic"}[L.nmz_ed_plan_is_fast(plan)]
+    if D.pg:  # every rank must hold the same plan (kernel, store, options), or the shards would not partition
+        from namazu_amd import dist as nd
+        nd.check_ed_plans(D.pg, L, plan, device=dev)
     d_knn = torch.empty(N * k, dtype=torch.int64, device=dev)
     d_parts = torch.empty(D.world * N * k, dtype=torch.int64, device=dev) if D.world > 1 else None
     d_out = torch.empty(N * k, dtype=torch.int64, device=dev) if D.world > 1 else d_knn

@@ -316,6 +316,24 @@ int nmz_ed_plan_create(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, u
  * them over RCCL instead of pushing the whole store through every device's PCIe link. */
 int nmz_ed_plan_create_dev(nmz_ctx *ctx, const uint64_t *off, const uint64_t *d_sym, uint32_t n_traces,
                            uint32_t band, nmz_ed_plan **out);
+/* Plan options (bit flags) of nmz_ed_plan_create_opts. 0 is the product's choice; the others select the
+ * alternative forms of the bit-parallel search, for A/B runs and tests. Whichever form a plan takes, a shard owns
+ * the same pairs (whole 64-query blocks, nmz_ed_block_shard), so shards may mix forms. The NMZ_ED_* environment
+ * knobs that add to these are read only when NMZ_AB=1 is set. */
+#define NMZ_ED_OPT_SINGLE_KERNEL 1u /* no two-phase search: the single kernel with its in-workgroup pre-filter */
+#define NMZ_ED_OPT_NO_QGRAM 2u      /* no q-gram lower-bound filter (the single kernel, without the filter) */
+#define NMZ_ED_OPT_COMPACT 4u       /* compact per-workgroup Peq tables even when the direct tables fit */
+#define NMZ_ED_OPT_HOST_BUILD 8u    /* the plan's streams built on the host instead of the device */
+/* sym (host) or d_sym (device, read during the call): exactly one of them when the store is not empty */
+int nmz_ed_plan_create_opts(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, const uint64_t *d_sym,
+                            uint32_t n_traces, uint32_t band, uint32_t opts, nmz_ed_plan **out);
+/* The plan's fingerprint, 8 words: version, kernel kind | band << 8 | template band << 40, n_traces, total
+ * symbols, two-phase | q-gram << 1 | compact << 2, block-row queries | pool << 32, FNV-1a 64 of the offsets, alphabet
+ * size. Ranks that search one store together must hold equal fingerprints: the device groups all_gather them when
+ * a plan is created and fail with NMZ_EINVAL when they differ. */
+#define NMZ_ED_FP_WORDS 8
+#define NMZ_ED_FP_VERSION 1u
+int nmz_ed_plan_fingerprint(const nmz_ed_plan *plan, uint64_t *fp /* [NMZ_ED_FP_WORDS] */);
 int nmz_ed_plan_destroy(nmz_ed_plan *plan);
 int nmz_ed_plan_is_fast(const nmz_ed_plan *plan);
 int nmz_ed_allpairs_knn_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys, void *stream);
@@ -327,8 +345,8 @@ int nmz_ed_allpairs_knn_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys,
  * so the merged lists take (band + 1, id) for the smallest ids not listed (not the trace
  * itself), in increasing id, up to k. On other plans the fill leaves complete lists
  * unchanged. (nmz_ed_allpairs_knn[_dev] fill by themselves.) */
-/* Host-only (no device work): the shard that owns query block qb (queries 64 qb .. 64 qb + 63) of the two-phase
- * bit-parallel search under nmz_ed_allpairs_knn_shard_dev with n_shards shards: every pair (i, j), i < j, belongs
+/* Host-only (no device work): the shard that owns query block qb (queries 64 qb .. 64 qb + 63) of the
+ * bit-parallel search (both forms: two-phase and the single kernel) under nmz_ed_allpairs_knn_shard_dev with n_shards shards: every pair (i, j), i < j, belongs
  * to the shard of block i / 64, in rotated snake order (in each period of 2 n_shards blocks, block r and its mirror
  * 2 n_shards - 1 - r form pair p = min(r, 2 n_shards - 1 - r), which goes to shard (p + period) mod n_shards). A
  * fixed rule, the same in every process (no environment knob). A shard whose entry lists exceed the two-phase limit
@@ -449,10 +467,16 @@ int nmz_random_sweep_topk_group(nmz_group *g, uint64_t seed0, uint64_t n_seeds, 
  * store reaches the devices as 1/n_ranks shares: rank r uploads symbols [r S, r S + S) (S = ceil(total / n_ranks))
  * through its own PCIe link, one RCCL all_gather over xGMI assembles the store on every device, and each device
  * builds its plan from device memory (nmz_ed_plan_create_dev). nmz_ed_group_plan_timing reports, per local device,
- * the share upload, the all_gather and the device plan build (ms, arrays of nmz_group_info's n_local_devices). */
+ * the share upload, the all_gather and the device plan build (ms, arrays of nmz_group_info's n_local_devices).
+ * After each local step (upload, plan build) the ranks exchange their status, so a rank that failed never leaves the
+ * others waiting in a collective; after the build they exchange their plans' fingerprints (nmz_ed_plan_fingerprint)
+ * and all fail with NMZ_EINVAL when any two differ. */
 typedef struct nmz_ed_group_plan nmz_ed_group_plan;
 int nmz_ed_group_plan_create(nmz_group *g, const uint64_t *off, const uint64_t *sym, uint32_t n_traces,
                              uint32_t band, nmz_ed_group_plan **out);
+/* The same with NMZ_ED_OPT_* plan options for every member's plan (nmz_ed_plan_create_opts). */
+int nmz_ed_group_plan_create_opts(nmz_group *g, const uint64_t *off, const uint64_t *sym, uint32_t n_traces,
+                                  uint32_t band, uint32_t opts, nmz_ed_group_plan **out);
 int nmz_ed_group_plan_timing(const nmz_ed_group_plan *gp, double *upload_ms, double *gather_ms, double *build_ms);
 int nmz_ed_group_plan_destroy(nmz_ed_group_plan *gp);
 int nmz_ed_group_allpairs_knn(nmz_ed_group_plan *gp, uint32_t k, uint32_t *knn_id, uint32_t *knn_dist);

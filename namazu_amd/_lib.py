@@ -26,6 +26,8 @@ NMZ_EV_FAULTABLE = 0x02
 NMZ_STAT_RNG_OVERFLOW = 0x01
 NMZ_NONE = 0xFFFFFFFF
 NMZ_ED_NCOUNTERS = 6
+NMZ_ED_OPT_SINGLE_KERNEL, NMZ_ED_OPT_NO_QGRAM, NMZ_ED_OPT_COMPACT, NMZ_ED_OPT_HOST_BUILD = 1, 2, 4, 8
+NMZ_ED_FP_WORDS = 8
 
 SCHED_STATS_DTYPE = np.dtype([
     ("sum_delay_ns", "<u8"), ("max_delay_ns", "<i8"), ("argmax_event", "<u4"),
@@ -89,6 +91,8 @@ SIGNATURES = {
     "nmz_ed_plan_create": (_int, [_P, _P, _P, _u32, _u32, ctypes.POINTER(_P)]),
     "nmz_ed_plan_destroy": (_int, [_P]),
     "nmz_ed_plan_create_dev": (_int, [_P, _P, _P, _u32, _u32, ctypes.POINTER(_P)]),
+    "nmz_ed_plan_create_opts": (_int, [_P, _P, _P, _P, _u32, _u32, _u32, ctypes.POINTER(_P)]),
+    "nmz_ed_plan_fingerprint": (_int, [_P, _P]),
     "nmz_ed_plan_is_fast": (_int, [_P]),
     "nmz_ed_block_shard": (_u32, [_u32, _u32]),
     "nmz_ed_allpairs_knn_dev": (_int, [_P, _u32, _P, _P]),
@@ -128,6 +132,7 @@ SIGNATURES = {
     "nmz_random_group_sweep": (_int, [_P, _u64, _u64, _u32, _P, _P]),
     "nmz_random_sweep_topk_group": (_int, [_P, _u64, _u64, _P, _P, _u32, _P, _u32, _P, _P]),
     "nmz_ed_group_plan_create": (_int, [_P, _P, _P, _u32, _u32, ctypes.POINTER(_P)]),
+    "nmz_ed_group_plan_create_opts": (_int, [_P, _P, _P, _u32, _u32, _u32, ctypes.POINTER(_P)]),
     "nmz_ed_group_plan_destroy": (_int, [_P]),
     "nmz_ed_group_plan_timing": (_int, [_P, _P, _P, _P]),
     "nmz_ed_group_allpairs_knn": (_int, [_P, _u32, _P, _P]),

@@ -422,10 +422,8 @@ struct nmz_ed_plan {
     uint32_t ndw = 0, lds_dw = 0;  // bv: dwords per Peq row per query, LDS dwords per workgroup
     uint64_t n_chunks = 0;         // bv: total chunks (64-query block row x ED_BV_POOL candidates)
     uint16_t *d_bsym = nullptr;
-    uint64_t *d_chunk_start = nullptr;  // bv: [G+1] per-row chunk starts of the current shard (rewritten per call)
-    std::vector<uint64_t> row_chunks;    // bv: chunks per 64-query block row
-    std::map<uint64_t, std::vector<uint64_t>> shard_start;  // bv: per (shard, n_shards) row starts (host; kept, so
-                                                             // an async copy from it never sees it rewritten)
+    uint64_t *d_chunk_start = nullptr;  // bv: [G+1] per-row chunk starts (single-kernel search)
+    std::vector<uint64_t> row_chunks;    // bv: chunks per block row
     uint64_t *d_counters = nullptr;  // bv: work counters of the latest search (nmz_ed_plan_counters)
     uint32_t *d_prof = nullptr;      // bv: [N][ED_QG_DW] q-gram profiles (ed_qgram_profiles)
     uint32_t rq = 64;                // bv: queries per block row
@@ -443,6 +441,8 @@ struct nmz_ed_plan {
     // fixed at creation (NMZ_ED_QGRAM / NMZ_ED_TWO_PHASE, A/B knobs read once per plan), so every shard and every
     // call of one plan takes the same search and deals pairs by the same rule
     bool qgram = true, two_phase = true;
+    uint32_t opts = 0;               // NMZ_ED_OPT_* the plan was created with (options | A/B knobs)
+    uint64_t total = 0, off_hash = 0;  // symbols in the store; FNV-1a of its offsets (nmz_ed_plan_fingerprint)
     uint16_t *d_qsym = nullptr, *d_csym = nullptr;
     uint64_t *d_qoff = nullptr, *d_coff = nullptr;
     uint32_t *d_gmax = nullptr, *d_len = nullptr;
@@ -526,19 +526,19 @@ constexpr uint64_t ED_DEVICE_REMAP_MIN = 1ULL << 20;
 // the two-phase search (filter tiles, then DP work items) when the q-gram filter is on; NMZ_ED_TWO_PHASE=0 keeps
 // the single-kernel search with its in-workgroup pre-filter (A/B runs)
 static bool ed_two_phase_enabled() {
-    const char *e = getenv("NMZ_ED_TWO_PHASE");
+    const char *e = ab_env("NMZ_ED_TWO_PHASE");
     return !(e && atoi(e) == 0);
 }
 
 static bool ed_qgram_enabled() {
-    const char *e = getenv("NMZ_ED_QGRAM");
+    const char *e = ab_env("NMZ_ED_QGRAM");
     return !(e && atoi(e) == 0);
 }
 
 // queries per block row of the bit-parallel search (NMZ_ED_RW overrides the multiple of 64 for A/B runs)
 static uint32_t ed_bv_row_queries() {
     static const uint32_t rq = [] {
-        const char *e = getenv("NMZ_ED_RW");
+        const char *e = ab_env("NMZ_ED_RW");
         const int v = e ? atoi(e) : (int)ED_BV_RW;
         return 64u * (uint32_t)((v >= 1 && v <= 32) ? v : (int)ED_BV_RW);
     }();
@@ -550,7 +550,7 @@ static uint32_t ed_bv_row_queries() {
 // bit-parallel LDS tables) so the caller falls back to the host build and the other kernels.
 // d_sym_in: the symbols already on the device (nmz_ed_plan_create_dev), else uploaded from sym.
 static int ed_plan_build_bv_device(nmz_ed_plan *p, const uint64_t *off, const uint64_t *sym, uint32_t N,
-                                   uint32_t band, uint32_t maxlen, const uint64_t *d_sym_in) {
+                                   uint32_t band, uint32_t maxlen, const uint64_t *d_sym_in, bool compact_opt) {
     hipStream_t st = p->ctx->stream;
     const uint64_t total = off[N];
     NMZ_CHECK(total == 0 || sym || d_sym_in, "sym is NULL");
@@ -580,14 +580,14 @@ static int ed_plan_build_bv_device(nmz_ed_plan *p, const uint64_t *off, const ui
     const uint32_t rq = ed_bv_row_queries();
     const uint32_t n_sym = (uint32_t)n_uniq, G = (N + rq - 1) / rq;
     p->pool = N >= 24576 ? 4 * ED_BV_POOL : (N >= 12288 ? 2 * ED_BV_POOL : ED_BV_POOL);
-    if (const char *e = getenv("NMZ_ED_POOL")) {
+    if (const char *e = ab_env("NMZ_ED_POOL")) {
         const uint32_t v = (uint32_t)atoi(e);
         if (v >= 256 && v % 256 == 0 && v <= 16384) p->pool = v;
     }
     // direct tables (every symbol of the store has a row) when they fit beside the pool kernels' extras, else
     // compact tables (decided after the streams exist: they need the traces' distinct counts)
     const uint64_t direct_bytes = (((uint64_t)(n_sym + 1) * ndw * 8 + 15) / 16) * 16;
-    const bool cmp = direct_bytes + bv_pool_extras(p->pool) > 65536 || getenv("NMZ_ED_COMPACT") != nullptr;
+    const bool cmp = direct_bytes + bv_pool_extras(p->pool) > 65536 || compact_opt;
     if (cmp) p->pool = std::min(p->pool, ED_BV_POOL);  // the single kernel's survivor list leaves room for rows
     p->bv = true;
     p->fast = true;
@@ -752,23 +752,39 @@ static int ed_plan_build_wide_device(nmz_ed_plan *p, const uint64_t *off, const 
 
 // d_sym: the symbols on the device instead of sym (host); the host build paths take a copy of them
 static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, uint32_t N, uint32_t band,
-                         nmz_ed_plan **out, const uint64_t *d_sym = nullptr) {
+                         nmz_ed_plan **out, const uint64_t *d_sym = nullptr, uint32_t opts = 0) {
     NMZ_CHECK(ctx && out, "NULL argument");
     NMZ_CHECK(N == 0 || off, "off is NULL");
+    NMZ_CHECK((opts & ~(uint32_t)(NMZ_ED_OPT_SINGLE_KERNEL | NMZ_ED_OPT_NO_QGRAM | NMZ_ED_OPT_COMPACT |
+                                  NMZ_ED_OPT_HOST_BUILD)) == 0, "unknown plan option bits");
+    // the A/B environment knobs (NMZ_AB=1 only) add to the options
+    if (!ed_two_phase_enabled()) opts |= NMZ_ED_OPT_SINGLE_KERNEL;
+    if (!ed_qgram_enabled()) opts |= NMZ_ED_OPT_NO_QGRAM;
+    if (ab_env("NMZ_ED_COMPACT")) opts |= NMZ_ED_OPT_COMPACT;
+    if (ab_env("NMZ_ED_HOST_REMAP")) opts |= NMZ_ED_OPT_HOST_BUILD;
     *out = nullptr;
     auto *p = new nmz_ed_plan();
-    p->qgram = ed_qgram_enabled();
-    p->two_phase = ed_two_phase_enabled();
-    p->ctx = ctx;
-    p->n = N;
-    p->band = band;
+    auto init = [&] {
+        p->qgram = !(opts & NMZ_ED_OPT_NO_QGRAM);
+        p->two_phase = !(opts & NMZ_ED_OPT_SINGLE_KERNEL);
+        p->opts = opts;
+        p->ctx = ctx;
+        p->n = N;
+        p->band = band;
+        p->total = N ? off[N] : 0;
+        uint64_t h = 0xcbf29ce484222325ull;  // FNV-1a over the offsets: the store's shape, for the fingerprint
+        for (uint32_t i = 0; i <= N; ++i) h = (h ^ off[i]) * 0x100000001b3ull;
+        p->off_hash = h;
+    };
+    init();
+    const bool compact_opt = (opts & NMZ_ED_OPT_COMPACT) != 0, host_build = (opts & NMZ_ED_OPT_HOST_BUILD) != 0;
     hipStream_t st = ctx->stream;
     const uint64_t total = N ? off[N] : 0;
     uint32_t maxlen = 0;
     for (uint32_t i = 0; i < N; ++i) maxlen = std::max<uint32_t>(maxlen, (uint32_t)(off[i + 1] - off[i]));
     if (ed_bv_supported(band) && maxlen + ed_bv_template(band) < MAX_FAST_LEN && total >= ED_DEVICE_REMAP_MIN &&
-        total < (1ULL << 31) && !getenv("NMZ_ED_HOST_REMAP")) {
-        const int rc = ed_plan_build_bv_device(p, off, sym, N, band, maxlen, d_sym);
+        total < (1ULL << 31) && !host_build) {
+        const int rc = ed_plan_build_bv_device(p, off, sym, N, band, maxlen, d_sym, compact_opt);
         if (rc == NMZ_OK) {
             *out = p;
             return NMZ_OK;
@@ -778,13 +794,9 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         delete p;
         if (!not_applicable) return rc;
         p = new nmz_ed_plan();  // alphabet too large for the bit-parallel tables: host build below
-        p->qgram = ed_qgram_enabled();
-        p->two_phase = ed_two_phase_enabled();
-        p->ctx = ctx;
-        p->n = N;
-        p->band = band;
+        init();
     }
-    if (ed_wide_supported(band) && total >= ED_DEVICE_REMAP_MIN && !getenv("NMZ_ED_HOST_REMAP")) {
+    if (ed_wide_supported(band) && total >= ED_DEVICE_REMAP_MIN && !host_build) {
         const int rc = ed_plan_build_wide_device(p, off, sym, N, band, maxlen, d_sym);
         if (rc == NMZ_OK) {
             *out = p;
@@ -794,11 +806,7 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         delete p;
         if (rc != 1) return rc;
         p = new nmz_ed_plan();  // alphabet or tables too large: the host build below
-        p->qgram = ed_qgram_enabled();
-        p->two_phase = ed_two_phase_enabled();
-        p->ctx = ctx;
-        p->n = N;
-        p->band = band;
+        init();
     }
     std::vector<uint64_t> hsym;  // the host paths read the symbols on the host
     if (d_sym && total) {
@@ -841,7 +849,7 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
     uint32_t n_sym = 0;
     const uint32_t pool0 = [&] {
         uint32_t pl = N >= 24576 ? 4 * ED_BV_POOL : (N >= 12288 ? 2 * ED_BV_POOL : ED_BV_POOL);
-        if (const char *e = getenv("NMZ_ED_POOL")) {
+        if (const char *e = ab_env("NMZ_ED_POOL")) {
             const uint32_t v = (uint32_t)atoi(e);
             if (v >= 256 && v % 256 == 0 && v <= 16384) pl = v;
         }
@@ -857,7 +865,7 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
         p->bw = bw;
         p->ndw = ndw;
         p->row_bytes = ndw * 8;
-        if (lds_bytes + bv_pool_extras(pool0) <= 65536 && !getenv("NMZ_ED_COMPACT")) {
+        if (lds_bytes + bv_pool_extras(pool0) <= 65536 && !compact_opt) {
             p->bv = true;
             p->lds_dw = (uint32_t)(lds_bytes / 4);
         } else {
@@ -1038,7 +1046,7 @@ __global__ void k_bv_items(const uint32_t *__restrict__ cnt, uint32_t n, uint32_
 // leave CUs idle until they end, so their length is the launch's tail (~1 item per CU slot): a shard of the
 // 8-GPU search has 1/8 of the items, so the tail weighs 8x more there.
 uint32_t ed_bv_item() {
-    if (const char *e = getenv("NMZ_ED_ITEM")) {
+    if (const char *e = ab_env("NMZ_ED_ITEM")) {
         const uint32_t v = (uint32_t)atoi(e);
         if (v >= 64 && v <= ED_BV_ITEM && (v & (v - 1)) == 0) return v;
     }
@@ -1052,24 +1060,9 @@ uint32_t ed_bv_item() {
 constexpr uint64_t ED_TP_MAX_ENTRIES = 1ULL << 30;  // 4 GiB of entries
 constexpr uint64_t ED_TP_MAX_REC_BYTES = 1ULL << 30;
 
-// The shard that owns query block qb (64 queries) of the two-phase search: rotated snake order. A query block's
-// work falls with qb inside the upper triangle (fewer candidates j > q) and inside every family of near-duplicates;
-// in each period of 2S blocks, block r and its mirror 2S-1-r form pair min(r, 2S-1-r), so linear trends cancel, and
-// the pair goes to shard (pair + period) mod S, so over the periods every shard takes every pair position. (A plain
-// snake gives shard s the same two positions in every period: when the work's own period matches -- families of 16
-// blocks at 8 shards -- shard 0 always held each family's first and last block, whose short candidate lists run the
-// DP less efficiently (1.15x); the MurmurHash3 deal of round 2 left max/mean 1.15. DESIGN.md section 6.) A fixed
-// rule, not a knob: one process per GPU computes its own shards' tiles, so the rule must be the same everywhere.
-// (Dealing runs of 4 or 16 consecutive blocks instead, to keep a family's candidates in one shard's L2, measured
-// worse: 8-shard sum / unsharded 1.17 / 1.16 clustered vs 1.14; profiles/r04/ed_deal_chunk_ab.)
-static uint32_t ed_block_shard(uint32_t qb, uint32_t n_shards) {
-    if (n_shards <= 1) return 0;
-    const uint32_t r = qb % (2 * n_shards), pr = r < n_shards ? r : 2 * n_shards - 1 - r;
-    return (pr + qb / (2 * n_shards)) % n_shards;
-}
 // the entry-list limit (NMZ_ED_TP_MAX_ENTRIES lowers it, so tests can force the single-kernel fallback)
 static uint64_t ed_tp_max_entries() {
-    if (const char *e = getenv("NMZ_ED_TP_MAX_ENTRIES")) {
+    if (const char *e = ab_env("NMZ_ED_TP_MAX_ENTRIES")) {
         const unsigned long long v = strtoull(e, nullptr, 10);
         if (v < ED_TP_MAX_ENTRIES) return v;
     }
@@ -1168,8 +1161,11 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     Q.recs = nullptr;
     Q.rec_cap = 0;
     // (NMZ_ED_QG_RECOMPUTE=1 skips the records: the recompute path, for tests)
-    const char *rc_env = getenv("NMZ_ED_QG_RECOMPUTE");
-    if (!(rc_env && atoi(rc_env) == 1) && p->tp_rec.ensure(Carve::bytes_for(rec_cap * 32 + 16, 1)) == NMZ_OK) {
+    const char *rc_env = ab_env("NMZ_ED_QG_RECOMPUTE");
+    // (the kernels count records with a u32 atomic, up to 128 per tile: a launch that could pass 2^32 of them would
+    // wrap the counter, so such searches recompute instead)
+    if (!(rc_env && atoi(rc_env) == 1) && n_tiles_all * 128 < (1ULL << 32) &&
+        p->tp_rec.ensure(Carve::bytes_for(rec_cap * 32 + 16, 1)) == NMZ_OK) {
         Q.recs = p->tp_rec.as<uint4>() + 1;
         Q.rec_cap = (uint32_t)rec_cap;
     }
@@ -1182,11 +1178,12 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     Q.n_shards = n_shards;
     Q.w = p->band;
     const uint32_t item = ed_bv_item();
-    // count pass + scans over tiles [t0, t1): entry and item totals
+    const uint64_t limit = std::min<uint64_t>(ed_tp_max_entries(), 0xFFFFFFFFull);
+    // count pass + scans over a tile list: entry and item totals
     uint32_t n_rec = 0;
-    auto count = [&](uint64_t t0, uint64_t t1, uint64_t &tot64, uint32_t &tot_items) -> int {
-        Q.tiles = tl.as<uint64_t>() + t0;
-        Q.n_tiles = t1 - t0;
+    auto count = [&](const uint64_t *tiles, uint64_t n_tiles, uint64_t &tot64, uint32_t &tot_items) -> int {
+        Q.tiles = tiles;
+        Q.n_tiles = n_tiles;
         NMZ_HIP(hipMemsetAsync(d_cnt, 0, (n_pairs + 1) * 4, st));
         if (Q.recs) NMZ_HIP(hipMemsetAsync(Q.n_rec, 0, 4, st));
         {
@@ -1209,6 +1206,8 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     };
     // write pass + DP of the tiles the last count pass covered
     auto write_dp = [&](uint64_t n_ent, uint32_t n_items) -> int {
+        // the u32 scans (entry and item offsets) hold only below 2^32 entries: a batch must never reach it
+        NMZ_CHECK(n_ent <= limit && n_ent < (1ULL << 32), "internal: a two-phase batch exceeds the entry limit");
         NMZ_TRY(p->tp_ent.ensure(Carve::bytes_for(n_ent + 1, 4)));
         Q.ent = p->tp_ent.as<uint32_t>();
         NMZ_HIP(hipMemcpyAsync(d_cur, d_poff, (uint64_t)n_pairs * 4, hipMemcpyDeviceToDevice, st));
@@ -1222,8 +1221,7 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     };
     uint64_t tot64 = 0;
     uint32_t tot_items = 0;
-    NMZ_TRY(count(0, n_tiles_all, tot64, tot_items));
-    const uint64_t limit = ed_tp_max_entries();
+    NMZ_TRY(count(tl.as<uint64_t>(), n_tiles_all, tot64, tot_items));
     if (tot64 <= limit) return write_dp(tot64, tot_items);
     // batches of whole query blocks: per-block totals from this count pass, then the lists and counters start over
     // (the count pass lists pairs with an empty trace, and adds to the counters)
@@ -1233,22 +1231,58 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     const size_t ng = grp.size() / 2;
     hipLaunchKernelGGL(k_knn_init, dim3(ceil_div((uint64_t)N * A.k, 256)), dim3(256), 0, st, d_knn, (uint64_t)N * A.k);
     NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_CNT_WORDS * 8, st));
+    // a query block's entry total (this count pass's per-pair counts)
+    auto block_entries = [&](size_t i) {
+        uint64_t c = 0;
+        for (uint32_t pp = 32 * qbs[i]; pp < std::min(32 * qbs[i] + 32, n_pairs); ++pp) c += cnt[pp];
+        return c;
+    };
+    DevBuf sub;  // the tile list of a batch narrower than one group (uploaded per batch)
+    struct R3 {
+        DevBuf &b;
+        ~R3() { b.release(); }
+    } rel_sub{sub};
     for (size_t b0 = 0; b0 < ng;) {
         uint64_t acc = 0;
         size_t b1 = b0;
         while (b1 < ng) {
             const size_t i1 = b1 + 1 < ng ? grp[2 * (b1 + 1)] : qbs.size();
             uint64_t c = 0;
-            for (size_t i = grp[2 * b1]; i < i1; ++i)
-                for (uint32_t pp = 32 * qbs[i]; pp < std::min(32 * qbs[i] + 32, n_pairs); ++pp) c += cnt[pp];
-            if (b1 > b0 && acc + c > limit) break;
+            for (size_t i = grp[2 * b1]; i < i1; ++i) c += block_entries(i);
+            if (acc + c > limit) break;
             acc += c;
             ++b1;
         }
-        const uint64_t t0 = grp[2 * b0 + 1], t1 = b1 < ng ? grp[2 * b1 + 1] : n_tiles_all;
-        NMZ_TRY(count(t0, t1, tot64, tot_items));
-        NMZ_TRY(write_dp(tot64, tot_items));
-        b0 = b1;
+        if (b1 > b0) {  // whole groups: their tiles are one contiguous range of the shard's list
+            const uint64_t t0 = grp[2 * b0 + 1], t1 = b1 < ng ? grp[2 * b1 + 1] : n_tiles_all;
+            NMZ_TRY(count(tl.as<uint64_t>() + t0, t1 - t0, tot64, tot_items));
+            NMZ_TRY(write_dp(tot64, tot_items));
+            b0 = b1;
+            continue;
+        }
+        // one group alone exceeds the limit: its query blocks in sub-batches, each with its own tile list (the
+        // group's superblock order, restricted to the sub-batch's blocks); a single block beyond the limit cannot
+        // be split further (64 queries x N candidates: N > 2^24 at the default limit) and fails loudly
+        const size_t i0 = grp[2 * b0], i1 = b0 + 1 < ng ? grp[2 * (b0 + 1)] : qbs.size();
+        for (size_t j0 = i0; j0 < i1;) {
+            uint64_t a = 0;
+            size_t j1 = j0;
+            while (j1 < i1 && (j1 == j0 || a + block_entries(j1) <= limit)) a += block_entries(j1++);
+            NMZ_CHECK(a <= limit, "one query block's candidate entries exceed the two-phase limit (too many traces)");
+            std::vector<uint64_t> tiles;
+            for (uint32_t cb0 = qbs[j0] / 4; cb0 < NCB; cb0 += ED_SC)
+                for (size_t i = j0; i < j1; ++i)
+                    for (uint32_t cb = std::max(cb0, qbs[i] / 4); cb < std::min(NCB, cb0 + ED_SC); ++cb)
+                        tiles.push_back(((uint64_t)qbs[i] << 32) | cb);
+            NMZ_TRY(sub.ensure(Carve::bytes_for(tiles.size() + 1, 8)));
+            NMZ_HIP(hipStreamSynchronize(st));  // the previous sub-batch's kernels have read the list
+            if (!tiles.empty())
+                NMZ_HIP(hipMemcpy(sub.ptr, tiles.data(), tiles.size() * 8, hipMemcpyHostToDevice));
+            NMZ_TRY(count(sub.as<uint64_t>(), tiles.size(), tot64, tot_items));
+            NMZ_TRY(write_dp(tot64, tot_items));
+            j0 = j1;
+        }
+        b0 = b0 + 1;
     }
     return NMZ_OK;
 }
@@ -1308,18 +1342,11 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
             if (rc < 0) return rc;
         }
         if (rc == 1) {  // the single-kernel search (no q-gram filter, or N >= 2^30): a plan-wide choice
-            // this shard's chunks per row: cr = ((shard - b) mod n_shards) + n_shards * t
-            std::vector<uint64_t> &ss = p->shard_start[((uint64_t)shard << 32) | n_shards];
-            if (ss.empty()) {
-                ss.assign(p->G + 1, 0);
-                for (uint32_t b = 0; b < p->G; ++b) {
-                    const uint64_t nch = p->row_chunks[b], rot = (shard + n_shards - b % n_shards) % n_shards;
-                    ss[b + 1] = ss[b] + (rot < nch ? (nch - rot + n_shards - 1) / n_shards : 0);
-                }
-            }
-            A.n_chunks = ss[p->G];
+            // every (row, chunk) of the plan is launched; a workgroup whose query block this shard does not own
+            // (ed_block_shard, the two-phase search's rule) exits at once, so a shard owns the same pairs whichever
+            // form of the search its plan took
+            A.n_chunks = p->n_chunks;
             if (A.n_chunks > 0) {
-                NMZ_HIP(hipMemcpyAsync(p->d_chunk_start, ss.data(), (p->G + 1) * 8, hipMemcpyHostToDevice, st));
                 A.rq = p->rq;
                 uint64_t blocks = A.n_chunks * (p->rq / 2);
                 blocks = (blocks + 7) / 8 * 8;
@@ -1718,6 +1745,30 @@ int nmz_ed_plan_create_dev(nmz_ctx *ctx, const uint64_t *off, const uint64_t *d_
     CtxGuard g(ctx);
     NMZ_TRY(g.rc);
     return ed_plan_build(ctx, off, nullptr, n_traces, band, out, d_sym);
+}
+
+int nmz_ed_plan_create_opts(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, const uint64_t *d_sym,
+                            uint32_t n_traces, uint32_t band, uint32_t opts, nmz_ed_plan **out) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    NMZ_CHECK(n_traces == 0 || off, "off is NULL");
+    NMZ_CHECK(!(sym && d_sym), "pass sym (host) or d_sym (device), not both");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    return ed_plan_build(ctx, off, sym, n_traces, band, out, d_sym, opts);
+}
+
+int nmz_ed_plan_fingerprint(const nmz_ed_plan *p, uint64_t *fp) {
+    NMZ_CHECK(p != nullptr && fp != nullptr, "NULL argument");
+    const uint64_t kind = p->wide ? 3 : (p->bv ? 2 : (p->fast ? 1 : 0));
+    fp[0] = NMZ_ED_FP_VERSION;
+    fp[1] = kind | (uint64_t)p->band << 8 | (uint64_t)(p->bv ? p->bw : p->ww) << 40;
+    fp[2] = p->n;
+    fp[3] = p->total;
+    fp[4] = (uint64_t)p->two_phase | (uint64_t)p->qgram << 1 | (uint64_t)p->cmp << 2;
+    fp[5] = (uint64_t)p->rq | (uint64_t)p->pool << 32;
+    fp[6] = p->off_hash;
+    fp[7] = p->n_sym;
+    return NMZ_OK;
 }
 
 int nmz_ed_allpairs_knn_dev(nmz_ed_plan *plan, uint32_t k, uint64_t *d_knn_keys, void *stream) {

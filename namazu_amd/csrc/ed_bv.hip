@@ -512,19 +512,19 @@ __global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv(EdBvArgs A) {
     const uint32_t wpc = A.rq / 2;  // workgroups per chunk
     const uint64_t lchunk = lb / wpc;
     if (lchunk >= A.n_chunks) return;
-    // this shard's lchunk-th chunk: row b (binary search of the shard's per-row starts), then the row's
-    // chunks dealt round-robin starting at rank (b mod n_shards), so every rank gets every n_shards-th chunk
-    // of every row and the chunks next to the diagonal rotate over the ranks row by row
+    // the lchunk-th chunk of the plan: row b (binary search of the per-row chunk starts), chunk cr of the row
     uint32_t lo = 0, hi = A.G;
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) / 2;
         if (A.chunk_start[mid] <= lchunk) lo = mid; else hi = mid;
     }
     const uint32_t b = lo;
-    const uint32_t rot = (A.shard + A.n_shards - b % A.n_shards) % A.n_shards;
-    const uint32_t cr = rot + A.n_shards * (uint32_t)(lchunk - A.chunk_start[b]);
+    const uint32_t cr = (uint32_t)(lchunk - A.chunk_start[b]);
     const uint32_t q1 = A.rq * b + 2 * (lb % wpc), q2 = q1 + 1;
     if (q1 >= A.N) return;  // whole workgroup
+    // the shard owns whole 64-query blocks (ed_block_shard, as in the two-phase search); q1 is even, so q1 and q2
+    // share one block
+    if (ed_block_shard(q1 / 64, A.n_shards) != A.shard) return;
     const bool has2 = q2 < A.N;
     const uint32_t n1 = A.len[q1], n2 = has2 ? A.len[q2] : 0;
     const uint32_t c0 = A.rq * b + A.pool * cr;

@@ -161,6 +161,53 @@ static int group_allgather(nmz_group *g, const std::vector<void *> &send, const 
     return NMZ_OK;
 }
 
+// Every member's `words` u64 (its local status first) to every member, rank order: one small RCCL all_gather that a
+// member which failed locally still enters, so no rank is left waiting in a collective another rank skipped.
+// all[i] = [n_ranks][words] as member i received it.
+static int group_exchange_words(nmz_group *g, const std::vector<std::vector<uint64_t>> &mine, size_t words,
+                                std::vector<std::vector<uint64_t>> &all) {
+    const size_t R = (size_t)g->n_ranks, n = g->m.size();
+    std::vector<DevBuf> buf(n);
+    std::vector<void *> send(n), recv(n);
+    all.assign(n, std::vector<uint64_t>(R * words, 0));
+    int rc = run_all(g, [&](size_t i) {
+        NMZ_TRY(buf[i].ensure(Carve::bytes_for(words, 8) + Carve::bytes_for(R * words, 8)));
+        Carve cv(buf[i].ptr);
+        send[i] = cv.take<uint64_t>(words);
+        recv[i] = cv.take<uint64_t>(R * words);
+        NMZ_HIP(hipMemcpy(send[i], mine[i].data(), words * 8, hipMemcpyHostToDevice));
+        return NMZ_OK;
+    });
+    if (rc == NMZ_OK) rc = group_allgather(g, send, recv, words * 8);
+    if (rc == NMZ_OK)
+        rc = run_all(g, [&](size_t i) {
+            NMZ_HIP(hipMemcpyAsync(all[i].data(), recv[i], R * words * 8, hipMemcpyDeviceToHost, g->m[i].ctx->stream));
+            NMZ_HIP(hipStreamSynchronize(g->m[i].ctx->stream));
+            return NMZ_OK;
+        });
+    const std::string msg = rc == NMZ_OK ? std::string() : std::string(nmz_last_error());
+    (void)run_all(g, [&](size_t i) {
+        buf[i].release();
+        return NMZ_OK;
+    });
+    return rc == NMZ_OK ? NMZ_OK : fail(rc, msg);
+}
+
+// after a step each member ran locally (status st[i], message msg[i]): every rank learns every rank's status;
+// NMZ_OK only when all succeeded, else the first failure (this process's own message when it failed here)
+static int group_agree_status(nmz_group *g, const std::vector<int> &st, const std::vector<std::string> &msg,
+                              const char *what) {
+    std::vector<std::vector<uint64_t>> mine(g->m.size()), all;
+    for (size_t i = 0; i < g->m.size(); ++i) mine[i] = {(uint64_t)(int64_t)st[i]};
+    NMZ_TRY(group_exchange_words(g, mine, 1, all));
+    for (size_t i = 0; i < g->m.size(); ++i)
+        if (st[i] != NMZ_OK) return fail(st[i], msg[i]);
+    for (size_t r = 0; r < all[0].size(); ++r)
+        if (all[0][r] != 0)
+            return fail((int)(int64_t)all[0][r], std::string(what) + " failed on rank " + std::to_string(r));
+    return NMZ_OK;
+}
+
 // the member whose copy of a merged result goes to the host: every rank of a multi-process group returns
 // its own (identical) copy; in one process, member 0's
 static bool reports(const nmz_group *g, size_t i) { return g->multi_process || i == 0; }
@@ -248,6 +295,7 @@ struct nmz_ed_group_plan {
     nmz_group *g;
     std::vector<nmz_ed_plan *> p;
     uint32_t n;
+    uint32_t opts = 0;  // NMZ_ED_OPT_* of every member's plan
     std::vector<double> upload_ms, gather_ms, build_ms;  // per local member (nmz_ed_group_plan_timing)
 };
 
@@ -606,6 +654,11 @@ int nmz_random_sweep_topk_group(nmz_group *g, uint64_t seed0, uint64_t n_seeds, 
 // ---- all-pairs banded edit distance k-NN ---------------------------------------------------------------------
 int nmz_ed_group_plan_create(nmz_group *g, const uint64_t *off, const uint64_t *sym, uint32_t n_traces,
                              uint32_t band, nmz_ed_group_plan **out) {
+    return nmz_ed_group_plan_create_opts(g, off, sym, n_traces, band, 0, out);
+}
+
+int nmz_ed_group_plan_create_opts(nmz_group *g, const uint64_t *off, const uint64_t *sym, uint32_t n_traces,
+                                  uint32_t band, uint32_t opts, nmz_ed_group_plan **out) {
     DeviceRestore dr;
     NMZ_CHECK(g && out, "NULL argument");
     *out = nullptr;
@@ -614,6 +667,7 @@ int nmz_ed_group_plan_create(nmz_group *g, const uint64_t *off, const uint64_t *
     auto *gp = new nmz_ed_group_plan();
     gp->g = g;
     gp->n = n_traces;
+    gp->opts = opts;
     gp->p.assign(g->m.size(), nullptr);
     gp->upload_ms.assign(g->m.size(), 0.0);
     gp->gather_ms.assign(g->m.size(), 0.0);
@@ -629,35 +683,75 @@ int nmz_ed_group_plan_create(nmz_group *g, const uint64_t *off, const uint64_t *
     std::vector<void *> send(g->m.size()), recv(g->m.size());
     using clk = std::chrono::steady_clock;
     auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
-    int rc = run_all(g, [&](size_t i) {
-        const auto t0 = clk::now();
-        GroupMember &mb = g->m[i];
-        hipStream_t st = mb.ctx->stream;
-        NMZ_TRY(full[i].ensure(Carve::bytes_for(share * R, 8)));
-        uint64_t *d = full[i].as<uint64_t>();
-        const uint64_t lo = std::min<uint64_t>((uint64_t)mb.rank * share, total);
-        const uint64_t hi = std::min<uint64_t>(lo + share, total);
-        if (hi > lo) NMZ_HIP(hipMemcpyAsync(d + (uint64_t)mb.rank * share, sym + lo, (hi - lo) * 8, hipMemcpyHostToDevice, st));
-        if (hi - lo < share)
-            NMZ_HIP(hipMemsetAsync(d + (uint64_t)mb.rank * share + (hi - lo), 0, (share - (hi - lo)) * 8, st));
-        NMZ_HIP(hipStreamSynchronize(st));  // pageable source
-        send[i] = d + (uint64_t)mb.rank * share;
-        recv[i] = d;
-        gp->upload_ms[i] = ms_since(t0);
+    // Each step that a rank runs locally (upload, plan build) is followed by an exchange of every rank's status, so
+    // a rank that failed does not leave the others waiting in the next collective (and all of them fail); after the
+    // build the ranks exchange their plans' fingerprints (nmz_ed_plan_fingerprint) and fail with NMZ_EINVAL when they
+    // differ: ranks whose plans took different kernels or stores would not search the same pairs.
+    const size_t n = g->m.size();
+    std::vector<int> st(n, NMZ_OK);
+    std::vector<std::string> msg(n);
+    auto local = [&](size_t i, const std::function<int()> &fn) {
+        st[i] = fn();
+        if (st[i] != NMZ_OK) msg[i] = nmz_last_error();
         return NMZ_OK;
+    };
+    int rc = run_all(g, [&](size_t i) {
+        return local(i, [&] {
+            const auto t0 = clk::now();
+            GroupMember &mb = g->m[i];
+            hipStream_t stm = mb.ctx->stream;
+            NMZ_TRY(full[i].ensure(Carve::bytes_for(share * R, 8)));
+            uint64_t *d = full[i].as<uint64_t>();
+            const uint64_t lo = std::min<uint64_t>((uint64_t)mb.rank * share, total);
+            const uint64_t hi = std::min<uint64_t>(lo + share, total);
+            if (hi > lo)
+                NMZ_HIP(hipMemcpyAsync(d + (uint64_t)mb.rank * share, sym + lo, (hi - lo) * 8, hipMemcpyHostToDevice,
+                                       stm));
+            if (hi - lo < share)
+                NMZ_HIP(hipMemsetAsync(d + (uint64_t)mb.rank * share + (hi - lo), 0, (share - (hi - lo)) * 8, stm));
+            NMZ_HIP(hipStreamSynchronize(stm));  // pageable source
+            send[i] = d + (uint64_t)mb.rank * share;
+            recv[i] = d;
+            gp->upload_ms[i] = ms_since(t0);
+            return NMZ_OK;
+        });
     });
+    if (rc == NMZ_OK) rc = group_agree_status(g, st, msg, "the store upload");
     if (rc == NMZ_OK) {
         const auto t0 = clk::now();
         rc = group_allgather(g, send, recv, share * 8);
         if (rc == NMZ_OK)
             rc = run_all(g, [&](size_t i) {
-                NMZ_HIP(hipStreamSynchronize(g->m[i].ctx->stream));
-                gp->gather_ms[i] = ms_since(t0);
-                const auto t1 = clk::now();
-                NMZ_TRY(nmz_ed_plan_create_dev(g->m[i].ctx, off, full[i].as<uint64_t>(), n_traces, band, &gp->p[i]));
-                gp->build_ms[i] = ms_since(t1);
-                return NMZ_OK;
+                return local(i, [&] {
+                    NMZ_HIP(hipStreamSynchronize(g->m[i].ctx->stream));
+                    gp->gather_ms[i] = ms_since(t0);
+                    const auto t1 = clk::now();
+                    NMZ_TRY(nmz_ed_plan_create_opts(g->m[i].ctx, off, nullptr, full[i].as<uint64_t>(), n_traces, band,
+                                                    gp->opts, &gp->p[i]));
+                    gp->build_ms[i] = ms_since(t1);
+                    return NMZ_OK;
+                });
             });
+    }
+    // the plans' fingerprints, with each rank's build status in front
+    if (rc == NMZ_OK) {
+        constexpr size_t W = 1 + NMZ_ED_FP_WORDS;
+        std::vector<std::vector<uint64_t>> mine(n, std::vector<uint64_t>(W, 0)), all;
+        for (size_t i = 0; i < n; ++i) {
+            mine[i][0] = (uint64_t)(int64_t)st[i];
+            if (st[i] == NMZ_OK) (void)nmz_ed_plan_fingerprint(gp->p[i], mine[i].data() + 1);
+        }
+        rc = group_exchange_words(g, mine, W, all);
+        for (size_t i = 0; rc == NMZ_OK && i < n; ++i)
+            if (st[i] != NMZ_OK) rc = fail(st[i], msg[i]);
+        for (size_t r = 0; rc == NMZ_OK && r < (size_t)R; ++r) {
+            if (all[0][r * W] != 0)
+                rc = fail((int)(int64_t)all[0][r * W], "the plan build failed on rank " + std::to_string(r));
+            else if (!std::equal(all[0].begin() + r * W, all[0].begin() + (r + 1) * W, all[0].begin()))
+                rc = fail(NMZ_EINVAL, "ranks built different edit-distance plans (fingerprint of rank " +
+                                          std::to_string(r) + " differs from rank 0's): kernel, band, store or "
+                                          "search options disagree");
+        }
     }
     (void)run_all(g, [&](size_t i) {  // the plans hold what they need
         (void)hipStreamSynchronize(g->m[i].ctx->stream);
@@ -665,10 +759,10 @@ int nmz_ed_group_plan_create(nmz_group *g, const uint64_t *off, const uint64_t *
         return NMZ_OK;
     });
     if (rc != NMZ_OK) {
-        const std::string msg = nmz_last_error();
+        const std::string m = nmz_last_error();
         for (auto *p : gp->p) (void)nmz_ed_plan_destroy(p);
         delete gp;
-        return fail(rc, msg);
+        return fail(rc, m);
     }
     ++g->n_plans;
     *out = gp;

@@ -279,6 +279,9 @@ inline void buckets_small(uint32_t *small, Buckets &b) {
 int bucket_seeds_counted(hipStream_t st, const uint64_t *d_h0, uint64_t n_seeds, uint32_t seeds_per_unit,
                          Buckets &b, uint32_t *zero_word = nullptr);
 // seeds per thread in the prefix + histogram kernels and in the scatter (tuning: NMZ_PREFIX_PT, NMZ_SCATTER_PT)
+// A/B and test knobs: an NMZ_* environment variable is read only when NMZ_AB=1 is set too, so that a production
+// process's environment never changes which kernel runs or how a search deals its pairs over ranks
+const char *ab_env(const char *name);
 uint32_t prefix_per_thread();
 uint32_t scatter_per_thread();
 

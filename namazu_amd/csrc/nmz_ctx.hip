@@ -205,8 +205,13 @@ __global__ __launch_bounds__(256) void k_bucket_scan(uint32_t *__restrict__ coun
 // (block, bucket) pair and one global atomic per non-empty pair reserves the
 // range, so the 256 global cursors see <= 256 atomics per block instead of one
 // per seed. Order inside a bucket is irrelevant: results go to the original index.
+const char *ab_env(const char *name) {
+    const char *ab = getenv("NMZ_AB");
+    return (ab && ab[0] == '1' && ab[1] == 0) ? getenv(name) : nullptr;
+}
+
 static uint32_t env_pow2(const char *name, uint32_t dflt, uint32_t lo, uint32_t hi) {
-    const char *e = getenv(name);
+    const char *e = ab_env(name);
     const uint32_t v = e ? (uint32_t)atoi(e) : dflt;
     return (v >= lo && v <= hi && (v & (v - 1)) == 0) ? v : dflt;
 }

@@ -24,6 +24,22 @@ struct Carve {
     static size_t bytes_for(size_t count, size_t elem) { return (count * elem + 255) & ~size_t(255); }
 };
 
+// The shard that owns query block qb (64 queries) of the bit-parallel search, in both its forms (two-phase and the
+// single kernel, so the pairs a shard owns do not depend on which form a rank's plan took): rotated snake order. A query block's
+// work falls with qb inside the upper triangle (fewer candidates j > q) and inside every family of near-duplicates;
+// in each period of 2S blocks, block r and its mirror 2S-1-r form pair min(r, 2S-1-r), so linear trends cancel, and
+// the pair goes to shard (pair + period) mod S, so over the periods every shard takes every pair position. (A plain
+// snake gives shard s the same two positions in every period: when the work's own period matches -- families of 16
+// blocks at 8 shards -- shard 0 always held each family's first and last block, whose short candidate lists run the
+// DP less efficiently (1.15x); the MurmurHash3 deal of round 2 left max/mean 1.15. DESIGN.md section 6.) A fixed
+// rule, not a knob: one process per GPU computes its own shards' tiles, so the rule must be the same everywhere.
+// (Dealing runs of 4 or 16 consecutive blocks instead, to keep a family's candidates in one shard's L2, measured
+// worse: 8-shard sum / unsharded 1.17 / 1.16 clustered vs 1.14; profiles/r04/ed_deal_chunk_ab.)
+__host__ __device__ inline uint32_t ed_block_shard(uint32_t qb, uint32_t n_shards) {
+    if (n_shards <= 1) return 0;
+    const uint32_t r = qb % (2 * n_shards), pr = r < n_shards ? r : 2 * n_shards - 1 - r;
+    return (pr + qb / (2 * n_shards)) % n_shards;
+}
 bool ed_bv_supported(uint32_t band);   // band <= 64
 uint32_t ed_bv_template(uint32_t band);  // the kernels' template band W >= band: 8, 16, 32 or 64
 // LDS of one bit-parallel workgroup: the kernels with a pool (k_ed_bv, k_ed_bv_dp) stay within 64 KiB (several

@@ -343,7 +343,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 // and fewer than 2^32 - 1 events per chunk (~e > 0). NMZ_RANDOM_K32=0 forces the general form.
 static bool random_k32(const RandomKParams &kp) {
     static const int env = [] {
-        const char *e = getenv("NMZ_RANDOM_K32");
+        const char *e = ab_env("NMZ_RANDOM_K32");
         return e ? atoi(e) : 1;
     }();
     if (!env) return false;
@@ -469,7 +469,7 @@ constexpr uint64_t RANDOM_EC_LARGE_SEEDS = 1ULL << 22;
 
 static uint32_t random_ec(uint64_t S) {
     static const uint32_t env = [] {
-        const char *e = getenv("NMZ_RANDOM_EC");
+        const char *e = ab_env("NMZ_RANDOM_EC");
         const uint32_t x = e ? (uint32_t)atoi(e) : 0u;
         return x >= 64 ? x : 0u;
     }();

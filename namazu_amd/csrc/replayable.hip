@@ -89,7 +89,7 @@ constexpr uint32_t REPLAY_SEEDS_PER_UNIT_MIN = 64 * 2;
 // tie flag -- 11 full-rate VOP2 per decision, no v_subb / v_max -- measured 0.98 ms.)
 static int replay_key_mode() {
     static int k = [] {
-        const char *e = getenv("NMZ_REPLAY_KEY");
+        const char *e = ab_env("NMZ_REPLAY_KEY");
         return (e && std::string(e) == "u64") ? 0 : 1;
     }();
     return k;
@@ -98,7 +98,7 @@ static int replay_key_mode() {
 // persistent workgroups (4 waves each) per CU: 8 = 8 waves/SIMD (NMZ_REPLAY_WG for A/B runs)
 static uint32_t replay_wg_per_cu() {
     static const uint32_t w = [] {
-        const char *e = getenv("NMZ_REPLAY_WG");
+        const char *e = ab_env("NMZ_REPLAY_WG");
         const int v = e ? atoi(e) : 8;
         return (uint32_t)((v >= 1 && v <= 16) ? v : 8);
     }();
@@ -108,7 +108,7 @@ static uint32_t replay_wg_per_cu() {
 // seeds per lane (default 2, the fastest measured; NMZ_REPLAY_U=2|4|8 for tuning)
 static int replay_u() {
     static int u = [] {
-        const char *e = getenv("NMZ_REPLAY_U");
+        const char *e = ab_env("NMZ_REPLAY_U");
         int v = e ? atoi(e) : 2;
         return (v == 2 || v == 4 || v == 8) ? v : 2;
     }();
@@ -1323,7 +1323,7 @@ constexpr uint32_t REPLAY_EC = 2048;  // events per work item (2048 vs 1024: sam
 
 static uint32_t replay_ec() {
     static uint32_t ec = [] {
-        const char *e = getenv("NMZ_REPLAY_EC");
+        const char *e = ab_env("NMZ_REPLAY_EC");
         uint32_t v = e ? (uint32_t)atoi(e) : REPLAY_EC;
         return (v >= 64 && v % 64 == 0) ? v : REPLAY_EC;
     }();
@@ -1334,7 +1334,7 @@ static uint32_t replay_ec() {
 // for rows too large for LDS)
 static bool replay_oq_enabled() {
     static const bool on = [] {
-        const char *e = getenv("NMZ_REPLAY_OQ");
+        const char *e = ab_env("NMZ_REPLAY_OQ");
         return !(e && std::string(e) == "0");
     }();
     return on;
@@ -1371,7 +1371,7 @@ static int oq_build(nmz_replayable_plan *p, const std::vector<ClassInfo> &cls, h
     p->oq_passes.clear();
     if (!p->mod.m32ok || E == 0) return NMZ_OK;
     uint64_t budget = OQ_LDS_MAX - OQ_TAIL_LDS;
-    if (const char *e = getenv("NMZ_REPLAY_OQ_BUDGET"))  // tests: force several passes on short traces
+    if (const char *e = ab_env("NMZ_REPLAY_OQ_BUDGET"))  // tests: force several passes on short traces
         budget = std::min<uint64_t>(budget, std::max<uint64_t>(4096, strtoull(e, nullptr, 10)));
     // segments: the classes whole when the whole row fits one pass, else sub-segments of <= OQ_SUBSEG events
     std::vector<ClassInfo> seg;
@@ -1523,7 +1523,7 @@ static bool use_wt(const nmz_replayable_plan *p) {
 // selection, for A/B runs)
 static bool wt_topk_enabled() {
     static const bool on = [] {
-        const char *e = getenv("NMZ_WT_TOPK");
+        const char *e = ab_env("NMZ_WT_TOPK");
         return !(e && std::string(e) == "0");
     }();
     return on;
@@ -1773,7 +1773,7 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
     // counters itself -- one upload and one launch. (NMZ_WT_FUSED=0 takes the separate kernels always: parity tests
     // and A/B runs.)
     std::vector<WtClass> woc;
-    const bool fused = E && !(getenv("NMZ_WT_FUSED") && atoi(getenv("NMZ_WT_FUSED")) == 0) &&
+    const bool fused = E && !(ab_env("NMZ_WT_FUSED") && atoi(ab_env("NMZ_WT_FUSED")) == 0) &&
                        wt_layout(p->wt, ctx, E, cls.data(), (uint32_t)cls.size(), p->mod, true, woc);
     size_t need = Carve::bytes_for(cls.size() + 1, sizeof(ClassInfo)) + Carve::bytes_for((size_t)256 * E + 1, 16) +
                   Carve::bytes_for(E + 1, 4) * 2 + Carve::bytes_for(nbytes + 1, 1);
@@ -1855,7 +1855,7 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
             uint32_t max_class = 0;
             for (const ClassInfo &c : cls) max_class = std::max(max_class, c.count);
             bool bad = false;
-            if (max_class <= SEG_SORT_MAX && !getenv("NMZ_REPLAY_RANKSORT")) {  // LDS bitonic sort per segment
+            if (max_class <= SEG_SORT_MAX && !ab_env("NMZ_REPLAY_RANKSORT")) {  // LDS bitonic sort per segment
                 hipLaunchKernelGGL(k_replayable_table_segsort, dim3(p->n_classes, 256), dim3(1024), 0, st,
                                    tmp.as<uint4>(), p->d_classes, E, p->d_table);
                 // no sync when the order-query images follow: oq_build synchronises after its kernels
@@ -2085,7 +2085,7 @@ int nmz_replayable_sweep_traces(nmz_ctx *ctx, uint32_t n_traces, const uint32_t 
     // builds and sweeps on four streams (NMZ_TRACES_MODE=0, profiles/r04/e2e_native_ab/). NMZ_TRACES_MODE=2: the
     // same, with trace i's top-k read after trace i + 1's sweep is enqueued instead of trace i + 2's
     static const int mode = [] {
-        const char *e = std::getenv("NMZ_TRACES_MODE");
+        const char *e = ab_env("NMZ_TRACES_MODE");
         return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 1;
     }();
     const bool same_stream = mode != 0;

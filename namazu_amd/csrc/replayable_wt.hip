@@ -1157,7 +1157,7 @@ static uint32_t bitlen(uint64_t x) {
 
 // read at every plan build (tests switch it per plan)
 bool wt_enabled() {
-    const char *e = getenv("NMZ_REPLAY_WT");
+    const char *e = ab_env("NMZ_REPLAY_WT");
     return !(e && std::string(e) == "0");
 }
 
@@ -1167,7 +1167,7 @@ static uint32_t wt_groups() {
         // one workgroup per row leaves half of each CU's wave slots and LDS to the step's other kernels (the seed
         // prefix, bucketing and top-k of the neighbouring pipelined steps): configs[1] step 0.116 -> 0.113 ms with
         // the fused top-k (profiles/r03y_wt_groups_ab.json); alone, 2 per row are 2 % faster
-        const char *e = getenv("NMZ_WT_G");
+        const char *e = ab_env("NMZ_WT_G");
         const int v = e ? atoi(e) : 1;
         return (uint32_t)((v == 1 || v == 2 || v == 4 || v == 8) ? v : 1);
     }();
@@ -1175,7 +1175,7 @@ static uint32_t wt_groups() {
 }
 static uint32_t wt_threads() {
     static const uint32_t t = [] {
-        const char *e = getenv("NMZ_WT_THREADS");
+        const char *e = ab_env("NMZ_WT_THREADS");
         const int v = e ? atoi(e) : 1024;
         return (uint32_t)((v >= 64 && v <= 1024 && v % 64 == 0) ? v : 1024);
     }();

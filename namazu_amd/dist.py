@@ -84,6 +84,27 @@ def all_gather_bytes(dist, tensor):
     return out
 
 
+def check_ed_plans(dist, L, plan, device="cpu"):
+    """Every rank's edit-distance plan fingerprint (nmz_ed_plan_fingerprint: kernel kind, band, store shape, search
+    options) to every rank; raises ValueError on every rank when any rank's differs from rank 0's. Ranks whose plans
+    took different kernels or hold different stores would not search the same pairs, and their merged k-NN would be
+    wrong without an error (the device groups make the same check inside nmz_ed_group_plan_create)."""
+    import ctypes
+
+    import torch
+
+    from namazu_amd import _lib
+    fp = np.zeros(_lib.NMZ_ED_FP_WORDS, np.uint64)
+    _lib.check(L.nmz_ed_plan_fingerprint(plan, ctypes.c_void_p(fp.ctypes.data)))
+    t = torch.from_numpy(fp.view(np.uint8).copy()).to(device)
+    parts = [p.cpu().numpy().view(np.uint64) for p in all_gather_bytes(dist, t)]
+    bad = [r for r, p in enumerate(parts) if not np.array_equal(p, parts[0])]
+    if bad:
+        raise ValueError(f"ranks {bad} built edit-distance plans whose fingerprint differs from rank 0's "
+                         f"(kernel, band, store or search options disagree): {[p.tolist() for p in parts]}")
+    return fp
+
+
 def gather_topk(dist, topk_np, k, device="cpu"):
     """All ranks contribute their top-k; every rank returns the merged global top-k."""
     import torch

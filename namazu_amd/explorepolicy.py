@@ -80,6 +80,11 @@ class SweepResult:
         self.topk = topk
 
 
+class ChannelClosed(queue.Empty):
+    """ActionChannel.get() on a closed channel (a subclass of queue.Empty, so `except queue.Empty` still catches it;
+    a consumer loop that must stop once the channel is closed catches this one first)."""
+
+
 class ActionChannel:
     """ExplorePolicy.ActionChan() over the library's time-bounded queue (nmz_tbqueue_*, the reference's
     BasicTBQueue, util/queue/impl.go:64-128): put_at(due_ns, action) hands an action to the native timer
@@ -126,19 +131,23 @@ class ActionChannel:
         self.put_at(self.L.nmz_monotonic_ns(), action)
 
     def get(self, block=True, timeout=None):
-        """Blocks until an action is released; queue.Empty on timeout, and once the channel is closed (a consumer
-        blocked in get() when close() runs returns with queue.Empty)."""
+        """Blocks until an action is released; queue.Empty on timeout, ChannelClosed (a queue.Empty) once the
+        channel is closed (a consumer blocked in get() when close() runs returns with ChannelClosed)."""
         i, due, rel = ctypes.c_uint64(), ctypes.c_int64(), ctypes.c_int64()
         t = -1 if (block and timeout is None) else int((timeout if block else 0) * 1e9)
         try:
             q = self._enter()
         except ValueError:
-            raise queue.Empty
+            raise ChannelClosed("ActionChannel is closed")
         try:
             rc = self.L.nmz_tbqueue_dequeue(q, t, ctypes.byref(i), ctypes.byref(due), ctypes.byref(rel))
         finally:
             self._leave()
         if rc == _lib.NMZ_EAGAIN:
+            with self._lock:
+                closed = self._closed
+            if closed:
+                raise ChannelClosed("ActionChannel is closed")
             raise queue.Empty
         _lib.check(rc)
         self.delivery_err_ns.append(rel.value - due.value)
@@ -158,7 +167,7 @@ class ActionChannel:
         return a.value, b.value, c.value  # enqueued, released, dequeued
 
     def close(self):
-        """Closes the channel: blocked get() calls return (queue.Empty), then the native queue is freed once no
+        """Closes the channel: blocked get() calls return (ChannelClosed), then the native queue is freed once no
         call is inside it (nmz_tbqueue_close, then nmz_tbqueue_destroy)."""
         with self._lock:
             if self._closed or not self.q:

@@ -296,10 +296,28 @@ class SimilarityIndex:
         if n == 0 or N == 0 or k == 0:
             return ids, ds
         if k > 64:
-            raise ValueError("nmz_ed_plan_query_knn answers k <= 64")
+            return self._query_pairs(queries, k)
         qset = TraceSet([np.asarray(q, np.uint64) for q in queries])
         _lib.check(_lib.load().nmz_ed_plan_query_knn(self.plan, _lib.ptr(qset.off), _lib.ptr(qset.sym), n, k,
                                                       _lib.ptr(ids), _lib.ptr(ds)))
+        return ids, ds
+
+    def _query_pairs(self, queries, k):
+        """k > 64 (the resident kernels keep at most 64 per query; the reference's search has no cap,
+        naive.go:235): every (query, stored trace) distance through nmz_ed_pairs on the GPU, one call per query,
+        ordered by (distance, id) on the host."""
+        n, N = len(queries), len(self.ts)
+        kk = min(k, N)
+        ids = np.full((n, k), _lib.NMZ_NONE, np.uint32)
+        ds = np.full((n, k), _lib.NMZ_NONE, np.uint32)
+        stored = [self.ts.trace(i) for i in range(N)]
+        pairs = np.stack([np.zeros(N, np.uint32), np.arange(1, N + 1, dtype=np.uint32)], 1)
+        for r, q in enumerate(queries):
+            both = TraceSet([np.asarray(q, np.uint64)] + stored)
+            d = ed_pairs(both, pairs, self.band, ctx=self.ctx)
+            order = np.lexsort((np.arange(N), d))[:kk]
+            ids[r, :kk] = order
+            ds[r, :kk] = d[order]
         return ids, ds
 
     def close(self):

@@ -33,7 +33,7 @@ def _inputs():
     return eh, ec, ts
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, opts_by_rank=(0, 0)):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     import torch
     import torch.distributed as dist
@@ -53,7 +53,15 @@ def _worker(rank, world, port, q):
         L = _lib.load()
         N, k = len(ts), 6
         plan = ctypes.c_void_p()
-        _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), N, 32, ctypes.byref(plan)))
+        _lib.check(L.nmz_ed_plan_create_opts(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), None, N, 32,
+                                             opts_by_rank[rank], ctypes.byref(plan)))
+        try:
+            nd.check_ed_plans(dist, L, plan)
+        except ValueError as e:
+            L.nmz_ed_plan_destroy(plan)
+            q.put((rank, "mismatch", str(e)))
+            ctx.close()
+            return
         part = torch.empty(N * k, dtype=torch.int64, device="cuda")
         _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, rank, world, ctypes.c_void_p(part.data_ptr()), stream))
         torch.cuda.synchronize()
@@ -114,3 +122,25 @@ def test_two_ranks_on_device_shard_and_merge(ctx):
     ost, _, _ = O.random_sweep(int(best["seed"]), 1, eh, ec, O.random_params(30_000_000, 100_000_000, 0.2))
     assert int(ost["n_fault"][0]) == int(best["n_fault"])
     assert st is not None
+
+
+def test_two_ranks_mismatched_ed_plans_fail(ctx):
+    """Rank 1 builds its plan with the single-kernel search (NMZ_ED_OPT_SINGLE_KERNEL): the plans' fingerprints
+    differ, so dist.check_ed_plans raises on both ranks before any shard runs, instead of merging k-NN lists from
+    searches that might deal pairs differently."""
+    from namazu_amd import _lib
+    world = 2
+    mctx = mp.get_context("spawn")
+    q = mctx.Queue()
+    port = _free_port()
+    procs = [mctx.Process(target=_worker, args=(r, world, port, q, (0, _lib.NMZ_ED_OPT_SINGLE_KERNEL)))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(r[0] for r in res) == [0, 1]
+    for rank, what, msg in res:
+        assert what == "mismatch" and "ranks [1]" in msg, (rank, what)

@@ -739,3 +739,94 @@ def test_knn_compact_tables_forced(ctx, monkeypatch, w):
         d = O.ed_pairs(ts.off, ts.sym, pairs, w, nthreads=16)
         order = np.lexsort((pairs[:, 1], d))[:k]
         assert ref_d[q].tolist() == d[order].tolist() and ref_i[q].tolist() == pairs[order, 1].tolist()
+
+
+def _fp(L, plan):
+    fp = np.zeros(_lib.NMZ_ED_FP_WORDS, np.uint64)
+    _lib.check(L.nmz_ed_plan_fingerprint(plan, _lib.ptr(fp)))
+    return fp
+
+
+@pytest.mark.parametrize("S", [3, 4, 8])
+def test_shards_partition_across_search_forms(ctx, S):
+    """A shard owns whole 64-query blocks (nmz_ed_block_shard) whichever form of the bit-parallel search its plan
+    took -- two-phase, single kernel, no q-gram filter, compact tables (NMZ_ED_OPT_*) -- so shards of one search
+    run with different forms still partition the pairs exactly: shard s here runs on plan s mod 4, and the merged,
+    filled lists equal the oracle's (a pair dropped or doubled would change them). The plans' fingerprints differ,
+    which is what the multi-rank paths check before a search (dist.check_ed_plans, nmz_ed_group_plan_create)."""
+    import torch
+    L = _lib.load()
+    rng = np.random.default_rng(S)
+    ts = _edited_family(700, 150, 24, 30, rng)
+    n, k, w = len(ts), 6, 32
+    forms = [0, _lib.NMZ_ED_OPT_SINGLE_KERNEL, _lib.NMZ_ED_OPT_NO_QGRAM, _lib.NMZ_ED_OPT_COMPACT]
+    plans = []
+    for o in forms:
+        p = ctypes.c_void_p()
+        _lib.check(L.nmz_ed_plan_create_opts(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), None, n, w, o,
+                                             ctypes.byref(p)))
+        assert L.nmz_ed_plan_is_fast(p) == 2
+        plans.append(p)
+    fps = [_fp(L, p) for p in plans]
+    assert all(not np.array_equal(fps[0], f) for f in fps[1:])
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    parts = torch.empty(S * n * k, dtype=torch.int64, device="cuda")
+    out = torch.empty(n * k, dtype=torch.int64, device="cuda")
+    for s in range(S):
+        _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plans[s % 4], k, s, S,
+                                                   ctypes.c_void_p(parts.data_ptr() + s * n * k * 8), stream))
+    _lib.check(L.nmz_knn_merge_dev(ctx.handle, ctypes.c_void_p(parts.data_ptr()), S, n, k,
+                                   ctypes.c_void_p(out.data_ptr()), stream))
+    _lib.check(L.nmz_ed_knn_fill_dev(plans[0], k, ctypes.c_void_p(out.data_ptr()), stream))
+    torch.cuda.synchronize()
+    for p in plans:
+        L.nmz_ed_plan_destroy(p)
+    keys = out.cpu().numpy().view(np.uint64).reshape(n, k)
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, w, k, nthreads=16)
+    assert np.array_equal((keys >> np.uint64(32)).astype(np.uint32), od)
+    assert np.array_equal((keys & np.uint64(0xFFFFFFFF)).astype(np.uint32), oi)
+
+
+def test_knobs_need_nmz_ab(ctx, monkeypatch):
+    """NMZ_* A/B knobs reach the library only under NMZ_AB=1: without it NMZ_ED_TWO_PHASE=0 / NMZ_ED_QGRAM=0 leave
+    the plan as the product builds it (same fingerprint), with it they change the plan."""
+    L = _lib.load()
+    ts = _edited_family(200, 100, 16, 20, np.random.default_rng(5))
+
+    def fp():
+        p = ctypes.c_void_p()
+        _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), len(ts), 32, ctypes.byref(p)))
+        f = _fp(L, p)
+        L.nmz_ed_plan_destroy(p)
+        return f
+
+    monkeypatch.delenv("NMZ_AB", raising=False)
+    monkeypatch.delenv("NMZ_ED_TWO_PHASE", raising=False)
+    monkeypatch.delenv("NMZ_ED_QGRAM", raising=False)
+    base = fp()
+    monkeypatch.setenv("NMZ_ED_TWO_PHASE", "0")
+    monkeypatch.setenv("NMZ_ED_QGRAM", "0")
+    assert np.array_equal(fp(), base)
+    monkeypatch.setenv("NMZ_AB", "1")
+    f = fp()
+    assert not np.array_equal(f, base) and int(f[4]) & 3 == 0 and int(base[4]) & 3 == 3
+
+
+def test_similarity_index_k_beyond_64(ctx):
+    """SimilarityIndex.query with k > 64 (the reference's search has no cap, naive.go:235): every pair distance on
+    the GPU (nmz_ed_pairs), ordered by (distance, id), equal to the oracle's brute force; k <= 64 answers agree with
+    its prefix."""
+    ts = _edited_family(150, 80, 12, 20, np.random.default_rng(8))
+    idx = hs.SimilarityIndex(ts, 16, ctx=ctx)
+    qs = [ts.trace(3), ts.trace(77)[:60]]
+    qi, qd = idx.query(qs, 100)
+    si, sd = idx.query(qs, 40)
+    idx.close()
+    n = len(ts)
+    for r, q in enumerate(qs):
+        both = hs.TraceSet([q] + [ts.trace(i) for i in range(n)])
+        pairs = np.stack([np.zeros(n, np.uint32), np.arange(1, n + 1, dtype=np.uint32)], 1)
+        d = O.ed_pairs(both.off, both.sym, pairs, 16)
+        order = np.lexsort((np.arange(n), d))[:100]
+        assert qi[r].tolist() == order.tolist() and qd[r].tolist() == d[order].tolist()
+        assert si[r].tolist() == qi[r, :40].tolist() and sd[r].tolist() == qd[r, :40].tolist()

@@ -8,7 +8,7 @@ import time
 import pytest
 
 from namazu_amd import _lib
-from namazu_amd.explorepolicy import ActionChannel
+from namazu_amd.explorepolicy import ActionChannel, ChannelClosed
 
 
 def test_release_order_and_equal_due_times():
@@ -31,7 +31,8 @@ def test_release_order_and_equal_due_times():
 
 @pytest.mark.parametrize("consumers", [1, 4])
 def test_close_wakes_blocked_consumers(consumers):
-    """close() while consumers block in get() (no timeout): every consumer returns with queue.Empty, close()
+    """close() while consumers block in get() (no timeout): every consumer returns with ChannelClosed (a
+    queue.Empty, distinct from a timeout), close()
     returns after they have left the native queue, and later calls fail cleanly. Repeated, so a consumer still
     inside nmz_tbqueue_dequeue when the queue is freed would show up as a crash or a hang."""
     for _ in range(25):
@@ -43,8 +44,10 @@ def test_close_wakes_blocked_consumers(consumers):
             started.wait()
             try:
                 out.append(ch.get())
-            except queue.Empty:
+            except ChannelClosed:
                 out.append("closed")
+            except queue.Empty:
+                out.append("timeout")
 
         ts = [threading.Thread(target=consume) for _ in range(consumers)]
         for t in ts:
@@ -56,7 +59,7 @@ def test_close_wakes_blocked_consumers(consumers):
             t.join(timeout=10)
             assert not t.is_alive()
         assert out == ["closed"] * consumers
-        with pytest.raises(queue.Empty):
+        with pytest.raises(ChannelClosed):
             ch.get(timeout=0)
         with pytest.raises(ValueError):
             ch.put(1)
@@ -75,3 +78,17 @@ def test_native_close_then_destroy():
     assert L.nmz_tbqueue_dequeue(q, -1, ctypes.byref(i), ctypes.byref(d), ctypes.byref(r)) == _lib.NMZ_EAGAIN
     assert L.nmz_tbqueue_enqueue(q, 8, 0) != 0
     _lib.check(L.nmz_tbqueue_destroy(q))
+
+
+def test_timeout_is_not_closed():
+    """A timed-out get() on an open channel raises plain queue.Empty (not ChannelClosed), so a consumer loop
+    `except ChannelClosed: break / except queue.Empty: continue` neither exits early nor spins after close."""
+    ch = ActionChannel()
+    try:
+        with pytest.raises(queue.Empty) as e:
+            ch.get(timeout=0.001)
+        assert not isinstance(e.value, ChannelClosed)
+    finally:
+        ch.close()
+    with pytest.raises(ChannelClosed):
+        ch.get(timeout=0.001)
