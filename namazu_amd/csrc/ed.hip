@@ -1207,7 +1207,7 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     // write pass + DP of the tiles the last count pass covered
     auto write_dp = [&](uint64_t n_ent, uint32_t n_items) -> int {
         // the u32 scans (entry and item offsets) hold only below 2^32 entries: a batch must never reach it
-        NMZ_CHECK(n_ent <= limit && n_ent < (1ULL << 32), "internal: a two-phase batch exceeds the entry limit");
+        NMZ_CHECK(n_ent < (1ULL << 32), "internal: a two-phase batch reaches 2^32 entries");
         NMZ_TRY(p->tp_ent.ensure(Carve::bytes_for(n_ent + 1, 4)));
         Q.ent = p->tp_ent.as<uint32_t>();
         NMZ_HIP(hipMemcpyAsync(d_cur, d_poff, (uint64_t)n_pairs * 4, hipMemcpyDeviceToDevice, st));
@@ -1261,14 +1261,15 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
             continue;
         }
         // one group alone exceeds the limit: its query blocks in sub-batches, each with its own tile list (the
-        // group's superblock order, restricted to the sub-batch's blocks); a single block beyond the limit cannot
-        // be split further (64 queries x N candidates: N > 2^24 at the default limit) and fails loudly
+        // group's superblock order, restricted to the sub-batch's blocks); a single block cannot be split further:
+        // it runs alone, and fails loudly only at 2^32 entries (64 queries x N candidates: N >= 2^26)
         const size_t i0 = grp[2 * b0], i1 = b0 + 1 < ng ? grp[2 * (b0 + 1)] : qbs.size();
         for (size_t j0 = i0; j0 < i1;) {
             uint64_t a = 0;
             size_t j1 = j0;
             while (j1 < i1 && (j1 == j0 || a + block_entries(j1) <= limit)) a += block_entries(j1++);
-            NMZ_CHECK(a <= limit, "one query block's candidate entries exceed the two-phase limit (too many traces)");
+            // (a block alone may pass the batching limit; it must stay below the u32 scans' 2^32)
+            NMZ_CHECK(a < (1ULL << 32), "one query block's candidate entries reach 2^32 (too many traces)");
             std::vector<uint64_t> tiles;
             for (uint32_t cb0 = qbs[j0] / 4; cb0 < NCB; cb0 += ED_SC)
                 for (size_t i = j0; i < j1; ++i)
