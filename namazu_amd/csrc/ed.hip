@@ -438,6 +438,12 @@ struct nmz_ed_plan {
     std::map<uint64_t, nmz::DevBuf> tile_list;      // per (shard, n_shards): the shard's tiles (qb << 32 | cb)
     std::map<uint64_t, uint64_t> tile_count;
     nmz::DevBuf tp_mem, tp_ent, tp_rec;
+    struct TpSizes {
+        uint64_t tot64;
+        uint32_t items, n_rec;
+    };
+    std::map<uint64_t, TpSizes> tp_sizes;  // per (shard, n_shards): entry total, DP items, records of its searches
+    uint32_t *d_tp_mismatch = nullptr;     // (in tp_mem) set when a search's totals differ from tp_sizes
     // fixed at creation (NMZ_ED_QGRAM / NMZ_ED_TWO_PHASE, A/B knobs read once per plan), so every shard and every
     // call of one plan takes the same search and deals pairs by the same rule
     bool qgram = true, two_phase = true;
@@ -1069,6 +1075,13 @@ static uint64_t ed_tp_max_entries() {
     return ED_TP_MAX_ENTRIES;
 }
 
+// the cached two-phase sizes against this search's own (ed_bv_two_phase): flag[0] = 1 on any difference
+__global__ void k_tp_verify(const uint64_t *__restrict__ tot64, const uint32_t *__restrict__ items,
+                            const uint32_t *__restrict__ n_rec, uint64_t e_tot, uint32_t e_items, uint32_t e_rec,
+                            uint32_t *__restrict__ flag) {
+    if (threadIdx.x == 0 && (*tot64 != e_tot || *items != e_items || *n_rec != e_rec)) atomicOr(flag, 1u);
+}
+
 // one block: sum of n u32 counts in u64
 __global__ __launch_bounds__(1024) void k_sum_u32_u64(const uint32_t *__restrict__ cnt, uint32_t n,
                                                       uint64_t *__restrict__ out) {
@@ -1142,6 +1155,13 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
                              Carve::bytes_for(4, 4) + Carve::bytes_for(1, 8)));
     Carve cv(p->tp_mem.ptr);
     uint64_t *d_tot64 = cv.take<uint64_t>(1);
+    {
+        uint32_t *f = cv.take<uint32_t>(4);
+        if (f != p->d_tp_mismatch) {  // a new scratch buffer: its flag starts clear
+            NMZ_HIP(hipMemsetAsync(f, 0, 16, st));
+            p->d_tp_mismatch = f;
+        }
+    }
     uint32_t *d_cnt = cv.take<uint32_t>(n_pairs + 1), *d_poff = cv.take<uint32_t>(n_pairs + 1);
     uint32_t *d_items = cv.take<uint32_t>(n_pairs + 1), *d_ioff = cv.take<uint32_t>(n_pairs + 1);
     uint32_t *d_cur = cv.take<uint32_t>(n_pairs + 1);
@@ -1181,7 +1201,9 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     const uint64_t limit = std::min<uint64_t>(ed_tp_max_entries(), 0xFFFFFFFFull);
     // count pass + scans over a tile list: entry and item totals
     uint32_t n_rec = 0;
-    auto count = [&](const uint64_t *tiles, uint64_t n_tiles, uint64_t &tot64, uint32_t &tot_items) -> int {
+    // readback = false (sizes known from an earlier search of this shard): everything stays on the device
+    auto count = [&](const uint64_t *tiles, uint64_t n_tiles, uint64_t &tot64, uint32_t &tot_items,
+                     bool readback = true) -> int {
         Q.tiles = tiles;
         Q.n_tiles = n_tiles;
         NMZ_HIP(hipMemsetAsync(d_cnt, 0, (n_pairs + 1) * 4, st));
@@ -1198,6 +1220,7 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
         // near-duplicates), so their totals are trusted only once this sum is within the limit
         hipLaunchKernelGGL(k_sum_u32_u64, dim3(1), dim3(1024), 0, st, d_cnt, n_pairs, d_tot64);
         NMZ_HIP(hipGetLastError());
+        if (!readback) return NMZ_OK;
         NMZ_HIP(hipMemcpyAsync(&tot64, d_tot64, 8, hipMemcpyDeviceToHost, st));
         NMZ_HIP(hipMemcpyAsync(&tot_items, d_ioff + n_pairs, 4, hipMemcpyDeviceToHost, st));
         if (Q.recs) NMZ_HIP(hipMemcpyAsync(&n_rec, Q.n_rec, 4, hipMemcpyDeviceToHost, st));
@@ -1221,8 +1244,26 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     };
     uint64_t tot64 = 0;
     uint32_t tot_items = 0;
+    // The sizes the host needs before the write pass and the DP (entry total, work items, survivor records) are
+    // fixed by the plan and the shard: the first search of a shard reads them back (one synchronisation), later
+    // searches enqueue every kernel with those sizes and no host round trip; a one-thread kernel compares them with
+    // this search's own totals and flags a difference (nmz_ed_plan_counters reports it; none can occur: the plan is
+    // immutable and the filter deterministic)
+    auto cached = p->tp_sizes.find(key);
+    if (cached != p->tp_sizes.end() && Q.recs && cached->second.tot64 <= limit) {
+        const nmz_ed_plan::TpSizes &z = cached->second;
+        NMZ_TRY(count(tl.as<uint64_t>(), n_tiles_all, tot64, tot_items, false));
+        hipLaunchKernelGGL(k_tp_verify, dim3(1), dim3(64), 0, st, d_tot64, d_ioff + n_pairs, Q.n_rec, z.tot64, z.items,
+                           z.n_rec, p->d_tp_mismatch);
+        NMZ_HIP(hipGetLastError());
+        n_rec = z.n_rec;
+        return write_dp(z.tot64, z.items);
+    }
     NMZ_TRY(count(tl.as<uint64_t>(), n_tiles_all, tot64, tot_items));
-    if (tot64 <= limit) return write_dp(tot64, tot_items);
+    if (tot64 <= limit) {
+        if (Q.recs && n_rec <= Q.rec_cap) p->tp_sizes[key] = nmz_ed_plan::TpSizes{tot64, tot_items, n_rec};
+        return write_dp(tot64, tot_items);
+    }
     // batches of whole query blocks: per-block totals from this count pass, then the lists and counters start over
     // (the count pass lists pairs with an empty trace, and adds to the counters)
     std::vector<uint32_t> cnt(n_pairs);
@@ -1462,6 +1503,12 @@ int nmz_ed_plan_counters(nmz_ed_plan *plan, uint64_t *out, void *stream) {
     NMZ_HIP(hipStreamSynchronize(st));
     for (uint32_t sidx = 0; sidx < ED_CNT_STRIPES; ++sidx)
         for (int i = 0; i < ED_BV_NCOUNTERS; ++i) out[i] += lines[sidx * ED_CNT_LINE + i];
+    if (plan->d_tp_mismatch) {
+        uint32_t f = 0;
+        NMZ_HIP(hipMemcpyAsync(&f, plan->d_tp_mismatch, 4, hipMemcpyDeviceToHost, st));
+        NMZ_HIP(hipStreamSynchronize(st));
+        NMZ_CHECK(f == 0, "internal: a two-phase search's totals differed from the shard's cached sizes");
+    }
     return NMZ_OK;
 }
 

@@ -2036,6 +2036,9 @@ int nmz_replayable_seeds_destroy(nmz_replayable_seeds *seeds) {
 #ifndef NMZ_TRACES_ONE_STREAM
 #define NMZ_TRACES_ONE_STREAM 0
 #endif
+#ifndef NMZ_TRACES_DEFAULT_MODE
+#define NMZ_TRACES_DEFAULT_MODE 1
+#endif
 int nmz_replayable_sweep_traces(nmz_ctx *ctx, uint32_t n_traces, const uint32_t *const *hint_off,
                                 const uint8_t *const *hint_bytes, const uint32_t *n_events, int64_t max_interval_ns,
                                 uint64_t seed_lo, uint64_t n_seeds, uint32_t k, nmz_topk_entry *topk) {
@@ -2084,12 +2087,15 @@ int nmz_replayable_sweep_traces(nmz_ctx *ctx, uint32_t n_traces, const uint32_t 
     // (two streams in all, each serial: build, sweep, build, ...): 0.179 ms per trace against 0.188 with the
     // builds and sweeps on four streams (NMZ_TRACES_MODE=0, profiles/r04/e2e_native_ab/). NMZ_TRACES_MODE=2: the
     // same, with trace i's top-k read after trace i + 1's sweep is enqueued instead of trace i + 2's
-    static const int mode = [] {
+    // NMZ_TRACES_MODE=3: the Python-driven stream's schedule (bench.py end_to_end): builds on the two contexts'
+    // streams, sweeps on two streams of their own (four in all), trace i + 2's build enqueued before trace i's
+    // sweep, trace i - 1's top-k read once trace i's sweep is enqueued
+    const int mode = [] {
         const char *e = ab_env("NMZ_TRACES_MODE");
-        return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 1;
+        return e && e[0] >= '0' && e[0] <= '3' ? e[0] - '0' : NMZ_TRACES_DEFAULT_MODE;
     }();
-    const bool same_stream = mode != 0;
-    const uint32_t lag = mode == 2 ? 1 : 2;
+    const bool same_stream = mode == 1 || mode == 2;
+    const uint32_t lag = (mode == 2 || mode == 3) ? 1 : 2;
     for (uint32_t i = 0; i < n_traces && rc == NMZ_OK; ++i) {
         if (!same_stream && i + AHEAD < n_traces) rc = make(i + AHEAD);
         if (rc != NMZ_OK) break;

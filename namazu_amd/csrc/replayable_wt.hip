@@ -824,6 +824,25 @@ struct WtTopkState {
     unsigned long long cand_idx[WT_CAND];
 };
 
+#ifdef WT_TRACE
+// timing-only builds (-DWT_TRACE, G = 1): wall_clock64 per (row, wave) at the kernel start [9], after staging [0] and
+// at the end of each of up to 8 chunks [1..8]; read with nmz_debug_wt_trace (tools/k1_trace.py --wt)
+__device__ unsigned long long g_wt_trace[256][16][10];
+#define WT_TSTAMP(slot)                                                                                      \
+    do {                                                                                                     \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < 256 && (slot) < 10)                                      \
+            g_wt_trace[blockIdx.x][threadIdx.x >> 6][(slot)] = wall_clock64();                               \
+    } while (0)
+#else
+#define WT_TSTAMP(slot) \
+    do {                \
+    } while (0)
+#endif
+
+#ifndef WT_PRIO_TAIL
+#define WT_PRIO_TAIL 16
+#endif
+
 // G workgroups per row L: each stages the row image into LDS and takes a contiguous share of the row's chunks of
 // 64 NS seeds (NS per lane), which its waves take one at a time from an LDS counter.
 template <bool BIG, int NS>
@@ -847,6 +866,7 @@ __global__ __launch_bounds__(1024) void k_replayable_sweep_wt(
         return;
     }
     if (span && threadIdx.x == 0) atomicMax(span, ~(unsigned long long)wall_clock64());
+    WT_TSTAMP(9);
     {
         const uint4 *__restrict__ src = blob + (uint64_t)L * rb16;
         // every load of a pass in flight at once (indices clamped to the image, stores unconditional)
@@ -865,6 +885,10 @@ __global__ __launch_bounds__(1024) void k_replayable_sweep_wt(
         }
     }
     __syncthreads();
+    WT_TSTAMP(0);
+#ifdef WT_TRACE
+    uint32_t n_done = 0;
+#endif
     const char *img = reinterpret_cast<const char *>(wt_lds);
     const uint4 *__restrict__ row = table + (uint64_t)L * E;
     const uint64_t rsum = rowsum[L];
@@ -885,6 +909,12 @@ __global__ __launch_bounds__(1024) void k_replayable_sweep_wt(
         idxn[u] = sorted_idx[jn];
     }
     while (ch < c1) {
+#if WT_PRIO_TAIL > 0
+        // the row's last chunks: the SIMD arbiter serves older waves first, so a chunk taken late by a young wave
+        // waits behind them and then runs alone at the end of the row; raising the priority of the waves on the
+        // last chunks lets them finish together with the rest
+        if (ch + WT_PRIO_TAIL >= c1) __builtin_amdgcn_s_setprio(3);
+#endif
         const uint32_t j0 = s0 + ch * CS + lane;
         uint64_t h0[NS];
         uint32_t idx[NS];
@@ -935,6 +965,9 @@ __global__ __launch_bounds__(1024) void k_replayable_sweep_wt(
             }
             if (lane == 0) atomicMax(reinterpret_cast<unsigned long long *>(ctr + 2), (unsigned long long)km);
         }
+#ifdef WT_TRACE
+        if (++n_done <= 8) WT_TSTAMP(n_done);
+#endif
         ch = chn;
     }
     if (span || tk) {
@@ -1345,6 +1378,12 @@ int wt_sweep(const WtState &w, nmz_ctx *ctx, hipStream_t st, const Buckets &b, c
 }
 
 }  // namespace nmz
+
+#ifdef WT_TRACE
+extern "C" int nmz_debug_wt_trace(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(nmz::g_wt_trace), sizeof(nmz::g_wt_trace)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #ifdef WT_BUILD_TRACE
 extern "C" int nmz_debug_wt_build_trace(unsigned long long *out, uint32_t n) {

@@ -830,3 +830,35 @@ def test_similarity_index_k_beyond_64(ctx):
         order = np.lexsort((np.arange(n), d))[:100]
         assert qi[r].tolist() == order.tolist() and qd[r].tolist() == d[order].tolist()
         assert si[r].tolist() == qi[r, :40].tolist() and sd[r].tolist() == qd[r, :40].tolist()
+
+
+def test_repeated_shard_searches_use_cached_sizes(ctx):
+    """A shard's second and later two-phase searches enqueue every kernel with the sizes its first search read
+    back (no host round trip); the kernels still run in full, so the lists equal the first search's and the
+    oracle's, and a device check of this search's own totals against the cached ones passes
+    (nmz_ed_plan_counters raises otherwise)."""
+    import torch
+    L = _lib.load()
+    ts = _edited_family(600, 160, 20, 30, np.random.default_rng(31))
+    n, k, w, S = len(ts), 6, 32, 3
+    plan = ctypes.c_void_p()
+    _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), n, w, ctypes.byref(plan)))
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    parts = torch.empty(S * n * k, dtype=torch.int64, device="cuda")
+    out = torch.empty(n * k, dtype=torch.int64, device="cuda")
+    runs = []
+    cnt = np.zeros(_lib.NMZ_ED_NCOUNTERS, np.uint64)
+    for rep in range(3):
+        for s in range(S):
+            _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, s, S,
+                                                       ctypes.c_void_p(parts.data_ptr() + s * n * k * 8), stream))
+        _lib.check(L.nmz_knn_merge_dev(ctx.handle, ctypes.c_void_p(parts.data_ptr()), S, n, k,
+                                       ctypes.c_void_p(out.data_ptr()), stream))
+        _lib.check(L.nmz_ed_knn_fill_dev(plan, k, ctypes.c_void_p(out.data_ptr()), stream))
+        _lib.check(L.nmz_ed_plan_counters(plan, _lib.ptr(cnt), stream))
+        runs.append(out.cpu().numpy().view(np.uint64).reshape(n, k).copy())
+    L.nmz_ed_plan_destroy(plan)
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, w, k, nthreads=16)
+    ref = (od.astype(np.uint64) << np.uint64(32)) | oi.astype(np.uint64)
+    for r in runs:
+        assert np.array_equal(r, ref)

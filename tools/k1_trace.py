@@ -1,6 +1,7 @@
-"""Per-wave timeline of one K1 (order-query) launch, from a -DOQ_TRACE build (GPU box).
+"""Per-wave timeline of one K1 launch, from a -DOQ_TRACE build (order-query kernel) or a -DWT_TRACE build
+(wavelet-tree kernel, --wt) (GPU box).
 
-  NMZ_LIB_PATH=.../libnmz_gpu_trace.so python tools/k1_trace.py
+  NMZ_LIB_PATH=.../libnmz_gpu_trace.so python tools/k1_trace.py [--wt]
 
 Stamps (wall_clock64, 100 MHz) per (row, wave): kernel start, row image staged, end of each 64-seed chunk.
 """
@@ -64,18 +65,24 @@ def main():
     ctx.close()
 
 
+WT = "--wt" in sys.argv
+
+
 def report(L):
     tr = np.zeros((256, 16, 10), np.uint64)
-    L.nmz_debug_oq_trace.argtypes = [ctypes.c_void_p]
-    assert L.nmz_debug_oq_trace(tr.ctypes.data) == 0
+    fn = L.nmz_debug_wt_trace if WT else L.nmz_debug_oq_trace
+    fn.argtypes = [ctypes.c_void_p]
+    assert fn(tr.ctypes.data) == 0
     tr = tr.astype(np.int64)
+
     t0 = tr[:, :, 9].min()
     start = (tr[:, :, 9] - t0) / 100.0  # us
     staged = (tr[:, :, 0] - t0) / 100.0
-    ends = np.where(tr[:, :, 1:8] > 0, (tr[:, :, 1:8] - t0) / 100.0, np.nan)
-    tail_end = np.where(tr[:, :, 8] > 0, (tr[:, :, 8] - t0) / 100.0, np.nan)
+    ce = 9 if WT else 8  # chunk-end slots 1..ce-1 (the WT trace has no cooperative-tail slot)
+    ends = np.where(tr[:, :, 1:ce] > 0, (tr[:, :, 1:ce] - t0) / 100.0, np.nan)
+    tail_end = np.full(tr.shape[:2], np.nan) if WT else np.where(tr[:, :, 8] > 0, (tr[:, :, 8] - t0) / 100.0, np.nan)
     last = np.fmax(np.nanmax(ends, axis=2), tail_end)
-    nchunks = np.sum(tr[:, :, 1:8] > 0, axis=2)
+    nchunks = np.sum(tr[:, :, 1:ce] > 0, axis=2)
     if np.any(~np.isnan(tail_end)):
         rows_t = ~np.all(np.isnan(tail_end), axis=1)
         tail_dur = np.nanmax(tail_end, axis=1) - np.nanmax(np.nanmax(ends, axis=2), axis=1)
@@ -86,7 +93,7 @@ def report(L):
     print(f"staging done:    min {staged.min():.1f} median {np.median(staged):.1f} max {staged.max():.1f} us; "
           f"staging time median {np.median(staged - start):.1f} us")
     dur = np.diff(np.concatenate([staged[:, :, None], ends], axis=2), axis=2)
-    for k in range(7):
+    for k in range(dur.shape[2]):
         d = dur[:, :, k]
         if np.all(np.isnan(d)):
             break
