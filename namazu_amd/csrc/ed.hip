@@ -440,7 +440,7 @@ struct nmz_ed_plan {
     nmz::DevBuf tp_mem, tp_ent, tp_rec;
     struct TpSizes {
         uint64_t tot64;
-        uint32_t items, n_rec;
+        uint32_t items, n_rec, item;
     };
     std::map<uint64_t, TpSizes> tp_sizes;  // per (shard, n_shards): entry total, DP items, records of its searches
     uint32_t *d_tp_mismatch = nullptr;     // (in tp_mem) set when a search's totals differ from tp_sizes
@@ -1059,6 +1059,19 @@ uint32_t ed_bv_item() {
     return ED_BV_ITEM;
 }
 
+// The item size of a search with n_ent DP entries: about ED_DP_ITEMS_TARGET items (8 per workgroup slot of the
+// chip), a power of two in [128, ED_BV_ITEM]. Large items keep every lane busy (a lane refills from its item's
+// entries as its pairs end); small ones shorten the last round of a launch, which dominates a shard's search when
+// its entries are few (configs[2], 8 shards, item 4096 -> 256: clustered shard DP 9.75 -> 9.45 ms, survey 0.41-0.62
+// -> 0.35-0.41 ms, profiles/r05/ed_item_ab). An NMZ_ED_ITEM setting (A/B) wins.
+constexpr uint64_t ED_DP_ITEMS_TARGET = 8ull * 256 * 5;
+uint32_t ed_bv_pick_item(uint64_t n_ent) {
+    if (ab_env("NMZ_ED_ITEM")) return ed_bv_item();
+    uint32_t it = 128;
+    while (it < ED_BV_ITEM && (uint64_t)it * 2 * ED_DP_ITEMS_TARGET <= n_ent) it *= 2;
+    return it;
+}
+
 // The two-phase bit-parallel search of one shard (nmz_internal.h EdQgArgs): filter count pass, scans (entry and
 // work-item offsets; the two totals come back to the host to size the entry lists and the DP grid), write pass,
 // DP over the work items. Returns 1 when the entry lists would exceed ED_TP_MAX_ENTRIES (caller falls back to
@@ -1197,7 +1210,8 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     Q.shard = shard;
     Q.n_shards = n_shards;
     Q.w = p->band;
-    const uint32_t item = ed_bv_item();
+    // entries per DP work item: from the search's entry total (ed_bv_pick_item) unless NMZ_ED_ITEM fixes it
+    uint32_t item = ed_bv_item();
     const uint64_t limit = std::min<uint64_t>(ed_tp_max_entries(), 0xFFFFFFFFull);
     // count pass + scans over a tile list: entry and item totals
     uint32_t n_rec = 0;
@@ -1244,6 +1258,17 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     };
     uint64_t tot64 = 0;
     uint32_t tot_items = 0;
+    // the DP items of the last count pass again under another item size (the first search of a shard, once its
+    // entry total is known)
+    auto reitem = [&](uint32_t it) -> int {
+        item = it;
+        hipLaunchKernelGGL(k_bv_items, dim3(ceil_div(n_pairs + 1, 256)), dim3(256), 0, st, d_cnt, n_pairs, item,
+                           d_items);
+        NMZ_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_items, d_ioff, (int)n_pairs + 1, st));
+        NMZ_HIP(hipMemcpyAsync(&tot_items, d_ioff + n_pairs, 4, hipMemcpyDeviceToHost, st));
+        NMZ_HIP(hipStreamSynchronize(st));
+        return NMZ_OK;
+    };
     // The sizes the host needs before the write pass and the DP (entry total, work items, survivor records) are
     // fixed by the plan and the shard: the first search of a shard reads them back (one synchronisation), later
     // searches enqueue every kernel with those sizes and no host round trip; a one-thread kernel compares them with
@@ -1252,6 +1277,7 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     auto cached = p->tp_sizes.find(key);
     if (cached != p->tp_sizes.end() && Q.recs && cached->second.tot64 <= limit) {
         const nmz_ed_plan::TpSizes &z = cached->second;
+        item = z.item;
         NMZ_TRY(count(tl.as<uint64_t>(), n_tiles_all, tot64, tot_items, false));
         hipLaunchKernelGGL(k_tp_verify, dim3(1), dim3(64), 0, st, d_tot64, d_ioff + n_pairs, Q.n_rec, z.tot64, z.items,
                            z.n_rec, p->d_tp_mismatch);
@@ -1261,7 +1287,9 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     }
     NMZ_TRY(count(tl.as<uint64_t>(), n_tiles_all, tot64, tot_items));
     if (tot64 <= limit) {
-        if (Q.recs && n_rec <= Q.rec_cap) p->tp_sizes[key] = nmz_ed_plan::TpSizes{tot64, tot_items, n_rec};
+        const uint32_t it = ed_bv_pick_item(tot64);
+        if (it != item) NMZ_TRY(reitem(it));
+        if (Q.recs && n_rec <= Q.rec_cap) p->tp_sizes[key] = nmz_ed_plan::TpSizes{tot64, tot_items, n_rec, item};
         return write_dp(tot64, tot_items);
     }
     // batches of whole query blocks: per-block totals from this count pass, then the lists and counters start over
