@@ -88,10 +88,11 @@ __global__ __launch_bounds__(256) void k_trace_sig(const uint64_t *__restrict__ 
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t t = blockIdx.x * waves_per_block + wv;
     if (wv >= waves_per_block || t >= N) return;  // whole waves only: no block-wide barrier below
-    // volatile: lanes read counters other lanes of the wave wrote (LDS ops of one wave execute in order)
-    volatile uint32_t *cnt = cnt_all + (size_t)wv * max_ent;
+    // the wave's own counters (LDS ops of one wave execute in order; compiler barriers keep the order in the code)
+    uint32_t *cnt = cnt_all + (size_t)wv * max_ent;
     if (PO)
         for (uint32_t i = lane; i < max_ent; i += 64) cnt[i] = 0;
+    __asm__ volatile("" ::: "memory");
     const uint64_t base = off[t], n = off[t + 1] - base;
     uint64_t acc1 = 0, acc2 = 0;
     uint32_t counted = 0;
@@ -124,16 +125,21 @@ __global__ __launch_bounds__(256) void k_trace_sig(const uint64_t *__restrict__ 
             const uint32_t e = take ? e0 : 0u;
             // lanes holding the same entity: intersect, bit by bit of the id, the ballot of lanes that agree
             // on that bit (kbits ballots per 64 elements instead of one per distinct entity)
-            uint64_t same = __ballot(take);
+            // (as the lanes that differ from this one in some bit: one XOR-OR per ballot, no per-lane select)
+            uint64_t diff = ~__builtin_amdgcn_ballot_w64(take);
+            const uint32_t et = take ? e : 0xffffffffu;  // untaken lanes set every bit: no ballot needs `take`
             for (uint32_t b = 0; b < kbits; ++b) {
-                const bool bit = (e >> b) & 1u;
-                const uint64_t B = __ballot(take && bit);
-                same &= bit ? B : ~B;
+                const uint32_t bm = (uint32_t)((int32_t)(et << (31 - b)) >> 31);  // all ones when bit b is set
+                const uint64_t B = __builtin_amdgcn_ballot_w64(bm != 0);
+                diff |= B ^ (((uint64_t)bm << 32) | bm);
             }
+            const uint64_t same = ~diff;
             if (take) {
-                const uint32_t before = cnt[e];  // every lane reads before any lane of the wave writes
+                const uint32_t before = cnt[e];
                 rank = before + (uint32_t)__popcll(same & below);
-                if ((same >> lane) == 1ull) cnt[e] = before + (uint32_t)__popcll(same);  // the group's last lane
+                // every lane of the wave has read (one LDS instruction) before the group's last lane stores
+                __asm__ volatile("" ::: "memory");
+                if ((same >> lane) == 1ull) cnt[e] = before + (uint32_t)__popcll(same);
             }
         }
         if (take) {
