@@ -840,7 +840,7 @@ __device__ unsigned long long g_wt_trace[256][16][10];
 #endif
 
 #ifndef WT_PRIO_TAIL
-#define WT_PRIO_TAIL 16
+#define WT_PRIO_TAIL 0  // 8, 16, 32: no change in K1 (profiles/r05/k1/prio_ab)
 #endif
 
 // G workgroups per row L: each stages the row image into LDS and takes a contiguous share of the row's chunks of
