@@ -426,8 +426,6 @@ struct nmz_ed_plan {
     std::vector<uint64_t> row_chunks;    // bv: chunks per block row
     uint64_t *d_counters = nullptr;  // bv: work counters of the latest search (nmz_ed_plan_counters)
     uint32_t *d_prof = nullptr;      // bv: [N][ED_QG_DW] q-gram profiles (ed_qgram_profiles)
-    uint32_t *d_profc = nullptr;     // bv: [N][ED_QG_CDW] coarse profiles (two-phase filter; built at its first search)
-    nmz::DevBuf profc_mem;
     uint32_t rq = 64;                // bv: queries per block row
     uint32_t maxlen = 0;
     uint32_t bw = 0;                 // bv: the kernels' template band W >= band (8, 16, 32, 64)
@@ -1182,14 +1180,8 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     uint32_t *d_cur = cv.take<uint32_t>(n_pairs + 1);
     void *d_scan = cv.take<char>(scan_bytes);
     const uint64_t n_tiles_all = p->tile_count[key];
-    if (!p->d_profc) {  // the coarse profiles, once per plan (from the fine ones)
-        NMZ_TRY(p->profc_mem.ensure(Carve::bytes_for((uint64_t)N * ED_QG_CDW + 4, 4)));
-        p->d_profc = p->profc_mem.as<uint32_t>();
-        NMZ_TRY(ed_qgram_coarse(reinterpret_cast<const uint32_t *>(A.prof), N, p->d_profc, st));
-    }
     EdQgArgs Q;
     Q.prof = A.prof;
-    Q.profc = reinterpret_cast<const uint4 *>(p->d_profc);
     Q.len = A.len;
     Q.knn = A.knn;
     Q.counters = A.counters;
@@ -1516,7 +1508,6 @@ int nmz_ed_plan_destroy(nmz_ed_plan *plan) {
         plan->tp_mem.release();
         plan->tp_ent.release();
         plan->tp_rec.release();
-        plan->profc_mem.release();
         for (auto &kv : plan->tile_list) kv.second.release();
     }
     delete plan;

@@ -644,53 +644,9 @@ __device__ __forceinline__ uint64_t qg_tile_of_block() {
     return (uint64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
 }
 
-// Coarse q-gram profiles: 32 buckets, each the (saturated) sum of 4 consecutive fine buckets -- one fine dword, summed
-// by v_sad_u8 against 0. |clamp(sum a) - clamp(sum c)| <= sum |a - c| (the clamp and the triangle inequality), so a
-// coarse L1 is a lower bound of the fine L1: coarse L1 > 4w settles a pair exactly as the fine bound would, in a
-// quarter of the v_sad_u8 (the filter's issue floor); the fine L1 runs only for the pairs the coarse one keeps.
-__global__ void k_qg_coarse(const uint32_t *__restrict__ prof, uint32_t N, uint32_t *__restrict__ coarse) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (trace, coarse dword)
-    if (t >= (uint64_t)N * ED_QG_CDW) return;
-    const uint32_t *f = prof + (t / ED_QG_CDW) * ED_QG_DW + (t % ED_QG_CDW) * 4;
-    uint32_t w = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) w |= min(__builtin_amdgcn_sad_u8(f[b], 0u, 0u), 255u) << (8 * b);
-    coarse[t] = w;
-}
-
-int ed_qgram_coarse(const uint32_t *prof, uint32_t N, uint32_t *coarse, hipStream_t st) {
-    if (N == 0) return NMZ_OK;
-    const uint64_t n = (uint64_t)N * ED_QG_CDW;
-    hipLaunchKernelGGL(k_qg_coarse, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, prof, N, coarse);
-    NMZ_HIP(hipGetLastError());
-    return NMZ_OK;
-}
-
-__device__ __forceinline__ uint32_t qg_l1_coarse(const uint4 (&c)[ED_QG_CDW / 4], const uint4 *q) {
-    uint32_t s = 0;
-#pragma unroll
-    for (int r = 0; r < (int)ED_QG_CDW / 4; ++r) {
-        const uint4 a = q[r];
-        s = __builtin_amdgcn_sad_u8(c[r].x, a.x, s);
-        s = __builtin_amdgcn_sad_u8(c[r].y, a.y, s);
-        s = __builtin_amdgcn_sad_u8(c[r].z, a.z, s);
-        s = __builtin_amdgcn_sad_u8(c[r].w, a.w, s);
-    }
-    return s;
-}
-
-#ifndef NMZ_QG_WAVES
-#define NMZ_QG_WAVES 0
-#endif
-#if NMZ_QG_WAVES > 0
-#define NMZ_QG_ATTR __attribute__((amdgpu_waves_per_eu(NMZ_QG_WAVES, NMZ_QG_WAVES)))
-#else
-#define NMZ_QG_ATTR
-#endif
 template <bool COUNT>
-__global__ __launch_bounds__(256) NMZ_QG_ATTR void k_ed_qg_filter(EdQgArgs A) {
+__global__ __launch_bounds__(256) void k_ed_qg_filter(EdQgArgs A) {
     __shared__ uint4 qp[64][ED_QG_DW / 4];
-    __shared__ uint4 qpc[64][ED_QG_CDW / 4];
     __shared__ uint32_t qlen[64];
     const uint64_t t = qg_tile_of_block();
     if (t >= A.n_tiles) return;
@@ -701,22 +657,15 @@ __global__ __launch_bounds__(256) NMZ_QG_ATTR void k_ed_qg_filter(EdQgArgs A) {
         qp[i / (ED_QG_DW / 4)][i % (ED_QG_DW / 4)] =
             q < A.N ? A.prof[(uint64_t)q * (ED_QG_DW / 4) + i % (ED_QG_DW / 4)] : make_uint4(0, 0, 0, 0);
     }
-    if (threadIdx.x < 64 * (ED_QG_CDW / 4)) {
-        const uint32_t q = 64 * qb + threadIdx.x / (ED_QG_CDW / 4);
-        qpc[threadIdx.x / (ED_QG_CDW / 4)][threadIdx.x % (ED_QG_CDW / 4)] =
-            q < A.N ? A.profc[(uint64_t)q * (ED_QG_CDW / 4) + threadIdx.x % (ED_QG_CDW / 4)] : make_uint4(0, 0, 0, 0);
-    }
     if (threadIdx.x < 64) qlen[threadIdx.x] = 64 * qb + threadIdx.x < A.N ? A.len[64 * qb + threadIdx.x] : 0u;
     __syncthreads();
     const uint32_t j = 256 * cb + threadIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const bool jv = j < A.N;
     const uint32_t m = jv ? A.len[j] : 0u;
-    // the candidate's coarse profile now; its fine profile once a pair of the tile needs it (wave-uniform)
-    uint4 cpc[ED_QG_CDW / 4], cp[ED_QG_DW / 4];
+    uint4 cp[ED_QG_DW / 4];
 #pragma unroll
-    for (int r = 0; r < (int)ED_QG_CDW / 4; ++r)
-        cpc[r] = jv ? A.profc[(uint64_t)j * (ED_QG_CDW / 4) + r] : make_uint4(0, 0, 0, 0);
-    bool have_fine = false;
+    for (int r = 0; r < (int)ED_QG_DW / 4; ++r)
+        cp[r] = jv ? A.prof[(uint64_t)j * (ED_QG_DW / 4) + r] : make_uint4(0, 0, 0, 0);
     // empty traces (n + m <= w results, listed here) are rare: a tile without one runs the loop without that path
     const bool any_empty =
         __syncthreads_or((jv && m == 0) || (threadIdx.x < 64 && 64 * qb + threadIdx.x < A.N && qlen[threadIdx.x] == 0));
@@ -748,19 +697,9 @@ __global__ __launch_bounds__(256) NMZ_QG_ATTR void k_ed_qg_filter(EdQgArgs A) {
                 a2 = false;
             }
         }
-        // q-gram bound: L1 > 4w => ED_w = w + 1, no DP; the coarse L1 (a lower bound of the fine one) first
-        bool f1 = a1 && qg_l1_coarse(cpc, qpc[2 * pp]) > 4 * A.w;
-        bool f2 = a2 && qg_l1_coarse(cpc, qpc[2 * pp + 1]) > 4 * A.w;
-        if (__any((a1 && !f1) || (a2 && !f2))) {
-            if (!have_fine) {
-#pragma unroll
-                for (int r = 0; r < (int)ED_QG_DW / 4; ++r)
-                    cp[r] = jv ? A.prof[(uint64_t)j * (ED_QG_DW / 4) + r] : make_uint4(0, 0, 0, 0);
-                have_fine = true;
-            }
-            f1 = f1 || (a1 && qg_l1_reg(cp, qp[2 * pp]) > 4 * A.w);
-            f2 = f2 || (a2 && qg_l1_reg(cp, qp[2 * pp + 1]) > 4 * A.w);
-        }
+        // q-gram bound: L1 > 4w => ED_w = w + 1, no DP
+        const bool f1 = a1 && qg_l1_reg(cp, qp[2 * pp]) > 4 * A.w;
+        const bool f2 = a2 && qg_l1_reg(cp, qp[2 * pp + 1]) > 4 * A.w;
         c_qgram += (uint32_t)f1 + (uint32_t)f2;
         a1 = a1 && !f1;
         a2 = a2 && !f2;

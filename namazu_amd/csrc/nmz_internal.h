@@ -82,7 +82,6 @@ constexpr uint32_t ED_CNT_STRIPES = 64, ED_CNT_LINE = 16, ED_CNT_WORDS = ED_CNT_
 // packed 4 per dword. One edit changes at most 4 bigram counts by one, so ED >= L1(profile_a, profile_b) / 4
 // (merging bigrams into buckets and saturating only lower the L1); L1 > 4w settles ED_w = w + 1 without a DP.
 constexpr uint32_t ED_QG_BUCKETS = 128, ED_QG_DW = ED_QG_BUCKETS / 4;
-constexpr uint32_t ED_QG_CDW = ED_QG_DW / 4;  // coarse profiles: 32 buckets of 4 fine ones (ed_bv.hip k_qg_coarse)
 int ed_qgram_profiles(const uint16_t *bs, const uint64_t *soff, const uint32_t *len, uint32_t N, uint32_t *prof,
                       hipStream_t st);
 // Two-phase bit-parallel search (ed_bv.hip), used when the q-gram filter is on:
@@ -95,7 +94,6 @@ constexpr uint32_t ED_BV_ITEM = 4096;  // the largest item
 uint32_t ed_bv_item();
 struct EdQgArgs {
     const uint4 *prof;           // [N][ED_QG_DW / 4] q-gram profiles
-    const uint4 *profc;          // [N][ED_QG_CDW / 4] coarse profiles (ed_qgram_coarse)
     const uint32_t *len;         // [N]
     uint64_t *knn;               // [N][k]: in-band results decided here (an empty trace in the length band)
     uint64_t *counters;          // [ED_BV_NCOUNTERS] or nullptr (count pass only)
@@ -113,7 +111,6 @@ struct EdQgArgs {
     uint32_t w;                  // band
 };
 int ed_qg_filter_launch(const EdQgArgs &A, bool count, hipStream_t st);
-int ed_qgram_coarse(const uint32_t *prof, uint32_t N, uint32_t *coarse, hipStream_t st);
 int ed_qg_scatter_launch(const EdQgArgs &A, uint32_t n_rec, hipStream_t st);
 int ed_bv_dp_launch(const EdBvArgs &A, const uint32_t *ioff, const uint32_t *poff, const uint32_t *ent,
                     uint32_t n_pairs, uint32_t n_items, uint32_t item, uint32_t bw, bool cmp, hipStream_t st);

@@ -42,17 +42,11 @@ LEGS = {
 
 def dp_pairs_of_run(leg_dir):
     """DP pairs of the profiled run's own search (bench JSON line on stdout: trace.json), or None."""
-    # bench.py prints each secondary leg on its own line ({"secondary_leg": ...}) before the compact headline
-    # (older runs: one line with a "secondary" list)
     try:
-        lines = [json.loads(x) for x in open(os.path.join(leg_dir, "trace.json")).read().strip().splitlines()
-                 if x.startswith("{")]
-    except (OSError, ValueError):
+        line = json.loads(open(os.path.join(leg_dir, "trace.json")).read().strip().splitlines()[-1])
+    except (OSError, ValueError, IndexError):
         return None
-    legs = [x["secondary_leg"] for x in lines if "secondary_leg" in x]
-    for x in lines:
-        legs += x.get("secondary", []) if isinstance(x.get("secondary"), list) else []
-    for sec in legs:
+    for sec in line.get("secondary", []):
         if sec.get("search", {}).get("dp_pairs"):
             return int(sec["search"]["dp_pairs"])
     return None
