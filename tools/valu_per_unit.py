@@ -42,11 +42,17 @@ LEGS = {
 
 def dp_pairs_of_run(leg_dir):
     """DP pairs of the profiled run's own search (bench JSON line on stdout: trace.json), or None."""
+    # bench.py prints each secondary leg on its own line ({"secondary_leg": ...}) before the compact headline
+    # (older runs: one line with a "secondary" list)
     try:
-        line = json.loads(open(os.path.join(leg_dir, "trace.json")).read().strip().splitlines()[-1])
-    except (OSError, ValueError, IndexError):
+        lines = [json.loads(x) for x in open(os.path.join(leg_dir, "trace.json")).read().strip().splitlines()
+                 if x.startswith("{")]
+    except (OSError, ValueError):
         return None
-    for sec in line.get("secondary", []):
+    legs = [x["secondary_leg"] for x in lines if "secondary_leg" in x]
+    for x in lines:
+        legs += x.get("secondary", []) if isinstance(x.get("secondary"), list) else []
+    for sec in legs:
         if sec.get("search", {}).get("dp_pairs"):
             return int(sec["search"]["dp_pairs"])
     return None
