@@ -2037,7 +2037,7 @@ int nmz_replayable_seeds_destroy(nmz_replayable_seeds *seeds) {
 #define NMZ_TRACES_ONE_STREAM 0
 #endif
 #ifndef NMZ_TRACES_DEFAULT_MODE
-#define NMZ_TRACES_DEFAULT_MODE 1
+#define NMZ_TRACES_DEFAULT_MODE 4
 #endif
 int nmz_replayable_sweep_traces(nmz_ctx *ctx, uint32_t n_traces, const uint32_t *const *hint_off,
                                 const uint8_t *const *hint_bytes, const uint32_t *n_events, int64_t max_interval_ns,
@@ -2068,8 +2068,14 @@ int nmz_replayable_sweep_traces(nmz_ctx *ctx, uint32_t n_traces, const uint32_t 
     NMZ_TRY(seeds_create_locked(ctx, nullptr, nullptr, S, seed_lo, &ss));
     nmz_ctx *ctxs[2] = {ctx, ctx->helper};
     std::vector<nmz_replayable_plan *> plans(n_traces, nullptr);
+    const int mode = [] {
+        const char *e = ab_env("NMZ_TRACES_MODE");
+        return e && e[0] >= '0' && e[0] <= '5' ? e[0] - '0' : NMZ_TRACES_DEFAULT_MODE;
+    }();
     auto make = [&](uint32_t j) {
-        return plan_create(ctxs[j % 2], hint_off[j], hint_bytes[j], n_events[j], max_interval_ns, S, &plans[j], true);
+        // mode 4: every build on the helper context's stream, every sweep on ctx's: a two-stage pipeline
+        nmz_ctx *bc = mode >= 4 ? ctx->helper : ctxs[j % 2];
+        return plan_create(bc, hint_off[j], hint_bytes[j], n_events[j], max_interval_ns, S, &plans[j], true);
     };
     auto finish = [&](uint32_t j) -> int {
         const int r = hipEventSynchronize(ctx->sweep_ev[j % 3]) == hipSuccess ? NMZ_OK
@@ -2083,23 +2089,23 @@ int nmz_replayable_sweep_traces(nmz_ctx *ctx, uint32_t n_traces, const uint32_t 
     constexpr uint32_t AHEAD = 2;
     int rc = NMZ_OK;
     for (uint32_t j = 0; j < std::min(AHEAD, n_traces) && rc == NMZ_OK; ++j) rc = make(j);
-    // trace i sweeps on the stream its plan was built on, and trace i + 2's build is enqueued behind that sweep
-    // (two streams in all, each serial: build, sweep, build, ...): 0.179 ms per trace against 0.188 with the
-    // builds and sweeps on four streams (NMZ_TRACES_MODE=0, profiles/r04/e2e_native_ab/). NMZ_TRACES_MODE=2: the
-    // same, with trace i's top-k read after trace i + 1's sweep is enqueued instead of trace i + 2's
-    // NMZ_TRACES_MODE=3: the Python-driven stream's schedule (bench.py end_to_end): builds on the two contexts'
-    // streams, sweeps on two streams of their own (four in all), trace i + 2's build enqueued before trace i's
-    // sweep, trace i - 1's top-k read once trace i's sweep is enqueued
-    const int mode = [] {
-        const char *e = ab_env("NMZ_TRACES_MODE");
-        return e && e[0] >= '0' && e[0] <= '3' ? e[0] - '0' : NMZ_TRACES_DEFAULT_MODE;
-    }();
+    // The schedule (NMZ_TRACES_MODE, A/B). 4, the default: a two-stage pipeline -- every plan build on the helper
+    // context's stream, two traces ahead, every sweep (+ top-k + its copy to the host) on ctx's stream behind the
+    // build it waits for, trace i - 1's top-k read once trace i's sweep is enqueued: 0.153-0.155 ms per trace over
+    // 64 traces, against 0.154-0.156 for the Python-driven stream in the same process (profiles/r05/traces_mode_ab).
+    // 1: trace i sweeps on the stream its plan was built on, trace i + 2's build behind that sweep (two streams,
+    // each serial): 0.165. 2: 1 with trace i's top-k read after trace i + 1's sweep. 3: the Python loop's own
+    // four-stream schedule (builds on the two contexts' streams, sweeps on two more): 0.185. 0: builds and sweeps on
+    // four streams, lag 2 (round 4: 0.188). 5: 4 with the sweeps alternating over two streams.
     const bool same_stream = mode == 1 || mode == 2;
-    const uint32_t lag = (mode == 2 || mode == 3) ? 1 : 2;
+    const uint32_t lag = (mode >= 2) ? 1 : 2;
     for (uint32_t i = 0; i < n_traces && rc == NMZ_OK; ++i) {
         if (!same_stream && i + AHEAD < n_traces) rc = make(i + AHEAD);
         if (rc != NMZ_OK) break;
-        hipStream_t st = same_stream ? ctxs[i % 2]->stream : ctx->sweep_st[NMZ_TRACES_ONE_STREAM ? 0 : i % 2];
+        hipStream_t st = mode == 4   ? ctx->stream
+                         : mode == 5 ? (i % 2 ? ctx->sweep_st[0] : ctx->stream)
+                         : same_stream ? ctxs[i % 2]->stream
+                                       : ctx->sweep_st[NMZ_TRACES_ONE_STREAM ? 0 : i % 2];
         rc = replayable_run(plans[i], st, nullptr, nullptr, S, d_st[i % 2], seed_lo, k, d_tk[i % 2], 0, ss);
         if (rc != NMZ_OK) break;
         if (hipMemcpyAsync(h_tk + (size_t)(i % 3) * k, d_tk[i % 2], (size_t)k * sizeof(nmz_topk_entry),

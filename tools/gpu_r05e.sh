@@ -1,11 +1,11 @@
 #!/bin/bash
 # nmz_replayable_sweep_traces schedules (NMZ_TRACES_MODE 1 = two serial streams, 3 = the Python loop's four-stream
 # schedule) against the Python-driven stream, same process each: bench.py's replayable leg. usage: tools/gpu_r05e.sh <tag>
-tag=${1:-r05e}
+tag=${1:-r05e}; shift; MODES=${*:-1 3}
 O=gpurun_out/$tag
 mkdir -p $O
 for rep in 1 2; do
-  for m in 1 3; do
+  for m in $MODES; do
     NMZ_AB=1 NMZ_TRACES_MODE=$m timeout -k 10 150 python bench.py --legs replayable --no-cpu-baseline --steps 20 --warmup 5 --full-record $O/mode${m}_$rep.json > /dev/null 2> $O/mode${m}_$rep.err || exit $?
   done
 done
