@@ -228,6 +228,38 @@ __device__ __forceinline__ void bv_step2(BvState<BvShape<W>::KF> &S1, BvState<Bv
     }
 }
 
+// one query of the interleaved pair tables (addr already + 4 * query slot): its dwords are 8 bytes apart
+template <int W, int t, bool SLOW>
+__device__ __forceinline__ void bv_step1(BvState<BvShape<W>::KF> &S, const uint32_t *peq_bytes, uint32_t addr,
+                                         uint32_t j, uint32_t m, uint32_t n, bool &run, uint32_t &r, uint32_t w1) {
+    using SH = BvShape<W>;
+    const uint32_t *pp = (const uint32_t *)((const char *)peq_bytes + addr);
+    uint32_t d[SH::ND];
+#pragma unroll
+    for (int k = 0; k < SH::ND; ++k) d[k] = pp[2 * k];
+    bv_column<W, t>(S, d);
+    if constexpr (SLOW) {
+        if (j == m && run) {
+            const uint32_t Tj = S.T + (t + 1) - __builtin_popcount(S.acc >> (31 - t));
+            r = min(bv_extract<W>(S, Tj, n + W - m), w1);
+            run = false;
+        }
+    }
+}
+
+template <int W, bool CMP, bool SLOW, int t = 0>
+__device__ __forceinline__ void bv_block1(BvState<BvShape<W>::KF> &S, const uint32_t *peq, const uint16_t *rmap,
+                                          const uint32_t (&sym)[16], uint32_t base, uint32_t j0, uint32_t m,
+                                          uint32_t n, bool &run, uint32_t &r, uint32_t w1) {
+    if constexpr (t < 32) {
+        const uint32_t w = sym[t / 2];
+        const uint32_t s = (t & 1) ? (w >> 16) : (w & 0xffffu);
+        const uint32_t addr = (CMP ? (uint32_t)rmap[s] : s) + base;
+        bv_step1<W, t, SLOW>(S, peq, addr, j0 + t + 1, m, n, run, r, w1);
+        bv_block1<W, CMP, SLOW, t + 1>(S, peq, rmap, sym, base, j0, m, n, run, r, w1);
+    }
+}
+
 // rmap: the compact tables' map symbol id -> row byte offset (LDS, CMP only)
 template <int W, bool CMP, bool SLOW, int t = 0>
 __device__ __forceinline__ void bv_block(BvState<BvShape<W>::KF> &S1, BvState<BvShape<W>::KF> &S2,
@@ -381,6 +413,10 @@ __device__ __forceinline__ void qg_l1x2(const uint4 *__restrict__ cp, const uint
     }
 }
 
+#ifndef NMZ_ED_DP_MONO
+#define NMZ_ED_DP_MONO 1
+#endif
+
 // Occupancy: 5 waves/SIMD (<= 96 VGPRs; the compiler spills 6 VGPRs outside the 32-column block). configs[2]
 // clustered, 100k x 2,048: 1.509 s at the unconstrained 100 VGPRs (4 waves), 1.487 s at 5, 1.667 s at 6 (31
 // spills, some in the block refill path). NMZ_ED_BV_WAVES overrides for A/B builds.
@@ -498,6 +534,59 @@ __device__ __forceinline__ void bv_dp_run(const EdBvArgs &A, const uint32_t *peq
             active = false;
             need = true;
         }
+    }
+}
+
+// An item of at most 128 entries (a sparse search: a query pair with a few DP candidates): lane 2e + s runs the
+// single pair (query s of the pair, entry e's candidate) when entry e needs it, one query state per lane instead of
+// two. A lane of the paired loop above steps both queries for every candidate, so a pair whose other query was
+// settled by the filter (most of them when the entries are few) cost a full second column step; here a lane's
+// chain is half as long, and a workgroup's 256 lanes still hold every pair of the item (no refill).
+template <int W, bool CMP, class Fetch>
+__device__ __forceinline__ void bv_dp_mono(const EdBvArgs &A, const uint32_t *peq, uint32_t ns, uint32_t q1,
+                                           uint32_t q2, uint32_t n1, uint32_t n2, Fetch fetch, uint32_t &c_dp_pairs,
+                                           uint32_t &c_in_band, uint32_t &c_blocks, uint32_t &c_dp_cand,
+                                           uint32_t &c_live) {
+    using SH = BvShape<W>;
+    const uint32_t lane = threadIdx.x & 63, e = threadIdx.x >> 1, sq = threadIdx.x & 1;
+    const uint32_t w = A.w, w1 = A.w + 1;
+    const uint16_t *rmap = (const uint16_t *)(peq + A.rmap_dw);
+    uint32_t j = 0;
+    bool run = false;
+    if (e < ns) {
+        bool a1, a2;
+        fetch(e, j, a1, a2);
+        run = sq ? a2 : a1;
+        if (sq == 0) c_dp_cand += 1;  // an entry counts once
+    }
+    bool active = run;
+    c_dp_pairs += (uint32_t)run;
+    const uint32_t m = active ? A.len[j] : 0u, n = sq ? n2 : n1;
+    const uint16_t *stream = active ? A.bsym + A.soff[j] : A.bsym;  // idle lanes read a valid stream
+    uint32_t r = w1;
+    BvState<SH::KF> S;
+    bv_init<W>(S);
+    uint32_t cur[16], nxt[16];
+    bv_load_block(cur, stream, 0);
+    for (uint32_t kb = 0; __any(active); ++kb) {
+        c_blocks += (uint32_t)active;
+        c_live += (uint32_t)(active && run);
+        bv_load_block(nxt, stream, kb + 1);  // streams carry one spare block
+        const uint32_t j0 = 32 * kb, base = (kb + 1) * 8 + 4 * sq;
+        const bool here = active && run && m > j0 && m <= j0 + 32;
+        if (__any(here)) {
+            bv_block1<W, CMP, true>(S, peq, rmap, cur, base, j0, m, n, run, r, w1);
+        } else {
+            bv_block1<W, CMP, false>(S, peq, rmap, cur, base, j0, m, n, run, r, w1);
+        }
+        S.T += 32 - __builtin_popcount(S.acc);
+        if (run && bv_lower_bound<W>(S, S.T) > w) run = false;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) cur[k] = nxt[k];
+        const bool fin = active && !run;
+        if (__any(fin))
+            bv_publish(A, fin, j, q1, q2, sq == 1, sq ? w1 : r, sq ? r : w1, lane, w, c_in_band);
+        if (fin) active = false;
     }
 }
 
@@ -809,14 +898,19 @@ __global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv_dp(EdBvArgs A, con
                          has2 ? A.bsym + A.soff[q2] : nullptr, n2);
     __syncthreads();
     uint32_t c_dp_pairs = 0, c_in_band = 0, c_blocks = 0, c_dp_cand = 0, c_live = 0;
-    bv_dp_run<W, CMP>(A, peq, pool_next, ns, q1, q2, n1, n2, has2,
-                 [&](uint32_t i, uint32_t &jj, bool &a1, bool &a2) {
-                     const uint32_t e = ent[e0 + i];
-                     jj = e & 0x3fffffffu;
-                     a1 = (e >> 30) & 1u;
-                     a2 = e >> 31;
-                 },
-                 c_dp_pairs, c_in_band, c_blocks, c_dp_cand, c_live);
+    auto fetch = [&](uint32_t i, uint32_t &jj, bool &a1, bool &a2) {
+        const uint32_t e = ent[e0 + i];
+        jj = e & 0x3fffffffu;
+        a1 = (e >> 30) & 1u;
+        a2 = e >> 31;
+    };
+#if NMZ_ED_DP_MONO
+    if (ns <= 128)  // workgroup-uniform
+        bv_dp_mono<W, CMP>(A, peq, ns, q1, q2, n1, n2, fetch, c_dp_pairs, c_in_band, c_blocks, c_dp_cand, c_live);
+    else
+#endif
+        bv_dp_run<W, CMP>(A, peq, pool_next, ns, q1, q2, n1, n2, has2, fetch, c_dp_pairs, c_in_band, c_blocks,
+                          c_dp_cand, c_live);
     bv_flush_counters(A.counters, c_dp_pairs, c_in_band, c_blocks, c_dp_cand, c_live, 0);
 }
 

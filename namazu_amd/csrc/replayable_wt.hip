@@ -845,8 +845,18 @@ __device__ unsigned long long g_wt_trace[256][16][10];
 
 // G workgroups per row L: each stages the row image into LDS and takes a contiguous share of the row's chunks of
 // 64 NS seeds (NS per lane), which its waves take one at a time from an LDS counter.
+// The row image (~84 KB at configs[1]) allows one workgroup (16 waves, 4 per SIMD) per CU, so registers beyond the 64
+// that 8 waves/SIMD would need cost no occupancy; NMZ_WT_WAVES=4 lets the compiler schedule with up to 128 (A/B)
+#ifndef NMZ_WT_WAVES
+#define NMZ_WT_WAVES 0
+#endif
+#if NMZ_WT_WAVES > 0
+#define NMZ_WT_ATTR __attribute__((amdgpu_waves_per_eu(NMZ_WT_WAVES, NMZ_WT_WAVES)))
+#else
+#define NMZ_WT_ATTR
+#endif
 template <bool BIG, int NS>
-__global__ __launch_bounds__(1024) void k_replayable_sweep_wt(
+__global__ __launch_bounds__(1024) NMZ_WT_ATTR void k_replayable_sweep_wt(
     const uint32_t *__restrict__ bucket_off, const uint64_t *__restrict__ sorted_h0,
     const uint32_t *__restrict__ sorted_idx, const uint4 *__restrict__ table, uint32_t E,
     const uint4 *__restrict__ blob, uint32_t rb16, const unsigned long long *__restrict__ rowsum,
