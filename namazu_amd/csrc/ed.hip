@@ -444,6 +444,8 @@ struct nmz_ed_plan {
     };
     std::map<uint64_t, TpSizes> tp_sizes;  // per (shard, n_shards): entry total, DP items, records of its searches
     uint32_t *d_tp_mismatch = nullptr;     // (in tp_mem) set when a search's totals differ from tp_sizes
+    uint32_t *d_rec_clear = nullptr;       // the record counter last cleared by a memset (tp_rec moves when it grows)
+    bool tp_dirty = false;                 // a count pass's counts not yet taken back by its write pass
     // fixed at creation (NMZ_ED_QGRAM / NMZ_ED_TWO_PHASE, A/B knobs read once per plan), so every shard and every
     // call of one plan takes the same search and deals pairs by the same rule
     bool qgram = true, two_phase = true;
@@ -1042,12 +1044,6 @@ static int ed_plan_build(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym,
     return NMZ_OK;
 }
 
-// work items per query pair: ceil(entries / item) (items[n_pairs] = 0 closes the scan)
-__global__ void k_bv_items(const uint32_t *__restrict__ cnt, uint32_t n, uint32_t item, uint32_t *__restrict__ items) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i <= n) items[i] = i < n ? (cnt[i] + item - 1) / item : 0u;
-}
-
 // Entries per DP work item. One workgroup runs one item with its pair's Peq tables; the last items of a launch
 // leave CUs idle until they end, so their length is the launch's tail (~1 item per CU slot): a shard of the
 // 8-GPU search has 1/8 of the items, so the tail weighs 8x more there.
@@ -1088,28 +1084,151 @@ static uint64_t ed_tp_max_entries() {
     return ED_TP_MAX_ENTRIES;
 }
 
-// the cached two-phase sizes against this search's own (ed_bv_two_phase): flag[0] = 1 on any difference
-__global__ void k_tp_verify(const uint64_t *__restrict__ tot64, const uint32_t *__restrict__ items,
-                            const uint32_t *__restrict__ n_rec, uint64_t e_tot, uint32_t e_items, uint32_t e_rec,
-                            uint32_t *__restrict__ flag) {
-    if (threadIdx.x == 0 && (*tot64 != e_tot || *items != e_items || *n_rec != e_rec)) atomicOr(flag, 1u);
+// The two-phase search's offsets after a count pass (ed_bv_two_phase), in two launches: k_tp_reduce sums each
+// block's chunk of query pairs (DP entries, work items of `item` entries), k_tp_scan turns the sums into the pairs'
+// entry offsets (poff) and work-item offsets (ioff). The last block writes the 64-bit entry total (the u32 offsets
+// wrap beyond 2^32 entries, so they are trusted only while the total is within the batching limit), compares the
+// totals with a shard's cached sizes (flag), and moves the survivor-record counter to rec_out, leaving it at zero
+// for the next count pass. (These were hipcub scans of the two arrays, an item kernel, a one-block sum, a verify
+// kernel, a cursor copy and two clears: 11 launches and ~55 us per search, a fixed cost each shard of the 8-GPU
+// search paid once more.)
+constexpr uint32_t TP_PER_THREAD = 8, TP_TILE = 256 * TP_PER_THREAD, TP_MAX_BLOCKS = 256;
+struct TpScanArgs {
+    const uint32_t *cnt;    // [n] DP entries per query pair
+    uint32_t n, lg_item;    // pairs; log2 entries per work item
+    uint32_t chunk, nb;     // pairs per block (a multiple of TP_TILE), blocks (<= TP_MAX_BLOCKS)
+    uint64_t *agg;          // [2 TP_MAX_BLOCKS]: block b's entries, items
+    uint32_t *poff, *ioff;  // [n + 1]
+    uint64_t *tot64;
+    uint32_t *n_rec, *rec_out;  // the record counter (or nullptr) and where its value goes
+    uint32_t *flag;         // or nullptr: no cached sizes to compare
+    uint64_t e_tot;
+    uint32_t e_items, e_rec;
+};
+
+__device__ __forceinline__ uint32_t tp_items(uint32_t c, uint32_t lg) { return (c + (1u << lg) - 1) >> lg; }
+
+// block-wide sums of two u64 (256 threads); every thread gets them
+__device__ __forceinline__ void tp_block_sum(uint64_t &a, uint64_t &b, uint64_t (*sh)[4]) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        a += __shfl_xor((unsigned long long)a, off, 64);
+        b += __shfl_xor((unsigned long long)b, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        sh[0][threadIdx.x >> 6] = a;
+        sh[1][threadIdx.x >> 6] = b;
+    }
+    __syncthreads();
+    a = sh[0][0] + sh[0][1] + sh[0][2] + sh[0][3];
+    b = sh[1][0] + sh[1][1] + sh[1][2] + sh[1][3];
+    __syncthreads();
 }
 
-// one block: sum of n u32 counts in u64
-__global__ __launch_bounds__(1024) void k_sum_u32_u64(const uint32_t *__restrict__ cnt, uint32_t n,
-                                                      uint64_t *__restrict__ out) {
-    __shared__ uint64_t part[16];
-    uint64_t s = 0;
-    for (uint32_t i = threadIdx.x; i < n; i += 1024) s += cnt[i];
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t t = 0;
-        for (int w = 0; w < 16; ++w) t += part[w];
-        *out = t;
+__global__ __launch_bounds__(256) void k_tp_reduce(TpScanArgs A) {
+    __shared__ uint64_t sh[2][4];
+    const uint32_t lo = blockIdx.x * A.chunk, hi = min(A.n, lo + A.chunk);
+    uint64_t e = 0, it = 0;
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += 256) {
+        const uint32_t c = A.cnt[i];
+        e += c;
+        it += tp_items(c, A.lg_item);
     }
+    tp_block_sum(e, it, sh);
+    if (threadIdx.x == 0) {
+        A.agg[2 * blockIdx.x] = e;
+        A.agg[2 * blockIdx.x + 1] = it;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_tp_scan(TpScanArgs A) {
+    __shared__ uint64_t sh[2][4];
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    uint64_t ce = 0, ci = 0;  // the entries and items before this block (nb <= 256: one sum per thread)
+    if (t < blockIdx.x) {
+        ce = A.agg[2 * t];
+        ci = A.agg[2 * t + 1];
+    }
+    tp_block_sum(ce, ci, sh);
+    const uint32_t hi = min(A.n, (blockIdx.x + 1) * A.chunk);
+    for (uint32_t base = blockIdx.x * A.chunk; base < hi; base += TP_TILE) {
+        const uint32_t i0 = base + TP_PER_THREAD * t;
+        uint32_t c[TP_PER_THREAD];
+        if (i0 + TP_PER_THREAD <= hi) {
+            const uint4 x = *(const uint4 *)(A.cnt + i0), y = *(const uint4 *)(A.cnt + i0 + 4);
+            c[0] = x.x, c[1] = x.y, c[2] = x.z, c[3] = x.w, c[4] = y.x, c[5] = y.y, c[6] = y.z, c[7] = y.w;
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < TP_PER_THREAD; ++k) c[k] = i0 + k < hi ? A.cnt[i0 + k] : 0u;
+        }
+        uint64_t se = 0, si = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < TP_PER_THREAD; ++k) {
+            se += c[k];
+            si += tp_items(c[k], A.lg_item);
+        }
+        // the thread's exclusive prefix inside the tile: wave scan, then the earlier waves' totals
+        uint64_t xe = se, xi = si;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t ue = __shfl_up((unsigned long long)xe, d, 64), ui = __shfl_up((unsigned long long)xi, d, 64);
+            if (lane >= (uint32_t)d) {
+                xe += ue;
+                xi += ui;
+            }
+        }
+        if (lane == 63) {
+            sh[0][wv] = xe;
+            sh[1][wv] = xi;
+        }
+        __syncthreads();
+        uint64_t pe = ce + xe - se, pi = ci + xi - si, te = 0, ti = 0;
+        for (uint32_t w = 0; w < 4; ++w) {
+            if (w < wv) {
+                pe += sh[0][w];
+                pi += sh[1][w];
+            }
+            te += sh[0][w];
+            ti += sh[1][w];
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < TP_PER_THREAD; ++k) {
+            if (i0 + k < hi) {
+                A.poff[i0 + k] = (uint32_t)pe;
+                A.ioff[i0 + k] = (uint32_t)pi;
+            }
+            pe += c[k];
+            pi += tp_items(c[k], A.lg_item);
+        }
+        ce += te;
+        ci += ti;
+    }
+    if (blockIdx.x + 1 == A.nb && t == 0) {
+        A.poff[A.n] = (uint32_t)ce;
+        A.ioff[A.n] = (uint32_t)ci;
+        *A.tot64 = ce;
+        const uint32_t r = A.n_rec ? *A.n_rec : 0u;
+        if (A.n_rec) {
+            *A.rec_out = r;
+            *A.n_rec = 0;
+        }
+        if (A.flag && (ce != A.e_tot || (uint32_t)ci != A.e_items || r != A.e_rec)) atomicOr(A.flag, 1u);
+    }
+}
+
+static int tp_offsets(TpScanArgs &A, uint32_t item, hipStream_t st) {
+    A.lg_item = 0;
+    while ((1u << A.lg_item) < item) ++A.lg_item;
+    NMZ_CHECK((1u << A.lg_item) == item, "internal: the work-item size is not a power of two");
+    const uint32_t tiles = (A.n + TP_TILE - 1) / TP_TILE;
+    A.nb = std::min(tiles, TP_MAX_BLOCKS);
+    A.chunk = (tiles + A.nb - 1) / A.nb * TP_TILE;
+    A.nb = (A.n + A.chunk - 1) / A.chunk;
+    hipLaunchKernelGGL(k_tp_reduce, dim3(A.nb), dim3(256), 0, st, A);
+    hipLaunchKernelGGL(k_tp_scan, dim3(A.nb), dim3(256), 0, st, A);
+    NMZ_HIP(hipGetLastError());
+    return NMZ_OK;
 }
 
 // The shard's tiles in query-block order; the count pass sizes the entry lists. Entry lists beyond
@@ -1161,24 +1280,22 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
         if (!tiles.empty()) NMZ_HIP(hipMemcpy(tl.ptr, tiles.data(), tiles.size() * 8, hipMemcpyHostToDevice));
         p->tile_count[key] = tiles.size();
     }
-    size_t scan_bytes = 0;
-    NMZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                             (int)n_pairs + 1, st));
-    NMZ_TRY(p->tp_mem.ensure(5 * Carve::bytes_for(n_pairs + 1, 4) + Carve::bytes_for(scan_bytes, 1) +
-                             Carve::bytes_for(4, 4) + Carve::bytes_for(1, 8)));
+    // scratch: {mismatch flag, record count out}, the entry total, the offset kernels' block sums, the per-pair
+    // counts (zero between searches: the write pass takes back what the count pass added) and offsets
+    const size_t tp_bytes = Carve::bytes_for(4, 4) + Carve::bytes_for(1, 8) + Carve::bytes_for(2 * TP_MAX_BLOCKS, 8) +
+                            3 * Carve::bytes_for(n_pairs + 1, 4);
+    NMZ_TRY(p->tp_mem.ensure(tp_bytes));
     Carve cv(p->tp_mem.ptr);
-    uint64_t *d_tot64 = cv.take<uint64_t>(1);
-    {
-        uint32_t *f = cv.take<uint32_t>(4);
-        if (f != p->d_tp_mismatch) {  // a new scratch buffer: its flag starts clear
-            NMZ_HIP(hipMemsetAsync(f, 0, 16, st));
-            p->d_tp_mismatch = f;
-        }
-    }
+    uint32_t *f = cv.take<uint32_t>(4);
+    uint64_t *d_tot64 = cv.take<uint64_t>(1), *d_agg = cv.take<uint64_t>(2 * TP_MAX_BLOCKS);
     uint32_t *d_cnt = cv.take<uint32_t>(n_pairs + 1), *d_poff = cv.take<uint32_t>(n_pairs + 1);
-    uint32_t *d_items = cv.take<uint32_t>(n_pairs + 1), *d_ioff = cv.take<uint32_t>(n_pairs + 1);
-    uint32_t *d_cur = cv.take<uint32_t>(n_pairs + 1);
-    void *d_scan = cv.take<char>(scan_bytes);
+    uint32_t *d_ioff = cv.take<uint32_t>(n_pairs + 1);
+    if (f != p->d_tp_mismatch) {  // a new scratch buffer: flag and counts start clear
+        NMZ_HIP(hipMemsetAsync(p->tp_mem.ptr, 0, tp_bytes, st));
+        p->d_tp_mismatch = f;
+    } else if (p->tp_dirty) {  // an earlier search stopped between its count and write passes
+        NMZ_HIP(hipMemsetAsync(d_cnt, 0, (n_pairs + 1) * 4, st));
+    }
     const uint64_t n_tiles_all = p->tile_count[key];
     EdQgArgs Q;
     Q.prof = A.prof;
@@ -1186,7 +1303,7 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     Q.knn = A.knn;
     Q.counters = A.counters;
     Q.cnt = d_cnt;
-    Q.cur = d_cur;
+    Q.poff = d_poff;
     Q.ent = nullptr;
     // the count pass's survivor records (32 B per (wave, query pair) with survivors) let the write pass scatter
     // without recomputing the filter; room for 16 per tile (a record list that overflows: the write pass recomputes)
@@ -1203,6 +1320,11 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
         Q.rec_cap = (uint32_t)rec_cap;
     }
     Q.n_rec = Q.recs ? p->tp_rec.as<uint32_t>() : nullptr;  // the counter in the buffer's first 16 bytes
+    // (k_tp_scan leaves it at zero; a new buffer or an interrupted search clears it here)
+    if (Q.n_rec && (Q.n_rec != p->d_rec_clear || p->tp_dirty)) {
+        NMZ_HIP(hipMemsetAsync(Q.n_rec, 0, 4, st));
+        p->d_rec_clear = Q.n_rec;
+    }
     Q.N = N;
     Q.k = A.k;
     Q.QB = QB;
@@ -1216,28 +1338,41 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     // count pass + scans over a tile list: entry and item totals
     uint32_t n_rec = 0;
     // readback = false (sizes known from an earlier search of this shard): everything stays on the device
+    // the offset kernels' arguments (tp_offsets); verify = a shard's cached sizes to compare with
+    auto offsets = [&](bool with_rec, const nmz_ed_plan::TpSizes *verify) -> int {
+        TpScanArgs S{};
+        S.cnt = d_cnt;
+        S.n = n_pairs;
+        S.agg = d_agg;
+        S.poff = d_poff;
+        S.ioff = d_ioff;
+        S.tot64 = d_tot64;
+        S.n_rec = with_rec ? Q.n_rec : nullptr;
+        S.rec_out = f + 1;
+        S.flag = verify ? p->d_tp_mismatch : nullptr;
+        if (verify) {
+            S.e_tot = verify->tot64;
+            S.e_items = verify->items;
+            S.e_rec = verify->n_rec;
+        }
+        return tp_offsets(S, item, st);
+    };
     auto count = [&](const uint64_t *tiles, uint64_t n_tiles, uint64_t &tot64, uint32_t &tot_items,
-                     bool readback = true) -> int {
+                     const nmz_ed_plan::TpSizes *verify = nullptr) -> int {
         Q.tiles = tiles;
         Q.n_tiles = n_tiles;
-        NMZ_HIP(hipMemsetAsync(d_cnt, 0, (n_pairs + 1) * 4, st));
-        if (Q.recs) NMZ_HIP(hipMemsetAsync(Q.n_rec, 0, 4, st));
+        p->tp_dirty = true;  // until the write pass has taken the counts back
         {
             KernelTimer kt(p->ctx, st, "ed_qg_filter");
             NMZ_TRY(ed_qg_filter_launch(Q, true, st));
         }
-        NMZ_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_cnt, d_poff, (int)n_pairs + 1, st));
-        hipLaunchKernelGGL(k_bv_items, dim3(ceil_div(n_pairs + 1, 256)), dim3(256), 0, st, d_cnt, n_pairs, item,
-                           d_items);
-        NMZ_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_items, d_ioff, (int)n_pairs + 1, st));
-        // the entry total in 64 bits: the u32 scans above wrap beyond 2^32 entries (about N^2 / 4 for a store of
-        // near-duplicates), so their totals are trusted only once this sum is within the limit
-        hipLaunchKernelGGL(k_sum_u32_u64, dim3(1), dim3(1024), 0, st, d_cnt, n_pairs, d_tot64);
-        NMZ_HIP(hipGetLastError());
-        if (!readback) return NMZ_OK;
+        // the entry total in 64 bits: the u32 offsets wrap beyond 2^32 entries (about N^2 / 4 for a store of
+        // near-duplicates), so they are trusted only once this total is within the limit
+        NMZ_TRY(offsets(true, verify));
+        if (verify) return NMZ_OK;
         NMZ_HIP(hipMemcpyAsync(&tot64, d_tot64, 8, hipMemcpyDeviceToHost, st));
         NMZ_HIP(hipMemcpyAsync(&tot_items, d_ioff + n_pairs, 4, hipMemcpyDeviceToHost, st));
-        if (Q.recs) NMZ_HIP(hipMemcpyAsync(&n_rec, Q.n_rec, 4, hipMemcpyDeviceToHost, st));
+        if (Q.recs) NMZ_HIP(hipMemcpyAsync(&n_rec, f + 1, 4, hipMemcpyDeviceToHost, st));
         NMZ_HIP(hipStreamSynchronize(st));
         return NMZ_OK;
     };
@@ -1247,12 +1382,12 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
         NMZ_CHECK(n_ent < (1ULL << 32), "internal: a two-phase batch reaches 2^32 entries");
         NMZ_TRY(p->tp_ent.ensure(Carve::bytes_for(n_ent + 1, 4)));
         Q.ent = p->tp_ent.as<uint32_t>();
-        NMZ_HIP(hipMemcpyAsync(d_cur, d_poff, (uint64_t)n_pairs * 4, hipMemcpyDeviceToDevice, st));
         {
             KernelTimer kt(p->ctx, st, "ed_qg_filter");
             if (Q.recs && n_rec <= Q.rec_cap) NMZ_TRY(ed_qg_scatter_launch(Q, n_rec, st));
             else NMZ_TRY(ed_qg_filter_launch(Q, false, st));
         }
+        p->tp_dirty = false;
         KernelTimer kt(p->ctx, st, "ed_bv_dp");
         return ed_bv_dp_launch(A, d_ioff, d_poff, Q.ent, n_pairs, n_items, item, p->bw, p->cmp, st);
     };
@@ -1262,9 +1397,7 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     // entry total is known)
     auto reitem = [&](uint32_t it) -> int {
         item = it;
-        hipLaunchKernelGGL(k_bv_items, dim3(ceil_div(n_pairs + 1, 256)), dim3(256), 0, st, d_cnt, n_pairs, item,
-                           d_items);
-        NMZ_HIP(hipcub::DeviceScan::ExclusiveSum(d_scan, scan_bytes, d_items, d_ioff, (int)n_pairs + 1, st));
+        NMZ_TRY(offsets(false, nullptr));
         NMZ_HIP(hipMemcpyAsync(&tot_items, d_ioff + n_pairs, 4, hipMemcpyDeviceToHost, st));
         NMZ_HIP(hipStreamSynchronize(st));
         return NMZ_OK;
@@ -1278,10 +1411,7 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     if (cached != p->tp_sizes.end() && Q.recs && cached->second.tot64 <= limit) {
         const nmz_ed_plan::TpSizes &z = cached->second;
         item = z.item;
-        NMZ_TRY(count(tl.as<uint64_t>(), n_tiles_all, tot64, tot_items, false));
-        hipLaunchKernelGGL(k_tp_verify, dim3(1), dim3(64), 0, st, d_tot64, d_ioff + n_pairs, Q.n_rec, z.tot64, z.items,
-                           z.n_rec, p->d_tp_mismatch);
-        NMZ_HIP(hipGetLastError());
+        NMZ_TRY(count(tl.as<uint64_t>(), n_tiles_all, tot64, tot_items, &z));
         n_rec = z.n_rec;
         return write_dp(z.tot64, z.items);
     }
@@ -1296,6 +1426,7 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     // (the count pass lists pairs with an empty trace, and adds to the counters)
     std::vector<uint32_t> cnt(n_pairs);
     NMZ_HIP(hipMemcpy(cnt.data(), d_cnt, (size_t)n_pairs * 4, hipMemcpyDeviceToHost));
+    NMZ_HIP(hipMemsetAsync(d_cnt, 0, (n_pairs + 1) * 4, st));  // (no write pass took this count pass's counts)
     shard_tiles(nullptr);
     const size_t ng = grp.size() / 2;
     hipLaunchKernelGGL(k_knn_init, dim3(ceil_div((uint64_t)N * A.k, 256)), dim3(256), 0, st, d_knn, (uint64_t)N * A.k);

@@ -808,7 +808,7 @@ __global__ __launch_bounds__(256) void k_ed_qg_filter(EdQgArgs A) {
             const uint32_t leader = (uint32_t)__ffsll((unsigned long long)mask) - 1;
             const uint32_t n = (uint32_t)__popcll(mask), p = q1 >> 1;
             uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(COUNT ? &A.cnt[p] : &A.cur[p], n);
+            if (lane == leader) base = COUNT ? atomicAdd(&A.cnt[p], n) : A.poff[p] + atomicSub(&A.cnt[p], n) - n;
             if (!COUNT) {
                 base = __shfl(base, leader, 64);
                 if (sv)
@@ -826,7 +826,7 @@ __global__ __launch_bounds__(256) void k_ed_qg_filter(EdQgArgs A) {
     if (COUNT) bv_flush_counters(A.counters, 0, c_in_band, 0, 0, 0, c_qgram);
 }
 
-// The write pass from the count pass's records (EdQgArgs::recs): a wave per record -- one cursor atomic and the
+// The write pass from the count pass's records (EdQgArgs::recs): a wave per record -- one count atomic and the
 // entries; no profile loads, no L1s, and nothing read for the (wave, pair)s without survivors (most of them: the
 // dense per-tile ballots this replaces were 2 KiB per tile, 0.6 GB read per launch on configs[2]).
 __global__ __launch_bounds__(256) void k_ed_qg_scatter(EdQgArgs A, uint32_t n_rec) {
@@ -836,7 +836,10 @@ __global__ __launch_bounds__(256) void k_ed_qg_scatter(EdQgArgs A, uint32_t n_re
         const uint4 h = A.recs[2 * (uint64_t)r], g = A.recs[2 * (uint64_t)r + 1];
         const uint64_t m1 = ((uint64_t)h.w << 32) | h.z, m2 = ((uint64_t)g.y << 32) | g.x, mask = m1 | m2;
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&A.cur[h.x], (uint32_t)__popcll(mask));
+        if (lane == 0) {  // the pair's next free slots, from its end down (the count pass's count returns to 0)
+            const uint32_t c = (uint32_t)__popcll(mask);
+            base = A.poff[h.x] + atomicSub(&A.cnt[h.x], c) - c;
+        }
         base = __shfl(base, 0, 64);
         const uint64_t bit = 1ull << lane;
         if (mask & bit)

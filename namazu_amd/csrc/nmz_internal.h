@@ -98,8 +98,9 @@ struct EdQgArgs {
     uint64_t *knn;               // [N][k]: in-band results decided here (an empty trace in the length band)
     uint64_t *counters;          // [ED_BV_NCOUNTERS] or nullptr (count pass only)
     const uint64_t *tiles;       // [n_tiles] this shard's tiles, qb << 32 | cb
-    uint32_t *cnt;               // count pass: [n_pairs] entries per query pair
-    uint32_t *cur;               // write pass: [n_pairs] cursors, starting at the pairs' entry offsets
+    uint32_t *cnt;               // [n_pairs] entries per query pair: the count pass adds, the write pass takes
+                                 // them back (its slots: poff[p] + the count left), so they end at zero again
+    const uint32_t *poff;        // write pass: [n_pairs] the pairs' entry offsets
     uint32_t *ent;               // write pass: the entries
     uint4 *recs;                 // count pass: one record per (wave, query pair) with survivors -- {pair, first
                                  // candidate, run1 ballot} and {run2 ballot} (2 uint4) -- for the scatter pass, or

@@ -13,5 +13,5 @@ for it in "$@"; do
     fi
   done
 done
-for f in $O/*.json; do python3 -c "
+for f in $O/*_traces_*.json; do python3 -c "
 import json;d=json.load(open('$f'));print('$f', round(d['unsharded_ms'],3), round(d['sum_shard_ms'],3), round(d['max_shard_ms'],3), round(d['speedup_bound'],3), 'dp', [round(r['dp_ms'],3) for r in d['per_shard']])"; done
