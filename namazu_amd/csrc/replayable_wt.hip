@@ -433,6 +433,9 @@ __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__re
         uint32_t *pmi = reinterpret_cast<uint32_t *>(img + ci.o_pm);
 #pragma unroll
         for (uint32_t k = 0; k < PP; ++k) {
+#ifdef WT_ABL_PM
+            break;
+#endif
             const uint32_t j = j0 + k;
             if (j <= n) {
                 const uint32_t lo = max(exu, k ? pre[k - 1] : 0u);  // positions < j
@@ -558,6 +561,22 @@ __device__ __forceinline__ uint32_t wt_ones(const uint2 *__restrict__ lvl, uint3
     return w.y + __popc(w.x & ((1u << (p & 31)) - 1u)) - (s >> 1);
 }
 
+#if defined(WT_ABL_LV) && WT_ABL_LV == 1
+#define WT_MK(i)                                                       \
+    ({                                                                 \
+        const uint2 mk_v_ = reinterpret_cast<const uint2 *>(mk)[(i) >> 1]; \
+        mk_v_.x ^ mk_v_.y;                                             \
+    })
+#elif defined(WT_ABL_LV) && WT_ABL_LV == 2
+#define WT_MK(i)                                                       \
+    ({                                                                 \
+        const uint4 mk_v_ = reinterpret_cast<const uint4 *>(mk)[(i) >> 2]; \
+        mk_v_.x ^ mk_v_.y ^ mk_v_.z ^ mk_v_.w;                         \
+    })
+#else
+#define WT_MK(i) mk[i]
+#endif
+
 // One seed's statistics over one segment: adds d Hm + (n - d) Hm2 to sum, the segment's wraps to W, and folds its
 // maximum key {t, ~e} into key.
 // wave-uniform constants the sweep keeps in VGPRs (operands of VOP2 forms)
@@ -659,7 +678,11 @@ __device__ __forceinline__ void wt_seed_class(const WtVConst &vc, const WtClass 
             const uint32_t nl = (uint32_t)nH[u];
             while (d[u] < n && chi[d[u]] == nh[u] && row[ci.start + d[u]].x <= nl) ++d[u];
         }
+#ifdef WT_ABL_PM
+        pmd[u] = 0;  // timing only (results wrong when a part wraps): the row image without pm
+#else
         pmd[u] = pm[d[u]];  // the parts' largest ranks (used when a part has nothing below its bound)
+#endif
     }
     // descents along R_A's and R_B's paths with the prefix [0, d) down to R's 32-rank block, branch-free with every
     // read of a level in flight: counts of ranks >= R, and the deepest level where a part's elements below R branch
@@ -668,6 +691,9 @@ __device__ __forceinline__ void wt_seed_class(const WtVConst &vc, const WtClass 
     const uint32_t *__restrict__ mk = reinterpret_cast<const uint32_t *>(img + ci.o_mk);
 #ifdef WT_ABL_COUNT
     const uint32_t K = ci.K, nw = ci.nw, lb = 0;
+#elif defined(WT_ABL_LV)
+    // timing only: WT_ABL_LV fewer levels and 2^WT_ABL_LV-times wider mask reads (64- / 128-rank blocks' cost)
+    const uint32_t K = ci.K, nw = ci.nw, lb = wt_levels(K) > WT_ABL_LV ? wt_levels(K) - WT_ABL_LV : 0;
 #else
     const uint32_t K = ci.K, nw = ci.nw, lb = wt_levels(K);
 #endif
@@ -735,7 +761,7 @@ __device__ __forceinline__ void wt_seed_class(const WtVConst &vc, const WtClass 
 #pragma unroll
     for (int u = 0; u < NS; ++u) {
         const uint32_t bA = RA[u] & ~31u, bB = RB[u] & ~31u, rA = RA[u] & 31u, rB = RB[u] & 31u;
-        const uint32_t mA = mk[bA + (bA >> 5) + oA[u]], mB = mk[bB + (bB >> 5) + oB[u]];
+        const uint32_t mA = WT_MK(bA + (bA >> 5) + oA[u]), mB = WT_MK(bB + (bB >> 5) + oB[u]);
         cA[u] += __popc(mA >> rA);
         cB[u] += __popc(mB >> rB);
         W[u] += cA[u] + (n - RB[u]) - cB[u];
@@ -786,8 +812,8 @@ __device__ __forceinline__ void wt_seed_class(const WtVConst &vc, const WtClass 
     // entries from qB on (of the block's min(n - sB, 32))
 #pragma unroll
     for (int u = 0; u < NS; ++u) {
-        const uint32_t vA = mk[sA[u] + (sA[u] >> 5) + qA[u]];
-        const uint32_t vB = ~mk[sB[u] + (sB[u] >> 5) + qB[u]] & (0xffffffffu >> (32u - min(nv - sB[u], 32u)));
+        const uint32_t vA = WT_MK(sA[u] + (sA[u] >> 5) + qA[u]);
+        const uint32_t vB = ~WT_MK(sB[u] + (sB[u] >> 5) + qB[u]) & (0xffffffffu >> (32u - min(nv - sB[u], 32u)));
         const uint32_t bA = RA[u] & ~31u, bB = RB[u] & ~31u;
         const uint32_t pA = hitA[u] ? bA + 31u - __clz(belA[u]) : wrapA[u] ? (pmd[u] & 0xffffu) : sA[u] + 31u - __clz(vA);
         const uint32_t pB = hitB[u] ? bB + 31u - __clz(belB[u]) : wrapB[u] ? (pmd[u] >> 16) : sB[u] + 31u - __clz(vB);
@@ -1273,7 +1299,9 @@ bool wt_layout(WtState &w, nmz_ctx *ctx, uint32_t E, const ClassInfo *cls, uint3
         o.o_ic = (uint32_t)off;
         off += r16(256 * 2);
         o.o_pm = (uint32_t)off;
+#ifndef WT_ABL_PM
         off += r16((uint64_t)(o.n + 1) * 4);
+#endif
         o.o_mk = (uint32_t)off;
         off += r16((uint64_t)(o.n / 32 + 1) * 33 * 4);
     }
