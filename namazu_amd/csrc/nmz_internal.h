@@ -169,6 +169,7 @@ struct ClassInfo {
 struct WtState {
     bool on = false;
     uint32_t rb16 = 0, n_classes = 0, msh = 0;
+    uint32_t bb = 5;                        // rank blocks of 2^bb ranks below the tree's levels (replayable_wt.hip)
     uint4 *d_blob = nullptr;                // [256][rb16] row images
     unsigned long long *d_rowsum = nullptr;  // [256] sum of C mod m over the row
     void *d_classes = nullptr;              // [n_classes] segment descriptors
@@ -183,13 +184,12 @@ struct WtClass {
     uint32_t o_chi, o_e;      //   Cm by rank (+ sentinel); C's high word by position (+ sentinel); e by rank (u16)
     uint32_t o_im, o_ic;      //   bucket indexes (u16): first rank with Cm >= b << msh (257); first position
                               //   with C_hi >= b << 24 (256)
-    uint32_t o_pm;            //   per d in [0, n]: {largest rank at positions < d, largest rank at positions >= d}
-                              //   (u16 pairs: the maximum of a part none of whose Cm is below its bound)
     uint32_t K, nw;           // rank bits (2^K > n); words per level (n / 32 + 1)
     uint32_t rS;              // lifting-search rounds (the largest bucket's bit length; set by the plan kernel)
-    uint32_t o_mk;            //   block masks [n / 32 + 1][33]: the ranks (bit r & 31) among the first o entries
-                              //   of each 32-rank block's node, o = 0..32
+    uint32_t o_mk;            //   block masks [(n >> bb) + 1][2^bb + 1] of 2^bb bits: the ranks (bit r mod 2^bb)
+                              //   among the first o entries of each 2^bb-rank block's node, o = 0..2^bb
     uint32_t order;           // plan kernel: the segment whose rows the order-th group of 256 workgroups builds
+    uint32_t pad;
 };
 static_assert(sizeof(WtClass) == 64, "WtClass layout");
 

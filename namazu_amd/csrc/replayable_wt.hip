@@ -53,8 +53,72 @@ __device__ unsigned long long g_wt_build_trace[WT_TRACE_WGS * WT_TRACE_PHASES];
 
 // WtClass (the segment descriptor) is in nmz_internal.h: the plan's host code packs it with the plan's inputs
 
-// the tree stores the levels above the 32-rank blocks; the blocks' masks stand for the last five
-__host__ __device__ constexpr uint32_t wt_levels(uint32_t K) { return K > 5 ? K - 5 : 0; }
+// The tree stores the levels above the rank blocks of 2^bb ranks (bb = 5, 6 or 7: 32-, 64- or 128-rank blocks, the
+// plan's choice, wt_layout); the blocks' prefix masks stand for the last bb levels. A wider block takes levels off
+// both descents (each level one dependent LDS read per chain) for a larger image: ~2^bb / 8 bytes of masks per
+// event (4, 8, 16). configs[1] (profiles/r05/k1/blocks_ab): bb = 6 takes K1 0.0656 -> 0.0623 ms and the pipelined
+// step 0.0721 -> 0.0712 ms (84 KB images); bb = 7 (118 KB) runs K1 at 0.066 ms (its 128-bit mask arithmetic) and
+// leaves the step's other kernels too little LDS beside it (step 0.082 ms), so plans take at most bb = 6.
+__host__ __device__ constexpr uint32_t wt_levels(uint32_t K, uint32_t bb) { return K > bb ? K - bb : 0; }
+// block masks' bytes: (n >> bb) + 1 blocks of 2^bb + 1 prefix masks of 2^bb bits
+__host__ __device__ constexpr uint64_t wt_mask_bytes(uint32_t n, uint32_t bb) {
+    return (uint64_t)((n >> bb) + 1) * ((1u << bb) + 1) * ((1u << bb) / 8);
+}
+
+// A block's prefix mask (2^BB bits) and the few operations the descents need on it
+template <int BB>
+struct WtMask;
+template <>
+struct WtMask<5> {
+    using T = uint32_t;
+    static __device__ __forceinline__ T load(const char *mk, uint32_t i) {
+        return reinterpret_cast<const uint32_t *>(mk)[i];
+    }
+    static __device__ __forceinline__ uint32_t count_ge(T v, uint32_t r) { return __popc(v >> r); }  // bits >= r
+    static __device__ __forceinline__ T below(T v, uint32_t r) { return __builtin_amdgcn_ubfe(v, 0u, r); }  // r < 32
+    static __device__ __forceinline__ T low(T v, uint32_t s) { return v & (0xffffffffu >> (32u - s)); }  // 1..32
+    static __device__ __forceinline__ T inv(T v) { return ~v; }
+    static __device__ __forceinline__ bool any(T v) { return v != 0; }
+    static __device__ __forceinline__ uint32_t top(T v) { return 31u - __clz(v); }  // v != 0
+};
+template <>
+struct WtMask<6> {
+    using T = uint64_t;
+    static __device__ __forceinline__ T load(const char *mk, uint32_t i) {
+        return reinterpret_cast<const uint64_t *>(mk)[i];
+    }
+    static __device__ __forceinline__ uint32_t count_ge(T v, uint32_t r) { return (uint32_t)__popcll(v >> r); }
+    static __device__ __forceinline__ T below(T v, uint32_t r) { return v & ((1ull << r) - 1ull); }
+    static __device__ __forceinline__ T low(T v, uint32_t s) { return v & (~0ull >> (64u - s)); }
+    static __device__ __forceinline__ T inv(T v) { return ~v; }
+    static __device__ __forceinline__ bool any(T v) { return v != 0; }
+    static __device__ __forceinline__ uint32_t top(T v) { return 63u - (uint32_t)__clzll(v); }
+};
+struct WtMask128 {
+    uint64_t lo, hi;
+};
+template <>
+struct WtMask<7> {
+    using T = WtMask128;
+    static __device__ __forceinline__ T load(const char *mk, uint32_t i) {
+        const uint4 x = reinterpret_cast<const uint4 *>(mk)[i];
+        return T{((uint64_t)x.y << 32) | x.x, ((uint64_t)x.w << 32) | x.z};
+    }
+    static __device__ __forceinline__ uint32_t count_ge(T v, uint32_t r) {
+        return r < 64 ? (uint32_t)(__popcll(v.lo >> r) + __popcll(v.hi)) : (uint32_t)__popcll(v.hi >> (r - 64));
+    }
+    static __device__ __forceinline__ T below(T v, uint32_t r) {
+        return r < 64 ? T{v.lo & ((1ull << r) - 1ull), 0ull} : T{v.lo, v.hi & ((1ull << (r - 64)) - 1ull)};
+    }
+    static __device__ __forceinline__ T low(T v, uint32_t s) {
+        return s <= 64 ? T{v.lo & (~0ull >> (64u - s)), 0ull} : T{v.lo, v.hi & (~0ull >> (128u - s))};
+    }
+    static __device__ __forceinline__ T inv(T v) { return T{~v.lo, ~v.hi}; }
+    static __device__ __forceinline__ bool any(T v) { return (v.lo | v.hi) != 0; }
+    static __device__ __forceinline__ uint32_t top(T v) {
+        return v.hi ? 127u - (uint32_t)__clzll(v.hi) : 63u - (uint32_t)__clzll(v.lo);
+    }
+};
 
 // ---------------------------------------------------------------------------------------------------------------
 // plan: one workgroup per (segment, row L). Sorts the segment's keys (Cm << 32 | (0xffff - e) << 16 | position)
@@ -107,7 +171,7 @@ struct WtHints {
     uint32_t n_zero1;
 };
 
-template <bool FUSED>
+template <bool FUSED, int BB>
 __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__restrict__ table, uint32_t E,
                                                                WtClass *__restrict__ classes, uint32_t msh,
                                                                uint32_t mbits, uint4 *__restrict__ blob, uint32_t rb16,
@@ -396,61 +460,12 @@ __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__re
     if (tid == 0) atomicMax(&classes[c].rS, 32u - __clz(max(bmax[2], bmax[3])));
 #endif
     WT_STAMP(5);
-    // prefix / suffix maxima of the ranks: pm[d] = {max rank at positions < d, max rank at positions >= d};
-    // PP positions per thread, wave scans (up for the prefix, down for the suffix), then the wave totals
-    {
-        constexpr uint32_t PP = WT_NMAX / WT_BT;
-        const uint32_t j0 = PP * tid;
-        uint32_t v[PP], pre[PP], suf[PP];
-#pragma unroll
-        for (uint32_t k = 0; k < PP; ++k) v[k] = j0 + k < n ? (uint32_t)S0[j0 + k] : 0u;
-        pre[0] = v[0];
-        suf[PP - 1] = v[PP - 1];
-#pragma unroll
-        for (uint32_t k = 1; k < PP; ++k) {
-            pre[k] = max(pre[k - 1], v[k]);
-            suf[PP - 1 - k] = max(suf[PP - k], v[PP - 1 - k]);
-        }
-        uint32_t up = pre[PP - 1], dn = suf[0], exu = 0, exd = 0;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t a = __shfl_up(up, o, 64), b = __shfl_down(dn, o, 64);
-            if (lane >= (uint32_t)o) {
-                up = max(up, a);
-                exu = max(exu, a);
-            }
-            if (lane + o < 64) {
-                dn = max(dn, b);
-                exd = max(exd, b);
-            }
-        }
-        if (lane == 63) wb[wave] = up;
-        if (lane == 0) wb[16 + wave] = dn;
-        __syncthreads();
-        for (uint32_t w = 0; w < WT_BW; ++w) {
-            if (w < wave) exu = max(exu, wb[w]);
-            if (w > wave) exd = max(exd, wb[16 + w]);
-        }
-        uint32_t *pmi = reinterpret_cast<uint32_t *>(img + ci.o_pm);
-#pragma unroll
-        for (uint32_t k = 0; k < PP; ++k) {
-#ifdef WT_ABL_PM
-            break;
-#endif
-            const uint32_t j = j0 + k;
-            if (j <= n) {
-                const uint32_t lo = max(exu, k ? pre[k - 1] : 0u);  // positions < j
-                const uint32_t hi = j < n ? max(exd, suf[k]) : 0u;  // positions >= j
-                pmi[j] = lo | hi << 16;
-            }
-        }
-        __syncthreads();  // wb is the level loop's next
-    }
     WT_STAMP(6);
     // wavelet levels above the 32-rank blocks. Per level, wave w ballots a contiguous range of 64-position groups
     // (bit K-1-l of the rank at each position, in this level's order), the 8 wave totals give each wave its ones
     // before its range, and every position's destination in the next level's order follows from the ones before it
     // in its node: one barrier for the totals, one for the next order (no serial scan of the words).
-    const uint32_t K = ci.K, nw = ci.nw, lb = wt_levels(K);
+    const uint32_t K = ci.K, nw = ci.nw, lb = wt_levels(K, BB);
     uint2 *lv = reinterpret_cast<uint2 *>(img + ci.o_lv);
     uint16_t *cur = S0, *nxt = S0 + WT_NMAX;
     constexpr uint32_t MAXG = (WT_NMAX / 64 + 1 + WT_BW - 1) / WT_BW;  // groups per wave, at most
@@ -499,20 +514,58 @@ __global__ __launch_bounds__(WT_BT) void k_replayable_wt_build(const uint4 *__re
         nxt = t;
     }
     WT_STAMP(7);
-    // level lb: the node of block b holds the ranks [32 b, 32 b + 32) in position order (all n ranks when K <= 5);
-    // mk[b][o] = OR of bit (rank & 31) over its first o entries: a prefix OR per block, 32 lanes per block
-    uint32_t *mk = reinterpret_cast<uint32_t *>(img + ci.o_mk);
-    const uint32_t nbk = n / 32 + 1;
-    for (uint32_t b0 = 2 * wave; b0 < nbk; b0 += 2 * WT_BW) {
-        const uint32_t b = b0 + (lane >> 5), j = 32 * b + (lane & 31);
-        uint32_t v = (b < nbk && j < n) ? 1u << (cur[j] & 31) : 0u;
-        for (int o = 1; o < 32; o <<= 1) {
-            const uint32_t u = __shfl_up(v, o, 64);
-            if ((lane & 31) >= (uint32_t)o) v |= u;
+    // level lb: the node of block b holds the ranks [2^BB b, 2^BB (b + 1)) in position order (all n ranks when K <= BB);
+    // entry o of block b = the OR of bit (rank mod 2^BB) over the block's first o entries: a prefix OR per block
+    const uint32_t nbk = (n >> BB) + 1;
+    if constexpr (BB == 5) {  // two blocks per wave step, 32 lanes each
+        uint32_t *mk = reinterpret_cast<uint32_t *>(img + ci.o_mk);
+        for (uint32_t b0 = 2 * wave; b0 < nbk; b0 += 2 * WT_BW) {
+            const uint32_t b = b0 + (lane >> 5), j = 32 * b + (lane & 31);
+            uint32_t v = (b < nbk && j < n) ? 1u << (cur[j] & 31) : 0u;
+            for (int o = 1; o < 32; o <<= 1) {
+                const uint32_t u = __shfl_up(v, o, 64);
+                if ((lane & 31) >= (uint32_t)o) v |= u;
+            }
+            if (b < nbk) {
+                mk[b * 33 + (lane & 31) + 1] = v;
+                if ((lane & 31) == 0) mk[b * 33] = 0;
+            }
         }
-        if (b < nbk) {
-            mk[b * 33 + (lane & 31) + 1] = v;
-            if ((lane & 31) == 0) mk[b * 33] = 0;
+    } else if constexpr (BB == 6) {  // a block per wave step
+        uint64_t *mk = reinterpret_cast<uint64_t *>(img + ci.o_mk);
+        for (uint32_t b = wave; b < nbk; b += WT_BW) {
+            const uint32_t j = 64 * b + lane;
+            unsigned long long v = j < n ? 1ull << (cur[j] & 63) : 0ull;
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned long long u = __shfl_up(v, o, 64);
+                if (lane >= (uint32_t)o) v |= u;
+            }
+            mk[b * 65 + lane + 1] = v;
+            if (lane == 0) mk[b * 65] = 0;
+        }
+    } else {  // a block per wave step, in two halves of 64 entries (the second half ORs in the first's total)
+        uint4 *mk = reinterpret_cast<uint4 *>(img + ci.o_mk);
+        for (uint32_t b = wave; b < nbk; b += WT_BW) {
+            unsigned long long clo = 0, chi = 0;
+            for (uint32_t hf = 0; hf < 2; ++hf) {
+                const uint32_t j = 128 * b + 64 * hf + lane, r = j < n ? (uint32_t)(cur[j] & 127) : 0u;
+                unsigned long long lo = (j < n && r < 64) ? 1ull << r : 0ull;
+                unsigned long long hi = (j < n && r >= 64) ? 1ull << (r - 64) : 0ull;
+                for (int o = 1; o < 64; o <<= 1) {
+                    const unsigned long long ul = __shfl_up(lo, o, 64), uh = __shfl_up(hi, o, 64);
+                    if (lane >= (uint32_t)o) {
+                        lo |= ul;
+                        hi |= uh;
+                    }
+                }
+                lo |= clo;
+                hi |= chi;
+                mk[b * 129 + 64 * hf + lane + 1] =
+                    make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+                clo = __shfl(lo, 63, 64);
+                chi = __shfl(hi, 63, 64);
+            }
+            if (lane == 0) mk[b * 129] = make_uint4(0u, 0u, 0u, 0u);
         }
     }
 #ifdef WT_BUILD_TRACE
@@ -561,21 +614,6 @@ __device__ __forceinline__ uint32_t wt_ones(const uint2 *__restrict__ lvl, uint3
     return w.y + __popc(w.x & ((1u << (p & 31)) - 1u)) - (s >> 1);
 }
 
-#if defined(WT_ABL_LV) && WT_ABL_LV == 1
-#define WT_MK(i)                                                       \
-    ({                                                                 \
-        const uint2 mk_v_ = reinterpret_cast<const uint2 *>(mk)[(i) >> 1]; \
-        mk_v_.x ^ mk_v_.y;                                             \
-    })
-#elif defined(WT_ABL_LV) && WT_ABL_LV == 2
-#define WT_MK(i)                                                       \
-    ({                                                                 \
-        const uint4 mk_v_ = reinterpret_cast<const uint4 *>(mk)[(i) >> 2]; \
-        mk_v_.x ^ mk_v_.y ^ mk_v_.z ^ mk_v_.w;                         \
-    })
-#else
-#define WT_MK(i) mk[i]
-#endif
 
 // One seed's statistics over one segment: adds d Hm + (n - d) Hm2 to sum, the segment's wraps to W, and folds its
 // maximum key {t, ~e} into key.
@@ -587,7 +625,7 @@ struct WtVConst {
 // NS seeds per lane (arrays indexed by u, unrolled): the wave-uniform control -- segment parameters, lifting
 // rounds, level constants, loop trips, ballots -- is paid once for NS seeds, and the NS seeds' read chains are
 // independent, so a wave keeps 2 NS dependent LDS chains in flight per descent level instead of 2.
-template <bool BIG, int NS>
+template <bool BIG, int NS, int BB>
 __device__ __forceinline__ void wt_seed_class(const WtVConst &vc, const WtClass &ci, const char *__restrict__ img,
                                               const uint4 *__restrict__ row, const uint64_t (&h0)[NS], uint32_t m,
                                               uint64_t mu, uint32_t m_k64, uint32_t msh, uint64_t (&sum)[NS],
@@ -617,7 +655,6 @@ __device__ __forceinline__ void wt_seed_class(const WtVConst &vc, const WtClass 
     const uint16_t *__restrict__ ev = reinterpret_cast<const uint16_t *>(img + ci.o_e);
     const uint16_t *__restrict__ im = reinterpret_cast<const uint16_t *>(img + ci.o_im);
     const uint16_t *__restrict__ ic = reinterpret_cast<const uint16_t *>(img + ci.o_ic);
-    const uint32_t *__restrict__ pm = reinterpret_cast<const uint32_t *>(img + ci.o_pm);
     uint32_t nh[NS], XA[NS], XB[NS];
     const uint32_t *pa[NS], *pb[NS], *pc[NS];
 #pragma unroll
@@ -666,7 +703,7 @@ __device__ __forceinline__ void wt_seed_class(const WtVConst &vc, const WtClass 
     }
     // (LDS addresses: the low words of the generic pointers)
     auto lo = [](const uint32_t *q) { return (uint32_t)reinterpret_cast<uintptr_t>(q); };
-    uint32_t d[NS], RA[NS], RB[NS], pmd[NS];
+    uint32_t d[NS], RA[NS], RB[NS];
 #pragma unroll
     for (int u = 0; u < NS; ++u) {
         RA[u] = (lo(pb[u]) - lo(cm)) >> 2;
@@ -678,24 +715,19 @@ __device__ __forceinline__ void wt_seed_class(const WtVConst &vc, const WtClass 
             const uint32_t nl = (uint32_t)nH[u];
             while (d[u] < n && chi[d[u]] == nh[u] && row[ci.start + d[u]].x <= nl) ++d[u];
         }
-#ifdef WT_ABL_PM
-        pmd[u] = 0;  // timing only (results wrong when a part wraps): the row image without pm
-#else
-        pmd[u] = pm[d[u]];  // the parts' largest ranks (used when a part has nothing below its bound)
-#endif
     }
     // descents along R_A's and R_B's paths with the prefix [0, d) down to R's 32-rank block, branch-free with every
     // read of a level in flight: counts of ranks >= R, and the deepest level where a part's elements below R branch
     // off (the predecessor's subtree: node start s, prefix offset q)
     const uint2 *__restrict__ lv = reinterpret_cast<const uint2 *>(img + ci.o_lv);
-    const uint32_t *__restrict__ mk = reinterpret_cast<const uint32_t *>(img + ci.o_mk);
+    const char *__restrict__ mk = img + ci.o_mk;
+    using MK = WtMask<BB>;
+    using MT = typename MK::T;
+    constexpr uint32_t BW = 1u << BB, BM = BW - 1;
 #ifdef WT_ABL_COUNT
     const uint32_t K = ci.K, nw = ci.nw, lb = 0;
-#elif defined(WT_ABL_LV)
-    // timing only: WT_ABL_LV fewer levels and 2^WT_ABL_LV-times wider mask reads (64- / 128-rank blocks' cost)
-    const uint32_t K = ci.K, nw = ci.nw, lb = wt_levels(K) > WT_ABL_LV ? wt_levels(K) - WT_ABL_LV : 0;
 #else
-    const uint32_t K = ci.K, nw = ci.nw, lb = wt_levels(K);
+    const uint32_t K = ci.K, nw = ci.nw, lb = wt_levels(K, BB);
 #endif
     uint32_t oA[NS], oB[NS], cA[NS], cB[NS], lA[NS], sA[NS], qA[NS], lB[NS], sB[NS], qB[NS];
 #pragma unroll
@@ -753,29 +785,39 @@ __device__ __forceinline__ void wt_seed_class(const WtVConst &vc, const WtClass 
             lvl += nw;
         }
     }
-    // R's 32-rank block: its node's first o entries are the prefix part's elements in it (mk: their ranks' bits), so
+    // R's rank block: its node's first o entries are the prefix part's elements in it (mk: their ranks' bits), so
     // the ranks >= R among them finish the counts, and those below R hold the part's predecessor when any are there
-    uint32_t belA[NS], belB[NS];
+    MT belA[NS], belB[NS];
     bool hitA[NS], hitB[NS], wrapA[NS], wrapB[NS];
     uint32_t l0 = WT_NONE;
 #pragma unroll
     for (int u = 0; u < NS; ++u) {
-        const uint32_t bA = RA[u] & ~31u, bB = RB[u] & ~31u, rA = RA[u] & 31u, rB = RB[u] & 31u;
-        const uint32_t mA = WT_MK(bA + (bA >> 5) + oA[u]), mB = WT_MK(bB + (bB >> 5) + oB[u]);
-        cA[u] += __popc(mA >> rA);
-        cB[u] += __popc(mB >> rB);
+        const uint32_t bA = RA[u] & ~BM, bB = RB[u] & ~BM, rA = RA[u] & BM, rB = RB[u] & BM;
+        const MT mA = MK::load(mk, bA + (bA >> BB) + oA[u]), mB = MK::load(mk, bB + (bB >> BB) + oB[u]);
+        cA[u] += MK::count_ge(mA, rA);
+        cB[u] += MK::count_ge(mB, rB);
         W[u] += cA[u] + (n - RB[u]) - cB[u];
-        belA[u] = __builtin_amdgcn_ubfe(mA, 0u, rA);
-        belB[u] = __builtin_amdgcn_ubfe(~mB, 0u, rB);
+        belA[u] = MK::below(mA, rA);
+        belB[u] = MK::below(MK::inv(mB), rB);
         // predecessors: in R's block when a part has an element below R there; else from the deepest branch-off
         // level down to a block (second descent: the prefix part takes the largest rank among the first qA entries of
         // node sA, the suffix part the largest among entries qB.. of node sB); a part with nothing below its bound
-        // wraps, and its maximum is its largest rank overall (pm). Levels no lane of the wave needs are skipped.
-        hitA[u] = belA[u] != 0;
-        hitB[u] = belB[u] != 0;
-        wrapA[u] = !hitA[u] && lA[u] == WT_NONE;
-        wrapB[u] = !hitB[u] && lB[u] == WT_NONE;
-        const bool dA = d[u] > 0 && !hitA[u] && !wrapA[u], dB = d[u] < n && !hitB[u] && !wrapB[u];
+        // wraps, and its maximum is its largest rank overall: the same descent from the root (node 0, the part's
+        // positions [0, d) or [d, n)). Levels no lane of the wave needs are skipped. (A per-d table of the parts'
+        // largest ranks answered the wrap case with one read but cost 4 B per event of the row image.)
+        hitA[u] = MK::any(belA[u]);
+        hitB[u] = MK::any(belB[u]);
+        wrapA[u] = d[u] > 0 && !hitA[u] && lA[u] == WT_NONE;
+        wrapB[u] = d[u] < n && !hitB[u] && lB[u] == WT_NONE;
+        if (wrapA[u]) {
+            lA[u] = 0;
+            qA[u] = d[u];
+        }
+        if (wrapB[u]) {
+            lB[u] = 0;
+            qB[u] = d[u];
+        }
+        const bool dA = d[u] > 0 && !hitA[u], dB = d[u] < n && !hitB[u];
         if (!dA) lA[u] = lb;
         if (!dB) lB[u] = lb;
         // the branch-off node: the left child recorded at level lA - 1 starts at R & ~(2^(K - lA + 1) - 1)
@@ -812,11 +854,11 @@ __device__ __forceinline__ void wt_seed_class(const WtVConst &vc, const WtClass 
     // entries from qB on (of the block's min(n - sB, 32))
 #pragma unroll
     for (int u = 0; u < NS; ++u) {
-        const uint32_t vA = WT_MK(sA[u] + (sA[u] >> 5) + qA[u]);
-        const uint32_t vB = ~WT_MK(sB[u] + (sB[u] >> 5) + qB[u]) & (0xffffffffu >> (32u - min(nv - sB[u], 32u)));
-        const uint32_t bA = RA[u] & ~31u, bB = RB[u] & ~31u;
-        const uint32_t pA = hitA[u] ? bA + 31u - __clz(belA[u]) : wrapA[u] ? (pmd[u] & 0xffffu) : sA[u] + 31u - __clz(vA);
-        const uint32_t pB = hitB[u] ? bB + 31u - __clz(belB[u]) : wrapB[u] ? (pmd[u] >> 16) : sB[u] + 31u - __clz(vB);
+        const MT vA = MK::load(mk, sA[u] + (sA[u] >> BB) + qA[u]);
+        const MT vB = MK::low(MK::inv(MK::load(mk, sB[u] + (sB[u] >> BB) + qB[u])), min(nv - sB[u], BW));
+        const uint32_t bA = RA[u] & ~BM, bB = RB[u] & ~BM;
+        const uint32_t pA = hitA[u] ? bA + MK::top(belA[u]) : sA[u] + MK::top(vA);
+        const uint32_t pB = hitB[u] ? bB + MK::top(belB[u]) : sB[u] + MK::top(vB);
         if (d[u] > 0) {
             const uint32_t t = Hm[u] + cm[pA] - (wrapA[u] ? m : 0u);
             const uint64_t k = ((uint64_t)t << 32) | (0xffffffffu - ev[pA]);
@@ -881,7 +923,7 @@ __device__ unsigned long long g_wt_trace[256][16][10];
 #else
 #define NMZ_WT_ATTR
 #endif
-template <bool BIG, int NS>
+template <bool BIG, int NS, int BB>
 __global__ __launch_bounds__(1024) NMZ_WT_ATTR void k_replayable_sweep_wt(
     const uint32_t *__restrict__ bucket_off, const uint64_t *__restrict__ sorted_h0,
     const uint32_t *__restrict__ sorted_idx, const uint4 *__restrict__ table, uint32_t E,
@@ -973,7 +1015,7 @@ __global__ __launch_bounds__(1024) NMZ_WT_ATTR void k_replayable_sweep_wt(
 #pragma unroll
         for (int u = 0; u < NS; ++u) sum[u] = key[u] = W[u] = 0;
         for (uint32_t c = 0; c < n_classes; ++c)
-            wt_seed_class<BIG, NS>(vc, classes[c], img, row, h0, m, mu, m_k64, msh, sum, W, key);
+            wt_seed_class<BIG, NS, BB>(vc, classes[c], img, row, h0, m, mu, m_k64, msh, sum, W, key);
         uint64_t km = 0;  // the chunk's largest sum, in the top-k's order (int64, as an order-preserving u64 key)
 #pragma unroll
         for (int u = 0; u < NS; ++u) {
@@ -1085,14 +1127,20 @@ __global__ __launch_bounds__(256) void k_wt_topk_scan(const uint64_t *__restrict
 #define NMZ_WT_SEL_THREADS 512
 #endif
 constexpr uint32_t WT_SEL_THREADS = NMZ_WT_SEL_THREADS;
+constexpr uint32_t WT_SEL_CHUNK = 2048, WT_SEL_KEEP = (WT_CAND / WT_SEL_CHUNK) * 64;
 __global__ __launch_bounds__(WT_SEL_THREADS) void k_wt_topk_select(const uint64_t *__restrict__ sums,
                                                                    const uint32_t *__restrict__ sorted_idx, uint64_t S,
                                                                    uint64_t seed0, uint32_t k,
                                                                    WtTopkState *__restrict__ tk,
                                                                    nmz_topk_entry *__restrict__ out) {
     constexpr uint32_t NT = WT_SEL_THREADS, NW = NT / 64;
-    __shared__ unsigned long long ck[WT_CAND];
-    __shared__ uint32_t ci[WT_CAND];
+    // candidates sorted in chunks of WT_SEL_CHUNK, each chunk's best k kept aside, then the kept ones sorted: 26 KB of
+    // LDS instead of 48 for one sort of WT_CAND, so the kernel fits beside a K1 workgroup whose row image has wider
+    // rank blocks (it waits for a whole CU otherwise: +8 us per configs[1] step)
+    __shared__ unsigned long long ck[WT_SEL_CHUNK];
+    __shared__ uint32_t ci[WT_SEL_CHUNK];
+    __shared__ unsigned long long sk[WT_SEL_KEEP];
+    __shared__ uint32_t si[WT_SEL_KEEP];
     __shared__ unsigned long long bk[NW], bs[NW];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t c = tk->n_cand;
@@ -1108,32 +1156,58 @@ __global__ __launch_bounds__(WT_SEL_THREADS) void k_wt_topk_select(const uint64_
         // every seed at or above the scan's tau is a candidate (hundreds to a few thousand: a row whose sums peak
         // high holds many near its peak): a bitonic sort of (key desc, seed asc) in LDS, padded with key 0 (a real
         // key has its top bit set: sums are non-negative)
-        uint32_t p2 = 1;
-        while (p2 < c) p2 <<= 1;
-        for (uint32_t i = threadIdx.x; i < p2; i += NT) {
-            ck[i] = i < c ? tk->cand_key[i] : 0ull;
-            ci[i] = i < c ? (uint32_t)tk->cand_idx[i] : ~0u;
-        }
-        for (uint32_t kk = 2; kk <= p2; kk <<= 1)
-            for (uint32_t j = kk >> 1; j; j >>= 1) {
-                __syncthreads();
-                for (uint32_t i = threadIdx.x; i < p2; i += NT) {
-                    const uint32_t l = i ^ j;
-                    if (l > i) {
-                        const unsigned long long a = ck[i], b = ck[l];
-                        const uint32_t ia = ci[i], ib = ci[l];
-                        // l better than i (key desc, seed asc; padding last)
-                        const bool lb = b > a || (b == a && b != 0 && seed0 + ib < seed0 + ia);
-                        if (lb == ((i & kk) == 0)) {
-                            ck[i] = b;
-                            ck[l] = a;
-                            ci[i] = ib;
-                            ci[l] = ia;
+        // bitonic sort of ck/ci[0, p2) (key desc, seed asc; padding last)
+        auto sort = [&](uint32_t p2) {
+            for (uint32_t kk = 2; kk <= p2; kk <<= 1)
+                for (uint32_t j = kk >> 1; j; j >>= 1) {
+                    __syncthreads();
+                    for (uint32_t i = threadIdx.x; i < p2; i += NT) {
+                        const uint32_t l = i ^ j;
+                        if (l > i) {
+                            const unsigned long long a = ck[i], b = ck[l];
+                            const uint32_t ia = ci[i], ib = ci[l];
+                            // l better than i
+                            const bool lb = b > a || (b == a && b != 0 && seed0 + ib < seed0 + ia);
+                            if (lb == ((i & kk) == 0)) {
+                                ck[i] = b;
+                                ck[l] = a;
+                                ci[i] = ib;
+                                ci[l] = ia;
+                            }
                         }
                     }
                 }
+            __syncthreads();
+        };
+        auto pow2 = [](uint32_t x) {
+            uint32_t p = 1;
+            while (p < x) p <<= 1;
+            return p;
+        };
+        const uint32_t nch = c > WT_SEL_CHUNK ? (c + WT_SEL_CHUNK - 1) / WT_SEL_CHUNK : 1;
+        for (uint32_t q = 0; q < nch; ++q) {
+            const uint32_t lo = q * WT_SEL_CHUNK, cc = min(c - lo, WT_SEL_CHUNK), p2 = pow2(cc);
+            for (uint32_t i = threadIdx.x; i < p2; i += NT) {
+                ck[i] = i < cc ? tk->cand_key[lo + i] : 0ull;
+                ci[i] = i < cc ? (uint32_t)tk->cand_idx[lo + i] : ~0u;
             }
-        __syncthreads();
+            sort(p2);
+            if (nch > 1) {  // the chunk's best k aside (a seed outside them is beaten by k of this chunk alone)
+                for (uint32_t i = threadIdx.x; i < k; i += NT) {
+                    sk[q * k + i] = ck[i];
+                    si[q * k + i] = ci[i];
+                }
+                __syncthreads();
+            }
+        }
+        if (nch > 1) {
+            const uint32_t p2 = pow2(nch * k);
+            for (uint32_t i = threadIdx.x; i < p2; i += NT) {
+                ck[i] = i < nch * k ? sk[i] : 0ull;
+                ci[i] = i < nch * k ? si[i] : ~0u;
+            }
+            sort(p2);
+        }
         for (uint32_t r = threadIdx.x; r < k; r += NT) {
             if (r < c) {
                 nmz_topk_entry e;
@@ -1251,6 +1325,13 @@ static uint32_t wt_threads() {
     return t;
 }
 
+// the widest rank blocks a plan may take: 64 ranks (NMZ_WT_BB = 5 | 6 | 7, A/B and tests; read at every plan build)
+static uint32_t wt_max_bb() {
+    const char *e = ab_env("NMZ_WT_BB");
+    const int v = e ? atoi(e) : 6;
+    return (uint32_t)((v >= 5 && v <= 7) ? v : 6);
+}
+
 constexpr size_t WT_BUILD_LDS = WT_NMAX * 8 * 2 + WT_NMAX / 2 * 4 + 2 * (WT_NMAX / 32 + 4) * 4 + 520 * 4 +
                                 WT_BW * 8 + 16;
 
@@ -1276,6 +1357,7 @@ bool wt_layout(WtState &w, nmz_ctx *ctx, uint32_t E, const ClassInfo *cls, uint3
         }
     }
     n_cls = (uint32_t)seg.size();
+    auto layout = [&](uint32_t bb) -> uint64_t {
     oc.assign(n_cls, WtClass{});
     uint64_t off = 0;
     for (uint32_t c = 0; c < n_cls; ++c) {
@@ -1287,7 +1369,7 @@ bool wt_layout(WtState &w, nmz_ctx *ctx, uint32_t E, const ClassInfo *cls, uint3
         o.K = bitlen(o.n);  // 2^K > n >= every bound R
         o.nw = o.n / 32 + 1;
         o.o_lv = (uint32_t)off;
-        off += r16((uint64_t)wt_levels(o.K) * o.nw * 8);
+        off += r16((uint64_t)wt_levels(o.K, bb) * o.nw * 8);
         o.o_cm = (uint32_t)off;
         off += r16((uint64_t)(o.n + WT_PAD) * 4);
         o.o_chi = (uint32_t)off;
@@ -1298,13 +1380,15 @@ bool wt_layout(WtState &w, nmz_ctx *ctx, uint32_t E, const ClassInfo *cls, uint3
         off += r16(257 * 2);
         o.o_ic = (uint32_t)off;
         off += r16(256 * 2);
-        o.o_pm = (uint32_t)off;
-#ifndef WT_ABL_PM
-        off += r16((uint64_t)(o.n + 1) * 4);
-#endif
         o.o_mk = (uint32_t)off;
-        off += r16((uint64_t)(o.n / 32 + 1) * 33 * 4);
+        off += r16(wt_mask_bytes(o.n, bb));
     }
+    return off;
+    };
+    // the widest rank blocks whose row image fits LDS (NMZ_WT_BB caps the width, A/B and tests)
+    uint32_t bb = wt_max_bb();
+    uint64_t off = layout(bb);
+    while (bb > 5 && std::max<uint64_t>(16, r16(off)) + 16 > WT_LDS_MAX) off = layout(--bb);
     {  // the plan kernel's dispatch order: segments by size, largest first
         std::vector<uint32_t> ord(n_cls);
         std::iota(ord.begin(), ord.end(), 0u);
@@ -1315,10 +1399,18 @@ bool wt_layout(WtState &w, nmz_ctx *ctx, uint32_t E, const ClassInfo *cls, uint3
     if (rb + 16 > WT_LDS_MAX) return false;
     // function attributes are per device: once per context (a context owns one device; its calls are serialised)
     if (!ctx->wt_lds_attr) {
-        for (const void *f : {reinterpret_cast<const void *>(k_replayable_sweep_wt<false, 1>),
-                              reinterpret_cast<const void *>(k_replayable_sweep_wt<true, 1>),
-                              reinterpret_cast<const void *>(k_replayable_wt_build<false>),
-                              reinterpret_cast<const void *>(k_replayable_wt_build<true>)})
+        for (const void *f : {reinterpret_cast<const void *>(k_replayable_sweep_wt<false, 1, 5>),
+                              reinterpret_cast<const void *>(k_replayable_sweep_wt<true, 1, 5>),
+                              reinterpret_cast<const void *>(k_replayable_sweep_wt<false, 1, 6>),
+                              reinterpret_cast<const void *>(k_replayable_sweep_wt<true, 1, 6>),
+                              reinterpret_cast<const void *>(k_replayable_sweep_wt<false, 1, 7>),
+                              reinterpret_cast<const void *>(k_replayable_sweep_wt<true, 1, 7>),
+                              reinterpret_cast<const void *>(k_replayable_wt_build<false, 5>),
+                              reinterpret_cast<const void *>(k_replayable_wt_build<true, 5>),
+                              reinterpret_cast<const void *>(k_replayable_wt_build<false, 6>),
+                              reinterpret_cast<const void *>(k_replayable_wt_build<true, 6>),
+                              reinterpret_cast<const void *>(k_replayable_wt_build<false, 7>),
+                              reinterpret_cast<const void *>(k_replayable_wt_build<true, 7>)})
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WT_LDS_MAX) != hipSuccess) {
                 (void)hipGetLastError();  // not sticky for the launches that follow: keep the order-query sweep
                 return false;
@@ -1326,6 +1418,7 @@ bool wt_layout(WtState &w, nmz_ctx *ctx, uint32_t E, const ClassInfo *cls, uint3
         ctx->wt_lds_attr = true;
     }
     w.rb16 = (uint32_t)(rb / 16);
+    w.bb = bb;
     w.n_classes = n_cls;
     w.msh = mod.m32 > 255 ? bitlen(mod.m32) - 8 : 0;
     return true;
@@ -1341,12 +1434,12 @@ int wt_launch(WtState &w, const uint4 *d_table, uint32_t E, const ModParams &mod
     if (hints)
         hz = WtHints{hints->hoff, hints->hbytes, hints->perm, mod.m, mod.mu, hints->table, hints->zero0, hints->n_zero0,
                      hints->zero1, hints->n_zero1};
-    if (hints)
-        hipLaunchKernelGGL(k_replayable_wt_build<true>, dim3(w.n_classes, 256), dim3(WT_BT), WT_BUILD_LDS, st, nullptr,
-                           E, d_cls, w.msh, bitlen(mod.m32), w.d_blob, w.rb16, d_rowsum, hz);
-    else
-        hipLaunchKernelGGL(k_replayable_wt_build<false>, dim3(w.n_classes, 256), dim3(WT_BT), WT_BUILD_LDS, st,
-                           d_table, E, d_cls, w.msh, bitlen(mod.m32), w.d_blob, w.rb16, d_rowsum, hz);
+    auto kern = hints ? (w.bb == 7 ? k_replayable_wt_build<true, 7>
+                         : w.bb == 6 ? k_replayable_wt_build<true, 6> : k_replayable_wt_build<true, 5>)
+                      : (w.bb == 7 ? k_replayable_wt_build<false, 7>
+                         : w.bb == 6 ? k_replayable_wt_build<false, 6> : k_replayable_wt_build<false, 5>);
+    hipLaunchKernelGGL(kern, dim3(w.n_classes, 256), dim3(WT_BT), WT_BUILD_LDS, st, hints ? nullptr : d_table, E,
+                       d_cls, w.msh, bitlen(mod.m32), w.d_blob, w.rb16, d_rowsum, hz);
     NMZ_HIP(hipGetLastError());
     if (sync) NMZ_HIP(hipStreamSynchronize(st));  // the plan is complete when it is returned
     w.on = true;
@@ -1406,7 +1499,10 @@ int wt_sweep(const WtState &w, nmz_ctx *ctx, hipStream_t st, const Buckets &b, c
     const bool big = mod.m32 >= 0x80000000u;
     // one seed per lane: two (NS = 2, 106 VGPRs) measured slower, K1 span 0.074 vs 0.059 ms
     // (profiles/r04/k1_ns2_rejected/)
-    auto kern = big ? k_replayable_sweep_wt<true, 1> : k_replayable_sweep_wt<false, 1>;
+    auto kern = big ? (w.bb == 7 ? k_replayable_sweep_wt<true, 1, 7>
+                       : w.bb == 6 ? k_replayable_sweep_wt<true, 1, 6> : k_replayable_sweep_wt<true, 1, 5>)
+                    : (w.bb == 7 ? k_replayable_sweep_wt<false, 1, 7>
+                       : w.bb == 6 ? k_replayable_sweep_wt<false, 1, 6> : k_replayable_sweep_wt<false, 1, 5>);
     const size_t lds = w.rb16 * 16u + 16u;
     hipLaunchKernelGGL(kern, dim3(256 * G), dim3(nt), lds, st, b.offset, b.sorted_h0, b.sorted_idx,
                        d_table, E, w.d_blob, w.rb16, w.d_rowsum, static_cast<const WtClass *>(w.d_classes),

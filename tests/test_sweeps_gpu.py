@@ -26,13 +26,18 @@ def rep_oracle(seeds, hints, m, n_dump=0):
 
 
 # ---------------------------------------------------------------- K1
-@pytest.fixture(params=["wt", "wt_sep", "oq"])
+@pytest.fixture(params=["wt", "wt_sep", "wt_bb7", "wt_bb5", "oq"])
 def k1(request, monkeypatch):
     """K1's two statistics kernels: wavelet trees (the default) and order queries (NMZ_REPLAY_WT=0 at plan
     creation); plans that neither fits take the per-decision sweep either way. "wt" builds the wavelet-tree plan
     with the fused plan kernel (it computes and C-sorts the correction table itself), "wt_sep" with the separate
-    table, sort and plan kernels (NMZ_WT_FUSED=0, the path for classes of 4,096 events or more)."""
+    table, sort and plan kernels (NMZ_WT_FUSED=0, the path for classes of 4,096 events or more). The wavelet plans
+    take the widest rank blocks (at most 64 ranks) whose row image fits LDS; "wt_bb7" / "wt_bb5" set the cap to 128 /
+    32 ranks (NMZ_WT_BB: 32 is the width of larger rows)."""
     monkeypatch.delenv("NMZ_WT_FUSED", raising=False)
+    monkeypatch.delenv("NMZ_WT_BB", raising=False)
+    if request.param in ("wt_bb7", "wt_bb5"):
+        monkeypatch.setenv("NMZ_WT_BB", request.param[-1])
     if request.param == "oq":
         monkeypatch.setenv("NMZ_REPLAY_WT", "0")
     else:
@@ -522,6 +527,8 @@ def test_replayable_plan_create_async(ctx):
     (100_000_000, 9000, 120, 64, 2**64 - 4000),  # candidates above the k-th workgroup maximum; seeds wrap
     (7, 6000, 100, 33, 3),                    # sums 0..600: heavy ties, candidates overflow -> gated selection
     (1, 5000, 40, 16, 11),                    # maxInterval 1: every sum 0, every seed a candidate -> gated
+    (1, 3000, 40, 64, 2**64 - 1500),          # 3,000 tied candidates: two sorted chunks, then their best 64 each
+    (1, 4096, 30, 5, 9),                      # exactly WT_CAND candidates: the last chunk full
     (2**31 + 3, 4000, 60, 1, 0),              # k = 1, m >= 2^31
 ])
 def test_replayable_sweep_topk_dev_matches_separate_selection(ctx, m, S, E, k, seed0):

@@ -11,8 +11,8 @@ def bitlen(x):
     return x.bit_length()
 
 
-def build(cm, e, chi):
-    """cm, e, chi per position (C order). Returns the image as Python lists."""
+def build(cm, e, chi, bb=5):
+    """cm, e, chi per position (C order); rank blocks of 2^bb ranks. Returns the image as Python lists."""
     n = len(cm)
     keys = sorted(((cm[i] << 32) | ((0xFFFF - e[i]) << 16) | i) for i in range(n))
     cm_r = [k >> 32 for k in keys] + [0xFFFFFFFF]
@@ -21,7 +21,7 @@ def build(cm, e, chi):
     for j, k in enumerate(keys):
         S[k & 0xFFFF] = j
     K = bitlen(n)
-    lb = K - 5 if K > 5 else 0  # levels above the 32-rank blocks
+    lb = K - bb if K > bb else 0  # levels above the 2^bb-rank blocks
     nw = n // 32 + 1
     lv = []
     cur = S
@@ -46,23 +46,23 @@ def build(cm, e, chi):
             nxt[(s0 + h + r1) if (v & h) else (j - r1)] = v
         assert None not in nxt
         cur = nxt
-    # level lb: the node of a 32-rank block b holds ranks [32b, 32b + 32) in position order; mk[b][o] = the set of
-    # those ranks (bit r & 31) among the node's first o entries
-    nb = n // 32 + 1
+    # level lb: the node of a block b holds ranks [BW b, BW b + BW) in position order; mk[b][o] = the set of
+    # those ranks (bit r mod BW) among the node's first o entries
+    BW = 1 << bb
+    nb = (n >> bb) + 1
     mk = []
     for b in range(nb):
         row = [0]
         acc = 0
-        for j in range(32):
-            p = 32 * b + j
+        for j in range(BW):
+            p = BW * b + j
             if p < n:
-                assert cur[p] >> 5 == b
-                acc |= 1 << (cur[p] & 31)
+                assert cur[p] >> bb == b
+                acc |= 1 << (cur[p] & (BW - 1))
             row.append(acc)
         mk.append(row)
-    pm_lo = [max(S[:dd]) if dd else 0 for dd in range(n + 1)]
-    pm_hi = [max(S[dd:]) if dd < n else 0 for dd in range(n + 1)]
-    return dict(pm_lo=pm_lo, pm_hi=pm_hi, n=n, K=K, lb=lb, nw=nw, lv=lv, mk=mk, cm=cm_r, e=e_r, chi=list(chi) + [0xFFFFFFFF])
+    return dict(n=n, K=K, lb=lb, nw=nw, lv=lv, mk=mk, cm=cm_r, e=e_r, chi=list(chi) + [0xFFFFFFFF],
+                bb=bb)
 
 
 def ones(lvl, s, p):
@@ -103,11 +103,13 @@ def query(img, d, RA, RB, Hm, Hm2, m):
         else:
             cB += o
             oB = z
-    # the 32-rank block of R: its first o entries are the node's prefix elements
-    F = 0xFFFFFFFF
-    mA = mk[RA >> 5][oA]
-    mB = mk[RB >> 5][oB]
-    rA, rB = RA & 31, RB & 31
+    # the rank block of R: its first o entries are the node's prefix elements
+    bb = img["bb"]
+    BW = 1 << bb
+    F = (1 << BW) - 1
+    mA = mk[RA >> bb][oA]
+    mB = mk[RB >> bb][oB]
+    rA, rB = RA & (BW - 1), RB & (BW - 1)
     cA += bin(mA >> rA).count("1")
     cB += bin(mB >> rB).count("1")
     W = cA + (n - RB) - cB
@@ -115,10 +117,15 @@ def query(img, d, RA, RB, Hm, Hm2, m):
     belB = (~mB & F) & ((1 << rB) - 1)
     hasA, hasB = d > 0, d < n
     hitA, hitB = belA != 0, belB != 0
-    wrapA = not hitA and lA is NONE
-    wrapB = not hitB and lB is NONE
-    dA = hasA and not hitA and not wrapA  # descend from the tracked level
-    dB = hasB and not hitB and not wrapB
+    wrapA = hasA and not hitA and lA is NONE
+    wrapB = hasB and not hitB and lB is NONE
+    # a part with nothing below its bound: its largest rank overall, by the same descent from the root
+    if wrapA:
+        lA, sA, qA = 0, 0, d
+    if wrapB:
+        lB, sB, qB = 0, 0, d
+    dA = hasA and not hitA  # descend from the tracked level
+    dB = hasB and not hitB
     lA = lA if dA else lb
     lB = lB if dB else lb
     # the kernel does not track the node start: it rebuilds it from the level (R & ~(2^(K - l + 1) - 1))
@@ -146,21 +153,22 @@ def query(img, d, RA, RB, Hm, Hm2, m):
                 qB -= o
     def top(x):
         return x.bit_length() - 1
-    if hitA:
-        pA = (RA & ~31) + top(belA)
-    elif wrapA:
-        pA = img["pm_lo"][d]
+    pA = pB = None
+    if not hasA:
+        pass
+    elif hitA:
+        pA = (RA & ~(BW - 1)) + top(belA)
     else:
-        v = mk[sA >> 5][qA]
+        v = mk[sA >> bb][qA]
         assert v
         pA = sA + top(v)
-    if hitB:
-        pB = (RB & ~31) + top(belB)
-    elif wrapB:
-        pB = img["pm_hi"][d]
+    if not hasB:
+        pass
+    elif hitB:
+        pB = (RB & ~(BW - 1)) + top(belB)
     else:
-        size = min(n - sB, 32)
-        v = (~mk[sB >> 5][qB] & F) & (F >> (32 - size))
+        size = min(n - sB, BW)
+        v = (~mk[sB >> bb][qB] & F) & (F >> (BW - size))
         assert v
         pB = sB + top(v)
     kA = kB = None
@@ -191,13 +199,14 @@ def main():
     trials = int(sys.argv[1]) if len(sys.argv) > 1 else 300
     rng = random.Random(7)
     for t in range(trials):
-        n = rng.choice([9, 10, 15, 16, 31, 32, 33, 63, 64, 65, 96, 100, 127, 128, 129, 200, 255, 256, 257, 511, 512, 700, 1024, 2079])
+        n = rng.choice([9, 10, 15, 16, 31, 32, 33, 63, 64, 65, 96, 100, 127, 128, 129, 200, 255, 256, 257, 511, 512, 700,
+                        1024, 2079])
         m = rng.choice([1, 2, 3, 7, 100, 1000, 10 ** 8, (1 << 30) - 1, (1 << 31) + 5, (1 << 32) - 1])
         dup = rng.random() < 0.3
         vals = [rng.randrange(m) for _ in range(max(1, n // 8 if dup else n))]
         cm = [rng.choice(vals) for _ in range(n)]
         e = rng.sample(range(4096), n)
-        img = build(cm, e, [0] * n)
+        img = build(cm, e, [0] * n, bb=rng.choice([5, 6, 7]))
         for _ in range(30):
             d = rng.choice([0, n, rng.randrange(n + 1)])
             Hm = rng.randrange(m)
