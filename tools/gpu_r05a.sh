@@ -12,7 +12,7 @@ if [ "$2" != "skip-tests" ]; then
   [ $rc -eq 0 ] || exit $rc
   timeout -k 10 150 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit $?
 fi
-timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 --full-record $O/bench_full.json > $O/bench.out 2> $O/bench.err || exit $?
+timeout -k 10 400 python bench.py --full-record $O/bench_full.json > $O/bench.out 2> $O/bench.err || exit $?
 tail -c 600 $O/bench.out
 cd /tmp && export TMPDIR=/tmp
 B="python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-secondary --full-record $O/bench_prof_full.json"
