@@ -200,6 +200,7 @@ def _to_single(t):
     (150, 16, 50, 300, 400, 0.05),     # several 64-element steps, actions without events
     (120, 200, 100, 400, 5000, 0.0),   # > 64 distinct entities per step
     (40, 5000, 1, 6000, 20000, 0.0),   # > 4096 entities: one wave per workgroup
+    (6, 1, 66000, 70000, 50, 0.0),     # ranks past the 65,536-entry key table (inline keys)
 ])
 def test_unique_curves_vs_oracle(ctx, n, n_ent, lmin, lmax, n_events, p_none):
     rng = np.random.default_rng(n + n_ent)
@@ -209,7 +210,8 @@ def test_unique_curves_vs_oracle(ctx, n, n_ent, lmin, lmax, n_events, p_none):
     exact = hs.unique_trace_curve(traces, po_reduction=False, ctx=ctx)
     assert po == O.unique_curve_po(raw)
     assert exact == O.unique_curve_exact([[s for _, s in t] for t in raw])
-    assert po[-1] < exact[-1]  # the shuffled repeats are PO-equal only
+    if n_ent > 1:
+        assert po[-1] < exact[-1]  # the shuffled repeats are PO-equal only
 
 
 @pytest.mark.gpu
