@@ -69,15 +69,10 @@ __global__ void k_rank_keys(ulonglong2 *__restrict__ keys) {
 }
 
 // the pair (symbol s, rank r) -> two 64-bit summands: t = fmix64(s ^ ka(r)) and a second, different nonlinear
-// function of t and kb(r) (one more 64-bit multiply instead of another fmix64). SMALL: every rank of the step is
-// below RANK_KEYS (the step's first element index + 64 <= RANK_KEYS, a wave-uniform test: a rank never exceeds its
-// element's index), so the inline keys -- two more fmix64, 12 of the 21 multiplies per element, computed and
-// discarded by a select before -- are not in the code path
-template <bool SMALL>
+// function of t and kb(r) (one more 64-bit multiply instead of another fmix64)
 __device__ __forceinline__ void mix2(uint64_t s, uint32_t r, const ulonglong2 *__restrict__ keys, uint64_t &a,
                                      uint64_t &b) {
-    const ulonglong2 k =
-        (SMALL || r < RANK_KEYS) ? keys[r] : make_ulonglong2(rank_key_a(r), rank_key_b(r));
+    const ulonglong2 k = r < RANK_KEYS ? keys[r] : make_ulonglong2(rank_key_a(r), rank_key_b(r));
     const uint64_t t = fmix64(s ^ k.x);
     a = t;
     const uint64_t u = (t ^ k.y) * 0x94d049bb133111ebULL;
@@ -149,8 +144,7 @@ __global__ __launch_bounds__(256) void k_trace_sig(const uint64_t *__restrict__ 
         }
         if (take) {
             uint64_t a, b;
-            if (c + 64 <= RANK_KEYS) mix2<true>(s, rank, keys, a, b);
-            else mix2<false>(s, rank, keys, a, b);
+            mix2(s, rank, keys, a, b);
             acc1 += a;
             acc2 += b;
             counted += 1;
