@@ -41,6 +41,7 @@ namespace nmz {
 constexpr uint32_t SIG_WAVES = 4;             // waves (traces) per workgroup
 constexpr uint32_t SIG_MAX_ENT_LDS = 4096;    // entity counters per wave at 4 waves per workgroup (64 KiB)
 constexpr uint32_t SIG_MAX_ENT = 16384;       // one wave per workgroup beyond that
+constexpr uint32_t SIG_MASK_ENT = 1024;       // entity masks (k_trace_sig MODE 2) up to this many entities: 48 KiB
 #ifndef NMZ_SIG_U
 #define NMZ_SIG_U 4
 #endif
@@ -79,19 +80,30 @@ __device__ __forceinline__ void mix2(uint64_t s, uint32_t r, const ulonglong2 *_
     b = u ^ (u >> 29);
 }
 
-template <bool PO>
+// MODE 0: exact (rank = position); 1: PO, a lane's entity group from kbits ballots (one per bit of the id);
+// 2: PO, the group from a per-wave LDS mask per entity (every lane ORs its bit into its entity's mask and reads it
+// back: 2 LDS instructions instead of ~7 VALU per id bit; for traces of at most SIG_MASK_ENT entities)
+template <int MODE>
 __global__ __launch_bounds__(256) void k_trace_sig(const uint64_t *__restrict__ off, const uint64_t *__restrict__ sym,
                                                    const uint32_t *__restrict__ ent, uint32_t N, uint32_t max_ent,
                                                    uint32_t kbits, uint32_t waves_per_block,
                                                    const ulonglong2 *__restrict__ keys, uint64_t *__restrict__ sig) {
-    extern __shared__ uint32_t cnt_all[];
+    constexpr bool PO = MODE != 0;
+    extern __shared__ uint64_t sig_lds[];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t t = blockIdx.x * waves_per_block + wv;
     if (wv >= waves_per_block || t >= N) return;  // whole waves only: no block-wide barrier below
-    // the wave's own counters (LDS ops of one wave execute in order; compiler barriers keep the order in the code)
-    uint32_t *cnt = cnt_all + (size_t)wv * max_ent;
+    // the wave's own counters (and entity masks, MODE 2) (LDS ops of one wave execute in order; compiler barriers
+    // keep the order in the code)
+    // MODE 2: every wave's [max_ent] u64 masks, then every wave's counters
+    uint64_t *msk = sig_lds + (size_t)wv * max_ent;
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(MODE == 2 ? sig_lds + (size_t)waves_per_block * max_ent : sig_lds) +
+                    (size_t)wv * max_ent;
     if (PO)
-        for (uint32_t i = lane; i < max_ent; i += 64) cnt[i] = 0;
+        for (uint32_t i = lane; i < max_ent; i += 64) {
+            cnt[i] = 0;
+            if (MODE == 2) msk[i] = 0;
+        }
     __asm__ volatile("" ::: "memory");
     const uint64_t base = off[t], n = off[t + 1] - base;
     uint64_t acc1 = 0, acc2 = 0;
@@ -123,6 +135,23 @@ __global__ __launch_bounds__(256) void k_trace_sig(const uint64_t *__restrict__ 
             const uint32_t e0 = valid ? ev[k] : NMZ_NONE;
             take = valid && e0 < max_ent;  // NMZ_NONE (no event) skipped; ids past the bound never index LDS
             const uint32_t e = take ? e0 : 0u;
+            if constexpr (MODE == 2) {
+                // lanes holding the same entity: each ORs its bit into the entity's mask, then reads it back
+                if (take) atomicOr(reinterpret_cast<unsigned long long *>(msk + e), 1ull << lane);
+                __asm__ volatile("" ::: "memory");
+                if (take) {
+                    const uint64_t same = msk[e];
+                    const uint32_t before = cnt[e];
+                    rank = before + (uint32_t)__popcll(same & below);
+                    // every lane of the wave has read (one LDS instruction each) before the group's last lane
+                    // stores the count and clears the mask for the next step
+                    __asm__ volatile("" ::: "memory");
+                    if ((same >> lane) == 1ull) {
+                        cnt[e] = before + (uint32_t)__popcll(same);
+                        msk[e] = 0;
+                    }
+                }
+            } else {
             // lanes holding the same entity: intersect, bit by bit of the id, the ballot of lanes that agree
             // on that bit (kbits ballots per 64 elements instead of one per distinct entity)
             // (as the lanes that differ from this one in some bit: one XOR-OR per ballot, no per-lane select)
@@ -140,6 +169,7 @@ __global__ __launch_bounds__(256) void k_trace_sig(const uint64_t *__restrict__ 
                 // every lane of the wave has read (one LDS instruction) before the group's last lane stores
                 __asm__ volatile("" ::: "memory");
                 if ((same >> lane) == 1ull) cnt[e] = before + (uint32_t)__popcll(same);
+            }
             }
         }
         if (take) {
@@ -211,7 +241,7 @@ static int sig_launch(nmz_ctx *ctx, const uint64_t *d_off, const uint64_t *d_sym
     }
     const ulonglong2 *keys = kb.as<ulonglong2>();
     if (!d_ent) {
-        hipLaunchKernelGGL(k_trace_sig<false>, dim3(ceil_div(N, SIG_WAVES)), dim3(64 * SIG_WAVES), 0, st, d_off, d_sym,
+        hipLaunchKernelGGL(k_trace_sig<0>, dim3(ceil_div(N, SIG_WAVES)), dim3(64 * SIG_WAVES), 0, st, d_off, d_sym,
                            nullptr, N, 0u, 0u, SIG_WAVES, keys, d_sig);
     } else {
         NMZ_CHECK(max_ent <= SIG_MAX_ENT, "more than 16384 distinct entities in one trace");
@@ -219,8 +249,14 @@ static int sig_launch(nmz_ctx *ctx, const uint64_t *d_off, const uint64_t *d_sym
         const uint32_t wpb = me <= SIG_MAX_ENT_LDS ? SIG_WAVES : 1;
         uint32_t kbits = 0;
         while ((1u << kbits) < me) ++kbits;
-        hipLaunchKernelGGL(k_trace_sig<true>, dim3(ceil_div(N, wpb)), dim3(64 * wpb), (size_t)wpb * me * 4, st, d_off,
-                           d_sym, d_ent, N, me, kbits, wpb, keys, d_sig);
+        const char *ab = ab_env("NMZ_SIG_MASKS");  // (A/B: NMZ_SIG_MASKS=0 takes the ballots)
+        if (me <= SIG_MASK_ENT && !(ab && ab[0] == '0'))
+            hipLaunchKernelGGL(k_trace_sig<2>, dim3(ceil_div(N, SIG_WAVES)), dim3(64 * SIG_WAVES),
+                               (size_t)SIG_WAVES * me * 12, st, d_off, d_sym, d_ent, N, me, kbits, SIG_WAVES, keys,
+                               d_sig);
+        else
+            hipLaunchKernelGGL(k_trace_sig<1>, dim3(ceil_div(N, wpb)), dim3(64 * wpb), (size_t)wpb * me * 4, st, d_off,
+                               d_sym, d_ent, N, me, kbits, wpb, keys, d_sig);
     }
     NMZ_HIP(hipGetLastError());
     return NMZ_OK;

@@ -198,7 +198,8 @@ def _to_single(t):
 @pytest.mark.parametrize("n,n_ent,lmin,lmax,n_events,p_none", [
     (200, 4, 0, 30, 40, 0.0),          # short traces, empty ones
     (150, 16, 50, 300, 400, 0.05),     # several 64-element steps, actions without events
-    (120, 200, 100, 400, 5000, 0.0),   # > 64 distinct entities per step
+    (120, 200, 100, 400, 5000, 0.0),   # > 64 distinct entities per step (entity masks in LDS)
+    (60, 2000, 1, 3000, 8000, 0.0),    # > 1,024 entities: the per-bit ballots, four waves per workgroup
     (40, 5000, 1, 6000, 20000, 0.0),   # > 4096 entities: one wave per workgroup
     (6, 1, 66000, 70000, 50, 0.0),     # ranks past the 65,536-entry key table (inline keys)
 ])

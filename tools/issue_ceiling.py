@@ -52,8 +52,8 @@ KERNELS = {
     "k_ed_qg_filter:survey": "_ZN3nmz14k_ed_qg_filterILb1E",
     "k_ed_qg_filter:clustered": "_ZN3nmz14k_ed_qg_filterILb1E",
     # visualize: one wave per trace, 64 elements per step (PO: entity ballots + LDS rank counters + the mix)
-    "k_trace_sig:po": "_ZN3nmz11k_trace_sigILb1E",
-    "k_trace_sig:exact": "_ZN3nmz11k_trace_sigILb0E",
+    "k_trace_sig:po": "_ZN3nmz11k_trace_sigILi2E",
+    "k_trace_sig:exact": "_ZN3nmz11k_trace_sigILi0E",
 }
 
 # cycles per wave64 instruction per SIMD at 8 waves/SIMD, tools/ubench/bv_rates.hip (profiles/r03ub_issue_rates.log)

@@ -35,8 +35,8 @@ LEGS = {
     "ed_wide": [("void nmz::k_ed_wide<4>", "k_ed_wide", "pair", 256 * 255 // 2)],
     # one launch per mode per step (PO first, then exact): the profile's average mixes both modes, so the
     # per-mode figures come from the two kernel instantiations
-    "visualize": [("void nmz::k_trace_sig<true>", "k_trace_sig:po", "trace", 100_000),
-                  ("void nmz::k_trace_sig<false>", "k_trace_sig:exact", "trace", 100_000)],
+    "visualize": [("void nmz::k_trace_sig<2>", "k_trace_sig:po", "trace", 100_000),
+                  ("void nmz::k_trace_sig<0>", "k_trace_sig:exact", "trace", 100_000)],
 }
 
 
