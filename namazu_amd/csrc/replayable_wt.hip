@@ -1080,19 +1080,20 @@ __global__ __launch_bounds__(256) void k_wt_topk_scan(const uint64_t *__restrict
         v[r] = i < S ? sums[i] : 0ull;
     }
     for (uint32_t i = threadIdx.x; i < m; i += 256) g[i] = tk->gmax[(uint64_t)i * n / m];
-    if (threadIdx.x == 0) tau_s = 0;  // fewer groups than k: every seed is a candidate
+    // fewer groups than k: every seed is a candidate (tau 0); else the k-th largest sampled maximum = the smallest
+    // of those with fewer than k others above them (one count per value, no tie count)
+    if (threadIdx.x == 0) tau_s = m >= k ? ~0ull : 0ull;
     __syncthreads();
     if (m >= k) {
+        unsigned long long best = ~0ull;
         for (uint32_t i = threadIdx.x; i < m; i += 256) {
             const unsigned long long x = g[i];
-            uint32_t gt = 0, eq = 0;
+            uint32_t gt = 0;
 #pragma unroll 8
-            for (uint32_t j = 0; j < m; ++j) {
-                gt += g[j] > x;
-                eq += g[j] == x;
-            }
-            if (gt < k && k <= gt + eq) tau_s = x;  // every writer writes the same value
+            for (uint32_t j = 0; j < m; ++j) gt += g[j] > x;
+            if (gt < k) best = x < best ? x : best;
         }
+        if (best != ~0ull) atomicMin(&tau_s, best);
     }
     __syncthreads();
     const unsigned long long t = tau_s;
@@ -1474,6 +1475,8 @@ int wt_topk(hipStream_t st, void *scratch, const uint32_t *sorted_idx, uint64_t 
     Carve cv(scratch);
     WtTopkState *tk = cv.take<WtTopkState>(1);
     const uint64_t *sums = cv.take<uint64_t>(S);
+    // (64 blocks, for less of the per-block tau derivation, made the configs[1] step slower: 0.072 -> 0.077 ms, the
+    // longer scan delaying its stream's next step)
     const unsigned blocks = (unsigned)std::min<uint64_t>(ceil_div(S, 256), 256);
     hipLaunchKernelGGL(k_wt_topk_scan, dim3(blocks), dim3(256), 0, st, sums, sorted_idx, S, 256 * wt_groups(), k, tk);
     hipLaunchKernelGGL(k_wt_topk_select, dim3(1), dim3(WT_SEL_THREADS), 0, st, sums, sorted_idx, S, seed0, k, tk,
