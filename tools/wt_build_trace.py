@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from namazu_amd import _lib  # noqa: E402
 from namazu_amd.explorepolicy import to_csr  # noqa: E402
 
-PHASES = ["entries (fused: FNV + C sort) + row sum", "keys", "Cm sort", "rank arrays", "bucket indexes", "pm scans", "levels",
+PHASES = ["entries (fused: FNV + C sort) + row sum", "keys", "Cm sort", "rank arrays", "bucket indexes", "(empty: the per-d maxima, removed in round 5)", "levels",
           "block masks"]  # between the kernel's stamps 0..8
 NP = 10
 TICK_US = 0.01  # wall_clock64 at 100 MHz
