@@ -31,7 +31,12 @@
 
 namespace nmz {
 
-constexpr uint32_t WT_BRUTE = 8;       // segments of at most this many events: per-event decisions
+#ifndef NMZ_WT_BRUTE
+#define NMZ_WT_BRUTE 8
+#endif
+// segments of at most this many events: per-event decisions (32, for configs[1]'s 25-event segment: K1 0.062 ->
+// 0.0675 ms, profiles/r05/k1/brute_ab)
+constexpr uint32_t WT_BRUTE = NMZ_WT_BRUTE;
 constexpr uint32_t WT_NMAX = 4096;     // largest segment the plan kernel sorts in LDS
 constexpr uint32_t WT_LDS_MAX = 160 * 1024 - 256;  // dynamic LDS; the sweep kernel's few static bytes need the rest
 constexpr uint32_t WT_NONE = 0xffffffffu;
