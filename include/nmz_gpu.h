@@ -379,6 +379,12 @@ int nmz_ed_plan_query_knn(nmz_ed_plan *plan, const uint64_t *q_off, const uint64
  * reference interface. */
 #define NMZ_ED_NCOUNTERS 6
 int nmz_ed_plan_counters(nmz_ed_plan *plan, uint64_t *out, void *stream);
+/* Test hook, not part of the reference interface: the two-phase search's offset kernels (k_tp_reduce, k_tp_scan)
+ * on caller data. d_cnt[n] (device) -> d_poff[n + 1] = exclusive prefix sums of the counts mod 2^32,
+ * d_ioff[n + 1] = exclusive prefix sums of ceil(count / item) mod 2^32, *d_tot = the 64-bit count total;
+ * item a power of two. Enqueued on `stream` (NULL = the context's stream), synchronised before it returns. */
+int nmz_debug_tp_offsets(nmz_ctx *ctx, const uint32_t *d_cnt, uint32_t n, uint32_t item, uint32_t *d_poff,
+                         uint32_t *d_ioff, uint64_t *d_tot, void *stream);
 
 /* ---- trace equality classes (nmz tools visualize) ------------------------
  * Replaces the O(n^2) loops of cli/tools/visualize.go:51-172 (gnuplot): trace i is a

@@ -100,6 +100,7 @@ SIGNATURES = {
     "nmz_knn_merge_dev": (_int, [_P, _P, _u32, _u32, _u32, _P, _P]),
     "nmz_ed_knn_fill_dev": (_int, [_P, _u32, _P, _P]),
     "nmz_ed_plan_counters": (_int, [_P, _P, _P]),
+    "nmz_debug_tp_offsets": (_int, [_P, _P, _u32, _u32, _P, _P, _P, _P]),
     "nmz_ed_plan_query_knn": (_int, [_P, _P, _P, _u32, _u32, _P, _P]),
     "nmz_trace_signatures": (_int, [_P, _P, _P, _P, _u32, _P]),
     "nmz_unique_traces": (_int, [_P, _P, _P, _P, _u32, _P]),

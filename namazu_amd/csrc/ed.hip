@@ -1650,6 +1650,33 @@ int nmz_ed_plan_is_fast(const nmz_ed_plan *plan) {
     return plan->wide ? 3 : (plan->bv ? 2 : (plan->fast ? 1 : 0));
 }
 
+int nmz_debug_tp_offsets(nmz_ctx *ctx, const uint32_t *d_cnt, uint32_t n, uint32_t item, uint32_t *d_poff,
+                         uint32_t *d_ioff, uint64_t *d_tot, void *stream) {
+    NMZ_CHECK(ctx != nullptr && d_cnt != nullptr && d_poff != nullptr && d_ioff != nullptr && d_tot != nullptr,
+              "NULL argument");
+    NMZ_CHECK(n > 0 && n < (1u << 30), "n out of range");
+    NMZ_CHECK(item > 0 && (item & (item - 1)) == 0, "item must be a power of two");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    DevBuf agg;
+    struct R {
+        DevBuf &b;
+        ~R() { b.release(); }
+    } rel{agg};
+    NMZ_TRY(agg.ensure(2 * TP_MAX_BLOCKS * 8));
+    TpScanArgs S{};
+    S.cnt = d_cnt;
+    S.n = n;
+    S.agg = agg.as<uint64_t>();
+    S.poff = d_poff;
+    S.ioff = d_ioff;
+    S.tot64 = d_tot;
+    NMZ_TRY(tp_offsets(S, item, st));
+    NMZ_HIP(hipStreamSynchronize(st));
+    return NMZ_OK;
+}
+
 int nmz_ed_plan_counters(nmz_ed_plan *plan, uint64_t *out, void *stream) {
     NMZ_CHECK(plan != nullptr && out != nullptr, "NULL argument");
     for (int i = 0; i < NMZ_ED_NCOUNTERS; ++i) out[i] = 0;

@@ -862,3 +862,33 @@ def test_repeated_shard_searches_use_cached_sizes(ctx):
     ref = (od.astype(np.uint64) << np.uint64(32)) | oi.astype(np.uint64)
     for r in runs:
         assert np.array_equal(r, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,item,big", [(1, 128, False), (2047, 128, False), (2048, 4096, False),
+                                         (2049, 256, False), (256 * 2048 + 5, 128, False),
+                                         (3_000_001, 1024, False), (20, 128, True)])
+def test_two_phase_offset_kernels(ctx, n, item, big):
+    """k_tp_reduce + k_tp_scan (the two-phase search's offsets after its count pass) against numpy: entry offsets and
+    work-item offsets as exclusive sums mod 2^32, the 64-bit entry total. n past 256 x 2,048 pairs makes every block
+    scan several 2,048-pair tiles; `big` counts push the total past 2^32 (the offsets wrap, the total must not)."""
+    import ctypes
+
+    import torch
+    L = _lib.load()
+    rng = np.random.default_rng(n + item)
+    cnt = (rng.integers(2**28, 2**30, n) if big else rng.integers(0, 40, n)).astype(np.uint32)
+    cnt[rng.random(n) < 0.3] = 0
+    d_cnt = torch.from_numpy(cnt.view(np.int32)).cuda()
+    d_poff = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
+    d_ioff = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
+    d_tot = torch.zeros(1, dtype=torch.int64, device="cuda")
+    _lib.check(L.nmz_debug_tp_offsets(ctx.handle, ctypes.c_void_p(d_cnt.data_ptr()), n, item,
+                                      ctypes.c_void_p(d_poff.data_ptr()), ctypes.c_void_p(d_ioff.data_ptr()),
+                                      ctypes.c_void_p(d_tot.data_ptr()), None))
+    c64 = cnt.astype(np.uint64)
+    exp_p = np.concatenate([[0], np.cumsum(c64)]).astype(np.uint64)
+    exp_i = np.concatenate([[0], np.cumsum((c64 + item - 1) // item)]).astype(np.uint64)
+    assert np.array_equal(d_poff.cpu().numpy().view(np.uint32), (exp_p & 0xFFFFFFFF).astype(np.uint32))
+    assert np.array_equal(d_ioff.cpu().numpy().view(np.uint32), (exp_i & 0xFFFFFFFF).astype(np.uint32))
+    assert int(d_tot.cpu().numpy().view(np.uint64)[0]) == int(exp_p[-1])
