@@ -224,3 +224,84 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def query_quantile(img, d, RA, RB, Hm, Hm2, m):
+    """As query(), with the predecessors by a count-guided descent from the root (no branch-off tracking in the
+    count descent): the part's predecessor of R is its (#elements below R)-th smallest, or its largest when none is
+    below R (it wraps)."""
+    n, lb, lv, mk, cm, ev, K, bb = img["n"], img["lb"], img["lv"], img["mk"], img["cm"], img["e"], img["K"], img["bb"]
+    BW = 1 << bb
+    F = (1 << BW) - 1
+    oA = oB = d
+    cA = cB = 0
+    for l in range(lb):
+        h = 1 << (K - l - 1)
+        msk = ~(2 * h - 1)
+        s = RA & msk
+        o = ones(lv[l], s, s + oA)
+        if RA & h:
+            oA = o
+        else:
+            cA += o
+            oA = oA - o
+        s = RB & msk
+        o = ones(lv[l], s, s + oB)
+        if RB & h:
+            oB = o
+        else:
+            cB += o
+            oB = oB - o
+    mA = mk[RA >> bb][oA]
+    mB = mk[RB >> bb][oB]
+    cA += bin(mA >> (RA & (BW - 1))).count("1")
+    cB += bin(mB >> (RB & (BW - 1))).count("1")
+    W = cA + (n - RB) - cB
+
+    def top(x):
+        return x.bit_length() - 1
+
+    def below(x):  # bits [0, x) of a block mask, x may pass the block
+        return F if x >= BW else (1 << max(x, 0)) - 1
+
+    kA = kB = None
+    if d > 0:
+        lt = d - cA
+        wrap = lt == 0
+        k = d - 1 if wrap else lt - 1
+        s, q = 0, d
+        for l in range(lb):
+            h = 1 << (K - l - 1)
+            o = ones(lv[l], s, s + q)
+            z = q - o
+            if k < z:
+                q = z
+            else:
+                k -= z
+                s += h
+                q = o
+        v = mk[s >> bb][q] & (F if wrap else below(RA - s))
+        pA = s + top(v)
+        t = (Hm + cm[pA] - (m if wrap else 0)) % (1 << 32)
+        kA = (t << 32) | (0xFFFFFFFF - ev[pA])
+    if d < n:
+        lt = RB - (d - cB)
+        wrap = lt == 0
+        k = n - d - 1 if wrap else lt - 1
+        s, q = 0, d
+        for l in range(lb):
+            h = 1 << (K - l - 1)
+            o = ones(lv[l], s, s + q)
+            zl = min(n - s, h)
+            zs = zl - (q - o)  # zeros of the node from entry q on
+            if k < zs:
+                q = q - o
+            else:
+                k -= zs
+                s += h
+                q = o
+        v = (~mk[s >> bb][q] & F) & (F >> (BW - min(n - s, BW))) & (F if wrap else below(RB - s))
+        pB = s + top(v)
+        t = (Hm2 + cm[pB] - (m if wrap else 0)) % (1 << 32)
+        kB = (t << 32) | (0xFFFFFFFF - ev[pB])
+    return W, kA, kB
