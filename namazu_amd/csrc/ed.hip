@@ -1100,7 +1100,10 @@ struct TpScanArgs {
     uint64_t *agg;          // [2 TP_MAX_BLOCKS]: block b's entries, items
     uint32_t *poff, *ioff;  // [n + 1]
     uint64_t *tot64;
-    uint32_t *n_rec, *rec_out;  // the record counter (or nullptr) and where its value goes
+    uint32_t *n_rec, *rec_out;  // the records' stripe counters (or nullptr) and where their total goes (UINT32_MAX
+                                // when a stripe overflowed rec_share: the write pass then recomputes)
+    uint32_t *rec_cnt;          // [ED_REC_STRIPES] the stripes' counts, for the scatter
+    uint32_t rec_share;
     uint32_t *flag;         // or nullptr: no cached sizes to compare
     uint64_t e_tot;
     uint32_t e_items, e_rec;
@@ -1204,16 +1207,25 @@ __global__ __launch_bounds__(256) void k_tp_scan(TpScanArgs A) {
         ce += te;
         ci += ti;
     }
-    if (blockIdx.x + 1 == A.nb && t == 0) {
-        A.poff[A.n] = (uint32_t)ce;
-        A.ioff[A.n] = (uint32_t)ci;
-        *A.tot64 = ce;
-        const uint32_t r = A.n_rec ? *A.n_rec : 0u;
-        if (A.n_rec) {
-            *A.rec_out = r;
-            *A.n_rec = 0;
+    if (blockIdx.x + 1 == A.nb && t < 64) {  // the last block's first wave: totals, record counts, the check
+        uint32_t r = 0;
+        bool over = false;
+        if (A.n_rec) {  // (ED_REC_STRIPES == 64: a lane per stripe)
+            const uint32_t c = A.n_rec[t * ED_REC_LINE];
+            A.rec_cnt[t] = c;
+            A.n_rec[t * ED_REC_LINE] = 0;
+            over = __ballot(c > A.rec_share) != 0;
+            r = c;
+            for (int o = 32; o >= 1; o >>= 1) r += __shfl_xor(r, o, 64);
+            if (over) r = 0xFFFFFFFFu;
         }
-        if (A.flag && (ce != A.e_tot || (uint32_t)ci != A.e_items || r != A.e_rec)) atomicOr(A.flag, 1u);
+        if (t == 0) {
+            A.poff[A.n] = (uint32_t)ce;
+            A.ioff[A.n] = (uint32_t)ci;
+            *A.tot64 = ce;
+            if (A.n_rec) *A.rec_out = r;
+            if (A.flag && (ce != A.e_tot || (uint32_t)ci != A.e_items || r != A.e_rec)) atomicOr(A.flag, 1u);
+        }
     }
 }
 
@@ -1280,14 +1292,16 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
         if (!tiles.empty()) NMZ_HIP(hipMemcpy(tl.ptr, tiles.data(), tiles.size() * 8, hipMemcpyHostToDevice));
         p->tile_count[key] = tiles.size();
     }
-    // scratch: {mismatch flag, record count out}, the entry total, the offset kernels' block sums, the per-pair
-    // counts (zero between searches: the write pass takes back what the count pass added) and offsets
+    // scratch: {mismatch flag, record count out}, the entry total, the offset kernels' block sums, the records'
+    // per-stripe counts, the per-pair counts (zero between searches: the write pass takes back what the count pass
+    // added) and offsets
     const size_t tp_bytes = Carve::bytes_for(4, 4) + Carve::bytes_for(1, 8) + Carve::bytes_for(2 * TP_MAX_BLOCKS, 8) +
-                            3 * Carve::bytes_for(n_pairs + 1, 4);
+                            Carve::bytes_for(ED_REC_STRIPES, 4) + 3 * Carve::bytes_for(n_pairs + 1, 4);
     NMZ_TRY(p->tp_mem.ensure(tp_bytes));
     Carve cv(p->tp_mem.ptr);
     uint32_t *f = cv.take<uint32_t>(4);
     uint64_t *d_tot64 = cv.take<uint64_t>(1), *d_agg = cv.take<uint64_t>(2 * TP_MAX_BLOCKS);
+    uint32_t *d_rec_cnt = cv.take<uint32_t>(ED_REC_STRIPES);
     uint32_t *d_cnt = cv.take<uint32_t>(n_pairs + 1), *d_poff = cv.take<uint32_t>(n_pairs + 1);
     uint32_t *d_ioff = cv.take<uint32_t>(n_pairs + 1);
     if (f != p->d_tp_mismatch) {  // a new scratch buffer: flag and counts start clear
@@ -1306,25 +1320,32 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     Q.poff = d_poff;
     Q.ent = nullptr;
     // the count pass's survivor records (32 B per (wave, query pair) with survivors) let the write pass scatter
-    // without recomputing the filter; room for 16 per tile (a record list that overflows: the write pass recomputes)
+    // without recomputing the filter; room for 16 per tile, in ED_REC_STRIPES equal regions (a stripe that overflows
+    // its region: the write pass recomputes)
     const uint64_t rec_cap = std::min<uint64_t>(n_tiles_all * 16, ED_TP_MAX_REC_BYTES / 32);
+    // (at least 256 per stripe: a small search's few workgroups each land in one stripe, up to 128 records each)
+    const uint64_t rec_share = std::max<uint64_t>((rec_cap + ED_REC_STRIPES - 1) / ED_REC_STRIPES, 256);
+    constexpr size_t REC_CTR_BYTES = (size_t)ED_REC_STRIPES * ED_REC_LINE * 4;  // the stripe counters, then records
     Q.recs = nullptr;
     Q.rec_cap = 0;
+    Q.rec_cnt = d_rec_cnt;
     // (NMZ_ED_QG_RECOMPUTE=1 skips the records: the recompute path, for tests)
     const char *rc_env = ab_env("NMZ_ED_QG_RECOMPUTE");
     // (the kernels count records with a u32 atomic, up to 128 per tile: a launch that could pass 2^32 of them would
     // wrap the counter, so such searches recompute instead)
     if (!(rc_env && atoi(rc_env) == 1) && n_tiles_all * 128 < (1ULL << 32) &&
-        p->tp_rec.ensure(Carve::bytes_for(rec_cap * 32 + 16, 1)) == NMZ_OK) {
-        Q.recs = p->tp_rec.as<uint4>() + 1;
-        Q.rec_cap = (uint32_t)rec_cap;
+        p->tp_rec.ensure(Carve::bytes_for(REC_CTR_BYTES + rec_share * ED_REC_STRIPES * 32, 1)) == NMZ_OK) {
+        Q.recs = p->tp_rec.as<uint4>() + REC_CTR_BYTES / 16;
+        Q.rec_cap = (uint32_t)rec_share;
     }
-    Q.n_rec = Q.recs ? p->tp_rec.as<uint32_t>() : nullptr;  // the counter in the buffer's first 16 bytes
-    // (k_tp_scan leaves it at zero; a new buffer or an interrupted search clears it here)
+    Q.n_rec = Q.recs ? p->tp_rec.as<uint32_t>() : nullptr;  // the stripe counters, at the buffer's start
+    // (k_tp_scan leaves them at zero; a new buffer or an interrupted search clears them here)
     if (Q.n_rec && (Q.n_rec != p->d_rec_clear || p->tp_dirty)) {
-        NMZ_HIP(hipMemsetAsync(Q.n_rec, 0, 4, st));
+        NMZ_HIP(hipMemsetAsync(Q.n_rec, 0, REC_CTR_BYTES, st));
         p->d_rec_clear = Q.n_rec;
     }
+    // records in the regions (UINT32_MAX when a stripe overflowed its region)
+    const uint64_t rec_total_cap = rec_share * ED_REC_STRIPES;
     Q.N = N;
     Q.k = A.k;
     Q.QB = QB;
@@ -1349,6 +1370,8 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
         S.tot64 = d_tot64;
         S.n_rec = with_rec ? Q.n_rec : nullptr;
         S.rec_out = f + 1;
+        S.rec_cnt = d_rec_cnt;
+        S.rec_share = Q.rec_cap;
         S.flag = verify ? p->d_tp_mismatch : nullptr;
         if (verify) {
             S.e_tot = verify->tot64;
@@ -1384,7 +1407,7 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
         Q.ent = p->tp_ent.as<uint32_t>();
         {
             KernelTimer kt(p->ctx, st, "ed_qg_filter");
-            if (Q.recs && n_rec <= Q.rec_cap) NMZ_TRY(ed_qg_scatter_launch(Q, n_rec, st));
+            if (Q.recs && n_rec <= rec_total_cap) NMZ_TRY(ed_qg_scatter_launch(Q, n_rec, st));
             else NMZ_TRY(ed_qg_filter_launch(Q, false, st));
         }
         p->tp_dirty = false;
@@ -1419,7 +1442,7 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     if (tot64 <= limit) {
         const uint32_t it = ed_bv_pick_item(tot64);
         if (it != item) NMZ_TRY(reitem(it));
-        if (Q.recs && n_rec <= Q.rec_cap) p->tp_sizes[key] = nmz_ed_plan::TpSizes{tot64, tot_items, n_rec, item};
+        if (Q.recs && n_rec <= rec_total_cap) p->tp_sizes[key] = nmz_ed_plan::TpSizes{tot64, tot_items, n_rec, item};
         return write_dp(tot64, tot_items);
     }
     // batches of whole query blocks: per-block totals from this count pass, then the lists and counters start over

@@ -797,10 +797,12 @@ __global__ __launch_bounds__(256) void k_ed_qg_filter(EdQgArgs A) {
         if (COUNT && A.recs && mask) {  // the survivors for the scatter pass: one record per (wave, pair)
             const uint64_t m1 = __ballot(a1), m2 = __ballot(a2);
             if (lane == 0) {
-                const uint32_t r = atomicAdd(A.n_rec, 1u);
+                const uint32_t sp = blockIdx.x % ED_REC_STRIPES;
+                const uint32_t r = atomicAdd(A.n_rec + sp * ED_REC_LINE, 1u);
                 if (r < A.rec_cap) {
-                    A.recs[2 * (uint64_t)r] = make_uint4(q1 >> 1, 256 * cb + 64 * wave, (uint32_t)m1, (uint32_t)(m1 >> 32));
-                    A.recs[2 * (uint64_t)r + 1] = make_uint4((uint32_t)m2, (uint32_t)(m2 >> 32), 0u, 0u);
+                    const uint64_t slot = (uint64_t)sp * A.rec_cap + r;
+                    A.recs[2 * slot] = make_uint4(q1 >> 1, 256 * cb + 64 * wave, (uint32_t)m1, (uint32_t)(m1 >> 32));
+                    A.recs[2 * slot + 1] = make_uint4((uint32_t)m2, (uint32_t)(m2 >> 32), 0u, 0u);
                 }
             }
         }
@@ -829,11 +831,30 @@ __global__ __launch_bounds__(256) void k_ed_qg_filter(EdQgArgs A) {
 // The write pass from the count pass's records (EdQgArgs::recs): a wave per record -- one count atomic and the
 // entries; no profile loads, no L1s, and nothing read for the (wave, pair)s without survivors (most of them: the
 // dense per-tile ballots this replaces were 2 KiB per tile, 0.6 GB read per launch on configs[2]).
+// (records sit in ED_REC_STRIPES regions of rec_cap: record g of the n_rec is in the stripe whose prefix of counts
+// holds it)
+static_assert(ED_REC_STRIPES == 64, "the scatter's prefix sums take one wave");
 __global__ __launch_bounds__(256) void k_ed_qg_scatter(EdQgArgs A, uint32_t n_rec) {
+    __shared__ uint32_t pre[ED_REC_STRIPES];
     const uint32_t lane = threadIdx.x & 63;
+    if (threadIdx.x < 64) {  // exclusive prefix sums of the stripes' counts (ED_REC_STRIPES == 64: one wave)
+        const uint32_t c = A.rec_cnt[lane];
+        uint32_t inc = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(inc, o, 64);
+            if (lane >= (uint32_t)o) inc += v;
+        }
+        pre[lane] = inc - c;
+    }
+    __syncthreads();
     const uint32_t nw = gridDim.x * 4;
-    for (uint32_t r = blockIdx.x * 4 + (threadIdx.x >> 6); r < n_rec; r += nw) {
-        const uint4 h = A.recs[2 * (uint64_t)r], g = A.recs[2 * (uint64_t)r + 1];
+    for (uint32_t g0 = blockIdx.x * 4 + (threadIdx.x >> 6); g0 < n_rec; g0 += nw) {
+        uint32_t lo = 0;  // the last stripe whose prefix is <= g0 (empty stripes share their successor's prefix)
+#pragma unroll
+        for (uint32_t st = ED_REC_STRIPES / 2; st; st >>= 1)
+            if (pre[lo + st] <= g0) lo += st;
+        const uint64_t r = (uint64_t)lo * A.rec_cap + (g0 - pre[lo]);
+        const uint4 h = A.recs[2 * r], g = A.recs[2 * r + 1];
         const uint64_t m1 = ((uint64_t)h.w << 32) | h.z, m2 = ((uint64_t)g.y << 32) | g.x, mask = m1 | m2;
         uint32_t base = 0;
         if (lane == 0) {  // the pair's next free slots, from its end down (the count pass's count returns to 0)

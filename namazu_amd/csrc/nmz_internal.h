@@ -104,13 +104,17 @@ struct EdQgArgs {
     uint32_t *ent;               // write pass: the entries
     uint4 *recs;                 // count pass: one record per (wave, query pair) with survivors -- {pair, first
                                  // candidate, run1 ballot} and {run2 ballot} (2 uint4) -- for the scatter pass, or
-                                 // nullptr (the write pass recomputes the filter)
-    uint32_t *n_rec;             // records appended (may exceed rec_cap: then the write pass recomputes)
-    uint32_t rec_cap;
+                                 // nullptr (the write pass recomputes the filter); ED_REC_STRIPES regions of rec_cap
+    uint32_t *n_rec;             // [ED_REC_STRIPES * ED_REC_LINE] records appended per stripe (workgroup mod
+                                 // ED_REC_STRIPES; one counter per 128-byte line: a single counter for the grid
+                                 // serialised ~10^5-10^6 same-address atomics); past rec_cap the write pass recomputes
+    const uint32_t *rec_cnt;     // scatter pass: [ED_REC_STRIPES] the count pass's records per stripe
+    uint32_t rec_cap;            // records per stripe
     uint64_t n_tiles;
     uint32_t N, k, QB, NCB, shard, n_shards;
     uint32_t w;                  // band
 };
+constexpr uint32_t ED_REC_STRIPES = 64, ED_REC_LINE = 32;
 int ed_qg_filter_launch(const EdQgArgs &A, bool count, hipStream_t st);
 int ed_qg_scatter_launch(const EdQgArgs &A, uint32_t n_rec, hipStream_t st);
 int ed_bv_dp_launch(const EdBvArgs &A, const uint32_t *ioff, const uint32_t *poff, const uint32_t *ent,
