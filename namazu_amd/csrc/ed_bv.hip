@@ -338,6 +338,9 @@ __device__ __forceinline__ void bv_publish(const EdBvArgs &A, bool fin, uint32_t
                                             uint32_t &in_band) {
     const bool b1 = fin && r1 <= w, b2 = fin && v2 && r2 <= w;
     in_band += (uint32_t)b1 + (uint32_t)b2;
+#ifdef NMZ_ABL_PUBLISH
+    return;  // timing only: results not listed
+#endif
     if (b1) bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, ((uint64_t)r1 << 32) | q1);
     if (b2) bv_knn_insert(A.knn + (uint64_t)j * A.k, A.k, ((uint64_t)r2 << 32) | q2);
     if (__any(b1)) bv_knn_insert_wave(A.knn + (uint64_t)q1 * A.k, A.k, b1 ? (((uint64_t)r1 << 32) | j) : UINT64_MAX, lane);
