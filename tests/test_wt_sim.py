@@ -22,7 +22,9 @@ def test_wt_sim_block_widths():
                     Hm, Hm2 = rng.randrange(m), rng.randrange(m)
                     RA = sum(1 for x in cm if x < m - Hm)
                     RB = sum(1 for x in cm if x < m - Hm2)
-                    W, kA, kB = wt_sim.query(img, d, RA, RB, Hm, Hm2, m)
                     bW, bk = wt_sim.brute(cm, e, d, Hm, Hm2, m)
-                    assert W == bW
-                    assert max(x for x in (kA, kB) if x is not None) == bk
+                    # the kernel's descents, and the count-guided alternative measured and rejected in round 5
+                    for q in (wt_sim.query, wt_sim.query_quantile):
+                        W, kA, kB = q(img, d, RA, RB, Hm, Hm2, m)
+                        assert W == bW
+                        assert max(x for x in (kA, kB) if x is not None) == bk
