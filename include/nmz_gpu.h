@@ -134,10 +134,15 @@ int nmz_replayable_decide_host(const uint8_t *seed, uint32_t seed_len, const uin
 /* FNV-1a 64 of n byte strings (an event's canonical JSON -> its identity) */
 int nmz_fnv1a64_batch_host(const uint64_t *off, const uint8_t *bytes, uint64_t n, uint64_t *out);
 
-/* Time-bounded queue (util/queue/impl.go:64-128 BasicTBQueue; host only): items are released at their due time
- * (CLOCK_MONOTONIC ns, nmz_monotonic_ns) by one timer thread, equal due times in enqueue order; consumers block in
- * dequeue (the policy's ActionChan). A released item records its release time, so release - due is the
- * delivered-delay error of the online path. */
+/* Time-bounded queue (util/queue/impl.go:64-128 BasicTBQueue; host only). One timer thread releases two kinds of
+ * item, times in CLOCK_MONOTONIC ns (nmz_monotonic_ns):
+ *   nmz_tbqueue_enqueue       a ranged item (min != max, impl.go:120-126): released at due_ns = enqueue + its drawn
+ *                             duration;
+ *   nmz_tbqueue_enqueue_fixed a fixed-duration item (min == max, impl.go:77-89,117-119): one FIFO lane whose head is
+ *                             released at max(its enqueue, the previous fixed item's release) + duration, so a burst
+ *                             of n items of duration d leaves at d, 2d, ..., nd, in enqueue order.
+ * Equal due times release in enqueue order; consumers block in dequeue (the policy's ActionChan). A released item
+ * records its due and release times, so release - due is the delivered-delay error of the online path. */
 typedef struct nmz_tbqueue nmz_tbqueue;
 int nmz_tbqueue_create(nmz_tbqueue **out);
 /* close: no further enqueues; every consumer blocked in dequeue (and every later dequeue) returns NMZ_EAGAIN.
@@ -148,6 +153,7 @@ int nmz_tbqueue_close(nmz_tbqueue *q);
 int nmz_tbqueue_destroy(nmz_tbqueue *q);
 int64_t nmz_monotonic_ns(void);
 int nmz_tbqueue_enqueue(nmz_tbqueue *q, uint64_t id, int64_t due_ns);
+int nmz_tbqueue_enqueue_fixed(nmz_tbqueue *q, uint64_t id, int64_t enqueued_ns, int64_t duration_ns);
 /* timeout_ns < 0: wait forever; NMZ_EAGAIN when nothing was released in time */
 int nmz_tbqueue_dequeue(nmz_tbqueue *q, int64_t timeout_ns, uint64_t *id, int64_t *due_ns, int64_t *released_ns);
 int nmz_tbqueue_stats(nmz_tbqueue *q, uint64_t *enqueued, uint64_t *released, uint64_t *dequeued);

@@ -115,6 +115,7 @@ SIGNATURES = {
     "nmz_tbqueue_destroy": (_int, [_P]),
     "nmz_monotonic_ns": (_i64, []),
     "nmz_tbqueue_enqueue": (_int, [_P, _u64, _i64]),
+    "nmz_tbqueue_enqueue_fixed": (_int, [_P, _u64, _i64, _i64]),
     "nmz_tbqueue_dequeue": (_int, [_P, _i64, ctypes.POINTER(_u64), ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
     "nmz_tbqueue_stats": (_int, [_P, ctypes.POINTER(_u64), ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     # device groups (multi-GPU inside the C ABI, csrc/group.hip)

@@ -20,9 +20,12 @@ the decision. NMZ_ONLINE=gpu decides queued events in GPU launches
 instead. Without the library nothing runs (namazu_amd._lib raises).
 
 QueueEvent never blocks on the consumer (randompolicy_test.go:112-118 asserts it):
-it decides the event and returns; a delivery thread puts each action on
-ActionChan at its enqueue time + its delay, as the reference's per-event
-goroutine + time.After does (replayablepolicy.go:121-125, util/queue/impl.go:110-128).
+it decides the event and returns; the time-bounded queue puts each action on
+ActionChan by the reference's release rules: a ranged or replayable action at its
+enqueue time + its delay (the per-event goroutine + time.After of
+replayablepolicy.go:121-125 and util/queue/impl.go:120-126), a fixed-duration one
+(min == max) through one FIFO lane whose head's timer starts when the previous
+fixed action was released (util/queue/impl.go:77-89,117-119).
 """
 import collections
 import ctypes
@@ -87,10 +90,12 @@ class ChannelClosed(queue.Empty):
 
 class ActionChannel:
     """ExplorePolicy.ActionChan() over the library's time-bounded queue (nmz_tbqueue_*, the reference's
-    BasicTBQueue, util/queue/impl.go:64-128): put_at(due_ns, action) hands an action to the native timer
-    thread, which releases it at its due time (CLOCK_MONOTONIC ns); get() blocks (with the GIL released) until an
-    action is released, like a receive on the Go channel. Equal due times keep their enqueue order. Each get()
-    records the action's delivered-delay error (release time - due time, both taken natively)."""
+    BasicTBQueue, util/queue/impl.go:64-128): put_at(due_ns, action) hands a ranged action to the native timer
+    thread, which releases it at its due time (CLOCK_MONOTONIC ns); put_fixed(enqueued_ns, duration_ns, action) puts a
+    fixed-duration action on the serial lane (released at max(enqueue, previous fixed release) + duration,
+    impl.go:77-89); get() blocks (with the GIL released) until an action is released, like a receive on the Go
+    channel. Equal due times keep their enqueue order. Each get() records the action's delivered-delay error
+    (release time - due time, both taken natively) and last_release_ns the release time of the last action got."""
 
     def __init__(self, history=100_000):
         self.L = _lib.load()
@@ -103,6 +108,7 @@ class ActionChannel:
         self._calls = 0  # native calls in flight: close() frees the queue only after they have returned
         self._closed = False
         self.delivery_err_ns = collections.deque(maxlen=history)
+        self.last_release_ns = None
 
     def _enter(self):
         with self._lock:
@@ -124,6 +130,16 @@ class ActionChannel:
                 i = next(self._ids)
                 self._items[i] = action
             _lib.check(self.L.nmz_tbqueue_enqueue(q, i, int(due_ns)))
+        finally:
+            self._leave()
+
+    def put_fixed(self, enqueued_ns, duration_ns, action):
+        q = self._enter()
+        try:
+            with self._lock:
+                i = next(self._ids)
+                self._items[i] = action
+            _lib.check(self.L.nmz_tbqueue_enqueue_fixed(q, i, int(enqueued_ns), int(duration_ns)))
         finally:
             self._leave()
 
@@ -151,6 +167,7 @@ class ActionChannel:
             raise queue.Empty
         _lib.check(rc)
         self.delivery_err_ns.append(rel.value - due.value)
+        self.last_release_ns = rel.value
         with self._lock:
             return self._items.pop(i.value)
 
@@ -189,7 +206,7 @@ class ActionChannel:
 
 
 class OnlineDecider:
-    """The QueueEvent engine: each event's decision, then its delivery at enqueue time + delay.
+    """The QueueEvent engine: each event's decision, then its delivery by the reference queue's release rules.
 
     The reference decides at enqueue, on the caller's goroutine (util/queue/impl.go:35-46,110-128;
     replayablepolicy.go:116-126), and delivers after time.After(delay). Two ways to decide:
@@ -198,10 +215,13 @@ class OnlineDecider:
         shared code, no launch), so a decision never waits for a GPU launch or for other events;
       * "gpu" (NMZ_ONLINE=gpu): a decision thread decides the queued events in GPU launches of at most
         `max_batch` events (nmz_random_decide / nmz_replayable_decide).
-    Each action goes to ActionChan at its enqueue time + its delay: the library's time-bounded queue releases it
-    from a native timer thread (ActionChannel; without one, a Python delivery thread). latencies_ns holds the
-    enqueue-to-decided time of recent events, delivery_err_ns the delivered-delay error (actual delivery -
-    (enqueue + decided delay)); bench.py reports their percentiles. A GPU decision failure is kept and raised by
+    A decision is (delay, action) or (delay, action, fixed). A ranged action (fixed false) goes to ActionChan at its
+    enqueue time + its delay; a fixed-duration one (the random policy's min == max) goes through one FIFO lane,
+    released at max(its enqueue, the previous fixed release) + delay (util/queue/impl.go:77-89). The library's
+    time-bounded queue releases both from a native timer thread (ActionChannel; without one, a Python delivery
+    thread runs the same two rules). latencies_ns holds the enqueue-to-decided time of recent events,
+    delivery_err_ns the delivered-delay error (actual delivery - the rule's due time); bench.py reports their
+    percentiles. A GPU decision failure is kept and raised by
     the next submit(), where a Go policy would panic (randompolicy.go:343, replayablepolicy.go:120)."""
 
     def __init__(self, decide_batch, deliver, decide_one=None, history=100_000, max_batch=64, chan=None):
@@ -214,6 +234,8 @@ class OnlineDecider:
         self._pending = []
         self._cv = threading.Condition()
         self._heap = []
+        self._fixed = collections.deque()  # Python delivery's fixed lane: (enqueue_ns, duration_ns, action)
+        self._fixed_last = None
         self._hcv = threading.Condition()
         self._seq = itertools.count()
         self.latencies_ns = collections.deque(maxlen=history)
@@ -236,12 +258,20 @@ class OnlineDecider:
     def _now(self):
         return _lib.load().nmz_monotonic_ns() if self._chan is not None else time.monotonic_ns()
 
-    def _schedule(self, due_ns, action):
+    def _schedule(self, t0, decision):
+        delay, action = max(int(decision[0]), 0), decision[1]
+        fixed = len(decision) > 2 and bool(decision[2])
         if self._chan is not None:
-            self._chan.put_at(due_ns, action)
+            if fixed:
+                self._chan.put_fixed(t0, delay, action)
+            else:
+                self._chan.put_at(t0 + delay, action)
             return
         with self._hcv:
-            heapq.heappush(self._heap, (due_ns, next(self._seq), action))
+            if fixed:
+                self._fixed.append((t0, delay, next(self._seq), action))
+            else:
+                heapq.heappush(self._heap, (t0 + delay, next(self._seq), action))
             self._hcv.notify()
 
     def submit(self, event):
@@ -253,9 +283,9 @@ class OnlineDecider:
                     self._start()
         t0 = self._now()
         if self.mode == "host":
-            delay, action = self._decide_one(event)  # raises like the reference's panic
+            decision = self._decide_one(event)  # raises like the reference's panic
             self.latencies_ns.append(self._now() - t0)
-            self._schedule(t0 + max(int(delay), 0), action)
+            self._schedule(t0, decision)
             with self._cv:
                 self._n_in += 1
                 self._n_decided += 1
@@ -303,34 +333,49 @@ class OnlineDecider:
                 return
             now = self._now()
             self.batch_sizes.append(len(batch))
-            for (t0, _), (delay, action) in zip(batch, out):
+            for (t0, _), decision in zip(batch, out):
                 self.latencies_ns.append(now - t0)
-                self._schedule(t0 + max(int(delay), 0), action)
+                self._schedule(t0, decision)
             with self._cv:
                 self._n_decided += len(batch)
                 self._cv.notify_all()
 
+    def _next_due(self):
+        """(due, seq, lane) of the next action to deliver, or None: the heap's top or the fixed lane's head, whose
+        timer starts at max(its enqueue, the previous fixed delivery) (util/queue/impl.go:77-89)."""
+        cands = []
+        if self._heap:
+            cands.append((self._heap[0][0], self._heap[0][1], 0))
+        if self._fixed:
+            t0, d, seq, _ = self._fixed[0]
+            start = t0 if self._fixed_last is None else max(t0, self._fixed_last)
+            cands.append((start + d, seq, 1))
+        return min(cands) if cands else None
+
     def _deliver_loop(self):
-        """Python delivery for a caller-supplied deliver() (no ActionChannel): every action due, in due order."""
+        """Python delivery for a caller-supplied deliver() (no ActionChannel): the same two release rules as the
+        native queue, one action at a time in due order."""
         while True:
             with self._hcv:
                 while True:
-                    if self._heap:
-                        wait_ns = self._heap[0][0] - time.monotonic_ns()
+                    nxt = self._next_due()
+                    if nxt is not None:
+                        wait_ns = nxt[0] - time.monotonic_ns()
                         if wait_ns <= 0:
                             break
                         self._hcv.wait(wait_ns / 1e9)
                     else:
                         self._hcv.wait()
-                now = time.monotonic_ns()
-                due_items = []
-                while self._heap and self._heap[0][0] <= now:
-                    due_items.append(heapq.heappop(self._heap))
-            for due, _, action in due_items:
-                self._deliver(action)
-                self.delivery_err_ns.append(time.monotonic_ns() - due)
+                due, _, lane = nxt
+                action = heapq.heappop(self._heap)[2] if lane == 0 else self._fixed.popleft()[3]
+            self._deliver(action)
+            now = time.monotonic_ns()
+            self.delivery_err_ns.append(now - due)
+            with self._hcv:
+                if lane == 1:
+                    self._fixed_last = now
             with self._cv:
-                self._n_delivered += len(due_items)
+                self._n_delivered += 1
 
 
 class ExplorePolicy:
@@ -358,7 +403,8 @@ class ExplorePolicy:
 
     def QueueEvent(self, event):
         """Non-blocking (never waits for the action's consumer): the event is decided at enqueue, as the reference
-        does, and its action is delivered at enqueue + delay by the policy's delivery thread."""
+        does, and its action is released by the time-bounded queue (at enqueue + delay, or through the serial
+        fixed-duration lane for the random policy's min == max items)."""
         self.online.submit(event)
 
     def _decide_batch(self, events):
@@ -571,9 +617,22 @@ class Random(ExplorePolicy):
         d, f = self.decide_events([event])
         return int(d[0]), bool(f[0])
 
+    def is_fixed(self, event):
+        """QueueEvent's queue kind (randompolicy.go:332-346 + util/queue/impl.go:117-119): the event's interval
+        bounds after the prioritized x0.8 are equal, so its item goes through BasicTBQueue's fixed-duration lane."""
+        p = self._cached_params()
+        pr = 1 if event.EntityID() in self.PrioritizedEntities else 0
+        return p.min_ns[pr] == p.max_ns[pr]
+
+    def _cached_params(self):
+        key = (self.MinInterval, self.MaxInterval, self.FaultActionProbability)
+        if getattr(self, "_params_key", None) != key:
+            self._params, self._params_key = self.params(), key
+        return self._params
+
     def _decide_batch(self, events):
         d, f = self.decide_events(events)
-        return [(int(dl), e.DefaultFaultAction() if fl else e.DefaultAction())
+        return [(int(dl), e.DefaultFaultAction() if fl else e.DefaultAction(), self.is_fixed(e))
                 for dl, fl, e in zip(d.tolist(), f.tolist(), events)]
 
     def event_class(self, ev):
@@ -592,13 +651,13 @@ class Random(ExplorePolicy):
         h = ctypes.c_uint64()
         _lib.check(L.nmz_fnv1a64_batch_host(off, js or None, 1, ctypes.byref(h)))
         cls = ctypes.c_uint8(self.event_class(event))
-        key = (self.MinInterval, self.MaxInterval, self.FaultActionProbability)
-        if getattr(self, "_params_key", None) != key:
-            self._params, self._params_key = self.params(), key
+        p = self._cached_params()
         d, f = ctypes.c_int64(), ctypes.c_uint8()
         _lib.check(L.nmz_random_decide_host(int(self.Seed), ctypes.byref(h), ctypes.byref(cls), 1,
-                                            ctypes.byref(self._params), ctypes.byref(d), ctypes.byref(f)))
-        return d.value, (event.DefaultFaultAction() if f.value else event.DefaultAction())
+                                            ctypes.byref(p), ctypes.byref(d), ctypes.byref(f)))
+        pr = 1 if cls.value & _lib.NMZ_EV_PRIORITIZED else 0
+        return (d.value, (event.DefaultFaultAction() if f.value else event.DefaultAction()),
+                p.min_ns[pr] == p.max_ns[pr])
 
 
 RegisterKnownExplorePolicies()
