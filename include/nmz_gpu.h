@@ -324,8 +324,11 @@ int nmz_ed_plan_create_dev(nmz_ctx *ctx, const uint64_t *off, const uint64_t *d_
                            uint32_t band, nmz_ed_plan **out);
 /* Plan options (bit flags) of nmz_ed_plan_create_opts. 0 is the product's choice; the others select the
  * alternative forms of the bit-parallel search, for A/B runs and tests. Whichever form a plan takes, a shard owns
- * the same pairs (whole 64-query blocks, nmz_ed_block_shard), so shards may mix forms. The NMZ_ED_* environment
- * knobs that add to these are read only when NMZ_AB=1 is set. */
+ * the same pairs (whole 64-query blocks, nmz_ed_block_shard), so within ONE process the shards of a search may run on
+ * plans of different forms and still partition the pairs (tests/test_ed_gpu.py checks this). The multi-rank paths do
+ * not allow the mix: the device groups and namazu_amd/dist.check_ed_plans require equal fingerprints, which include
+ * the form bits, and fail with NMZ_EINVAL otherwise. The NMZ_ED_* environment knobs that add to these are read only
+ * when NMZ_AB=1 is set. */
 #define NMZ_ED_OPT_SINGLE_KERNEL 1u /* no two-phase search: the single kernel with its in-workgroup pre-filter */
 #define NMZ_ED_OPT_NO_QGRAM 2u      /* no q-gram lower-bound filter (the single kernel, without the filter) */
 #define NMZ_ED_OPT_COMPACT 4u       /* compact per-workgroup Peq tables even when the direct tables fit */
@@ -443,6 +446,10 @@ int nmz_open_group_rank(const uint8_t *id, int n_ranks, int rank, int device, ui
  * still alive (destroy them first). No call on the group may start once close has begun. */
 int nmz_close_group(nmz_group *g);
 int nmz_group_info(const nmz_group *g, int *n_ranks, int *n_local_devices, uint32_t *n_shards);
+/* Collectives this process has entered on the group so far. Every group call that exchanges results first enters
+ * one status all_gather (every rank, whatever failed locally) and then, only when every rank succeeded, its payload
+ * collective, so a failed call enters the same collectives on every rank (tests check the sequence with this). */
+int nmz_group_collectives(const nmz_group *g, uint64_t *n);
 
 /* replayable sweep over a group (replayablepolicy.go:100-114 per decision, as nmz_replayable_sweep): one plan
  * per device, kept for repeated sweeps; stats[n_seeds] (may be NULL) and the merged topk[k] (k <= 256, .seed =

@@ -444,8 +444,14 @@ struct nmz_ed_plan {
     };
     std::map<uint64_t, TpSizes> tp_sizes;  // per (shard, n_shards): entry total, DP items, records of its searches
     uint32_t *d_tp_mismatch = nullptr;     // (in tp_mem) set when a search's totals differ from tp_sizes
-    uint32_t *d_rec_clear = nullptr;       // the record counter last cleared by a memset (tp_rec moves when it grows)
+    uint64_t tp_mem_gen = 0, tp_rec_gen = 0;  // DevBuf::gen of tp_mem / tp_rec when their counters were last cleared
     bool tp_dirty = false;                 // a count pass's counts not yet taken back by its write pass
+    // the mismatch flag as of the last search enqueued with cached sizes: copied to pinned host memory behind an
+    // event, read (ed_tp_flag_check) by the shard's next search without waiting, or with a wait by the synchronous
+    // entry points (nmz_ed_plan_counters, the group search)
+    uint32_t *h_tp_flag = nullptr;
+    hipEvent_t tp_flag_ev = nullptr;
+    bool tp_flag_armed = false;
     // fixed at creation (NMZ_ED_QGRAM / NMZ_ED_TWO_PHASE, A/B knobs read once per plan), so every shard and every
     // call of one plan takes the same search and deals pairs by the same rule
     bool qgram = true, two_phase = true;
@@ -1243,6 +1249,48 @@ static int tp_offsets(TpScanArgs &A, uint32_t item, hipStream_t st) {
     return NMZ_OK;
 }
 
+// The mismatch flag of searches enqueued with a shard's cached sizes (see ed_bv_two_phase). arm: after such a
+// search, copy the flag to pinned host memory behind an event. check: read that copy -- without waiting (the shard's
+// next search: a copy not yet landed is read by a later call, the device flag stays set until reported), or after
+// synchronising `st` (wait: the synchronous entry points) -- and, when set, clear it, drop every cached size (the
+// next search recounts) and fail.
+int ed_tp_flag_arm(nmz_ed_plan *p, hipStream_t st) {
+    if (!p->d_tp_mismatch) return NMZ_OK;
+    if (!p->h_tp_flag) {
+        NMZ_HIP(hipHostMalloc((void **)&p->h_tp_flag, 4, hipHostMallocDefault));
+        *p->h_tp_flag = 0;
+    }
+    if (!p->tp_flag_ev) NMZ_HIP(hipEventCreateWithFlags(&p->tp_flag_ev, hipEventDisableTiming));
+    NMZ_HIP(hipMemcpyAsync(p->h_tp_flag, p->d_tp_mismatch, 4, hipMemcpyDeviceToHost, st));
+    NMZ_HIP(hipEventRecord(p->tp_flag_ev, st));
+    p->tp_flag_armed = true;
+    return NMZ_OK;
+}
+
+int ed_tp_flag_check(nmz_ed_plan *p, bool wait, hipStream_t st) {
+    if (!p->d_tp_mismatch) return NMZ_OK;
+    uint32_t f = 0;
+    if (wait) {
+        NMZ_HIP(hipMemcpyAsync(&f, p->d_tp_mismatch, 4, hipMemcpyDeviceToHost, st));
+        NMZ_HIP(hipStreamSynchronize(st));
+    } else {
+        if (!p->tp_flag_armed) return NMZ_OK;
+        const hipError_t q = hipEventQuery(p->tp_flag_ev);
+        if (q == hipErrorNotReady) return NMZ_OK;
+        if (q != hipSuccess) return fail(NMZ_EHIP, "hipEventQuery failed");
+        f = *p->h_tp_flag;
+    }
+    p->tp_flag_armed = false;
+    if (!f) return NMZ_OK;
+    NMZ_HIP(hipMemsetAsync(p->d_tp_mismatch, 0, 4, st));
+    if (p->h_tp_flag) *p->h_tp_flag = 0;
+    p->tp_sizes.clear();
+    p->tp_dirty = true;  // the skipped write pass left the count pass's counts in place
+    return fail(NMZ_EHIP, "internal: a two-phase search's totals differed from the shard's cached sizes; that search "
+                          "wrote no entries and ran no DP (its k-NN lists are incomplete), and the cached sizes are "
+                          "dropped");
+}
+
 // The shard's tiles in query-block order; the count pass sizes the entry lists. Entry lists beyond
 // ed_tp_max_entries() are split: the shard's query blocks run in batches (whole blocks, at least one per batch) whose
 // entries fit, each batch a count pass, scans, the write pass and the DP. Every shard of a search therefore covers
@@ -1297,6 +1345,8 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     // added) and offsets
     const size_t tp_bytes = Carve::bytes_for(4, 4) + Carve::bytes_for(1, 8) + Carve::bytes_for(2 * TP_MAX_BLOCKS, 8) +
                             Carve::bytes_for(ED_REC_STRIPES, 4) + 3 * Carve::bytes_for(n_pairs + 1, 4);
+    // an earlier search of this plan whose sizes contradicted the cache is reported here (without waiting for it)
+    NMZ_TRY(ed_tp_flag_check(p, false, st));
     NMZ_TRY(p->tp_mem.ensure(tp_bytes));
     Carve cv(p->tp_mem.ptr);
     uint32_t *f = cv.take<uint32_t>(4);
@@ -1304,9 +1354,10 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     uint32_t *d_rec_cnt = cv.take<uint32_t>(ED_REC_STRIPES);
     uint32_t *d_cnt = cv.take<uint32_t>(n_pairs + 1), *d_poff = cv.take<uint32_t>(n_pairs + 1);
     uint32_t *d_ioff = cv.take<uint32_t>(n_pairs + 1);
-    if (f != p->d_tp_mismatch) {  // a new scratch buffer: flag and counts start clear
+    if (p->tp_mem.gen != p->tp_mem_gen || f != p->d_tp_mismatch) {  // a new scratch buffer: flag and counts clear
         NMZ_HIP(hipMemsetAsync(p->tp_mem.ptr, 0, tp_bytes, st));
         p->d_tp_mismatch = f;
+        p->tp_mem_gen = p->tp_mem.gen;
     } else if (p->tp_dirty) {  // an earlier search stopped between its count and write passes
         NMZ_HIP(hipMemsetAsync(d_cnt, 0, (n_pairs + 1) * 4, st));
     }
@@ -1319,6 +1370,8 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     Q.cnt = d_cnt;
     Q.poff = d_poff;
     Q.ent = nullptr;
+    Q.ent_cap = 0;
+    Q.abort = f;  // the mismatch flag: the write pass and the DP skip when it is set
     // the count pass's survivor records (32 B per (wave, query pair) with survivors) let the write pass scatter
     // without recomputing the filter; room for 16 per tile, in ED_REC_STRIPES equal regions (a stripe that overflows
     // its region: the write pass recomputes)
@@ -1339,10 +1392,11 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
         Q.rec_cap = (uint32_t)rec_share;
     }
     Q.n_rec = Q.recs ? p->tp_rec.as<uint32_t>() : nullptr;  // the stripe counters, at the buffer's start
-    // (k_tp_scan leaves them at zero; a new buffer or an interrupted search clears them here)
-    if (Q.n_rec && (Q.n_rec != p->d_rec_clear || p->tp_dirty)) {
+    // (k_tp_scan leaves them at zero; a new allocation -- tp_rec's generation changed, whatever its address -- or
+    // an interrupted search clears them here)
+    if (Q.n_rec && (p->tp_rec.gen != p->tp_rec_gen || p->tp_dirty)) {
         NMZ_HIP(hipMemsetAsync(Q.n_rec, 0, REC_CTR_BYTES, st));
-        p->d_rec_clear = Q.n_rec;
+        p->tp_rec_gen = p->tp_rec.gen;
     }
     // records in the regions (UINT32_MAX when a stripe overflowed its region)
     const uint64_t rec_total_cap = rec_share * ED_REC_STRIPES;
@@ -1374,7 +1428,9 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
         S.rec_share = Q.rec_cap;
         S.flag = verify ? p->d_tp_mismatch : nullptr;
         if (verify) {
-            S.e_tot = verify->tot64;
+            // (NMZ_ED_TP_FAKE_MISMATCH=1, a test knob: compare against a wrong total, so the flag path runs)
+            const char *fake = ab_env("NMZ_ED_TP_FAKE_MISMATCH");
+            S.e_tot = verify->tot64 + ((fake && atoi(fake) == 1) ? 1 : 0);
             S.e_items = verify->items;
             S.e_rec = verify->n_rec;
         }
@@ -1405,6 +1461,7 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
         NMZ_CHECK(n_ent < (1ULL << 32), "internal: a two-phase batch reaches 2^32 entries");
         NMZ_TRY(p->tp_ent.ensure(Carve::bytes_for(n_ent + 1, 4)));
         Q.ent = p->tp_ent.as<uint32_t>();
+        Q.ent_cap = n_ent;  // entry writes past the sizes the lists were made for are dropped
         {
             KernelTimer kt(p->ctx, st, "ed_qg_filter");
             if (Q.recs && n_rec <= rec_total_cap) NMZ_TRY(ed_qg_scatter_launch(Q, n_rec, st));
@@ -1412,7 +1469,7 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
         }
         p->tp_dirty = false;
         KernelTimer kt(p->ctx, st, "ed_bv_dp");
-        return ed_bv_dp_launch(A, d_ioff, d_poff, Q.ent, n_pairs, n_items, item, p->bw, p->cmp, st);
+        return ed_bv_dp_launch(A, d_ioff, d_poff, Q.ent, n_pairs, n_items, item, p->bw, p->cmp, st, f);
     };
     uint64_t tot64 = 0;
     uint32_t tot_items = 0;
@@ -1428,15 +1485,18 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     // The sizes the host needs before the write pass and the DP (entry total, work items, survivor records) are
     // fixed by the plan and the shard: the first search of a shard reads them back (one synchronisation), later
     // searches enqueue every kernel with those sizes and no host round trip; a one-thread kernel compares them with
-    // this search's own totals and flags a difference (nmz_ed_plan_counters reports it; none can occur: the plan is
-    // immutable and the filter deterministic)
+    // this search's own totals and flags a difference. None can occur (the plan is immutable and the filter
+    // deterministic), but if one did, the flagged search's write pass and DP skip (no write past lists sized for the
+    // cached totals, no DP over offsets that disagree with them) and the shard's next search, or the next
+    // synchronous call, reports it and drops the cache (ed_tp_flag_check)
     auto cached = p->tp_sizes.find(key);
     if (cached != p->tp_sizes.end() && Q.recs && cached->second.tot64 <= limit) {
         const nmz_ed_plan::TpSizes &z = cached->second;
         item = z.item;
         NMZ_TRY(count(tl.as<uint64_t>(), n_tiles_all, tot64, tot_items, &z));
         n_rec = z.n_rec;
-        return write_dp(z.tot64, z.items);
+        NMZ_TRY(write_dp(z.tot64, z.items));
+        return ed_tp_flag_arm(p, st);
     }
     NMZ_TRY(count(tl.as<uint64_t>(), n_tiles_all, tot64, tot_items));
     if (tot64 <= limit) {
@@ -1663,6 +1723,8 @@ int nmz_ed_plan_destroy(nmz_ed_plan *plan) {
         plan->tp_ent.release();
         plan->tp_rec.release();
         for (auto &kv : plan->tile_list) kv.second.release();
+        if (plan->tp_flag_ev) (void)hipEventSynchronize(plan->tp_flag_ev), (void)hipEventDestroy(plan->tp_flag_ev);
+        if (plan->h_tp_flag) (void)hipHostFree(plan->h_tp_flag);
     }
     delete plan;
     return NMZ_OK;
@@ -1679,6 +1741,7 @@ int nmz_debug_tp_offsets(nmz_ctx *ctx, const uint32_t *d_cnt, uint32_t n, uint32
               "NULL argument");
     NMZ_CHECK(n > 0 && n < (1u << 30), "n out of range");
     NMZ_CHECK(item > 0 && (item & (item - 1)) == 0, "item must be a power of two");
+    NMZ_CHECK(((uintptr_t)d_cnt & 15) == 0, "d_cnt must be 16-byte aligned (the scan loads uint4)");
     CtxGuard g(ctx);
     NMZ_TRY(g.rc);
     hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
@@ -1712,13 +1775,7 @@ int nmz_ed_plan_counters(nmz_ed_plan *plan, uint64_t *out, void *stream) {
     NMZ_HIP(hipStreamSynchronize(st));
     for (uint32_t sidx = 0; sidx < ED_CNT_STRIPES; ++sidx)
         for (int i = 0; i < ED_BV_NCOUNTERS; ++i) out[i] += lines[sidx * ED_CNT_LINE + i];
-    if (plan->d_tp_mismatch) {
-        uint32_t f = 0;
-        NMZ_HIP(hipMemcpyAsync(&f, plan->d_tp_mismatch, 4, hipMemcpyDeviceToHost, st));
-        NMZ_HIP(hipStreamSynchronize(st));
-        NMZ_CHECK(f == 0, "internal: a two-phase search's totals differed from the shard's cached sizes");
-    }
-    return NMZ_OK;
+    return ed_tp_flag_check(plan, true, st);
 }
 
 }  // extern "C"
@@ -2109,6 +2166,8 @@ int nmz_ed_allpairs_knn(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, 
             p->tp_ent.release();
             p->tp_rec.release();
             for (auto &kv : p->tile_list) kv.second.release();
+            if (p->tp_flag_ev) (void)hipEventSynchronize(p->tp_flag_ev), (void)hipEventDestroy(p->tp_flag_ev);
+            if (p->h_tp_flag) (void)hipHostFree(p->h_tp_flag);
             delete p;
         }
     } pg{plan};

@@ -742,6 +742,7 @@ __global__ __launch_bounds__(256) void k_ed_qg_filter(EdQgArgs A) {
     __shared__ uint32_t qlen[64];
     const uint64_t t = qg_tile_of_block();
     if (t >= A.n_tiles) return;
+    if (!COUNT && A.abort && *A.abort) return;  // the search's sizes differ from the cached ones: write nothing
     const uint64_t tq = A.tiles[t];
     const uint32_t qb = (uint32_t)(tq >> 32), cb = (uint32_t)tq;
     for (uint32_t i = threadIdx.x; i < 64 * (ED_QG_DW / 4); i += 256) {
@@ -816,9 +817,8 @@ __global__ __launch_bounds__(256) void k_ed_qg_filter(EdQgArgs A) {
             if (lane == leader) base = COUNT ? atomicAdd(&A.cnt[p], n) : A.poff[p] + atomicSub(&A.cnt[p], n) - n;
             if (!COUNT) {
                 base = __shfl(base, leader, 64);
-                if (sv)
-                    A.ent[base + __popcll(mask & ((1ull << lane) - 1))] =
-                        j | ((uint32_t)a1 << 30) | ((uint32_t)a2 << 31);
+                const uint64_t e = (uint64_t)base + __popcll(mask & ((1ull << lane) - 1));
+                if (sv && e < A.ent_cap) A.ent[e] = j | ((uint32_t)a1 << 30) | ((uint32_t)a2 << 31);
             }
         }
     };
@@ -850,6 +850,7 @@ __global__ __launch_bounds__(256) void k_ed_qg_scatter(EdQgArgs A, uint32_t n_re
         pre[lane] = inc - c;
     }
     __syncthreads();
+    if (A.abort && *A.abort) return;  // the search's sizes differ from the cached ones: write nothing
     const uint32_t nw = gridDim.x * 4;
     for (uint32_t g0 = blockIdx.x * 4 + (threadIdx.x >> 6); g0 < n_rec; g0 += nw) {
         uint32_t lo = 0;  // the last stripe whose prefix is <= g0 (empty stripes share their successor's prefix)
@@ -865,10 +866,9 @@ __global__ __launch_bounds__(256) void k_ed_qg_scatter(EdQgArgs A, uint32_t n_re
             base = A.poff[h.x] + atomicSub(&A.cnt[h.x], c) - c;
         }
         base = __shfl(base, 0, 64);
-        const uint64_t bit = 1ull << lane;
-        if (mask & bit)
-            A.ent[base + __popcll(mask & (bit - 1))] =
-                (h.y + lane) | ((uint32_t)((m1 & bit) != 0) << 30) | ((uint32_t)((m2 & bit) != 0) << 31);
+        const uint64_t bit = 1ull << lane, e = (uint64_t)base + __popcll(mask & (bit - 1));
+        if ((mask & bit) && e < A.ent_cap)
+            A.ent[e] = (h.y + lane) | ((uint32_t)((m1 & bit) != 0) << 30) | ((uint32_t)((m2 & bit) != 0) << 31);
     }
 }
 
@@ -896,12 +896,14 @@ template <int W, bool CMP>
 __global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv_dp(EdBvArgs A, const uint32_t *__restrict__ ioff,
                                                                 const uint32_t *__restrict__ poff,
                                                                 const uint32_t *__restrict__ ent, uint32_t n_pairs,
-                                                                uint32_t n_items, uint32_t item) {
+                                                                uint32_t n_items, uint32_t item,
+                                                                const uint32_t *__restrict__ abort) {
     extern __shared__ uint32_t peq[];
     uint32_t &pool_next = peq[A.lds_dw];
     const uint32_t nblk = gridDim.x, per_xcd = nblk / 8;
     const uint32_t lb = (blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
     if (lb >= n_items) return;
+    if (abort && *abort) return;  // sizes from a cache that this search's totals contradict: no DP over them
     uint32_t lo = 0, hi = n_pairs;
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) / 2;
@@ -942,12 +944,14 @@ __global__ __launch_bounds__(256) NMZ_ED_BV_ATTR void k_ed_bv_dp(EdBvArgs A, con
 }
 
 int ed_bv_dp_launch(const EdBvArgs &A, const uint32_t *ioff, const uint32_t *poff, const uint32_t *ent,
-                    uint32_t n_pairs, uint32_t n_items, uint32_t item, uint32_t bw, bool cmp, hipStream_t st) {
+                    uint32_t n_pairs, uint32_t n_items, uint32_t item, uint32_t bw, bool cmp, hipStream_t st,
+                    const uint32_t *abort) {
     if (n_items == 0) return NMZ_OK;
     const unsigned blocks = (n_items + 7) / 8 * 8;  // a multiple of 8 for the XCD remap
     const size_t lds = (size_t)A.lds_dw * 4 + 16;
 #define NMZ_DP(Wv, C) \
-    hipLaunchKernelGGL((k_ed_bv_dp<Wv, C>), dim3(blocks), dim3(256), lds, st, A, ioff, poff, ent, n_pairs, n_items, item)
+    hipLaunchKernelGGL((k_ed_bv_dp<Wv, C>), dim3(blocks), dim3(256), lds, st, A, ioff, poff, ent, n_pairs, n_items, \
+                       item, abort)
     switch (bw * 2 + (cmp ? 1 : 0)) {
         case 16: NMZ_DP(8, false); break;
         case 17: NMZ_DP(8, true); break;

@@ -14,10 +14,21 @@
 // deal (nmz_ed_allpairs_knn_shard_dev: rotated snake order, nmz_ed_block_shard). Each rank merges its shards' results on its device, one RCCL all_gather
 // over xGMI exchanges the ranks' lists (k x 24 B top-k, or N x k x 8 B k-NN keys), and a deterministic merge
 // -- (n_fault desc, sum_delay desc, seed asc) / (dist asc, id asc) -- gives every rank the same result.
+//
+// No rank may leave the others waiting in a collective. Every group call therefore runs its local steps (plan
+// builds, shard sweeps, list merges) with their status recorded rather than returned, then enters one small status
+// all_gather (group_agree_status) that every rank always enters, and only when every rank succeeded the payload
+// collective. The status exchange itself cannot fail before its collective: its device and pinned host buffers are
+// allocated when the group opens, and a rank whose staging copy fails leaves the failure sentinel (all ones) that
+// its send buffer holds between exchanges, so its peers read a failure. NMZ_GROUP_FAIL (an A/B test knob, read only
+// with NMZ_AB=1) injects a local failure at one step -- "sweep", "topk", "ed_search" or "exchange" -- on the rank
+// NMZ_GROUP_FAIL_RANK (default 0), and nmz_group_collectives counts the collectives this process entered, so a test
+// checks that a failed call keeps the collective sequence in step.
 #include <rccl/rccl.h>
 
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -81,12 +92,19 @@ class DeviceWorker {
     std::thread th_;  // last: started after the members above exist
 };
 
+// words per rank of the status / fingerprint exchange (a status word + nmz_ed_plan_fingerprint's words)
+constexpr size_t XW_WORDS = 1 + NMZ_ED_FP_WORDS;
+
 struct GroupMember {
     nmz_ctx *ctx = nullptr;
     int rank = 0;
     ncclComm_t comm = nullptr;
     std::unique_ptr<DeviceWorker> worker;
     DevBuf buf[4];  // group scratch on this device: [0] exchange (send | recv), [1] merge scratch, [2] shard outputs
+    // the status exchange, allocated at group open: device send [XW_WORDS] | recv [n_ranks][XW_WORDS], and pinned
+    // host staging of the same layout
+    DevBuf xw;
+    uint64_t *xw_host = nullptr;
 };
 
 }  // namespace nmz
@@ -98,6 +116,7 @@ struct nmz_group {
     bool multi_process = false;
     std::mutex mu;        // group calls are serialised (their contexts and scratch are the group's own)
     uint32_t n_plans = 0;  // live group plans (nmz_close_group refuses to free a group they still use)
+    uint64_t n_coll = 0;   // collectives this process has entered (nmz_group_collectives)
 };
 
 namespace nmz {
@@ -144,6 +163,7 @@ static std::pair<uint64_t, uint64_t> shard_range(uint64_t total, uint32_t n, uin
 // members' streams (ordered after the work that filled send). One RCCL group call covers every local device.
 static int group_allgather(nmz_group *g, const std::vector<void *> &send, const std::vector<void *> &recv,
                            size_t bytes) {
+    ++g->n_coll;
     NMZ_NCCL(ncclGroupStart());
     for (size_t i = 0; i < g->m.size(); ++i) {
         GroupMember &mb = g->m[i];
@@ -161,35 +181,61 @@ static int group_allgather(nmz_group *g, const std::vector<void *> &send, const 
     return NMZ_OK;
 }
 
-// Every member's `words` u64 (its local status first) to every member, rank order: one small RCCL all_gather that a
-// member which failed locally still enters, so no rank is left waiting in a collective another rank skipped.
-// all[i] = [n_ranks][words] as member i received it.
+// NMZ_GROUP_FAIL=<step> (with NMZ_AB=1): member `mb` fails locally at `step` when it is rank NMZ_GROUP_FAIL_RANK
+static int injected(const GroupMember &mb, const char *step) {
+    const char *e = ab_env("NMZ_GROUP_FAIL");
+    if (!e || std::strcmp(e, step) != 0) return NMZ_OK;
+    const char *r = ab_env("NMZ_GROUP_FAIL_RANK");
+    if ((r ? atoi(r) : 0) != mb.rank) return NMZ_OK;
+    return fail(NMZ_EHIP, std::string("injected failure at ") + step + " (NMZ_GROUP_FAIL) on rank " +
+                              std::to_string(mb.rank));
+}
+
+// Every member's `words` u64 (its local status first) to every member, rank order: one small RCCL all_gather that
+// every member always enters (its buffers were allocated at group open), so no rank is left waiting in a collective
+// another rank skipped. A member whose staging copy fails still enters: its send buffer holds the failure sentinel
+// (all ones, re-armed after every exchange), which its peers read as a failed status. all[i] = [n_ranks][words] as
+// member i received it; the first local failure is returned after the collective.
 static int group_exchange_words(nmz_group *g, const std::vector<std::vector<uint64_t>> &mine, size_t words,
                                 std::vector<std::vector<uint64_t>> &all) {
     const size_t R = (size_t)g->n_ranks, n = g->m.size();
-    std::vector<DevBuf> buf(n);
+    if (words > XW_WORDS) return fail(NMZ_EINVAL, "status exchange too wide");  // a static property of the callers
     std::vector<void *> send(n), recv(n);
-    all.assign(n, std::vector<uint64_t>(R * words, 0));
-    int rc = run_all(g, [&](size_t i) {
-        NMZ_TRY(buf[i].ensure(Carve::bytes_for(words, 8) + Carve::bytes_for(R * words, 8)));
-        Carve cv(buf[i].ptr);
-        send[i] = cv.take<uint64_t>(words);
-        recv[i] = cv.take<uint64_t>(R * words);
-        NMZ_HIP(hipMemcpy(send[i], mine[i].data(), words * 8, hipMemcpyHostToDevice));
+    std::vector<int> lrc(n, NMZ_OK);
+    std::vector<std::string> lmsg(n);
+    all.assign(n, std::vector<uint64_t>(R * words, UINT64_MAX));
+    (void)run_all(g, [&](size_t i) {
+        GroupMember &mb = g->m[i];
+        send[i] = mb.xw.as<uint64_t>();
+        recv[i] = mb.xw.as<uint64_t>() + XW_WORDS;
+        std::memcpy(mb.xw_host, mine[i].data(), words * 8);
+        int rc = injected(mb, "exchange");
+        if (rc == NMZ_OK && hipMemcpyAsync(send[i], mb.xw_host, words * 8, hipMemcpyHostToDevice, mb.ctx->stream) !=
+                                hipSuccess)
+            rc = fail(NMZ_EHIP, "staging the status exchange failed");
+        if (rc != NMZ_OK) {
+            lrc[i] = rc;
+            lmsg[i] = nmz_last_error();
+        }
         return NMZ_OK;
     });
-    if (rc == NMZ_OK) rc = group_allgather(g, send, recv, words * 8);
-    if (rc == NMZ_OK)
+    int rc = group_allgather(g, send, recv, words * 8);
+    std::string msg = rc == NMZ_OK ? std::string() : std::string(nmz_last_error());
+    if (rc == NMZ_OK) {
         rc = run_all(g, [&](size_t i) {
-            NMZ_HIP(hipMemcpyAsync(all[i].data(), recv[i], R * words * 8, hipMemcpyDeviceToHost, g->m[i].ctx->stream));
-            NMZ_HIP(hipStreamSynchronize(g->m[i].ctx->stream));
+            GroupMember &mb = g->m[i];
+            hipStream_t st = mb.ctx->stream;
+            uint64_t *h = mb.xw_host + XW_WORDS;
+            NMZ_HIP(hipMemcpyAsync(h, recv[i], R * words * 8, hipMemcpyDeviceToHost, st));
+            NMZ_HIP(hipMemsetAsync(send[i], 0xff, XW_WORDS * 8, st));  // re-arm the sentinel for the next exchange
+            NMZ_HIP(hipStreamSynchronize(st));
+            std::memcpy(all[i].data(), h, R * words * 8);
             return NMZ_OK;
         });
-    const std::string msg = rc == NMZ_OK ? std::string() : std::string(nmz_last_error());
-    (void)run_all(g, [&](size_t i) {
-        buf[i].release();
-        return NMZ_OK;
-    });
+        if (rc != NMZ_OK) msg = nmz_last_error();
+    }
+    for (size_t i = 0; i < n; ++i)
+        if (lrc[i] != NMZ_OK) return fail(lrc[i], lmsg[i]);
     return rc == NMZ_OK ? NMZ_OK : fail(rc, msg);
 }
 
@@ -199,13 +245,28 @@ static int group_agree_status(nmz_group *g, const std::vector<int> &st, const st
                               const char *what) {
     std::vector<std::vector<uint64_t>> mine(g->m.size()), all;
     for (size_t i = 0; i < g->m.size(); ++i) mine[i] = {(uint64_t)(int64_t)st[i]};
-    NMZ_TRY(group_exchange_words(g, mine, 1, all));
+    const int xrc = group_exchange_words(g, mine, 1, all);
     for (size_t i = 0; i < g->m.size(); ++i)
         if (st[i] != NMZ_OK) return fail(st[i], msg[i]);
+    if (xrc != NMZ_OK) return xrc;
     for (size_t r = 0; r < all[0].size(); ++r)
         if (all[0][r] != 0)
-            return fail((int)(int64_t)all[0][r], std::string(what) + " failed on rank " + std::to_string(r));
+            return fail(all[0][r] == UINT64_MAX ? NMZ_EHIP : (int)(int64_t)all[0][r],
+                        std::string(what) + " failed on rank " + std::to_string(r));
     return NMZ_OK;
+}
+
+// runs fn(member index) on every member and records its status instead of returning it (the call continues to
+// the status agreement whatever happened locally)
+static void run_all_local(nmz_group *g, std::vector<int> &st, std::vector<std::string> &msg,
+                          const std::function<int(size_t)> &fn) {
+    st.assign(g->m.size(), NMZ_OK);
+    msg.assign(g->m.size(), std::string());
+    (void)run_all(g, [&](size_t i) {
+        st[i] = fn(i);
+        if (st[i] != NMZ_OK) msg[i] = nmz_last_error();
+        return NMZ_OK;
+    });
 }
 
 // the member whose copy of a merged result goes to the host: every rank of a multi-process group returns
@@ -218,6 +279,13 @@ static int group_init_member(nmz_group *g, int device, int rank) {
     mb.rank = rank;
     mb.worker.reset(new DeviceWorker(device));
     g->m.push_back(std::move(mb));
+    // the status exchange's buffers, armed with the failure sentinel
+    GroupMember &m = g->m.back();
+    const size_t bytes = (1 + (size_t)g->n_ranks) * XW_WORDS * 8;
+    NMZ_HIP(hipSetDevice(device));
+    NMZ_TRY(m.xw.ensure(bytes));
+    NMZ_HIP(hipHostMalloc((void **)&m.xw_host, bytes, hipHostMallocDefault));
+    NMZ_HIP(hipMemset(m.xw.ptr, 0xff, XW_WORDS * 8));
     return NMZ_OK;
 }
 
@@ -227,6 +295,8 @@ static void group_free(nmz_group *g) {
             (void)hipSetDevice(mb.ctx->device);
             (void)hipDeviceSynchronize();
             for (DevBuf &b : mb.buf) b.release();
+            mb.xw.release();
+            if (mb.xw_host) (void)hipHostFree(mb.xw_host);
         }
         if (mb.comm) (void)ncclCommDestroy(mb.comm);
         mb.worker.reset();
@@ -236,14 +306,20 @@ static void group_free(nmz_group *g) {
 }
 
 // ---- top-k exchange shared by both sweeps -------------------------------------------------------------
-// Member i has written its shards' top-k lists ([n_local][k] at lists_i); merge them into one list, all_gather
-// the ranks' lists, merge those into the final k and copy it to `topk` (host).
+// Member i has written its shards' top-k lists ([n_local][k] at lists_i) unless its sweep failed (st[i]); merge
+// them into one list, agree on every rank's status, all_gather the ranks' lists, merge those into the final k and
+// copy it to `topk` (host).
 static int group_topk_exchange(nmz_group *g, uint32_t k, const std::vector<nmz_topk_entry *> &lists,
-                               const std::vector<uint32_t> &n_local, nmz_topk_entry *topk) {
+                               const std::vector<uint32_t> &n_local, nmz_topk_entry *topk,
+                               const std::vector<int> &sweep_st, const std::vector<std::string> &sweep_msg) {
     const size_t R = (size_t)g->n_ranks;
     std::vector<void *> send(g->m.size()), recv(g->m.size());
-    NMZ_TRY(run_all(g, [&](size_t i) {
+    std::vector<int> st2;
+    std::vector<std::string> msg2;
+    run_all_local(g, st2, msg2, [&](size_t i) {
+        if (sweep_st[i] != NMZ_OK) return fail(sweep_st[i], sweep_msg[i]);  // the sweep failed here: nothing to merge
         GroupMember &mb = g->m[i];
+        NMZ_TRY(injected(mb, "topk"));
         const size_t lb = Carve::bytes_for(k, sizeof(nmz_topk_entry));
         NMZ_TRY(mb.buf[0].ensure(lb + Carve::bytes_for(R * k, sizeof(nmz_topk_entry))));
         NMZ_TRY(mb.buf[1].ensure(Carve::bytes_for(std::max<size_t>(R, n_local[i]) * k + k, sizeof(nmz_topk_entry))));
@@ -260,7 +336,8 @@ static int group_topk_exchange(nmz_group *g, uint32_t k, const std::vector<nmz_t
             return NMZ_OK;
         }
         return topk_merge_lists(st, lists[i], mb.buf[1].as<nmz_topk_entry>(), n_local[i], k, s);
-    }));
+    });
+    NMZ_TRY(group_agree_status(g, st2, msg2, "the sweep"));
     NMZ_TRY(group_allgather(g, send, recv, (size_t)k * sizeof(nmz_topk_entry)));
     return run_all(g, [&](size_t i) {
         if (!reports(g, i)) return NMZ_OK;
@@ -323,8 +400,11 @@ static int group_sweep(nmz_group *g, uint64_t n_seeds, uint32_t k, nmz_sched_sta
     NMZ_CHECK(k == 0 || topk, "topk is NULL");
     std::vector<nmz_topk_entry *> lists(g->m.size());
     std::vector<uint32_t> n_local(g->m.size());
-    NMZ_TRY(run_all(g, [&](size_t i) {
+    std::vector<int> st;
+    std::vector<std::string> msg;
+    run_all_local(g, st, msg, [&](size_t i) {
         GroupMember &mb = g->m[i];
+        NMZ_TRY(injected(mb, "sweep"));
         const std::vector<uint32_t> mine = shards_of(g, mb.rank);
         n_local[i] = (uint32_t)mine.size();
         uint64_t mx = 0;
@@ -347,9 +427,13 @@ static int group_sweep(nmz_group *g, uint64_t n_seeds, uint32_t k, nmz_sched_sta
             }
         }
         return NMZ_OK;
-    }));
-    if (k == 0) return NMZ_OK;
-    return group_topk_exchange(g, k, lists, n_local, topk);
+    });
+    if (k == 0) {  // no collective: each rank reports its own shards
+        for (size_t i = 0; i < st.size(); ++i)
+            if (st[i] != NMZ_OK) return fail(st[i], msg[i]);
+        return NMZ_OK;
+    }
+    return group_topk_exchange(g, k, lists, n_local, topk, st, msg);
 }
 
 static int group_merge_knn(GroupMember &mb, uint64_t *parts, uint32_t n_parts, uint32_t N, uint32_t k,
@@ -459,6 +543,12 @@ int nmz_close_group(nmz_group *g) {
         NMZ_CHECK(g->n_plans == 0, "the group still has live plans: destroy them before closing the group");
     }
     group_free(g);
+    return NMZ_OK;
+}
+
+int nmz_group_collectives(const nmz_group *g, uint64_t *n) {
+    NMZ_CHECK(g && n, "NULL argument");
+    *n = g->n_coll;
     return NMZ_OK;
 }
 
@@ -801,9 +891,12 @@ int nmz_ed_group_allpairs_knn(nmz_ed_group_plan *gp, uint32_t k, uint32_t *knn_i
     const size_t R = (size_t)g->n_ranks;
     std::vector<void *> send(g->m.size()), recv(g->m.size());
     std::vector<uint64_t *> tmp(g->m.size());
-    // 1. each rank's shards into partial lists, merged into its send list
-    NMZ_TRY(run_all(g, [&](size_t i) {
+    // 1. each rank's shards into partial lists, merged into its send list (status recorded, then agreed on)
+    std::vector<int> lst;
+    std::vector<std::string> lmsg;
+    run_all_local(g, lst, lmsg, [&](size_t i) {
         GroupMember &mb = g->m[i];
+        NMZ_TRY(injected(mb, "ed_search"));
         const std::vector<uint32_t> mine = shards_of(g, mb.rank);
         const uint64_t nl = std::max<size_t>(mine.size(), 1);
         NMZ_TRY(mb.buf[0].ensure(Carve::bytes_for(nk, 8) * (1 + R)));
@@ -821,8 +914,10 @@ int nmz_ed_group_allpairs_knn(nmz_ed_group_plan *gp, uint32_t k, uint32_t *knn_i
         }
         for (size_t j = 0; j < mine.size(); ++j)
             NMZ_TRY(nmz_ed_allpairs_knn_shard_dev(gp->p[i], k, mine[j], g->n_shards, parts + j * nk, nullptr));
+        NMZ_TRY(ed_tp_flag_check(gp->p[i], true, st));  // a search whose sizes contradicted its cache fails here
         return group_merge_knn(mb, parts, (uint32_t)mine.size(), N, k, (uint64_t *)send[i], tmp[i]);
-    }));
+    });
+    NMZ_TRY(group_agree_status(g, lst, lmsg, "the edit-distance search"));
     // 2. the ranks' lists to every rank (RCCL over xGMI)
     NMZ_TRY(group_allgather(g, send, recv, nk * 8));
     // 3. merge + complete (band + 1 for the pairs no shard listed) + split into ids and distances

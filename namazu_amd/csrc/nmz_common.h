@@ -44,6 +44,7 @@ struct DevBuf {
     void *ptr = nullptr;
     size_t cap = 0;
     std::vector<DevBuf> *pool = nullptr;
+    uint64_t gen = 0;  // bumped whenever ensure() hands out a different allocation (its contents are then undefined)
     int ensure(size_t bytes);
     void release();
     template <typename T>

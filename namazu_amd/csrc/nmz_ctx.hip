@@ -59,6 +59,7 @@ void HostPin::release() {
 
 int DevBuf::ensure(size_t bytes) {
     if (bytes <= cap) return NMZ_OK;
+    ++gen;
     // a pooled buffer that grows goes back to the pool, where the next plan of this context may take it and
     // memset / upload into it on another stream: kernels of earlier calls that still read it must be done
     // (unpooled buffers are released with hipFree, which synchronises by itself)

@@ -113,12 +113,21 @@ struct EdQgArgs {
     uint64_t n_tiles;
     uint32_t N, k, QB, NCB, shard, n_shards;
     uint32_t w;                  // band
+    // write pass: the entry lists' capacity, and a device flag that, when set, makes the write pass (and the DP,
+    // ed_bv_dp_launch's `abort`) skip: a search enqueued with a shard's cached sizes whose own totals differ
+    // (k_tp_scan sets it) must not write past lists sized for the cached totals
+    uint64_t ent_cap;
+    const uint32_t *abort;
 };
 constexpr uint32_t ED_REC_STRIPES = 64, ED_REC_LINE = 32;
+// the two-phase search's cached-size mismatch flag (ed.hip): wait = synchronise `st` and read it; otherwise read the
+// last search's pinned copy if it has landed. Fails (and resets the flag and the cache) when it is set.
+int ed_tp_flag_check(nmz_ed_plan *p, bool wait, hipStream_t st);
 int ed_qg_filter_launch(const EdQgArgs &A, bool count, hipStream_t st);
 int ed_qg_scatter_launch(const EdQgArgs &A, uint32_t n_rec, hipStream_t st);
 int ed_bv_dp_launch(const EdBvArgs &A, const uint32_t *ioff, const uint32_t *poff, const uint32_t *ent,
-                    uint32_t n_pairs, uint32_t n_items, uint32_t item, uint32_t bw, bool cmp, hipStream_t st);
+                    uint32_t n_pairs, uint32_t n_items, uint32_t item, uint32_t bw, bool cmp, hipStream_t st,
+                    const uint32_t *abort = nullptr);
 // single-query search on a bit-parallel plan (ed_bv.hip k_ed_bv_query): 1-2 external queries vs every stored trace
 struct EdBvQueryArgs {
     const uint16_t *bsym;  // the plan's stored streams

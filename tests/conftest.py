@@ -12,9 +12,18 @@ def pytest_configure(config):
 
 
 @pytest.fixture(autouse=True)
-def _ab_knobs(monkeypatch):
-    """The library reads its NMZ_* A/B and test knobs only under NMZ_AB=1 (csrc ab_env); the tests that set a knob
-    need it. tests/test_ed_gpu.py::test_knobs_need_nmz_ab checks that without it a knob changes nothing."""
+def _production_env(monkeypatch):
+    """Every test starts from a production environment: no NMZ_* variable from the caller's shell reaches the
+    library (the A/B and test knobs, csrc ab_env, are read only under NMZ_AB=1, and NMZ_REPLAY_SEED changes
+    Replayable.LoadConfig)."""
+    for k in [k for k in os.environ if k.startswith("NMZ_")]:
+        monkeypatch.delenv(k)
+
+
+@pytest.fixture
+def ab_knobs(monkeypatch):
+    """NMZ_AB=1 for a test that sets an A/B or test knob (the library ignores the knobs without it;
+    tests/test_ed_gpu.py::test_knobs_need_nmz_ab checks that)."""
     monkeypatch.setenv("NMZ_AB", "1")
 
 

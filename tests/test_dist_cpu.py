@@ -128,7 +128,7 @@ def test_merge_topk_is_order_independent():
 
 
 @pytest.mark.parametrize("deal", [None, "snake", "hash"])
-def test_ed_pair_dealing_matches_library(monkeypatch, deal):
+def test_ed_pair_dealing_matches_library(ab_knobs, monkeypatch, deal):
     """dist.ed_block_shard restates the library's dealing rule (csrc/ed.hip ed_block_shard; host-only entry point).
     The rule is fixed: the round-3 A/B knobs (NMZ_ED_DEAL, NMZ_ED_DEAL_UNIT) set in a process's environment change
     nothing, so ranks with different environments still deal the same blocks (a rank that dealt differently would

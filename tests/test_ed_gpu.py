@@ -42,7 +42,7 @@ def test_knn_fast_kernel(ctx, n, lmin, lmax, w, mut, k):
 
 
 @pytest.mark.parametrize("pool", [256, 2048, 4096])
-def test_knn_bv_pool_sizes(ctx, monkeypatch, pool):
+def test_knn_bv_pool_sizes(ab_knobs, ctx, monkeypatch, pool):
     """k_ed_bv workgroups own pools of 256..4096 candidates (the plan picks 4096 for N >= 24576);
     forced here on a smaller N with short ragged traces, vs the oracle."""
     monkeypatch.setenv("NMZ_ED_POOL", str(pool))
@@ -450,7 +450,7 @@ def test_search_similar_on_storage_uses_resident_index(ctx, tmp_path):
     assert st.SearchSimilar(t3, 2, 8)[0] == (3, 0) and st._index is first  # reused, not rebuilt
 
 
-def test_device_and_host_plan_builds_agree(ctx, monkeypatch):
+def test_device_and_host_plan_builds_agree(ab_knobs, ctx, monkeypatch):
     """Stores of >= 2^20 symbols build the bit-parallel plan on the device (sort/unique + binary-search remap);
     NMZ_ED_HOST_REMAP forces the host build. Both give the oracle's k-NN lists and the same single-query answers
     (the query dictionary comes from the device's sorted symbols)."""
@@ -472,7 +472,7 @@ def test_device_and_host_plan_builds_agree(ctx, monkeypatch):
         assert ds_d[q].tolist() == d[order].tolist() and ids_d[q].tolist() == pairs[order, 1].tolist()
 
 
-def test_device_plan_symbols_zero_and_all_ones(ctx, monkeypatch):
+def test_device_plan_symbols_zero_and_all_ones(ab_knobs, ctx, monkeypatch):
     """The device plan's distinct-symbol set (an LDS + global hash set, csrc/unique.hip) keeps 0 and 2^64 - 1 (its
     free-slot value) as symbols like any other: same k-NN lists as the host build and the oracle."""
     rng = np.random.default_rng(78)
@@ -497,7 +497,7 @@ def test_device_plan_symbols_zero_and_all_ones(ctx, monkeypatch):
         assert ds_d[q].tolist() == d[order].tolist() and ids_d[q].tolist() == pairs[order, 1].tolist()
 
 
-def test_wide_device_and_host_plan_builds_agree(ctx, monkeypatch):
+def test_wide_device_and_host_plan_builds_agree(ab_knobs, ctx, monkeypatch):
     """Wide-band stores of >= 2^20 symbols build k_ed_wide's plan on the device (hash-set alphabet + remap kernel,
     ids by sorted rank instead of first appearance); NMZ_ED_HOST_REMAP forces the host build. Same k-NN lists,
     and the oracle's for sampled queries."""
@@ -556,7 +556,7 @@ def _edited_family(n, length, alphabet, max_edits, rng):
 
 @pytest.mark.parametrize("recompute", [False, True])
 @pytest.mark.parametrize("w,alphabet,max_edits", [(32, 48, 90), (16, 6, 40), (8, 200, 25)])
-def test_knn_qgram_filter_exact(ctx, monkeypatch, w, alphabet, max_edits, recompute):
+def test_knn_qgram_filter_exact(ab_knobs, ctx, monkeypatch, w, alphabet, max_edits, recompute):
     """The q-gram lower bound (bigram profiles > 4w apart => ED_w = w + 1 without a DP) and the in-band-only
     publishing + k_knn_fill: the all-pairs k-NN equals the oracle's and the run with the filter off, the counters
     show pairs settled by the bound and pairs that ran the DP, and the shard path (merge + fill) agrees too. The
@@ -611,7 +611,7 @@ def test_knn_qgram_filter_exact(ctx, monkeypatch, w, alphabet, max_edits, recomp
 
 
 @pytest.mark.parametrize("limit", [0, 1, 500, "mid"])
-def test_knn_two_phase_entry_limit_batches(ctx, monkeypatch, limit):
+def test_knn_two_phase_entry_limit_batches(ab_knobs, ctx, monkeypatch, limit):
     """Entry lists beyond the two-phase limit (2^30 entries; NMZ_ED_TP_MAX_ENTRIES lowers it) run in batches of
     whole query blocks after the count pass (csrc/ed.hip ed_bv_two_phase). The count pass lists pairs with an empty
     trace before the total is known, so the batches must start from empty lists: near-duplicates with empty traces
@@ -717,7 +717,7 @@ def test_knn_compact_tables_5000_symbol_store(ctx):
 
 
 @pytest.mark.parametrize("w", [8, 21, 32, 64])
-def test_knn_compact_tables_forced(ctx, monkeypatch, w):
+def test_knn_compact_tables_forced(ab_knobs, ctx, monkeypatch, w):
     """NMZ_ED_COMPACT forces the compact tables on a small-alphabet store: the same lists as the direct tables
     and the oracle, through the two-phase search, the single-kernel search (NMZ_ED_TWO_PHASE=0) and both plan
     builds (device: >= 2^20 symbols; NMZ_ED_HOST_REMAP: host)."""
@@ -892,3 +892,64 @@ def test_two_phase_offset_kernels(ctx, n, item, big):
     assert np.array_equal(d_poff.cpu().numpy().view(np.uint32), (exp_p & 0xFFFFFFFF).astype(np.uint32))
     assert np.array_equal(d_ioff.cpu().numpy().view(np.uint32), (exp_i & 0xFFFFFFFF).astype(np.uint32))
     assert int(d_tot.cpu().numpy().view(np.uint64)[0]) == int(exp_p[-1])
+
+
+def test_cached_size_mismatch_skips_writes_and_surfaces(ab_knobs, ctx, monkeypatch):
+    """A shard's later searches run with the sizes its first search read back (csrc/ed.hip ed_bv_two_phase); a
+    one-thread check flags a search whose own totals differ. NMZ_ED_TP_FAKE_MISMATCH forces the flag on a cached
+    search: that search writes no entry and runs no DP (nothing past the lists sized for the cached totals), the
+    shard's next search reports it (NMZ_EHIP) and drops the cache, and the search after that is whole again and
+    equals the oracle. nmz_ed_plan_counters reports a pending flag too."""
+    import torch
+    L = _lib.load()
+    ts = _edited_family(300, 150, 16, 30, np.random.default_rng(21))
+    n, k, w = len(ts), 8, 32
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, w, k, nthreads=16)
+    plan = ctypes.c_void_p()
+    _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), n, w, ctypes.byref(plan)))
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    keys = torch.empty(n * k, dtype=torch.int64, device="cuda")
+
+    def search():
+        rc = L.nmz_ed_allpairs_knn_shard_dev(plan, k, 0, 1, ctypes.c_void_p(keys.data_ptr()), stream)
+        torch.cuda.synchronize()
+        return rc
+
+    def lists():
+        out = torch.empty_like(keys)
+        out.copy_(keys)
+        torch.cuda.synchronize()  # the copy (torch's stream) before the fill (the context's stream)
+        _lib.check(L.nmz_ed_knn_fill_dev(plan, k, ctypes.c_void_p(out.data_ptr()), stream))
+        torch.cuda.synchronize()
+        kk = out.cpu().numpy().view(np.uint64).reshape(n, k)
+        return (kk & np.uint64(0xFFFFFFFF)).astype(np.uint32), (kk >> np.uint64(32)).astype(np.uint32)
+
+    try:
+        assert L.nmz_ed_plan_is_fast(plan) == 2
+        for _ in range(2):  # the first search reads its sizes back, the second runs from the cache
+            assert search() == _lib.NMZ_OK
+            ids, ds = lists()
+            assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+        monkeypatch.setenv("NMZ_ED_TP_FAKE_MISMATCH", "1")
+        assert search() == _lib.NMZ_OK  # enqueued with the cached sizes; the check flags it on the device
+        monkeypatch.delenv("NMZ_ED_TP_FAKE_MISMATCH")
+        ids, ds = lists()
+        assert not (np.array_equal(ids, oi) and np.array_equal(ds, od))  # the flagged search ran no DP
+        cnt = np.zeros(_lib.NMZ_ED_NCOUNTERS, np.uint64)
+        assert L.nmz_ed_plan_counters(plan, _lib.ptr(cnt), stream) == _lib.NMZ_EHIP
+        assert "cached sizes" in _lib.last_error()
+        _lib.check(L.nmz_ed_plan_counters(plan, _lib.ptr(cnt), stream))  # reported once, then clear
+        for _ in range(2):  # recounted (the cache was dropped), then cached again
+            assert search() == _lib.NMZ_OK
+            ids, ds = lists()
+            assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+        # the non-waiting report: the shard's next search fails with the flag of the previous one
+        monkeypatch.setenv("NMZ_ED_TP_FAKE_MISMATCH", "1")
+        assert search() == _lib.NMZ_OK
+        monkeypatch.delenv("NMZ_ED_TP_FAKE_MISMATCH")
+        assert search() == _lib.NMZ_EHIP
+        assert search() == _lib.NMZ_OK
+        ids, ds = lists()
+        assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+    finally:
+        L.nmz_ed_plan_destroy(plan)

@@ -213,3 +213,66 @@ def test_group_rejects_bad_arguments():
     h = ctypes.c_void_p()
     assert L.nmz_open_group(0, 0, ctypes.byref(h)) == _lib.NMZ_EINVAL  # no device
     assert L.nmz_open_group(1 << 31, 0, ctypes.byref(h)) == _lib.NMZ_EINVAL  # no such device
+
+
+def _collectives(g):
+    n = ctypes.c_uint64()
+    _lib.check(g.L.nmz_group_collectives(g.handle, ctypes.byref(n)))
+    return n.value
+
+
+@pytest.mark.parametrize("where", ["sweep", "topk", "exchange", "ed_search"])
+@pytest.mark.parametrize("rank_form", [False, True])
+def test_group_failure_keeps_collectives_in_step(ab_knobs, monkeypatch, where, rank_form):
+    """A rank that fails locally still enters the status all_gather in front of every payload collective
+    (csrc/group.hip group_agree_status), so no peer waits in a collective it skipped. NMZ_GROUP_FAIL injects the
+    failure at one step: the call returns the injected error, it entered exactly the status collective (the one
+    its peers enter too; a healthy call enters the status collective and the payload all_gather), and the group's
+    next call succeeds with the oracle's result. For "exchange" the status exchange's own staging fails: the rank
+    still enters, and its send buffer's failure sentinel tells the peers."""
+    if rank_form:
+        g = G.Group((0,), n_shards=3, unique_id=G.Group.unique_id(), n_ranks=1, rank=0)
+    else:
+        g = G.Group((0,), n_shards=3)
+    try:
+        E, n, k = 256, 300, 8
+        rng = np.random.default_rng(11)
+        evhash = rng.integers(0, 2**64, size=E, dtype=np.uint64)
+        evclass = rng.integers(0, 4, size=E).astype(np.uint8)
+        params = _lib.resolve_random_params(30_000_000, 100_000_000, 0.1)
+        ost, _, _ = O.random_sweep(5, n, evhash, evclass, O.random_params(30_000_000, 100_000_000, 0.1), nthreads=16)
+        ts = _family(120, 100, 12, 30, 3)
+        oi, od = O.ed_allpairs_knn(ts.off, ts.sym, 16, k, nthreads=16)
+        p = G.RandomGroupPlan(g, evhash, evclass, params, max_seeds_per_shard=n)
+        e = G.EdGroupPlan(g, ts, 16)
+        try:
+            def call():
+                if where == "ed_search":
+                    return e.knn(k)
+                return p.sweep(5, n, k=k)
+
+            c0 = _collectives(g)
+            call()
+            healthy = _collectives(g) - c0
+            assert healthy == 2  # status agreement + payload all_gather
+            monkeypatch.setenv("NMZ_GROUP_FAIL", where)
+            c0 = _collectives(g)
+            with pytest.raises(_lib.NmzError, match="injected failure at " + where):
+                call()
+            assert _collectives(g) - c0 == 1  # the status all_gather only, as on every healthy peer
+            monkeypatch.setenv("NMZ_GROUP_FAIL_RANK", "1")  # another rank's knob: not this one
+            call()
+            monkeypatch.delenv("NMZ_GROUP_FAIL")
+            c0 = _collectives(g)
+            if where == "ed_search":
+                ids, ds = call()
+                assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+            else:
+                st, tk = call()
+                assert np.array_equal(st, ost) and np.array_equal(tk, O.topk_from_stats(ost, 5, k))
+            assert _collectives(g) - c0 == 2
+        finally:
+            p.close()
+            e.close()
+    finally:
+        g.close()

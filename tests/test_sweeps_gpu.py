@@ -27,7 +27,7 @@ def rep_oracle(seeds, hints, m, n_dump=0):
 
 # ---------------------------------------------------------------- K1
 @pytest.fixture(params=["wt", "wt_sep", "wt_bb7", "wt_bb5", "oq"])
-def k1(request, monkeypatch):
+def k1(ab_knobs, request, monkeypatch):
     """K1's two statistics kernels: wavelet trees (the default) and order queries (NMZ_REPLAY_WT=0 at plan
     creation); plans that neither fits take the per-decision sweep either way. "wt" builds the wavelet-tree plan
     with the fused plan kernel (it computes and C-sorts the correction table itself), "wt_sep" with the separate
@@ -47,7 +47,7 @@ def k1(request, monkeypatch):
     return request.param
 
 
-def test_replayable_plan_kernel_choice(ctx, monkeypatch):
+def test_replayable_plan_kernel_choice(ab_knobs, ctx, monkeypatch):
     """configs[1]-shaped traces take the wavelet-tree kernel (classes of 4,096 events or more as sub-segments);
     NMZ_REPLAY_WT=0 or a row image beyond LDS the order-query kernel; maxInterval >= 2^32 the per-decision sweep."""
     L = _lib.load()
@@ -202,7 +202,7 @@ def test_replayable_long_trace_multi_pass(ctx, k1, E, m):
 
 
 @pytest.mark.parametrize("budget,m", [(16384, 100_000_000), (30_000, 7), (60_000, 2**31 + 9)])
-def test_replayable_forced_passes(ctx, monkeypatch, budget, m):
+def test_replayable_forced_passes(ab_knobs, ctx, monkeypatch, budget, m):
     """NMZ_REPLAY_OQ_BUDGET shrinks the row-image budget so a 3,000-event trace runs as many passes over small
     sub-segments (and the rows' partial chunks accumulate across passes); results equal the oracle's."""
     monkeypatch.setenv("NMZ_REPLAY_OQ_BUDGET", str(budget))
@@ -358,7 +358,7 @@ def test_replayable_topk_large_sweep(ctx, E, m, k):
 
 
 @pytest.mark.parametrize("kind", ["csr", "decimal"])
-def test_replayable_seed_set(ctx, monkeypatch, kind):
+def test_replayable_seed_set(ab_knobs, ctx, monkeypatch, kind):
     """nmz_replayable_sweep_seeds_topk_dev over one prepared seed set (prefix hashes bucketed once) == the plain
     sweep of the same seeds, on every statistics path: wavelet trees (fused and separate plan builds), order
     queries, and the per-decision sweeps (maxInterval >= 2^32: the prepared hashes bucketed per sweep), stats and
