@@ -3,13 +3,17 @@
 
 Headline workload (BASELINE.json configs[1]): replayable-policy seed sweep,
 2^20 seeds x 4096-event ZooKeeper-style packet trace, maxInterval 100 ms, on
-each GPU (weak scaling: every rank sweeps its own 2^20 seeds per step; steps
-are pipelined over 3 plans / HIP streams, each slot with its own seed range,
-so one step's latency-bound kernels overlap the neighbouring steps). One step =
-  seed prefix hashing + bucketing + the K1 sweep (stats for every seed)
-  + per-rank top-64 selection (+ RCCL all_gather and merge when N > 1).
+each GPU (weak scaling: every rank sweeps 2^20 seeds per step). Step i sweeps a
+fresh range of decimal seeds, (i * N + rank) * 2^20 .., so no seed is swept
+twice; steps are pipelined over 3 plans / HIP streams so one step's
+latency-bound kernels overlap the neighbouring steps. One step =
+  seed prefix hashing (seed strings generated on the device) + bucketing +
+  the K1 sweep (stats for every seed) + that batch's top-64;
+after the last step, inside the timing: the device merge of the steps' top-64
+lists (+ RCCL all_gather and the host merge when N > 1).
 Inputs are resident in HBM before the timed region; the per-trace plan
-(correction tables) is built once, outside it.
+(correction tables) is built once, outside it. Defaults are the driver's
+settings (--steps 20 --warmup 5).
 
 Metric: schedule decisions/s (seeds x events / s), whole job.
 Also reported (same JSON line): the roofline of the dominant kernel
@@ -142,7 +146,8 @@ def roofline_valu(kernel, units, kernel_ms):
 HEADLINE_MAX_BYTES = 4096
 HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
                  "vs_baseline", "dtype", "data", "config")
-ROOFLINE_KEYS = ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic", "kernel_ms", "kernel_ms_source",
+ROOFLINE_KEYS = ("bound", "kernel", "achieved", "peak", "unit", "frac", "declared_model_frac",
+                 "declared_model_ops_per_unit", "traffic", "kernel_ms", "kernel_ms_source",
                  "ops_per_unit", "units_per_launch", "unit_kind", "frac_of_issue_ceiling", "frac_at_clock",
                  "clock_ghz", "kernel_ms_span", "kernel_ms_serial_span", "kernel_ms_events", "stale", "ops_source")
 CPU_KEYS = ("value", "unit", "cores", "kind", "sample", "parity_with_gpu", "seconds")
@@ -291,13 +296,17 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     S, E = args.seeds, args.events
     hints = zk_hints(E)
     hoff, hb = to_csr(hints)
-    # Consecutive steps are pipelined over NP plans and HIP streams (NMZ_BENCH_PIPELINE, default 3), each
-    # slot sweeping its own range of S seeds: the latency-bound kernels around one step's sweep (seed
-    # prefix, bucketing, merge, top-k) and the tail of its persistent sweep grid overlap the neighbouring
-    # steps. Every step does all of its work on its own batch.
+    # The job: K = args.steps batches of S fresh seeds per rank. Timed step i sweeps the decimal seeds
+    # (i * world + rank) * S .. + S - 1 (generated on the device: nmz_replayable_sweep_decimal_topk_dev, no seed
+    # CSR), so no step re-sweeps another's seeds; its top-64 goes to slot i of a [K][64] list buffer. After the last
+    # step one device merge (nmz_topk_merge_dev) gives the rank's top-64 of the whole job, (N > 1) one RCCL
+    # all_gather brings every rank's list, and the host merges them: all inside the timed region.
+    # Consecutive steps are pipelined over NP plans and HIP streams (NMZ_BENCH_PIPELINE, default 3): the
+    # latency-bound kernels around one step's sweep (seed prefix, bucketing, top-k) and the tail of its persistent
+    # sweep grid overlap the neighbouring steps. Every step does all of its work on its own batch.
     NP = max(1, int(os.environ.get("NMZ_BENCH_PIPELINE", "3")))
-    seed_lo = [(D.rank * NP + sp) * S for sp in range(NP)]
-    csr = [decimal_csr(lo, S) for lo in seed_lo]
+    K_TOP = 64
+    csr0 = decimal_csr(D.rank * S, S)  # timed step 0's seeds: the CPU baseline's sample and the end-to-end seeds
     plans = []
     t0 = time.time()
     for _ in range(NP):
@@ -309,94 +318,99 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     k1 = k1_kernel(L, plans[0])
     dev = torch.device("cuda", D.local_rank)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(NP - 1)]
-    d_soff = [torch.from_numpy(so.view(np.int32)).to(dev) for so, _ in csr]
-    d_sb = [torch.from_numpy(sb).to(dev) for _, sb in csr]
     d_stats = [torch.empty(S * 32, dtype=torch.uint8, device=dev) for _ in range(NP)]
-    K_TOP = 64
-    # per-slot top-k buffers: the RCCL all_gather of a step (async, on the process group's stream) overlaps
-    # the following steps; a slot is rewritten only after the gather that reads it has completed
-    d_topk = [torch.empty(K_TOP * 24, dtype=torch.uint8, device=dev) for _ in range(NP)]
-    gathered = [[torch.empty_like(d_topk[0]) for _ in range(D.world)] for _ in range(NP)] if D.world > 1 else None
-    pending = [None] * NP
-    it = [0]
+    n_lists = max(args.steps, 1)
+    d_lists = torch.empty(n_lists * K_TOP * 24, dtype=torch.uint8, device=dev)
+    d_scratch = torch.empty_like(d_lists)
+    d_job = torch.empty(K_TOP * 24, dtype=torch.uint8, device=dev)
+    gathered = [torch.empty_like(d_job) for _ in range(D.world)] if D.world > 1 else None
+    # seed ranges outside the job's for the untimed launches (warm-up, kernel timing)
+    spare_lo = (args.steps + 1) * D.world * S + D.rank * S
 
-    def step(sp=None):
-        if sp is None:
-            sp = it[0] % NP
-            it[0] += 1
+    def sweep(sp, lo, out_list):
         with torch.cuda.stream(streams[sp]):
-            if pending[sp] is not None:
-                pending[sp].wait()
-                pending[sp] = None
-            # sweep + top-k in one call
-            _lib.check(L.nmz_replayable_sweep_topk_dev(plans[sp], ctypes.c_void_p(d_soff[sp].data_ptr()),
-                                                       ctypes.c_void_p(d_sb[sp].data_ptr()), S, seed_lo[sp], K_TOP,
-                                                       ctypes.c_void_p(d_stats[sp].data_ptr()),
-                                                       ctypes.c_void_p(d_topk[sp].data_ptr()),
-                                                       ctypes.c_void_p(streams[sp].cuda_stream)))
-            if D.pg:
-                pending[sp] = D.pg.all_gather(gathered[sp], d_topk[sp], async_op=True)
+            _lib.check(L.nmz_replayable_sweep_decimal_topk_dev(plans[sp], lo, S, K_TOP,
+                                                               ctypes.c_void_p(d_stats[sp].data_ptr()),
+                                                               ctypes.c_void_p(out_list),
+                                                               ctypes.c_void_p(streams[sp].cuda_stream)))
 
-    def drain():
-        for sp in range(NP):
-            if pending[sp] is not None:
-                with torch.cuda.stream(streams[sp]):
-                    pending[sp].wait()
-                pending[sp] = None
+    def step(i):
+        sweep(i % NP, (i * D.world + D.rank) * S, d_lists.data_ptr() + (i % n_lists) * K_TOP * 24)
 
-    def outputs():
-        if D.pg:
-            return [t for g in gathered for t in g]
-        return list(d_topk)
+    def join():  # stream 0 waits for the other slots' work
+        for sp in range(1, NP):
+            streams[0].wait_stream(streams[sp])
 
-    for _ in range(max(args.warmup, NP)):
-        step()
-    drain()
+    for j in range(max(args.warmup, NP)):
+        sweep(j % NP, spare_lo, d_lists.data_ptr() + (j % n_lists) * K_TOP * 24)
+    join()
+    # the job merge's kernels and the host merge, once outside the timing (first launches load their code)
+    _lib.check(L.nmz_topk_merge_dev(ctx.handle, ctypes.c_void_p(d_lists.data_ptr()), n_lists, K_TOP,
+                                    ctypes.c_void_p(d_scratch.data_ptr()), ctypes.c_void_p(d_job.data_ptr()),
+                                    ctypes.c_void_p(streams[0].cuda_stream)))
+    merge_topk(d_job.cpu().numpy().tobytes(), K_TOP)
     torch.cuda.synchronize()
     # the roofline's kernel time: K1 launched back to back on ONE stream (no other stream's kernels beside it, the
     # way rocprofv3 --kernel-trace times a dispatch), HIP events around each K1 launch plus its in-kernel span;
     # enough launches that the engine clock has ramped (a handful after an idle sync run slow)
     tot, cnt = ctypes.c_double(), ctypes.c_uint64()
     for _ in range(20):
-        step(0)
-    drain()
+        sweep(0, spare_lo, d_job.data_ptr())
     _lib.check(L.nmz_timing_enable(ctx.handle, 1))
     L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
     L.nmz_timing_read_span(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
     for _ in range(50):
-        step(0)
-    drain()
+        sweep(0, spare_lo, d_job.data_ptr())
     torch.cuda.synchronize()
     _lib.check(L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
     kern_ms = tot.value / max(cnt.value, 1)
     _lib.check(L.nmz_timing_read_span(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
     kern_ms_serial_span = tot.value / cnt.value if cnt.value else None
     _lib.check(L.nmz_timing_enable(ctx.handle, 0))
-    # the timed region: exactly args.steps pipelined steps; K1's launches are bracketed by HIP events on their
-    # own streams (nmz_timing_*), so the roofline's kernel time comes from these same launches
-    it[0] = 0
+    # the timed region: exactly args.steps pipelined steps + the job's merge; K1's launches are bracketed by HIP
+    # events on their own streams (nmz_timing_*), so the roofline's kernel time comes from these same launches
     _lib.check(L.nmz_timing_enable(ctx.handle, 1))
     L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
     L.nmz_timing_read_span(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
     D.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    drain()
+    for i in range(args.steps):
+        step(i)
+    join()
+    with torch.cuda.stream(streams[0]):
+        _lib.check(L.nmz_topk_merge_dev(ctx.handle, ctypes.c_void_p(d_lists.data_ptr()), args.steps, K_TOP,
+                                        ctypes.c_void_p(d_scratch.data_ptr()), ctypes.c_void_p(d_job.data_ptr()),
+                                        ctypes.c_void_p(streams[0].cuda_stream)))
+        if D.pg:
+            D.pg.all_gather(gathered, d_job)
+        parts = [g.cpu().numpy() for g in gathered] if D.pg else [d_job.cpu().numpy()]
+    merged = merge_topk(b"".join(x.tobytes() for x in parts), K_TOP)
     torch.cuda.synchronize()
     D.barrier()
     el = time.perf_counter() - t0
     _lib.check(L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
     kern_ms_timed = tot.value / max(cnt.value, 1)
-    # the same launches' execution spans as the order-query kernel records them (first workgroup start to last
-    # workgroup end): a pipelined launch's HIP events also time its wait for the CUs another stream's K1 holds
+    # the same launches' execution spans as the kernel records them (first workgroup start to last workgroup
+    # end): a pipelined launch's HIP events also time its wait for the CUs another stream's K1 holds
     _lib.check(L.nmz_timing_read_span(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
     kern_ms_span = tot.value / cnt.value if cnt.value else None
     _lib.check(L.nmz_timing_enable(ctx.handle, 0))
-    merged = merge_topk(b"".join(o.cpu().numpy().tobytes() for o in outputs()), K_TOP)
     el_max = D.max(torch, el)
+    # the job's answer, checked outside the timing: every step's list is the exact top-64 of its own range, so the
+    # job's top-64 is the merge of those lists; timed step 0's stats (seeds "0".."S-1" on rank 0) for the CPU
+    # baseline's parity check
+    lists = np.frombuffer(d_lists.cpu().numpy().tobytes(), dtype=_lib.TOPK_DTYPE)
+    job_ok = True
+    if D.world == 1:
+        want = merge_topk(b"".join(lists[i * K_TOP:(i + 1) * K_TOP].tobytes() for i in range(args.steps)), K_TOP)
+        job_ok = bool(np.array_equal(want, merged))
+    sweep(0, D.rank * S, d_job.data_ptr())
+    torch.cuda.synchronize()
     stats = np.frombuffer(d_stats[0].cpu().numpy().tobytes(), dtype=_lib.SCHED_STATS_DTYPE)
+    seed_lo = [D.rank * S]
+    d_soff = [torch.from_numpy(csr0[0].view(np.int32)).to(dev)]
+    d_sb = [torch.from_numpy(csr0[1]).to(dev)]
     for plan in plans:
         L.nmz_replayable_plan_destroy(plan)
     # configs[1] as stated, end to end: a new trace's plan (tables built and sorted from host hints) + one
@@ -521,9 +535,9 @@ def bench_replayable(args, torch, D, ctx, L, stream):
         heads = [int(x) for x in out["seed"][::K_TOP]]
         e2e_native = dict(traces=T, ms_per_trace=float(np.median(ms)), ms_per_trace_runs=ms, top1=heads[:4],
                           agrees=heads == e2e_heads)
-    return dict(S=S, E=E, hints=(hoff, hb), seeds=csr[0], elapsed=el_max,
+    return dict(S=S, E=E, hints=(hoff, hb), seeds=csr0, elapsed=el_max,
                 kern_ms=kern_ms, kern_ms_events=kern_ms_timed, kern_ms_serial_span=kern_ms_serial_span,
-                kern_ms_span=kern_ms_span, plan_ms=plan_ms, stats=stats, topk=merged, pipeline=NP,
+                kern_ms_span=kern_ms_span, plan_ms=plan_ms, stats=stats, topk=merged, pipeline=NP, job_ok=job_ok,
                 e2e_s=e2e, e2e_plan_s=e2e_plan, e2e_pipe=e2e_pipe, e2e_native=e2e_native, k1_kernel=k1)
 
 
@@ -1032,6 +1046,10 @@ def headline_line(args, torch, D, ctx, L, stream):
         "data": "synthetic (ZooKeeper-style hints: signed decimal SplitMix64, seed 0x5EED; decimal seeds)",
         "config": {"workload": "configs[1] replayable seed sweep", "seeds_per_gpu": r["S"], "events": r["E"],
                    "max_interval_ns": MAX_INTERVAL_NS, "topk": 64, "pipeline_streams": r["pipeline"],
+                   "seeds": "a fresh range of 2^20 decimal seeds per step and rank (seeds (i*N + rank)*2^20 ..)",
+                   "unit_kind": "stats-equivalent decision: a (seed, event) decision whose effect on the seed's "
+                                "statistics (sum, max, argmax, top-64) the sweep covers, bit-exact vs the "
+                                "per-decision oracle; K1 derives them from searches, not event by event",
                    "parallelism": f"seed-range x{D.world}" + (" + RCCL all_gather top-k" if D.world > 1 else "")},
         "roofline": roofline_valu(r["k1_kernel"], dec_launch, r["kern_ms"]),
         # a new trace's plan (tables + segment sorts + allocations), median over the end-to-end traces;
@@ -1039,8 +1057,10 @@ def headline_line(args, torch, D, ctx, L, stream):
         "plan_ms": float(np.median(r["e2e_plan_s"])) * 1e3,
         "plan_ms_first_three": r["plan_ms"],
         "topk_head": [int(x) for x in r["topk"]["seed"][:4]],
-        "steady_state": "value re-sweeps one trace's resident plan each step (plan built once, before the timed "
-                        "region); end_to_end below builds a new trace's plan inside the timing",
+        "job_topk_equals_merge_of_step_lists": r["job_ok"],
+        "steady_state": "value: one trace's resident plan (built once, before the timed region) sweeps a fresh seed "
+                        "range every step, and the job's top-64 is merged on the device (+ RCCL all_gather for N > "
+                        "1) inside the timing; end_to_end below builds a new trace's plan inside the timing",
     }
     one = {"value": dec_launch / float(np.median(r["e2e_s"])), "unit": "decisions/s",
            "ms_median": float(np.median(r["e2e_s"])) * 1e3, "traces": len(r["e2e_s"]),
@@ -1100,7 +1120,14 @@ def headline_line(args, torch, D, ctx, L, stream):
     hoff = r["hints"][0]
     mean_len = float(np.mean(np.diff(hoff.astype(np.int64))))
     if line["roofline"]:
-        line["roofline"]["declared_model_ops_per_unit"] = 6 * mean_len + 18
+        rf = line["roofline"]
+        rf["declared_model_ops_per_unit"] = 6 * mean_len + 18
+        # the same decisions priced at SURVEY 8(d)'s per-decision model (the reference's byte-serial FNV over
+        # seed || hint, then the modulo) over the measured K1 time: far above 1, because K1 does not decide event by
+        # event (unit_kind); frac (measured lane-instructions) is the kernel's own utilisation
+        if rf.get("kernel_ms"):
+            rf["declared_model_frac"] = (rf["declared_model_ops_per_unit"] * dec_launch / (rf["kernel_ms"] * 1e-3) /
+                                         1e12 / PEAK_VALU_TOPS)
     if D.rank == 0 and D.world == 1 and args.cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_replayable(r, args)
     return line
@@ -1208,8 +1235,9 @@ def write_final(out_fd, line, path):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    # the driver's settings (python bench.py --steps 20 --warmup 5): a run with no flags measures what it measures
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--seeds", type=int, default=1 << 20)
     ap.add_argument("--events", type=int, default=4096)
     ap.add_argument("--cpu-seeds", type=int, default=1 << 18)

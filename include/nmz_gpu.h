@@ -294,6 +294,12 @@ int nmz_random_sweep_dev(nmz_random_plan *plan, uint64_t seed0, uint64_t n_seeds
  * k <= 256 (here and for the sweeps' topk outputs); NMZ_EINVAL otherwise. */
 int nmz_topk_select_dev(nmz_ctx *ctx, const nmz_sched_stats *d_stats, uint64_t n, uint64_t seed0,
                         uint32_t k, nmz_topk_entry *d_out, void *stream);
+/* Merge n_lists top-k lists (d_lists[n_lists][k], each sorted as the sweeps write them: n_fault desc, sum_delay
+ * desc, seed asc) into the best k (d_out[k]): the lists of several sweeps over disjoint seed ranges (successive
+ * batches of one job, or the shards of one rank) become the job's top-k. d_lists and d_scratch (same size) are
+ * overwritten. k <= 256. */
+int nmz_topk_merge_dev(nmz_ctx *ctx, nmz_topk_entry *d_lists, uint64_t n_lists, uint32_t k,
+                       nmz_topk_entry *d_scratch, nmz_topk_entry *d_out, void *stream);
 
 /* ---- trace similarity (banded Levenshtein over event-hash sequences) ------
  * Traces in CSR: off[n_traces+1] (element offsets) into sym[] (uint64 event

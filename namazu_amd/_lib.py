@@ -125,6 +125,7 @@ SIGNATURES = {
     "nmz_close_group": (_int, [_P]),
     "nmz_group_info": (_int, [_P, ctypes.POINTER(_int), ctypes.POINTER(_int), ctypes.POINTER(_u32)]),
     "nmz_group_collectives": (_int, [_P, ctypes.POINTER(_u64)]),
+    "nmz_topk_merge_dev": (_int, [_P, _P, _u64, _u32, _P, _P, _P]),
     "nmz_replayable_group_plan_create": (_int, [_P, _P, _P, _u32, _i64, _u64, ctypes.POINTER(_P)]),
     "nmz_replayable_group_plan_destroy": (_int, [_P]),
     "nmz_replayable_group_sweep": (_int, [_P, _P, _P, _u64, _u32, _P, _P]),

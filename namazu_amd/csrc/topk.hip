@@ -207,6 +207,18 @@ int topk_select(hipStream_t st, const nmz_sched_stats *d_stats, uint64_t n, uint
 
 using namespace nmz;
 
+extern "C" int nmz_topk_merge_dev(nmz_ctx *ctx, nmz_topk_entry *d_lists, uint64_t n_lists, uint32_t k,
+                                  nmz_topk_entry *d_scratch, nmz_topk_entry *d_out, void *stream) {
+    NMZ_CHECK(ctx != nullptr, "ctx is NULL");
+    NMZ_CHECK(k <= 256, "k must be <= 256");
+    if (k == 0 || n_lists == 0) return NMZ_OK;
+    NMZ_CHECK(d_lists && d_scratch && d_out, "NULL argument");
+    NMZ_CHECK(n_lists < (1ULL << 31), "too many lists");
+    CtxGuard g(ctx);
+    NMZ_TRY(g.rc);
+    return topk_merge_lists(stream ? (hipStream_t)stream : ctx->stream, d_lists, d_scratch, n_lists, k, d_out);
+}
+
 extern "C" int nmz_topk_select_dev(nmz_ctx *ctx, const nmz_sched_stats *d_stats, uint64_t n, uint64_t seed0,
                                    uint32_t k, nmz_topk_entry *d_out, void *stream) {
     NMZ_CHECK(ctx != nullptr, "ctx is NULL");
