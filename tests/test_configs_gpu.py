@@ -198,3 +198,47 @@ def test_config4_long_traces_wide_band(ctx):
     oi, od = O.ed_allpairs_knn(ts.off, ts.sym, 4096, 3, nthreads=16)
     assert np.array_equal(ids, oi) and np.array_equal(ds, od)
     assert od[0, 0] < 4096 and (od == 4097).any()
+
+
+def test_config2_full_size_100k_traces(ctx):
+    """configs[2] at its stated size: 100,000 stored traces x 2,048 events (the bench's clustered store: families of
+    1,024 near-duplicate runs, the last family partial), w = 32, k = 8, through the resident plan. Three queries
+    (first trace, a mid-family trace, the last trace) against the oracle's full-band DP over all 99,999 other
+    traces; every pair counted once (DP or q-gram settled: equal lengths keep every pair in the length band); the
+    nearest neighbour in band for nearly every trace; and the 8-shard search (the plan's query-block deal +
+    nmz_knn_merge_dev + fill) equal to the unsharded lists bit for bit."""
+    import ctypes
+    import torch
+    from namazu_amd import synth
+    N, Lx, w, k, S = 100_000, 2048, 32, 8, 8
+    ts = synth.clustered_traces(N, Lx, family=1024)
+    L = _lib.load()
+    plan = ctypes.c_void_p()
+    _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), N, w, ctypes.byref(plan)))
+    try:
+        assert L.nmz_ed_plan_is_fast(plan) == 2
+        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        d_keys = torch.empty(N * k, dtype=torch.int64, device="cuda")
+        _lib.check(L.nmz_ed_allpairs_knn_dev(plan, k, ctypes.c_void_p(d_keys.data_ptr()), stream))
+        cnt = np.zeros(_lib.NMZ_ED_NCOUNTERS, np.uint64)
+        _lib.check(L.nmz_ed_plan_counters(plan, _lib.ptr(cnt), stream))
+        keys = d_keys.cpu().numpy().view(np.uint64).reshape(N, k)
+        assert int(cnt[0]) + int(cnt[5]) == N * (N - 1) // 2
+        parts = torch.empty(S * N * k, dtype=torch.int64, device="cuda")
+        for s in range(S):
+            _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, s, S, ctypes.c_void_p(parts.data_ptr() + s * N * k * 8),
+                                                       stream))
+        out = torch.empty(N * k, dtype=torch.int64, device="cuda")
+        _lib.check(L.nmz_knn_merge_dev(ctx.handle, ctypes.c_void_p(parts.data_ptr()), S, N, k,
+                                       ctypes.c_void_p(out.data_ptr()), stream))
+        _lib.check(L.nmz_ed_knn_fill_dev(plan, k, ctypes.c_void_p(out.data_ptr()), stream))
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint64).reshape(N, k), keys)
+    finally:
+        L.nmz_ed_plan_destroy(plan)
+    ids = (keys & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    ds = (keys >> np.uint64(32)).astype(np.uint32)
+    assert (ds[:, 0] <= w).mean() > 0.99
+    for q in [0, 51_234, N - 1]:
+        od, oi, _ = _brute_knn(ts, q, w, k)
+        assert ds[q].tolist() == od and ids[q].tolist() == oi, q
