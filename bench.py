@@ -843,6 +843,28 @@ def bench_config0(args, torch, D, ctx, L):
     run(events[:50], False)  # warm-up
     burst = run(events, False)
     single = run(events[:300], True)
+    # the fixed-duration lane (BasicTBQueue's one goroutine for min == max, util/queue/impl.go:77-89): the random
+    # policy with maxInterval unset (= minInterval = 1 ms), a 200-event burst through QueueEvent: released in order
+    # at ~1, 2, ..., 200 ms, each at (the previous release or its enqueue) + 1 ms
+    f = Random()
+    f.LoadConfig(Config({"explorePolicy": "random", "explorePolicyParam": {"minInterval": "1ms", "seed": 1}}))
+    ch = f.ActionChan()
+    t0 = ch.L.nmz_monotonic_ns()
+    for ev in events[:200]:
+        f.QueueEvent(ev)
+    rel = []
+    for _ in range(200):
+        ch.get(timeout=10)
+        rel.append(ch.last_release_ns - t0)
+    rel = np.array(rel, np.float64)
+    late = np.array(list(ch.delivery_err_ns)[-200:], np.float64) / 1e3
+    fixed_lane = dict(events=200, duration_ms=1.0, last_release_ms=float(rel[-1] / 1e6),
+                      min_gap_ms=float(np.diff(rel).min() / 1e6),
+                      release_after_rule_us=dict(p50=float(np.percentile(late, 50)), p99=float(np.percentile(late, 99)),
+                                                 max=float(late.max())),
+                      what="random policy, maxInterval = minInterval = 1 ms: one FIFO lane, item k released at "
+                           "max(its enqueue, release k-1) + 1 ms (impl.go:77-89); the burst ends at ~200 ms")
+    ch.close()
     return dict(metric="configs[0] random policy, one seed over one 10k-event trace", unit="decisions/s",
                 cpu_1core=dict(value=E / cpu_s, seconds=round(cpu_s, 4), kind="port",
                                note="oracle/nmz_oracle.c: full Go rand.Seed per decision, as the reference reseeds "
@@ -850,6 +872,7 @@ def bench_config0(args, torch, D, ctx, L):
                 gpu_batch=dict(value=E / min(times), ms=min(times) * 1e3,
                                note="nmz_random_decide, the whole trace in one call (host arrays in and out)"),
                 parity_with_gpu=parity,
+                fixed_duration_lane=fixed_lane,
                 queue_event_latency_us=dict(mode=q.online.mode, burst=burst, one_at_a_time=single,
                                             what="enqueue -> decided inside QueueEvent (nmz_random_decide_host: the "
                                                  "kernels' closed forms on the host); delivered-delay error = "
