@@ -42,7 +42,7 @@ SIMDS = 256 * 4
 
 # kernel entry in valu_per_unit.json -> mangled symbol prefix
 KERNELS = {
-    "k_replayable_sweep_wt": "_ZN3nmz21k_replayable_sweep_wtILb0ELi1ELi7E",
+    "k_replayable_sweep_wt": "_ZN3nmz21k_replayable_sweep_wtILb0ELi1ELi6E",
     "k_random_sweep": "_ZN3nmz14k_random_sweepILb1E",
     "k_ed_bv_dp:clustered": "_ZN3nmz10k_ed_bv_dpILi32ELb0E",
     "k_ed_bv_dp:alphabet": "_ZN3nmz10k_ed_bv_dpILi32ELb1E",
