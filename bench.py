@@ -144,6 +144,7 @@ def roofline_valu(kernel, units, kernel_ms):
 # (configs[1]: value, roofline, cpu_baseline, a short per-leg summary) capped at HEADLINE_MAX_BYTES; every
 # secondary leg goes out as its own earlier line ({"secondary_leg": ...}) and the full record to a file.
 HEADLINE_MAX_BYTES = 4096
+NMZ_TIMING_SPANS = 2  # nmz_timing_enable mode: in-kernel spans only (include/nmz_gpu.h)
 HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
                  "vs_baseline", "dtype", "data", "config")
 ROOFLINE_KEYS = ("bound", "kernel", "achieved", "peak", "unit", "frac", "declared_model_frac",
@@ -323,7 +324,24 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     d_lists = torch.empty(n_lists * K_TOP * 24, dtype=torch.uint8, device=dev)
     d_scratch = torch.empty_like(d_lists)
     d_job = torch.empty(K_TOP * 24, dtype=torch.uint8, device=dev)
-    gathered = [torch.empty_like(d_job) for _ in range(D.world)] if D.world > 1 else None
+    # N > 1: every rank's job list lands in one [N][64] buffer (views of it as all_gather's outputs) and the device
+    # merges them (nmz_topk_merge_dev), so the host only copies the final 64 entries (pinned, asynchronous)
+    d_gath = torch.empty(max(D.world, 1) * K_TOP * 24, dtype=torch.uint8, device=dev)
+    gathered = list(d_gath.view(D.world, K_TOP * 24).unbind(0)) if D.world > 1 else None
+    d_final = torch.empty_like(d_job)
+    h_final = torch.empty(K_TOP * 24, dtype=torch.uint8).pin_memory()
+    done_ev = torch.cuda.Event()
+    # the host merge of the job (one list per rank) is the check outside the timing; NMZ_BENCH_HOST_MERGE=1 times
+    # it instead of the device merge (A/B)
+    host_merge = os.environ.get("NMZ_BENCH_HOST_MERGE") == "1"
+    # how the last step's stream learns that the other slots are done before the job merge: "event" (stream waits:
+    # barrier packets on the last stream's queue) or "host" (the host waits for those streams, which end first, then
+    # enqueues the merge: measured slower, 0.075-0.077 vs 0.070-0.071 ms per step -- the host's wake-up costs more)
+    host_join = os.environ.get("NMZ_BENCH_JOIN", "event") == "host"
+    # the timed K1 launches record their own execution spans (in-kernel wall clock, no HIP event records between
+    # a stream's launches: each record is a marker the queue stalls on, ~6 us at the step's ends);
+    # NMZ_BENCH_TIMED_EVENTS=1 brackets them with HIP events as well (A/B of their cost)
+    timed_events = os.environ.get("NMZ_BENCH_TIMED_EVENTS", "0") == "1"
     # seed ranges outside the job's for the untimed launches (warm-up, kernel timing)
     spare_lo = (args.steps + 1) * D.world * S + D.rank * S
 
@@ -337,9 +355,10 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     def step(i):
         sweep(i % NP, (i * D.world + D.rank) * S, d_lists.data_ptr() + (i % n_lists) * K_TOP * 24)
 
-    def join():  # stream 0 waits for the other slots' work
-        for sp in range(1, NP):
-            streams[0].wait_stream(streams[sp])
+    def join(last=0):  # stream `last` waits for the other slots' work
+        for sp in range(NP):
+            if sp != last:
+                streams[last].wait_stream(streams[sp])
 
     for j in range(max(args.warmup, NP)):
         sweep(j % NP, spare_lo, d_lists.data_ptr() + (j % n_lists) * K_TOP * 24)
@@ -369,30 +388,58 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     _lib.check(L.nmz_timing_enable(ctx.handle, 0))
     # the timed region: exactly args.steps pipelined steps + the job's merge; K1's launches are bracketed by HIP
     # events on their own streams (nmz_timing_*), so the roofline's kernel time comes from these same launches
-    _lib.check(L.nmz_timing_enable(ctx.handle, 1))
+    _lib.check(L.nmz_timing_enable(ctx.handle, 1 if timed_events else NMZ_TIMING_SPANS))
     L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
     L.nmz_timing_read_span(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
+    # the job's merges run on the stream of the last step (in order behind its top-k; the other slots' streams
+    # finished earlier, so waiting for them costs no cross-queue round trip at the end)
+    last = (args.steps - 1) % NP if args.steps else 0
     D.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
-    join()
-    with torch.cuda.stream(streams[0]):
+    enq = time.perf_counter() - t0  # the host's enqueue time of the steps (host-bound pipeline when ~ el)
+    if host_join:
+        # the other slots' last steps end while the last step's sweep still runs: the host waits for them and
+        # then enqueues the merge behind the last step, in order on its stream (no cross-queue barrier packet)
+        for sp in range(NP):
+            if sp != last:
+                streams[sp].synchronize()
+    else:
+        join(last)
+    with torch.cuda.stream(streams[last]):
+        sl = ctypes.c_void_p(streams[last].cuda_stream)
         _lib.check(L.nmz_topk_merge_dev(ctx.handle, ctypes.c_void_p(d_lists.data_ptr()), args.steps, K_TOP,
                                         ctypes.c_void_p(d_scratch.data_ptr()), ctypes.c_void_p(d_job.data_ptr()),
-                                        ctypes.c_void_p(streams[0].cuda_stream)))
-        if D.pg:
-            D.pg.all_gather(gathered, d_job)
-        parts = [g.cpu().numpy() for g in gathered] if D.pg else [d_job.cpu().numpy()]
-    merged = merge_topk(b"".join(x.tobytes() for x in parts), K_TOP)
+                                        sl))
+        if host_merge:
+            if D.pg:
+                D.pg.all_gather(gathered, d_job)
+            parts = [g.cpu().numpy() for g in gathered] if D.pg else [d_job.cpu().numpy()]
+            merged = merge_topk(b"".join(x.tobytes() for x in parts), K_TOP)
+        else:
+            fin = d_job
+            if D.pg:
+                D.pg.all_gather(gathered, d_job)
+                _lib.check(L.nmz_topk_merge_dev(ctx.handle, ctypes.c_void_p(d_gath.data_ptr()), D.world, K_TOP,
+                                                ctypes.c_void_p(d_scratch.data_ptr()),
+                                                ctypes.c_void_p(d_final.data_ptr()), sl))
+                fin = d_final
+            h_final.copy_(fin, non_blocking=True)
+            done_ev.record()
+            done_ev.synchronize()
+            merged = np.frombuffer(h_final.numpy().tobytes(), dtype=_lib.TOPK_DTYPE).copy()
     torch.cuda.synchronize()
     D.barrier()
     el = time.perf_counter() - t0
-    _lib.check(L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
-    kern_ms_timed = tot.value / max(cnt.value, 1)
-    # the same launches' execution spans as the kernel records them (first workgroup start to last workgroup
-    # end): a pipelined launch's HIP events also time its wait for the CUs another stream's K1 holds
+    kern_ms_timed = None
+    if timed_events:
+        _lib.check(L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
+        kern_ms_timed = tot.value / max(cnt.value, 1)
+    # the timed launches' execution spans as the kernel records them (first workgroup start to last workgroup end;
+    # the union over launches that overlap): a pipelined launch's HIP events would also time its wait for the CUs
+    # another stream's K1 holds
     _lib.check(L.nmz_timing_read_span(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
     kern_ms_span = tot.value / cnt.value if cnt.value else None
     _lib.check(L.nmz_timing_enable(ctx.handle, 0))
@@ -400,11 +447,15 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     # the job's answer, checked outside the timing: every step's list is the exact top-64 of its own range, so the
     # job's top-64 is the merge of those lists; timed step 0's stats (seeds "0".."S-1" on rank 0) for the CPU
     # baseline's parity check
+    # (N > 1: the rank's own list is that merge, and the job's list the host merge of the gathered rank lists)
     lists = np.frombuffer(d_lists.cpu().numpy().tobytes(), dtype=_lib.TOPK_DTYPE)
-    job_ok = True
+    own = np.frombuffer(d_job.cpu().numpy().tobytes(), dtype=_lib.TOPK_DTYPE)
+    want = merge_topk(b"".join(lists[i * K_TOP:(i + 1) * K_TOP].tobytes() for i in range(args.steps)), K_TOP)
+    job_ok = bool(np.array_equal(want, own))
     if D.world == 1:
-        want = merge_topk(b"".join(lists[i * K_TOP:(i + 1) * K_TOP].tobytes() for i in range(args.steps)), K_TOP)
-        job_ok = bool(np.array_equal(want, merged))
+        job_ok = job_ok and bool(np.array_equal(want, merged))
+    elif not host_merge:
+        job_ok = job_ok and bool(np.array_equal(merge_topk(d_gath.cpu().numpy().tobytes(), K_TOP), merged))
     sweep(0, D.rank * S, d_job.data_ptr())
     torch.cuda.synchronize()
     stats = np.frombuffer(d_stats[0].cpu().numpy().tobytes(), dtype=_lib.SCHED_STATS_DTYPE)
@@ -537,7 +588,7 @@ def bench_replayable(args, torch, D, ctx, L, stream):
                           agrees=heads == e2e_heads)
     return dict(S=S, E=E, hints=(hoff, hb), seeds=csr0, elapsed=el_max,
                 kern_ms=kern_ms, kern_ms_events=kern_ms_timed, kern_ms_serial_span=kern_ms_serial_span,
-                kern_ms_span=kern_ms_span, plan_ms=plan_ms, stats=stats, topk=merged, pipeline=NP, job_ok=job_ok,
+                kern_ms_span=kern_ms_span, enqueue_ms=enq * 1e3, plan_ms=plan_ms, stats=stats, topk=merged, pipeline=NP, job_ok=job_ok,
                 e2e_s=e2e, e2e_plan_s=e2e_plan, e2e_pipe=e2e_pipe, e2e_native=e2e_native, k1_kernel=k1)
 
 
@@ -1081,7 +1132,10 @@ def headline_line(args, torch, D, ctx, L, stream):
         "plan_ms_first_three": r["plan_ms"],
         "topk_head": [int(x) for x in r["topk"]["seed"][:4]],
         "job_topk_equals_merge_of_step_lists": r["job_ok"],
-        "steady_state": "value: one trace's resident plan (built once, before the timed region) sweeps a fresh seed "
+        # host time to enqueue the K steps (the timed region's first part): close to ms_per_step * K means the
+        # host's launches, not the GPU, set the step
+        "enqueue_ms": r["enqueue_ms"],
+        "steady_state":"value: one trace's resident plan (built once, before the timed region) sweeps a fresh seed "
                         "range every step, and the job's top-64 is merged on the device (+ RCCL all_gather for N > "
                         "1) inside the timing; end_to_end below builds a new trace's plan inside the timing",
     }

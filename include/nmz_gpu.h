@@ -106,7 +106,10 @@ int nmz_abi_version(void);
 int nmz_device_count(int *count);
 
 /* Kernel timing (HIP events recorded on the launch stream around the dominant
- * kernels: "replayable_sweep", "random_sweep", "ed_tile"). */
+ * kernels: "replayable_sweep", "random_sweep", "ed_tile"). on = 0 off, 1 events and
+ * spans, NMZ_TIMING_SPANS (2) the kernels' own spans only (no event records between a
+ * stream's launches: each record is a marker the queue waits on, ~6 us). */
+#define NMZ_TIMING_SPANS 2
 int nmz_timing_enable(nmz_ctx *ctx, int on);
 int nmz_timing_read(nmz_ctx *ctx, const char *kernel, double *total_ms, uint64_t *count, int reset);
 /* The same kernels' execution spans as the kernels record them (first workgroup start to last workgroup end,

@@ -69,6 +69,7 @@ struct HostPin {
 // Optional HIP-event timing of the dominant kernels (bench.py reads it).
 struct NmzTiming {
     bool enabled = false;
+    bool spans_only = false;  // NMZ_TIMING_SPANS: span slots, no events
     std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> events;
     std::vector<hipEvent_t> pool;
     // in-kernel execution spans: slot = {max ~start, max end} of wall_clock64() over the launch's workgroups
@@ -105,6 +106,7 @@ struct KernelTimer {
     hipStream_t st;
     const char *name;
     hipEvent_t a = nullptr, b = nullptr;
+    bool spans_only = false;
     KernelTimer(nmz_ctx *c, hipStream_t s, const char *n);
     ~KernelTimer();
     // a fresh span slot for a kernel that records its own execution span (nullptr when timing is off)
@@ -251,40 +253,41 @@ __host__ __device__ inline void stats_empty(nmz_sched_stats &s) {
 // ---------------------------------------------------------------------------
 inline unsigned ceil_div(uint64_t a, uint64_t b) { return (unsigned)((a + b - 1) / b); }
 
-// seed bucketing by FNV low byte (shared by both sweeps)
-// The 256 global bucket counters and cursors take device-scope atomics from
-// every block; one counter per 128-byte line (stride BUCKET_STRIDE) spreads
-// them over the L2 channels instead of serialising them on 8 lines.
-constexpr uint32_t BUCKET_STRIDE = 32;
-constexpr size_t BUCKET_SMALL_U32 = 2 * 256 * BUCKET_STRIDE + 260 + 4;  // count, cursor, offset, n_units
+// seed bucketing by FNV low byte (shared by both sweeps): a counting sort with no global atomics. The prefix
+// kernels hash blocks of BUCKET_BLK seeds and store each block's 256 bucket counts in its own row of b.hist (every
+// row is written whole, so nothing needs zeroing); k_bucket_colscan turns each bucket's column of rows, in place,
+// into the rows' offsets inside the bucket and the bucket's total; k_bucket_scatter scans the totals into the
+// bucket starts and writes each block's seeds from start + row offset (block 0 also writes the starts and the work
+// units). (Device-scope atomics on 256 shared counters from every block -- the previous form -- serialise on
+// their words: ~11 ns each, 11 + 16 us per 2^20 seeds.)
+constexpr uint32_t BUCKET_PT = 8;                 // seeds per thread of the prefix and scatter blocks (256 threads)
+constexpr uint32_t BUCKET_BLK = 256 * BUCKET_PT;  // seeds per histogram row
+constexpr size_t BUCKET_SMALL_U32 = 260 + 4 + 256;  // offset, n_units, total
+inline uint64_t bucket_rows(uint64_t S) { return (S + BUCKET_BLK - 1) / BUCKET_BLK; }
+inline size_t bucket_hist_u32(uint64_t S) { return (size_t)(bucket_rows(S) ? bucket_rows(S) : 1) * 256; }
 struct Buckets {
-    uint32_t *count;       // [256 * BUCKET_STRIDE]
+    uint32_t *hist;        // [bucket_rows(S)][256]: the blocks' counts, then (k_bucket_colscan) their offsets
     uint32_t *offset;      // [257]
-    uint32_t *cursor;      // [256 * BUCKET_STRIDE]
     uint32_t *n_units;     // [1]
+    uint32_t *total;       // [256] bucket sizes
     uint4 *units;          // [max_units] {L, start, count, 0}
     uint64_t *sorted_h0;   // [S]
     uint32_t *sorted_idx;  // [S]
 };
 
 inline void buckets_small(uint32_t *small, Buckets &b) {
-    b.count = small;
-    b.cursor = small + 256 * BUCKET_STRIDE;
-    b.offset = small + 2 * 256 * BUCKET_STRIDE;
-    b.n_units = b.offset + 260;
+    b.offset = small;
+    b.n_units = small + 260;
+    b.total = small + 264;
 }
 
-// b.count must already hold the 256 bucket counts (filled by the caller's prefix kernel); the scan
-// re-zeroes them (and *zero_word, if given) for the next call, so the counters must be zeroed once
-// when the scratch is allocated
+// b.hist must already hold the bucket_rows(n_seeds) rows of counts (the caller's prefix kernel, blocks of
+// BUCKET_BLK seeds); *zero_word, if given, is zeroed for the caller's work-item counter
 int bucket_seeds_counted(hipStream_t st, const uint64_t *d_h0, uint64_t n_seeds, uint32_t seeds_per_unit,
                          Buckets &b, uint32_t *zero_word = nullptr);
-// seeds per thread in the prefix + histogram kernels and in the scatter (tuning: NMZ_PREFIX_PT, NMZ_SCATTER_PT)
 // A/B and test knobs: an NMZ_* environment variable is read only when NMZ_AB=1 is set too, so that a production
 // process's environment never changes which kernel runs or how a search deals its pairs over ranks
 const char *ab_env(const char *name);
-uint32_t prefix_per_thread();
-uint32_t scatter_per_thread();
 
 
 }  // namespace nmz

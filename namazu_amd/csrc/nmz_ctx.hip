@@ -123,13 +123,17 @@ static hipEvent_t timing_event(nmz_ctx *c) {
 
 KernelTimer::KernelTimer(nmz_ctx *c, hipStream_t s, const char *n) : ctx(c), st(s), name(n) {
     if (!ctx || !ctx->timing.enabled) return;
+    if (ctx->timing.spans_only) {
+        spans_only = true;
+        return;
+    }
     a = timing_event(ctx);
     b = timing_event(ctx);
     if (a) (void)hipEventRecord(a, st);
 }
 
 unsigned long long *KernelTimer::span() {
-    if (!a || !b) return nullptr;
+    if (!spans_only && (!a || !b)) return nullptr;
     NmzTiming &t = ctx->timing;
     if (!t.span_dev) {
         if (hipMalloc(&t.span_dev, NMZ_SPAN_SLOTS * 16) != hipSuccess) {
@@ -156,93 +160,84 @@ KernelTimer::~KernelTimer() {
 // wave's lanes share one row of the per-event tables and every table read in
 // the sweep loop is wave-uniform (scalar loads, no LDS, no gathers).
 // ---------------------------------------------------------------------------
-// one block of 256 threads: exclusive scan of the 256 bucket counts and the
-// work-unit table (bucket, start, count) with units of `per_unit` seeds.
-__global__ __launch_bounds__(256) void k_bucket_scan(uint32_t *__restrict__ count,
-                                                     uint32_t *__restrict__ offset,
-                                                     uint32_t *__restrict__ cursor,
-                                                     uint32_t per_unit, uint4 *__restrict__ units,
-                                                     uint32_t *__restrict__ n_units,
-                                                     uint32_t *__restrict__ zero_word) {
-    __shared__ uint32_t off[257];
-    __shared__ uint32_t uoff[257];
-    __shared__ uint2 wsum[4];
-    const uint32_t t = threadIdx.x;
-    const uint32_t lane = t & 63, w = t >> 6;
-    const uint32_t c0 = count[t * BUCKET_STRIDE];
-    // leave the counters zeroed for the next sweep's prefix kernel (and the caller's work-item
-    // counter): no memset launches per step; plan creation zeroes them once
-    count[t * BUCKET_STRIDE] = 0;
-    if (zero_word && t == 0) *zero_word = 0;
-    const uint32_t u0 = (c0 + per_unit - 1) / per_unit;
-    // inclusive wave scan of (count, units), then the 4 wave totals
-    uint32_t a = c0, b = u0;
+// one block per bucket b: the column b of the prefix kernels' rows of counts (hist[rows][256]) becomes, in place,
+// each row's offset inside the bucket (the counts of the earlier rows), and total[b] the bucket's size. Thread t
+// owns the rows [t q, (t + 1) q) (q = 2 for 2^20 seeds): one load round trip, a block scan, the stores.
+__global__ __launch_bounds__(256) void k_bucket_colscan(uint32_t *__restrict__ hist, uint32_t rows,
+                                                        uint32_t *__restrict__ total) {
+    __shared__ uint32_t wsum[4];
+    const uint32_t b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t q = (rows + 255) / 256, r0 = min(rows, t * q), r1 = min(rows, r0 + q);
+    uint32_t s = 0;
+    for (uint32_t r = r0; r < r1; ++r) s += hist[(size_t)r * 256 + b];
+    uint32_t a = s;
     for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t pa = __shfl_up(a, d, 64), pb = __shfl_up(b, d, 64);
-        if (lane >= d) a += pa, b += pb;
+        const uint32_t x = __shfl_up(a, d, 64);
+        if (lane >= d) a += x;
     }
-    if (lane == 63) wsum[w] = make_uint2(a, b);
+    if (lane == 63) wsum[w] = a;
     __syncthreads();
-    uint32_t ba = 0, bb = 0;
-    for (uint32_t i = 0; i < w; ++i) ba += wsum[i].x, bb += wsum[i].y;
-    off[t] = ba + a - c0;
-    uoff[t] = bb + b - u0;
-    if (t == 255) {
-        off[256] = ba + a;
-        uoff[256] = bb + b;
-        *n_units = bb + b;
+    uint32_t run = a - s;
+    for (uint32_t x = 0; x < w; ++x) run += wsum[x];
+    if (t == 255) total[b] = run + s;
+    for (uint32_t r = r0; r < r1; ++r) {
+        const uint32_t v = hist[(size_t)r * 256 + b];
+        hist[(size_t)r * 256 + b] = run;
+        run += v;
     }
-    __syncthreads();
-    offset[t] = off[t];
-    if (t == 0) offset[256] = off[256];
-    cursor[t * BUCKET_STRIDE] = 0;
-    const uint32_t c = c0;
-    uint32_t u = uoff[t];
-    for (uint32_t s = 0; s < c; s += per_unit, ++u)
-        units[u] = make_uint4(t, off[t] + s, min(per_unit, c - s), 0);
 }
 
-// Scatter with block-local ranks: LDS atomics rank each seed inside its
-// (block, bucket) pair and one global atomic per non-empty pair reserves the
-// range, so the 256 global cursors see <= 256 atomics per block instead of one
-// per seed. Order inside a bucket is irrelevant: results go to the original index.
 const char *ab_env(const char *name) {
     const char *ab = getenv("NMZ_AB");
     return (ab && ab[0] == '1' && ab[1] == 0) ? getenv(name) : nullptr;
 }
 
-static uint32_t env_pow2(const char *name, uint32_t dflt, uint32_t lo, uint32_t hi) {
-    const char *e = ab_env(name);
-    const uint32_t v = e ? (uint32_t)atoi(e) : dflt;
-    return (v >= lo && v <= hi && (v & (v - 1)) == 0) ? v : dflt;
-}
-
-uint32_t prefix_per_thread() {
-    static const uint32_t v = env_pow2("NMZ_PREFIX_PT", 8, 1, 64);
-    return v;
-}
-
-uint32_t scatter_per_thread() {
-    static const uint32_t v = env_pow2("NMZ_SCATTER_PT", 16, 4, 16);
-    return v;
-}
-
-
-// The block's seeds are first counting-sorted by bucket in LDS (block-local ranks from LDS atomics, a scan of the
-// 256 counts), then written out in that order: consecutive threads write consecutive slots of one bucket's range,
-// so a wave's stores are runs of ~SCATTER_PER_THREAD entries instead of 64 scattered 8-B writes.
-template <uint32_t SCATTER_PER_THREAD>
+// Scatter of one block of BUCKET_BLK seeds (the prefix kernel's block of the same index). Every block scans the
+// 256 bucket totals into the bucket starts (block 0 also writes them, the work-unit table (bucket, start, count)
+// of `per_unit` seeds and the caller's zeroed work-item counter); the block's write base in bucket b is b's start +
+// its row offset from k_bucket_colscan. The block's seeds are first counting-sorted by bucket in LDS (block-local
+// ranks from LDS atomics, a scan of the 256 counts), then written out in that order: consecutive threads write
+// consecutive slots of one bucket's range, so a wave's stores are runs of ~BUCKET_PT entries instead of 64
+// scattered 8-B writes. Order inside a bucket is irrelevant: results go to the original index.
 __global__ __launch_bounds__(256) void k_bucket_scatter(const uint64_t *__restrict__ h0, uint64_t n,
-                                                        const uint32_t *__restrict__ offset,
-                                                        uint32_t *__restrict__ cursor,
+                                                        const uint32_t *__restrict__ rowoff,
+                                                        const uint32_t *__restrict__ total,
+                                                        uint32_t *__restrict__ offset, uint32_t per_unit,
+                                                        uint4 *__restrict__ units, uint32_t *__restrict__ n_units,
+                                                        uint32_t *__restrict__ zero_word,
                                                         uint64_t *__restrict__ sorted_h0,
                                                         uint32_t *__restrict__ sorted_idx) {
-    constexpr uint32_t NB = 256 * SCATTER_PER_THREAD;
+    constexpr uint32_t SCATTER_PER_THREAD = BUCKET_PT, NB = BUCKET_BLK;
     __shared__ uint32_t cnt[256], base[256], loff[256];
     __shared__ uint16_t si[NB];  // the block's seeds in bucket order (offsets in the block; h0 re-read from L2)
     __shared__ uint32_t wsum[4];
+    __shared__ uint2 wsum2[4];
     const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
     cnt[t] = 0;
+    {  // bucket starts (and, block 0, the unit table): inclusive wave scans of (count, units), the 4 wave totals
+        const uint32_t c0 = total[t], u0 = (c0 + per_unit - 1) / per_unit;
+        uint32_t a = c0, bu = u0;
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t pa = __shfl_up(a, d, 64), pb = __shfl_up(bu, d, 64);
+            if (lane >= d) a += pa, bu += pb;
+        }
+        if (lane == 63) wsum2[w] = make_uint2(a, bu);
+        __syncthreads();
+        uint32_t ba = 0, bb = 0;
+        for (uint32_t i = 0; i < w; ++i) ba += wsum2[i].x, bb += wsum2[i].y;
+        const uint32_t start = ba + a - c0;
+        base[t] = start + rowoff[(size_t)blockIdx.x * 256 + t];
+        if (blockIdx.x == 0) {
+            offset[t] = start;
+            if (t == 255) {
+                offset[256] = ba + a;
+                *n_units = bb + bu;
+            }
+            if (zero_word && t == 0) *zero_word = 0;
+            uint32_t u = bb + bu - u0;
+            for (uint32_t x = 0; x < c0; x += per_unit, ++u) units[u] = make_uint4(t, start + x, min(per_unit, c0 - x), 0);
+        }
+    }
     __syncthreads();
     const uint64_t b0 = (uint64_t)blockIdx.x * NB;
     uint64_t hv[SCATTER_PER_THREAD];
@@ -255,7 +250,6 @@ __global__ __launch_bounds__(256) void k_bucket_scatter(const uint64_t *__restri
     }
     __syncthreads();
     const uint32_t c = cnt[t];
-    if (c) base[t] = offset[t] + atomicAdd(&cursor[t * BUCKET_STRIDE], c);
     // exclusive scan of the 256 counts: the buckets' local offsets
     uint32_t a = c;
     for (uint32_t d = 1; d < 64; d <<= 1) {
@@ -293,15 +287,11 @@ __global__ __launch_bounds__(256) void k_bucket_scatter(const uint64_t *__restri
 
 int bucket_seeds_counted(hipStream_t st, const uint64_t *d_h0, uint64_t n_seeds, uint32_t per_unit, Buckets &b,
                          uint32_t *zero_word) {
-    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(256), 0, st, b.count, b.offset, b.cursor, per_unit,
-                       b.units, b.n_units, zero_word);
-    if (n_seeds)
-    {
-        const uint32_t pt = scatter_per_thread();
-        auto kern = pt == 4 ? k_bucket_scatter<4> : pt == 8 ? k_bucket_scatter<8> : k_bucket_scatter<16>;
-        hipLaunchKernelGGL(kern, dim3(ceil_div(n_seeds, 256 * pt)), dim3(256), 0, st, d_h0, n_seeds, b.offset,
-                           b.cursor, b.sorted_h0, b.sorted_idx);
-    }
+    const uint32_t rows = (uint32_t)bucket_rows(n_seeds);
+    hipLaunchKernelGGL(k_bucket_colscan, dim3(256), dim3(256), 0, st, b.hist, rows, b.total);
+    // (no seeds: one block writes the empty bucket starts and unit table)
+    hipLaunchKernelGGL(k_bucket_scatter, dim3(rows ? rows : 1), dim3(256), 0, st, d_h0, n_seeds, b.hist, b.total,
+                       b.offset, per_unit, b.units, b.n_units, zero_word, b.sorted_h0, b.sorted_idx);
     NMZ_HIP(hipGetLastError());
     return NMZ_OK;
 }
@@ -380,7 +370,9 @@ int nmz_close(nmz_ctx *ctx) {
 int nmz_timing_enable(nmz_ctx *ctx, int on) {
     NMZ_CHECK(ctx != nullptr, "ctx is NULL");
     std::lock_guard<std::mutex> lk(ctx->mu);
+    NMZ_CHECK(on >= 0 && on <= NMZ_TIMING_SPANS, "on must be 0, 1 or NMZ_TIMING_SPANS");
     ctx->timing.enabled = on != 0;
+    ctx->timing.spans_only = on == NMZ_TIMING_SPANS;
     return NMZ_OK;
 }
 

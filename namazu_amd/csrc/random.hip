@@ -227,8 +227,9 @@ __host__ __device__ __forceinline__ uint64_t seed_prefix(uint64_t seed) {
 }
 
 __global__ __launch_bounds__(256) void k_random_prefix(uint64_t seed0, uint64_t n, uint64_t *__restrict__ h0,
-                                                       uint32_t *__restrict__ count, uint32_t ppt) {
-    // fused bucket histogram (low byte of h0), as in k_seed_prefix
+                                                       uint32_t *__restrict__ rows) {
+    // fused bucket histogram (low byte of h0), as in k_seed_prefix: the block's row of `rows` (Buckets)
+    constexpr uint32_t ppt = BUCKET_PT;
     __shared__ uint32_t hist[256];
     hist[threadIdx.x] = 0;
     __syncthreads();
@@ -242,7 +243,7 @@ __global__ __launch_bounds__(256) void k_random_prefix(uint64_t seed0, uint64_t 
         }
     }
     __syncthreads();
-    if (hist[threadIdx.x]) atomicAdd(&count[threadIdx.x * BUCKET_STRIDE], hist[threadIdx.x]);
+    rows[(size_t)blockIdx.x * 256 + threadIdx.x] = hist[threadIdx.x];
 }
 
 // Work item = (unit of <= 64 seeds sharing the low byte L, chunk of ec events), handed out by a global atomic
@@ -478,7 +479,7 @@ static uint32_t random_ec(uint64_t S) {
 
 static size_t random_seed_scratch_bytes(uint64_t S) {
     return Carve::bytes_for(S, 8) * 2 + Carve::bytes_for(S, 4) + Carve::bytes_for(BUCKET_SMALL_U32, 4) +
-           Carve::bytes_for(S / 64 + 257, 16) + Carve::bytes_for(4, 4);
+           Carve::bytes_for(bucket_hist_u32(S), 4) + Carve::bytes_for(S / 64 + 257, 16) + Carve::bytes_for(4, 4);
 }
 
 static Buckets carve_random(void *p, uint64_t S, uint64_t **h0, uint32_t **counter) {
@@ -488,6 +489,7 @@ static Buckets carve_random(void *p, uint64_t S, uint64_t **h0, uint32_t **count
     b.sorted_h0 = cv.take<uint64_t>(S);
     b.sorted_idx = cv.take<uint32_t>(S);
     buckets_small(cv.take<uint32_t>(BUCKET_SMALL_U32), b);
+    b.hist = cv.take<uint32_t>(bucket_hist_u32(S));
     b.units = cv.take<uint4>(S / 64 + 257);
     *counter = cv.take<uint32_t>(4);
     return b;
@@ -518,13 +520,6 @@ static int random_plan_create(nmz_ctx *ctx, const uint64_t *evhash, const uint8_
     int rc = p->table_mem.ensure(Carve::bytes_for((size_t)256 * E + 1, 16) + Carve::bytes_for(E + 1, 8) +
                                  Carve::bytes_for(E + 1, 1));
     if (rc == NMZ_OK) rc = p->seed_scratch.ensure(random_seed_scratch_bytes(max_seeds));
-    if (rc == NMZ_OK) {  // bucket counters start at zero (k_bucket_scan re-zeroes them)
-        uint64_t *h0_unused;
-        uint32_t *counter_unused;
-        Buckets b0 = carve_random(p->seed_scratch.ptr, max_seeds, &h0_unused, &counter_unused);
-        if (hipMemsetAsync(b0.count, 0, 256 * BUCKET_STRIDE * sizeof(uint32_t), ctx->stream) != hipSuccess)
-            rc = fail(NMZ_EHIP, "hipMemsetAsync of the seed scratch failed");
-    }
     if (rc != NMZ_OK) return cleanup(rc);
     Carve cv(p->table_mem.ptr);
     p->d_table = cv.take<uint4>((size_t)256 * E + 1);
@@ -549,8 +544,7 @@ static int random_run(nmz_random_plan *p, hipStream_t st, uint64_t seed0, uint64
     uint64_t *d_h0;
     uint32_t *d_counter;
     Buckets b = carve_random(p->seed_scratch.ptr, p->max_seeds, &d_h0, &d_counter);
-    hipLaunchKernelGGL(k_random_prefix, dim3(ceil_div(S, 256 * prefix_per_thread())), dim3(256), 0, st, seed0, S, d_h0,
-                       b.count, prefix_per_thread());
+    hipLaunchKernelGGL(k_random_prefix, dim3(ceil_div(S, BUCKET_BLK)), dim3(256), 0, st, seed0, S, d_h0, b.hist);
     const uint64_t max_units = S / 64 + 256;
     NMZ_TRY(bucket_seeds_counted(st, d_h0, S, 64, b, d_counter));
     const uint32_t ec = random_ec(S);

@@ -304,9 +304,9 @@ constexpr uint32_t SEED_LDS_BYTES = NMZ_SEED_LDS_BYTES;
 constexpr uint32_t SEED_LDS_MAX_SEEDS = NMZ_SEED_LDS_BYTES >= 16384 ? 256 * 16 : 256 * 8;
 __global__ __launch_bounds__(256) void k_seed_prefix(const uint32_t *__restrict__ soff,
                                                      const uint8_t *__restrict__ sbytes, uint64_t n,
-                                                     uint64_t *__restrict__ h0, uint32_t *__restrict__ count,
-                                                     uint32_t ppt) {
-    // fused bucket histogram (low byte of h0): LDS counts, one global atomic per (block, bucket)
+                                                     uint64_t *__restrict__ h0, uint32_t *__restrict__ rows) {
+    // fused bucket histogram (low byte of h0): LDS counts, stored as the block's row of `rows` (Buckets)
+    constexpr uint32_t ppt = BUCKET_PT;
     __shared__ uint32_t hist[256];
     __shared__ uint32_t so[SEED_LDS_BYTES ? SEED_LDS_MAX_SEEDS + 1 : 1];
     __shared__ uint32_t sb[SEED_LDS_BYTES ? SEED_LDS_BYTES / 4 : 1];
@@ -356,7 +356,7 @@ __global__ __launch_bounds__(256) void k_seed_prefix(const uint32_t *__restrict_
         }
     }
     __syncthreads();
-    if (hist[threadIdx.x]) atomicAdd(&count[threadIdx.x * BUCKET_STRIDE], hist[threadIdx.x]);
+    rows[(size_t)blockIdx.x * 256 + threadIdx.x] = hist[threadIdx.x];
 }
 
 // FNV over the 9 decimal digits of x (< 10^9), most significant first; leading zeros are hashed only once
@@ -392,9 +392,10 @@ __device__ __forceinline__ uint64_t fnv_decimal_u64(uint64_t h, uint64_t v) {
 // prefix hashes it (fnv_decimal_u64, ~300 VALU) into LDS once, then each seed takes its prefix's state and two FNV
 // steps (~25 VALU per seed instead of ~300). Seeds below 100, and a block whose range wraps past 2^64, hash
 // every seed in full.
-constexpr uint32_t DEC_MAX_PREFIX = 64;  // 256 ppt / 100 + 2 <= 64 for ppt <= 16
+constexpr uint32_t DEC_MAX_PREFIX = 64;  // 256 ppt / 100 + 2 <= 64 for ppt = BUCKET_PT <= 16
 __global__ __launch_bounds__(256) void k_seed_prefix_decimal(uint64_t seed_lo, uint64_t n, uint64_t *__restrict__ h0,
-                                                             uint32_t *__restrict__ count, uint32_t ppt) {
+                                                             uint32_t *__restrict__ rows) {
+    constexpr uint32_t ppt = BUCKET_PT;
     __shared__ uint32_t hist[256];
     __shared__ uint64_t ph[DEC_MAX_PREFIX];
     hist[threadIdx.x] = 0;
@@ -423,7 +424,7 @@ __global__ __launch_bounds__(256) void k_seed_prefix_decimal(uint64_t seed_lo, u
         }
     }
     __syncthreads();
-    if (hist[threadIdx.x]) atomicAdd(&count[threadIdx.x * BUCKET_STRIDE], hist[threadIdx.x]);
+    rows[(size_t)blockIdx.x * 256 + threadIdx.x] = hist[threadIdx.x];
 }
 
 // ---------------------------------------------------------------------------
@@ -1484,7 +1485,7 @@ static int oq_build(nmz_replayable_plan *p, const std::vector<ClassInfo> &cls, h
 static size_t seed_scratch_bytes(uint64_t S) {
     uint64_t max_units = S / REPLAY_SEEDS_PER_UNIT_MIN + 257;
     return Carve::bytes_for(S, 8) * 2 + Carve::bytes_for(S, 4) + Carve::bytes_for(BUCKET_SMALL_U32, 4) +
-           Carve::bytes_for(max_units, 16) + Carve::bytes_for(4, 4);
+           Carve::bytes_for(bucket_hist_u32(S), 4) + Carve::bytes_for(max_units, 16) + Carve::bytes_for(4, 4);
 }
 
 static size_t partial_bytes(uint64_t S, uint32_t E, int U, uint32_t ec) {
@@ -1506,6 +1507,7 @@ static SeedScratch carve_seed_scratch(void *p, uint64_t S) {
     s.b.sorted_h0 = cv.take<uint64_t>(S);
     s.b.sorted_idx = cv.take<uint32_t>(S);
     buckets_small(cv.take<uint32_t>(BUCKET_SMALL_U32), s.b);
+    s.b.hist = cv.take<uint32_t>(bucket_hist_u32(S));
     s.b.units = cv.take<uint4>(S / REPLAY_SEEDS_PER_UNIT_MIN + 257);
     s.counter = cv.take<uint32_t>(4);
     return s;
@@ -1538,7 +1540,7 @@ struct nmz_replayable_seeds {
     uint64_t S = 0;
     nmz::DevBuf mem;
     nmz::SeedScratch sc{};
-    uint32_t *hist = nullptr;  // [256 * BUCKET_STRIDE] the prefix kernel's row counts
+    uint32_t *hist = nullptr;  // [bucket_hist_u32(S)] the prefix kernel's rows of bucket counts
 };
 
 namespace nmz {
@@ -1562,15 +1564,15 @@ static int replayable_stats(nmz_replayable_plan *p, hipStream_t st, const uint32
         NMZ_CHECK(S <= p->max_seeds, "more seeds than the plan was created for");
         sc = carve_seed_scratch(p->seed_scratch.ptr, p->max_seeds);
         if (pre) {  // a per-decision sweep of prepared seeds: their hashes and row counts, bucketed here
-            NMZ_HIP(hipMemcpyAsync(sc.b.count, pre->hist, 256 * BUCKET_STRIDE * sizeof(uint32_t),
+            NMZ_HIP(hipMemcpyAsync(sc.b.hist, pre->hist, bucket_hist_u32(S) * sizeof(uint32_t),
                                    hipMemcpyDeviceToDevice, st));
             sc.h0 = pre->sc.h0;
         } else if (d_soff) {
-            hipLaunchKernelGGL(k_seed_prefix, dim3(ceil_div(S, 256 * prefix_per_thread())), dim3(256), 0, st, d_soff,
-                               d_sbytes, S, sc.h0, sc.b.count, prefix_per_thread());
+            hipLaunchKernelGGL(k_seed_prefix, dim3(ceil_div(S, BUCKET_BLK)), dim3(256), 0, st, d_soff, d_sbytes, S,
+                               sc.h0, sc.b.hist);
         } else {
-            hipLaunchKernelGGL(k_seed_prefix_decimal, dim3(ceil_div(S, 256 * prefix_per_thread())), dim3(256), 0, st,
-                               dec_lo, S, sc.h0, sc.b.count, prefix_per_thread());
+            hipLaunchKernelGGL(k_seed_prefix_decimal, dim3(ceil_div(S, BUCKET_BLK)), dim3(256), 0, st, dec_lo, S,
+                               sc.h0, sc.b.hist);
         }
     }
     const bool bucketed = pre && stats_kernel;
@@ -1783,10 +1785,9 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
     const bool seeds = E && p->mod.kind != MOD_ZERO;
     if (rc == NMZ_OK && seeds) {
         rc = p->seed_scratch.ensure(seed_scratch_bytes(max_seeds));
-        if (rc == NMZ_OK) {  // bucket counters and the work-item counter start at zero (k_bucket_scan re-zeroes)
+        if (rc == NMZ_OK) {  // the work-item counter starts at zero (k_bucket_scatter re-zeroes it)
             sc0 = carve_seed_scratch(p->seed_scratch.ptr, max_seeds);
-            if (!fused && (hipMemsetAsync(sc0.b.count, 0, 256 * BUCKET_STRIDE * sizeof(uint32_t), st) != hipSuccess ||
-                           hipMemsetAsync(sc0.counter, 0, 4 * sizeof(uint32_t), st) != hipSuccess))
+            if (!fused && hipMemsetAsync(sc0.counter, 0, 4 * sizeof(uint32_t), st) != hipSuccess)
                 rc = fail(NMZ_EHIP, "hipMemsetAsync of the seed scratch failed");
         }
     }
@@ -1840,8 +1841,7 @@ static int plan_create(nmz_ctx *ctx, const uint32_t *hint_off, const uint8_t *hi
             return cleanup(fail(NMZ_EHIP, "plan upload failed"));
         if (fused) {
             const WtPlanHints hz{d_hoff, d_hbytes, d_perm, p->d_table,
-                                 seeds ? sc0.b.count : nullptr, seeds ? 256 * BUCKET_STRIDE : 0u,
-                                 seeds ? sc0.counter : nullptr, seeds ? 4u : 0u};
+                                 nullptr, 0u, seeds ? sc0.counter : nullptr, seeds ? 4u : 0u};
             const int wrc = wt_launch(p->wt, p->d_table, E, p->mod, st, &hz, d_wcls, d_rowsum, !async);
             if (wrc != NMZ_OK) return cleanup(wrc);
         }
@@ -1914,7 +1914,7 @@ static int seeds_create_locked(nmz_ctx *ctx, const uint32_t *d_seed_off, const u
     s->S = n_seeds;
     s->mem.pool = &ctx->pool;  // a stream of seed sets of one size reuses one buffer (no hipMalloc per set)
     hipStream_t st = ctx->stream;
-    const int rc = s->mem.ensure(seed_scratch_bytes(n_seeds) + Carve::bytes_for(256 * BUCKET_STRIDE, 4));
+    const int rc = s->mem.ensure(seed_scratch_bytes(n_seeds) + Carve::bytes_for(bucket_hist_u32(n_seeds), 4));
     if (rc != NMZ_OK) {
         delete s;
         return rc;
@@ -1927,18 +1927,16 @@ static int seeds_create_locked(nmz_ctx *ctx, const uint32_t *d_seed_off, const u
         delete s;
         return fail(NMZ_EHIP, "seed set build failed");
     };
-    if (hipMemsetAsync(s->sc.b.count, 0, 256 * BUCKET_STRIDE * sizeof(uint32_t), st) != hipSuccess ||
-        hipMemsetAsync(s->sc.counter, 0, 4 * sizeof(uint32_t), st) != hipSuccess)
-        return fail_hip();
+    if (hipMemsetAsync(s->sc.counter, 0, 4 * sizeof(uint32_t), st) != hipSuccess) return fail_hip();
     if (d_seed_off)
-        hipLaunchKernelGGL(k_seed_prefix, dim3(ceil_div(n_seeds, 256 * prefix_per_thread())), dim3(256), 0, st,
-                           d_seed_off, d_seed_bytes, n_seeds, s->sc.h0, s->sc.b.count, prefix_per_thread());
+        hipLaunchKernelGGL(k_seed_prefix, dim3(ceil_div(n_seeds, BUCKET_BLK)), dim3(256), 0, st, d_seed_off,
+                           d_seed_bytes, n_seeds, s->sc.h0, s->sc.b.hist);
     else
-        hipLaunchKernelGGL(k_seed_prefix_decimal, dim3(ceil_div(n_seeds, 256 * prefix_per_thread())), dim3(256), 0,
-                           st, dec_lo, n_seeds, s->sc.h0, s->sc.b.count, prefix_per_thread());
+        hipLaunchKernelGGL(k_seed_prefix_decimal, dim3(ceil_div(n_seeds, BUCKET_BLK)), dim3(256), 0, st, dec_lo,
+                           n_seeds, s->sc.h0, s->sc.b.hist);
     if (hipGetLastError() != hipSuccess ||
-        hipMemcpyAsync(s->hist, s->sc.b.count, 256 * BUCKET_STRIDE * sizeof(uint32_t), hipMemcpyDeviceToDevice, st) !=
-            hipSuccess ||
+        hipMemcpyAsync(s->hist, s->sc.b.hist, bucket_hist_u32(n_seeds) * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                       st) != hipSuccess ||
         bucket_seeds_counted(st, s->sc.h0, n_seeds, OQ_WG, s->sc.b, s->sc.counter) != NMZ_OK ||
         hipStreamSynchronize(st) != hipSuccess)
         return fail_hip();

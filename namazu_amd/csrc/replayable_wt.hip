@@ -1102,28 +1102,50 @@ __global__ __launch_bounds__(256) void k_wt_topk_scan(const uint64_t *__restrict
     }
     __syncthreads();
     const unsigned long long t = tau_s;
-    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // the block's candidates of one round of PF sums per thread are counted in registers and block-scanned, and ONE
+    // returning atomic per block reserves their range: a returning atomic per candidate wave (the previous form,
+    // hundreds to thousands on one word at ~11 ns each) serialised the scan
+    __shared__ uint32_t wsum[4], base_s;
     for (uint64_t i0 = (uint64_t)blockIdx.x * 256; i0 < S; i0 += PF * stride) {
+        uint32_t flags = 0;
 #pragma unroll
         for (uint32_t r = 0; r < PF; ++r) {
             const uint64_t i = i0 + threadIdx.x + r * stride;
             if (i0 != (uint64_t)blockIdx.x * 256) v[r] = i < S ? sums[i] : 0ull;  // past the first PF rounds
             const unsigned long long key = v[r] ^ (1ull << 63);
-            const bool in = i < S && key >= t;
-            const uint64_t bal = __ballot(in);
-            if (!bal) continue;
-            const uint32_t first = __ffsll((unsigned long long)bal) - 1;
-            uint32_t base = 0;
-            if (lane == first) base = atomicAdd(&tk->n_cand, (uint32_t)__popcll(bal));
-            base = __shfl(base, first, 64);
-            if (in) {
-                const uint32_t pos = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
-                if (pos < WT_CAND) {
-                    tk->cand_key[pos] = key;
-                    tk->cand_idx[pos] = sorted_idx[i];
+            flags |= (i < S && key >= t) ? 1u << r : 0u;
+        }
+        const uint32_t n = __popc(flags);
+        uint32_t a = n;
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t x = __shfl_up(a, d, 64);
+            if (lane >= d) a += x;
+        }
+        if (lane == 63) wsum[w] = a;
+        __syncthreads();
+        uint32_t pre = 0, total = 0;
+        for (uint32_t x = 0; x < 4; ++x) {
+            pre += x < w ? wsum[x] : 0u;
+            total += wsum[x];
+        }
+        if (total) {
+            if (threadIdx.x == 0) base_s = atomicAdd(&tk->n_cand, total);
+            __syncthreads();
+            uint32_t pos = base_s + pre + a - n;
+#pragma unroll
+            for (uint32_t r = 0; r < PF; ++r) {
+                if (flags >> r & 1u) {
+                    if (pos < WT_CAND) {
+                        const uint64_t i = i0 + threadIdx.x + r * stride;
+                        tk->cand_key[pos] = v[r] ^ (1ull << 63);
+                        tk->cand_idx[pos] = sorted_idx[i];
+                    }
+                    ++pos;
                 }
             }
         }
+        __syncthreads();  // wsum and base_s are rewritten by the next round
     }
 }
 
