@@ -286,6 +286,25 @@ class Dist:
         return float(t.item())
 
 
+_HIP = []
+
+
+def _hip():
+    """The HIP runtime torch loaded (hipMemcpyAsync for the bench's own copies on the library's streams)."""
+    if not _HIP:
+        h = ctypes.CDLL("libamdhip64.so")
+        h.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                     ctypes.c_void_p]
+        h.hipMemcpyAsync.restype = ctypes.c_int
+        _HIP.append(h)
+    return _HIP[0]
+
+
+def hip_check(rc):
+    if rc != 0:
+        raise RuntimeError(f"HIP error {rc}")
+
+
 def merge_topk(entries, k):
     from namazu_amd.dist import merge_topk as _merge
     return _merge([entries], k)
@@ -305,20 +324,25 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     # Consecutive steps are pipelined over NP plans and HIP streams (NMZ_BENCH_PIPELINE, default 3): the
     # latency-bound kernels around one step's sweep (seed prefix, bucketing, top-k) and the tail of its persistent
     # sweep grid overlap the neighbouring steps. Every step does all of its work on its own batch.
+    # Each pipeline slot is its own context (nmz_open) and runs on that context's stream (nmz_ctx_stream): streams
+    # that share one of the process's hardware queues (GPU_MAX_HW_QUEUES, 4) dispatch in order, so a sweep waiting
+    # for the CUs another slot's sweep holds would stall the kernels queued behind it on the other slot -- measured
+    # 83 us per step with torch pool streams vs 59 with the contexts' own streams (tools/step_ab.py, 200 steps)
     NP = max(1, int(os.environ.get("NMZ_BENCH_PIPELINE", "3")))
     K_TOP = 64
     csr0 = decimal_csr(D.rank * S, S)  # timed step 0's seeds: the CPU baseline's sample and the end-to-end seeds
+    ctxs = [ctx] + [_lib.Context(D.local_rank) for _ in range(NP - 1)]
     plans = []
     t0 = time.time()
-    for _ in range(NP):
+    for sp in range(NP):
         plan = ctypes.c_void_p()
-        _lib.check(L.nmz_replayable_plan_create(ctx.handle, host_ptr(hoff), host_ptr(hb), E, MAX_INTERVAL_NS, S,
+        _lib.check(L.nmz_replayable_plan_create(ctxs[sp].handle, host_ptr(hoff), host_ptr(hb), E, MAX_INTERVAL_NS, S,
                                                 ctypes.byref(plan)))
         plans.append(plan)
     plan_ms = (time.time() - t0) * 1e3 / NP
     k1 = k1_kernel(L, plans[0])
     dev = torch.device("cuda", D.local_rank)
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(NP - 1)]
+    streams = [torch.cuda.ExternalStream(c.stream(), device=dev) for c in ctxs]
     d_stats = [torch.empty(S * 32, dtype=torch.uint8, device=dev) for _ in range(NP)]
     n_lists = max(args.steps, 1)
     d_lists = torch.empty(n_lists * K_TOP * 24, dtype=torch.uint8, device=dev)
@@ -345,12 +369,13 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     # seed ranges outside the job's for the untimed launches (warm-up, kernel timing)
     spare_lo = (args.steps + 1) * D.world * S + D.rank * S
 
+    torch.cuda.synchronize()  # the buffers above (allocated on torch's stream) before the contexts' streams use them
+
     def sweep(sp, lo, out_list):
-        with torch.cuda.stream(streams[sp]):
-            _lib.check(L.nmz_replayable_sweep_decimal_topk_dev(plans[sp], lo, S, K_TOP,
-                                                               ctypes.c_void_p(d_stats[sp].data_ptr()),
-                                                               ctypes.c_void_p(out_list),
-                                                               ctypes.c_void_p(streams[sp].cuda_stream)))
+        _lib.check(L.nmz_replayable_sweep_decimal_topk_dev(plans[sp], lo, S, K_TOP,
+                                                           ctypes.c_void_p(d_stats[sp].data_ptr()),
+                                                           ctypes.c_void_p(out_list),
+                                                           ctypes.c_void_p(streams[sp].cuda_stream)))
 
     def step(i):
         sweep(i % NP, (i * D.world + D.rank) * S, d_lists.data_ptr() + (i % n_lists) * K_TOP * 24)
@@ -386,11 +411,12 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     _lib.check(L.nmz_timing_read_span(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
     kern_ms_serial_span = tot.value / cnt.value if cnt.value else None
     _lib.check(L.nmz_timing_enable(ctx.handle, 0))
-    # the timed region: exactly args.steps pipelined steps + the job's merge; K1's launches are bracketed by HIP
-    # events on their own streams (nmz_timing_*), so the roofline's kernel time comes from these same launches
-    _lib.check(L.nmz_timing_enable(ctx.handle, 1 if timed_events else NMZ_TIMING_SPANS))
-    L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
-    L.nmz_timing_read_span(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
+    # the timed region: exactly args.steps pipelined steps + the job's merge; K1's launches record their spans
+    # (timing is per context: every slot's context records its own launches)
+    for c in ctxs:
+        _lib.check(L.nmz_timing_enable(c.handle, 1 if timed_events else NMZ_TIMING_SPANS))
+        L.nmz_timing_read(c.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
+        L.nmz_timing_read_span(c.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1)
     # the job's merges run on the stream of the last step (in order behind its top-k; the other slots' streams
     # finished earlier, so waiting for them costs no cross-queue round trip at the end)
     last = (args.steps - 1) % NP if args.steps else 0
@@ -426,7 +452,10 @@ def bench_replayable(args, torch, D, ctx, L, stream):
                                                 ctypes.c_void_p(d_scratch.data_ptr()),
                                                 ctypes.c_void_p(d_final.data_ptr()), sl))
                 fin = d_final
-            h_final.copy_(fin, non_blocking=True)
+            # the 1.5 KB answer to pinned host memory on the last slot's stream (a plain hipMemcpyAsync: torch's
+            # pinned allocator would record the library context's stream on the buffer)
+            hip_check(_hip().hipMemcpyAsync(ctypes.c_void_p(h_final.data_ptr()), ctypes.c_void_p(fin.data_ptr()),
+                                            ctypes.c_size_t(K_TOP * 24), 2, sl))
             done_ev.record()
             done_ev.synchronize()
             merged = np.frombuffer(h_final.numpy().tobytes(), dtype=_lib.TOPK_DTYPE).copy()
@@ -434,15 +463,19 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     D.barrier()
     el = time.perf_counter() - t0
     kern_ms_timed = None
+    ev_tot = ev_cnt = sp_tot = sp_cnt = 0
+    for c in ctxs:
+        if timed_events:
+            _lib.check(L.nmz_timing_read(c.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
+            ev_tot, ev_cnt = ev_tot + tot.value, ev_cnt + cnt.value
+        # the timed launches' execution spans as the kernel records them (first workgroup start to last workgroup
+        # end): a pipelined launch's HIP events would also time its wait for the CUs another stream's K1 holds
+        _lib.check(L.nmz_timing_read_span(c.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
+        sp_tot, sp_cnt = sp_tot + tot.value, sp_cnt + cnt.value
+        _lib.check(L.nmz_timing_enable(c.handle, 0))
     if timed_events:
-        _lib.check(L.nmz_timing_read(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
-        kern_ms_timed = tot.value / max(cnt.value, 1)
-    # the timed launches' execution spans as the kernel records them (first workgroup start to last workgroup end;
-    # the union over launches that overlap): a pipelined launch's HIP events would also time its wait for the CUs
-    # another stream's K1 holds
-    _lib.check(L.nmz_timing_read_span(ctx.handle, b"replayable_sweep", ctypes.byref(tot), ctypes.byref(cnt), 1))
-    kern_ms_span = tot.value / cnt.value if cnt.value else None
-    _lib.check(L.nmz_timing_enable(ctx.handle, 0))
+        kern_ms_timed = ev_tot / max(ev_cnt, 1)
+    kern_ms_span = sp_tot / sp_cnt if sp_cnt else None
     el_max = D.max(torch, el)
     # the job's answer, checked outside the timing: every step's list is the exact top-64 of its own range, so the
     # job's top-64 is the merge of those lists; timed step 0's stats (seeds "0".."S-1" on rank 0) for the CPU
@@ -464,6 +497,9 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     d_sb = [torch.from_numpy(csr0[1]).to(dev)]
     for plan in plans:
         L.nmz_replayable_plan_destroy(plan)
+    torch.cuda.synchronize()
+    for c in ctxs[1:]:
+        c.close()
     # configs[1] as stated, end to end: a new trace's plan (tables built and sorted from host hints) + one
     # 2^20-seed sweep with top-k + the copy of the top-k to the host, per trace
     e2e, e2e_plan, e2e_heads = [], [], []

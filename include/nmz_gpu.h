@@ -104,6 +104,10 @@ int nmz_close(nmz_ctx *ctx);
 const char *nmz_last_error(void); /* thread-local, valid until the next call on this thread */
 int nmz_abi_version(void);
 int nmz_device_count(int *count);
+/* The context's own stream (hipStream_t as void*): what a NULL stream argument of the *_dev entry points means.
+ * Each context's stream is created by the library (hipStreamCreateWithFlags), so contexts' streams are distinct
+ * streams a caller may pipeline over (one plan per stream) and order its own work against. */
+int nmz_ctx_stream(nmz_ctx *ctx, void **stream);
 
 /* Kernel timing (HIP events recorded on the launch stream around the dominant
  * kernels: "replayable_sweep", "random_sweep", "ed_tile"). on = 0 off, 1 events and

@@ -67,6 +67,7 @@ SIGNATURES = {
     "nmz_last_error": (ctypes.c_char_p, []),
     "nmz_abi_version": (_int, []),
     "nmz_device_count": (_int, [ctypes.POINTER(_int)]),
+    "nmz_ctx_stream": (_int, [_P, ctypes.POINTER(_P)]),
     "nmz_random_params_resolve": (_int, [_i64, _i64, ctypes.c_double, _P]),
     "nmz_fnv1a64_batch": (_int, [_P, _P, _P, _u64, _P]),
     "nmz_replayable_sweep": (_int, [_P, _P, _P, _u64, _P, _P, _u32, _i64, _P, _P, _u64, _u32, _P]),
@@ -216,6 +217,12 @@ class Context:
         check(self._lib.nmz_open(int(device), ctypes.byref(h)))
         self.handle = h
         self.device = device
+
+    def stream(self):
+        """The context's own HIP stream handle (int): what a NULL stream argument means."""
+        s = ctypes.c_void_p()
+        check(self._lib.nmz_ctx_stream(self.handle, ctypes.byref(s)))
+        return s.value
 
     def close(self):
         if self.handle:

@@ -314,6 +314,12 @@ int nmz_device_count(int *count) {
     return NMZ_OK;
 }
 
+int nmz_ctx_stream(nmz_ctx *ctx, void **stream) {
+    NMZ_CHECK(ctx != nullptr && stream != nullptr, "NULL argument");
+    *stream = ctx->stream;
+    return NMZ_OK;
+}
+
 int nmz_open(int device, nmz_ctx **out) {
     NMZ_CHECK(out != nullptr, "out is NULL");
     *out = nullptr;
@@ -371,8 +377,20 @@ int nmz_timing_enable(nmz_ctx *ctx, int on) {
     NMZ_CHECK(ctx != nullptr, "ctx is NULL");
     std::lock_guard<std::mutex> lk(ctx->mu);
     NMZ_CHECK(on >= 0 && on <= NMZ_TIMING_SPANS, "on must be 0, 1 or NMZ_TIMING_SPANS");
-    ctx->timing.enabled = on != 0;
-    ctx->timing.spans_only = on == NMZ_TIMING_SPANS;
+    NmzTiming &t = ctx->timing;
+    if (on && !t.span_dev) {  // the span slots now, not at a timed launch (hipMalloc synchronises the device)
+        DeviceRestore dr;
+        NMZ_HIP(hipSetDevice(ctx->device));
+        NMZ_HIP(hipMalloc(&t.span_dev, NMZ_SPAN_SLOTS * 16));
+        const hipError_t e = hipMemset(t.span_dev, 0, NMZ_SPAN_SLOTS * 16);
+        if (e != hipSuccess) {
+            (void)hipFree(t.span_dev);
+            t.span_dev = nullptr;
+            return fail(NMZ_EHIP, std::string("hipMemset of the span slots: ") + hipGetErrorString(e));
+        }
+    }
+    t.enabled = on != 0;
+    t.spans_only = on == NMZ_TIMING_SPANS;
     return NMZ_OK;
 }
 
