@@ -27,7 +27,6 @@ torch.distributed.run (one rank per GPU, RCCL).
 """
 import argparse
 import ctypes
-import gc
 import json
 import os
 import sys
@@ -354,7 +353,9 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     gathered = list(d_gath.view(D.world, K_TOP * 24).unbind(0)) if D.world > 1 else None
     d_final = torch.empty_like(d_job)
     h_final = torch.empty(K_TOP * 24, dtype=torch.uint8).pin_memory()
-    done_ev = torch.cuda.Event()
+    h_view = h_final.numpy()  # (a view made before the timing: reading the answer is a numpy copy)
+    done_ev = torch.cuda.Event(enable_timing=True)
+    start_ev = torch.cuda.Event(enable_timing=True)  # the GPU's own span of the timed region (vs the host clock)
     # the host merge of the job (one list per rank) is the check outside the timing; NMZ_BENCH_HOST_MERGE=1 times
     # it instead of the device merge (A/B)
     host_merge = os.environ.get("NMZ_BENCH_HOST_MERGE") == "1"
@@ -362,6 +363,7 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     # barrier packets on the last stream's queue) or "host" (the host waits for those streams, which end first, then
     # enqueues the merge: measured slower, 0.075-0.077 vs 0.070-0.071 ms per step -- the host's wake-up costs more)
     host_join = os.environ.get("NMZ_BENCH_JOIN", "event") == "host"
+    spin = os.environ.get("NMZ_BENCH_SPIN", "1") == "1"
     # the timed K1 launches record their own execution spans (in-kernel wall clock, no HIP event records between
     # a stream's launches: each record is a marker the queue stalls on, ~6 us at the step's ends);
     # NMZ_BENCH_TIMED_EVENTS=1 brackets them with HIP events as well (A/B of their cost)
@@ -423,9 +425,11 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     D.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    start_ev.record(streams[0])
     for i in range(args.steps):
         step(i)
     enq = time.perf_counter() - t0  # the host's enqueue time of the steps (host-bound pipeline when ~ el)
+    marks = {}
     if host_join:
         # the other slots' last steps end while the last step's sweep still runs: the host waits for them and
         # then enqueues the merge behind the last step, in order on its stream (no cross-queue barrier packet)
@@ -434,6 +438,7 @@ def bench_replayable(args, torch, D, ctx, L, stream):
                 streams[sp].synchronize()
     else:
         join(last)
+    marks["joined"] = time.perf_counter() - t0
     with torch.cuda.stream(streams[last]):
         sl = ctypes.c_void_p(streams[last].cuda_stream)
         _lib.check(L.nmz_topk_merge_dev(ctx.handle, ctypes.c_void_p(d_lists.data_ptr()), args.steps, K_TOP,
@@ -457,11 +462,28 @@ def bench_replayable(args, torch, D, ctx, L, stream):
             hip_check(_hip().hipMemcpyAsync(ctypes.c_void_p(h_final.data_ptr()), ctypes.c_void_p(fin.data_ptr()),
                                             ctypes.c_size_t(K_TOP * 24), 2, sl))
             done_ev.record()
+    marks["copy_enqueued"] = time.perf_counter() - t0
+    if not host_merge:
+        if spin:  # the host polls for the answer
+            while not done_ev.query():
+                pass
+        else:
             done_ev.synchronize()
-            merged = np.frombuffer(h_final.numpy().tobytes(), dtype=_lib.TOPK_DTYPE).copy()
+        marks["answer_seen"] = time.perf_counter() - t0
+        if os.environ.get("NMZ_BENCH_READ") == "string_at":  # A/B: the bytes through ctypes
+            merged = np.frombuffer(ctypes.string_at(h_final.data_ptr(), K_TOP * 24), dtype=_lib.TOPK_DTYPE)
+        else:
+            merged = h_view.view(_lib.TOPK_DTYPE).copy()
+    marks["answer_read"] = time.perf_counter() - t0
+    if os.environ.get("NMZ_BENCH_STREAM_SYNC") == "1":  # A/B: each slot's stream first
+        for st_ in streams:
+            st_.synchronize()
+        marks["streams_synced"] = time.perf_counter() - t0
     torch.cuda.synchronize()
+    marks["synchronized"] = time.perf_counter() - t0
     D.barrier()
     el = time.perf_counter() - t0
+    marks = {k: round(v * 1e6, 1) for k, v in marks.items()}
     kern_ms_timed = None
     ev_tot = ev_cnt = sp_tot = sp_cnt = 0
     for c in ctxs:
@@ -476,6 +498,7 @@ def bench_replayable(args, torch, D, ctx, L, stream):
     if timed_events:
         kern_ms_timed = ev_tot / max(ev_cnt, 1)
     kern_ms_span = sp_tot / sp_cnt if sp_cnt else None
+    gpu_ms = start_ev.elapsed_time(done_ev) if not host_merge else None
     el_max = D.max(torch, el)
     # the job's answer, checked outside the timing: every step's list is the exact top-64 of its own range, so the
     # job's top-64 is the merge of those lists; timed step 0's stats (seeds "0".."S-1" on rank 0) for the CPU
@@ -624,7 +647,7 @@ def bench_replayable(args, torch, D, ctx, L, stream):
                           agrees=heads == e2e_heads)
     return dict(S=S, E=E, hints=(hoff, hb), seeds=csr0, elapsed=el_max,
                 kern_ms=kern_ms, kern_ms_events=kern_ms_timed, kern_ms_serial_span=kern_ms_serial_span,
-                kern_ms_span=kern_ms_span, enqueue_ms=enq * 1e3, plan_ms=plan_ms, stats=stats, topk=merged, pipeline=NP, job_ok=job_ok,
+                kern_ms_span=kern_ms_span, enqueue_ms=enq * 1e3, gpu_ms=gpu_ms, host_marks_us=marks, plan_ms=plan_ms, stats=stats, topk=merged, pipeline=NP, job_ok=job_ok,
                 e2e_s=e2e, e2e_plan_s=e2e_plan, e2e_pipe=e2e_pipe, e2e_native=e2e_native, k1_kernel=k1)
 
 
@@ -1171,6 +1194,10 @@ def headline_line(args, torch, D, ctx, L, stream):
         # host time to enqueue the K steps (the timed region's first part): close to ms_per_step * K means the
         # host's launches, not the GPU, set the step
         "enqueue_ms": r["enqueue_ms"],
+        # the GPU's clock over the same region (HIP event before step 0 on the first slot's stream -> the event after
+        # the answer's copy): the rest of ms_per_step * K is the host's (first launch, wake-up after the last event)
+        "gpu_ms": r["gpu_ms"],
+        "host_marks_us": r["host_marks_us"],  # host clock from the region's start at each step of its end
         "steady_state":"value: one trace's resident plan (built once, before the timed region) sweeps a fresh seed "
                         "range every step, and the job's top-64 is merged on the device (+ RCCL all_gather for N > "
                         "1) inside the timing; end_to_end below builds a new trace's plan inside the timing",

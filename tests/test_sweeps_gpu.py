@@ -357,6 +357,37 @@ def test_replayable_topk_large_sweep(ctx, E, m, k):
     assert tk.tolist() == O.topk_from_stats(st, 10**12, k).tolist()
 
 
+@pytest.mark.parametrize("lo,S", [(0, 1 << 17), (3, 5000), (95, 1 << 17), (9_999_950, 1 << 17),
+                                  (10**12 + 37, 1 << 17), (2**64 - (1 << 17) - 250, 1 << 17),
+                                  (2**64 - 1000, 1 << 13), (123_400, 1_638_350)])
+def test_decimal_sweep_at_scale(ctx, lo, S):
+    """Decimal seed ranges (device-generated strings) of 5,000 to 1.6 M seeds: the bucketing's per-block count rows
+    (up to 800), their column scans and the scatter, vs the oracle over the decimal strings (wrapping past 2^64;
+    the largest case on its first 32,768 seeds), twice through one plan (nothing left from the first sweep); the
+    sweep's top-64 == the top-64 of its stats."""
+    import torch
+    L = _lib.load()
+    E, m, k = 512, 100_000_000, 64
+    hints = zk_hints(E, np.random.default_rng(lo % 1000 + S))
+    ho, hb = to_csr(hints)
+    plan = ctypes.c_void_p()
+    _lib.check(L.nmz_replayable_plan_create(ctx.handle, _lib.ptr(ho), _lib.ptr(hb), E, m, S, ctypes.byref(plan)))
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    d_st = torch.zeros(S * 32, dtype=torch.uint8, device="cuda")
+    d_tk = torch.zeros(k * 24, dtype=torch.uint8, device="cuda")
+    for _ in range(2):
+        _lib.check(L.nmz_replayable_sweep_decimal_topk_dev(plan, lo, S, k, ctypes.c_void_p(d_st.data_ptr()),
+                                                           ctypes.c_void_p(d_tk.data_ptr()), stream))
+    torch.cuda.synchronize()
+    L.nmz_replayable_plan_destroy(plan)
+    st = np.frombuffer(d_st.cpu().numpy().tobytes(), dtype=_lib.SCHED_STATS_DTYPE)
+    n_or = S if S <= (1 << 17) else 1 << 15
+    ost, _ = rep_oracle([str((lo + i) % 2**64) for i in range(n_or)], hints, m)
+    assert st[:n_or].tobytes() == ost.tobytes()
+    tk = np.frombuffer(d_tk.cpu().numpy().tobytes(), dtype=_lib.TOPK_DTYPE)
+    assert tk.tolist() == O.topk_from_stats(st, lo, k).tolist()
+
+
 @pytest.mark.parametrize("kind", ["csr", "decimal"])
 def test_replayable_seed_set(ab_knobs, ctx, monkeypatch, kind):
     """nmz_replayable_sweep_seeds_topk_dev over one prepared seed set (prefix hashes bucketed once) == the plain
