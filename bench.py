@@ -27,6 +27,7 @@ torch.distributed.run (one rank per GPU, RCCL).
 """
 import argparse
 import ctypes
+import gc
 import json
 import os
 import sys
