@@ -46,6 +46,14 @@ constexpr uint32_t SIG_MASK_ENT = 1024;       // entity masks (k_trace_sig MODE 
 #define NMZ_SIG_U 4
 #endif
 constexpr uint32_t SIG_U = NMZ_SIG_U;  // 64-element steps loaded together per wave
+#ifndef NMZ_SIG_PIPE
+#define NMZ_SIG_PIPE 2
+#endif
+#ifndef NMZ_SIG_UX
+#define NMZ_SIG_UX 4
+#endif
+constexpr int SIG_PIPE = NMZ_SIG_PIPE;  // PO modes: the rank-key gather mixed one step later (1) or after the
+                                       // batch's ranks (2) (k_trace_sig)
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t x) {
     x ^= x >> 33;
@@ -71,13 +79,20 @@ __global__ void k_rank_keys(ulonglong2 *__restrict__ keys) {
 
 // the pair (symbol s, rank r) -> two 64-bit summands: t = fmix64(s ^ ka(r)) and a second, different nonlinear
 // function of t and kb(r) (one more 64-bit multiply instead of another fmix64)
-__device__ __forceinline__ void mix2(uint64_t s, uint32_t r, const ulonglong2 *__restrict__ keys, uint64_t &a,
-                                     uint64_t &b) {
-    const ulonglong2 k = r < RANK_KEYS ? keys[r] : make_ulonglong2(rank_key_a(r), rank_key_b(r));
+__device__ __forceinline__ ulonglong2 rank_keys(uint32_t r, const ulonglong2 *__restrict__ keys) {
+    return r < RANK_KEYS ? keys[r] : make_ulonglong2(rank_key_a(r), rank_key_b(r));
+}
+
+__device__ __forceinline__ void mix2k(uint64_t s, ulonglong2 k, uint64_t &a, uint64_t &b) {
     const uint64_t t = fmix64(s ^ k.x);
     a = t;
     const uint64_t u = (t ^ k.y) * 0x94d049bb133111ebULL;
     b = u ^ (u >> 29);
+}
+
+__device__ __forceinline__ void mix2(uint64_t s, uint32_t r, const ulonglong2 *__restrict__ keys, uint64_t &a,
+                                     uint64_t &b) {
+    mix2k(s, rank_keys(r, keys), a, b);
 }
 
 // MODE 0: exact (rank = position); 1: PO, a lane's entity group from kbits ballots (one per bit of the id);
@@ -109,13 +124,21 @@ __global__ __launch_bounds__(256) void k_trace_sig(const uint64_t *__restrict__ 
     uint64_t acc1 = 0, acc2 = 0;
     uint32_t counted = 0;
     const uint64_t below = (1ULL << lane) - 1;
+    bool pend = false;  // SIG_PIPE: the previous step's element, its keys gathered, not yet mixed
+    uint64_t ps = 0;
+    ulonglong2 pk = make_ulonglong2(0ull, 0ull);
     // PO mode: SIG_U steps' loads in flight per wave (one step at a time, the rank step's LDS round trip and the
     // next load's latency did not overlap: 0.73 -> 0.65 ms for 100k x 2,048); exact mode one step (measured
     // 3 % slower with four)
-    constexpr uint32_t U = PO ? SIG_U : 1;
+    constexpr uint32_t U = PO ? SIG_U : NMZ_SIG_UX;
     for (uint64_t c0 = 0; c0 < n; c0 += 64 * U) {
       uint64_t sv[U];
       uint32_t ev[U];
+      ulonglong2 bk[U];  // SIG_PIPE 2: the batch's gathered keys, symbols and takes
+      uint64_t bs[U];
+      bool bt[U];
+#pragma unroll
+      for (uint32_t k = 0; k < U; ++k) bt[k] = false;
 #pragma unroll
       for (uint32_t k = 0; k < U; ++k) {
           const uint64_t ic = min(c0 + 64 * k + lane, n - 1);  // n > 0 here: a valid element
@@ -172,7 +195,26 @@ __global__ __launch_bounds__(256) void k_trace_sig(const uint64_t *__restrict__ 
             }
             }
         }
-        if (take) {
+        if (SIG_PIPE == 2) {
+            // the batch's ranks first (every step's keys gather in flight), the mixes after the batch
+            bk[k] = take ? rank_keys(rank, keys) : make_ulonglong2(0ull, 0ull);
+            bs[k] = s;
+            bt[k] = take;
+        } else if (PO && SIG_PIPE) {
+            // software pipeline: this step's keys[rank] gather is issued now and mixed one step later, so its
+            // latency overlaps the next step's LDS round trips (the rank chain) instead of stalling the wave
+            const ulonglong2 kk = take ? rank_keys(rank, keys) : make_ulonglong2(0ull, 0ull);
+            if (pend) {
+                uint64_t a, b;
+                mix2k(ps, pk, a, b);
+                acc1 += a;
+                acc2 += b;
+                counted += 1;
+            }
+            pend = take;
+            ps = s;
+            pk = kk;
+        } else if (take) {
             uint64_t a, b;
             mix2(s, rank, keys, a, b);
             acc1 += a;
@@ -180,6 +222,24 @@ __global__ __launch_bounds__(256) void k_trace_sig(const uint64_t *__restrict__ 
             counted += 1;
         }
       }
+      if (SIG_PIPE == 2) {
+#pragma unroll
+        for (uint32_t k = 0; k < U; ++k)
+            if (bt[k]) {
+                uint64_t a, b;
+                mix2k(bs[k], bk[k], a, b);
+                acc1 += a;
+                acc2 += b;
+                counted += 1;
+            }
+      }
+    }
+    if (PO && SIG_PIPE == 1 && pend) {
+        uint64_t a, b;
+        mix2k(ps, pk, a, b);
+        acc1 += a;
+        acc2 += b;
+        counted += 1;
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
