@@ -260,6 +260,78 @@ __device__ __forceinline__ void bv_block1(BvState<BvShape<W>::KF> &S, const uint
     }
 }
 
+// The one-query block with its Peq reads issued NMZ_ED_PF columns ahead. Column t's rows depend only on the block's
+// symbols, but bv_block1 reads each column's rows one column before its step, so a chain-bound wave (a sparse
+// shard's DP: ~1 wave per SIMD) waits most of an LDS round trip in every column. Here a compact store's symbols are
+// mapped to row offsets once per block (sym is overwritten: the caller replaces it with the next block), then a ring
+// of PF columns' rows stays in flight ahead of the step. Under the kernel's 96-VGPR cap (5 waves/SIMD) PF = 3 adds no
+// spill to the direct-table kernels (PF 4: 14 more scratch ops outside the block, PF 6: 6 inside it); with compact
+// tables the in-place row mapping spills (47 scratch ops at PF 3 against 14), so those keep bv_block1 unless
+// NMZ_ED_PF_CMP=1 (an A/B build).
+#ifndef NMZ_ED_PF
+#define NMZ_ED_PF 3
+#endif
+#ifndef NMZ_ED_PF_CMP
+#define NMZ_ED_PF_CMP 0
+#endif
+#ifndef NMZ_ED_PF_SB
+#define NMZ_ED_PF_SB 0
+#endif
+#if NMZ_ED_PF > 0
+template <int W>
+__device__ __forceinline__ void bv_fetch1(uint32_t (&d)[BvShape<W>::ND], const uint32_t *peq_bytes, uint32_t addr) {
+    const uint32_t *pp = (const uint32_t *)((const char *)peq_bytes + addr);
+#pragma unroll
+    for (int k = 0; k < BvShape<W>::ND; ++k) d[k] = pp[2 * k];
+}
+
+template <int W, int PF, bool SLOW, int t>
+__device__ __forceinline__ void bv_cols1(BvState<BvShape<W>::KF> &S, uint32_t (&ring)[PF][BvShape<W>::ND],
+                                         const uint32_t *peq, const uint32_t (&sym)[16], uint32_t base, uint32_t j0,
+                                         uint32_t m, uint32_t n, bool &run, uint32_t &r, uint32_t w1) {
+    if constexpr (t < 32) {
+        using SH = BvShape<W>;
+        uint32_t d[SH::ND];
+#pragma unroll
+        for (int k = 0; k < SH::ND; ++k) d[k] = ring[t % PF][k];
+        if constexpr (t + PF < 32) {
+            const uint32_t w = sym[(t + PF) / 2];
+            bv_fetch1<W>(ring[t % PF], peq, (((t + PF) & 1) ? (w >> 16) : (w & 0xffffu)) + base);
+#if NMZ_ED_PF_SB
+            __builtin_amdgcn_sched_barrier(0);  // keep the reads here (the scheduler sinks them to their use)
+#endif
+        }
+        bv_column<W, t>(S, d);
+        if constexpr (SLOW) {
+            if (j0 + t + 1 == m && run) {
+                const uint32_t Tj = S.T + (t + 1) - __builtin_popcount(S.acc >> (31 - t));
+                r = min(bv_extract<W>(S, Tj, n + W - m), w1);
+                run = false;
+            }
+        }
+        bv_cols1<W, PF, SLOW, t + 1>(S, ring, peq, sym, base, j0, m, n, run, r, w1);
+    }
+}
+
+template <int W, bool CMP, bool SLOW>
+__device__ __forceinline__ void bv_block1_pf(BvState<BvShape<W>::KF> &S, const uint32_t *peq, const uint16_t *rmap,
+                                             uint32_t (&sym)[16], uint32_t base, uint32_t j0, uint32_t m, uint32_t n,
+                                             bool &run, uint32_t &r, uint32_t w1) {
+    constexpr int PF = NMZ_ED_PF;
+    if constexpr (CMP) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sym[i] = (uint32_t)rmap[sym[i] & 0xffffu] | ((uint32_t)rmap[sym[i] >> 16] << 16);
+    }
+    uint32_t ring[PF][BvShape<W>::ND];
+#pragma unroll
+    for (int t = 0; t < PF; ++t) {
+        const uint32_t w = sym[t / 2];
+        bv_fetch1<W>(ring[t], peq, ((t & 1) ? (w >> 16) : (w & 0xffffu)) + base);
+    }
+    bv_cols1<W, PF, SLOW, 0>(S, ring, peq, sym, base, j0, m, n, run, r, w1);
+}
+#endif
+
 // rmap: the compact tables' map symbol id -> row byte offset (LDS, CMP only)
 template <int W, bool CMP, bool SLOW, int t = 0>
 __device__ __forceinline__ void bv_block(BvState<BvShape<W>::KF> &S1, BvState<BvShape<W>::KF> &S2,
@@ -577,10 +649,21 @@ __device__ __forceinline__ void bv_dp_mono(const EdBvArgs &A, const uint32_t *pe
         bv_load_block(nxt, stream, kb + 1);  // streams carry one spare block
         const uint32_t j0 = 32 * kb, base = (kb + 1) * 8 + 4 * sq;
         const bool here = active && run && m > j0 && m <= j0 + 32;
-        if (__any(here)) {
-            bv_block1<W, CMP, true>(S, peq, rmap, cur, base, j0, m, n, run, r, w1);
-        } else {
-            bv_block1<W, CMP, false>(S, peq, rmap, cur, base, j0, m, n, run, r, w1);
+#if NMZ_ED_PF > 0
+        if constexpr (!CMP || NMZ_ED_PF_CMP) {
+            if (__any(here)) {
+                bv_block1_pf<W, CMP, true>(S, peq, rmap, cur, base, j0, m, n, run, r, w1);
+            } else {
+                bv_block1_pf<W, CMP, false>(S, peq, rmap, cur, base, j0, m, n, run, r, w1);
+            }
+        } else
+#endif
+        {
+            if (__any(here)) {
+                bv_block1<W, CMP, true>(S, peq, rmap, cur, base, j0, m, n, run, r, w1);
+            } else {
+                bv_block1<W, CMP, false>(S, peq, rmap, cur, base, j0, m, n, run, r, w1);
+            }
         }
         S.T += 32 - __builtin_popcount(S.acc);
         if (run && bv_lower_bound<W>(S, S.T) > w) run = false;
