@@ -332,6 +332,76 @@ __device__ __forceinline__ void bv_block1_pf(BvState<BvShape<W>::KF> &S, const u
 }
 #endif
 
+// The two-query block (bv_dp_run's lanes: both queries of the pair per candidate) with its Peq reads issued
+// NMZ_ED_PF2 columns ahead (direct tables; 0 = bv_block, which reads each column one column before its step). The
+// paired loop runs at 5 waves per SIMD, so other waves cover most of the LDS latency: configs[2] clustered leg
+// 73.5 -> 71.5 ms at 2 (r06z, 2 runs each), 74.1 ms at 3 (50 more scratch ops outside the block); compact tables
+// keep bv_block (their symbols need the row map first).
+#ifndef NMZ_ED_PF2
+#define NMZ_ED_PF2 2
+#endif
+#if NMZ_ED_PF2 > 0
+template <int W>
+__device__ __forceinline__ void bv_fetch2(uint2 (&d)[BvShape<W>::ND], const uint32_t *peq_bytes, uint32_t addr) {
+    const uint2 *pp = (const uint2 *)((const char *)peq_bytes + addr);
+#pragma unroll
+    for (int k = 0; k < BvShape<W>::ND; ++k) d[k] = pp[k];
+}
+
+template <int W, int PF, bool SLOW, int t>
+__device__ __forceinline__ void bv_cols2(BvState<BvShape<W>::KF> &S1, BvState<BvShape<W>::KF> &S2,
+                                         uint2 (&ring)[PF][BvShape<W>::ND], const uint32_t *peq,
+                                         const uint32_t (&sym)[16], uint32_t base, uint32_t j0, uint32_t m,
+                                         uint32_t n1, uint32_t n2, bool &run1, bool &run2, uint32_t &r1,
+                                         uint32_t &r2, uint32_t w1) {
+    if constexpr (t < 32) {
+        using SH = BvShape<W>;
+        uint32_t d1[SH::ND], d2[SH::ND];
+#pragma unroll
+        for (int k = 0; k < SH::ND; ++k) {
+            d1[k] = ring[t % PF][k].x;
+            d2[k] = ring[t % PF][k].y;
+        }
+        if constexpr (t + PF < 32) {
+            const uint32_t w = sym[(t + PF) / 2];
+            bv_fetch2<W>(ring[t % PF], peq, (((t + PF) & 1) ? (w >> 16) : (w & 0xffffu)) + base);
+        }
+        bv_column<W, t>(S1, d1);
+        bv_column<W, t>(S2, d2);
+        if constexpr (SLOW) {
+            if (j0 + t + 1 == m) {
+                if (run1) {
+                    const uint32_t Tj = S1.T + (t + 1) - __builtin_popcount(S1.acc >> (31 - t));
+                    r1 = min(bv_extract<W>(S1, Tj, n1 + W - m), w1);
+                    run1 = false;
+                }
+                if (run2) {
+                    const uint32_t Tj = S2.T + (t + 1) - __builtin_popcount(S2.acc >> (31 - t));
+                    r2 = min(bv_extract<W>(S2, Tj, n2 + W - m), w1);
+                    run2 = false;
+                }
+            }
+        }
+        bv_cols2<W, PF, SLOW, t + 1>(S1, S2, ring, peq, sym, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
+    }
+}
+
+template <int W, bool SLOW>
+__device__ __forceinline__ void bv_block_pf(BvState<BvShape<W>::KF> &S1, BvState<BvShape<W>::KF> &S2,
+                                            const uint32_t *peq, const uint32_t (&sym)[16], uint32_t base,
+                                            uint32_t j0, uint32_t m, uint32_t n1, uint32_t n2, bool &run1,
+                                            bool &run2, uint32_t &r1, uint32_t &r2, uint32_t w1) {
+    constexpr int PF = NMZ_ED_PF2;
+    uint2 ring[PF][BvShape<W>::ND];
+#pragma unroll
+    for (int t = 0; t < PF; ++t) {
+        const uint32_t w = sym[t / 2];
+        bv_fetch2<W>(ring[t], peq, ((t & 1) ? (w >> 16) : (w & 0xffffu)) + base);
+    }
+    bv_cols2<W, PF, SLOW, 0>(S1, S2, ring, peq, sym, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
+}
+#endif
+
 // rmap: the compact tables' map symbol id -> row byte offset (LDS, CMP only)
 template <int W, bool CMP, bool SLOW, int t = 0>
 __device__ __forceinline__ void bv_block(BvState<BvShape<W>::KF> &S1, BvState<BvShape<W>::KF> &S2,
@@ -591,10 +661,21 @@ __device__ __forceinline__ void bv_dp_run(const EdBvArgs &A, const uint32_t *peq
         const uint32_t j0 = 32 * lkb;
         const uint32_t base = (lkb + 1) * 8;
         const bool here = active && (run1 || run2) && m > j0 && m <= j0 + 32;
-        if (__any(here)) {
-            bv_block<W, CMP, true>(S1, S2, peq, rmap, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
-        } else {
-            bv_block<W, CMP, false>(S1, S2, peq, rmap, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
+#if NMZ_ED_PF2 > 0
+        if constexpr (!CMP) {
+            if (__any(here)) {
+                bv_block_pf<W, true>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
+            } else {
+                bv_block_pf<W, false>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
+            }
+        } else
+#endif
+        {
+            if (__any(here)) {
+                bv_block<W, CMP, true>(S1, S2, peq, rmap, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
+            } else {
+                bv_block<W, CMP, false>(S1, S2, peq, rmap, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
+            }
         }
         S1.T += 32 - __builtin_popcount(S1.acc);
         S2.T += 32 - __builtin_popcount(S2.acc);
@@ -1166,10 +1247,21 @@ __global__ __launch_bounds__(256) void k_ed_bv_query(EdBvQueryArgs A) {
         const uint32_t j0 = 32 * lkb;
         const uint32_t base = (lkb + 1) * 8;
         const bool here = active && (run1 || run2) && m > j0 && m <= j0 + 32;
-        if (__any(here)) {
-            bv_block<W, CMP, true>(S1, S2, peq, rmap, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
-        } else {
-            bv_block<W, CMP, false>(S1, S2, peq, rmap, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
+#if NMZ_ED_PF2 > 0
+        if constexpr (!CMP) {
+            if (__any(here)) {
+                bv_block_pf<W, true>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
+            } else {
+                bv_block_pf<W, false>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
+            }
+        } else
+#endif
+        {
+            if (__any(here)) {
+                bv_block<W, CMP, true>(S1, S2, peq, rmap, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
+            } else {
+                bv_block<W, CMP, false>(S1, S2, peq, rmap, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
+            }
         }
         S1.T += 32 - __builtin_popcount(S1.acc);
         S2.T += 32 - __builtin_popcount(S2.acc);
