@@ -333,12 +333,17 @@ __device__ __forceinline__ void bv_block1_pf(BvState<BvShape<W>::KF> &S, const u
 #endif
 
 // The two-query block (bv_dp_run's lanes: both queries of the pair per candidate) with its Peq reads issued
-// NMZ_ED_PF2 columns ahead (direct tables; 0 = bv_block, which reads each column one column before its step). The
+// NMZ_ED_PF2 columns ahead (0 = bv_block, which reads each column one column before its step). The
 // paired loop runs at 5 waves per SIMD, so other waves cover most of the LDS latency: configs[2] clustered leg
-// 73.5 -> 71.5 ms at 2 (r06z, 2 runs each), 74.1 ms at 3 (50 more scratch ops outside the block); compact tables
-// keep bv_block (their symbols need the row map first).
+// 73.5 -> 71.5 ms at 2 (r06z, 2 runs each), 74.1 ms at 3 (50 more scratch ops outside the block). Compact tables
+// map each symbol to its row offset PF columns before that column's read (a ring of PF offsets; mapping the whole
+// block in place spilled 26 scratch ops into the block): configs[2] 3,572-symbol store 81.0 -> 75.5 ms (r06ac).
+// NMZ_ED_PF2_CMP=0 keeps bv_block for compact tables (an A/B build).
 #ifndef NMZ_ED_PF2
 #define NMZ_ED_PF2 2
+#endif
+#ifndef NMZ_ED_PF2_CMP
+#define NMZ_ED_PF2_CMP 1
 #endif
 #if NMZ_ED_PF2 > 0
 template <int W>
@@ -348,11 +353,31 @@ __device__ __forceinline__ void bv_fetch2(uint2 (&d)[BvShape<W>::ND], const uint
     for (int k = 0; k < BvShape<W>::ND; ++k) d[k] = pp[k];
 }
 
-template <int W, int PF, bool SLOW, int t>
+template <int t>
+__device__ __forceinline__ uint32_t bv_sym_at(const uint32_t (&sym)[16]) {
+    const uint32_t w = sym[t / 2];
+    return (t & 1) ? (w >> 16) : (w & 0xffffu);
+}
+
+// the first PF columns' reads (and, compact tables, the next PF columns' row offsets)
+template <int W, bool CMP, int PF, int t>
+__device__ __forceinline__ void bv_block_pf_pro(uint2 (&ring)[PF][BvShape<W>::ND], uint32_t (&ra)[PF],
+                                                const uint32_t *peq, const uint16_t *rmap, const uint32_t (&sym)[16],
+                                                uint32_t base) {
+    if constexpr (t < PF) {
+        const uint32_t s = bv_sym_at<t>(sym);
+        bv_fetch2<W>(ring[t], peq, (CMP ? (uint32_t)rmap[s] : s) + base);
+        if constexpr (CMP) ra[t] = rmap[bv_sym_at<t + PF>(sym)];
+        bv_block_pf_pro<W, CMP, PF, t + 1>(ring, ra, peq, rmap, sym, base);
+    }
+}
+
+// (compact tables: ra holds the row offsets of the next PF columns to fetch, mapped PF columns before their fetch)
+template <int W, bool CMP, int PF, bool SLOW, int t>
 __device__ __forceinline__ void bv_cols2(BvState<BvShape<W>::KF> &S1, BvState<BvShape<W>::KF> &S2,
-                                         uint2 (&ring)[PF][BvShape<W>::ND], const uint32_t *peq,
-                                         const uint32_t (&sym)[16], uint32_t base, uint32_t j0, uint32_t m,
-                                         uint32_t n1, uint32_t n2, bool &run1, bool &run2, uint32_t &r1,
+                                         uint2 (&ring)[PF][BvShape<W>::ND], uint32_t (&ra)[PF], const uint32_t *peq,
+                                         const uint16_t *rmap, const uint32_t (&sym)[16], uint32_t base, uint32_t j0,
+                                         uint32_t m, uint32_t n1, uint32_t n2, bool &run1, bool &run2, uint32_t &r1,
                                          uint32_t &r2, uint32_t w1) {
     if constexpr (t < 32) {
         using SH = BvShape<W>;
@@ -363,8 +388,8 @@ __device__ __forceinline__ void bv_cols2(BvState<BvShape<W>::KF> &S1, BvState<Bv
             d2[k] = ring[t % PF][k].y;
         }
         if constexpr (t + PF < 32) {
-            const uint32_t w = sym[(t + PF) / 2];
-            bv_fetch2<W>(ring[t % PF], peq, (((t + PF) & 1) ? (w >> 16) : (w & 0xffffu)) + base);
+            bv_fetch2<W>(ring[t % PF], peq, (CMP ? ra[t % PF] : bv_sym_at<t + PF>(sym)) + base);
+            if constexpr (CMP && t + 2 * PF < 32) ra[t % PF] = rmap[bv_sym_at<t + 2 * PF>(sym)];
         }
         bv_column<W, t>(S1, d1);
         bv_column<W, t>(S2, d2);
@@ -382,23 +407,21 @@ __device__ __forceinline__ void bv_cols2(BvState<BvShape<W>::KF> &S1, BvState<Bv
                 }
             }
         }
-        bv_cols2<W, PF, SLOW, t + 1>(S1, S2, ring, peq, sym, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
+        bv_cols2<W, CMP, PF, SLOW, t + 1>(S1, S2, ring, ra, peq, rmap, sym, base, j0, m, n1, n2, run1, run2, r1, r2,
+                                          w1);
     }
 }
 
-template <int W, bool SLOW>
+template <int W, bool CMP, bool SLOW>
 __device__ __forceinline__ void bv_block_pf(BvState<BvShape<W>::KF> &S1, BvState<BvShape<W>::KF> &S2,
-                                            const uint32_t *peq, const uint32_t (&sym)[16], uint32_t base,
-                                            uint32_t j0, uint32_t m, uint32_t n1, uint32_t n2, bool &run1,
-                                            bool &run2, uint32_t &r1, uint32_t &r2, uint32_t w1) {
+                                            const uint32_t *peq, const uint16_t *rmap, const uint32_t (&sym)[16],
+                                            uint32_t base, uint32_t j0, uint32_t m, uint32_t n1, uint32_t n2,
+                                            bool &run1, bool &run2, uint32_t &r1, uint32_t &r2, uint32_t w1) {
     constexpr int PF = NMZ_ED_PF2;
     uint2 ring[PF][BvShape<W>::ND];
-#pragma unroll
-    for (int t = 0; t < PF; ++t) {
-        const uint32_t w = sym[t / 2];
-        bv_fetch2<W>(ring[t], peq, ((t & 1) ? (w >> 16) : (w & 0xffffu)) + base);
-    }
-    bv_cols2<W, PF, SLOW, 0>(S1, S2, ring, peq, sym, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
+    uint32_t ra[PF];
+    bv_block_pf_pro<W, CMP, PF, 0>(ring, ra, peq, rmap, sym, base);
+    bv_cols2<W, CMP, PF, SLOW, 0>(S1, S2, ring, ra, peq, rmap, sym, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
 }
 #endif
 
@@ -662,11 +685,11 @@ __device__ __forceinline__ void bv_dp_run(const EdBvArgs &A, const uint32_t *peq
         const uint32_t base = (lkb + 1) * 8;
         const bool here = active && (run1 || run2) && m > j0 && m <= j0 + 32;
 #if NMZ_ED_PF2 > 0
-        if constexpr (!CMP) {
+        if constexpr (!CMP || NMZ_ED_PF2_CMP) {
             if (__any(here)) {
-                bv_block_pf<W, true>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
+                bv_block_pf<W, CMP, true>(S1, S2, peq, rmap, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
             } else {
-                bv_block_pf<W, false>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
+                bv_block_pf<W, CMP, false>(S1, S2, peq, rmap, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
             }
         } else
 #endif
@@ -1248,11 +1271,11 @@ __global__ __launch_bounds__(256) void k_ed_bv_query(EdBvQueryArgs A) {
         const uint32_t base = (lkb + 1) * 8;
         const bool here = active && (run1 || run2) && m > j0 && m <= j0 + 32;
 #if NMZ_ED_PF2 > 0
-        if constexpr (!CMP) {
+        if constexpr (!CMP || NMZ_ED_PF2_CMP) {
             if (__any(here)) {
-                bv_block_pf<W, true>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
+                bv_block_pf<W, CMP, true>(S1, S2, peq, rmap, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
             } else {
-                bv_block_pf<W, false>(S1, S2, peq, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
+                bv_block_pf<W, CMP, false>(S1, S2, peq, rmap, cur, base, j0, m, n1, n2, run1, run2, r1, r2, w1);
             }
         } else
 #endif
