@@ -6,7 +6,8 @@ work chunk) one after the other on one device and records, per shard, the kernel
 k_ed_bv's executed-block counter. The job finishes when the slowest rank does, so max / mean of these is
 the dealing's loss at n_shards GPUs. ED_BAL_ORDER=reverse runs the shards last to first (separates a trend over
 the run, e.g. the clock, from one over the shard index); ED_BAL_REPS=r times each shard r times back to back and
-keeps the last. usage: ed_shard_balance.py [generator] [n_shards] > out.json
+keeps the last. The record's "uninstrumented" block times every search again with the library's timing off (two
+events around ED_BAL_OUTER back-to-back searches): the bound without the per-phase event markers. usage: ed_shard_balance.py [generator] [n_shards] > out.json
 """
 import ctypes
 import json
@@ -67,8 +68,39 @@ def main():
         rows.append({"shard": s, "kernel_ms": tot.value, "filter_ms": ph[b"ed_qg_filter"][0].value,
                      "dp_ms": ph[b"ed_bv_dp"][0].value, "dp_pairs": int(cnt[0]), "blocks": int(cnt[2]),
                      "in_band": int(cnt[1])})
-    L.nmz_ed_plan_destroy(plan)
     rows.sort(key=lambda r: r["shard"])
+    # The same searches with the library's timing off, each timed from outside: two events around ED_BAL_OUTER
+    # back-to-back searches on the search's own stream. The instrumented pass above records an event pair per
+    # timed phase inside every search (each record a queue marker of ~6 us): a fixed cost that 8 shards pay 8
+    # times and the unsharded search once, which an 8-GPU job without timing does not pay at all.
+    _lib.check(L.nmz_timing_enable(ctx.handle, 0))
+    n_outer = max(1, int(os.environ.get("ED_BAL_OUTER", "4")))
+
+    # (`stream` is torch's default stream, handle 0: the library then runs on its context's own stream, which the
+    # events must bracket)
+    cst = torch.cuda.ExternalStream(ctx.stream()) if stream.value is None else torch.cuda.current_stream()
+
+    def outer(s, n_sh):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(cst)
+        for _ in range(n_outer):
+            _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, s, n_sh, ctypes.c_void_p(d.data_ptr()), stream))
+        e1.record(cst)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / n_outer
+
+    u0 = outer(0, 1)
+    for r in rows:
+        r["outer_ms"] = outer(r["shard"], S)
+    u1 = outer(0, 1)  # again after the shards: a drift check
+    L.nmz_ed_plan_destroy(plan)
+    om = np.array([r["outer_ms"] for r in rows])
+    u = (u0 + u1) / 2
+    uninstrumented = {"unsharded_ms": u, "unsharded_ms_before_after": [u0, u1], "max_shard_ms": float(om.max()),
+                      "sum_shard_ms": float(om.sum()), "sum_over_unsharded": float(om.sum() / u),
+                      "time_max_over_mean": float(om.max() / om.mean()), "speedup_bound": float(u / om.max()),
+                      "searches_per_timing": n_outer}
     ms = np.array([r["kernel_ms"] for r in rows])
     bl = np.array([r["blocks"] for r in rows], np.float64)
     print(json.dumps({"generator": gen, "traces": N, "events": Lx, "band": w, "shards": S, "per_shard": rows,
@@ -78,7 +110,8 @@ def main():
                       "max_shard_ms": float(ms.max()), "speedup_bound": float(full_ms / ms.max()),
                       "item": int(os.environ.get("NMZ_ED_ITEM", "4096")),
                       "deal": os.environ.get("NMZ_ED_DEAL", "snake"),
-                      "order": "reverse" if order[0] else "forward", "reps": reps}, indent=1))
+                      "order": "reverse" if order[0] else "forward", "reps": reps,
+                      "uninstrumented": uninstrumented}, indent=1))
 
 
 if __name__ == "__main__":
