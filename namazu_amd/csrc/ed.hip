@@ -24,6 +24,8 @@
 // Generic path (k_ed_generic): one thread per pair, any band, u64 symbols,
 // band row in global scratch. Used for nmz_ed_pairs and as the fallback.
 #include <algorithm>
+#include <chrono>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -341,6 +343,14 @@ __global__ void k_knn_init(uint64_t *knn, uint64_t n) {
     if (i < n) knn[i] = UINT64_MAX;
 }
 
+// a search's start: its k-NN lists and (bit-parallel plans) the work counters in one launch (a separate memset of
+// the counters was one more queue entry per search, ~5 us: a shard of a sharded search pays it once per shard)
+__global__ void k_knn_init_cnt(uint64_t *knn, uint64_t n, uint64_t *counters, uint32_t n_cnt) {
+    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) knn[i] = UINT64_MAX;
+    if (counters && i < n_cnt) counters[i] = 0;
+}
+
 __global__ void k_knn_final(const uint64_t *__restrict__ knn, uint64_t n, uint32_t *__restrict__ ids,
                             uint32_t *__restrict__ ds) {
     uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -446,11 +456,12 @@ struct nmz_ed_plan {
     uint32_t *d_tp_mismatch = nullptr;     // (in tp_mem) set when a search's totals differ from tp_sizes
     uint64_t tp_mem_gen = 0, tp_rec_gen = 0;  // DevBuf::gen of tp_mem / tp_rec when their counters were last cleared
     bool tp_dirty = false;                 // a count pass's counts not yet taken back by its write pass
-    // the mismatch flag as of the last search enqueued with cached sizes: copied to pinned host memory behind an
-    // event, read (ed_tp_flag_check) by the shard's next search without waiting, or with a wait by the synchronous
-    // entry points (nmz_ed_plan_counters, the group search)
+    // the mismatch flag as of the last search enqueued with cached sizes: that search's offsets scan writes {its
+    // sequence number, the flag} to these pinned words, read (ed_tp_flag_check) by the shard's next search without
+    // waiting once the number has landed, or read from the device with a wait by the synchronous entry points
+    // (nmz_ed_plan_counters, the group search)
     uint32_t *h_tp_flag = nullptr;
-    hipEvent_t tp_flag_ev = nullptr;
+    uint32_t tp_seq = 0;
     bool tp_flag_armed = false;
     // fixed at creation (NMZ_ED_QGRAM / NMZ_ED_TWO_PHASE, A/B knobs read once per plan), so every shard and every
     // call of one plan takes the same search and deals pairs by the same rule
@@ -1113,6 +1124,8 @@ struct TpScanArgs {
     uint32_t *flag;         // or nullptr: no cached sizes to compare
     uint64_t e_tot;
     uint32_t e_items, e_rec;
+    uint32_t *h_flag;       // with flag: pinned host words {seq, flag} the check publishes (ed_tp_flag_check)
+    uint32_t seq;
 };
 
 __device__ __forceinline__ uint32_t tp_items(uint32_t c, uint32_t lg) { return (c + (1u << lg) - 1) >> lg; }
@@ -1230,7 +1243,16 @@ __global__ __launch_bounds__(256) void k_tp_scan(TpScanArgs A) {
             A.ioff[A.n] = (uint32_t)ci;
             *A.tot64 = ce;
             if (A.n_rec) *A.rec_out = r;
-            if (A.flag && (ce != A.e_tot || (uint32_t)ci != A.e_items || r != A.e_rec)) atomicOr(A.flag, 1u);
+            if (A.flag) {
+                if (ce != A.e_tot || (uint32_t)ci != A.e_items || r != A.e_rec) atomicOr(A.flag, 1u);
+                // the device flag as it now stands (sticky until reported) to the host, then the search's sequence
+                // number: the host reads the flag once it sees the number (no copy, no event on the queue)
+                if (A.h_flag) {
+                    const uint32_t fv = __hip_atomic_load(A.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(A.h_flag + 1, fv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(A.h_flag, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            }
         }
     }
 }
@@ -1249,22 +1271,31 @@ static int tp_offsets(TpScanArgs &A, uint32_t item, hipStream_t st) {
     return NMZ_OK;
 }
 
-// The mismatch flag of searches enqueued with a shard's cached sizes (see ed_bv_two_phase). arm: after such a
-// search, copy the flag to pinned host memory behind an event. check: read that copy -- without waiting (the shard's
-// next search: a copy not yet landed is read by a later call, the device flag stays set until reported), or after
-// synchronising `st` (wait: the synchronous entry points) -- and, when set, clear it, drop every cached size (the
-// next search recounts) and fail.
-int ed_tp_flag_arm(nmz_ed_plan *p, hipStream_t st) {
-    if (!p->d_tp_mismatch) return NMZ_OK;
+// The mismatch flag of searches enqueued with a shard's cached sizes (see ed_bv_two_phase). Such a search's offsets
+// scan compares its totals with the cache, sets the device flag on a difference and writes {its sequence number, the
+// flag as it now stands} to pinned host words (no copy or event on the queue: each was ~5-10 us per search). arm:
+// mark that a search was enqueued. check: read the host words -- without waiting (the shard's next search: a number
+// not yet landed is read by a later call, the device flag stays set until reported) -- or the device flag after
+// synchronising `st` (wait: the synchronous entry points); when set, clear it, drop every cached size (the next
+// search recounts) and fail.
+int ed_tp_flag_host(nmz_ed_plan *p) {
     if (!p->h_tp_flag) {
-        NMZ_HIP(hipHostMalloc((void **)&p->h_tp_flag, 4, hipHostMallocDefault));
-        *p->h_tp_flag = 0;
+        NMZ_HIP(hipHostMalloc((void **)&p->h_tp_flag, 8, hipHostMallocCoherent));  // device stores reach it directly
+        p->h_tp_flag[0] = p->h_tp_flag[1] = 0;
+        p->tp_seq = 0;
     }
-    if (!p->tp_flag_ev) NMZ_HIP(hipEventCreateWithFlags(&p->tp_flag_ev, hipEventDisableTiming));
-    NMZ_HIP(hipMemcpyAsync(p->h_tp_flag, p->d_tp_mismatch, 4, hipMemcpyDeviceToHost, st));
-    NMZ_HIP(hipEventRecord(p->tp_flag_ev, st));
-    p->tp_flag_armed = true;
     return NMZ_OK;
+}
+
+int ed_tp_flag_arm(nmz_ed_plan *p, hipStream_t) {
+    if (!p->d_tp_mismatch) return NMZ_OK;
+    p->tp_flag_armed = true;  // the search's scan publishes {tp_seq, flag} to h_tp_flag
+    return NMZ_OK;
+}
+
+// the scan of the last armed search has published its flag (then no kernel writes h_tp_flag any more)
+static bool ed_tp_flag_landed(const nmz_ed_plan *p) {
+    return __atomic_load_n(&p->h_tp_flag[0], __ATOMIC_ACQUIRE) == p->tp_seq;
 }
 
 int ed_tp_flag_check(nmz_ed_plan *p, bool wait, hipStream_t st) {
@@ -1274,21 +1305,31 @@ int ed_tp_flag_check(nmz_ed_plan *p, bool wait, hipStream_t st) {
         NMZ_HIP(hipMemcpyAsync(&f, p->d_tp_mismatch, 4, hipMemcpyDeviceToHost, st));
         NMZ_HIP(hipStreamSynchronize(st));
     } else {
-        if (!p->tp_flag_armed) return NMZ_OK;
-        const hipError_t q = hipEventQuery(p->tp_flag_ev);
-        if (q == hipErrorNotReady) return NMZ_OK;
-        if (q != hipSuccess) return fail(NMZ_EHIP, "hipEventQuery failed");
-        f = *p->h_tp_flag;
+        if (!p->tp_flag_armed || !p->h_tp_flag) return NMZ_OK;
+        if (!ed_tp_flag_landed(p)) return NMZ_OK;  // not yet: a later call reads it (the device flag stays set)
+        f = __atomic_load_n(&p->h_tp_flag[1], __ATOMIC_ACQUIRE);
     }
     p->tp_flag_armed = false;
     if (!f) return NMZ_OK;
     NMZ_HIP(hipMemsetAsync(p->d_tp_mismatch, 0, 4, st));
-    if (p->h_tp_flag) *p->h_tp_flag = 0;
+    if (p->h_tp_flag) p->h_tp_flag[1] = 0;
     p->tp_sizes.clear();
     p->tp_dirty = true;  // the skipped write pass left the count pass's counts in place
     return fail(NMZ_EHIP, "internal: a two-phase search's totals differed from the shard's cached sizes; that search "
                           "wrote no entries and ran no DP (its k-NN lists are incomplete), and the cached sizes are "
                           "dropped");
+}
+
+// before the pinned flag words are freed: the last armed search's scan has written them (bounded wait, then a device
+// synchronisation)
+void ed_tp_flag_release(nmz_ed_plan *p) {
+    if (!p->h_tp_flag) return;
+    if (p->tp_seq) {
+        for (int i = 0; i < 200000 && !ed_tp_flag_landed(p); ++i) std::this_thread::sleep_for(std::chrono::microseconds(50));
+        if (!ed_tp_flag_landed(p)) (void)hipDeviceSynchronize();
+    }
+    (void)hipHostFree(p->h_tp_flag);
+    p->h_tp_flag = nullptr;
 }
 
 // The shard's tiles in query-block order; the count pass sizes the entry lists. Entry lists beyond
@@ -1427,6 +1468,8 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
         S.rec_cnt = d_rec_cnt;
         S.rec_share = Q.rec_cap;
         S.flag = verify ? p->d_tp_mismatch : nullptr;
+        S.h_flag = verify ? p->h_tp_flag : nullptr;
+        S.seq = p->tp_seq;
         if (verify) {
             // (NMZ_ED_TP_FAKE_MISMATCH=1, a test knob: compare against a wrong total, so the flag path runs)
             const char *fake = ab_env("NMZ_ED_TP_FAKE_MISMATCH");
@@ -1493,6 +1536,8 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
     if (cached != p->tp_sizes.end() && Q.recs && cached->second.tot64 <= limit) {
         const nmz_ed_plan::TpSizes &z = cached->second;
         item = z.item;
+        NMZ_TRY(ed_tp_flag_host(p));
+        ++p->tp_seq;  // this search's number: its scan publishes it with the flag
         NMZ_TRY(count(tl.as<uint64_t>(), n_tiles_all, tot64, tot_items, &z));
         n_rec = z.n_rec;
         NMZ_TRY(write_dp(z.tot64, z.items));
@@ -1575,7 +1620,12 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
                       uint32_t n_shards = 1) {
     const uint32_t N = p->n;
     if (N == 0 || k == 0) return NMZ_OK;
-    hipLaunchKernelGGL(k_knn_init, dim3(ceil_div((uint64_t)N * k, 256)), dim3(256), 0, st, d_knn, (uint64_t)N * k);
+    {
+        uint64_t *cnt = p->bv ? p->d_counters : nullptr;  // zeroed with the lists (was a memset per search)
+        const uint64_t nl = (uint64_t)N * k, nt = std::max<uint64_t>(nl, cnt ? ED_CNT_WORDS : 0);
+        hipLaunchKernelGGL(k_knn_init_cnt, dim3(ceil_div(nt, 256)), dim3(256), 0, st, d_knn, nl, cnt,
+                           (uint32_t)ED_CNT_WORDS);
+    }
     if (p->wide) {
         EdWideArgs A;
         A.sym = p->d_qsym;
@@ -1618,7 +1668,6 @@ static int ed_knn_run(nmz_ed_plan *p, hipStream_t st, uint32_t k, uint64_t *d_kn
         A.row_bytes = p->row_bytes;
         A.shard = shard;
         A.n_shards = n_shards;
-        NMZ_HIP(hipMemsetAsync(p->d_counters, 0, ED_CNT_WORDS * 8, st));
         int rc = 1;
         if (A.prof && p->two_phase) {  // filter tiles + DP work items (the search's "ed_bv" time)
             KernelTimer kt(p->ctx, st, "ed_bv");
@@ -1723,8 +1772,7 @@ int nmz_ed_plan_destroy(nmz_ed_plan *plan) {
         plan->tp_ent.release();
         plan->tp_rec.release();
         for (auto &kv : plan->tile_list) kv.second.release();
-        if (plan->tp_flag_ev) (void)hipEventSynchronize(plan->tp_flag_ev), (void)hipEventDestroy(plan->tp_flag_ev);
-        if (plan->h_tp_flag) (void)hipHostFree(plan->h_tp_flag);
+        ed_tp_flag_release(plan);
     }
     delete plan;
     return NMZ_OK;
@@ -2166,8 +2214,7 @@ int nmz_ed_allpairs_knn(nmz_ctx *ctx, const uint64_t *off, const uint64_t *sym, 
             p->tp_ent.release();
             p->tp_rec.release();
             for (auto &kv : p->tile_list) kv.second.release();
-            if (p->tp_flag_ev) (void)hipEventSynchronize(p->tp_flag_ev), (void)hipEventDestroy(p->tp_flag_ev);
-            if (p->h_tp_flag) (void)hipHostFree(p->h_tp_flag);
+            ed_tp_flag_release(p);
             delete p;
         }
     } pg{plan};
