@@ -461,7 +461,8 @@ struct nmz_ed_plan {
     // waiting once the number has landed, or read from the device with a wait by the synchronous entry points
     // (nmz_ed_plan_counters, the group search)
     uint32_t *h_tp_flag = nullptr;
-    uint32_t tp_seq = 0;
+    uint32_t tp_seq = 0;       // the latest cached search's number
+    uint32_t tp_seq_sent = 0;  // the latest number whose scan was enqueued (the last writer of h_tp_flag)
     bool tp_flag_armed = false;
     // fixed at creation (NMZ_ED_QGRAM / NMZ_ED_TWO_PHASE, A/B knobs read once per plan), so every shard and every
     // call of one plan takes the same search and deals pairs by the same rule
@@ -1293,9 +1294,9 @@ int ed_tp_flag_arm(nmz_ed_plan *p, hipStream_t) {
     return NMZ_OK;
 }
 
-// the scan of the last armed search has published its flag (then no kernel writes h_tp_flag any more)
-static bool ed_tp_flag_landed(const nmz_ed_plan *p) {
-    return __atomic_load_n(&p->h_tp_flag[0], __ATOMIC_ACQUIRE) == p->tp_seq;
+// the scan of search number `seq` has published its flag
+static bool ed_tp_flag_landed(const nmz_ed_plan *p, uint32_t seq) {
+    return __atomic_load_n(&p->h_tp_flag[0], __ATOMIC_ACQUIRE) == seq;
 }
 
 int ed_tp_flag_check(nmz_ed_plan *p, bool wait, hipStream_t st) {
@@ -1306,7 +1307,7 @@ int ed_tp_flag_check(nmz_ed_plan *p, bool wait, hipStream_t st) {
         NMZ_HIP(hipStreamSynchronize(st));
     } else {
         if (!p->tp_flag_armed || !p->h_tp_flag) return NMZ_OK;
-        if (!ed_tp_flag_landed(p)) return NMZ_OK;  // not yet: a later call reads it (the device flag stays set)
+        if (!ed_tp_flag_landed(p, p->tp_seq)) return NMZ_OK;  // not yet: a later call reads it (the flag stays set)
         f = __atomic_load_n(&p->h_tp_flag[1], __ATOMIC_ACQUIRE);
     }
     p->tp_flag_armed = false;
@@ -1324,9 +1325,10 @@ int ed_tp_flag_check(nmz_ed_plan *p, bool wait, hipStream_t st) {
 // synchronisation)
 void ed_tp_flag_release(nmz_ed_plan *p) {
     if (!p->h_tp_flag) return;
-    if (p->tp_seq) {
-        for (int i = 0; i < 200000 && !ed_tp_flag_landed(p); ++i) std::this_thread::sleep_for(std::chrono::microseconds(50));
-        if (!ed_tp_flag_landed(p)) (void)hipDeviceSynchronize();
+    if (const uint32_t seq = p->tp_seq_sent) {
+        for (int i = 0; i < 200000 && !ed_tp_flag_landed(p, seq); ++i)
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        if (!ed_tp_flag_landed(p, seq)) (void)hipDeviceSynchronize();
     }
     (void)hipHostFree(p->h_tp_flag);
     p->h_tp_flag = nullptr;
@@ -1477,7 +1479,9 @@ static int ed_bv_two_phase(nmz_ed_plan *p, hipStream_t st, EdBvArgs &A, uint64_t
             S.e_items = verify->items;
             S.e_rec = verify->n_rec;
         }
-        return tp_offsets(S, item, st);
+        const int rc = tp_offsets(S, item, st);
+        if (rc == NMZ_OK && S.h_flag) p->tp_seq_sent = S.seq;
+        return rc;
     };
     auto count = [&](const uint64_t *tiles, uint64_t n_tiles, uint64_t &tot64, uint32_t &tot_items,
                      const nmz_ed_plan::TpSizes *verify = nullptr) -> int {
