@@ -894,6 +894,47 @@ def test_two_phase_offset_kernels(ctx, n, item, big):
     assert int(d_tot.cpu().numpy().view(np.uint64)[0]) == int(exp_p[-1])
 
 
+def test_cached_searches_back_to_back_then_destroy(ctx):
+    """Cached searches publish their mismatch flag from the offsets scan into pinned host words (csrc/ed.hip
+    ed_tp_flag_*: a sequence number, then the flag; no copy or event on the queue). Enqueued back to back without a
+    synchronisation, none reports a mismatch (a number not yet landed is read later) and the last one's lists equal
+    the oracle; destroying the plan right after a burst waits for the last scan's words before freeing them."""
+    import torch
+    L = _lib.load()
+    ts = _edited_family(300, 150, 16, 30, np.random.default_rng(23))
+    n, k, w = len(ts), 8, 32
+    oi, od = O.ed_allpairs_knn(ts.off, ts.sym, w, k, nthreads=16)
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    keys = torch.empty(n * k, dtype=torch.int64, device="cuda")
+    for destroy_in_flight in (False, True):
+        plan = ctypes.c_void_p()
+        _lib.check(L.nmz_ed_plan_create(ctx.handle, _lib.ptr(ts.off), _lib.ptr(ts.sym), n, w, ctypes.byref(plan)))
+        try:
+            assert L.nmz_ed_plan_is_fast(plan) == 2
+            _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, 0, 1, ctypes.c_void_p(keys.data_ptr()), stream))
+            torch.cuda.synchronize()  # sizes read back: the searches below run from the cache
+            for _ in range(8):
+                _lib.check(L.nmz_ed_allpairs_knn_shard_dev(plan, k, 0, 1, ctypes.c_void_p(keys.data_ptr()), stream))
+            if destroy_in_flight:  # the burst is still running: destroy waits for its last scan's words
+                L.nmz_ed_plan_destroy(plan)
+                plan = None
+                torch.cuda.synchronize()
+                continue
+            torch.cuda.synchronize()
+            out = keys.clone()
+            torch.cuda.synchronize()
+            _lib.check(L.nmz_ed_knn_fill_dev(plan, k, ctypes.c_void_p(out.data_ptr()), stream))
+            torch.cuda.synchronize()
+            kk = out.cpu().numpy().view(np.uint64).reshape(n, k)
+            ids, ds = (kk & np.uint64(0xFFFFFFFF)).astype(np.uint32), (kk >> np.uint64(32)).astype(np.uint32)
+            assert np.array_equal(ids, oi) and np.array_equal(ds, od)
+            cnt = np.zeros(_lib.NMZ_ED_NCOUNTERS, np.uint64)
+            _lib.check(L.nmz_ed_plan_counters(plan, _lib.ptr(cnt), stream))  # no mismatch pending
+        finally:
+            if plan is not None:
+                L.nmz_ed_plan_destroy(plan)
+
+
 def test_cached_size_mismatch_skips_writes_and_surfaces(ab_knobs, ctx, monkeypatch):
     """A shard's later searches run with the sizes its first search read back (csrc/ed.hip ed_bv_two_phase); a
     one-thread check flags a search whose own totals differ. NMZ_ED_TP_FAKE_MISMATCH forces the flag on a cached
